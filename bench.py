@@ -1,0 +1,113 @@
+"""Headline benchmark: FL rounds/s on the BASELINE.json config.
+
+CIFAR-10 half-width ResNet-18, 100 clients (10 per round), single-shot DBA with 4
+distributed attackers (rounds 203/205/207/209), FedAvg — ``configs/cifar_params.yaml`` —
+on synthetic CIFAR-shaped data and random-init weights (no network: no dataset download,
+no pretrained checkpoint).  One "step" is one complete FL round exactly as the reference
+defines it: client selection, every client's local training (benign 2 epochs, attackers 6
+poisoned epochs + model-replacement scaling), every local and global test the reference
+runs (per-client clean tests, attacker poison/trigger tests, global clean + combined
+trigger + 4 per-trigger ASR tests), aggregation, CSV output.  Nothing is skipped.
+
+Rounds start at 201 (the reference resumes from a 200-round pretrain), so with the default
+``--warmup 2`` the timed window 203..210 contains all four poison rounds.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...     # one rank per GPU over RCCL
+
+Strong scaling: the round's work is fixed; N GPUs split its clients (LPT) and its
+evaluation images.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import tempfile
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from dba_mod_amd import config as C  # noqa: E402
+from dba_mod_amd import ops  # noqa: E402
+from dba_mod_amd.fl.server import Server  # noqa: E402
+from dba_mod_amd.parallel.dist import init_distributed, shutdown  # noqa: E402
+
+METRIC = "FL rounds/sec + backdoor ASR & main-task acc, ResNet-18 CIFAR-10 100 clients"
+# reference design, CIFAR FL throughput ≈ 0.0085 rounds/s (8-vCPU estimate;
+# the reference repo publishes no number of its own)
+BASELINE_ROUNDS_PER_S = 0.0085
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=8)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--config", default=os.path.join(ROOT, "configs", "cifar_params.yaml"))
+    ap.add_argument("--aggregation", default=None, help="override: mean | geom_median | foolsgold")
+    ap.add_argument("--cpu", action="store_true")
+    ap.add_argument("--set", dest="overrides", nargs="*", default=[])
+    args = ap.parse_args()
+
+    dctx = init_distributed(prefer_gpu=not args.cpu)
+    over = {"resumed_model": False, "start_epoch": 201, "synthetic_data": True, "save_model": False}
+    if args.aggregation:
+        over["aggregation_methods"] = args.aggregation
+    over.update(C.parse_override(args.overrides))
+    params = C.load_params(args.config, over)
+    tmp = tempfile.mkdtemp(prefix="dba_bench_")
+    server = Server(params, dctx, write_outputs=True, folder=tmp)
+    import logging
+    logging.getLogger("logger").setLevel(logging.WARNING)
+
+    epoch = server.start_epoch
+    for _ in range(args.warmup):
+        server.run_round(epoch)
+        epoch += 1
+
+    def sync():
+        if dctx.device.type == "cuda":
+            torch.cuda.synchronize(dctx.device)
+        dctx.barrier()
+
+    sync()
+    t0 = time.perf_counter()
+    last = {}
+    for _ in range(args.steps):
+        last = server.run_round(epoch)
+        epoch += 1
+    sync()
+    elapsed = dctx.all_reduce_max(time.perf_counter() - t0)
+    rps = args.steps / elapsed if elapsed > 0 else 0.0
+    if dctx.is_main:
+        out = {
+            "metric": METRIC, "value": round(rps, 4), "unit": "rounds/s", "n_gpus": dctx.world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1000.0 * elapsed / max(1, args.steps), 2),
+            "higher_is_better": True, "scaling": "strong",
+            "vs_baseline": round(rps / BASELINE_ROUNDS_PER_S, 2),
+            "dtype": "bf16" if server.dtype == torch.bfloat16 else "fp32",
+            "data": "synthetic (CIFAR-10 shapes/class sizes, random-init weights)",
+            "config": {"model": "ResNet-18 (half-width, CIFAR-10)", "global_batch": 64 * int(params["no_models"]),
+                       "seq_len": None, "parallelism": f"client-dp{dctx.world}",
+                       "clients_total": int(params["number_of_total_participants"]),
+                       "clients_per_round": int(params["no_models"]),
+                       "attackers": params.adversary_list, "aggregation": params["aggregation_methods"],
+                       "rounds_timed": f"{epoch - args.steps}..{epoch - 1}",
+                       "baseline_source": "BASELINE.md §4 reference-design estimate 0.0085 rounds/s"},
+            "ops_backend": ops.backend_name(dctx.device),
+            "global_acc": round(float(last.get("global_acc", 0.0)), 3),
+            "global_asr": round(float(last.get("global_asr", 0.0)), 3),
+            "phases_last_round_s": {k: round(v, 4) for k, v in last.get("phases", {}).items()},
+        }
+        print(json.dumps(out), flush=True)
+    shutdown(dctx)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,215 @@
+"""Experiment configuration: the reference's YAML schema, loaded into a typed dict.
+
+The reference drives everything from one YAML file passed as ``--params`` and read into
+a plain dict (reference ``main.py:88-92``); it mutates the dict at run time
+(``helper.py:44-48``, ``image_helper.py:63``) and reads dynamic per-trigger keys such as
+``{i}_poison_pattern`` / ``{i}_poison_epochs``.  ``Params`` keeps that
+exact dict behaviour (so reference YAML files load unchanged, unknown/dead keys are kept
+and ignored), adds the new framework's own keys with defaults that reproduce reference
+behaviour, and exposes typed helpers for the dynamic keys.
+
+Constants mirror reference ``config.py:4-13``.
+"""
+from __future__ import annotations
+
+import copy
+import os
+from typing import Any, Dict, Iterable, List, Optional, Sequence
+
+import yaml
+
+AGGR_MEAN = "mean"
+AGGR_GEO_MED = "geom_median"
+AGGR_FOOLSGOLD = "foolsgold"
+AGGREGATIONS = (AGGR_MEAN, AGGR_GEO_MED, AGGR_FOOLSGOLD)
+
+TYPE_LOAN = "loan"
+TYPE_CIFAR = "cifar"
+TYPE_MNIST = "mnist"
+TYPE_TINYIMAGENET = "tiny-imagenet-200"
+TYPES = (TYPE_LOAN, TYPE_CIFAR, TYPE_MNIST, TYPE_TINYIMAGENET)
+
+# reference config.py:7-8 (declared but unused there; kept for API parity)
+MAX_UPDATE_NORM = 1000
+PATIENCE_ITER = 20
+
+# Defaults of keys the reference reads (so partial YAMLs work) and of the new keys this
+# framework adds.  Reference keys default to the values of utils/cifar_params.yaml.
+_DEFAULTS: Dict[str, Any] = {
+    # --- reference keys --------------------------------------------------------------
+    "test_batch_size": 64,
+    "batch_size": 64,
+    "lr": 0.1,
+    "poison_lr": 0.05,
+    "momentum": 0.9,
+    "decay": 0.0005,
+    "epochs": 1,
+    "internal_epochs": 1,
+    "internal_poison_epochs": 6,
+    "poisoning_per_batch": 5,
+    "aggr_epoch_interval": 1,
+    "aggregation_methods": AGGR_MEAN,
+    "geom_median_maxiter": 10,
+    "fg_use_memory": True,
+    "participants_namelist": list(range(10)),
+    "no_models": 10,
+    "number_of_total_participants": 100,
+    "is_random_namelist": True,
+    "is_random_adversary": False,
+    "is_poison": False,
+    "baseline": False,
+    "scale_weights_poison": 100,
+    "eta": 0.1,
+    "sampling_dirichlet": True,
+    "dirichlet_alpha": 0.5,
+    "poison_label_swap": 2,
+    "adversary_list": [],
+    "centralized_test_trigger": True,
+    "trigger_num": 0,
+    "poison_epochs": [],
+    "poison_step_lr": True,
+    "alpha_loss": 1.0,
+    "diff_privacy": False,
+    "sigma": 0.01,
+    "save_model": False,
+    "save_on_epochs": [],
+    "resumed_model": False,
+    "resumed_model_name": "",
+    "vis_train": False,
+    "vis_train_batch_loss": False,
+    "vis_trigger_split_test": False,
+    "batch_track_distance": False,
+    "tied": False,
+    # --- new keys (this framework) -----------------------------------------------------
+    "seed": 1,                    # reference seeds python/torch with 1 (main.py:36-38,86)
+    "data_dir": "./data",         # torchvision root in the reference (image_helper.py:175)
+    "save_dir": "saved_models",   # run-dir parent (helper.py:35)
+    "synthetic_data": "auto",     # auto: real files if present under data_dir, else synthetic
+    "synthetic_train_size": None,  # override synthetic dataset sizes (tests / smoke runs)
+    "synthetic_test_size": None,
+    "compute_dtype": "auto",      # auto: bf16 on GPU (MFMA), fp32 on CPU
+    "eval_batch_size": 1024,      # per-model eval chunk (reference: 64; a free parameter, D13)
+    "aggregate_bn_buffers": True,  # D2: deltas/aggregation include BN running stats
+    "best_on_clean_loss": False,   # D6: reference keys .best on the poison-test loss
+    "visdom": False,               # live plots need a visdom server; JSONL stream always on
+    "metrics_jsonl": True,
+    "max_rounds": None,            # stop after this many rounds (bench / smoke)
+    "local_eval": True,            # per-client local tests (reference behaviour)
+    "graph_capture": True,         # HIP-graph the grouped training step on GPU
+}
+
+# keys whose value may legitimately be a python list of ints/strings
+_CLIENT_ID_KEYS = ("adversary_list", "participants_namelist")
+
+
+class Params(dict):
+    """dict with typed accessors; behaves exactly like the reference's params dict."""
+
+    def __init__(self, data: Optional[Dict[str, Any]] = None, **kw: Any) -> None:
+        super().__init__()
+        merged = copy.deepcopy(_DEFAULTS)
+        if data:
+            merged.update(data)
+        merged.update(kw)
+        super().update(merged)
+        self._validate()
+
+    # ------------------------------------------------------------------ helpers
+    def _validate(self) -> None:
+        t = self.get("type")
+        if t is not None and t not in TYPES:
+            raise ValueError(f"unknown workload type {t!r}; expected one of {TYPES}")
+        if self["aggregation_methods"] not in AGGREGATIONS:
+            raise ValueError(f"unknown aggregation {self['aggregation_methods']!r}")
+        if self["aggregation_methods"] == AGGR_FOOLSGOLD and self["aggr_epoch_interval"] != 1:
+            # reference image_train.py:24 'only works for aggr_epoch_interval=1'
+            raise ValueError("foolsgold requires aggr_epoch_interval == 1")
+
+    @property
+    def type(self) -> str:
+        return self["type"]
+
+    @property
+    def adversary_list(self) -> List[Any]:
+        return list(self.get("adversary_list") or [])
+
+    def poison_pattern(self, idx: int) -> List[List[int]]:
+        """Pixel (row, col) list of local trigger ``idx``; ``-1`` = union of all (global).
+
+        reference image_helper.py:328-335
+        """
+        if idx == -1:
+            out: List[List[int]] = []
+            for i in range(int(self["trigger_num"])):
+                out.extend(self.get(f"{i}_poison_pattern", []))
+            return out
+        return list(self.get(f"{idx}_poison_pattern", []))
+
+    def poison_epochs_of(self, adv_index: int) -> List[int]:
+        """Rounds in which adversary ``adv_index`` poisons (reference image_train.py:38-43)."""
+        key = f"{adv_index}_poison_epochs"
+        if key in self:
+            return list(self[key])
+        return list(self.get("poison_epochs") or [])
+
+    def trigger_features(self, idx: int) -> List[tuple]:
+        """LOAN trigger (feature name, value) pairs; ``-1`` = all triggers (test.py:62-67)."""
+        if idx == -1:
+            out: List[tuple] = []
+            for j in range(int(self["trigger_num"])):
+                out.extend(zip(self.get(f"{j}_poison_trigger_names", []),
+                               self.get(f"{j}_poison_trigger_values", [])))
+            return out
+        return list(zip(self.get(f"{idx}_poison_trigger_names", []),
+                        self.get(f"{idx}_poison_trigger_values", [])))
+
+    def adversary_index(self, name: Any) -> int:
+        """Index of ``name`` in adversary_list or -1 (reference image_train.py:40-46)."""
+        for i, a in enumerate(self.adversary_list):
+            if _same_client(a, name):
+                return i
+        return -1
+
+    def is_adversary(self, name: Any) -> bool:
+        return self.adversary_index(name) >= 0
+
+    def to_plain(self) -> Dict[str, Any]:
+        return {k: v for k, v in self.items()}
+
+
+def _same_client(a: Any, b: Any) -> bool:
+    if a == b:
+        return True
+    try:
+        return int(a) == int(b)
+    except (TypeError, ValueError):
+        return str(a) == str(b)
+
+
+def load_params(path: str, overrides: Optional[Dict[str, Any]] = None) -> Params:
+    """Load a reference-style YAML file (``yaml.safe_load``: reference used the PyYAML<6
+    ``yaml.load(f)`` API, quirk D8)."""
+    with open(path, "r") as f:
+        data = yaml.safe_load(f) or {}
+    if not isinstance(data, dict):
+        raise ValueError(f"{path}: top level must be a mapping")
+    if overrides:
+        data.update(overrides)
+    return Params(data)
+
+
+def parse_override(items: Iterable[str]) -> Dict[str, Any]:
+    """``key=value`` CLI overrides; values are parsed as YAML scalars/lists."""
+    out: Dict[str, Any] = {}
+    for it in items:
+        if "=" not in it:
+            raise ValueError(f"override {it!r} is not key=value")
+        k, v = it.split("=", 1)
+        out[k.strip()] = yaml.safe_load(v)
+    return out
+
+
+def default_dataset_name(t: str) -> str:
+    """Run-name default per workload (reference main.py:96-108)."""
+    return {TYPE_LOAN: "loan", TYPE_CIFAR: "cifar", TYPE_MNIST: "mnist",
+            TYPE_TINYIMAGENET: "tiny"}[t]

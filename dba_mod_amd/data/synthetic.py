@@ -1,0 +1,189 @@
+"""Synthetic datasets with the reference workloads' exact shapes and class sizes.
+
+There is no network in this environment, so the torchvision downloads of the reference
+(``image_helper.py:176-220``) and the Kaggle LendingClub CSVs (``utils/process_loan_data.sh``)
+cannot be fetched.  These generators produce *learnable* stand-ins:
+
+* every class owns a smooth random template (low-frequency field, per-channel tint);
+* every image is its class template, randomly shifted by a few pixels, contrast-jittered
+  and corrupted by pixel noise, quantised to uint8 (the reference feeds ``ToTensor``
+  = uint8/255 images with no normalisation, ``image_helper.py:176-201``).
+
+Class sizes match the real datasets so the Dirichlet partitioner reproduces the reference's
+annotated shard sizes: CIFAR-10 5000/1000 per class, MNIST's real per-class
+counts, Tiny-ImageNet 500/50 per class for 200 classes.
+
+Images are stored NHWC uint8 — the device-resident layout the gather kernel reads.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Tuple
+
+import numpy as np
+
+# real per-class counts of MNIST train / test (digits 0..9)
+MNIST_TRAIN_COUNTS = [5923, 6742, 5958, 6131, 5842, 5421, 5918, 6265, 5851, 5949]
+MNIST_TEST_COUNTS = [980, 1135, 1032, 1010, 982, 892, 958, 1028, 974, 1009]
+
+
+@dataclass
+class ImageDataset:
+    """Host-side image dataset: uint8 NHWC images + int64 labels."""
+    images: np.ndarray          # [N, H, W, C] uint8
+    labels: np.ndarray          # [N] int64
+    num_classes: int
+    name: str = ""
+
+    def __len__(self) -> int:
+        return int(self.labels.shape[0])
+
+    @property
+    def shape(self) -> Tuple[int, int, int]:
+        return tuple(self.images.shape[1:])  # type: ignore[return-value]
+
+
+@dataclass
+class TabularDataset:
+    """One LOAN state: float features + int labels, train/test already split."""
+    name: str
+    train_x: np.ndarray         # [Ntr, F] float32
+    train_y: np.ndarray         # [Ntr] int64
+    test_x: np.ndarray
+    test_y: np.ndarray
+    columns: List[str] = field(default_factory=list)
+
+
+def _class_order_labels(counts: List[int], rng: np.random.RandomState) -> np.ndarray:
+    labels = np.concatenate([np.full(c, k, dtype=np.int64) for k, c in enumerate(counts)])
+    rng.shuffle(labels)  # interleave classes like a real dataset file
+    return labels
+
+
+def _smooth_field(rng: np.random.RandomState, h: int, w: int, c: int, coarse: int) -> np.ndarray:
+    """Low-frequency random field in [0,1] of shape [h, w, c] (bilinear upsample)."""
+    g = rng.rand(coarse + 1, coarse + 1, c).astype(np.float32)
+    ys = np.linspace(0, coarse, h, dtype=np.float32)
+    xs = np.linspace(0, coarse, w, dtype=np.float32)
+    y0 = np.floor(ys).astype(int).clip(0, coarse - 1)
+    x0 = np.floor(xs).astype(int).clip(0, coarse - 1)
+    fy = (ys - y0)[:, None, None]
+    fx = (xs - x0)[None, :, None]
+    a = g[y0][:, x0]
+    b = g[y0][:, x0 + 1]
+    cc = g[y0 + 1][:, x0]
+    d = g[y0 + 1][:, x0 + 1]
+    return (a * (1 - fy) * (1 - fx) + b * (1 - fy) * fx + cc * fy * (1 - fx) + d * fy * fx)
+
+
+def make_image_dataset(counts: List[int], h: int, w: int, c: int, seed: int,
+                       noise: float = 0.45, shift: int = 3, coarse: int = 4,
+                       templates: Optional[np.ndarray] = None,
+                       name: str = "") -> Tuple[ImageDataset, np.ndarray]:
+    """Generate a dataset; returns (dataset, class templates) so train/test share templates."""
+    rng = np.random.RandomState(seed)
+    k = len(counts)
+    if templates is None:
+        trng = np.random.RandomState(seed * 7919 + 17)
+        shared = _smooth_field(trng, h + 2 * shift, w + 2 * shift, c, coarse)
+        # classes share 65% of their template: separable, but not trivially so
+        templates = np.stack([0.65 * shared + 0.35 * _smooth_field(trng, h + 2 * shift, w + 2 * shift, c, coarse)
+                              for _ in range(k)]).astype(np.float32)
+    labels = _class_order_labels(counts, rng)
+    n = labels.shape[0]
+    out = np.empty((n, h, w, c), dtype=np.uint8)
+    chunk = 4096
+    for s in range(0, n, chunk):
+        e = min(n, s + chunk)
+        lab = labels[s:e]
+        dy = rng.randint(0, 2 * shift + 1, size=e - s)
+        dx = rng.randint(0, 2 * shift + 1, size=e - s)
+        contrast = rng.uniform(0.6, 1.2, size=(e - s, 1, 1, 1)).astype(np.float32)
+        bright = rng.uniform(-0.15, 0.15, size=(e - s, 1, 1, 1)).astype(np.float32)
+        imgs = np.empty((e - s, h, w, c), dtype=np.float32)
+        for i in range(e - s):
+            t = templates[lab[i]]
+            imgs[i] = t[dy[i]:dy[i] + h, dx[i]:dx[i] + w]
+        imgs = (imgs - 0.5) * contrast + 0.5 + bright
+        imgs += rng.randn(e - s, h, w, c).astype(np.float32) * noise
+        out[s:e] = np.clip(imgs * 255.0 + 0.5, 0, 255).astype(np.uint8)
+    return ImageDataset(out, labels, k, name), templates
+
+
+def _scaled_counts(counts: List[int], total: Optional[int]) -> List[int]:
+    if total is None:
+        return list(counts)
+    s = sum(counts)
+    return [max(1, int(round(c * total / s))) for c in counts]
+
+
+def synthetic_image_pair(kind: str, seed: int = 1, train_size: Optional[int] = None,
+                         test_size: Optional[int] = None) -> Tuple[ImageDataset, ImageDataset]:
+    """(train, test) synthetic datasets for 'mnist' | 'cifar' | 'tiny-imagenet-200'."""
+    if kind == "mnist":
+        tr_c, te_c, hwc = MNIST_TRAIN_COUNTS, MNIST_TEST_COUNTS, (28, 28, 1)
+    elif kind == "cifar":
+        tr_c, te_c, hwc = [5000] * 10, [1000] * 10, (32, 32, 3)
+    elif kind == "tiny-imagenet-200":
+        tr_c, te_c, hwc = [500] * 200, [50] * 200, (64, 64, 3)
+    else:
+        raise ValueError(kind)
+    tr_c = _scaled_counts(tr_c, train_size)
+    te_c = _scaled_counts(te_c, test_size)
+    h, w, c = hwc
+    coarse = 3 if kind == "mnist" else 4
+    train, tmpl = make_image_dataset(tr_c, h, w, c, seed=seed * 1000 + 1, coarse=coarse,
+                                     name=f"{kind}-train")
+    test, _ = make_image_dataset(te_c, h, w, c, seed=seed * 1000 + 2, coarse=coarse,
+                                 templates=tmpl, name=f"{kind}-test")
+    return train, test
+
+
+# ---------------------------------------------------------------------------- LOAN
+US_STATES = ["AK", "AL", "AR", "AZ", "CA", "CO", "CT", "DC", "DE", "FL", "GA", "HI", "IA",
+             "ID", "IL", "IN", "KS", "KY", "LA", "MA", "MD", "ME", "MI", "MN", "MO", "MS",
+             "MT", "NC", "ND", "NE", "NH", "NJ", "NM", "NV", "NY", "OH", "OK", "OR", "PA",
+             "RI", "SC", "SD", "TN", "TX", "UT", "VA", "VT", "WA", "WI", "WV", "WY"]
+# trigger features named in utils/loan_params.yaml (low/high importance sets)
+LOAN_NAMED_FEATURES = ["num_tl_120dpd_2m", "num_tl_90g_dpd_24m", "pub_rec_bankruptcies",
+                       "pub_rec", "acc_now_delinq", "tax_liens", "out_prncp",
+                       "total_pymnt_inv", "out_prncp_inv", "total_rec_prncp",
+                       "last_pymnt_amnt", "all_util"]
+LOAN_NUM_FEATURES = 91   # reference loan_model.py:11 in_dim
+LOAN_NUM_CLASSES = 9     # loan_helper.py:149-152
+
+
+def loan_columns() -> List[str]:
+    cols = list(LOAN_NAMED_FEATURES)
+    k = 0
+    while len(cols) < LOAN_NUM_FEATURES:
+        cols.append(f"feat_{k:02d}")
+        k += 1
+    return cols
+
+
+def synthetic_loan(seed: int = 1, total_rows: int = 120000) -> List[TabularDataset]:
+    """51 per-state tabular datasets (91 features, 9 classes), 80/20 split.
+
+    Feature scales mimic the reference preprocessing (``loan_preprocess.py``: values
+    divided down to roughly O(1-10)).  Labels come from a fixed random linear teacher so
+    the task is learnable; class priors are skewed like LendingClub's.
+    """
+    rng = np.random.RandomState(seed * 31 + 5)
+    cols = loan_columns()
+    f = len(cols)
+    teacher = rng.randn(f, LOAN_NUM_CLASSES).astype(np.float32)
+    prior = np.log(np.array([40, 35, 3, 2, 12, 1.5, 0.5, 3, 3], dtype=np.float32))
+    weights = rng.gamma(1.2, 1.0, size=len(US_STATES))
+    weights = weights / weights.sum()
+    out: List[TabularDataset] = []
+    for si, st in enumerate(US_STATES):
+        n = max(60, int(total_rows * weights[si]))
+        x = np.abs(rng.randn(n, f).astype(np.float32)) * rng.uniform(0.2, 3.0, size=(1, f)).astype(np.float32)
+        logits = x @ teacher * 0.6 + prior + rng.randn(n, LOAN_NUM_CLASSES).astype(np.float32) * 0.5
+        y = logits.argmax(1).astype(np.int64)
+        perm = np.random.RandomState(42 + si).permutation(n)  # stands in for random_state=42
+        n_te = int(np.ceil(n * 0.2))
+        te, tr = perm[:n_te], perm[n_te:]
+        out.append(TabularDataset(st, x[tr], y[tr], x[te], y[te], cols))
+    return out

@@ -1,0 +1,374 @@
+"""The FL round orchestrator — equivalent of the reference's ``main.py`` round loop
+(``main.py:135-235``), re-designed for one process per GPU.
+
+Per round: select clients (identically on every rank) → plan → LPT-place clients on ranks →
+grouped concurrent local training → one all-gather of client snapshots → aggregation
+(FedAvg / RFA / FoolsGold, redundantly on every rank) → batched, image-sharded evaluation
+with one counter all-reduce → CSV rows / checkpoint / metrics on rank 0.
+"""
+from __future__ import annotations
+
+import datetime
+import logging
+import os
+import time
+from typing import Any, Dict, List, Optional, Tuple
+
+import numpy as np
+import torch
+import yaml
+
+from .. import config as C
+from .. import ops
+from ..parallel.dist import DistCtx
+from ..utils import checkpoint as ckpt
+from ..utils import native
+from ..utils.csv_record import CsvRecorder
+from ..utils.observability import MetricsStream, PhaseTimer, Plotter, dict_html, setup_logger
+from . import aggregate as agg
+from .evaluate import Evaluator
+from .plan import ClientPlan, RoundPlan, build_round_plan, select_clients
+from .trainer import ClientResult, GroupTrainer
+from .workload import Workload, build_workload
+
+log = logging.getLogger("logger")
+
+
+def compute_dtype_for(params: C.Params, device: torch.device) -> torch.dtype:
+    cd = str(params["compute_dtype"]).lower()
+    if cd == "auto":
+        return torch.bfloat16 if device.type == "cuda" else torch.float32
+    return {"bf16": torch.bfloat16, "bfloat16": torch.bfloat16, "fp32": torch.float32,
+            "float32": torch.float32}[cd]
+
+
+class Server:
+    def __init__(self, params: C.Params, dctx: DistCtx, write_outputs: bool = True,
+                 folder: Optional[str] = None) -> None:
+        self.params = params
+        self.d = dctx
+        self.device = dctx.device
+        self.dtype = compute_dtype_for(params, self.device)
+        self.current_time = datetime.datetime.now().strftime("%b.%d_%H.%M.%S")
+        self.name = params.get("name", C.default_dataset_name(params.type))
+        self.write = write_outputs and dctx.is_main
+        self.folder = folder or os.path.join(params["save_dir"], f"model_{self.name}_{self.current_time}")
+        if self.write:
+            os.makedirs(self.folder, exist_ok=True)
+        setup_logger(self.folder if self.write else None, dctx.is_main)
+        log.info(f"current path: {self.folder}")
+        if not params.get("environment_name"):
+            params["environment_name"] = self.name
+        params["current_time"] = self.current_time
+        params["folder_path"] = self.folder
+
+        self.wl: Workload = build_workload(params, self.device)
+        self.spec = self.wl.spec
+        log.info("load data done")
+        self._init_model()
+        log.info("create model done")
+        if params["is_poison"]:
+            log.info(f"Poisoned following participants: {params.adversary_list}")
+        self.trainer = GroupTrainer(self.wl, params, self.dtype,
+                                    max_groups=int(params.get("max_concurrent_clients", 16)))
+        self.evaluator = Evaluator(self.wl, self.dtype, chunk=int(params["eval_batch_size"]),
+                                   max_groups=int(params.get("eval_max_groups", 24)))
+        self.fg = agg.FoolsGold(bool(params["fg_use_memory"]))
+        if getattr(self, "_fg_aux", None):
+            self.fg.load_state(self._fg_aux)
+        self.csv = CsvRecorder(self.folder, enabled=self.write)
+        self.metrics = MetricsStream(os.path.join(self.folder, "metrics.jsonl")
+                                     if (self.write and params["metrics_jsonl"]) else None)
+        self.plot = Plotter(params["environment_name"],
+                            os.path.join(self.folder, "vis_events.jsonl") if self.write else None,
+                            live=bool(params["visdom"]) and self.write)
+        self.plot.text(dict_html(params, self.current_time))
+        self.best_loss = float("inf")
+        self.timer = PhaseTimer(self.device)
+        if self.write:
+            with open(os.path.join(self.folder, "params.yaml"), "w") as f:
+                yaml.safe_dump(params.to_plain(), f)
+        self.last_round: Dict[str, Any] = {}
+
+    # ------------------------------------------------------------------ model
+    def _init_model(self) -> None:
+        p = self.params
+        self.counter = 0
+        if p["resumed_model"]:
+            path = os.path.join(p["save_dir"], str(p["resumed_model_name"]))
+            if not os.path.exists(path):
+                raise FileNotFoundError(
+                    f"resumed_model: {path} not found (pretrained checkpoints are not shipped); "
+                    f"run with resumed_model=false [start_epoch=N] or pretrain first")
+            flat, ep, lr, self.counter = ckpt.load_checkpoint(path, self.spec)
+            self.start_epoch = ep + 1
+            if lr is not None:
+                p["lr"] = float(lr)
+            log.info(f"Loaded parameters from saved model: LR is {p['lr']} and current epoch is {self.start_epoch}")
+            aux = ckpt.load_aux(path + ".aux")
+            if aux is not None:
+                ckpt.restore_rng(aux["rng"], self.wl.py_rng, self.wl.np_rng)
+                self._fg_aux = aux.get("foolsgold")
+        else:
+            flat = self.spec.init_flat(int(p["seed"]))
+            self.start_epoch = int(p.get("start_epoch") or 1)
+        self.global_state = flat.to(self.device)
+        if self.d.enabled:   # identical by construction; make it bit-identical anyway
+            self.d.broadcast_(self.global_state, 0)
+
+    # ------------------------------------------------------------------ round
+    def run_round(self, epoch: int) -> Dict[str, Any]:
+        p = self.params
+        t_round = time.perf_counter()
+        self.timer.reset()
+        with self.timer.phase("select"):
+            agents, adversarial = select_clients(p, self.wl, epoch)
+        log.info(f"Server Epoch:{epoch} choose agents : {agents}.")
+        pre_acc = None
+        if p.type == C.TYPE_LOAN and p["is_poison"] and not p["baseline"] and adversarial:
+            pre_acc = self._loan_preeval()
+        plan = build_round_plan(p, self.wl, epoch, agents, adversarial, pre_acc)
+
+        costs = [c.cost for c in plan.clients]
+        owners, _ = native.lpt_assign(costs, self.d.world)
+        mine = [c for c, o in zip(plan.clients, owners) if o == self.d.rank]
+        with self.timer.phase("train"):
+            results = self.trainer.train(mine, self.global_state)
+        with self.timer.phase("gather"):
+            bank, fg_grads, cstats = self._gather(plan, owners, results)
+        with self.timer.phase("aggregate"):
+            self._aggregate(plan, bank, fg_grads, adversarial)
+            bank[0].copy_(self.global_state)
+        with self.timer.phase("eval"):
+            acc = self.evaluator.run(bank, plan.jobs, self.d.rank, self.d.world)
+            self.d.all_reduce_(acc)
+            res = acc.cpu().numpy()
+        with self.timer.phase("io"):
+            summary = self._record(plan, res, cstats)
+            val_loss = summary["val_loss"]
+            self._save_model(epoch, val_loss)
+            self.csv.save(bool(p["is_poison"]))
+        dt = time.perf_counter() - t_round
+        phases = self.timer.reset()
+        summary.update({"epoch": epoch, "round_s": dt, "phases": phases, "clients_on_rank": len(mine),
+                        "backend": ops.backend_name(self.device)})
+        self.metrics.emit(summary)
+        log.info(f"Done in {dt} sec.")
+        self.last_round = summary
+        return summary
+
+    def run(self) -> None:
+        p = self.params
+        n = 0
+        for epoch in range(self.start_epoch, int(p["epochs"]) + 1, int(p["aggr_epoch_interval"])):
+            self.run_round(epoch)
+            n += 1
+            if p["max_rounds"] is not None and n >= int(p["max_rounds"]):
+                break
+        log.info("Saving all the graphs.")
+        log.info(f"This run has a label: {p['current_time']}. Visdom environment: {p['environment_name']}")
+
+    # ---------------------------------------------------------------- helpers
+    def _loan_preeval(self) -> float:
+        from .plan import EvalJob
+        job = EvalJob(0, "poison", self.wl.global_trigger_id, "preeval")
+        acc = self.evaluator.run(self.global_state[None], [job], self.d.rank, self.d.world)
+        self.d.all_reduce_(acc)
+        r = acc[0].cpu().numpy()
+        v = 100.0 * r[1] / max(r[2], 1)
+        log.info(v)
+        return float(v)
+
+    def _gather(self, plan: RoundPlan, owners: List[int], results: List[ClientResult]
+                ) -> Tuple[torch.Tensor, Optional[torch.Tensor], Dict[Any, Dict[str, Any]]]:
+        """All snapshots + FoolsGold grads + per-client stats onto every rank."""
+        S, P = self.spec.S, self.spec.P
+        world, rank = self.d.world, self.d.rank
+        by_name = {r.name: r for r in results}
+        slot_owner: Dict[int, int] = {}
+        for c, o in zip(plan.clients, owners):
+            for ph in c.phases:
+                for s in (ph.pre_scale_snap, ph.post_snap):
+                    if s is not None:
+                        slot_owner[s] = o
+        per_rank = [[s for s in sorted(slot_owner) if slot_owner[s] == r] for r in range(world)]
+        k_max = max(1, max(len(x) for x in per_rank))
+        local_rows = []
+        for s in per_rank[rank]:
+            for r in results:
+                if s in r.snapshots:
+                    local_rows.append(r.snapshots[s])
+                    break
+        local = torch.stack(local_rows) if local_rows else torch.zeros(0, S, device=self.device)
+        bank = torch.zeros(plan.n_snapshots, S, dtype=torch.float32, device=self.device)
+        if world == 1:
+            for i, s in enumerate(per_rank[0]):
+                bank[s] = local[i]
+        else:
+            allrows = self.d.all_gather_rows(local, k_max)
+            for r in range(world):
+                for i, s in enumerate(per_rank[r]):
+                    bank[s] = allrows[r * k_max + i]
+        fg_grads = None
+        n = len(plan.clients)
+        if self.params["aggregation_methods"] == C.AGGR_FOOLSGOLD:
+            fg_grads = torch.zeros(n, P, dtype=torch.float32, device=self.device)
+            for i, c in enumerate(plan.clients):
+                if c.name in by_name:
+                    fg_grads[i] = by_name[c.name].fg_grad
+            self.d.all_reduce_(fg_grads)
+        # per-client scalars: stats [max_slots, 3] + scale distances [interval]
+        max_slots = max(sum(ph.internal_epochs for ph in c.phases) for c in plan.clients)
+        interval = int(self.params["aggr_epoch_interval"])
+        W = max_slots * 3 + interval
+        sc = torch.zeros(n, W, dtype=torch.float64)
+        for i, c in enumerate(plan.clients):
+            r = by_name.get(c.name)
+            if r is None:
+                continue
+            st = torch.from_numpy(r.stats.astype(np.float64))
+            sc[i, :st.numel()] = st.reshape(-1)
+            for k, ph in enumerate(c.phases):
+                sc[i, max_slots * 3 + k] = r.scale_dist.get(ph.epoch, 0.0)
+        if self.d.enabled:
+            scd = sc.to(self.device)
+            self.d.all_reduce_(scd)
+            sc = scd.cpu()
+        cstats: Dict[Any, Dict[str, Any]] = {}
+        for i, c in enumerate(plan.clients):
+            st = sc[i, :max_slots * 3].reshape(max_slots, 3).numpy()
+            dists = {ph.epoch: float(sc[i, max_slots * 3 + k]) for k, ph in enumerate(c.phases)}
+            cstats[c.name] = {"stats": st, "dist": dists}
+        return bank, fg_grads, cstats
+
+    def _aggregate(self, plan: RoundPlan, bank: torch.Tensor, fg_grads: Optional[torch.Tensor],
+                   adversarial: List[Any]) -> None:
+        p = self.params
+        method = p["aggregation_methods"]
+        n_upd = self.spec.S if p["aggregate_bn_buffers"] else self.spec.P
+        finals = bank[[c.final_snap for c in plan.clients]]
+        names = [c.name for c in plan.clients]
+        dp_seed = (int(p["seed"]) * 7919 + plan.epoch) & 0x7FFFFFFF
+        if method == C.AGGR_MEAN:
+            agg.fedavg(self.global_state, finals, float(p["eta"]), int(p["no_models"]),
+                       bool(p["diff_privacy"]), float(p["sigma"]), dp_seed, n_upd)
+        elif method == C.AGGR_GEO_MED:
+            ns = [c.num_samples for c in plan.clients]
+            self._log_poison_ratio("rfa", names, ns)
+            updated, wv, alphas, calls = agg.geometric_median(
+                self.global_state, finals, ns, float(p["eta"]), int(p["geom_median_maxiter"]),
+                bool(p["diff_privacy"]), float(p["sigma"]), dp_seed, n_upd)
+            self.csv.add_weight_result(names, wv, alphas)
+            self._plot_weights(names, wv, alphas, adversarial, plan.epoch)
+        elif method == C.AGGR_FOOLSGOLD:
+            ns = [c.num_samples for c in plan.clients]
+            self._log_poison_ratio("foolsgold", names, ns)
+            t0 = time.time()
+            agg_grad, wv, alpha = self.fg.aggregate(fg_grads, names, self.spec.fg_feature_slice())
+            log.info(f"[foolsgold agg] wv: {wv}")
+            agg.foolsgold_server_step(self.global_state, agg_grad, self.spec.P, float(p["eta"]),
+                                      float(p["lr"]), float(p["decay"]))
+            print("model aggregation took {}s".format(time.time() - t0))
+            self.csv.add_weight_result(names, wv.tolist(), alpha.tolist())
+            self._plot_weights(names, wv.tolist(), alpha.tolist(), adversarial, plan.epoch)
+
+    def _log_poison_ratio(self, tag: str, names: List[Any], ns: List[int]) -> None:
+        p = self.params
+        adv = sum(n for nm, n in zip(names, ns) if p.is_adversary(nm)) / max(1, sum(ns))
+        log.info(f"[{tag} agg] training data poison_ratio: {adv}  data num: {ns}")
+        log.info(f"[{tag} agg] considering poison per batch poison_fraction: "
+                 f"{adv * p['poisoning_per_batch'] / p['batch_size']}")
+
+    def _plot_weights(self, names, wv, alphas, adversarial, epoch) -> None:
+        for nm, w, a in zip(names, wv, alphas):
+            tag = f"{nm}_poisoned" if any(C._same_client(nm, x) for x in adversarial) else str(nm)
+            self.plot.line(f"aggregation_weight_{self.current_time}", epoch, float(w), tag)
+            self.plot.line(f"fg_alpha_{self.current_time}", epoch, float(a), tag)
+
+    def _record(self, plan: RoundPlan, res: np.ndarray, cstats: Dict[Any, Dict[str, Any]]) -> Dict[str, Any]:
+        p = self.params
+        loan = p.type == C.TYPE_LOAN
+        csv = self.csv
+        out: Dict[str, Any] = {"val_loss": None}
+
+        def jres(j: int) -> Tuple[float, float, int, int]:
+            ls, corr, tot = res[j]
+            tot_i = int(round(tot))
+            corr_i = int(round(corr))
+            loss = ls / tot if tot else 0.0
+            acc = 100.0 * corr / tot if tot else 0.0
+            return float(loss), float(acc), corr_i, tot_i
+
+        cum_internal: Dict[Any, int] = {}
+        for kind, payload in plan.rows:
+            if kind == "train":
+                name, ph, ie = payload
+                st = cstats[name]["stats"][ph.stat_slot0 + ie]
+                size = int(round(st[2]))
+                total_l = float(st[0]) / size if size else 0.0
+                acc = 100.0 * float(st[1]) / size if size else 0.0
+                if loan:
+                    cum_internal[name] = cum_internal.get(name, 0) + 1
+                    tle = plan.epoch - 1 + cum_internal[name]
+                else:
+                    tle = (ph.epoch - 1) * ph.internal_epochs + ie + 1
+                tag = "PoisonTrain" if ph.poison else "Train"
+                log.info(f"___{tag} {self.spec.arch},  epoch {ph.epoch:3d}, local model {name}, "
+                         f"internal_epoch {ie + 1:3d},  Average loss: {total_l:.4f}, "
+                         f"Accuracy: {int(round(st[1]))}/{size} ({acc:.4f}%)")
+                csv.train_result.append([name, tle, ph.epoch, ie + 1, total_l, acc, int(round(st[1])), size])
+            elif kind in ("test", "poison"):
+                name, ep, j = payload
+                loss, acc, corr, tot = jres(j)
+                row = [name, ep, loss, acc, corr, tot]
+                (csv.test_result if kind == "test" else csv.posiontest_result).append(row)
+                log.info(f"___Test {name} poisoned: {kind == 'poison'}, epoch: {ep}: Average loss: {loss:.4f}, "
+                         f"Accuracy: {corr}/{tot} ({acc:.4f}%)")
+                if name == "global":
+                    if kind == "test":
+                        out["global_acc"], out["global_loss"] = acc, loss
+                        self.plot.line(f"test_acc_{self.current_time}", ep, acc, "global")
+                    else:
+                        out["global_asr"], out["poison_loss"] = acc, loss
+                        self.plot.line(f"poison_test_acc_{self.current_time}", ep, acc, "global")
+            elif kind == "trigger":
+                name, tname, ep, j = payload
+                loss, acc, corr, tot = jres(j)
+                csv.poisontriggertest_result.append([name, tname, "", ep, loss, acc, corr, tot])
+                if name == "global":
+                    out.setdefault("trigger_asr", {})[tname] = acc
+                if p["vis_trigger_split_test"]:
+                    self.plot.line(f"poison_trigger_acc_{self.current_time}", ep, acc, tname)
+            elif kind == "scale":
+                name, ph = payload
+                dist = cstats[name]["dist"].get(ph.epoch, 0.0)
+                csv.scale_temp_one_row.append(ph.epoch)
+                csv.scale_temp_one_row.append(round(dist, 4))
+                log.info(f"Scaled Norm after poisoning, distance: {dist}")
+            elif kind == "scale_acc":
+                if csv.scale_temp_one_row:
+                    csv.scale_temp_one_row.append(round(out.get("global_acc", 0.0), 4))
+        if p["is_poison"] and not p["best_on_clean_loss"]:
+            out["val_loss"] = out.get("poison_loss", out.get("global_loss"))   # D6
+        else:
+            out["val_loss"] = out.get("global_loss")
+        return out
+
+    def _save_model(self, epoch: int, val_loss: Optional[float]) -> None:
+        p = self.params
+        if not (self.write and p["save_model"]):
+            return
+        log.info("saving model")
+        name = os.path.join(self.folder, "model_last.pt.tar")
+        ckpt.save_checkpoint(name, self.spec, self.global_state, epoch, float(p["lr"]), self.counter)
+        aux = {"rng": ckpt.rng_state(self.wl.py_rng, self.wl.np_rng), "foolsgold": self.fg.state(),
+               "epoch": int(epoch)}
+        ckpt.save_aux(name + ".aux", aux)
+        if epoch in list(p["save_on_epochs"] or []):
+            log.info(f"Saving model on epoch {epoch}")
+            ckpt.save_checkpoint(f"{name}.epoch_{epoch}", self.spec, self.global_state, epoch, float(p["lr"]),
+                                 self.counter)
+            ckpt.save_aux(f"{name}.epoch_{epoch}.aux", aux)
+        if val_loss is not None and val_loss < self.best_loss:
+            ckpt.save_checkpoint(f"{name}.best", self.spec, self.global_state, epoch, float(p["lr"]), self.counter)
+            self.best_loss = val_loss

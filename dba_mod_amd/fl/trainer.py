@@ -1,0 +1,218 @@
+"""Grouped client trainer: all of a rank's clients train *concurrently* as one replica group.
+
+The reference trains the round's clients one after another on one shared model with a
+fresh optimizer each (``image_train.py:21-36``), synchronising with the host on every batch
+(``.item()`` at ``:105,223``).  Here a rank's G clients are G rows of flat ``[G, S]`` replica
+buffers; each grouped step gathers every client's next batch (one kernel), runs the
+grouped forward/backward (every conv launch covers all G clients — this is what fills 256
+CUs at batch 64), and applies a per-client SGD step with per-client learning rate and
+momentum-reset flags.  Clients with fewer steps simply go inactive (``nvalid = 0``: every
+kernel skips them) — the control flow is static, so on GPU the whole step is captured once
+into a HIP graph and replayed; per-step inputs are one packed descriptor row copied
+device-to-device before each replay.  Loss/accuracy counters stay on the device and are
+read once per round.
+"""
+from __future__ import annotations
+
+import logging
+import struct
+from dataclasses import dataclass, field
+from typing import Any, Dict, List, Optional, Tuple
+
+import numpy as np
+import torch
+
+from .. import config as C
+from .. import ops
+from ..models import program as prog
+from ..models.spec import ModelSpec
+from ..utils import native
+from .plan import ClientPlan, RoundPlan
+from .workload import Workload
+
+log = logging.getLogger("logger")
+
+
+@dataclass
+class ClientResult:
+    name: Any
+    snapshots: Dict[int, torch.Tensor]        # snapshot slot -> state [S] (device)
+    fg_grad: Optional[torch.Tensor]           # [P] summed gradients (FoolsGold)
+    stats: np.ndarray                         # [n_slots, 3] loss_sum(batch-mean), correct, count
+    scale_dist: Dict[int, float] = field(default_factory=dict)   # phase epoch -> distance
+    num_samples: int = 0
+    steps: int = 0
+
+
+class _GroupBuffers:
+    """Static per-G buffers (and the captured graph) reused across rounds."""
+
+    def __init__(self, spec: ModelSpec, G: int, B: int, max_slots: int, device: torch.device,
+                 wdtype: torch.dtype, fg: bool) -> None:
+        S, P = spec.S, spec.P
+        self.G, self.B, self.max_slots = G, B, max_slots
+        self.state = torch.zeros(G, S, dtype=torch.float32, device=device)
+        self.wcomp = self.state if wdtype == torch.float32 else torch.zeros(G, P, dtype=wdtype, device=device)
+        self.grads = torch.zeros(G, P, dtype=torch.float32, device=device)
+        self.mom = torch.zeros(G, P, dtype=torch.float32, device=device)
+        self.fg = torch.zeros(G, P, dtype=torch.float32, device=device) if fg else None
+        self.base = torch.zeros(G, S, dtype=torch.float32, device=device)   # phase-start states
+        self.stats = torch.zeros(3, G * max_slots, dtype=torch.float32, device=device)
+        self.nan_flag = torch.zeros(1, dtype=torch.float32, device=device)
+        # packed descriptor: idx[G*B] poison_n[G] trig[G] first[G] active[G] nvalid[G] slot[G] seed[G] lr[G]
+        self.D = G * B + 8 * G
+        self.desc = torch.zeros(self.D, dtype=torch.int32, device=device)
+        o = G * B
+        self.idx = self.desc[:o].view(G, B)
+        names = ["poison_n", "trig", "first", "active", "nvalid", "slot", "seed", "lr_bits"]
+        for k, n in enumerate(names):
+            setattr(self, n, self.desc[o + k * G:o + (k + 1) * G])
+        self.lr = self.lr_bits.view(torch.float32)
+        self.graph: Optional[torch.cuda.CUDAGraph] = None
+
+
+class GroupTrainer:
+    def __init__(self, wl: Workload, params: C.Params, compute_dtype: torch.dtype,
+                 max_groups: int = 16) -> None:
+        self.wl, self.params, self.spec = wl, params, wl.spec
+        self.device = wl.device
+        self.dtype = compute_dtype
+        self.max_groups = max_groups
+        self._bufs: Dict[Tuple[int, int], _GroupBuffers] = {}
+        self.use_graph = (self.device.type == "cuda" and bool(params["graph_capture"])
+                          and ops.backend_name(self.device) == "hip")
+        self.fg = params["aggregation_methods"] == C.AGGR_FOOLSGOLD
+        self.momentum = float(params["momentum"])
+        self.wd = float(params["decay"])
+        self.B = int(params["batch_size"])
+        self.target = int(params["poison_label_swap"])
+
+    # ------------------------------------------------------------------ step
+    def _step(self, b: _GroupBuffers) -> None:
+        wl = self.wl
+        if wl.kind == "image":
+            x, y = ops.gather_images(wl.train_store.images, wl.train_store.labels, b.idx, wl.trig_masks,
+                                     b.trig, b.poison_n, self.target, b.seed if wl.flip_train else None,
+                                     self.dtype)
+        else:
+            x, y = ops.gather_rows(wl.train_store.rows, wl.train_store.labels, b.idx, wl.trig_cols,
+                                   wl.trig_vals, b.trig, b.poison_n, self.target, self.dtype)
+        ctx = prog.Ctx(self.spec, b.state, b.wcomp, None, train=True, grads=b.grads,
+                       nvalid=b.nvalid, dropout_seed=b.seed, act_dtype=self.dtype)
+        logits = prog.forward(ctx, x)
+        loss, correct, dl = ops.softmax_xent(logits, y, True, True)
+        if self.spec.arch == "loan":   # reference LoanNet raises on NaN outputs (loan_model.py:25-26)
+            b.nan_flag += torch.isnan(loss).any().float()
+        b.grads.zero_()
+        ctx.tape.backward(logits, dl)
+        ops.sgd_step(b.state[:, :self.spec.P], b.grads, b.mom, b.lr, b.first, b.active, self.momentum,
+                     self.wd, shadow=(b.wcomp if b.wcomp is not b.state else None), fg_accum=b.fg)
+        flat_slot = torch.arange(b.G, device=self.device, dtype=torch.int64) * b.max_slots + b.slot.long()
+        b.stats[0].index_add_(0, flat_slot, loss)
+        b.stats[1].index_add_(0, flat_slot, correct)
+        b.stats[2].index_add_(0, flat_slot, b.nvalid.float())
+
+    def _buffers(self, G: int, max_slots: int) -> _GroupBuffers:
+        key = (G, max_slots)
+        if key not in self._bufs:
+            wdt = self.dtype if self.device.type == "cuda" else torch.float32
+            self._bufs[key] = _GroupBuffers(self.spec, G, self.B, max_slots, self.device, wdt, self.fg)
+        return self._bufs[key]
+
+    def _run_step(self, b: _GroupBuffers) -> None:
+        if not self.use_graph:
+            self._step(b)
+            return
+        if b.graph is None:
+            b.desc.copy_(b._cur)
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):   # warm-up outside capture (allocator, lazy init)
+                self._step(b)
+            torch.cuda.current_stream().wait_stream(s)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self._step(b)
+            b.graph = g
+            # the warm-up and capture executed the step twice: replay state is restored by
+            # the caller (train() re-initialises before the real loop).
+            return
+        b.graph.replay()
+
+    # ----------------------------------------------------------------- train
+    def train(self, clients: List[ClientPlan], global_state: torch.Tensor) -> List[ClientResult]:
+        out: List[ClientResult] = []
+        for w0 in range(0, len(clients), self.max_groups):
+            out.extend(self._train_wave(clients[w0:w0 + self.max_groups], global_state))
+        return out
+
+    def _train_wave(self, clients: List[ClientPlan], global_state: torch.Tensor) -> List[ClientResult]:
+        G = len(clients)
+        if G == 0:
+            return []
+        max_slots = max(sum(ph.internal_epochs for ph in c.phases) for c in clients)
+        max_slots = 1 << (max_slots - 1).bit_length()
+        b = self._buffers(G, max_slots)
+        T = max(len(c.steps) for c in clients)
+        host = native.pack_steps(clients, G, self.B, T, max_slots)   # [T, D] int32 (C++ runtime)
+        sched = torch.from_numpy(host).to(self.device, non_blocking=True)
+        if self.use_graph and b.graph is None:
+            b._cur = sched[0]
+            self._reset(b, global_state)
+            self._run_step(b)            # capture (mutates buffers; reset below)
+        self._reset(b, global_state)
+
+        events = self._events(clients)
+        snaps: Dict[int, Dict[int, torch.Tensor]] = {g: {} for g in range(G)}
+        dists: Dict[int, Dict[int, float]] = {g: {} for g in range(G)}
+        pend_dist: List[Tuple[int, int, torch.Tensor]] = []
+        for t in range(T):
+            b.desc.copy_(sched[t], non_blocking=True)
+            self._run_step(b)
+            for (g, ph) in events.get(t + 1, []):
+                self._phase_end(b, g, ph, snaps, pend_dist)
+        res: List[ClientResult] = []
+        stats = b.stats.view(3, G, b.max_slots).permute(1, 2, 0).cpu().numpy()
+        if self.spec.arch == "loan" and float(b.nan_flag.item()) > 0:
+            raise ValueError("NaN in LoanNet forward (reference loan_model.py:25-26)")
+        for g, e, d in pend_dist:
+            dists[g][e] = float(d.sqrt().item())
+        for g, c in enumerate(clients):
+            nsl = sum(ph.internal_epochs for ph in c.phases)
+            res.append(ClientResult(c.name, snaps[g], b.fg[g].clone() if b.fg is not None else None,
+                                    stats[g, :nsl].copy(), dists[g], c.num_samples, len(c.steps)))
+        return res
+
+    def _reset(self, b: _GroupBuffers, global_state: torch.Tensor) -> None:
+        b.state.copy_(global_state[None].expand_as(b.state))
+        b.base.copy_(b.state)
+        if b.wcomp is not b.state:
+            b.wcomp.copy_(b.state[:, :self.spec.P])
+        b.mom.zero_()
+        b.stats.zero_()
+        b.nan_flag.zero_()
+        if b.fg is not None:
+            b.fg.zero_()
+
+    @staticmethod
+    def _events(clients: List[ClientPlan]) -> Dict[int, List[Tuple[int, Any]]]:
+        ev: Dict[int, List[Tuple[int, Any]]] = {}
+        for g, c in enumerate(clients):
+            for ph in c.phases:
+                ev.setdefault(ph.end_step, []).append((g, ph))
+        return ev
+
+    def _phase_end(self, b: _GroupBuffers, g: int, ph, snaps, pend_dist) -> None:
+        """End of a local round: optional model-replacement scaling + snapshots."""
+        P = self.spec.P
+        if ph.pre_scale_snap is not None:
+            snaps[g][ph.pre_scale_snap] = b.state[g].clone()
+            gamma = float(self.params["scale_weights_poison"])
+            scaled = ops.scale_from_base(b.state[g], b.base[g], gamma)
+            b.state[g].copy_(scaled)
+            if b.wcomp is not b.state:
+                b.wcomp[g].copy_(b.state[g, :P])
+            # distance over parameters only (helper.model_dist_norm, helper.py:65-71)
+            pend_dist.append((g, ph.epoch, ops.sq_dists(b.state[g:g + 1, :P], b.base[g, :P])[0]))
+        snaps[g][ph.post_snap] = b.state[g].clone()
+        b.base[g].copy_(b.state[g])

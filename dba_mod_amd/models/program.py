@@ -1,0 +1,312 @@
+"""Functional model programs over grouped replicas, with a minimal reverse-mode tape.
+
+One forward definition per architecture serves three modes:
+
+* ``train`` — BatchNorm with batch statistics (running stats updated in place), every op
+  records a backward closure on a :class:`Tape`; ``Tape.backward`` writes parameter
+  gradients straight into the flat ``[G, P]`` gradient buffer (no autograd, no per-tensor
+  ``.grad``), so the whole step is a fixed launch sequence that a HIP graph can capture.
+* ``eval`` — BatchNorm folded into the conv weights/bias (:func:`fold_bank`), so every conv
+  is one kernel with a fused bias + residual + ReLU epilogue.
+
+All activations are ``[G, N, H, W, C]``: G client replicas (training) or G eval jobs, each
+selecting its weights through ``wsel``.  Reference forward definitions: see
+:mod:`dba_mod_amd.models.mirror`.
+"""
+from __future__ import annotations
+
+from typing import Callable, Dict, List, Optional, Tuple
+
+import torch
+
+from .. import ops
+from .spec import ModelSpec
+
+Tensor = torch.Tensor
+BN_EPS = 1e-5
+BN_MOMENTUM = 0.1
+
+
+class Tape:
+    """Reverse-mode tape: nodes hold (outputs, inputs, backward closure)."""
+
+    def __init__(self) -> None:
+        self.nodes: List[Tuple[Tuple[Tensor, ...], Tuple[Optional[Tensor], ...], Callable]] = []
+        self._produced: set = set()
+
+    def record(self, outputs: Tuple[Tensor, ...], inputs: Tuple[Optional[Tensor], ...], bwd: Callable) -> None:
+        self.nodes.append((outputs, inputs, bwd))
+        for o in outputs:
+            self._produced.add(id(o))
+
+    def needs_grad(self, t: Optional[Tensor]) -> bool:
+        return t is not None and id(t) in self._produced
+
+    def backward(self, out: Tensor, grad: Tensor) -> None:
+        grads: Dict[int, Tensor] = {id(out): grad}
+        for outputs, inputs, bwd in reversed(self.nodes):
+            gouts = [grads.pop(id(o), None) for o in outputs]
+            if all(g is None for g in gouts):
+                continue
+            gins = bwd(*gouts)
+            for inp, gi in zip(inputs, gins):
+                if gi is None or inp is None or not self.needs_grad(inp):
+                    continue
+                k = id(inp)
+                grads[k] = grads[k] + gi if k in grads else gi
+        self.nodes.clear()
+        self._produced.clear()
+
+
+class Ctx:
+    """Per-forward context: where the weights live, which mode, the tape.
+
+    ``state``   fp32 ``[Gm, S]`` (params | BN buffers) — master weights and running stats.
+    ``wcomp``   weights in compute dtype ``[Gm, >=P]`` (bf16 shadow on GPU; = state on CPU).
+    ``grads``   fp32 ``[G, P]`` gradient buffer (train mode only).
+    ``folded``  eval mode: {conv name: (w', b')} from :func:`fold_bank`.
+    """
+
+    def __init__(self, spec: ModelSpec, state: Tensor, wcomp: Tensor, wsel: Optional[Tensor],
+                 train: bool, grads: Optional[Tensor] = None, nvalid: Optional[Tensor] = None,
+                 folded: Optional[Dict[str, Tuple[Tensor, Tensor]]] = None,
+                 dropout_seed: Optional[Tensor] = None,
+                 act_dtype: torch.dtype = torch.float32) -> None:
+        self.spec, self.state, self.wcomp, self.wsel = spec, state, wcomp, wsel
+        self.train, self.grads, self.nvalid, self.folded = train, grads, nvalid, folded
+        self.tape = Tape() if train else None
+        self.dropout_seed = dropout_seed
+        self._drop_ctr = 0
+        self.act_dtype = act_dtype
+
+    # ----------------------------------------------------------------- weights
+    def w(self, name: str) -> Tensor:
+        return self.spec.view(self.wcomp, name)
+
+    def m(self, name: str) -> Tensor:
+        return self.spec.view(self.state, name)
+
+    def g(self, name: str) -> Tensor:
+        assert self.grads is not None
+        return self.spec.view(self.grads, name)
+
+    # ------------------------------------------------------------------ layers
+    def conv_bn(self, x: Tensor, conv: str, bn: str, stride: int, pad: int, relu: bool,
+                residual: Optional[Tensor] = None) -> Tensor:
+        if not self.train:
+            wf, bf = self.folded[conv]
+            return ops.conv2d(x, wf, self.wsel, stride, pad, bias=bf, residual=residual, relu=relu,
+                              nvalid=self.nvalid)
+        w = self.w(conv)
+        y = ops.conv2d(x, w, self.wsel, stride, pad, nvalid=self.nvalid)
+        gamma, beta = self.m(bn + ".weight"), self.m(bn + ".bias")
+        out, mean, invstd = ops.bn_train(y, gamma, beta, self.m(bn + ".running_mean"),
+                                         self.m(bn + ".running_var"), self.nvalid, BN_MOMENTUM,
+                                         BN_EPS, relu, residual)
+        in_hw = (x.shape[2], x.shape[3])
+        kh, kw = w.shape[2], w.shape[3]
+        need_dx = self.tape.needs_grad(x)
+
+        def bwd(dout: Tensor):
+            dy = ops.bn_train_bwd(dout, y, out, mean, invstd, gamma, self.nvalid, relu,
+                                  self.g(bn + ".weight"), self.g(bn + ".bias"))
+            ops.conv2d_wgrad(dy, x, stride, pad, kh, kw, self.g(conv), nvalid=self.nvalid)
+            dx = (ops.conv2d_dgrad(dy, w, self.wsel, stride, pad, in_hw, nvalid=self.nvalid)
+                  if need_dx else None)
+            dres = None
+            if residual is not None:
+                dres = ops.relu_mask_bwd(dout, out) if relu else dout
+            return dx, dres
+
+        self.tape.record((out,), (x, residual), bwd)
+        return out
+
+    def conv(self, x: Tensor, name: str, stride: int, pad: int, bias: Optional[str], relu: bool) -> Tensor:
+        """Conv with its own bias (MnistNet); also used for linear layers as 1x1 convs."""
+        if not self.train and self.folded is not None and name in self.folded:
+            w, b = self.folded[name]
+        else:
+            w, b = self.w(name), (self.m(bias) if bias is not None else None)
+        y = ops.conv2d(x, w, self.wsel, stride, pad, bias=b, relu=relu, nvalid=self.nvalid)
+        if not self.train:
+            return y
+        in_hw = (x.shape[2], x.shape[3])
+        kh, kw = w.shape[2], w.shape[3]
+        need_dx = self.tape.needs_grad(x)
+
+        def bwd(dout: Tensor):
+            d = ops.relu_mask_bwd(dout, y) if relu else dout
+            ops.conv2d_wgrad(d, x, stride, pad, kh, kw, self.g(name),
+                             self.g(bias) if bias is not None else None, nvalid=self.nvalid)
+            return (ops.conv2d_dgrad(d, w, self.wsel, stride, pad, in_hw, nvalid=self.nvalid)
+                    if need_dx else None,)
+
+        self.tape.record((y,), (x,), bwd)
+        return y
+
+    def linear(self, x: Tensor, name: str, bias: str, relu: bool) -> Tensor:
+        """x [G, N, F] -> [G, N, Out] via the 1x1-conv kernel (weights [Out, 1, 1, F])."""
+        G, N, Fd = x.shape
+        x4 = self.reshape(x, (G, N, 1, 1, Fd))
+        y4 = self._lin_conv(x4, name, bias, relu)
+        return self.reshape(y4, (G, N, y4.shape[-1]))
+
+    def _lin_conv(self, x4: Tensor, name: str, bias: str, relu: bool) -> Tensor:
+        if not self.train and self.folded is not None and name in self.folded:
+            w, b = self.folded[name]
+        else:
+            wv = self.w(name)
+            w = wv.reshape(wv.shape[0], wv.shape[1], 1, 1, wv.shape[2])
+            b = self.m(bias)
+        y = ops.conv2d(x4, w, self.wsel, 1, 0, bias=b, relu=relu, nvalid=self.nvalid)
+        if not self.train:
+            return y
+        need_dx = self.tape.needs_grad(x4)
+        gv = self.g(name)
+
+        def bwd(dout: Tensor):
+            d = ops.relu_mask_bwd(dout, y) if relu else dout
+            ops.conv2d_wgrad(d, x4, 1, 0, 1, 1, gv.reshape(gv.shape[0], gv.shape[1], 1, 1, gv.shape[2]),
+                             self.g(bias), nvalid=self.nvalid)
+            return (ops.conv2d_dgrad(d, w, self.wsel, 1, 0, (1, 1), nvalid=self.nvalid)
+                    if need_dx else None,)
+
+        self.tape.record((y,), (x4,), bwd)
+        return y
+
+    def reshape(self, x: Tensor, shape: Tuple[int, ...]) -> Tensor:
+        y = x.reshape(shape)
+        if self.train and y is not x:
+            in_shape = x.shape
+            self.tape.record((y,), (x,), lambda d: (d.reshape(in_shape),))
+        return y
+
+    def maxpool(self, x: Tensor, k: int, s: int, p: int) -> Tensor:
+        y, ind = ops.maxpool2d(x, k, s, p)
+        if self.train:
+            shp = tuple(x.shape)
+            self.tape.record((y,), (x,), lambda d: (ops.maxpool2d_bwd(d, ind, shp),))
+        return y
+
+    def gap(self, x: Tensor) -> Tensor:
+        y = ops.avgpool_global(x)
+        if self.train:
+            hw = (x.shape[2], x.shape[3])
+            self.tape.record((y,), (x,), lambda d: (ops.avgpool_global_bwd(d, hw),))
+        return y
+
+    def dropout(self, x: Tensor, p: float) -> Tensor:
+        if not self.train:
+            return x
+        seeds, salt = self.dropout_seed, self._drop_ctr
+        self._drop_ctr += 1
+        y = ops.dropout(x, p, seeds, salt)
+        self.tape.record((y,), (x,), lambda d: (ops.dropout_bwd(d, p, seeds, salt),))
+        return y
+
+
+# ------------------------------------------------------------------- architectures
+def _resnet_cifar(ctx: Ctx, x: Tensor) -> Tensor:
+    out = ctx.conv_bn(x, "conv1.weight", "bn1", 1, 1, relu=True)
+    cin = 32
+    for li, w in enumerate((32, 64, 128, 256)):
+        for bi in range(2):
+            stride = 2 if (li > 0 and bi == 0) else 1
+            pre = f"layer{li + 1}.{bi}."
+            a = ctx.conv_bn(out, pre + "conv1.weight", pre + "bn1", stride, 1, relu=True)
+            if stride != 1 or cin != w:
+                sc = ctx.conv_bn(out, pre + "shortcut.0.weight", pre + "shortcut.1", stride, 0, relu=False)
+            else:
+                sc = out
+            out = ctx.conv_bn(a, pre + "conv2.weight", pre + "bn2", 1, 1, relu=True, residual=sc)
+            cin = w
+    out = ctx.gap(out)
+    G, N = out.shape[:2]
+    return ctx.linear(ctx.reshape(out, (G, N, out.shape[-1])), "linear.weight", "linear.bias", relu=False)
+
+
+def _resnet_tiny(ctx: Ctx, x: Tensor) -> Tensor:
+    out = ctx.conv_bn(x, "conv1.weight", "bn1", 2, 3, relu=True)
+    out = ctx.maxpool(out, 3, 2, 1)
+    cin = 64
+    for li, w in enumerate((64, 128, 256, 512)):
+        for bi in range(2):
+            stride = 2 if (li > 0 and bi == 0) else 1
+            pre = f"layer{li + 1}.{bi}."
+            if stride != 1 or cin != w:
+                sc = ctx.conv_bn(out, pre + "downsample.0.weight", pre + "downsample.1", stride, 0, relu=False)
+            else:
+                sc = out
+            a = ctx.conv_bn(out, pre + "conv1.weight", pre + "bn1", stride, 1, relu=True)
+            out = ctx.conv_bn(a, pre + "conv2.weight", pre + "bn2", 1, 1, relu=True, residual=sc)
+            cin = w
+    out = ctx.gap(out)
+    G, N = out.shape[:2]
+    return ctx.linear(ctx.reshape(out, (G, N, out.shape[-1])), "fc.weight", "fc.bias", relu=False)
+
+
+def _mnist(ctx: Ctx, x: Tensor) -> Tensor:
+    a = ctx.conv(x, "conv1.weight", 1, 0, "conv1.bias", relu=True)
+    a = ctx.maxpool(a, 2, 2, 0)
+    b = ctx.conv(a, "conv2.weight", 1, 0, "conv2.bias", relu=True)
+    b = ctx.maxpool(b, 2, 2, 0)
+    G, N = b.shape[:2]
+    f = ctx.reshape(b, (G, N, -1))
+    h = ctx.linear(f, "fc1.weight", "fc1.bias", relu=True)
+    # log_softmax of the reference is folded into the loss (idempotent, quirk D7)
+    return ctx.linear(h, "fc2.weight", "fc2.bias", relu=False)
+
+
+def _loan(ctx: Ctx, x: Tensor) -> Tensor:
+    h = ctx.linear(x, "layer1.0.weight", "layer1.0.bias", relu=True)
+    h = ctx.dropout(h, 0.5)
+    h = ctx.linear(h, "layer2.0.weight", "layer2.0.bias", relu=True)
+    h = ctx.dropout(h, 0.5)
+    return ctx.linear(h, "layer3.0.weight", "layer3.0.bias", relu=False)
+
+
+FORWARDS: Dict[str, Callable[[Ctx, Tensor], Tensor]] = {
+    "resnet18_cifar": _resnet_cifar, "resnet18_tiny": _resnet_tiny, "mnist": _mnist, "loan": _loan,
+}
+
+
+def forward(ctx: Ctx, x: Tensor) -> Tensor:
+    return FORWARDS[ctx.spec.arch](ctx, x)
+
+
+# ------------------------------------------------------------------------ BN folding
+def _conv_bn_pairs(spec: ModelSpec) -> List[Tuple[str, str]]:
+    pairs = []
+    for e in spec.params:
+        if e.kind != "conv_w":
+            continue
+        n = e.name
+        if n.endswith("shortcut.0.weight"):
+            pairs.append((n, n.replace("shortcut.0.weight", "shortcut.1")))
+        elif n.endswith("downsample.0.weight"):
+            pairs.append((n, n.replace("downsample.0.weight", "downsample.1")))
+        else:
+            bn = n.replace("conv", "bn").replace(".weight", "")
+            if bn + ".weight" in spec.by_name:
+                pairs.append((n, bn))
+    return pairs
+
+
+def fold_bank(spec: ModelSpec, state: Tensor, dtype: torch.dtype) -> Dict[str, Tuple[Tensor, Tensor]]:
+    """Eval weights for a ``[Gm, S]`` bank of model states: BN folded into each conv; plain
+    convs/linears converted to the compute dtype with their fp32 bias."""
+    out: Dict[str, Tuple[Tensor, Tensor]] = {}
+    for conv, bn in _conv_bn_pairs(spec):
+        out[conv] = ops.bn_fold(spec.view(state, conv), None, spec.view(state, bn + ".weight"),
+                                spec.view(state, bn + ".bias"), spec.view(state, bn + ".running_mean"),
+                                spec.view(state, bn + ".running_var"), BN_EPS, dtype)
+    for e in spec.params:
+        if e.name in out or e.kind not in ("conv_w", "lin_w"):
+            continue
+        bias = e.name.replace(".weight", ".bias")
+        w = spec.view(state, e.name)
+        if w.dim() == 3:  # linear [Gm, Out, In] -> [Gm, Out, 1, 1, In]
+            w = w.reshape(w.shape[0], w.shape[1], 1, 1, w.shape[2])
+        b = spec.view(state, bias).contiguous() if bias in spec.by_name else None
+        out[e.name] = (w.to(dtype).contiguous(), b)
+    return out

@@ -1,0 +1,60 @@
+"""Framework ops: one entry point per kernel, dispatched by the tensors' device.
+
+* GPU tensors run the hand-written CDNA4 HIP kernels of ``csrc/kernels`` (gfx950), loaded
+  from the in-tree ``libdba_kernels.so`` through :mod:`dba_mod_amd.ops.hip`.  If that
+  library is missing on a GPU box the call fails loudly — there is no silent fallback.
+* CPU tensors run :mod:`dba_mod_amd.ops.reference` (plain PyTorch fp32), which is also the
+  numerics oracle of the GPU tests.
+
+``DBA_OPS=reference`` forces the reference implementation on GPU tensors too (explicit
+A/B baselining only; bench.py reports which backend ran).
+"""
+from __future__ import annotations
+
+import os
+from typing import Any
+
+import torch
+
+from . import reference as _ref
+
+_FORCE_REF = os.environ.get("DBA_OPS", "").lower() == "reference"
+_hip_mod = None
+
+
+def hip_module():
+    global _hip_mod
+    if _hip_mod is None:
+        from . import hip as _h  # raises with a clear message if the .so is missing
+        _hip_mod = _h
+    return _hip_mod
+
+
+def backend_for(t: torch.Tensor):
+    if t.is_cuda and not _FORCE_REF:
+        return hip_module()
+    return _ref
+
+
+def backend_name(device: torch.device) -> str:
+    return "hip" if (device.type == "cuda" and not _FORCE_REF) else "reference"
+
+
+def _dispatch(name: str):
+    def fn(*args: Any, **kw: Any):
+        first = next(a for a in list(args) + list(kw.values()) if isinstance(a, torch.Tensor))
+        return getattr(backend_for(first), name)(*args, **kw)
+    fn.__name__ = name
+    fn.__doc__ = getattr(_ref, name).__doc__
+    return fn
+
+
+_OPS = ["gather_images", "gather_rows", "conv2d", "conv2d_dgrad", "conv2d_wgrad", "bn_train",
+        "bn_train_bwd", "relu_mask_bwd", "bn_fold", "maxpool2d", "maxpool2d_bwd", "avgpool_global",
+        "avgpool_global_bwd", "dropout", "dropout_bwd", "softmax_xent", "sgd_step",
+        "scale_from_base", "add_noise_scaled", "sq_dists", "weighted_sum", "gram"]
+
+for _n in _OPS:
+    globals()[_n] = _dispatch(_n)
+
+__all__ = list(_OPS) + ["backend_for", "backend_name", "hip_module"]

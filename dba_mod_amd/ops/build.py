@@ -1,0 +1,110 @@
+"""In-tree build of the native libraries.
+
+* ``libdba_kernels.so`` — every HIP kernel (``csrc/kernels/*.hip``), compiled by ``hipcc
+  --offload-arch=gfx950`` into one code object per source and linked into one shared
+  library with a C ABI (launchers take raw device pointers + the caller's HIP stream).
+* ``libdba_runtime.so`` — the host runtime (``csrc/runtime/*.cpp``), plain g++.
+
+Both land in ``dba_mod_amd/_lib/`` so they travel with the repo snapshot to the GPU box
+(they are git-ignored, not gpurun-ignored).  ``python -m dba_mod_amd.ops.build`` rebuilds.
+"""
+from __future__ import annotations
+
+import glob
+import os
+import subprocess
+import sys
+import time
+from concurrent.futures import ThreadPoolExecutor
+from typing import List
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+LIBDIR = os.path.join(ROOT, "dba_mod_amd", "_lib")
+CSRC = os.path.join(ROOT, "csrc")
+ARCH = os.environ.get("DBA_OFFLOAD_ARCH", "gfx950")
+
+
+def kernels_path() -> str:
+    return os.path.join(LIBDIR, "libdba_kernels.so")
+
+
+def runtime_path() -> str:
+    return os.path.join(LIBDIR, "libdba_runtime.so")
+
+
+def _srcs(sub: str, ext: str) -> List[str]:
+    return sorted(glob.glob(os.path.join(CSRC, sub, f"*{ext}")))
+
+
+def _newest(paths: List[str]) -> float:
+    return max([os.path.getmtime(p) for p in paths] or [0.0])
+
+
+def runtime_stale() -> bool:
+    p = runtime_path()
+    return (not os.path.exists(p)) or _newest(_srcs("runtime", ".cpp")) > os.path.getmtime(p)
+
+
+def kernels_stale() -> bool:
+    p = kernels_path()
+    deps = _srcs("kernels", ".hip") + _srcs("kernels", ".hpp")
+    return (not os.path.exists(p)) or _newest(deps) > os.path.getmtime(p)
+
+
+def _run(cmd: List[str]) -> None:
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"build failed: {' '.join(cmd)}\n{r.stdout}")
+
+
+def build_runtime(verbose: bool = False) -> str:
+    os.makedirs(LIBDIR, exist_ok=True)
+    out = runtime_path()
+    tmp = out + f".tmp{os.getpid()}"
+    _run(["g++", "-O3", "-std=c++17", "-shared", "-fPIC", "-o", tmp] + _srcs("runtime", ".cpp"))
+    os.replace(tmp, out)
+    if verbose:
+        print(f"built {out}")
+    return out
+
+
+def build_kernels(verbose: bool = False, jobs: int = 8) -> str:
+    os.makedirs(LIBDIR, exist_ok=True)
+    objdir = os.path.join(LIBDIR, "obj")
+    os.makedirs(objdir, exist_ok=True)
+    hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+    srcs = _srcs("kernels", ".hip")
+    hdr_time = _newest(_srcs("kernels", ".hpp"))
+    flags = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-munsafe-fp-atomics",
+             "-I", os.path.join(CSRC, "kernels")]
+
+    def one(src: str) -> str:
+        obj = os.path.join(objdir, os.path.basename(src) + ".o")
+        if os.path.exists(obj) and os.path.getmtime(obj) >= max(os.path.getmtime(src), hdr_time):
+            return obj
+        t0 = time.time()
+        _run([hipcc] + flags + ["-c", src, "-o", obj + ".tmp"])
+        os.replace(obj + ".tmp", obj)
+        if verbose:
+            print(f"  {os.path.basename(src)}: {time.time() - t0:.1f}s")
+        return obj
+
+    with ThreadPoolExecutor(max_workers=max(1, min(jobs, len(srcs)))) as ex:
+        objs = list(ex.map(one, srcs))
+    out = kernels_path()
+    tmp = out + f".tmp{os.getpid()}"
+    _run([hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", tmp] + objs)
+    os.replace(tmp, out)
+    if verbose:
+        print(f"built {out}")
+    return out
+
+
+def build_all(verbose: bool = True) -> None:
+    build_runtime(verbose)
+    build_kernels(verbose)
+
+
+if __name__ == "__main__":
+    build_all(verbose=True)
+    sys.exit(0)

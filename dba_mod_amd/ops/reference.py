@@ -1,0 +1,362 @@
+"""Plain-PyTorch fp32 reference implementation of every framework op.
+
+This is (a) the implementation used for CPU tensors (the world_size=1 plumbing config and
+the unit tests) and (b) the numerics oracle the HIP kernels are tested against.  Layouts
+are the device layouts: activations ``[G, N, H, W, C]`` (group = client replica / eval job),
+conv weights ``[Gm, Cout, KH, KW, Cin]`` (possibly a strided view into a flat parameter
+buffer), per-group model selection ``wsel`` (group -> weight slot).
+
+Semantics follow the reference's stock-PyTorch ops: BatchNorm2d in
+train mode (biased var to normalise, unbiased var into running stats, momentum 0.1),
+cross-entropy mean/sum reductions, ``torch.optim.SGD`` with momentum + weight decay.
+"""
+from __future__ import annotations
+
+from typing import Optional, Sequence, Tuple
+
+import torch
+import torch.nn.functional as F
+
+from . import rng
+
+Tensor = torch.Tensor
+
+
+def _sel(w: Tensor, wsel: Optional[Tensor], g: int) -> Tensor:
+    return w[int(wsel[g])] if wsel is not None else w[g]
+
+
+def _nchw(x: Tensor) -> Tensor:
+    return x.permute(0, 3, 1, 2)
+
+
+def _nhwc(x: Tensor) -> Tensor:
+    return x.permute(0, 2, 3, 1)
+
+
+# Compute dtype of the reference implementation: fp32 (the kernels' accumulation dtype);
+# tests switch it to fp64 to get an oracle free of fp32 ReLU-mask flips.
+COMPUTE_DTYPE = torch.float32
+
+
+def _cdt() -> torch.dtype:
+    return COMPUTE_DTYPE
+
+
+def _rows_valid(nvalid: Optional[Tensor], g: int, n: int) -> int:
+    return n if nvalid is None else int(nvalid[g])
+
+
+# ------------------------------------------------------------------------- data ingest
+def gather_images(src: Tensor, labels: Tensor, idx: Tensor, trig_masks: Tensor, trig_id: Tensor,
+                  poison_n: Tensor, target: int, flip_seeds: Optional[Tensor], out_dtype: torch.dtype
+                  ) -> Tuple[Tensor, Tensor]:
+    """uint8 NHWC gather + /255 + optional h-flip + pixel trigger + relabel (K17/K19).
+
+    Row ``b`` of group ``g`` is flipped iff ``hash2(flip_seeds[g], b) & 1`` (per-client
+    seeds keep the result independent of how clients are placed on ranks/groups).
+    """
+    G, B = idx.shape
+    _, H, W, C = src.shape
+    valid = idx >= 0
+    safe = idx.clamp(min=0).long()
+    x = src[safe.reshape(-1)].reshape(G, B, H, W, C).to(torch.float32)
+    y = labels.long()[safe.reshape(-1)].reshape(G, B)
+    if flip_seeds is not None:
+        ctr = torch.arange(B, dtype=torch.int64, device=src.device)[None, :].expand(G, B)
+        flip = (rng.hash2(flip_seeds.to(torch.int64)[:, None], ctr) & 1).bool()
+        x = torch.where(flip[..., None, None, None], x.flip(3), x)
+    b_ar = torch.arange(B, device=src.device)[None, :]
+    tid = trig_id.long()
+    pois = (b_ar < poison_n.long()[:, None]) & (tid[:, None] >= 0) & valid
+    if trig_masks.numel() > 0:
+        m = trig_masks[tid.clamp(min=0)].bool()  # [G, H, W]
+        pm = pois[:, :, None, None] & m[:, None, :, :]
+        x = torch.where(pm[..., None], torch.full_like(x, 255.0), x)
+    y = torch.where(pois, torch.full_like(y, int(target)), y)
+    x = x * (1.0 / 255.0)
+    x = torch.where(valid[..., None, None, None], x, torch.zeros_like(x))
+    y = torch.where(valid, y, torch.full_like(y, -1))
+    return x.to(out_dtype), y.to(torch.int32)
+
+
+def gather_rows(src: Tensor, labels: Tensor, idx: Tensor, trig_cols: Tensor, trig_vals: Tensor,
+                trig_id: Tensor, poison_n: Tensor, target: int, out_dtype: torch.dtype
+                ) -> Tuple[Tensor, Tensor]:
+    """Tabular (LOAN) gather + feature trigger (K18): x[:, col] = value for poisoned rows."""
+    G, B = idx.shape
+    Fd = src.shape[1]
+    valid = idx >= 0
+    safe = idx.clamp(min=0).long()
+    x = src[safe.reshape(-1)].reshape(G, B, Fd).to(torch.float32).clone()
+    y = labels.long()[safe.reshape(-1)].reshape(G, B)
+    b_ar = torch.arange(B, device=src.device)[None, :]
+    tid = trig_id.long()
+    pois = (b_ar < poison_n.long()[:, None]) & (tid[:, None] >= 0) & valid
+    for g in range(G):
+        if int(tid[g]) < 0:
+            continue
+        cols = trig_cols[int(tid[g])]
+        vals = trig_vals[int(tid[g])]
+        rows = pois[g].nonzero().flatten()
+        for k in range(cols.shape[0]):
+            c = int(cols[k])
+            if c >= 0:
+                x[g, rows, c] = float(vals[k])
+    y = torch.where(pois, torch.full_like(y, int(target)), y)
+    x = torch.where(valid[..., None], x, torch.zeros_like(x))
+    y = torch.where(valid, y, torch.full_like(y, -1))
+    return x.to(out_dtype), y.to(torch.int32)
+
+
+# ------------------------------------------------------------------------------ conv
+def conv2d(x: Tensor, w: Tensor, wsel: Optional[Tensor], stride: int, pad: int,
+           bias: Optional[Tensor] = None, residual: Optional[Tensor] = None,
+           relu: bool = False, nvalid: Optional[Tensor] = None,
+           out_dtype: Optional[torch.dtype] = None) -> Tensor:
+    """y = act(conv(x, w) + bias + residual); NHWC in/out (K1, K3, K4, K8)."""
+    G = x.shape[0]
+    outs = []
+    for g in range(G):
+        wg = _sel(w, wsel, g).to(_cdt()).permute(0, 3, 1, 2)  # [Cout, Cin, KH, KW]
+        bg = _sel(bias, wsel, g).to(_cdt()) if bias is not None else None
+        yg = F.conv2d(_nchw(x[g].to(_cdt())), wg, bg, stride=stride, padding=pad)
+        yg = _nhwc(yg)
+        if residual is not None:
+            yg = yg + residual[g].to(_cdt())
+        if relu:
+            yg = torch.relu(yg)
+        outs.append(yg)
+    return torch.stack(outs).to(out_dtype or x.dtype)
+
+
+def conv2d_dgrad(dy: Tensor, w: Tensor, wsel: Optional[Tensor], stride: int, pad: int,
+                 in_hw: Tuple[int, int], nvalid: Optional[Tensor] = None,
+                 out_dtype: Optional[torch.dtype] = None) -> Tensor:
+    G, N = dy.shape[:2]
+    cin = w.shape[-1]
+    outs = []
+    for g in range(G):
+        wg = _sel(w, wsel, g).to(_cdt()).permute(0, 3, 1, 2)
+        dx = torch.nn.grad.conv2d_input((N, cin, in_hw[0], in_hw[1]), wg, _nchw(dy[g].to(_cdt())),
+                                        stride=stride, padding=pad)
+        outs.append(_nhwc(dx))
+    return torch.stack(outs).to(out_dtype or dy.dtype)
+
+
+def conv2d_wgrad(dy: Tensor, x: Tensor, stride: int, pad: int, kh: int, kw: int,
+                 dw: Tensor, dbias: Optional[Tensor] = None, nvalid: Optional[Tensor] = None) -> None:
+    """dw[g] += sum_rows dy (x) x  (fp32 accumulate into the flat grad buffer view)."""
+    G = dy.shape[0]
+    cout = dy.shape[-1]
+    cin = x.shape[-1]
+    for g in range(G):
+        gw = torch.nn.grad.conv2d_weight(_nchw(x[g].to(_cdt())), (cout, cin, kh, kw),
+                                         _nchw(dy[g].to(_cdt())), stride=stride, padding=pad)
+        dw[g] += gw.permute(0, 2, 3, 1)
+        if dbias is not None:
+            dbias[g] += dy[g].to(_cdt()).sum(dim=(0, 1, 2))
+
+
+# ------------------------------------------------------------------------ batch norm
+def bn_train(y: Tensor, gamma: Tensor, beta: Tensor, rmean: Tensor, rvar: Tensor,
+             nvalid: Optional[Tensor], momentum: float, eps: float, relu: bool,
+             residual: Optional[Tensor]) -> Tuple[Tensor, Tensor, Tensor]:
+    """Training-mode BN over valid rows (+residual, +ReLU); updates running stats in place."""
+    G, N = y.shape[:2]
+    C = y.shape[-1]
+    out = torch.zeros_like(y)
+    means = torch.zeros(G, C, dtype=_cdt(), device=y.device)
+    invstds = torch.zeros(G, C, dtype=_cdt(), device=y.device)
+    for g in range(G):
+        n = _rows_valid(nvalid, g, N)
+        if n == 0:
+            continue
+        yg = y[g, :n].to(_cdt())
+        flat = yg.reshape(-1, C)
+        cnt = flat.shape[0]
+        mean = flat.mean(0)
+        var = flat.var(0, unbiased=False)
+        invstd = torch.rsqrt(var + eps)
+        o = (yg - mean) * invstd * gamma[g].to(_cdt()) + beta[g].to(_cdt())
+        if residual is not None:
+            o = o + residual[g, :n].to(_cdt())
+        if relu:
+            o = torch.relu(o)
+        out[g, :n] = o.to(out.dtype)
+        unbiased = var * (cnt / max(cnt - 1, 1))
+        rmean[g] = (1 - momentum) * rmean[g] + momentum * mean
+        rvar[g] = (1 - momentum) * rvar[g] + momentum * unbiased
+        means[g] = mean
+        invstds[g] = invstd
+    return out, means, invstds
+
+
+def bn_train_bwd(dout: Tensor, y: Tensor, out: Tensor, mean: Tensor, invstd: Tensor,
+                 gamma: Tensor, nvalid: Optional[Tensor], relu: bool, dgamma: Tensor,
+                 dbeta: Tensor) -> Tensor:
+    """Backward of bn_train; returns d(pre-BN input) and, via relu mask, the grad that also
+    flows to the residual (= masked dout, returned by the caller when needed)."""
+    G, N = y.shape[:2]
+    C = y.shape[-1]
+    dy = torch.zeros_like(y)
+    for g in range(G):
+        n = _rows_valid(nvalid, g, N)
+        if n == 0:
+            continue
+        d = dout[g, :n].to(_cdt())
+        if relu:
+            d = d * (out[g, :n].to(_cdt()) > 0)
+        xhat = (y[g, :n].to(_cdt()) - mean[g]) * invstd[g]
+        cnt = d.numel() // C
+        sd = d.reshape(-1, C).sum(0)
+        sdx = (d * xhat).reshape(-1, C).sum(0)
+        dgamma[g] += sdx
+        dbeta[g] += sd
+        dx = gamma[g].to(_cdt()) * invstd[g] / cnt * (cnt * d - sd - xhat * sdx)
+        dy[g, :n] = dx.to(dy.dtype)
+    return dy
+
+
+def relu_mask_bwd(dout: Tensor, out: Tensor) -> Tensor:
+    return (dout.to(_cdt()) * (out.to(_cdt()) > 0)).to(dout.dtype)
+
+
+def bn_fold(w: Tensor, conv_bias: Optional[Tensor], gamma: Tensor, beta: Tensor,
+            rmean: Tensor, rvar: Tensor, eps: float, out_dtype: torch.dtype) -> Tuple[Tensor, Tensor]:
+    """Eval-mode BN folded into the preceding conv: w' = w*s, b' = (b - mean)*s + beta."""
+    s = gamma.to(_cdt()) * torch.rsqrt(rvar.to(_cdt()) + eps)  # [Gm, Cout]
+    wf = w.to(_cdt()) * s[:, :, None, None, None]
+    b0 = conv_bias.to(_cdt()) if conv_bias is not None else torch.zeros_like(s)
+    bf = (b0 - rmean.to(_cdt())) * s + beta.to(_cdt())
+    return wf.to(out_dtype), bf.contiguous()
+
+
+# --------------------------------------------------------------------------- pooling
+def maxpool2d(x: Tensor, k: int, s: int, p: int) -> Tuple[Tensor, Tensor]:
+    G, N, H, W, C = x.shape
+    y, ind = F.max_pool2d(_nchw(x.to(_cdt()).reshape(G * N, H, W, C)), k, s, p, return_indices=True)
+    return (_nhwc(y).reshape(G, N, y.shape[2], y.shape[3], C).to(x.dtype),
+            _nhwc(ind).reshape(G, N, y.shape[2], y.shape[3], C).to(torch.int32))
+
+
+def maxpool2d_bwd(dy: Tensor, ind: Tensor, in_shape: Sequence[int]) -> Tensor:
+    G, N, H, W, C = in_shape
+    Ho, Wo = dy.shape[2], dy.shape[3]
+    dyn = _nchw(dy.to(_cdt()).reshape(G * N, Ho, Wo, C)).contiguous()
+    indn = _nchw(ind.long().reshape(G * N, Ho, Wo, C)).contiguous()
+    dx = torch.zeros(G * N, C, H * W, dtype=_cdt(), device=dy.device)
+    dx.scatter_add_(2, indn.reshape(G * N, C, -1), dyn.reshape(G * N, C, -1))
+    return _nhwc(dx.reshape(G * N, C, H, W)).reshape(G, N, H, W, C).to(dy.dtype)
+
+
+def avgpool_global(x: Tensor) -> Tensor:
+    return x.to(_cdt()).mean(dim=(2, 3), keepdim=True).to(x.dtype)
+
+
+def avgpool_global_bwd(dy: Tensor, hw: Tuple[int, int]) -> Tensor:
+    H, W = hw
+    return (dy.to(_cdt()).expand(-1, -1, H, W, -1) / (H * W)).to(dy.dtype).contiguous()
+
+
+# --------------------------------------------------------------------------- dropout
+def dropout(x: Tensor, p: float, seeds: Tensor, salt: int) -> Tensor:
+    """Inverted dropout; element i of group g kept iff uniform(salted(seeds[g]), i) >= p."""
+    G = x.shape[0]
+    per = x[0].numel()
+    ctr = torch.arange(per, dtype=torch.int64, device=x.device)[None, :].expand(G, per)
+    s = rng.salted(seeds.to(torch.int64), salt)[:, None]
+    keep = (rng.uniform01(s, ctr) >= p).reshape(x.shape)
+    return (x.to(_cdt()) * keep / (1.0 - p)).to(x.dtype)
+
+
+def dropout_bwd(dy: Tensor, p: float, seeds: Tensor, salt: int) -> Tensor:
+    return dropout(dy, p, seeds, salt)
+
+
+# ---------------------------------------------------------------------------- loss
+def softmax_xent(logits: Tensor, labels: Tensor, mean: bool, want_grad: bool
+                 ) -> Tuple[Tensor, Tensor, Optional[Tensor]]:
+    """Per-group CE (mean over valid rows or sum) + correct count + dlogits (K9).
+
+    Rows with label < 0 are padding.  dlogits corresponds to the *mean* loss when
+    ``mean`` (training) and to the sum otherwise.
+    """
+    G, B, C = logits.shape
+    lf = logits.to(_cdt())
+    lab = labels.long()
+    valid = lab >= 0
+    logp = torch.log_softmax(lf, dim=-1)
+    nll = -logp.gather(-1, lab.clamp(min=0)[..., None]).squeeze(-1)
+    nll = torch.where(valid, nll, torch.zeros_like(nll))
+    cnt = valid.sum(1).clamp(min=1).to(_cdt())
+    loss = nll.sum(1) / cnt if mean else nll.sum(1)
+    pred = lf.argmax(-1)
+    correct = ((pred == lab) & valid).sum(1).to(_cdt())
+    dl = None
+    if want_grad:
+        dl = torch.softmax(lf, -1)
+        dl = dl - F.one_hot(lab.clamp(min=0), C).to(_cdt())
+        dl = torch.where(valid[..., None], dl, torch.zeros_like(dl))
+        if mean:
+            dl = dl / cnt[:, None, None]
+        dl = dl.to(logits.dtype)
+    return loss, correct, dl
+
+
+# ------------------------------------------------------------------------- optimizer
+def sgd_step(params: Tensor, grads: Tensor, mom: Tensor, lr: Tensor, first: Tensor, active: Tensor,
+             momentum: float, wd: float, shadow: Optional[Tensor] = None,
+             fg_accum: Optional[Tensor] = None) -> None:
+    """torch.optim.SGD(momentum, weight_decay) on [G, P] flat buffers (K10).
+
+    ``first[g]`` marks the first step of a freshly created optimizer (buffer := d_p).
+    ``fg_accum`` (FoolsGold) accumulates the raw per-batch gradients (image_train.py:94-100).
+    """
+    for g in range(params.shape[0]):
+        if int(active[g]) == 0:
+            continue
+        gr = grads[g]
+        if fg_accum is not None:
+            fg_accum[g] += gr
+        dp = gr + wd * params[g]
+        if int(first[g]):
+            mom[g] = dp
+        else:
+            mom[g] = momentum * mom[g] + dp
+        params[g] -= float(lr[g]) * mom[g]
+        if shadow is not None:
+            shadow[g] = params[g].to(shadow.dtype)
+
+
+# ---------------------------------------------------------------- flat / aggregation
+def scale_from_base(w: Tensor, base: Tensor, gamma: float) -> Tensor:
+    """Model-replacement scaling w' = base + gamma (w - base) (K11, image_train.py:166-171)."""
+    return base + (w - base) * gamma
+
+
+def add_noise_scaled(dst: Tensor, upd: Tensor, coef: float, sigma: float, seed: int,
+                     noise: bool) -> None:
+    """dst += coef*upd (+ N(0, sigma) per element if noise)  (K12, helper.py:240-257)."""
+    u = upd * coef
+    if noise:
+        ctr = torch.arange(u.numel(), dtype=torch.int64, device=u.device).reshape(u.shape)
+        u = u + sigma * rng.normal(seed, ctr)
+    dst += u
+
+
+def sq_dists(points: Tensor, m: Tensor) -> Tensor:
+    """||points[i] - m||^2 for all i in one pass (K13)."""
+    d = points.double() - m.double()[None]
+    return (d * d).sum(1)
+
+
+def weighted_sum(points: Tensor, wts: Tensor) -> Tensor:
+    """sum_i wts[i] * points[i] (K14/K16)."""
+    return (wts.double()[:, None] * points.double()).sum(0).to(points.dtype)
+
+
+def gram(feats: Tensor) -> Tensor:
+    """F F^T in float64 (K15)."""
+    f = feats.double()
+    return f @ f.t()
