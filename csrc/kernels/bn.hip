@@ -1,0 +1,280 @@
+// Training-mode BatchNorm for grouped NHWC activations and the
+// eval-mode BN fold into the preceding conv.
+//
+//   stats   : per-(group, channel) sum / sum-of-squares over the group's VALID rows
+//             (fp32 per-thread partials, fp64 cross-block atomics — no cancellation issue
+//             at CIFAR/Tiny row counts);
+//   finalize: mean, 1/std, running-stat update (unbiased var, momentum) in place in the
+//             flat replica state;
+//   apply   : y -> (y-mean)*invstd*gamma + beta (+residual) (ReLU), padded rows zeroed;
+//   backward: one fused reduce (sum d, sum d*xhat with the ReLU mask recomputed from the
+//             forward output) + one fused apply that also emits the residual-branch grad.
+#include "common.hpp"
+#include <algorithm>
+
+namespace {
+
+constexpr int kRowsPerBlock = 512;
+
+// sums[g][0][c] += sum x ; sums[g][1][c] += sum x^2   (STATS)
+// sums[g][0][c] += sum d ; sums[g][1][c] += sum d*xhat (BWD)
+template <bool BWD>
+__global__ __launch_bounds__(256) void bn_reduce_kernel(const uint16_t* __restrict__ y, const uint16_t* __restrict__ dout,
+                                                        const uint16_t* __restrict__ out, const float* __restrict__ mean,
+                                                        const float* __restrict__ invstd, int relu,
+                                                        const int* __restrict__ nvalid, int N, int HW, int C,
+                                                        double* __restrict__ sums) {
+  __shared__ float red[2][256][8];
+  const int g = blockIdx.y;
+  const int R = N * HW;
+  const int Rv = valid_rows(nvalid, g, N) * HW;
+  const int r0 = blockIdx.x * kRowsPerBlock;
+  if (r0 >= Rv) return;
+  const int r1 = min(Rv, r0 + kRowsPerBlock);
+  const int tpr = C / 8;                 // threads per row
+  const int rpp = 256 / tpr;             // rows per pass
+  const int tid = threadIdx.x;
+  const int cg = tid % tpr, rr = tid / tpr;
+  float s0[8], s1[8], mu[8], is[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { s0[e] = 0.f; s1[e] = 0.f; }
+  if (BWD) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { mu[e] = mean[g * C + cg * 8 + e]; is[e] = invstd[g * C + cg * 8 + e]; }
+  }
+  const long long gbase = (long long)g * R * C;
+  if (rr < rpp) {
+    for (int r = r0 + rr; r < r1; r += rpp) {
+      const long long o = gbase + (long long)r * C + cg * 8;
+      const uint4 yv = *(const uint4*)(y + o);
+      const uint16_t* yp = (const uint16_t*)&yv;
+      if (!BWD) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) { const float v = bf2f(yp[e]); s0[e] += v; s1[e] += v * v; }
+      } else {
+        const uint4 dv = *(const uint4*)(dout + o);
+        const uint16_t* dp = (const uint16_t*)&dv;
+        uint4 ov = make_uint4(0, 0, 0, 0);
+        if (relu) ov = *(const uint4*)(out + o);
+        const uint16_t* op = (const uint16_t*)&ov;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          float d = bf2f(dp[e]);
+          if (relu && !(bf2f(op[e]) > 0.f)) d = 0.f;
+          const float xh = (bf2f(yp[e]) - mu[e]) * is[e];
+          s0[e] += d; s1[e] += d * xh;
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { red[0][tid][e] = s0[e]; red[1][tid][e] = s1[e]; }
+  __syncthreads();
+  if (tid < tpr) {
+    for (int k = 1; k < rpp; ++k) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { s0[e] += red[0][tid + k * tpr][e]; s1[e] += red[1][tid + k * tpr][e]; }
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      atomicAdd(&sums[((long long)g * 2 + 0) * C + tid * 8 + e], (double)s0[e]);
+      atomicAdd(&sums[((long long)g * 2 + 1) * C + tid * 8 + e], (double)s1[e]);
+    }
+  }
+}
+
+__global__ void bn_finalize_kernel(const double* __restrict__ sums, const int* __restrict__ nvalid, int N, int HW,
+                                   int C, float* __restrict__ rm, float* __restrict__ rv, long long s_gstride,
+                                   float momentum, float eps, float* __restrict__ mean, float* __restrict__ invstd,
+                                   int G) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= G * C) return;
+  const int g = i / C, c = i % C;
+  const double n = (double)valid_rows(nvalid, g, N) * HW;
+  if (n <= 0) { mean[i] = 0.f; invstd[i] = 0.f; return; }
+  const double m = sums[((long long)g * 2) * C + c] / n;
+  double var = sums[((long long)g * 2 + 1) * C + c] / n - m * m;
+  var = var > 0 ? var : 0;
+  mean[i] = (float)m;
+  invstd[i] = (float)(1.0 / sqrt(var + (double)eps));
+  float* prm = rm + (long long)g * s_gstride + c;
+  float* prv = rv + (long long)g * s_gstride + c;
+  const double unb = n > 1 ? var * n / (n - 1) : var;
+  *prm = (float)((1.0 - momentum) * (*prm) + momentum * m);
+  *prv = (float)((1.0 - momentum) * (*prv) + momentum * unb);
+}
+
+__global__ void bn_apply_kernel(const uint16_t* __restrict__ y, const float* __restrict__ mean,
+                                const float* __restrict__ invstd, const float* __restrict__ gamma,
+                                const float* __restrict__ beta, long long p_gstride, const uint16_t* __restrict__ res,
+                                int relu, uint16_t* __restrict__ out, const int* __restrict__ nvalid, int G, int N,
+                                int HW, int C) {
+  const int c8 = C / 8;
+  const long long per = (long long)N * HW * c8;
+  const long long total = per * G;
+  for (long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x; t < total; t += (long long)gridDim.x * blockDim.x) {
+    const int g = (int)(t / per);
+    const long long rem = t - g * per;
+    const long long row = rem / c8;
+    const int c0 = (int)(rem - row * c8) * 8;
+    const long long o = t * 8;
+    uint4 res8 = make_uint4(0, 0, 0, 0);
+    if (row >= (long long)valid_rows(nvalid, g, N) * HW) {
+      *(uint4*)(out + o) = res8;
+      continue;
+    }
+    const uint4 yv = *(const uint4*)(y + o);
+    const uint16_t* yp = (const uint16_t*)&yv;
+    uint4 rv4 = make_uint4(0, 0, 0, 0);
+    if (res) rv4 = *(const uint4*)(res + o);
+    const uint16_t* rp = (const uint16_t*)&rv4;
+    uint16_t* op = (uint16_t*)&res8;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int c = c0 + e;
+      float v = (bf2f(yp[e]) - mean[g * C + c]) * invstd[g * C + c] * gamma[(long long)g * p_gstride + c] +
+                beta[(long long)g * p_gstride + c];
+      if (res) v += bf2f(rp[e]);
+      if (relu) v = fmaxf(v, 0.f);
+      op[e] = f2bf(v);
+    }
+    *(uint4*)(out + o) = res8;
+  }
+}
+
+__global__ void bn_bwd_apply_kernel(const uint16_t* __restrict__ dout, const uint16_t* __restrict__ out,
+                                    const uint16_t* __restrict__ y, const float* __restrict__ mean,
+                                    const float* __restrict__ invstd, const float* __restrict__ gamma,
+                                    long long p_gstride, const double* __restrict__ sums, int relu,
+                                    uint16_t* __restrict__ dy, uint16_t* __restrict__ dres,
+                                    const int* __restrict__ nvalid, int G, int N, int HW, int C) {
+  const int c8 = C / 8;
+  const long long per = (long long)N * HW * c8;
+  const long long total = per * G;
+  for (long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x; t < total; t += (long long)gridDim.x * blockDim.x) {
+    const int g = (int)(t / per);
+    const long long rem = t - g * per;
+    const long long row = rem / c8;
+    const int c0 = (int)(rem - row * c8) * 8;
+    const long long o = t * 8;
+    const int nv = valid_rows(nvalid, g, N) * HW;
+    uint4 z = make_uint4(0, 0, 0, 0);
+    if (row >= nv) {
+      *(uint4*)(dy + o) = z;
+      if (dres) *(uint4*)(dres + o) = z;
+      continue;
+    }
+    const float n = (float)nv;
+    const uint4 dv = *(const uint4*)(dout + o);
+    const uint4 yv = *(const uint4*)(y + o);
+    uint4 ov = z;
+    if (relu) ov = *(const uint4*)(out + o);
+    const uint16_t* dp = (const uint16_t*)&dv;
+    const uint16_t* yp = (const uint16_t*)&yv;
+    const uint16_t* op = (const uint16_t*)&ov;
+    uint4 r1 = z, r2 = z;
+    uint16_t* p1 = (uint16_t*)&r1;
+    uint16_t* p2 = (uint16_t*)&r2;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int c = c0 + e;
+      float d = bf2f(dp[e]);
+      if (relu && !(bf2f(op[e]) > 0.f)) d = 0.f;
+      const float is = invstd[g * C + c];
+      const float xh = (bf2f(yp[e]) - mean[g * C + c]) * is;
+      const float sd = (float)sums[((long long)g * 2) * C + c];
+      const float sdx = (float)sums[((long long)g * 2 + 1) * C + c];
+      const float v = gamma[(long long)g * p_gstride + c] * is / n * (n * d - sd - xh * sdx);
+      p1[e] = f2bf(v);
+      p2[e] = f2bf(d);
+    }
+    *(uint4*)(dy + o) = r1;
+    if (dres) *(uint4*)(dres + o) = r2;
+  }
+}
+
+__global__ void bn_param_grad_kernel(const double* __restrict__ sums, float* __restrict__ dgamma,
+                                     float* __restrict__ dbeta, long long g_gstride, int G, int C) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= G * C) return;
+  const int g = i / C, c = i % C;
+  dbeta[(long long)g * g_gstride + c] += (float)sums[((long long)g * 2) * C + c];
+  dgamma[(long long)g * g_gstride + c] += (float)sums[((long long)g * 2 + 1) * C + c];
+}
+
+// eval fold: wf[s][co][k] = w[s][co][k] * s_c ; bf[s][co] = (b0 - rm) * s_c + beta
+__global__ void bn_fold_kernel(const float* __restrict__ w, long long w_sstride, const float* __restrict__ cbias,
+                               const float* __restrict__ gamma, const float* __restrict__ beta,
+                               const float* __restrict__ rm, const float* __restrict__ rv, long long s_gstride,
+                               float eps, uint16_t* __restrict__ wf, float* __restrict__ bf, int slots, int Cout,
+                               int K) {
+  const long long per = (long long)Cout * K;
+  const long long total = per * slots;
+  for (long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x; t < total; t += (long long)gridDim.x * blockDim.x) {
+    const int s = (int)(t / per);
+    const long long rem = t - s * per;
+    const int co = (int)(rem / K);
+    const int k = (int)(rem - (long long)co * K);
+    const long long p = (long long)s * s_gstride + co;
+    const float sc = gamma[p] / sqrtf(rv[p] + eps);
+    wf[t] = f2bf(w[(long long)s * w_sstride + rem] * sc);
+    if (k == 0) {
+      const float b0 = cbias ? cbias[p] : 0.f;
+      bf[(long long)s * Cout + co] = (b0 - rm[p]) * sc + beta[p];
+    }
+  }
+}
+
+int egrid(long long n) { return (int)std::max(1LL, std::min(16384LL, (n + 255) / 256)); }
+
+}  // namespace
+
+DBA_EXPORT int dba_bn_stats(const void* y, const int* nvalid, int G, int N, int HW, int C, double* sums, void* stream) {
+  dim3 grid(ceil_div((long long)N * HW, kRowsPerBlock), G);
+  hipLaunchKernelGGL(bn_reduce_kernel<false>, grid, dim3(256), 0, (hipStream_t)stream, (const uint16_t*)y, nullptr,
+                     nullptr, nullptr, nullptr, 0, nvalid, N, HW, C, sums);
+  DBA_LAUNCH_CHECK();
+}
+
+DBA_EXPORT int dba_bn_finalize(const double* sums, const int* nvalid, int G, int N, int HW, int C, float* rm, float* rv,
+                               long long s_gstride, float momentum, float eps, float* mean, float* invstd,
+                               void* stream) {
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3(ceil_div(G * C, 256)), dim3(256), 0, (hipStream_t)stream, sums, nvalid,
+                     N, HW, C, rm, rv, s_gstride, momentum, eps, mean, invstd, G);
+  DBA_LAUNCH_CHECK();
+}
+
+DBA_EXPORT int dba_bn_apply(const void* y, const float* mean, const float* invstd, const float* gamma, const float* beta,
+                            long long p_gstride, const void* res, int relu, void* out, const int* nvalid, int G, int N,
+                            int HW, int C, void* stream) {
+  const long long n = (long long)G * N * HW * C / 8;
+  hipLaunchKernelGGL(bn_apply_kernel, dim3(egrid(n)), dim3(256), 0, (hipStream_t)stream, (const uint16_t*)y, mean,
+                     invstd, gamma, beta, p_gstride, (const uint16_t*)res, relu, (uint16_t*)out, nvalid, G, N, HW, C);
+  DBA_LAUNCH_CHECK();
+}
+
+DBA_EXPORT int dba_bn_bwd(const void* dout, const void* out, const void* y, const float* mean, const float* invstd,
+                          const float* gamma, long long p_gstride, int relu, float* dgamma, float* dbeta,
+                          long long g_gstride, void* dy, void* dres, double* sums, const int* nvalid, int G, int N,
+                          int HW, int C, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  dim3 grid(ceil_div((long long)N * HW, kRowsPerBlock), G);
+  hipLaunchKernelGGL(bn_reduce_kernel<true>, grid, dim3(256), 0, st, (const uint16_t*)y, (const uint16_t*)dout,
+                     (const uint16_t*)out, mean, invstd, relu, nvalid, N, HW, C, sums);
+  hipLaunchKernelGGL(bn_param_grad_kernel, dim3(ceil_div(G * C, 256)), dim3(256), 0, st, sums, dgamma, dbeta,
+                     g_gstride, G, C);
+  const long long n = (long long)G * N * HW * C / 8;
+  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(egrid(n)), dim3(256), 0, st, (const uint16_t*)dout,
+                     (const uint16_t*)out, (const uint16_t*)y, mean, invstd, gamma, p_gstride, sums, relu,
+                     (uint16_t*)dy, (uint16_t*)dres, nvalid, G, N, HW, C);
+  DBA_LAUNCH_CHECK();
+}
+
+DBA_EXPORT int dba_bn_fold(const float* w, long long w_sstride, const float* cbias, const float* gamma,
+                           const float* beta, const float* rm, const float* rv, long long s_gstride, float eps,
+                           void* wf, float* bf, int slots, int Cout, int K, void* stream) {
+  const long long n = (long long)slots * Cout * K;
+  hipLaunchKernelGGL(bn_fold_kernel, dim3(egrid(n)), dim3(256), 0, (hipStream_t)stream, w, w_sstride, cbias, gamma,
+                     beta, rm, rv, s_gstride, eps, (uint16_t*)wf, bf, slots, Cout, K);
+  DBA_LAUNCH_CHECK();
+}

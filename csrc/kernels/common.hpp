@@ -1,0 +1,76 @@
+// Shared device helpers for the DBA-on-MI355X kernel library (gfx950 / CDNA4 only).
+//
+// Conventions used by every kernel in this directory:
+//   * activations are NHWC with a leading replica/job group dim: [G][N][H][W][C];
+//   * bf16 tensors are passed as uint16_t (torch.bfloat16 bit pattern);
+//   * every launcher is `extern "C"`, takes raw device pointers + the caller's hipStream_t
+//     (torch's current stream, so launches are captured by HIP graphs) and returns the
+//     hipError_t of the launch;
+//   * per-group "valid rows" (nvalid[g] samples) gate every row reduction, so padded or
+//     inactive client replicas cost nothing and never pollute statistics.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define DBA_EXPORT extern "C" __attribute__((visibility("default")))
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;
+typedef __attribute__((ext_vector_type(4))) float f32x4_t;
+typedef __attribute__((ext_vector_type(16))) float f32x16_t;
+
+static constexpr int kWave = 64;
+
+__device__ __forceinline__ float bf2f(uint16_t v) {
+  return __uint_as_float(((uint32_t)v) << 16);
+}
+
+// round-to-nearest-even float -> bf16 (NaN preserved as quiet NaN)
+__device__ __forceinline__ uint16_t f2bf(float f) {
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 0x40);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+
+template <typename T> __device__ __forceinline__ float to_f(T v);
+template <> __device__ __forceinline__ float to_f<float>(float v) { return v; }
+template <> __device__ __forceinline__ float to_f<uint16_t>(uint16_t v) { return bf2f(v); }
+
+template <typename T> __device__ __forceinline__ T from_f(float v);
+template <> __device__ __forceinline__ float from_f<float>(float v) { return v; }
+template <> __device__ __forceinline__ uint16_t from_f<uint16_t>(float v) { return f2bf(v); }
+
+// lowbias32 — identical to dba_mod_amd/ops/rng.py and csrc/runtime/runtime.cpp
+__device__ __forceinline__ uint32_t lowbias32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7feb352dU;
+  x ^= x >> 15;
+  x *= 0x846ca68bU;
+  x ^= x >> 16;
+  return x;
+}
+__device__ __forceinline__ uint32_t hash2(uint32_t seed, uint32_t ctr) {
+  return lowbias32(ctr ^ lowbias32(seed));
+}
+__device__ __forceinline__ float uniform01(uint32_t seed, uint32_t ctr) {
+  return ((float)(hash2(seed, ctr) >> 8) + 0.5f) * (1.0f / 16777216.0f);
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, kWave));
+  return v;
+}
+
+__device__ __forceinline__ int valid_rows(const int* nvalid, int g, int n_per_group) {
+  return nvalid ? nvalid[g] : n_per_group;
+}
+
+static inline int ceil_div(long long a, long long b) { return (int)((a + b - 1) / b); }
+
+#define DBA_LAUNCH_CHECK() return (int)hipGetLastError()

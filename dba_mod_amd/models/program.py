@@ -108,14 +108,13 @@ class Ctx:
         need_dx = self.tape.needs_grad(x)
 
         def bwd(dout: Tensor):
-            dy = ops.bn_train_bwd(dout, y, out, mean, invstd, gamma, self.nvalid, relu,
-                                  self.g(bn + ".weight"), self.g(bn + ".bias"))
+            r = ops.bn_train_bwd(dout, y, out, mean, invstd, gamma, self.nvalid, relu,
+                                 self.g(bn + ".weight"), self.g(bn + ".bias"),
+                                 want_dres=residual is not None)
+            dy, dres = r if residual is not None else (r, None)
             ops.conv2d_wgrad(dy, x, stride, pad, kh, kw, self.g(conv), nvalid=self.nvalid)
             dx = (ops.conv2d_dgrad(dy, w, self.wsel, stride, pad, in_hw, nvalid=self.nvalid)
                   if need_dx else None)
-            dres = None
-            if residual is not None:
-                dres = ops.relu_mask_bwd(dout, out) if relu else dout
             return dx, dres
 
         self.tape.record((out,), (x, residual), bwd)
@@ -144,21 +143,23 @@ class Ctx:
         self.tape.record((y,), (x,), bwd)
         return y
 
-    def linear(self, x: Tensor, name: str, bias: str, relu: bool) -> Tensor:
-        """x [G, N, F] -> [G, N, Out] via the 1x1-conv kernel (weights [Out, 1, 1, F])."""
+    def linear(self, x: Tensor, name: str, bias: str, relu: bool, final: bool = False) -> Tensor:
+        """x [G, N, F] -> [G, N, Out] via the 1x1-conv kernel (weights [Out, 1, 1, F]).
+        ``final``: the logits layer writes fp32 (loss/argmax precision)."""
         G, N, Fd = x.shape
         x4 = self.reshape(x, (G, N, 1, 1, Fd))
-        y4 = self._lin_conv(x4, name, bias, relu)
+        y4 = self._lin_conv(x4, name, bias, relu, torch.float32 if final else None)
         return self.reshape(y4, (G, N, y4.shape[-1]))
 
-    def _lin_conv(self, x4: Tensor, name: str, bias: str, relu: bool) -> Tensor:
+    def _lin_conv(self, x4: Tensor, name: str, bias: str, relu: bool,
+                  out_dtype: Optional[torch.dtype] = None) -> Tensor:
         if not self.train and self.folded is not None and name in self.folded:
             w, b = self.folded[name]
         else:
             wv = self.w(name)
             w = wv.reshape(wv.shape[0], wv.shape[1], 1, 1, wv.shape[2])
             b = self.m(bias)
-        y = ops.conv2d(x4, w, self.wsel, 1, 0, bias=b, relu=relu, nvalid=self.nvalid)
+        y = ops.conv2d(x4, w, self.wsel, 1, 0, bias=b, relu=relu, nvalid=self.nvalid, out_dtype=out_dtype)
         if not self.train:
             return y
         need_dx = self.tape.needs_grad(x4)
@@ -185,7 +186,7 @@ class Ctx:
         y, ind = ops.maxpool2d(x, k, s, p)
         if self.train:
             shp = tuple(x.shape)
-            self.tape.record((y,), (x,), lambda d: (ops.maxpool2d_bwd(d, ind, shp),))
+            self.tape.record((y,), (x,), lambda d: (ops.maxpool2d_bwd(d, ind, shp, k, s, p),))
         return y
 
     def gap(self, x: Tensor) -> Tensor:
@@ -222,7 +223,7 @@ def _resnet_cifar(ctx: Ctx, x: Tensor) -> Tensor:
             cin = w
     out = ctx.gap(out)
     G, N = out.shape[:2]
-    return ctx.linear(ctx.reshape(out, (G, N, out.shape[-1])), "linear.weight", "linear.bias", relu=False)
+    return ctx.linear(ctx.reshape(out, (G, N, out.shape[-1])), "linear.weight", "linear.bias", relu=False, final=True)
 
 
 def _resnet_tiny(ctx: Ctx, x: Tensor) -> Tensor:
@@ -242,7 +243,7 @@ def _resnet_tiny(ctx: Ctx, x: Tensor) -> Tensor:
             cin = w
     out = ctx.gap(out)
     G, N = out.shape[:2]
-    return ctx.linear(ctx.reshape(out, (G, N, out.shape[-1])), "fc.weight", "fc.bias", relu=False)
+    return ctx.linear(ctx.reshape(out, (G, N, out.shape[-1])), "fc.weight", "fc.bias", relu=False, final=True)
 
 
 def _mnist(ctx: Ctx, x: Tensor) -> Tensor:
@@ -254,7 +255,7 @@ def _mnist(ctx: Ctx, x: Tensor) -> Tensor:
     f = ctx.reshape(b, (G, N, -1))
     h = ctx.linear(f, "fc1.weight", "fc1.bias", relu=True)
     # log_softmax of the reference is folded into the loss (idempotent, quirk D7)
-    return ctx.linear(h, "fc2.weight", "fc2.bias", relu=False)
+    return ctx.linear(h, "fc2.weight", "fc2.bias", relu=False, final=True)
 
 
 def _loan(ctx: Ctx, x: Tensor) -> Tensor:
@@ -262,7 +263,7 @@ def _loan(ctx: Ctx, x: Tensor) -> Tensor:
     h = ctx.dropout(h, 0.5)
     h = ctx.linear(h, "layer2.0.weight", "layer2.0.bias", relu=True)
     h = ctx.dropout(h, 0.5)
-    return ctx.linear(h, "layer3.0.weight", "layer3.0.bias", relu=False)
+    return ctx.linear(h, "layer3.0.weight", "layer3.0.bias", relu=False, final=True)
 
 
 FORWARDS: Dict[str, Callable[[Ctx, Tensor], Tensor]] = {

@@ -40,6 +40,14 @@ class Entry:
     to_sd: Optional[Callable[[torch.Tensor], torch.Tensor]] = None
 
 
+ALIGN = 64   # every entry starts on a 64-element boundary (256 B fp32 / 128 B bf16), so
+             # the kernels' 16-byte vector loads of weight rows are always aligned
+
+
+def _align(n: int) -> int:
+    return (n + ALIGN - 1) // ALIGN * ALIGN
+
+
 @dataclass
 class ModelSpec:
     arch: str
@@ -51,6 +59,7 @@ class ModelSpec:
     num_classes: int
     P: int = 0
     B: int = 0
+    n_params: int = 0              # true parameter count (P includes alignment padding)
     by_name: Dict[str, Entry] = field(default_factory=dict)
 
     @property
@@ -127,7 +136,7 @@ def _make_spec(arch: str, input_hwc: Tuple[int, ...], num_classes: int,
             if ".bn" in name or name.startswith("bn") or ".shortcut.1." in name or ".downsample.1." in name:
                 kind = "bn_w" if name.endswith("weight") else "bn_b"
         params.append(Entry(name, shp, kshape, off, p.numel(), kind, to_k, to_sd))
-        off += p.numel()
+        off = _align(off + p.numel())
     P = off
     buffers: List[Entry] = []
     counters: List[str] = []
@@ -137,9 +146,9 @@ def _make_spec(arch: str, input_hwc: Tuple[int, ...], num_classes: int,
             continue
         kind = "bn_mean" if name.endswith("running_mean") else "bn_var"
         buffers.append(Entry(name, tuple(b.shape), tuple(b.shape), off, b.numel(), kind))
-        off += b.numel()
+        off = _align(off + b.numel())
     spec = ModelSpec(arch, params, buffers, counters, list(m.state_dict().keys()), input_hwc,
-                     num_classes, P=P, B=off - P)
+                     num_classes, P=P, B=off - P, n_params=sum(e.numel for e in params))
     spec.by_name = {e.name: e for e in params + buffers}
     return spec
 

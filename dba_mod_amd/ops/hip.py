@@ -1,0 +1,373 @@
+"""GPU implementation of every framework op: thin ctypes bindings to ``libdba_kernels.so``.
+
+Each wrapper checks layouts, allocates outputs with the torch caching allocator and launches
+the hand-written gfx950 kernel on torch's *current* stream (so every launch is captured by
+``torch.cuda.graph``).  Signatures mirror :mod:`dba_mod_amd.ops.reference` exactly.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Optional, Sequence, Tuple
+
+import torch
+
+from . import build
+
+Tensor = torch.Tensor
+_BF16 = torch.bfloat16
+
+if not os.path.exists(build.kernels_path()):
+    raise ImportError(f"HIP kernel library missing: {build.kernels_path()} — run "
+                      f"`python -m dba_mod_amd.ops.build` (or __graft_entry__.build())")
+_L = ctypes.CDLL(build.kernels_path())
+
+_P = ctypes.c_void_p
+_I = ctypes.c_int
+_LL = ctypes.c_longlong
+_F = ctypes.c_float
+_U = ctypes.c_uint
+
+_SIGS = {
+    "dba_gather_images": [_P, _P, _P, _P, _P, _P, _I, _P, _P, _I, _P, _I, _I, _I, _I, _I, _P],
+    "dba_gather_rows": [_P, _P, _P, _P, _P, _I, _P, _P, _I, _P, _I, _P, _I, _I, _I, _P],
+    "dba_conv_fwd": [_P, _LL, _P, _LL, _P, _P, _LL, _P, _LL, _P, _LL, _I, _P] + [_I] * 14 + [_P],
+    "dba_conv_dgrad": [_P, _LL, _P, _LL, _P, _P, _LL, _P] + [_I] * 13 + [_P],
+    "dba_conv_wgrad": [_P, _LL, _P, _LL, _P, _LL, _P] + [_I] * 12 + [_P],
+    "dba_transpose_w": [_P, _LL, _P, _I, _I, _I, _I, _P],
+    "dba_colsum": [_P, _LL, _I, _P, _I, _I, _I, _P, _LL, _P],
+    "dba_bn_stats": [_P, _P, _I, _I, _I, _I, _P, _P],
+    "dba_bn_finalize": [_P, _P, _I, _I, _I, _I, _P, _P, _LL, _F, _F, _P, _P, _P],
+    "dba_bn_apply": [_P, _P, _P, _P, _P, _LL, _P, _I, _P, _P, _I, _I, _I, _I, _P],
+    "dba_bn_bwd": [_P, _P, _P, _P, _P, _P, _LL, _I, _P, _P, _LL, _P, _P, _P, _P, _I, _I, _I, _I, _P],
+    "dba_bn_fold": [_P, _LL, _P, _P, _P, _P, _P, _LL, _F, _P, _P, _I, _I, _I, _P],
+    "dba_relu_mask_bwd": [_P, _P, _P, _LL, _P],
+    "dba_maxpool": [_P, _P, _P, _LL, _I, _I, _I, _I, _I, _I, _I, _I, _P],
+    "dba_maxpool_bwd": [_P, _P, _P, _LL, _I, _I, _I, _I, _I, _I, _I, _I, _P],
+    "dba_avgpool": [_P, _P, _LL, _I, _I, _P],
+    "dba_avgpool_bwd": [_P, _P, _LL, _I, _I, _P],
+    "dba_dropout": [_P, _P, _I, _P, _U, _F, _LL, _I, _P],
+    "dba_softmax_xent": [_P, _P, _I, _I, _I, _I, _P, _P, _P, _P],
+    "dba_sgd_step": [_P, _LL, _P, _P, _P, _P, _P, _F, _F, _P, _P, _I, _I, _P],
+    "dba_scale_from_base": [_P, _P, _F, _P, _LL, _P],
+    "dba_add_noise_scaled": [_P, _P, _LL, _F, _F, _U, _I, _P],
+    "dba_sq_dists": [_P, _LL, _P, _I, _LL, _P, _P],
+    "dba_weighted_sum": [_P, _LL, _P, _I, _P, _LL, _P],
+    "dba_gram": [_P, _LL, _I, _I, _P, _P],
+}
+for _name, _args in _SIGS.items():
+    _fn = getattr(_L, _name)
+    _fn.argtypes = _args
+    _fn.restype = ctypes.c_int
+
+
+def _call(name: str, *args) -> None:
+    rc = getattr(_L, name)(*args)
+    if rc != 0:
+        raise RuntimeError(f"{name}: HIP error {rc}")
+
+
+def _ptr(t: Optional[Tensor]):
+    return None if t is None else t.data_ptr()
+
+
+def _stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _i32(t: Optional[Tensor]) -> Optional[Tensor]:
+    if t is None:
+        return None
+    return t if (t.dtype == torch.int32 and t.is_contiguous()) else t.to(torch.int32).contiguous()
+
+
+def _inner_contig(t: Tensor) -> bool:
+    """True if all dims but the first are densely packed (a strided row view)."""
+    exp = 1
+    for d in range(t.dim() - 1, 0, -1):
+        if t.shape[d] != 1 and t.stride(d) != exp:
+            return False
+        exp *= t.shape[d]
+    return True
+
+
+def _rowview(t: Tensor) -> Tuple[Tensor, int]:
+    if not _inner_contig(t):
+        t = t.contiguous()
+    return t, (t.stride(0) if t.shape[0] > 1 else int(torch.tensor(t.shape[1:]).prod()))
+
+
+def _bf16c(t: Tensor) -> Tensor:
+    if t.dtype != _BF16:
+        t = t.to(_BF16)
+    return t.contiguous()
+
+
+# ------------------------------------------------------------------------- data ingest
+def gather_images(src, labels, idx, trig_masks, trig_id, poison_n, target, flip_seeds, out_dtype):
+    G, B = idx.shape
+    _, H, W, C = src.shape
+    x = torch.empty(G, B, H, W, C, dtype=out_dtype, device=src.device)
+    y = torch.empty(G, B, dtype=torch.int32, device=src.device)
+    idx, trig_id, poison_n, fs = _i32(idx), _i32(trig_id), _i32(poison_n), _i32(flip_seeds)
+    _call("dba_gather_images", src.data_ptr(), _i32(labels).data_ptr(), idx.data_ptr(),
+          trig_masks.contiguous().data_ptr(), trig_id.data_ptr(), poison_n.data_ptr(), int(target), _ptr(fs),
+          x.data_ptr(), int(out_dtype == torch.float32), y.data_ptr(), G, B, H, W, C, _stream())
+    return x, y
+
+
+def gather_rows(src, labels, idx, trig_cols, trig_vals, trig_id, poison_n, target, out_dtype):
+    G, B = idx.shape
+    Fd = src.shape[1]
+    x = torch.empty(G, B, Fd, dtype=out_dtype, device=src.device)
+    y = torch.empty(G, B, dtype=torch.int32, device=src.device)
+    tc = _i32(trig_cols)
+    _call("dba_gather_rows", src.contiguous().data_ptr(), _i32(labels).data_ptr(), _i32(idx).data_ptr(),
+          tc.data_ptr(), trig_vals.float().contiguous().data_ptr(), int(tc.shape[1]), _i32(trig_id).data_ptr(),
+          _i32(poison_n).data_ptr(), int(target), x.data_ptr(), int(out_dtype == torch.float32), y.data_ptr(),
+          G, B, Fd, _stream())
+    return x, y
+
+
+# ------------------------------------------------------------------------------ conv
+def _check_w(w: Tensor) -> Tuple[Tensor, int]:
+    if w.dtype != _BF16:
+        w = w.to(_BF16)
+    return _rowview(w)
+
+
+def conv2d(x, w, wsel, stride, pad, bias=None, residual=None, relu=False, nvalid=None, out_dtype=None):
+    x = _bf16c(x)
+    G, N, H, W, Cin = x.shape
+    w, ws = _check_w(w)
+    Cout, KH, KW = w.shape[1], w.shape[2], w.shape[3]
+    assert w.shape[4] == Cin, (w.shape, x.shape)
+    Ho = (H + 2 * pad - KH) // stride + 1
+    Wo = (W + 2 * pad - KW) // stride + 1
+    out_dtype = out_dtype or _BF16
+    y = torch.empty(G, N, Ho, Wo, Cout, dtype=out_dtype, device=x.device)
+    bs = 0
+    if bias is not None:
+        bias = bias.float()
+        bias, bs = _rowview(bias)
+    if residual is not None:
+        residual = _bf16c(residual)
+    _call("dba_conv_fwd", x.data_ptr(), N * H * W * Cin, w.data_ptr(), ws, _ptr(_i32(wsel)), _ptr(bias), bs,
+          _ptr(residual), N * Ho * Wo * Cout, y.data_ptr(), N * Ho * Wo * Cout, int(out_dtype == torch.float32),
+          _ptr(_i32(nvalid)), G, N, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, int(relu), _stream())
+    return y
+
+
+def conv2d_dgrad(dy, w, wsel, stride, pad, in_hw, nvalid=None, out_dtype=None):
+    dy = _bf16c(dy)
+    G, N, Ho, Wo, Cout = dy.shape
+    w, ws = _check_w(w)
+    slots, _, KH, KW, Cin = w.shape
+    wt = torch.empty(slots, Cin, KH, KW, Cout, dtype=_BF16, device=dy.device)
+    _call("dba_transpose_w", w.data_ptr(), ws, wt.data_ptr(), slots, Cout, KH * KW, Cin, _stream())
+    H, W = in_hw
+    dx = torch.empty(G, N, H, W, Cin, dtype=_BF16, device=dy.device)
+    _call("dba_conv_dgrad", dy.data_ptr(), N * Ho * Wo * Cout, wt.data_ptr(), Cin * KH * KW * Cout,
+          _ptr(_i32(wsel)), dx.data_ptr(), N * H * W * Cin, _ptr(_i32(nvalid)), G, N, H, W, Cin, Ho, Wo, Cout,
+          KH, KW, stride, pad, _stream())
+    return dx if out_dtype in (None, _BF16) else dx.to(out_dtype)
+
+
+def conv2d_wgrad(dy, x, stride, pad, kh, kw, dw, dbias=None, nvalid=None):
+    dy = _bf16c(dy)
+    x = _bf16c(x)
+    G, N, Ho, Wo, Cout = dy.shape
+    _, _, H, W, Cin = x.shape
+    assert dw.dtype == torch.float32 and _inner_contig(dw)
+    _call("dba_conv_wgrad", dy.data_ptr(), N * Ho * Wo * Cout, x.data_ptr(), N * H * W * Cin, dw.data_ptr(),
+          dw.stride(0), _ptr(_i32(nvalid)), G, N, H, W, Cin, Ho, Wo, Cout, kh, kw, stride, pad, _stream())
+    if dbias is not None:
+        assert dbias.dtype == torch.float32 and dbias.stride(1) == 1
+        _call("dba_colsum", dy.data_ptr(), N * Ho * Wo * Cout, Ho * Wo, _ptr(_i32(nvalid)), G, N, Cout,
+              dbias.data_ptr(), dbias.stride(0), _stream())
+
+
+# ------------------------------------------------------------------------ batch norm
+def _same_stride(*ts: Tensor) -> int:
+    s = ts[0].stride(0)
+    for t in ts:
+        assert t.dtype == torch.float32 and t.stride(-1) == 1 and (t.shape[0] == 1 or t.stride(0) == s)
+    return s
+
+
+def bn_train(y, gamma, beta, rmean, rvar, nvalid, momentum, eps, relu, residual):
+    y = _bf16c(y)
+    G, N, H, W, C = y.shape
+    assert C % 8 == 0
+    ps = _same_stride(gamma, beta, rmean, rvar)
+    sums = torch.zeros(G, 2, C, dtype=torch.float64, device=y.device)
+    mean = torch.empty(G, C, dtype=torch.float32, device=y.device)
+    invstd = torch.empty(G, C, dtype=torch.float32, device=y.device)
+    nv = _ptr(_i32(nvalid))
+    _call("dba_bn_stats", y.data_ptr(), nv, G, N, H * W, C, sums.data_ptr(), _stream())
+    _call("dba_bn_finalize", sums.data_ptr(), nv, G, N, H * W, C, rmean.data_ptr(), rvar.data_ptr(), ps,
+          float(momentum), float(eps), mean.data_ptr(), invstd.data_ptr(), _stream())
+    out = torch.empty_like(y)
+    res = _bf16c(residual) if residual is not None else None
+    _call("dba_bn_apply", y.data_ptr(), mean.data_ptr(), invstd.data_ptr(), gamma.data_ptr(), beta.data_ptr(), ps,
+          _ptr(res), int(relu), out.data_ptr(), nv, G, N, H * W, C, _stream())
+    return out, mean, invstd
+
+
+def bn_train_bwd(dout, y, out, mean, invstd, gamma, nvalid, relu, dgamma, dbeta, want_dres=False):
+    dout = _bf16c(dout)
+    G, N, H, W, C = y.shape
+    ps = _same_stride(gamma)
+    gs = _same_stride(dgamma, dbeta)
+    sums = torch.zeros(G, 2, C, dtype=torch.float64, device=y.device)
+    dy = torch.empty_like(y)
+    dres = torch.empty_like(y) if want_dres else None
+    _call("dba_bn_bwd", dout.data_ptr(), out.data_ptr(), y.data_ptr(), mean.data_ptr(), invstd.data_ptr(),
+          gamma.data_ptr(), ps, int(relu), dgamma.data_ptr(), dbeta.data_ptr(), gs, dy.data_ptr(), _ptr(dres),
+          sums.data_ptr(), _ptr(_i32(nvalid)), G, N, H * W, C, _stream())
+    return (dy, dres) if want_dres else dy
+
+
+def relu_mask_bwd(dout, out):
+    dout = _bf16c(dout)
+    out = _bf16c(out)
+    din = torch.empty_like(dout)
+    _call("dba_relu_mask_bwd", dout.data_ptr(), out.data_ptr(), din.data_ptr(), dout.numel(), _stream())
+    return din
+
+
+def bn_fold(w, conv_bias, gamma, beta, rmean, rvar, eps, out_dtype):
+    assert w.dtype == torch.float32 and _inner_contig(w)
+    slots, Cout = w.shape[0], w.shape[1]
+    K = int(torch.tensor(w.shape[2:]).prod())
+    ss = _same_stride(gamma, beta, rmean, rvar)
+    wf = torch.empty(w.shape, dtype=_BF16, device=w.device)
+    bf = torch.empty(slots, Cout, dtype=torch.float32, device=w.device)
+    cb = None
+    if conv_bias is not None:
+        cb = conv_bias
+        assert _same_stride(cb) == ss
+    _call("dba_bn_fold", w.data_ptr(), w.stride(0), _ptr(cb), gamma.data_ptr(), beta.data_ptr(), rmean.data_ptr(),
+          rvar.data_ptr(), ss, float(eps), wf.data_ptr(), bf.data_ptr(), slots, Cout, K, _stream())
+    return (wf if out_dtype == _BF16 else wf.to(out_dtype)), bf
+
+
+# --------------------------------------------------------------------------- pooling
+def maxpool2d(x, k, s, p):
+    x = _bf16c(x)
+    G, N, H, W, C = x.shape
+    Ho = (H + 2 * p - k) // s + 1
+    Wo = (W + 2 * p - k) // s + 1
+    y = torch.empty(G, N, Ho, Wo, C, dtype=_BF16, device=x.device)
+    ind = torch.empty(G, N, Ho, Wo, C, dtype=torch.int32, device=x.device)
+    _call("dba_maxpool", x.data_ptr(), y.data_ptr(), ind.data_ptr(), G * N, H, W, C, Ho, Wo, k, s, p, _stream())
+    return y, ind
+
+
+def maxpool2d_bwd(dy, ind, in_shape, k, s, p):
+    dy = _bf16c(dy)
+    G, N, H, W, C = in_shape
+    Ho, Wo = dy.shape[2], dy.shape[3]
+    dx = torch.empty(G, N, H, W, C, dtype=_BF16, device=dy.device)
+    _call("dba_maxpool_bwd", dy.data_ptr(), ind.data_ptr(), dx.data_ptr(), G * N, H, W, C, Ho, Wo, k, s, p, _stream())
+    return dx
+
+
+def avgpool_global(x):
+    x = _bf16c(x)
+    G, N, H, W, C = x.shape
+    y = torch.empty(G, N, 1, 1, C, dtype=_BF16, device=x.device)
+    _call("dba_avgpool", x.data_ptr(), y.data_ptr(), G * N, H * W, C, _stream())
+    return y
+
+
+def avgpool_global_bwd(dy, hw):
+    dy = _bf16c(dy)
+    G, N = dy.shape[:2]
+    C = dy.shape[-1]
+    H, W = hw
+    dx = torch.empty(G, N, H, W, C, dtype=_BF16, device=dy.device)
+    _call("dba_avgpool_bwd", dy.data_ptr(), dx.data_ptr(), G * N, H * W, C, _stream())
+    return dx
+
+
+# --------------------------------------------------------------------------- dropout
+def dropout(x, p, seeds, salt):
+    x = x.contiguous()
+    y = torch.empty_like(x)
+    G = x.shape[0]
+    _call("dba_dropout", x.data_ptr(), y.data_ptr(), int(x.dtype == torch.float32), _i32(seeds).data_ptr(),
+          int(salt) & 0xFFFFFFFF, float(p), x.numel() // G, G, _stream())
+    return y
+
+
+def dropout_bwd(dy, p, seeds, salt):
+    return dropout(dy, p, seeds, salt)
+
+
+# ---------------------------------------------------------------------------- loss
+def softmax_xent(logits, labels, mean, want_grad):
+    lf = logits.float().contiguous()
+    G, B, C = lf.shape
+    loss = torch.empty(G, dtype=torch.float32, device=lf.device)
+    correct = torch.empty(G, dtype=torch.float32, device=lf.device)
+    dl = torch.empty(G, B, C, dtype=_BF16, device=lf.device) if want_grad else None
+    _call("dba_softmax_xent", lf.data_ptr(), _i32(labels).data_ptr(), G, B, C, int(bool(mean)), _ptr(dl),
+          loss.data_ptr(), correct.data_ptr(), _stream())
+    return loss, correct, dl
+
+
+# ------------------------------------------------------------------------- optimizer
+def sgd_step(params, grads, mom, lr, first, active, momentum, wd, shadow=None, fg_accum=None):
+    G, P = grads.shape
+    assert params.dtype == torch.float32 and params.stride(1) == 1 and params.stride(0) % 4 == 0
+    assert grads.is_contiguous() and mom.is_contiguous() and P % 4 == 0
+    if shadow is not None:
+        assert shadow.is_contiguous() and shadow.dtype == _BF16
+    _call("dba_sgd_step", params.data_ptr(), params.stride(0), grads.data_ptr(), mom.data_ptr(),
+          lr.float().contiguous().data_ptr(), _i32(first).data_ptr(), _i32(active).data_ptr(), float(momentum),
+          float(wd), _ptr(shadow), _ptr(fg_accum), G, P, _stream())
+
+
+# ---------------------------------------------------------------- flat / aggregation
+def scale_from_base(w, base, gamma):
+    w = w.contiguous()
+    base = base.contiguous()
+    out = torch.empty_like(w)
+    _call("dba_scale_from_base", w.data_ptr(), base.data_ptr(), float(gamma), out.data_ptr(), w.numel(), _stream())
+    return out
+
+
+def add_noise_scaled(dst, upd, coef, sigma, seed, noise):
+    assert dst.is_contiguous() and dst.dtype == torch.float32
+    upd = upd.float().contiguous()
+    _call("dba_add_noise_scaled", dst.data_ptr(), upd.data_ptr(), dst.numel(), float(coef), float(sigma),
+          int(seed) & 0xFFFFFFFF, int(bool(noise)), _stream())
+
+
+def sq_dists(points, m):
+    assert points.stride(1) == 1 and points.dtype == torch.float32
+    m = m.float().contiguous()
+    n, L = points.shape
+    out = torch.zeros(n, dtype=torch.float64, device=points.device)
+    _call("dba_sq_dists", points.data_ptr(), points.stride(0), m.data_ptr(), n, L, out.data_ptr(), _stream())
+    return out
+
+
+def weighted_sum(points, wts):
+    assert points.stride(1) == 1 and points.dtype == torch.float32
+    n, L = points.shape
+    out = torch.empty(L, dtype=torch.float32, device=points.device)
+    _call("dba_weighted_sum", points.data_ptr(), points.stride(0), wts.float().contiguous().data_ptr(), n,
+          out.data_ptr(), L, _stream())
+    return out
+
+
+def gram(feats):
+    f = feats.float()
+    if f.stride(1) != 1:
+        f = f.contiguous()
+    n, d = f.shape
+    out = torch.zeros(n, n, dtype=torch.float32, device=f.device)
+    _call("dba_gram", f.data_ptr(), f.stride(0), n, d, out.data_ptr(), _stream())
+    return out

@@ -127,6 +127,8 @@ def conv2d(x: Tensor, w: Tensor, wsel: Optional[Tensor], stride: int, pad: int,
         if relu:
             yg = torch.relu(yg)
         outs.append(yg)
+    if out_dtype == torch.float32 and _cdt() == torch.float64:
+        out_dtype = torch.float64
     return torch.stack(outs).to(out_dtype or x.dtype)
 
 
@@ -194,12 +196,15 @@ def bn_train(y: Tensor, gamma: Tensor, beta: Tensor, rmean: Tensor, rvar: Tensor
 
 def bn_train_bwd(dout: Tensor, y: Tensor, out: Tensor, mean: Tensor, invstd: Tensor,
                  gamma: Tensor, nvalid: Optional[Tensor], relu: bool, dgamma: Tensor,
-                 dbeta: Tensor) -> Tensor:
-    """Backward of bn_train; returns d(pre-BN input) and, via relu mask, the grad that also
-    flows to the residual (= masked dout, returned by the caller when needed)."""
+                 dbeta: Tensor, want_dres: bool = False):
+    """Backward of bn_train: d(pre-BN input); with ``want_dres`` also the grad flowing into
+    the residual branch (the ReLU-masked ``dout``)."""
     G, N = y.shape[:2]
     C = y.shape[-1]
     dy = torch.zeros_like(y)
+    dres = None
+    if want_dres:
+        dres = relu_mask_bwd(dout, out) if relu else dout.clone()
     for g in range(G):
         n = _rows_valid(nvalid, g, N)
         if n == 0:
@@ -215,6 +220,8 @@ def bn_train_bwd(dout: Tensor, y: Tensor, out: Tensor, mean: Tensor, invstd: Ten
         dbeta[g] += sd
         dx = gamma[g].to(_cdt()) * invstd[g] / cnt * (cnt * d - sd - xhat * sdx)
         dy[g, :n] = dx.to(dy.dtype)
+    if want_dres:
+        return dy, dres
     return dy
 
 
@@ -240,7 +247,7 @@ def maxpool2d(x: Tensor, k: int, s: int, p: int) -> Tuple[Tensor, Tensor]:
             _nhwc(ind).reshape(G, N, y.shape[2], y.shape[3], C).to(torch.int32))
 
 
-def maxpool2d_bwd(dy: Tensor, ind: Tensor, in_shape: Sequence[int]) -> Tensor:
+def maxpool2d_bwd(dy: Tensor, ind: Tensor, in_shape: Sequence[int], k: int, s: int, p: int) -> Tensor:
     G, N, H, W, C = in_shape
     Ho, Wo = dy.shape[2], dy.shape[3]
     dyn = _nchw(dy.to(_cdt()).reshape(G * N, Ho, Wo, C)).contiguous()

@@ -1,0 +1,268 @@
+"""HIP kernels vs the plain-PyTorch fp32 reference of the same op (GPU only).
+
+Every test runs the gfx950 kernel from ``libdba_kernels.so`` (never a fallback: the hip
+module raises if the library is missing) and compares against
+:mod:`dba_mod_amd.ops.reference` evaluated in fp32 on the same inputs.  Tolerances reflect
+bf16 operands with fp32 accumulation.
+"""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def H():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from dba_mod_amd.ops import hip
+    return hip
+
+
+@pytest.fixture(scope="module")
+def R():
+    from dba_mod_amd.ops import reference
+    return reference
+
+
+def _close(a, b, rtol, atol, what=""):
+    a, b = a.float().cpu(), b.float().cpu()
+    err = (a - b).abs()
+    tol = atol + rtol * b.abs()
+    bad = (err > tol).sum().item()
+    assert bad == 0, f"{what}: {bad}/{a.numel()} out of tol, max err {err.max().item():.3e}"
+
+
+def _rel(a, b):
+    a, b = a.float().cpu(), b.float().cpu()
+    return ((a - b).norm() / b.norm().clamp(min=1e-12)).item()
+
+
+CONV_CASES = [
+    # G, N, H, W, Cin, Cout, k, stride, pad
+    (3, 5, 32, 32, 3, 32, 3, 1, 1),      # CIFAR stem (generic path)
+    (2, 4, 32, 32, 32, 32, 3, 1, 1),     # layer1
+    (2, 4, 32, 32, 32, 64, 3, 2, 1),     # layer2.0.conv1 (stride 2)
+    (2, 4, 32, 32, 32, 64, 1, 2, 0),     # shortcut 1x1 s2
+    (2, 3, 8, 8, 128, 256, 3, 2, 1),     # layer4.0.conv1
+    (2, 3, 64, 64, 3, 64, 7, 2, 3),      # Tiny stem
+    (2, 6, 28, 28, 1, 20, 5, 1, 0),      # MnistNet conv1
+    (2, 6, 12, 12, 20, 50, 5, 1, 0),     # MnistNet conv2
+    (3, 7, 1, 1, 800, 500, 1, 1, 0),     # fc1 as 1x1
+    (3, 7, 1, 1, 256, 10, 1, 1, 0),      # CIFAR linear
+]
+
+
+@pytest.mark.parametrize("case", CONV_CASES)
+def test_conv_fwd_dgrad_wgrad(H, R, case):
+    G, N, Hh, Ww, Cin, Cout, k, s, p = case
+    dev = torch.device("cuda")
+    torch.manual_seed(0)
+    x = torch.randn(G, N, Hh, Ww, Cin, device=dev).bfloat16()
+    w = (torch.randn(G + 1, Cout, k, k, Cin, device=dev) * (1.0 / (k * k * Cin) ** 0.5)).bfloat16()
+    wsel = torch.tensor([(g + 1) % (G + 1) for g in range(G)], dtype=torch.int32, device=dev)
+    bias = torch.randn(G + 1, Cout, device=dev)
+    nvalid = torch.tensor([N] + [max(1, N - 2)] * (G - 1), dtype=torch.int32, device=dev)
+    Ho = (Hh + 2 * p - k) // s + 1
+    res = torch.randn(G, N, Ho, Ho, Cout, device=dev).bfloat16()
+    y = H.conv2d(x, w, wsel, s, p, bias=bias, residual=res, relu=True, nvalid=nvalid)
+    yr = R.conv2d(x.float(), w.float(), wsel, s, p, bias=bias, residual=res.float(), relu=True)
+    for g in range(G):
+        n = int(nvalid[g])
+        _close(y[g, :n], yr[g, :n], 2e-2, 3e-2, f"fwd g{g}")
+    # data gradient
+    dy = torch.randn(G, N, Ho, Ho, Cout, device=dev).bfloat16()
+    for g in range(G):
+        dy[g, int(nvalid[g]):] = 0
+    dx = H.conv2d_dgrad(dy, w, wsel, s, p, (Hh, Ww), nvalid=nvalid)
+    dxr = R.conv2d_dgrad(dy.float(), w.float(), wsel, s, p, (Hh, Ww))
+    for g in range(G):
+        n = int(nvalid[g])
+        assert _rel(dx[g, :n], dxr[g, :n]) < 1e-2, f"dgrad g{g}"
+    # weight gradient (+ bias grad), accumulated into a strided flat buffer view
+    P = Cout * k * k * Cin + 64
+    flat = torch.zeros(G, P, device=dev)
+    dw = flat[:, :Cout * k * k * Cin].view(G, Cout, k, k, Cin)
+    db = torch.zeros(G, Cout, device=dev)
+    H.conv2d_wgrad(dy, x, s, p, k, k, dw, db, nvalid=nvalid)
+    dwr = torch.zeros(G, Cout, k, k, Cin, device=dev)
+    dbr = torch.zeros(G, Cout, device=dev)
+    R.conv2d_wgrad(dy.float(), x.float(), s, p, k, k, dwr, dbr)
+    for g in range(G):
+        assert _rel(dw[g], dwr[g]) < 1e-2, f"wgrad g{g}"
+        assert _rel(db[g], dbr[g]) < 1e-3, f"bias grad g{g}"
+
+
+def test_conv_fp32_out_and_inactive_group(H, R):
+    dev = torch.device("cuda")
+    x = torch.randn(2, 4, 1, 1, 512, device=dev).bfloat16()
+    w = torch.randn(2, 200, 1, 1, 512, device=dev).bfloat16() * 0.05
+    nv = torch.tensor([4, 0], dtype=torch.int32, device=dev)
+    y = H.conv2d(x, w, None, 1, 0, nvalid=nv, out_dtype=torch.float32)
+    assert y.dtype == torch.float32
+    yr = R.conv2d(x.float(), w.float(), None, 1, 0)
+    assert _rel(y[0], yr[0]) < 1e-2
+
+
+@pytest.mark.parametrize("C,relu,with_res", [(32, True, False), (64, True, True), (256, False, False), (512, True, True)])
+def test_bn_train_fwd_bwd(H, R, C, relu, with_res):
+    dev = torch.device("cuda")
+    torch.manual_seed(1)
+    G, N, Hh = 3, 6, 4
+    y = (torch.randn(G, N, Hh, Hh, C, device=dev) * 2 + 0.5).bfloat16()
+    nvalid = torch.tensor([6, 3, 0], dtype=torch.int32, device=dev)
+    S = 4 * C + 64
+    st = torch.zeros(G, S, device=dev)
+    gamma, beta, rm, rv = (st[:, i * C:(i + 1) * C] for i in range(4))
+    gamma.copy_(torch.rand(G, C) + 0.5)
+    beta.copy_(torch.randn(G, C) * 0.1)
+    rv.fill_(1.0)
+    st_ref = st.clone()
+    res = torch.randn(G, N, Hh, Hh, C, device=dev).bfloat16() if with_res else None
+    out, mean, invstd = H.bn_train(y, gamma, beta, rm, rv, nvalid, 0.1, 1e-5, relu, res)
+    g_r, b_r, rm_r, rv_r = (st_ref[:, i * C:(i + 1) * C] for i in range(4))
+    out_r, mean_r, inv_r = R.bn_train(y.float(), g_r, b_r, rm_r, rv_r, nvalid, 0.1, 1e-5, relu,
+                                      res.float() if res is not None else None)
+    for g in range(2):
+        n = int(nvalid[g])
+        _close(out[g, :n], out_r[g, :n], 2e-2, 2e-2, "bn out")
+        _close(mean[g], mean_r[g], 1e-4, 1e-4, "mean")
+        _close(invstd[g], inv_r[g], 1e-3, 1e-4, "invstd")
+    _close(st[:, 2 * C:], st_ref[:, 2 * C:], 1e-4, 1e-5, "running stats")
+    assert out[1, 3:].float().abs().max().item() == 0.0        # padded rows zeroed
+    dout = torch.randn_like(out.float()).bfloat16()
+    gr = torch.zeros(G, 2 * C + 64, device=dev)
+    dy, dres = H.bn_train_bwd(dout, y, out, mean, invstd, gamma, nvalid, relu, gr[:, :C], gr[:, C:2 * C],
+                              want_dres=True)
+    gr_r = torch.zeros_like(gr)
+    dy_r, dres_r = R.bn_train_bwd(dout.float(), y.float(), out.float(), mean, invstd, gamma, nvalid, relu,
+                                  gr_r[:, :C], gr_r[:, C:2 * C], want_dres=True)
+    for g in range(2):
+        n = int(nvalid[g])
+        assert _rel(dy[g, :n], dy_r[g, :n]) < 2e-2
+        assert _rel(dres[g, :n], dres_r[g, :n]) < 1e-2
+    _close(gr, gr_r, 2e-2, 2e-2, "dgamma/dbeta")
+
+
+def test_bn_fold(H, R):
+    dev = torch.device("cuda")
+    slots, Cout, K = 3, 64, 288
+    S = Cout * K + 4 * Cout + 64
+    st = torch.randn(slots, S, device=dev)
+    w = st[:, :Cout * K].view(slots, Cout, 3, 3, 32)
+    o = Cout * K
+    gamma, beta, rm, rv = (st[:, o + i * Cout:o + (i + 1) * Cout] for i in range(4))
+    rv.abs_()
+    wf, bf = H.bn_fold(w, None, gamma, beta, rm, rv, 1e-5, torch.bfloat16)
+    wf_r, bf_r = R.bn_fold(w, None, gamma, beta, rm, rv, 1e-5, torch.float32)
+    _close(wf, wf_r, 1e-2, 1e-3, "wf")
+    _close(bf, bf_r, 1e-4, 1e-4, "bf")
+
+
+def test_gather_and_triggers(H, R):
+    dev = torch.device("cuda")
+    src = torch.randint(0, 256, (50, 32, 32, 3), dtype=torch.uint8, device=dev)
+    labels = torch.randint(0, 10, (50,), dtype=torch.int32, device=dev)
+    idx = torch.randint(0, 50, (3, 8), dtype=torch.int32, device=dev)
+    idx[2, 5:] = -1
+    masks = torch.zeros(2, 32, 32, dtype=torch.uint8, device=dev)
+    masks[0, 0, :6] = 1
+    masks[1, 4, 9:15] = 1
+    trig = torch.tensor([0, -1, 1], dtype=torch.int32, device=dev)
+    pn = torch.tensor([3, 0, 8], dtype=torch.int32, device=dev)
+    seeds = torch.tensor([11, 22, 33], dtype=torch.int32, device=dev)
+    for fs in (None, seeds):
+        for dt in (torch.bfloat16, torch.float32):
+            x, y = H.gather_images(src, labels, idx, masks, trig, pn, 2, fs, dt)
+            xr, yr = R.gather_images(src, labels, idx, masks, trig, pn, 2, fs, torch.float32)
+            _close(x, xr, 1e-2, 1e-6, "gather x")
+            assert torch.equal(y.cpu(), yr.cpu())
+    rows = torch.randn(40, 91, device=dev)
+    lab = torch.randint(0, 9, (40,), dtype=torch.int32, device=dev)
+    cols = torch.tensor([[0, 1], [2, -1]], dtype=torch.int32, device=dev)
+    vals = torch.tensor([[10.0, 80.0], [20.0, 0.0]], device=dev)
+    x, y = H.gather_rows(rows, lab, idx, cols, vals, trig, pn, 7, torch.float32)
+    xr, yr = R.gather_rows(rows, lab, idx, cols, vals, trig, pn, 7, torch.float32)
+    _close(x, xr, 0, 1e-6, "rows")
+    assert torch.equal(y.cpu(), yr.cpu())
+
+
+def test_pool_dropout_relu(H, R):
+    dev = torch.device("cuda")
+    x = torch.randn(2, 3, 24, 24, 20, device=dev).bfloat16()
+    for k, s, p in ((2, 2, 0), (3, 2, 1)):
+        y, ind = H.maxpool2d(x, k, s, p)
+        yr, indr = R.maxpool2d(x.float(), k, s, p)
+        _close(y, yr, 0, 0, "maxpool")
+        dy = torch.randn_like(y.float()).bfloat16()
+        dx = H.maxpool2d_bwd(dy, ind, tuple(x.shape), k, s, p)
+        dxr = R.maxpool2d_bwd(dy.float(), ind, tuple(x.shape), k, s, p)
+        _close(dx, dxr, 1e-2, 1e-2, "maxpool bwd")
+    a = torch.randn(2, 5, 4, 4, 64, device=dev).bfloat16()
+    _close(H.avgpool_global(a), R.avgpool_global(a.float()), 1e-2, 1e-2, "gap")
+    d = torch.randn(2, 5, 1, 1, 64, device=dev).bfloat16()
+    _close(H.avgpool_global_bwd(d, (4, 4)), R.avgpool_global_bwd(d.float(), (4, 4)), 1e-2, 1e-3, "gap bwd")
+    seeds = torch.tensor([5, 9], dtype=torch.int32, device=dev)
+    h = torch.randn(2, 7, 46, device=dev)
+    _close(H.dropout(h, 0.5, seeds, 3), R.dropout(h, 0.5, seeds, 3), 0, 1e-6, "dropout")
+    o = torch.randn(3, 1001, device=dev).bfloat16()
+    dd = torch.randn(3, 1001, device=dev).bfloat16()
+    _close(H.relu_mask_bwd(dd, o), R.relu_mask_bwd(dd.float(), o.float()), 0, 0, "relu mask")
+
+
+def test_softmax_xent(H, R):
+    dev = torch.device("cuda")
+    for C in (10, 200, 9):
+        logits = torch.randn(4, 70, C, device=dev) * 3
+        labels = torch.randint(0, C, (4, 70), dtype=torch.int32, device=dev)
+        labels[1, 40:] = -1
+        labels[3] = -1
+        for mean in (True, False):
+            l, c, d = H.softmax_xent(logits, labels, mean, True)
+            lr_, cr, dr = R.softmax_xent(logits, labels, mean, True)
+            _close(l, lr_, 1e-4, 1e-4, "loss")
+            assert torch.equal(c.cpu(), cr.cpu())
+            _close(d, dr, 1e-2, 1e-3, "dlogits")
+
+
+def test_sgd_step(H, R):
+    dev = torch.device("cuda")
+    G, P, S = 3, 1024, 1088
+    st = torch.randn(G, S, device=dev)
+    gr = torch.randn(G, P, device=dev)
+    mom = torch.randn(G, P, device=dev)
+    lr = torch.tensor([0.1, 0.05, 0.2], device=dev)
+    first = torch.tensor([1, 0, 0], dtype=torch.int32, device=dev)
+    act = torch.tensor([1, 1, 0], dtype=torch.int32, device=dev)
+    sh = torch.zeros(G, P, dtype=torch.bfloat16, device=dev)
+    fg = torch.zeros(G, P, device=dev)
+    st_r, mom_r, fg_r = st.clone(), mom.clone(), fg.clone()
+    H.sgd_step(st[:, :P], gr, mom, lr, first, act, 0.9, 5e-4, shadow=sh, fg_accum=fg)
+    R.sgd_step(st_r[:, :P], gr, mom_r, lr, first, act, 0.9, 5e-4, fg_accum=fg_r)
+    _close(st, st_r, 1e-6, 1e-6, "params")
+    _close(mom, mom_r, 1e-6, 1e-6, "momentum")
+    _close(fg, fg_r, 0, 0, "fg accum")
+    _close(sh[:2], st[:2, :P], 1e-2, 1e-6, "bf16 shadow")
+
+
+def test_flat_aggregation_ops(H, R):
+    dev = torch.device("cuda")
+    n, L = 10, 100_003
+    pts = torch.randn(n, L + 64, device=dev)[:, :L]
+    m = torch.randn(L, device=dev)
+    _close(H.sq_dists(pts, m), R.sq_dists(pts, m), 1e-5, 1e-3, "sq_dists")
+    wts = torch.rand(n, device=dev)
+    _close(H.weighted_sum(pts, wts), R.weighted_sum(pts, wts), 1e-4, 1e-4, "wsum")
+    base = torch.randn(L, device=dev)
+    w = torch.randn(L, device=dev)
+    _close(H.scale_from_base(w, base, 100.0), R.scale_from_base(w, base, 100.0), 1e-5, 1e-4, "scale")
+    for noise in (False, True):
+        d1 = torch.randn(L, device=dev)
+        d2 = d1.clone()
+        upd = torch.randn(L, device=dev)
+        H.add_noise_scaled(d1, upd, 0.01, 0.01, 1234, noise)
+        R.add_noise_scaled(d2, upd, 0.01, 0.01, 1234, noise)
+        _close(d1, d2, 1e-4, 1e-5, "noise add")
+    for nn_, d in ((10, 2560), (37, 5000), (4, 207)):
+        f = torch.randn(nn_, d, device=dev)
+        _close(H.gram(f), R.gram(f), 1e-4, 1e-2, "gram")

@@ -101,8 +101,11 @@ def test_state_dict_roundtrip_and_keys(arch):
 
 def test_param_counts_match_survey():
     # SURVEY §2.3 [measured]: parameter counts of the reference classes
-    assert get_spec("mnist").P == 431_080
-    assert get_spec("resnet18_cifar").P == 2_797_610
-    assert get_spec("resnet18_cifar").S == 2_797_610 + 4_800
-    assert get_spec("resnet18_tiny").P == 11_279_112
-    assert get_spec("loan").P == 5_529
+    assert get_spec("mnist").n_params == 431_080
+    assert get_spec("resnet18_cifar").n_params == 2_797_610
+    assert sum(e.numel for e in get_spec("resnet18_cifar").buffers) == 4_800
+    assert get_spec("resnet18_tiny").n_params == 11_279_112
+    assert get_spec("loan").n_params == 5_529
+    for a in ("mnist", "resnet18_cifar", "resnet18_tiny", "loan"):
+        s = get_spec(a)
+        assert all(e.offset % 64 == 0 for e in s.params + s.buffers) and s.P % 64 == 0 and s.S % 64 == 0
