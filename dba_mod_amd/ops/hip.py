@@ -31,8 +31,8 @@ _U = ctypes.c_uint
 _SIGS = {
     "dba_gather_images": [_P, _P, _P, _P, _P, _P, _I, _P, _P, _I, _P, _I, _I, _I, _I, _I, _P],
     "dba_gather_rows": [_P, _P, _P, _P, _P, _I, _P, _P, _I, _P, _I, _P, _I, _I, _I, _P],
-    "dba_conv_fwd": [_P, _LL, _P, _LL, _P, _P, _LL, _P, _LL, _P, _LL, _I, _P] + [_I] * 14 + [_P],
-    "dba_conv_dgrad": [_P, _LL, _P, _LL, _P, _P, _LL, _P] + [_I] * 13 + [_P],
+    "dba_conv_fwd": [_P, _LL, _P, _LL, _P, _P, _LL, _P, _LL, _P, _LL, _I, _P] + [_I] * 13 + [_P],
+    "dba_conv_dgrad": [_P, _LL, _P, _LL, _P, _P, _LL, _P] + [_I] * 12 + [_P],
     "dba_conv_wgrad": [_P, _LL, _P, _LL, _P, _LL, _P] + [_I] * 12 + [_P],
     "dba_transpose_w": [_P, _LL, _P, _I, _I, _I, _I, _P],
     "dba_colsum": [_P, _LL, _I, _P, _I, _I, _I, _P, _LL, _P],

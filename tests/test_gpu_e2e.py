@@ -25,6 +25,11 @@ def _rel(a, b):
 @pytest.mark.parametrize("arch,shp", [("resnet18_cifar", (32, 32, 3)), ("mnist", (28, 28, 1)),
                                       ("resnet18_tiny", (64, 64, 3)), ("loan", (91,))])
 def test_train_step_hip_vs_reference(dev, arch, shp):
+    """Grouped train step through the HIP kernels vs the fp32 reference.
+
+    At random init these ReLU+BN nets are chaotic: rounding only the *input* to bf16 moves the
+    fp32 gradient by ~20 % (measured on CPU), so the HIP (bf16 storage) gradient is checked
+    against that sensitivity band, and tightly on the well-conditioned final layer."""
     from dba_mod_amd import ops
     from dba_mod_amd.models import program as P
     from dba_mod_amd.models.spec import get_spec
@@ -38,32 +43,39 @@ def test_train_step_hip_vs_reference(dev, arch, shp):
     lab = torch.randint(0, spec.num_classes, (G, N), device=dev).int()
     lab = torch.where(torch.arange(N, device=dev)[None] < nval[:, None].long(), lab, torch.full_like(lab, -1))
     seeds = torch.tensor([1, 2, 3], dtype=torch.int32, device=dev)
-    results = {}
-    for name, mod, dt in (("hip", hip, torch.bfloat16), ("ref", reference, torch.float32)):
-        state = flat[None].repeat(G, 1).contiguous()
+
+    def run(mod, dt, xin, fl):
+        state = fl[None].repeat(G, 1).contiguous()
         wcomp = state[:, :spec.P].to(dt).contiguous() if dt != torch.float32 else state
         grads = torch.zeros(G, spec.P, device=dev)
-        # route every op of this pass to one implementation
         saved = {k: getattr(ops, k) for k in ops._OPS}
         for k in ops._OPS:
             setattr(ops, k, getattr(mod, k))
         try:
             ctx = P.Ctx(spec, state, wcomp, None, train=True, grads=grads, nvalid=nval, dropout_seed=seeds,
                         act_dtype=dt)
-            xx = x.to(dt)
-            logits = P.forward(ctx, xx)
-            loss, corr, dl = ops.softmax_xent(logits, lab, True, True)
+            logits = P.forward(ctx, xin.to(dt))
+            loss, _, dl = ops.softmax_xent(logits, lab, True, True)
             ctx.tape.backward(logits, dl)
         finally:
             for k, v in saved.items():
                 setattr(ops, k, v)
-        results[name] = (loss, grads, state)
-    lh, gh, sh = results["hip"]
-    lr_, gr, sr = results["ref"]
+        return loss, grads, state
+
+    lh, gh, sh = run(hip, torch.bfloat16, x, flat)
+    lr_, gr, sr = run(reference, torch.float32, x, flat)
+    flr = flat.clone()
+    flr[:spec.P] = flr[:spec.P].bfloat16().float()
+    _, gp, _ = run(reference, torch.float32, x.bfloat16().float(), flr)
+    fc = spec.params[-2]
     for g in range(2):
-        assert abs(lh[g].item() - lr_[g].item()) < 0.05 * max(1.0, abs(lr_[g].item()))
-        assert _rel(gh[g], gr[g]) < 0.08, (arch, g, _rel(gh[g], gr[g]))
-        assert _rel(sh[g, spec.P:], sr[g, spec.P:]) < 2e-2 if spec.B else True
+        assert abs(lh[g].item() - lr_[g].item()) < 0.03 * max(1.0, abs(lr_[g].item()))
+        band = _rel(gp[g], gr[g])
+        assert _rel(gh[g], gr[g]) < max(0.08, 1.6 * band), (arch, g, _rel(gh[g], gr[g]), band)
+        sl = slice(fc.offset, fc.offset + fc.numel)
+        assert _rel(gh[g, sl], gr[g, sl]) < 0.05, (arch, "final layer")
+        if spec.B:
+            assert _rel(sh[g, spec.P:], sr[g, spec.P:]) < 2e-2
     assert gh[2].abs().max().item() == 0.0          # inactive replica untouched
 
 

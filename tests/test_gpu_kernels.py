@@ -177,8 +177,8 @@ def test_gather_and_triggers(H, R):
             xr, yr = R.gather_images(src, labels, idx, masks, trig, pn, 2, fs, torch.float32)
             _close(x, xr, 1e-2, 1e-6, "gather x")
             assert torch.equal(y.cpu(), yr.cpu())
-    rows = torch.randn(40, 91, device=dev)
-    lab = torch.randint(0, 9, (40,), dtype=torch.int32, device=dev)
+    rows = torch.randn(50, 91, device=dev)          # idx above indexes rows 0..49
+    lab = torch.randint(0, 9, (50,), dtype=torch.int32, device=dev)
     cols = torch.tensor([[0, 1], [2, -1]], dtype=torch.int32, device=dev)
     vals = torch.tensor([[10.0, 80.0], [20.0, 0.0]], device=dev)
     x, y = H.gather_rows(rows, lab, idx, cols, vals, trig, pn, 7, torch.float32)
