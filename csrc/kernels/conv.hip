@@ -326,9 +326,10 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgradArgs a) {
   }
 }
 
-// dW^T for the data gradient: [slots][Co][T][Ci] -> [slots][Ci][T][Co]
+// dW^T for the data gradient: [slots][Co][T][Ci] -> [slots][Ci][T][Co]; with `flip` the taps
+// are also reversed (t -> T-1-t), turning a stride-1 dgrad into a forward conv (halo kernel)
 __global__ void transpose_w_kernel(const uint16_t* __restrict__ w, long long w_sstride, uint16_t* __restrict__ wt,
-                                   int slots, int Co, int T, int Ci) {
+                                   int slots, int Co, int T, int Ci, int flip) {
   const long long per = (long long)Co * T * Ci;
   const long long total = per * slots;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
@@ -338,7 +339,8 @@ __global__ void transpose_w_kernel(const uint16_t* __restrict__ w, long long w_s
     const int t = (int)(r % T);
     const int ci = (int)(r / T);
     // i indexes the OUTPUT [s][ci][t][co] (co fastest) -> coalesced writes
-    wt[i] = w[(long long)s * w_sstride + ((long long)co * T + t) * Ci + ci];
+    const int ts = flip ? T - 1 - t : t;
+    wt[i] = w[(long long)s * w_sstride + ((long long)co * T + ts) * Ci + ci];
   }
 }
 
@@ -423,11 +425,11 @@ DBA_EXPORT int dba_conv_wgrad(const void* dy, long long dy_gstride, const void* 
 }
 
 DBA_EXPORT int dba_transpose_w(const void* w, long long w_sstride, void* wt, int slots, int Co, int T, int Ci,
-                               void* stream) {
+                               int flip, void* stream) {
   const long long total = (long long)slots * Co * T * Ci;
   const int blocks = (int)std::min(4096LL, (total + 255) / 256);
   hipLaunchKernelGGL(transpose_w_kernel, dim3(std::max(1, blocks)), dim3(256), 0, (hipStream_t)stream,
-                     (const uint16_t*)w, w_sstride, (uint16_t*)wt, slots, Co, T, Ci);
+                     (const uint16_t*)w, w_sstride, (uint16_t*)wt, slots, Co, T, Ci, flip);
   DBA_LAUNCH_CHECK();
 }
 

@@ -1,0 +1,364 @@
+// Implicit-GEMM convolution, generation 2 (gfx950): the hot path for every conv / linear
+// whose source channel count is a multiple of 8 (all ResNet-18 layers, both passes).
+//
+// vs conv.hip (kept for odd channel counts):
+//   * v_mfma_f32_32x32x16_bf16 (half the LDS operand traffic per FLOP of 16x16x32);
+//   * BK = 64 per barrier, double-buffered LDS with register-staged prefetch: the global
+//     gathers of step k+1 are in flight while step k's MFMAs run;
+//   * LDS rows padded to 144 B: the 32 lanes of a fragment read hit 32 distinct bank slots
+//     (row*36 dwords mod 64 is a bijection over 16 consecutive rows);
+//   * the output tile is staged through LDS in fp32 and written back in 16-byte bf16 chunks
+//     (bias / residual / ReLU applied in that pass) instead of 2-byte scattered stores;
+//   * linearised block index with the N-tile fastest, so blocks sharing an A (activation)
+//     row panel are dispatched back to back.
+// Source segments of 8 channels never straddle a tap (Cs % 8 == 0), so every A load is one
+// aligned 16-B vector load whatever the tap geometry (stem 7x7/s2, 3x3, 1x1 shortcut, linear).
+#include "common.hpp"
+#include <algorithm>
+
+namespace {
+
+constexpr int BK2 = 64;
+constexpr int LP = BK2 + 8;   // u16 per LDS row (144 B)
+
+struct Igemm2Args {
+  const uint16_t* src; long long src_gstride;   // [G][N][Hs][Ws][Cs]
+  const uint16_t* w; long long w_sstride;       // [slots][Ncol][K]
+  const int* wsel;
+  const float* bias; long long b_sstride;
+  const uint16_t* res;                          // [G][M][Ncol] (same layout as out)
+  void* out; long long out_gstride;             // [G][M][Ncol]
+  const int* nvalid;
+  int N, Hs, Ws, Cs, Ho, Wo, Ncol, KH, KW, stride, pad, relu;
+  int tiles_n;
+};
+
+template <int MODE>
+__device__ __forceinline__ bool src_pos2(const Igemm2Args& a, int p, int q, int kh, int kw, int& hs, int& ws) {
+  if (MODE == 0) {
+    hs = p * a.stride - a.pad + kh;
+    ws = q * a.stride - a.pad + kw;
+    return (unsigned)hs < (unsigned)a.Hs && (unsigned)ws < (unsigned)a.Ws;
+  } else {
+    int th = p + a.pad - kh, tw = q + a.pad - kw;
+    if (th < 0 || tw < 0) return false;
+    if (a.stride != 1) {
+      if ((th % a.stride) | (tw % a.stride)) return false;
+      th /= a.stride;
+      tw /= a.stride;
+    }
+    hs = th; ws = tw;
+    return th < a.Hs && tw < a.Ws;
+  }
+}
+
+template <int BM, int BN, int WM, int WN, int MODE, typename OutT>
+__global__ __launch_bounds__(256) void igemm2_kernel(Igemm2Args a) {
+  constexpr int TM = BM / WM, TN = BN / WN;          // wave tile
+  constexpr int MI = TM / 32, NJ = TN / 32;          // 32x32 MFMA tiles per wave
+  constexpr int RA = BM * 8 / 256;                   // A 16-B loads per thread per k-step
+  constexpr int RB = (BN * 8 + 255) / 256;           // B 16-B loads per thread
+  static_assert(WM * WN == 4, "4 waves");
+  static_assert(MI >= 1 && NJ >= 1, "wave tile >= 32x32");
+  constexpr int LDS_AB = 2 * (BM + BN) * LP;         // u16
+  constexpr int LDS_C = BM * BN * 2;                  // u16 (fp32 staging)
+  __shared__ __attribute__((aligned(16))) uint16_t smem[LDS_AB > LDS_C ? LDS_AB : LDS_C];
+  uint16_t (*As)[BM][LP] = reinterpret_cast<uint16_t (*)[BM][LP]>(smem);
+  uint16_t (*Bs)[BN][LP] = reinterpret_cast<uint16_t (*)[BN][LP]>(smem + 2 * BM * LP);
+
+  const int g = blockIdx.y;
+  const int HoWo = a.Ho * a.Wo;
+  const int Mv = valid_rows(a.nvalid, g, a.N) * HoWo;
+  const int tn = blockIdx.x % a.tiles_n, tm = blockIdx.x / a.tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  if (m0 >= Mv) return;
+  const int K = a.KH * a.KW * a.Cs;
+  const int nk = (K + BK2 - 1) / BK2;
+  const uint16_t* __restrict__ src = a.src + (long long)g * a.src_gstride;
+  const int slot = a.wsel ? a.wsel[g] : g;
+  const uint16_t* __restrict__ Wp = a.w + (long long)slot * a.w_sstride;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WN, wn = wid % WN;
+
+  // staging geometry: A load i covers row (tid>>3) + 32*i, segment tid&7 (8 channels)
+  const int seg = tid & 7;
+  int rbase[RA], rp[RA], rq[RA];
+#pragma unroll
+  for (int i = 0; i < RA; ++i) {
+    const int m = m0 + (tid >> 3) + 32 * i;
+    if (m < Mv) {
+      const int n = m / HoWo, rem = m - n * HoWo;
+      rp[i] = rem / a.Wo;
+      rq[i] = rem - rp[i] * a.Wo;
+      rbase[i] = n;
+    } else {
+      rbase[i] = -1; rp[i] = 0; rq[i] = 0;
+    }
+  }
+  uint4 ra[RA], rb[RB];
+
+  auto load_tiles = [&](int kc) {
+    const int k = kc * BK2 + seg * 8;
+    const bool kin = k < K;
+    const int tap = k / a.Cs;
+    const int c = k - tap * a.Cs;
+    const int kh = tap / a.KW, kw = tap - kh * a.KW;
+#pragma unroll
+    for (int i = 0; i < RA; ++i) {
+      int hs, ws;
+      ra[i] = make_uint4(0, 0, 0, 0);
+      if (kin && rbase[i] >= 0 && src_pos2<MODE>(a, rp[i], rq[i], kh, kw, hs, ws))
+        ra[i] = *(const uint4*)(src + (((long long)rbase[i] * a.Hs + hs) * a.Ws + ws) * a.Cs + c);
+    }
+#pragma unroll
+    for (int i = 0; i < RB; ++i) {
+      const int r = (tid >> 3) + 32 * i;
+      rb[i] = make_uint4(0, 0, 0, 0);
+      if (r < BN && kin && n0 + r < a.Ncol) rb[i] = *(const uint4*)(Wp + (long long)(n0 + r) * K + k);
+    }
+  };
+  auto store_tiles = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < RA; ++i) *(uint4*)&As[buf][(tid >> 3) + 32 * i][seg * 8] = ra[i];
+#pragma unroll
+    for (int i = 0; i < RB; ++i) {
+      const int r = (tid >> 3) + 32 * i;
+      if (r < BN) *(uint4*)&Bs[buf][r][seg * 8] = rb[i];
+    }
+  };
+
+  f32x16_t acc[MI][NJ];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  load_tiles(0);
+  store_tiles(0);
+  __syncthreads();
+  const int fr = lane & 31, fk = (lane >> 5) * 8;
+  int cur = 0;
+  for (int kc = 0; kc < nk; ++kc) {
+    if (kc + 1 < nk) load_tiles(kc + 1);
+#pragma unroll
+    for (int kk = 0; kk < BK2; kk += 16) {
+      bf16x8_t af[MI], bfr[NJ];
+#pragma unroll
+      for (int i = 0; i < MI; ++i) af[i] = *(const bf16x8_t*)&As[cur][wm * TM + i * 32 + fr][kk + fk];
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) bfr[j] = *(const bf16x8_t*)&Bs[cur][wn * TN + j * 32 + fr][kk + fk];
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    if (kc + 1 < nk) store_tiles(cur ^ 1);
+    __syncthreads();
+    cur ^= 1;
+  }
+
+  // ---- epilogue: stage fp32 tile in LDS, then 8-wide vector pass with bias/res/ReLU
+  float* Cst = reinterpret_cast<float*>(smem);
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = wm * TM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        const int col = wn * TN + j * 32 + fr;
+        Cst[row * BN + col] = acc[i][j][r];
+      }
+  __syncthreads();
+  OutT* out = (OutT*)a.out + (long long)g * a.out_gstride;
+  const float* bias = a.bias ? a.bias + (long long)slot * a.b_sstride : nullptr;
+  const uint16_t* res = a.res ? a.res + (long long)g * a.out_gstride : nullptr;
+  constexpr int CH = BN / 8;                         // 8-col chunks per row
+  const bool full_n = (n0 + BN <= a.Ncol) && (a.Ncol % 8 == 0);
+  for (int e = tid; e < BM * CH; e += 256) {
+    const int row = e / CH, c8 = (e - row * CH) * 8;
+    const int m = m0 + row;
+    if (m >= Mv) continue;
+    float v[8];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) v[t] = Cst[row * BN + c8 + t];
+    const int n = n0 + c8;
+    const long long o = (long long)m * a.Ncol + n;
+    if (full_n) {
+      if (bias) {
+#pragma unroll
+        for (int t = 0; t < 8; ++t) v[t] += bias[n + t];
+      }
+      if (res) {
+        const uint4 rv = *(const uint4*)(res + o);
+        const uint16_t* rp2 = (const uint16_t*)&rv;
+#pragma unroll
+        for (int t = 0; t < 8; ++t) v[t] += bf2f(rp2[t]);
+      }
+      if (a.relu) {
+#pragma unroll
+        for (int t = 0; t < 8; ++t) v[t] = fmaxf(v[t], 0.f);
+      }
+      if constexpr (sizeof(OutT) == 2) {
+        uint4 pk;
+        uint16_t* pp = (uint16_t*)&pk;
+#pragma unroll
+        for (int t = 0; t < 8; ++t) pp[t] = f2bf(v[t]);
+        *(uint4*)((uint16_t*)out + o) = pk;
+      } else {
+#pragma unroll
+        for (int t = 0; t < 8; ++t) ((float*)out)[o + t] = v[t];
+      }
+    } else {
+      for (int t = 0; t < 8 && n + t < a.Ncol; ++t) {
+        float x = v[t] + (bias ? bias[n + t] : 0.f);
+        if (res) x += bf2f(res[o + t]);
+        if (a.relu) x = fmaxf(x, 0.f);
+        out[o + t] = from_f<OutT>(x);
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------- small-channel sources
+// Stems / first layers with Cs < 8 (CIFAR 3x3x3, Tiny 7x7x3, MNIST 5x5x1): every thread
+// gathers ONE output row's receptive field (k = tap*Cs + c, contiguous within a kernel row
+// in NHWC) straight into its LDS row; K <= 160 is consumed in 32-wide MFMA k-steps.
+template <typename OutT, int KMAX>
+__global__ __launch_bounds__(256) void igemm_small_kernel(Igemm2Args a) {
+  constexpr int BM = 256, BN = 32;
+  constexpr int LPs = KMAX + 8;
+  __shared__ __attribute__((aligned(16))) uint16_t As[BM][LPs];
+  __shared__ __attribute__((aligned(16))) uint16_t Bs[BN][LPs];
+  const int g = blockIdx.y;
+  const int HoWo = a.Ho * a.Wo;
+  const int Mv = valid_rows(a.nvalid, g, a.N) * HoWo;
+  const int tn = blockIdx.x % a.tiles_n, tm = blockIdx.x / a.tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  if (m0 >= Mv) return;
+  const int K = a.KH * a.KW * a.Cs;
+  const int Kp = (K + 31) & ~31;
+  const uint16_t* __restrict__ src = a.src + (long long)g * a.src_gstride;
+  const int slot = a.wsel ? a.wsel[g] : g;
+  const uint16_t* __restrict__ Wp = a.w + (long long)slot * a.w_sstride;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  {  // A: one row per thread
+    const int m = m0 + tid;
+    uint16_t* dst = As[tid];
+    if (m < Mv) {
+      const int n = m / HoWo, rem = m - n * HoWo, p = rem / a.Wo, q = rem - p * a.Wo;
+      int k = 0;
+      for (int kh = 0; kh < a.KH; ++kh) {
+        const int hs = p * a.stride - a.pad + kh;
+        const bool hin = (unsigned)hs < (unsigned)a.Hs;
+        for (int kw = 0; kw < a.KW; ++kw) {
+          const int ws = q * a.stride - a.pad + kw;
+          const bool in = hin && (unsigned)ws < (unsigned)a.Ws;
+          const uint16_t* s = src + (((long long)n * a.Hs + hs) * a.Ws + ws) * a.Cs;
+          for (int c = 0; c < a.Cs; ++c) dst[k++] = in ? s[c] : (uint16_t)0;
+        }
+      }
+      for (; k < Kp; ++k) dst[k] = 0;
+    } else {
+      for (int k = 0; k < Kp; ++k) dst[k] = 0;
+    }
+  }
+  for (int e = tid; e < BN * Kp; e += 256) {   // B: [BN][Kp], zero-padded
+    const int r = e / Kp, k = e - r * Kp;
+    Bs[r][k] = (k < K && n0 + r < a.Ncol) ? Wp[(long long)(n0 + r) * K + k] : (uint16_t)0;
+  }
+  __syncthreads();
+  // 4 waves x (64 rows x 32 cols): 2 MFMA 32x32 tiles per wave
+  f32x16_t acc[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[i][r] = 0.f;
+  const int fr = lane & 31, fk = (lane >> 5) * 8;
+  for (int kk = 0; kk < Kp; kk += 16) {
+    const bf16x8_t b = *(const bf16x8_t*)&Bs[fr][kk + fk];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const bf16x8_t av = *(const bf16x8_t*)&As[wid * 64 + i * 32 + fr][kk + fk];
+      acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, b, acc[i], 0, 0, 0);
+    }
+  }
+  OutT* out = (OutT*)a.out + (long long)g * a.out_gstride;
+  const float* bias = a.bias ? a.bias + (long long)slot * a.b_sstride : nullptr;
+  const uint16_t* res = a.res ? a.res + (long long)g * a.out_gstride : nullptr;
+  const int n = n0 + fr;
+  if (n >= a.Ncol) return;
+  const float bv = bias ? bias[n] : 0.f;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int m = m0 + wid * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+      if (m >= Mv) continue;
+      const long long o = (long long)m * a.Ncol + n;
+      float v = acc[i][r] + bv;
+      if (res) v += bf2f(res[o]);
+      if (a.relu) v = fmaxf(v, 0.f);
+      out[o] = from_f<OutT>(v);
+    }
+}
+
+template <int BM, int BN, int WM, int WN, int MODE, typename OutT>
+int launch2(Igemm2Args a, int G, hipStream_t st) {
+  const int M = a.N * a.Ho * a.Wo;
+  a.tiles_n = ceil_div(a.Ncol, BN);
+  dim3 grid((unsigned)(ceil_div(M, BM) * a.tiles_n), G);
+  hipLaunchKernelGGL((igemm2_kernel<BM, BN, WM, WN, MODE, OutT>), grid, dim3(256), 0, st, a);
+  DBA_LAUNCH_CHECK();
+}
+
+template <int MODE, typename OutT>
+int dispatch2(Igemm2Args a, int G, hipStream_t st) {
+  const long long M = (long long)a.N * a.Ho * a.Wo;
+  if (a.Ncol <= 32) return launch2<128, 32, 4, 1, MODE, OutT>(a, G, st);
+  if (a.Ncol <= 64) return launch2<128, 64, 2, 2, MODE, OutT>(a, G, st);
+  // wide outputs: 128x128 tiles unless the launch would not fill the chip
+  if (M * G / 128 * ((a.Ncol + 127) / 128) >= 512) return launch2<128, 128, 2, 2, MODE, OutT>(a, G, st);
+  return launch2<64, 128, 1, 4, MODE, OutT>(a, G, st);
+}
+
+}  // namespace
+
+// Returns -100 when the shape is not handled here (caller falls back to conv.hip kernels).
+DBA_EXPORT int dba_conv2_fwd(const void* x, long long x_gstride, const void* w, long long w_sstride, const int* wsel,
+                             const float* bias, long long b_sstride, const void* res, void* out, long long out_gstride,
+                             int out_f32, const int* nvalid, int G, int N, int H, int W, int Cin, int Ho, int Wo,
+                             int Cout, int KH, int KW, int stride, int pad, int relu, void* stream) {
+  Igemm2Args a{(const uint16_t*)x, x_gstride, (const uint16_t*)w, w_sstride, wsel, bias, b_sstride,
+               (const uint16_t*)res, out, out_gstride, nvalid, N, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, relu, 1};
+  hipStream_t st = (hipStream_t)stream;
+  if (Cin % 8 == 0)
+    return out_f32 ? dispatch2<0, float>(a, G, st) : dispatch2<0, uint16_t>(a, G, st);
+  if (Cin < 8 && KH * KW * Cin <= 160) {
+    a.tiles_n = ceil_div(Cout, 32);
+    dim3 grid((unsigned)(ceil_div((long long)N * Ho * Wo, 256) * a.tiles_n), G);
+    const bool k32 = KH * KW * Cin <= 32;
+    if (out_f32) {
+      if (k32) hipLaunchKernelGGL((igemm_small_kernel<float, 32>), grid, dim3(256), 0, st, a);
+      else hipLaunchKernelGGL((igemm_small_kernel<float, 160>), grid, dim3(256), 0, st, a);
+    } else {
+      if (k32) hipLaunchKernelGGL((igemm_small_kernel<uint16_t, 32>), grid, dim3(256), 0, st, a);
+      else hipLaunchKernelGGL((igemm_small_kernel<uint16_t, 160>), grid, dim3(256), 0, st, a);
+    }
+    DBA_LAUNCH_CHECK();
+  }
+  return -100;
+}
+
+DBA_EXPORT int dba_conv2_dgrad(const void* dy, long long dy_gstride, const void* wt, long long wt_sstride,
+                               const int* wsel, void* dx, long long dx_gstride, const int* nvalid, int G, int N, int H,
+                               int W, int Cin, int Ho, int Wo, int Cout, int KH, int KW, int stride, int pad,
+                               void* stream) {
+  if (Cout % 8 != 0) return -100;
+  Igemm2Args a{(const uint16_t*)dy, dy_gstride, (const uint16_t*)wt, wt_sstride, wsel, nullptr, 0, nullptr, dx,
+               dx_gstride, nvalid, N, Ho, Wo, Cout, H, W, Cin, KH, KW, stride, pad, 0, 1};
+  return dispatch2<1, uint16_t>(a, G, (hipStream_t)stream);
+}

@@ -34,7 +34,10 @@ _SIGS = {
     "dba_conv_fwd": [_P, _LL, _P, _LL, _P, _P, _LL, _P, _LL, _P, _LL, _I, _P] + [_I] * 13 + [_P],
     "dba_conv_dgrad": [_P, _LL, _P, _LL, _P, _P, _LL, _P] + [_I] * 12 + [_P],
     "dba_conv_wgrad": [_P, _LL, _P, _LL, _P, _LL, _P] + [_I] * 12 + [_P],
-    "dba_transpose_w": [_P, _LL, _P, _I, _I, _I, _I, _P],
+    "dba_conv2_fwd": [_P, _LL, _P, _LL, _P, _P, _LL, _P, _P, _LL, _I, _P] + [_I] * 13 + [_P],
+    "dba_conv2_dgrad": [_P, _LL, _P, _LL, _P, _P, _LL, _P] + [_I] * 12 + [_P],
+    "dba_transpose_w": [_P, _LL, _P, _I, _I, _I, _I, _I, _P],
+    "dba_halo_conv": [_P, _LL, _P, _LL, _P, _P, _LL, _P, _P, _LL, _I, _P] + [_I] * 9 + [_P],
     "dba_colsum": [_P, _LL, _I, _P, _I, _I, _I, _P, _LL, _P],
     "dba_bn_stats": [_P, _P, _I, _I, _I, _I, _P, _P],
     "dba_bn_finalize": [_P, _P, _I, _I, _I, _I, _P, _P, _LL, _F, _F, _P, _P, _P],
@@ -61,10 +64,14 @@ for _name, _args in _SIGS.items():
     _fn.restype = ctypes.c_int
 
 
-def _call(name: str, *args) -> None:
+NOT_HANDLED = -100   # a conv2 entry point declining a shape (odd channel counts)
+
+
+def _call(name: str, *args) -> int:
     rc = getattr(_L, name)(*args)
-    if rc != 0:
+    if rc != 0 and rc != NOT_HANDLED:
         raise RuntimeError(f"{name}: HIP error {rc}")
+    return rc
 
 
 def _ptr(t: Optional[Tensor]):
@@ -152,9 +159,22 @@ def conv2d(x, w, wsel, stride, pad, bias=None, residual=None, relu=False, nvalid
         bias, bs = _rowview(bias)
     if residual is not None:
         residual = _bf16c(residual)
-    _call("dba_conv_fwd", x.data_ptr(), N * H * W * Cin, w.data_ptr(), ws, _ptr(_i32(wsel)), _ptr(bias), bs,
-          _ptr(residual), N * Ho * Wo * Cout, y.data_ptr(), N * Ho * Wo * Cout, int(out_dtype == torch.float32),
-          _ptr(_i32(nvalid)), G, N, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, int(relu), _stream())
+    wsel_, nv_, f32 = _ptr(_i32(wsel)), _ptr(_i32(nvalid)), int(out_dtype == torch.float32)
+    # kernel selection by shape: halo-tiled direct conv (stride 1), gen-2 implicit GEMM
+    # (Cin % 8 == 0 or small-Cin stems), gen-1 implicit GEMM (odd channel counts)
+    rc = NOT_HANDLED
+    if stride == 1 and KH == KW:
+        rc = _call("dba_halo_conv", x.data_ptr(), N * H * W * Cin, w.data_ptr(), ws, wsel_, _ptr(bias), bs,
+                   _ptr(residual), y.data_ptr(), N * Ho * Wo * Cout, f32, nv_, G, N, H, W, Cin, Cout, KH, pad,
+                   int(relu), _stream())
+    if rc == NOT_HANDLED:
+        rc = _call("dba_conv2_fwd", x.data_ptr(), N * H * W * Cin, w.data_ptr(), ws, wsel_, _ptr(bias), bs,
+               _ptr(residual), y.data_ptr(), N * Ho * Wo * Cout, f32, nv_, G, N, H, W, Cin, Ho, Wo, Cout, KH, KW,
+               stride, pad, int(relu), _stream())
+    if rc == NOT_HANDLED:
+        _call("dba_conv_fwd", x.data_ptr(), N * H * W * Cin, w.data_ptr(), ws, wsel_, _ptr(bias), bs,
+              _ptr(residual), N * Ho * Wo * Cout, y.data_ptr(), N * Ho * Wo * Cout, f32, nv_, G, N, H, W, Cin, Ho,
+              Wo, Cout, KH, KW, stride, pad, int(relu), _stream())
     return y
 
 
@@ -163,13 +183,22 @@ def conv2d_dgrad(dy, w, wsel, stride, pad, in_hw, nvalid=None, out_dtype=None):
     G, N, Ho, Wo, Cout = dy.shape
     w, ws = _check_w(w)
     slots, _, KH, KW, Cin = w.shape
-    wt = torch.empty(slots, Cin, KH, KW, Cout, dtype=_BF16, device=dy.device)
-    _call("dba_transpose_w", w.data_ptr(), ws, wt.data_ptr(), slots, Cout, KH * KW, Cin, _stream())
     H, W = in_hw
     dx = torch.empty(G, N, H, W, Cin, dtype=_BF16, device=dy.device)
-    _call("dba_conv_dgrad", dy.data_ptr(), N * Ho * Wo * Cout, wt.data_ptr(), Cin * KH * KW * Cout,
-          _ptr(_i32(wsel)), dx.data_ptr(), N * H * W * Cin, _ptr(_i32(nvalid)), G, N, H, W, Cin, Ho, Wo, Cout,
-          KH, KW, stride, pad, _stream())
+    wt = torch.empty(slots, Cin, KH, KW, Cout, dtype=_BF16, device=dy.device)
+    if stride == 1 and KH == KW and pad == (KH - 1) // 2:
+        # stride-1 dgrad == forward conv of dY with tap-flipped, transposed weights
+        _call("dba_transpose_w", w.data_ptr(), ws, wt.data_ptr(), slots, Cout, KH * KW, Cin, 1, _stream())
+        rc = _call("dba_halo_conv", dy.data_ptr(), N * Ho * Wo * Cout, wt.data_ptr(), Cin * KH * KW * Cout,
+                   _ptr(_i32(wsel)), None, 0, None, dx.data_ptr(), N * H * W * Cin, 0, _ptr(_i32(nvalid)), G, N,
+                   Ho, Wo, Cout, Cin, KH, KH - 1 - pad, 0, _stream())
+        if rc != NOT_HANDLED:
+            return dx if out_dtype in (None, _BF16) else dx.to(out_dtype)
+    _call("dba_transpose_w", w.data_ptr(), ws, wt.data_ptr(), slots, Cout, KH * KW, Cin, 0, _stream())
+    args = (dy.data_ptr(), N * Ho * Wo * Cout, wt.data_ptr(), Cin * KH * KW * Cout, _ptr(_i32(wsel)), dx.data_ptr(),
+            N * H * W * Cin, _ptr(_i32(nvalid)), G, N, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, _stream())
+    if _call("dba_conv2_dgrad", *args) == NOT_HANDLED:
+        _call("dba_conv_dgrad", *args)
     return dx if out_dtype in (None, _BF16) else dx.to(out_dtype)
 
 

@@ -50,6 +50,10 @@ CONV_CASES = [
     (2, 6, 12, 12, 20, 50, 5, 1, 0),     # MnistNet conv2
     (3, 7, 1, 1, 800, 500, 1, 1, 0),     # fc1 as 1x1
     (3, 7, 1, 1, 256, 10, 1, 1, 0),      # CIFAR linear
+    (2, 5, 8, 8, 128, 128, 3, 1, 1),     # layer3 (halo kernel, 2 images per block)
+    (2, 4, 16, 16, 64, 64, 3, 1, 1),     # layer2 (halo kernel)
+    (3, 4, 32, 32, 32, 32, 1, 1, 0),     # 1x1 stride 1 (halo kernel)
+    (2, 3, 4, 4, 256, 256, 3, 1, 1),     # layer4 (halo does not fit LDS -> gen-2 GEMM)
 ]
 
 
