@@ -2,8 +2,8 @@
 // eval-mode BN fold into the preceding conv.
 //
 //   stats   : per-(group, channel) sum / sum-of-squares over the group's VALID rows
-//             (fp32 per-thread partials, fp64 cross-block atomics — no cancellation issue
-//             at CIFAR/Tiny row counts);
+//             (fp32 per-block partials, no atomics and no pre-zeroed buffers; the finalize
+//             pass sums them in fp64);
 //   finalize: mean, 1/std, running-stat update (unbiased var, momentum) in place in the
 //             flat replica state;
 //   apply   : y -> (y-mean)*invstd*gamma + beta (+residual) (ReLU), padded rows zeroed;
@@ -16,24 +16,29 @@ namespace {
 
 constexpr int kRowsPerBlock = 512;
 
-// sums[g][0][c] += sum x ; sums[g][1][c] += sum x^2   (STATS)
-// sums[g][0][c] += sum d ; sums[g][1][c] += sum d*xhat (BWD)
+// Per-block partial sums (no atomics, no pre-zeroing): part[g][blk][0][c] = sum x (STATS)
+// or sum d (BWD); part[g][blk][1][c] = sum x^2 or sum d*xhat.  Blocks past the valid rows
+// write zeros so the finalize pass can sum every slot unconditionally.
 template <bool BWD>
 __global__ __launch_bounds__(256) void bn_reduce_kernel(const uint16_t* __restrict__ y, const uint16_t* __restrict__ dout,
                                                         const uint16_t* __restrict__ out, const float* __restrict__ mean,
                                                         const float* __restrict__ invstd, int relu,
                                                         const int* __restrict__ nvalid, int N, int HW, int C,
-                                                        double* __restrict__ sums) {
+                                                        float* __restrict__ part) {
   __shared__ float red[2][256][8];
   const int g = blockIdx.y;
   const int R = N * HW;
   const int Rv = valid_rows(nvalid, g, N) * HW;
   const int r0 = blockIdx.x * kRowsPerBlock;
-  if (r0 >= Rv) return;
+  const int tid = threadIdx.x;
+  float* pg = part + ((long long)g * gridDim.x + blockIdx.x) * 2 * C;
+  if (r0 >= Rv) {
+    for (int c = tid; c < 2 * C; c += 256) pg[c] = 0.f;
+    return;
+  }
   const int r1 = min(Rv, r0 + kRowsPerBlock);
   const int tpr = C / 8;                 // threads per row
   const int rpp = 256 / tpr;             // rows per pass
-  const int tid = threadIdx.x;
   const int cg = tid % tpr, rr = tid / tpr;
   float s0[8], s1[8], mu[8], is[8];
 #pragma unroll
@@ -43,27 +48,25 @@ __global__ __launch_bounds__(256) void bn_reduce_kernel(const uint16_t* __restri
     for (int e = 0; e < 8; ++e) { mu[e] = mean[g * C + cg * 8 + e]; is[e] = invstd[g * C + cg * 8 + e]; }
   }
   const long long gbase = (long long)g * R * C;
-  if (rr < rpp) {
-    for (int r = r0 + rr; r < r1; r += rpp) {
-      const long long o = gbase + (long long)r * C + cg * 8;
-      const uint4 yv = *(const uint4*)(y + o);
-      const uint16_t* yp = (const uint16_t*)&yv;
-      if (!BWD) {
+  for (int r = r0 + rr; r < r1; r += rpp) {
+    const long long o = gbase + (long long)r * C + cg * 8;
+    const uint4 yv = *(const uint4*)(y + o);
+    const uint16_t* yp = (const uint16_t*)&yv;
+    if (!BWD) {
 #pragma unroll
-        for (int e = 0; e < 8; ++e) { const float v = bf2f(yp[e]); s0[e] += v; s1[e] += v * v; }
-      } else {
-        const uint4 dv = *(const uint4*)(dout + o);
-        const uint16_t* dp = (const uint16_t*)&dv;
-        uint4 ov = make_uint4(0, 0, 0, 0);
-        if (relu) ov = *(const uint4*)(out + o);
-        const uint16_t* op = (const uint16_t*)&ov;
+      for (int e = 0; e < 8; ++e) { const float v = bf2f(yp[e]); s0[e] += v; s1[e] += v * v; }
+    } else {
+      const uint4 dv = *(const uint4*)(dout + o);
+      const uint16_t* dp = (const uint16_t*)&dv;
+      uint4 ov = make_uint4(0, 0, 0, 0);
+      if (relu) ov = *(const uint4*)(out + o);
+      const uint16_t* op = (const uint16_t*)&ov;
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          float d = bf2f(dp[e]);
-          if (relu && !(bf2f(op[e]) > 0.f)) d = 0.f;
-          const float xh = (bf2f(yp[e]) - mu[e]) * is[e];
-          s0[e] += d; s1[e] += d * xh;
-        }
+      for (int e = 0; e < 8; ++e) {
+        float d = bf2f(dp[e]);
+        if (relu && !(bf2f(op[e]) > 0.f)) d = 0.f;
+        const float xh = (bf2f(yp[e]) - mu[e]) * is[e];
+        s0[e] += d; s1[e] += d * xh;
       }
     }
   }
@@ -77,14 +80,14 @@ __global__ __launch_bounds__(256) void bn_reduce_kernel(const uint16_t* __restri
     }
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      atomicAdd(&sums[((long long)g * 2 + 0) * C + tid * 8 + e], (double)s0[e]);
-      atomicAdd(&sums[((long long)g * 2 + 1) * C + tid * 8 + e], (double)s1[e]);
+      pg[tid * 8 + e] = s0[e];
+      pg[C + tid * 8 + e] = s1[e];
     }
   }
 }
 
-__global__ void bn_finalize_kernel(const double* __restrict__ sums, const int* __restrict__ nvalid, int N, int HW,
-                                   int C, float* __restrict__ rm, float* __restrict__ rv, long long s_gstride,
+__global__ void bn_finalize_kernel(const float* __restrict__ part, int nblk, const int* __restrict__ nvalid, int N,
+                                   int HW, int C, float* __restrict__ rm, float* __restrict__ rv, long long s_gstride,
                                    float momentum, float eps, float* __restrict__ mean, float* __restrict__ invstd,
                                    int G) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -92,8 +95,11 @@ __global__ void bn_finalize_kernel(const double* __restrict__ sums, const int* _
   const int g = i / C, c = i % C;
   const double n = (double)valid_rows(nvalid, g, N) * HW;
   if (n <= 0) { mean[i] = 0.f; invstd[i] = 0.f; return; }
-  const double m = sums[((long long)g * 2) * C + c] / n;
-  double var = sums[((long long)g * 2 + 1) * C + c] / n - m * m;
+  double s0 = 0, s1 = 0;
+  const float* pg = part + (long long)g * nblk * 2 * C;
+  for (int b = 0; b < nblk; ++b) { s0 += pg[b * 2 * C + c]; s1 += pg[b * 2 * C + C + c]; }
+  const double m = s0 / n;
+  double var = s1 / n - m * m;
   var = var > 0 ? var : 0;
   mean[i] = (float)m;
   invstd[i] = (float)(1.0 / sqrt(var + (double)eps));
@@ -110,16 +116,16 @@ __global__ void bn_apply_kernel(const uint16_t* __restrict__ y, const float* __r
                                 int relu, uint16_t* __restrict__ out, const int* __restrict__ nvalid, int G, int N,
                                 int HW, int C) {
   const int c8 = C / 8;
-  const long long per = (long long)N * HW * c8;
-  const long long total = per * G;
-  for (long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x; t < total; t += (long long)gridDim.x * blockDim.x) {
-    const int g = (int)(t / per);
-    const long long rem = t - g * per;
-    const long long row = rem / c8;
-    const int c0 = (int)(rem - row * c8) * 8;
-    const long long o = t * 8;
+  const int per = N * HW * c8;                 // < 2^31 for every model / batch size used
+  const int total = per * G;
+  for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x) {
+    const int g = t / per;
+    const int rem = t - g * per;
+    const int row = rem / c8;
+    const int c0 = (rem - row * c8) * 8;
+    const long long o = (long long)t * 8;
     uint4 res8 = make_uint4(0, 0, 0, 0);
-    if (row >= (long long)valid_rows(nvalid, g, N) * HW) {
+    if (row >= valid_rows(nvalid, g, N) * HW) {
       *(uint4*)(out + o) = res8;
       continue;
     }
@@ -145,18 +151,18 @@ __global__ void bn_apply_kernel(const uint16_t* __restrict__ y, const float* __r
 __global__ void bn_bwd_apply_kernel(const uint16_t* __restrict__ dout, const uint16_t* __restrict__ out,
                                     const uint16_t* __restrict__ y, const float* __restrict__ mean,
                                     const float* __restrict__ invstd, const float* __restrict__ gamma,
-                                    long long p_gstride, const double* __restrict__ sums, int relu,
+                                    long long p_gstride, const float* __restrict__ sums, int relu,
                                     uint16_t* __restrict__ dy, uint16_t* __restrict__ dres,
                                     const int* __restrict__ nvalid, int G, int N, int HW, int C) {
   const int c8 = C / 8;
-  const long long per = (long long)N * HW * c8;
-  const long long total = per * G;
-  for (long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x; t < total; t += (long long)gridDim.x * blockDim.x) {
-    const int g = (int)(t / per);
-    const long long rem = t - g * per;
-    const long long row = rem / c8;
-    const int c0 = (int)(rem - row * c8) * 8;
-    const long long o = t * 8;
+  const int per = N * HW * c8;                 // < 2^31 for every model / batch size used
+  const int total = per * G;
+  for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x) {
+    const int g = t / per;
+    const int rem = t - g * per;
+    const int row = rem / c8;
+    const int c0 = (rem - row * c8) * 8;
+    const long long o = (long long)t * 8;
     const int nv = valid_rows(nvalid, g, N) * HW;
     uint4 z = make_uint4(0, 0, 0, 0);
     if (row >= nv) {
@@ -182,8 +188,8 @@ __global__ void bn_bwd_apply_kernel(const uint16_t* __restrict__ dout, const uin
       if (relu && !(bf2f(op[e]) > 0.f)) d = 0.f;
       const float is = invstd[g * C + c];
       const float xh = (bf2f(yp[e]) - mean[g * C + c]) * is;
-      const float sd = (float)sums[((long long)g * 2) * C + c];
-      const float sdx = (float)sums[((long long)g * 2 + 1) * C + c];
+      const float sd = sums[((long long)g * 2) * C + c];
+      const float sdx = sums[((long long)g * 2 + 1) * C + c];
       const float v = gamma[(long long)g * p_gstride + c] * is / n * (n * d - sd - xh * sdx);
       p1[e] = f2bf(v);
       p2[e] = f2bf(d);
@@ -193,13 +199,20 @@ __global__ void bn_bwd_apply_kernel(const uint16_t* __restrict__ dout, const uin
   }
 }
 
-__global__ void bn_param_grad_kernel(const double* __restrict__ sums, float* __restrict__ dgamma,
-                                     float* __restrict__ dbeta, long long g_gstride, int G, int C) {
+// sums the backward partials into sums[g][2][C] and accumulates dgamma / dbeta
+__global__ void bn_bwd_finalize_kernel(const float* __restrict__ part, int nblk, float* __restrict__ sums,
+                                       float* __restrict__ dgamma, float* __restrict__ dbeta, long long g_gstride,
+                                       int G, int C) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= G * C) return;
   const int g = i / C, c = i % C;
-  dbeta[(long long)g * g_gstride + c] += (float)sums[((long long)g * 2) * C + c];
-  dgamma[(long long)g * g_gstride + c] += (float)sums[((long long)g * 2 + 1) * C + c];
+  double s0 = 0, s1 = 0;
+  const float* pg = part + (long long)g * nblk * 2 * C;
+  for (int b = 0; b < nblk; ++b) { s0 += pg[b * 2 * C + c]; s1 += pg[b * 2 * C + C + c]; }
+  sums[((long long)g * 2) * C + c] = (float)s0;
+  sums[((long long)g * 2 + 1) * C + c] = (float)s1;
+  dbeta[(long long)g * g_gstride + c] += (float)s0;
+  dgamma[(long long)g * g_gstride + c] += (float)s1;
 }
 
 // eval fold: wf[s][co][k] = w[s][co][k] * s_c ; bf[s][co] = (b0 - rm) * s_c + beta
@@ -229,18 +242,18 @@ int egrid(long long n) { return (int)std::max(1LL, std::min(16384LL, (n + 255) /
 
 }  // namespace
 
-DBA_EXPORT int dba_bn_stats(const void* y, const int* nvalid, int G, int N, int HW, int C, double* sums, void* stream) {
-  dim3 grid(ceil_div((long long)N * HW, kRowsPerBlock), G);
-  hipLaunchKernelGGL(bn_reduce_kernel<false>, grid, dim3(256), 0, (hipStream_t)stream, (const uint16_t*)y, nullptr,
-                     nullptr, nullptr, nullptr, 0, nvalid, N, HW, C, sums);
-  DBA_LAUNCH_CHECK();
-}
+DBA_EXPORT int dba_bn_partial_blocks(int N, int HW) { return ceil_div((long long)N * HW, kRowsPerBlock); }
 
-DBA_EXPORT int dba_bn_finalize(const double* sums, const int* nvalid, int G, int N, int HW, int C, float* rm, float* rv,
-                               long long s_gstride, float momentum, float eps, float* mean, float* invstd,
-                               void* stream) {
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3(ceil_div(G * C, 256)), dim3(256), 0, (hipStream_t)stream, sums, nvalid,
-                     N, HW, C, rm, rv, s_gstride, momentum, eps, mean, invstd, G);
+// part: [G][nblk][2][C] fp32 workspace (no initialisation needed)
+DBA_EXPORT int dba_bn_stats(const void* y, const int* nvalid, int G, int N, int HW, int C, float* part, float* rm,
+                            float* rv, long long s_gstride, float momentum, float eps, float* mean, float* invstd,
+                            void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  const int nblk = ceil_div((long long)N * HW, kRowsPerBlock);
+  hipLaunchKernelGGL(bn_reduce_kernel<false>, dim3(nblk, G), dim3(256), 0, st, (const uint16_t*)y, nullptr, nullptr,
+                     nullptr, nullptr, 0, nvalid, N, HW, C, part);
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3(ceil_div(G * C, 256)), dim3(256), 0, st, part, nblk, nvalid, N, HW, C,
+                     rm, rv, s_gstride, momentum, eps, mean, invstd, G);
   DBA_LAUNCH_CHECK();
 }
 
@@ -253,16 +266,18 @@ DBA_EXPORT int dba_bn_apply(const void* y, const float* mean, const float* invst
   DBA_LAUNCH_CHECK();
 }
 
+// part: [G][nblk][2][C] workspace followed by sums [G][2][C] (fp32, no initialisation needed)
 DBA_EXPORT int dba_bn_bwd(const void* dout, const void* out, const void* y, const float* mean, const float* invstd,
                           const float* gamma, long long p_gstride, int relu, float* dgamma, float* dbeta,
-                          long long g_gstride, void* dy, void* dres, double* sums, const int* nvalid, int G, int N,
+                          long long g_gstride, void* dy, void* dres, float* part, const int* nvalid, int G, int N,
                           int HW, int C, void* stream) {
   hipStream_t st = (hipStream_t)stream;
-  dim3 grid(ceil_div((long long)N * HW, kRowsPerBlock), G);
-  hipLaunchKernelGGL(bn_reduce_kernel<true>, grid, dim3(256), 0, st, (const uint16_t*)y, (const uint16_t*)dout,
-                     (const uint16_t*)out, mean, invstd, relu, nvalid, N, HW, C, sums);
-  hipLaunchKernelGGL(bn_param_grad_kernel, dim3(ceil_div(G * C, 256)), dim3(256), 0, st, sums, dgamma, dbeta,
-                     g_gstride, G, C);
+  const int nblk = ceil_div((long long)N * HW, kRowsPerBlock);
+  float* sums = part + (long long)G * nblk * 2 * C;
+  hipLaunchKernelGGL(bn_reduce_kernel<true>, dim3(nblk, G), dim3(256), 0, st, (const uint16_t*)y,
+                     (const uint16_t*)dout, (const uint16_t*)out, mean, invstd, relu, nvalid, N, HW, C, part);
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(ceil_div(G * C, 256)), dim3(256), 0, st, part, nblk, sums, dgamma,
+                     dbeta, g_gstride, G, C);
   const long long n = (long long)G * N * HW * C / 8;
   hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(egrid(n)), dim3(256), 0, st, (const uint16_t*)dout,
                      (const uint16_t*)out, (const uint16_t*)y, mean, invstd, gamma, p_gstride, sums, relu,

@@ -327,20 +327,21 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgradArgs a) {
 }
 
 // dW^T for the data gradient: [slots][Co][T][Ci] -> [slots][Ci][T][Co]; with `flip` the taps
-// are also reversed (t -> T-1-t), turning a stride-1 dgrad into a forward conv (halo kernel)
+// are also reversed (t -> T-1-t), turning a stride-1 dgrad into a forward conv (halo kernel).
+// One block row per slot, 32-bit indexing; output-ordered (coalesced writes).
 __global__ void transpose_w_kernel(const uint16_t* __restrict__ w, long long w_sstride, uint16_t* __restrict__ wt,
-                                   int slots, int Co, int T, int Ci, int flip) {
-  const long long per = (long long)Co * T * Ci;
-  const long long total = per * slots;
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
-    const int s = (int)(i / per);
-    long long r = i - s * per;
-    const int co = (int)(r % Co); r /= Co;
-    const int t = (int)(r % T);
-    const int ci = (int)(r / T);
-    // i indexes the OUTPUT [s][ci][t][co] (co fastest) -> coalesced writes
+                                   int Co, int T, int Ci, int flip) {
+  const int s = blockIdx.y;
+  const int per = Co * T * Ci;
+  const uint16_t* ws = w + (long long)s * w_sstride;
+  uint16_t* wo = wt + (long long)s * per;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < per; i += gridDim.x * blockDim.x) {
+    const int co = i % Co;
+    const int r = i / Co;
+    const int t = r % T;
+    const int ci = r / T;
     const int ts = flip ? T - 1 - t : t;
-    wt[i] = w[(long long)s * w_sstride + ((long long)co * T + ts) * Ci + ci];
+    wo[i] = ws[(co * T + ts) * Ci + ci];
   }
 }
 
@@ -426,10 +427,10 @@ DBA_EXPORT int dba_conv_wgrad(const void* dy, long long dy_gstride, const void* 
 
 DBA_EXPORT int dba_transpose_w(const void* w, long long w_sstride, void* wt, int slots, int Co, int T, int Ci,
                                int flip, void* stream) {
-  const long long total = (long long)slots * Co * T * Ci;
-  const int blocks = (int)std::min(4096LL, (total + 255) / 256);
-  hipLaunchKernelGGL(transpose_w_kernel, dim3(std::max(1, blocks)), dim3(256), 0, (hipStream_t)stream,
-                     (const uint16_t*)w, w_sstride, (uint16_t*)wt, slots, Co, T, Ci, flip);
+  const int per = Co * T * Ci;
+  const int bx = std::max(1, std::min(256, (per + 255) / 256));
+  hipLaunchKernelGGL(transpose_w_kernel, dim3(bx, slots), dim3(256), 0, (hipStream_t)stream, (const uint16_t*)w,
+                     w_sstride, (uint16_t*)wt, Co, T, Ci, flip);
   DBA_LAUNCH_CHECK();
 }
 

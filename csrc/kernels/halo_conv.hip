@@ -46,6 +46,10 @@ __global__ __launch_bounds__(256) void halo_conv_kernel(HaloArgs a) {
   const uint16_t* __restrict__ Wp = a.w + (long long)slot * a.w_sstride;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int s0 = tm * a.NI;                   // first segment of this block
+  const int K = a.KH * a.KH * a.C;
+  const int KP = K + 8;                       // padded B row (distinct bank slots per lane)
+  const int halo_elems = a.NI * (a.SR + a.KH - 1) * (a.W + a.KH - 1) * (a.C + 8);
+  uint16_t* Bs = smem + ((halo_elems + 7) & ~7);
 
   // ---- stage input rows + halo of all NI segments (16-byte chunks, zero outside image)
   {
@@ -68,6 +72,16 @@ __global__ __launch_bounds__(256) void halo_conv_kernel(HaloArgs a) {
       *(uint4*)&smem[((seg * HR + hr) * HW2 + hc) * PS + c8 * 8] = v;
     }
   }
+  // ---- stage this block's weight panel [BN][K] once (shared by the 4 waves)
+  {
+    const int k8n = K / 8;
+    for (int e = tid; e < BN * k8n; e += 256) {
+      const int r = e / k8n, k8 = e - r * k8n;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (n0 + r < a.Cout) v = *(const uint4*)(Wp + (long long)(n0 + r) * K + k8 * 8);
+      *(uint4*)&Bs[r * KP + k8 * 8] = v;
+    }
+  }
   // per-lane A-fragment base (pixel of each 32-row MFMA tile)
   int abase[MI];
 #pragma unroll
@@ -80,18 +94,11 @@ __global__ __launch_bounds__(256) void halo_conv_kernel(HaloArgs a) {
   }
   __syncthreads();
 
-  const int K = a.KH * KW * a.C;
   const int steps = K / 16;
   const int cpt = a.C / 16;                   // 16-channel chunks per tap
-  // B fragment pointers: column n0 + j*32 + (lane&31), k offset 8*(lane>>5)
-  const uint16_t* bptr[NJ];
-  bool bok[NJ];
+  int bbase[NJ];
 #pragma unroll
-  for (int j = 0; j < NJ; ++j) {
-    const int n = n0 + j * 32 + (lane & 31);
-    bok[j] = n < a.Cout;
-    bptr[j] = Wp + (long long)(bok[j] ? n : 0) * K + (lane >> 5) * 8;
-  }
+  for (int j = 0; j < NJ; ++j) bbase[j] = (j * 32 + (lane & 31)) * KP + (lane >> 5) * 8;
   f32x16_t acc[MI][NJ];
 #pragma unroll
   for (int i = 0; i < MI; ++i)
@@ -100,27 +107,20 @@ __global__ __launch_bounds__(256) void halo_conv_kernel(HaloArgs a) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  bf16x8_t bcur[NJ], bnxt[NJ];
-  const bf16x8_t zero8 = {};
-#pragma unroll
-  for (int j = 0; j < NJ; ++j) bcur[j] = bok[j] ? *(const bf16x8_t*)(bptr[j]) : zero8;
   int tap = 0, cc = 0;
   for (int s = 0; s < steps; ++s) {
-    if (s + 1 < steps) {
-#pragma unroll
-      for (int j = 0; j < NJ; ++j) bnxt[j] = bok[j] ? *(const bf16x8_t*)(bptr[j] + (s + 1) * 16) : zero8;
-    }
     const int kh = tap / KW, kw = tap - kh * KW;
     const int aoff = (kh * HW2 + kw) * PS + cc * 16;
+    bf16x8_t bfr[NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) bfr[j] = *(const bf16x8_t*)&Bs[bbase[j] + s * 16];
 #pragma unroll
     for (int i = 0; i < MI; ++i) {
       const bf16x8_t av = *(const bf16x8_t*)&smem[abase[i] + aoff];
 #pragma unroll
       for (int j = 0; j < NJ; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bcur[j], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bfr[j], acc[i][j], 0, 0, 0);
     }
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) bcur[j] = bnxt[j];
     if (++cc == cpt) { cc = 0; ++tap; }
   }
 
@@ -213,19 +213,21 @@ DBA_EXPORT int dba_halo_conv(const void* x, long long x_gstride, const void* w, 
                              long long out_gstride, int out_f32, const int* nvalid, int G, int N, int H, int W, int C,
                              int Cout, int KH, int pad, int relu, void* stream) {
   if (C % 16 != 0 || (KH != 1 && KH != 3) || pad != (KH - 1) / 2) return -100;
-  // one MFMA row group per wave by default; 2 when the output is narrow (more MFMA per B fragment)
-  const int MI = (Cout <= 32) ? 2 : 1;
+  // Halo tiling pays where activations dominate the operand traffic: narrow outputs
+  // (ResNet stage 1).  Wide layers are weight-dominated and go to the gen-2 GEMM.
+  if (Cout > 32) return -100;
+  const int MI = 2;
   const int BM = 4 * MI * 32;
   if (BM % W != 0) return -100;
   int SR = std::min(H, BM / W);
   if (H % SR != 0 || BM % (SR * W) != 0) return -100;
   const int NI = BM / (SR * W);
-  const size_t lds = (size_t)NI * (SR + KH - 1) * (W + KH - 1) * (C + 8) * 2;
-  if (lds > 150 * 1024) return -100;
+  const size_t halo = ((size_t)NI * (SR + KH - 1) * (W + KH - 1) * (C + 8) + 7) / 8 * 8;
+  const size_t lds = (halo + 32 * ((size_t)KH * KH * C + 8)) * 2;
+  if (lds > 96 * 1024) return -100;
   HaloArgs a{(const uint16_t*)x, x_gstride, (const uint16_t*)w, w_sstride, wsel, bias, b_sstride,
              (const uint16_t*)res, out, out_gstride, nvalid, N, H, W, C, Cout, KH, pad, relu, SR, NI, 1};
   hipStream_t st = (hipStream_t)stream;
-  if (MI == 2) return out_f32 ? launch_halo<2, 1, float>(a, G, lds, st) : launch_halo<2, 1, uint16_t>(a, G, lds, st);
-  if (Cout <= 64) return out_f32 ? launch_halo<1, 2, float>(a, G, lds, st) : launch_halo<1, 2, uint16_t>(a, G, lds, st);
-  return out_f32 ? launch_halo<1, 4, float>(a, G, lds, st) : launch_halo<1, 4, uint16_t>(a, G, lds, st);
+  (void)MI;
+  return out_f32 ? launch_halo<2, 1, float>(a, G, lds, st) : launch_halo<2, 1, uint16_t>(a, G, lds, st);
 }

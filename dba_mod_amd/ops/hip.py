@@ -39,8 +39,8 @@ _SIGS = {
     "dba_transpose_w": [_P, _LL, _P, _I, _I, _I, _I, _I, _P],
     "dba_halo_conv": [_P, _LL, _P, _LL, _P, _P, _LL, _P, _P, _LL, _I, _P] + [_I] * 9 + [_P],
     "dba_colsum": [_P, _LL, _I, _P, _I, _I, _I, _P, _LL, _P],
-    "dba_bn_stats": [_P, _P, _I, _I, _I, _I, _P, _P],
-    "dba_bn_finalize": [_P, _P, _I, _I, _I, _I, _P, _P, _LL, _F, _F, _P, _P, _P],
+    "dba_bn_stats": [_P, _P, _I, _I, _I, _I, _P, _P, _P, _LL, _F, _F, _P, _P, _P],
+    "dba_bn_partial_blocks": [_I, _I],
     "dba_bn_apply": [_P, _P, _P, _P, _P, _LL, _P, _I, _P, _P, _I, _I, _I, _I, _P],
     "dba_bn_bwd": [_P, _P, _P, _P, _P, _P, _LL, _I, _P, _P, _LL, _P, _P, _P, _P, _I, _I, _I, _I, _P],
     "dba_bn_fold": [_P, _LL, _P, _P, _P, _P, _P, _LL, _F, _P, _P, _I, _I, _I, _P],
@@ -229,12 +229,12 @@ def bn_train(y, gamma, beta, rmean, rvar, nvalid, momentum, eps, relu, residual)
     G, N, H, W, C = y.shape
     assert C % 8 == 0
     ps = _same_stride(gamma, beta, rmean, rvar)
-    sums = torch.zeros(G, 2, C, dtype=torch.float64, device=y.device)
+    nblk = _L.dba_bn_partial_blocks(N, H * W)
+    part = torch.empty(G * nblk * 2 * C, dtype=torch.float32, device=y.device)
     mean = torch.empty(G, C, dtype=torch.float32, device=y.device)
     invstd = torch.empty(G, C, dtype=torch.float32, device=y.device)
     nv = _ptr(_i32(nvalid))
-    _call("dba_bn_stats", y.data_ptr(), nv, G, N, H * W, C, sums.data_ptr(), _stream())
-    _call("dba_bn_finalize", sums.data_ptr(), nv, G, N, H * W, C, rmean.data_ptr(), rvar.data_ptr(), ps,
+    _call("dba_bn_stats", y.data_ptr(), nv, G, N, H * W, C, part.data_ptr(), rmean.data_ptr(), rvar.data_ptr(), ps,
           float(momentum), float(eps), mean.data_ptr(), invstd.data_ptr(), _stream())
     out = torch.empty_like(y)
     res = _bf16c(residual) if residual is not None else None
@@ -248,12 +248,13 @@ def bn_train_bwd(dout, y, out, mean, invstd, gamma, nvalid, relu, dgamma, dbeta,
     G, N, H, W, C = y.shape
     ps = _same_stride(gamma)
     gs = _same_stride(dgamma, dbeta)
-    sums = torch.zeros(G, 2, C, dtype=torch.float64, device=y.device)
+    nblk = _L.dba_bn_partial_blocks(N, H * W)
+    part = torch.empty(G * (nblk + 1) * 2 * C, dtype=torch.float32, device=y.device)
     dy = torch.empty_like(y)
     dres = torch.empty_like(y) if want_dres else None
     _call("dba_bn_bwd", dout.data_ptr(), out.data_ptr(), y.data_ptr(), mean.data_ptr(), invstd.data_ptr(),
           gamma.data_ptr(), ps, int(relu), dgamma.data_ptr(), dbeta.data_ptr(), gs, dy.data_ptr(), _ptr(dres),
-          sums.data_ptr(), _ptr(_i32(nvalid)), G, N, H * W, C, _stream())
+          part.data_ptr(), _ptr(_i32(nvalid)), G, N, H * W, C, _stream())
     return (dy, dres) if want_dres else dy
 
 
