@@ -66,9 +66,8 @@ def main() -> int:
     logging.getLogger("logger").setLevel(logging.WARNING)
 
     epoch = server.start_epoch
-    for _ in range(args.warmup):
-        server.run_round(epoch)
-        epoch += 1
+    server.run_rounds(range(epoch, epoch + args.warmup))      # pipelined, flushed at the end
+    epoch += args.warmup
 
     def sync():
         if dctx.device.type == "cuda":
@@ -77,10 +76,11 @@ def main() -> int:
 
     sync()
     t0 = time.perf_counter()
-    last = {}
-    for _ in range(args.steps):
-        last = server.run_round(epoch)
-        epoch += 1
+    # round r's evaluation overlaps round r+1's training; the last round is fully evaluated
+    # (flushed) inside the timed region, so exactly K complete rounds are timed
+    done = server.run_rounds(range(epoch, epoch + args.steps))
+    epoch += args.steps
+    last = done[-1] if done else {}
     sync()
     elapsed = dctx.all_reduce_max(time.perf_counter() - t0)
     rps = args.steps / elapsed if elapsed > 0 else 0.0

@@ -86,18 +86,35 @@ __global__ __launch_bounds__(256) void bn_reduce_kernel(const uint16_t* __restri
   }
 }
 
+// sums the nblk partials of (g, c) with 4 threads per channel; block = (g, 64 channels)
+__device__ __forceinline__ void sum_partials(const float* __restrict__ part, int nblk, int C, int g, int c, bool cok,
+                                             double& s0, double& s1) {
+  __shared__ double red[2][4][64];
+  const int lane_c = threadIdx.x & 63, q = threadIdx.x >> 6;
+  double a0 = 0, a1 = 0;
+  if (cok) {
+    const float* pg = part + (long long)g * nblk * 2 * C;
+    for (int b = q; b < nblk; b += 4) { a0 += pg[b * 2 * C + c]; a1 += pg[b * 2 * C + C + c]; }
+  }
+  red[0][q][lane_c] = a0;
+  red[1][q][lane_c] = a1;
+  __syncthreads();
+  s0 = red[0][0][lane_c] + red[0][1][lane_c] + red[0][2][lane_c] + red[0][3][lane_c];
+  s1 = red[1][0][lane_c] + red[1][1][lane_c] + red[1][2][lane_c] + red[1][3][lane_c];
+}
+
 __global__ void bn_finalize_kernel(const float* __restrict__ part, int nblk, const int* __restrict__ nvalid, int N,
                                    int HW, int C, float* __restrict__ rm, float* __restrict__ rv, long long s_gstride,
                                    float momentum, float eps, float* __restrict__ mean, float* __restrict__ invstd,
                                    int G) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= G * C) return;
-  const int g = i / C, c = i % C;
+  const int g = blockIdx.y;
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  double s0, s1;
+  sum_partials(part, nblk, C, g, c, c < C, s0, s1);
+  if (threadIdx.x >= 64 || c >= C) return;
+  const int i = g * C + c;
   const double n = (double)valid_rows(nvalid, g, N) * HW;
   if (n <= 0) { mean[i] = 0.f; invstd[i] = 0.f; return; }
-  double s0 = 0, s1 = 0;
-  const float* pg = part + (long long)g * nblk * 2 * C;
-  for (int b = 0; b < nblk; ++b) { s0 += pg[b * 2 * C + c]; s1 += pg[b * 2 * C + C + c]; }
   const double m = s0 / n;
   double var = s1 / n - m * m;
   var = var > 0 ? var : 0;
@@ -203,12 +220,11 @@ __global__ void bn_bwd_apply_kernel(const uint16_t* __restrict__ dout, const uin
 __global__ void bn_bwd_finalize_kernel(const float* __restrict__ part, int nblk, float* __restrict__ sums,
                                        float* __restrict__ dgamma, float* __restrict__ dbeta, long long g_gstride,
                                        int G, int C) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= G * C) return;
-  const int g = i / C, c = i % C;
-  double s0 = 0, s1 = 0;
-  const float* pg = part + (long long)g * nblk * 2 * C;
-  for (int b = 0; b < nblk; ++b) { s0 += pg[b * 2 * C + c]; s1 += pg[b * 2 * C + C + c]; }
+  const int g = blockIdx.y;
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  double s0, s1;
+  sum_partials(part, nblk, C, g, c, c < C, s0, s1);
+  if (threadIdx.x >= 64 || c >= C) return;
   sums[((long long)g * 2) * C + c] = (float)s0;
   sums[((long long)g * 2 + 1) * C + c] = (float)s1;
   dbeta[(long long)g * g_gstride + c] += (float)s0;
@@ -252,7 +268,7 @@ DBA_EXPORT int dba_bn_stats(const void* y, const int* nvalid, int G, int N, int 
   const int nblk = ceil_div((long long)N * HW, kRowsPerBlock);
   hipLaunchKernelGGL(bn_reduce_kernel<false>, dim3(nblk, G), dim3(256), 0, st, (const uint16_t*)y, nullptr, nullptr,
                      nullptr, nullptr, 0, nvalid, N, HW, C, part);
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3(ceil_div(G * C, 256)), dim3(256), 0, st, part, nblk, nvalid, N, HW, C,
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3(ceil_div(C, 64), G), dim3(256), 0, st, part, nblk, nvalid, N, HW, C,
                      rm, rv, s_gstride, momentum, eps, mean, invstd, G);
   DBA_LAUNCH_CHECK();
 }
@@ -276,7 +292,7 @@ DBA_EXPORT int dba_bn_bwd(const void* dout, const void* out, const void* y, cons
   float* sums = part + (long long)G * nblk * 2 * C;
   hipLaunchKernelGGL(bn_reduce_kernel<true>, dim3(nblk, G), dim3(256), 0, st, (const uint16_t*)y,
                      (const uint16_t*)dout, (const uint16_t*)out, mean, invstd, relu, nvalid, N, HW, C, part);
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(ceil_div(G * C, 256)), dim3(256), 0, st, part, nblk, sums, dgamma,
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(ceil_div(C, 64), G), dim3(256), 0, st, part, nblk, sums, dgamma,
                      dbeta, g_gstride, G, C);
   const long long n = (long long)G * N * HW * C / 8;
   hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(egrid(n)), dim3(256), 0, st, (const uint16_t*)dout,

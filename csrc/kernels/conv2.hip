@@ -319,10 +319,7 @@ template <int MODE, typename OutT>
 int dispatch2(Igemm2Args a, int G, hipStream_t st) {
   const long long M = (long long)a.N * a.Ho * a.Wo;
   if (a.Ncol <= 32) return launch2<128, 32, 4, 1, MODE, OutT>(a, G, st);
-  if (a.Ncol <= 64) {
-    if (M * G >= 256LL * 512) return launch2<256, 64, 4, 1, MODE, OutT>(a, G, st);
-    return launch2<128, 64, 2, 2, MODE, OutT>(a, G, st);
-  }
+  if (a.Ncol <= 64) return launch2<128, 64, 2, 2, MODE, OutT>(a, G, st);
   // wide outputs: 128x128 tiles unless the launch would not fill the chip
   if (M * G / 128 * ((a.Ncol + 127) / 128) >= 512) return launch2<128, 128, 2, 2, MODE, OutT>(a, G, st);
   return launch2<64, 128, 1, 4, MODE, OutT>(a, G, st);

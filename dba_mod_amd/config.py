@@ -96,6 +96,7 @@ _DEFAULTS: Dict[str, Any] = {
     "max_rounds": None,            # stop after this many rounds (bench / smoke)
     "local_eval": True,            # per-client local tests (reference behaviour)
     "graph_capture": True,         # HIP-graph the grouped training step on GPU
+    "overlap_eval": True,          # evaluate round r on a side stream under round r+1's training
 }
 
 # keys whose value may legitimately be a python list of ints/strings

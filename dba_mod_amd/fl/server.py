@@ -85,6 +85,15 @@ class Server:
         self.plot.text(dict_html(params, self.current_time))
         self.best_loss = float("inf")
         self.timer = PhaseTimer(self.device)
+        self._pending: Optional[Dict[str, Any]] = None
+        self._eval_stream = None
+        if self.device.type == "cuda" and bool(params.get("overlap_eval", True)):
+            # training runs on a HIGH-priority stream (its kernels are small and latency-bound,
+            # they win every CU that frees up); evaluation fills the rest at default priority
+            torch.cuda.synchronize(self.device)
+            self._main_stream = torch.cuda.Stream(self.device, priority=-1)
+            torch.cuda.set_stream(self._main_stream)
+            self._eval_stream = torch.cuda.Stream(self.device, priority=0)
         if self.write:
             with open(os.path.join(self.folder, "params.yaml"), "w") as f:
                 yaml.safe_dump(params.to_plain(), f)
@@ -117,18 +126,24 @@ class Server:
             self.d.broadcast_(self.global_state, 0)
 
     # ------------------------------------------------------------------ round
-    def run_round(self, epoch: int) -> Dict[str, Any]:
+    # ------------------------------------------------------------------ round
+    # A round is split in two halves so consecutive rounds can overlap on the GPU:
+    #   _train_half(r): select -> plan -> train -> gather -> aggregate   (training stream)
+    #   _eval_half(r):  batched evaluation of round r's snapshots + the new global model,
+    #                   enqueued on a LOW-priority stream, then CSV/checkpoint once it lands.
+    # Round r+1's training needs only the aggregated weights, never round r's test results,
+    # so the eval of round r runs underneath the (latency-bound) training of round r+1.
+    def _train_half(self, epoch: int) -> Dict[str, Any]:
         p = self.params
-        t_round = time.perf_counter()
-        self.timer.reset()
+        t0 = time.perf_counter()
         with self.timer.phase("select"):
             agents, adversarial = select_clients(p, self.wl, epoch)
         log.info(f"Server Epoch:{epoch} choose agents : {agents}.")
         pre_acc = None
         if p.type == C.TYPE_LOAN and p["is_poison"] and not p["baseline"] and adversarial:
+            self.flush()
             pre_acc = self._loan_preeval()
         plan = build_round_plan(p, self.wl, epoch, agents, adversarial, pre_acc)
-
         costs = [c.cost for c in plan.clients]
         owners, _ = native.lpt_assign(costs, self.d.world)
         mine = [c for c, o in zip(plan.clients, owners) if o == self.d.rank]
@@ -139,32 +154,77 @@ class Server:
         with self.timer.phase("aggregate"):
             self._aggregate(plan, bank, fg_grads, adversarial)
             bank[0].copy_(self.global_state)
-        with self.timer.phase("eval"):
-            acc = self.evaluator.run(bank, plan.jobs, self.d.rank, self.d.world)
-            self.d.all_reduce_(acc)
-            res = acc.cpu().numpy()
-        with self.timer.phase("io"):
-            summary = self._record(plan, res, cstats)
-            val_loss = summary["val_loss"]
-            self._save_model(epoch, val_loss)
-            self.csv.save(bool(p["is_poison"]))
-        dt = time.perf_counter() - t_round
-        phases = self.timer.reset()
-        summary.update({"epoch": epoch, "round_s": dt, "phases": phases, "clients_on_rank": len(mine),
-                        "backend": ops.backend_name(self.device)})
+        return {"epoch": epoch, "plan": plan, "bank": bank, "cstats": cstats, "t0": t0,
+                "clients_on_rank": len(mine), "phases": self.timer.reset()}
+
+    def _launch_eval(self, pend: Dict[str, Any]) -> None:
+        """Enqueue the round's evaluation on the eval stream (returns immediately)."""
+        if self._eval_stream is None:
+            pend["acc"] = self.evaluator.run(pend["bank"], pend["plan"].jobs, self.d.rank, self.d.world)
+            return
+        ready = torch.cuda.Event()
+        ready.record(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(self._eval_stream):
+            self._eval_stream.wait_event(ready)
+            pend["acc"] = self.evaluator.run(pend["bank"], pend["plan"].jobs, self.d.rank, self.d.world)
+            pend["done"] = torch.cuda.Event()
+            pend["done"].record(self._eval_stream)
+
+    def _finish(self, pend: Dict[str, Any]) -> Dict[str, Any]:
+        p = self.params
+        t_wait = time.perf_counter()
+        acc = pend["acc"]
+        if "done" in pend:
+            torch.cuda.current_stream(self.device).wait_event(pend["done"])
+        self.d.all_reduce_(acc)
+        res = acc.cpu().numpy()
+        t_io = time.perf_counter()
+        summary = self._record(pend["plan"], res, pend["cstats"])
+        self._save_model(pend["epoch"], summary["val_loss"], pend["bank"][0])
+        self.csv.save(bool(p["is_poison"]))
+        now = time.perf_counter()
+        phases = dict(pend["phases"])
+        phases["eval_wait"] = t_io - t_wait
+        phases["io"] = now - t_io
+        summary.update({"epoch": pend["epoch"], "round_s": now - pend["t0"], "phases": phases,
+                        "clients_on_rank": pend["clients_on_rank"], "backend": ops.backend_name(self.device)})
         self.metrics.emit(summary)
-        log.info(f"Done in {dt} sec.")
+        log.info(f"Done in {now - pend['t0']} sec.")
         self.last_round = summary
         return summary
 
+    def run_round(self, epoch: int) -> Dict[str, Any]:
+        """One complete round, evaluated before returning (no overlap)."""
+        self.flush()
+        pend = self._train_half(epoch)
+        self._launch_eval(pend)
+        return self._finish(pend)
+
+    def run_rounds(self, epochs) -> List[Dict[str, Any]]:
+        """Pipelined rounds: round r's evaluation overlaps round r+1's training."""
+        out: List[Dict[str, Any]] = []
+        for epoch in epochs:
+            pend = self._train_half(epoch)
+            if self._pending is not None:
+                out.append(self._finish(self._pending))
+                self._pending = None
+            self._launch_eval(pend)
+            self._pending = pend
+        out.extend(self.flush())
+        return out
+
+    def flush(self) -> List[Dict[str, Any]]:
+        if self._pending is None:
+            return []
+        pend, self._pending = self._pending, None
+        return [self._finish(pend)]
+
     def run(self) -> None:
         p = self.params
-        n = 0
-        for epoch in range(self.start_epoch, int(p["epochs"]) + 1, int(p["aggr_epoch_interval"])):
-            self.run_round(epoch)
-            n += 1
-            if p["max_rounds"] is not None and n >= int(p["max_rounds"]):
-                break
+        epochs = list(range(self.start_epoch, int(p["epochs"]) + 1, int(p["aggr_epoch_interval"])))
+        if p["max_rounds"] is not None:
+            epochs = epochs[:int(p["max_rounds"])]
+        self.run_rounds(epochs)
         log.info("Saving all the graphs.")
         log.info(f"This run has a label: {p['current_time']}. Visdom environment: {p['environment_name']}")
 
@@ -354,21 +414,21 @@ class Server:
             out["val_loss"] = out.get("global_loss")
         return out
 
-    def _save_model(self, epoch: int, val_loss: Optional[float]) -> None:
+    def _save_model(self, epoch: int, val_loss: Optional[float], state: Optional[torch.Tensor] = None) -> None:
         p = self.params
         if not (self.write and p["save_model"]):
             return
+        state = self.global_state if state is None else state
         log.info("saving model")
         name = os.path.join(self.folder, "model_last.pt.tar")
-        ckpt.save_checkpoint(name, self.spec, self.global_state, epoch, float(p["lr"]), self.counter)
+        ckpt.save_checkpoint(name, self.spec, state, epoch, float(p["lr"]), self.counter)
         aux = {"rng": ckpt.rng_state(self.wl.py_rng, self.wl.np_rng), "foolsgold": self.fg.state(),
                "epoch": int(epoch)}
         ckpt.save_aux(name + ".aux", aux)
         if epoch in list(p["save_on_epochs"] or []):
             log.info(f"Saving model on epoch {epoch}")
-            ckpt.save_checkpoint(f"{name}.epoch_{epoch}", self.spec, self.global_state, epoch, float(p["lr"]),
-                                 self.counter)
+            ckpt.save_checkpoint(f"{name}.epoch_{epoch}", self.spec, state, epoch, float(p["lr"]), self.counter)
             ckpt.save_aux(f"{name}.epoch_{epoch}.aux", aux)
         if val_loss is not None and val_loss < self.best_loss:
-            ckpt.save_checkpoint(f"{name}.best", self.spec, self.global_state, epoch, float(p["lr"]), self.counter)
+            ckpt.save_checkpoint(f"{name}.best", self.spec, state, epoch, float(p["lr"]), self.counter)
             self.best_loss = val_loss

@@ -83,8 +83,9 @@ class PhaseTimer:
         self.t: Dict[str, float] = {}
 
     def _sync(self) -> None:
+        # only the CURRENT stream: a device-wide sync would serialise the overlapped eval stream
         if self.sync and self.device.type == "cuda":
-            torch.cuda.synchronize(self.device)
+            torch.cuda.current_stream(self.device).synchronize()
 
     @contextmanager
     def phase(self, name: str) -> Iterator[None]:
