@@ -4,6 +4,8 @@
 //   * batched squared distances   ||p_i - m||^2 for ALL clients in one pass (RFA, helper.py:376-381)
 //   * weighted sum                sum_i w_i p_i                            (Weiszfeld / FoolsGold)
 //   * Gram matrix F F^T on the f32-input MFMA (v_mfma_f32_16x16x4_f32)     (FoolsGold cosine)
+//   * anomaly-evasion distance loss  a*CE + (1-a)*||w - w_g||  on the grouped replicas
+//     (helper.py:111-123, image_train.py:87-90, loan_train.py:114-117)
 #include "common.hpp"
 #include <algorithm>
 
@@ -81,7 +83,54 @@ __global__ __launch_bounds__(64) void gram_kernel(const float* __restrict__ F, l
   }
 }
 
+// nrm2[g] += ||w_g - base_g||^2 over the parameter region (replicas in their poison phase only)
+__global__ __launch_bounds__(256) void distnorm_kernel(const float* __restrict__ w, long long ws,
+                                                       const float* __restrict__ base, long long bs,
+                                                       const int* __restrict__ trig, const int* __restrict__ active,
+                                                       long long n, float* __restrict__ nrm2) {
+  __shared__ float red[4];
+  const int g = blockIdx.y;
+  if (trig[g] < 0 || active[g] == 0) return;
+  const float* wg = w + (long long)g * ws;
+  const float* bg = base + (long long)g * bs;
+  float s = 0.f;
+  for (long long k = blockIdx.x * (long long)blockDim.x + threadIdx.x; k < n; k += (long long)gridDim.x * blockDim.x) {
+    const float d = wg[k] - bg[k];
+    s = fmaf(d, d, s);
+  }
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) atomicAdd(nrm2 + g, red[0] + red[1] + red[2] + red[3]);
+}
+
+// d/dw [a*CE + (1-a)*||w-b||] = a*g + (1-a)(w-b)/||w-b||  (0 at w == b, torch's norm subgradient)
+__global__ void distgrad_kernel(const float* __restrict__ w, long long ws, const float* __restrict__ base,
+                                long long bs, float* __restrict__ grads, long long n, const int* __restrict__ trig,
+                                const int* __restrict__ active, float alpha, const float* __restrict__ nrm2) {
+  const int g = blockIdx.y;
+  if (trig[g] < 0 || active[g] == 0) return;
+  const float nr = sqrtf(nrm2[g]);
+  const float c = nr > 0.f ? (1.f - alpha) / nr : 0.f;
+  const float* wg = w + (long long)g * ws;
+  const float* bg = base + (long long)g * bs;
+  float* gg = grads + (long long)g * n;
+  for (long long k = blockIdx.x * (long long)blockDim.x + threadIdx.x; k < n; k += (long long)gridDim.x * blockDim.x)
+    gg[k] = fmaf(alpha, gg[k], c * (wg[k] - bg[k]));
+}
+
 }  // namespace
+
+DBA_EXPORT int dba_dist_loss_grad(const float* w, long long ws, const float* base, long long bs, float* grads,
+                                  long long n, int G, const int* trig, const int* active, float alpha, float* nrm2,
+                                  void* stream) {
+  const int bx = (int)std::max(1LL, std::min(256LL, (n + 2047) / 2048));
+  hipLaunchKernelGGL(distnorm_kernel, dim3(bx, G), dim3(256), 0, (hipStream_t)stream, w, ws, base, bs, trig, active,
+                     n, nrm2);
+  hipLaunchKernelGGL(distgrad_kernel, dim3(bx, G), dim3(256), 0, (hipStream_t)stream, w, ws, base, bs, grads, n, trig,
+                     active, alpha, nrm2);
+  DBA_LAUNCH_CHECK();
+}
 
 DBA_EXPORT int dba_scale_from_base(const float* w, const float* base, float gamma, float* out, long long n,
                                    void* stream) {

@@ -86,6 +86,8 @@ class GroupTrainer:
         self.wd = float(params["decay"])
         self.B = int(params["batch_size"])
         self.target = int(params["poison_label_swap"])
+        # anomaly-evasion distance term; every shipped config has alpha_loss = 1 (term off)
+        self.alpha = float(params["alpha_loss"])
 
     # ------------------------------------------------------------------ step
     def _step(self, b: _GroupBuffers) -> None:
@@ -105,6 +107,11 @@ class GroupTrainer:
             b.nan_flag += torch.isnan(loss).any().float()
         b.grads.zero_()
         ctx.tape.backward(logits, dl)
+        if self.alpha != 1.0:
+            # poison phases train on a*CE + (1-a)*||w - w_g|| with w_g the interval-start
+            # model (image_train.py:52-54,87-90; loan_train.py:61-63,114-117)
+            dist = ops.dist_loss_grad(b.state, b.base, b.grads, b.trig, b.active, self.alpha)
+            loss = torch.where(b.trig >= 0, self.alpha * loss + (1.0 - self.alpha) * dist, loss)
         ops.sgd_step(b.state[:, :self.spec.P], b.grads, b.mom, b.lr, b.first, b.active, self.momentum,
                      self.wd, shadow=(b.wcomp if b.wcomp is not b.state else None), fg_accum=b.fg)
         flat_slot = torch.arange(b.G, device=self.device, dtype=torch.int64) * b.max_slots + b.slot.long()

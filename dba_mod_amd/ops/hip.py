@@ -57,6 +57,7 @@ _SIGS = {
     "dba_sq_dists": [_P, _LL, _P, _I, _LL, _P, _P],
     "dba_weighted_sum": [_P, _LL, _P, _I, _P, _LL, _P],
     "dba_gram": [_P, _LL, _I, _I, _P, _P],
+    "dba_dist_loss_grad": [_P, _LL, _P, _LL, _P, _LL, _I, _P, _P, _F, _P, _P],
 }
 for _name, _args in _SIGS.items():
     _fn = getattr(_L, _name)
@@ -357,6 +358,16 @@ def sgd_step(params, grads, mom, lr, first, active, momentum, wd, shadow=None, f
     _call("dba_sgd_step", params.data_ptr(), params.stride(0), grads.data_ptr(), mom.data_ptr(),
           lr.float().contiguous().data_ptr(), _i32(first).data_ptr(), _i32(active).data_ptr(), float(momentum),
           float(wd), _ptr(shadow), _ptr(fg_accum), G, P, _stream())
+
+
+def dist_loss_grad(w, base, grads, trig, active, alpha):
+    G, P = grads.shape
+    assert w.dtype == torch.float32 and w.stride(1) == 1 and base.stride(1) == 1 and grads.is_contiguous()
+    assert w.shape[0] >= G and base.shape[0] >= G and w.shape[1] >= P and base.shape[1] >= P
+    nrm2 = torch.zeros(G, dtype=torch.float32, device=grads.device)
+    _call("dba_dist_loss_grad", w.data_ptr(), w.stride(0), base.data_ptr(), base.stride(0), grads.data_ptr(), P, G,
+          _i32(trig).data_ptr(), _i32(active).data_ptr(), float(alpha), nrm2.data_ptr(), _stream())
+    return nrm2.sqrt()
 
 
 # ---------------------------------------------------------------- flat / aggregation

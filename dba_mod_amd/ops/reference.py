@@ -336,6 +336,27 @@ def sgd_step(params: Tensor, grads: Tensor, mom: Tensor, lr: Tensor, first: Tens
             shadow[g] = params[g].to(shadow.dtype)
 
 
+def dist_loss_grad(w: Tensor, base: Tensor, grads: Tensor, trig: Tensor, active: Tensor,
+                   alpha: float) -> Tensor:
+    """Anomaly-evasion loss a*CE + (1-a)*||w - w_g||_2 (helper.py:111-123, image_train.py:87-90).
+
+    For replicas in a poison phase (``trig >= 0``) rewrites ``grads`` (the CE gradient) to
+    ``a*g + (1-a)(w - base)/||w - base||`` (0 where w == base, torch's norm subgradient);
+    returns the per-replica distance ``||w - base||`` over the parameter region.
+    """
+    G, P = grads.shape
+    out = torch.zeros(G, dtype=torch.float32, device=grads.device)
+    for g in range(G):
+        if int(trig[g]) < 0 or int(active[g]) == 0:
+            continue
+        d = w[g, :P] - base[g, :P]
+        nr = torch.linalg.vector_norm(d.double()).float()
+        out[g] = nr
+        c = (1.0 - alpha) / nr if float(nr) > 0 else 0.0
+        grads[g] = alpha * grads[g] + c * d
+    return out
+
+
 # ---------------------------------------------------------------- flat / aggregation
 def scale_from_base(w: Tensor, base: Tensor, gamma: float) -> Tensor:
     """Model-replacement scaling w' = base + gamma (w - base) (K11, image_train.py:166-171)."""

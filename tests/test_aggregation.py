@@ -120,3 +120,32 @@ def test_plan_multistep_lr_quirk():
     assert l10[:2] == [1.0, 1.0] and abs(l10[2] - 0.1) < 1e-12 and abs(l10[8] - 0.01) < 1e-12
     l5 = _multistep_lrs(1.0, 5, True)                               # LOAN steps the scheduler first
     assert abs(l5[0] - 0.1) < 1e-12 and abs(l5[-1] - 0.01) < 1e-12
+
+
+def test_dist_loss_grad_matches_autograd():
+    """reference.dist_loss_grad == autograd of a*CE + (1-a)*||w - w_g|| (helper.py:111-123)."""
+    from dba_mod_amd.ops import reference as R
+    torch.manual_seed(0)
+    G, P, S = 3, 300, 320
+    w = torch.randn(G, S, dtype=torch.float64)
+    base = w + 0.1 * torch.randn(G, S, dtype=torch.float64)
+    base[2] = w[2]
+    ce_grad = torch.randn(G, P, dtype=torch.float64)
+    trig = torch.tensor([1, -1, 0], dtype=torch.int32)
+    act = torch.ones(G, dtype=torch.int32)
+    alpha = 0.6
+    got = ce_grad.clone()
+    dist = R.dist_loss_grad(w, base, got, trig, act, alpha)
+    for g in range(G):
+        wv = w[g, :P].clone().requires_grad_(True)
+        lin = (ce_grad[g] * wv).sum()               # d(lin)/dw = ce_grad
+        if int(trig[g]) >= 0:
+            sv = torch.zeros(P, dtype=torch.float64)
+            sv[:] = wv - base[g, :P]
+            loss = alpha * lin + (1 - alpha) * torch.norm(sv, 2)
+        else:
+            loss = lin
+        loss.backward()
+        assert torch.allclose(got[g], wv.grad, atol=1e-10), g
+    assert float(dist[1]) == 0.0 and float(dist[2]) == 0.0
+    assert abs(float(dist[0]) - float(torch.norm(w[0, :P] - base[0, :P]))) < 1e-6

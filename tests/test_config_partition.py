@@ -71,3 +71,22 @@ def test_synthetic_shapes():
     assert np.bincount(te.labels).tolist() == [50] * 10
     states = synthetic.synthetic_loan(1, total_rows=5000)
     assert len(states) == 51 and states[0].train_x.shape[1] == 91
+
+
+@pytest.mark.parametrize("name", ["mnist_params", "cifar_params", "cifar_centralized", "tiny_params", "loan_params"])
+def test_shipped_configs_plan_their_poison_rounds(name):
+    """Every shipped config loads, builds its (synthetic) workload and plans its attack rounds."""
+    import torch
+    from dba_mod_amd.fl.plan import build_round_plan, select_clients
+    from dba_mod_amd.fl.workload import build_workload
+    p = C.load_params(os.path.join(ROOT, "configs", f"{name}.yaml"),
+                      {"resumed_model": False, "synthetic_data": True, "synthetic_train_size": 3000,
+                       "synthetic_test_size": 300})
+    wl = build_workload(p, torch.device("cpu"))
+    assert len(wl.participants_list) >= int(p["no_models"])
+    rounds = sorted({e for i in range(len(p.adversary_list)) for e in p.poison_epochs_of(i)})
+    assert rounds
+    agents, adversarial = select_clients(p, wl, rounds[0])
+    plan = build_round_plan(p, wl, rounds[0], agents, adversarial, loan_preeval_acc=0.0)
+    poisoners = [c for c in plan.clients if any(ph.poison for ph in c.phases)]
+    assert poisoners, name

@@ -121,3 +121,29 @@ def test_tiny_workload_round(tmp_path):
     s = Server(p, DistCtx(), write_outputs=False)
     r = s.run_round(1)
     assert np.isfinite(r["global_acc"])
+
+
+def test_distance_loss_changes_poisoned_update(tmp_path):
+    """alpha_loss < 1 adds (1-a)||w - w_g|| to the poison objective (image_train.py:87-90)."""
+    out = {}
+    for a in (1.0, 0.3):
+        s = Server(mnist_params(tmp_path / str(a), alpha_loss=a), DistCtx(), write_outputs=True)
+        s.run_round(12)
+        scale = list(csv.reader(open(os.path.join(s.folder, "scale_result.csv"))))
+        out[a] = float(scale[-1][1])          # attacker's post-scaling distance to the global model
+        assert np.isfinite(out[a])
+    # the distance term pulls the poisoned model towards w_g: smaller scaled distance
+    assert out[0.3] < out[1.0]
+
+
+def test_pipelined_rounds_match_sequential(tmp_path):
+    """Server.run_rounds (eval of r overlapped with training of r+1) == run_round loop."""
+    s1 = Server(mnist_params(tmp_path / "a"), DistCtx(), write_outputs=True)
+    seq = [s1.run_round(e) for e in (11, 12, 13)]
+    s2 = Server(mnist_params(tmp_path / "b"), DistCtx(), write_outputs=True)
+    pip = s2.run_rounds(range(11, 14))
+    assert len(pip) == 3
+    for a, b in zip(seq, pip):
+        assert a["global_acc"] == b["global_acc"] and a["global_asr"] == b["global_asr"]
+    for name in ("test_result.csv", "posiontest_result.csv", "train_result.csv"):
+        assert open(os.path.join(s1.folder, name)).read() == open(os.path.join(s2.folder, name)).read(), name

@@ -249,6 +249,22 @@ def test_sgd_step(H, R):
     _close(sh[:2], st[:2, :P], 1e-2, 1e-6, "bf16 shadow")
 
 
+def test_dist_loss_grad(H, R):
+    dev = torch.device("cuda")
+    G, P, S = 4, 5000, 5120
+    st = torch.randn(G, S, device=dev)
+    base = st + 0.01 * torch.randn(G, S, device=dev)
+    base[3] = st[3]                                   # w == base: zero subgradient
+    trig = torch.tensor([0, -1, 2, 1], dtype=torch.int32, device=dev)
+    act = torch.tensor([1, 1, 1, 1], dtype=torch.int32, device=dev)
+    gr = torch.randn(G, P, device=dev)
+    g2 = gr.clone()
+    d1 = H.dist_loss_grad(st, base, gr, trig, act, 0.7)
+    d2 = R.dist_loss_grad(st, base, g2, trig, act, 0.7)
+    _close(d1, d2, 1e-4, 1e-6, "distance")
+    _close(gr, g2, 1e-4, 1e-5, "grads")
+
+
 def test_flat_aggregation_ops(H, R):
     dev = torch.device("cuda")
     n, L = 10, 100_003

@@ -1,0 +1,53 @@
+"""Offline dataset preparation tools (reference utils/loan_preprocess.py, tinyimagenet_reformat.py)."""
+import os
+
+import numpy as np
+import pandas as pd
+
+from dba_mod_amd.data import readers
+from dba_mod_amd.tools import prep_loan, prep_tiny
+
+
+def test_loan_preprocess_encodes_scales_and_splits(tmp_path):
+    n = 60
+    rng = np.random.default_rng(0)
+    df = pd.DataFrame({
+        "id": np.arange(n), "url": ["u"] * n,                       # dropped
+        "loan_amnt": rng.uniform(1000, 30000, n),                    # mean > 1000   -> /10000
+        "int_rate": rng.uniform(11, 20, n),                          # (10, 100]     -> /10
+        "installment": rng.uniform(150, 900, n),                     # (100, 1000]   -> /100
+        "pub_rec": rng.integers(0, 3, n).astype(np.int64),           # <= 10         -> unchanged
+        "term": rng.choice([" 36 months", " 60 months"], n),         # object -> first-appearance codes
+        "loan_status": rng.choice(["Current", "Fully Paid", "Charged Off"], n),
+        "addr_state": rng.choice(["CA", "NY", "TX"], n),
+        "mths_since_last_delinq": [np.nan] * n,                      # dropped
+    })
+    df.loc[3, "int_rate"] = np.nan                                   # fillna(0) before scaling
+    out = prep_loan.preprocess(df)
+    assert "id" not in out and "url" not in out and "mths_since_last_delinq" not in out
+    np.testing.assert_allclose(out["loan_amnt"], df["loan_amnt"] / 10000)
+    np.testing.assert_allclose(out["installment"], df["installment"] / 100)
+    np.testing.assert_allclose(out["int_rate"], df["int_rate"].fillna(0) / 10)
+    assert (out["pub_rec"] == df["pub_rec"]).all()
+    first = list(dict.fromkeys(df["loan_status"]))
+    assert [first[c] for c in out["loan_status"]] == list(df["loan_status"])
+    files = prep_loan.split_by_state(out, str(tmp_path / "loan"))
+    assert sorted(os.path.basename(f) for f in files) == ["loan_CA.csv", "loan_NY.csv", "loan_TX.csv"]
+    # the framework's LOAN reader consumes the output directly
+    parts = readers.read_loan(str(tmp_path))
+    assert sum(len(p.train_y) + len(p.test_y) for p in parts) == n
+
+
+def test_tiny_reformat_moves_val_images(tmp_path):
+    root = tmp_path / "tiny-imagenet-200"
+    img = root / "val" / "images"
+    img.mkdir(parents=True)
+    ann = []
+    for i, wnid in enumerate(["n01", "n02", "n01"]):
+        (img / f"val_{i}.JPEG").write_bytes(b"x")
+        ann.append(f"val_{i}.JPEG\t{wnid}\t0\t0\t63\t63")
+    (root / "val" / "val_annotations.txt").write_text("\n".join(ann) + "\n")
+    assert prep_tiny.reformat_val(str(root)) == 3
+    assert sorted(os.listdir(root / "val")) == ["n01", "n02"]
+    assert sorted(os.listdir(root / "val" / "n01")) == ["val_0.JPEG", "val_2.JPEG"]
+    assert prep_tiny.reformat_val(str(root)) == 0                  # idempotent
