@@ -57,6 +57,7 @@ _SIGS = {
     "dba_sq_dists": [_P, _LL, _P, _I, _LL, _P, _P],
     "dba_weighted_sum": [_P, _LL, _P, _I, _P, _LL, _P],
     "dba_gram": [_P, _LL, _I, _I, _P, _P],
+    "dba_pconv": [_P, _LL, _P, _LL, _P, _P, _LL, _P, _P, _LL, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P],
     "dba_dist_loss_grad": [_P, _LL, _P, _LL, _P, _LL, _I, _P, _P, _F, _P, _P],
 }
 for _name, _args in _SIGS.items():
@@ -144,6 +145,24 @@ def _check_w(w: Tensor) -> Tuple[Tensor, int]:
     return _rowview(w)
 
 
+_PCONV = os.environ.get("DBA_PCONV", "1") != "0"
+_PCONV_SHAPES = {(32, 32, 32), (64, 64, 16)}     # (Cin, Cout, W): see csrc/kernels/pconv.hip
+_ZEROS = {}
+
+
+def _zeros(dev) -> Tensor:
+    """A small persistent zero page (halo padding source of the LDS-DMA conv kernels)."""
+    z = _ZEROS.get(dev)
+    if z is None:
+        z = _ZEROS[dev] = torch.zeros(256, dtype=torch.uint8, device=dev)
+    return z
+
+
+def _pconv_ok(Cin, Cout, H, W, KH, KW, stride, pad) -> bool:
+    return (_PCONV and stride == 1 and KH == 3 and KW == 3 and pad == 1 and H == W
+            and (Cin, Cout, W) in _PCONV_SHAPES)
+
+
 def conv2d(x, w, wsel, stride, pad, bias=None, residual=None, relu=False, nvalid=None, out_dtype=None):
     x = _bf16c(x)
     G, N, H, W, Cin = x.shape
@@ -164,7 +183,12 @@ def conv2d(x, w, wsel, stride, pad, bias=None, residual=None, relu=False, nvalid
     # kernel selection by shape: halo-tiled direct conv (stride 1), gen-2 implicit GEMM
     # (Cin % 8 == 0 or small-Cin stems), gen-1 implicit GEMM (odd channel counts)
     rc = NOT_HANDLED
-    if stride == 1 and KH == KW:
+    if (not f32 and _pconv_ok(Cin, Cout, H, W, KH, KW, stride, pad)
+            and (bias is None or (bs % 4 == 0 and bias.data_ptr() % 16 == 0))):
+        rc = _call("dba_pconv", x.data_ptr(), N * H * W * Cin, w.data_ptr(), ws, wsel_, _ptr(bias), bs,
+                   _ptr(residual), y.data_ptr(), N * Ho * Wo * Cout, nv_, _zeros(x.device).data_ptr(), G, N, H, W,
+                   Cin, Cout, 0, int(relu), _stream())
+    if rc == NOT_HANDLED and stride == 1 and KH == KW:
         rc = _call("dba_halo_conv", x.data_ptr(), N * H * W * Cin, w.data_ptr(), ws, wsel_, _ptr(bias), bs,
                    _ptr(residual), y.data_ptr(), N * Ho * Wo * Cout, f32, nv_, G, N, H, W, Cin, Cout, KH, pad,
                    int(relu), _stream())
@@ -186,6 +210,14 @@ def conv2d_dgrad(dy, w, wsel, stride, pad, in_hw, nvalid=None, out_dtype=None):
     slots, _, KH, KW, Cin = w.shape
     H, W = in_hw
     dx = torch.empty(G, N, H, W, Cin, dtype=_BF16, device=dy.device)
+    if _pconv_ok(Cout, Cin, H, W, KH, KW, stride, pad):
+        # stride-1 3x3 dgrad on the persistent kernel: transposed + flipped weight fragments
+        # are gathered in-kernel from the forward weights (no transpose pass)
+        rc = _call("dba_pconv", dy.data_ptr(), N * Ho * Wo * Cout, w.data_ptr(), ws, _ptr(_i32(wsel)), None, 0,
+                   None, dx.data_ptr(), N * H * W * Cin, _ptr(_i32(nvalid)), _zeros(dy.device).data_ptr(), G, N, H,
+                   W, Cout, Cin, 1, 0, _stream())
+        if rc != NOT_HANDLED:
+            return dx if out_dtype in (None, _BF16) else dx.to(out_dtype)
     wt = torch.empty(slots, Cin, KH, KW, Cout, dtype=_BF16, device=dy.device)
     if stride == 1 and KH == KW and pad == (KH - 1) // 2:
         # stride-1 dgrad == forward conv of dY with tap-flipped, transposed weights

@@ -1,0 +1,85 @@
+"""Kernel microbenchmarks on the real ResNet-18 (CIFAR) layer shapes.
+
+Times each HIP conv kernel family on the shapes the FL round actually runs — evaluation
+(17 folded-BN client models x 1024 images) and grouped training (10 clients x 64 images) —
+and prints achieved TFLOP/s, so kernel changes are judged on the chip, not guessed.
+
+    python -m dba_mod_amd.tools.bench_kernels [--reps 20] [--json out.json]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+
+import torch
+
+from dba_mod_amd.ops import hip as H
+
+# name, G, N, H, Cin, Cout, k, stride, pad
+SHAPES = [
+    ("eval.layer1", 17, 1024, 32, 32, 32, 3, 1, 1),
+    ("eval.layer2", 17, 1024, 16, 64, 64, 3, 1, 1),
+    ("eval.layer3", 17, 1024, 8, 128, 128, 3, 1, 1),
+    ("eval.layer4", 17, 1024, 4, 256, 256, 3, 1, 1),
+    ("eval.l2.0.conv1", 17, 1024, 32, 32, 64, 3, 2, 1),
+    ("train.layer1", 10, 64, 32, 32, 32, 3, 1, 1),
+    ("train.layer2", 10, 64, 16, 64, 64, 3, 1, 1),
+    ("train.layer3", 10, 64, 8, 128, 128, 3, 1, 1),
+    ("train.layer4", 10, 64, 4, 256, 256, 3, 1, 1),
+]
+
+
+def _time(fn, reps):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / reps * 1e-3
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--json", default=None)
+    args = ap.parse_args(argv)
+    dev = torch.device("cuda")
+    rows = []
+    for name, G, N, Hh, Cin, Cout, k, s, p in SHAPES:
+        torch.manual_seed(0)
+        x = torch.randn(G, N, Hh, Hh, Cin, device=dev).bfloat16()
+        w = (torch.randn(G, Cout, k, k, Cin, device=dev) * 0.05).bfloat16()
+        Ho = (Hh + 2 * p - k) // s + 1
+        dy = torch.randn(G, N, Ho, Ho, Cout, device=dev).bfloat16()
+        flops = 2.0 * G * N * Ho * Ho * Cout * k * k * Cin
+        rec = {"shape": name}
+        for tag, pc in (("fwd", True), ("fwd_nopconv", False)):
+            H._PCONV = pc
+            t = _time(lambda: H.conv2d(x, w, None, s, p, relu=True), args.reps)
+            rec[tag + "_us"] = round(t * 1e6, 1)
+            rec[tag + "_tflops"] = round(flops / t / 1e12, 1)
+        for tag, pc in (("dgrad", True), ("dgrad_nopconv", False)):
+            H._PCONV = pc
+            t = _time(lambda: H.conv2d_dgrad(dy, w, None, s, p, (Hh, Hh)), args.reps)
+            rec[tag + "_us"] = round(t * 1e6, 1)
+            rec[tag + "_tflops"] = round(flops / t / 1e12, 1)
+        H._PCONV = True
+        if name.startswith("train"):
+            dw = torch.zeros(G, Cout, k, k, Cin, device=dev)
+            t = _time(lambda: H.conv2d_wgrad(dy, x, s, p, k, k, dw), args.reps)
+            rec["wgrad_us"] = round(t * 1e6, 1)
+            rec["wgrad_tflops"] = round(flops / t / 1e12, 1)
+        rows.append(rec)
+        print(json.dumps(rec), flush=True)
+    if args.json:
+        with open(args.json, "w") as f:
+            json.dump(rows, f, indent=1)
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())

@@ -54,6 +54,8 @@ CONV_CASES = [
     (2, 4, 16, 16, 64, 64, 3, 1, 1),     # layer2 (halo kernel)
     (3, 4, 32, 32, 32, 32, 1, 1, 0),     # 1x1 stride 1 (halo kernel)
     (2, 3, 4, 4, 256, 256, 3, 1, 1),     # layer4 (halo does not fit LDS -> gen-2 GEMM)
+    (5, 40, 32, 32, 32, 32, 3, 1, 1),    # persistent kernel: block runs cross group boundaries
+    (4, 70, 16, 16, 64, 64, 3, 1, 1),    # persistent kernel, 64-channel geometry
 ]
 
 
@@ -95,6 +97,28 @@ def test_conv_fwd_dgrad_wgrad(H, R, case):
     for g in range(G):
         assert _rel(dw[g], dwr[g]) < 1e-2, f"wgrad g{g}"
         assert _rel(db[g], dbr[g]) < 1e-3, f"bias grad g{g}"
+
+
+@pytest.mark.parametrize("C,HW", [(32, 32), (64, 16)])
+def test_pconv_inactive_groups_and_slots(H, R, C, HW):
+    """Persistent conv: zero-valid groups in the middle, shared weight slots, fwd + dgrad."""
+    dev = torch.device("cuda")
+    torch.manual_seed(1)
+    G, N = 7, 9
+    x = torch.randn(G, N, HW, HW, C, device=dev).bfloat16()
+    w = (torch.randn(3, C, 3, 3, C, device=dev) * (1.0 / (9 * C) ** 0.5)).bfloat16()
+    wsel = torch.tensor([2, 0, 1, 1, 2, 0, 1], dtype=torch.int32, device=dev)
+    nvalid = torch.tensor([9, 0, 4, 0, 0, 9, 1], dtype=torch.int32, device=dev)
+    y = H.conv2d(x, w, wsel, 1, 1, nvalid=nvalid)
+    yr = R.conv2d(x.float(), w.float(), wsel, 1, 1)
+    dy = torch.randn(G, N, HW, HW, C, device=dev).bfloat16()
+    dx = H.conv2d_dgrad(dy, w, wsel, 1, 1, (HW, HW), nvalid=nvalid)
+    dxr = R.conv2d_dgrad(dy.float(), w.float(), wsel, 1, 1, (HW, HW))
+    for g in range(G):
+        n = int(nvalid[g])
+        if n:
+            _close(y[g, :n], yr[g, :n], 2e-2, 3e-2, f"fwd g{g}")
+            assert _rel(dx[g, :n], dxr[g, :n]) < 1e-2, f"dgrad g{g}"
 
 
 def test_conv_fp32_out_and_inactive_group(H, R):
