@@ -14,7 +14,14 @@
 
 namespace {
 
-constexpr int kRowsPerBlock = 512;
+// Rows per reduction block: ~16K elements per block (8 passes of 256 threads x 8 channels),
+// so narrow-spatial / wide-channel layers (ResNet stage 4: 16 px x 256 ch) still launch
+// enough blocks to cover the chip instead of 2 per replica.
+__host__ __device__ inline int rows_per_block(int C) {
+  const int rpp = 256 / (C / 8);
+  const int r = 16384 / C;
+  return r > rpp ? r : rpp;
+}
 
 // Per-block partial sums (no atomics, no pre-zeroing): part[g][blk][0][c] = sum x (STATS)
 // or sum d (BWD); part[g][blk][1][c] = sum x^2 or sum d*xhat.  Blocks past the valid rows
@@ -29,14 +36,15 @@ __global__ __launch_bounds__(256) void bn_reduce_kernel(const uint16_t* __restri
   const int g = blockIdx.y;
   const int R = N * HW;
   const int Rv = valid_rows(nvalid, g, N) * HW;
-  const int r0 = blockIdx.x * kRowsPerBlock;
+  const int rpb = rows_per_block(C);
+  const int r0 = blockIdx.x * rpb;
   const int tid = threadIdx.x;
   float* pg = part + ((long long)g * gridDim.x + blockIdx.x) * 2 * C;
   if (r0 >= Rv) {
     for (int c = tid; c < 2 * C; c += 256) pg[c] = 0.f;
     return;
   }
-  const int r1 = min(Rv, r0 + kRowsPerBlock);
+  const int r1 = min(Rv, r0 + rpb);
   const int tpr = C / 8;                 // threads per row
   const int rpp = 256 / tpr;             // rows per pass
   const int cg = tid % tpr, rr = tid / tpr;
@@ -127,6 +135,9 @@ __global__ void bn_finalize_kernel(const float* __restrict__ part, int nblk, con
   *prv = (float)((1.0 - momentum) * (*prv) + momentum * unb);
 }
 
+// Elementwise passes: 256 % (C/8) == 0, so every thread of the grid-stride loop always owns
+// the same 8 channels; their per-(replica, channel) coefficients are loaded once per replica
+// change instead of 4-7 scalar loads per element.
 __global__ void bn_apply_kernel(const uint16_t* __restrict__ y, const float* __restrict__ mean,
                                 const float* __restrict__ invstd, const float* __restrict__ gamma,
                                 const float* __restrict__ beta, long long p_gstride, const uint16_t* __restrict__ res,
@@ -135,14 +146,26 @@ __global__ void bn_apply_kernel(const uint16_t* __restrict__ y, const float* __r
   const int c8 = C / 8;
   const int per = N * HW * c8;                 // < 2^31 for every model / batch size used
   const int total = per * G;
-  for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x) {
+  const int tid0 = blockIdx.x * blockDim.x + threadIdx.x;
+  const int c0 = (tid0 % c8) * 8;
+  int gc = -1, nvr = 0;
+  float sc[8], sh[8];
+  for (int t = tid0; t < total; t += gridDim.x * blockDim.x) {
     const int g = t / per;
-    const int rem = t - g * per;
-    const int row = rem / c8;
-    const int c0 = (rem - row * c8) * 8;
+    if (g != gc) {
+      gc = g;
+      nvr = valid_rows(nvalid, g, N) * HW;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int c = c0 + e;
+        sc[e] = invstd[g * C + c] * gamma[(long long)g * p_gstride + c];
+        sh[e] = beta[(long long)g * p_gstride + c] - mean[g * C + c] * sc[e];
+      }
+    }
+    const int row = (t - g * per) / c8;
     const long long o = (long long)t * 8;
     uint4 res8 = make_uint4(0, 0, 0, 0);
-    if (row >= valid_rows(nvalid, g, N) * HW) {
+    if (row >= nvr) {
       *(uint4*)(out + o) = res8;
       continue;
     }
@@ -154,9 +177,7 @@ __global__ void bn_apply_kernel(const uint16_t* __restrict__ y, const float* __r
     uint16_t* op = (uint16_t*)&res8;
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      const int c = c0 + e;
-      float v = (bf2f(yp[e]) - mean[g * C + c]) * invstd[g * C + c] * gamma[(long long)g * p_gstride + c] +
-                beta[(long long)g * p_gstride + c];
+      float v = fmaf(bf2f(yp[e]), sc[e], sh[e]);
       if (res) v += bf2f(rp[e]);
       if (relu) v = fmaxf(v, 0.f);
       op[e] = f2bf(v);
@@ -165,6 +186,7 @@ __global__ void bn_apply_kernel(const uint16_t* __restrict__ y, const float* __r
   }
 }
 
+// dy = gamma*is/n * (n*d - sum d - xhat * sum d*xhat) = A*d + B*y + K per (replica, channel)
 __global__ void bn_bwd_apply_kernel(const uint16_t* __restrict__ dout, const uint16_t* __restrict__ out,
                                     const uint16_t* __restrict__ y, const float* __restrict__ mean,
                                     const float* __restrict__ invstd, const float* __restrict__ gamma,
@@ -174,20 +196,36 @@ __global__ void bn_bwd_apply_kernel(const uint16_t* __restrict__ dout, const uin
   const int c8 = C / 8;
   const int per = N * HW * c8;                 // < 2^31 for every model / batch size used
   const int total = per * G;
-  for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x) {
+  const int tid0 = blockIdx.x * blockDim.x + threadIdx.x;
+  const int c0 = (tid0 % c8) * 8;
+  int gc = -1, nv = 0;
+  float A[8], B[8], K[8];
+  for (int t = tid0; t < total; t += gridDim.x * blockDim.x) {
     const int g = t / per;
-    const int rem = t - g * per;
-    const int row = rem / c8;
-    const int c0 = (rem - row * c8) * 8;
+    if (g != gc) {
+      gc = g;
+      nv = valid_rows(nvalid, g, N) * HW;
+      const float n = (float)(nv > 0 ? nv : 1);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int c = c0 + e;
+        const float is = invstd[g * C + c];
+        const float ga = gamma[(long long)g * p_gstride + c] * is;
+        const float sd = sums[((long long)g * 2) * C + c];
+        const float sdx = sums[((long long)g * 2 + 1) * C + c];
+        A[e] = ga;
+        B[e] = -ga * is * sdx / n;
+        K[e] = -ga * sd / n - B[e] * mean[g * C + c];
+      }
+    }
+    const int row = (t - g * per) / c8;
     const long long o = (long long)t * 8;
-    const int nv = valid_rows(nvalid, g, N) * HW;
     uint4 z = make_uint4(0, 0, 0, 0);
     if (row >= nv) {
       *(uint4*)(dy + o) = z;
       if (dres) *(uint4*)(dres + o) = z;
       continue;
     }
-    const float n = (float)nv;
     const uint4 dv = *(const uint4*)(dout + o);
     const uint4 yv = *(const uint4*)(y + o);
     uint4 ov = z;
@@ -200,15 +238,9 @@ __global__ void bn_bwd_apply_kernel(const uint16_t* __restrict__ dout, const uin
     uint16_t* p2 = (uint16_t*)&r2;
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      const int c = c0 + e;
       float d = bf2f(dp[e]);
       if (relu && !(bf2f(op[e]) > 0.f)) d = 0.f;
-      const float is = invstd[g * C + c];
-      const float xh = (bf2f(yp[e]) - mean[g * C + c]) * is;
-      const float sd = sums[((long long)g * 2) * C + c];
-      const float sdx = sums[((long long)g * 2 + 1) * C + c];
-      const float v = gamma[(long long)g * p_gstride + c] * is / n * (n * d - sd - xh * sdx);
-      p1[e] = f2bf(v);
+      p1[e] = f2bf(fmaf(A[e], d, fmaf(B[e], bf2f(yp[e]), K[e])));
       p2[e] = f2bf(d);
     }
     *(uint4*)(dy + o) = r1;
@@ -258,14 +290,14 @@ int egrid(long long n) { return (int)std::max(1LL, std::min(16384LL, (n + 255) /
 
 }  // namespace
 
-DBA_EXPORT int dba_bn_partial_blocks(int N, int HW) { return ceil_div((long long)N * HW, kRowsPerBlock); }
+DBA_EXPORT int dba_bn_partial_blocks(int N, int HW, int C) { return ceil_div((long long)N * HW, rows_per_block(C)); }
 
 // part: [G][nblk][2][C] fp32 workspace (no initialisation needed)
 DBA_EXPORT int dba_bn_stats(const void* y, const int* nvalid, int G, int N, int HW, int C, float* part, float* rm,
                             float* rv, long long s_gstride, float momentum, float eps, float* mean, float* invstd,
                             void* stream) {
   hipStream_t st = (hipStream_t)stream;
-  const int nblk = ceil_div((long long)N * HW, kRowsPerBlock);
+  const int nblk = ceil_div((long long)N * HW, rows_per_block(C));
   hipLaunchKernelGGL(bn_reduce_kernel<false>, dim3(nblk, G), dim3(256), 0, st, (const uint16_t*)y, nullptr, nullptr,
                      nullptr, nullptr, 0, nvalid, N, HW, C, part);
   hipLaunchKernelGGL(bn_finalize_kernel, dim3(ceil_div(C, 64), G), dim3(256), 0, st, part, nblk, nvalid, N, HW, C,
@@ -288,7 +320,7 @@ DBA_EXPORT int dba_bn_bwd(const void* dout, const void* out, const void* y, cons
                           long long g_gstride, void* dy, void* dres, float* part, const int* nvalid, int G, int N,
                           int HW, int C, void* stream) {
   hipStream_t st = (hipStream_t)stream;
-  const int nblk = ceil_div((long long)N * HW, kRowsPerBlock);
+  const int nblk = ceil_div((long long)N * HW, rows_per_block(C));
   float* sums = part + (long long)G * nblk * 2 * C;
   hipLaunchKernelGGL(bn_reduce_kernel<true>, dim3(nblk, G), dim3(256), 0, st, (const uint16_t*)y,
                      (const uint16_t*)dout, (const uint16_t*)out, mean, invstd, relu, nvalid, N, HW, C, part);

@@ -425,8 +425,56 @@ DBA_EXPORT int dba_conv_wgrad(const void* dy, long long dy_gstride, const void* 
   DBA_LAUNCH_CHECK();
 }
 
+// w[s][co][t][ci] -> wt[s][ci][t'][co] through a 64x64 LDS tile: 16-byte loads along ci,
+// 16-byte stores along co (the naive kernel above reads with a T*Ci stride).  Slots whose
+// replica is inactive this step (nvalid[s] == 0, slot == replica) are skipped.
+__global__ __launch_bounds__(256) void transpose_w_tiled_kernel(const uint16_t* __restrict__ w, long long w_sstride,
+                                                                uint16_t* __restrict__ wt, int Co, int T, int Ci,
+                                                                int flip, const int* __restrict__ nvalid) {
+  __shared__ uint16_t tile[64][64 + 2];
+  const int s = blockIdx.z;
+  if (nvalid && nvalid[s] == 0) return;
+  const int t = blockIdx.y;
+  const int tci = (Ci + 63) / 64;
+  const int co0 = (blockIdx.x / tci) * 64, ci0 = (blockIdx.x % tci) * 64;
+  const uint16_t* ws = w + (long long)s * w_sstride;
+  uint16_t* wo = wt + (long long)s * Co * T * Ci;
+  const int tid = threadIdx.x;
+  const int ts = flip ? T - 1 - t : t;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int e = tid + 256 * i;               // 64 rows x 8 chunks
+    const int r = e >> 3, c8 = (e & 7) * 8;
+    const int co = co0 + r, ci = ci0 + c8;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (co < Co && ci < Ci) v = *(const uint4*)(ws + ((long long)co * T + ts) * Ci + ci);
+    const uint16_t* pv = (const uint16_t*)&v;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) tile[r][c8 + j] = pv[j];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int e = tid + 256 * i;
+    const int r = e >> 3, c8 = (e & 7) * 8;    // r: ci within tile, c8: co chunk
+    const int ci = ci0 + r, co = co0 + c8;
+    if (ci >= Ci || co >= Co) continue;
+    uint4 v;
+    uint16_t* pv = (uint16_t*)&v;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) pv[j] = tile[c8 + j][r];
+    *(uint4*)(wo + ((long long)ci * T + t) * Co + co) = v;
+  }
+}
+
 DBA_EXPORT int dba_transpose_w(const void* w, long long w_sstride, void* wt, int slots, int Co, int T, int Ci,
-                               int flip, void* stream) {
+                               int flip, const int* nvalid, void* stream) {
+  if (Co % 8 == 0 && Ci % 8 == 0) {
+    dim3 grid(ceil_div(Co, 64) * ceil_div(Ci, 64), T, slots);
+    hipLaunchKernelGGL(transpose_w_tiled_kernel, grid, dim3(256), 0, (hipStream_t)stream, (const uint16_t*)w,
+                       w_sstride, (uint16_t*)wt, Co, T, Ci, flip, nvalid);
+    DBA_LAUNCH_CHECK();
+  }
   const int per = Co * T * Ci;
   const int bx = std::max(1, std::min(256, (per + 255) / 256));
   hipLaunchKernelGGL(transpose_w_kernel, dim3(bx, slots), dim3(256), 0, (hipStream_t)stream, (const uint16_t*)w,

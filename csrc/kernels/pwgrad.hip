@@ -1,0 +1,207 @@
+// Halo-tiled weight gradient for the stride-1 3x3 convolutions (ResNet-18 stages 1-4):
+//   dW[co][kh][kw][ci] += sum over pixels of dY[px][co] * X[px shifted by (kh-1, kw-1)][ci]
+//
+// The reduction axis is the PIXEL, but NHWC stores pixels as rows with channels
+// contiguous — both MFMA operands need their k (pixel) index inside a lane.  gfx950's
+// transposing LDS read (ds_read_b64_tr_b16) delivers exactly that from the natural
+// row-major images, so the tiles stream global -> LDS untouched (LDS-DMA) and are
+// consumed column-wise:
+//   * A = dY^T (32 output channels x 16 pixels), B = X_tap (16 pixels x 32 input channels);
+//   * a block owns a (CO x CI) channel slice of one client replica and a contiguous run of
+//     (image, row-segment) tiles; per tile it stages the dY tile [SR*W][CO] and the input
+//     halo [(SR+2) x (W+2)][CI] once and reuses the halo for all 9 taps (no im2col);
+//   * one wave per (32-co, 32-ci, kernel row kh) owns 3 accumulators (kw = 0..2);
+//   * double-buffered DMA: tile t+1 lands while tile t computes, one barrier per tile;
+//   * 64-channel images use a 16-byte-chunk XOR swizzle (bit 2 of the chunk by bit 1 of the
+//     pixel) so the 4 rows of every transposed read hit distinct bank slots;
+//   * the block's partial dW leaves by fp32 atomics (split-K over pixel runs) into the flat
+//     gradient buffer.
+#include "common.hpp"
+#include <algorithm>
+
+namespace {
+
+typedef short v4i16_t __attribute__((ext_vector_type(4)));
+
+struct PwArgs {
+  const uint16_t* dy; long long dy_gstride;     // [G][N][H][W][Cout]
+  const uint16_t* x; long long x_gstride;       // [G][N][H][W][Cin]
+  float* dw; long long dw_gstride;              // [G][Cout][3][3][Cin] (fp32, accumulated)
+  const int* nvalid;
+  const uint16_t* zeros;
+  int N, H, Cout, Cin;
+  int atomic;                                   // split-K over pixel runs (> 1 block per output)
+};
+
+template <int CH>
+__device__ __forceinline__ int swz_px(int px) {   // chunk XOR for a CH-channel image row
+  if constexpr (CH == 64) return ((px >> 1) & 1) << 2;
+  else return 0;
+}
+
+// byte offset of (row, channel col) in a CH-channel image with the swizzle; col % 4 == 0
+template <int CH>
+__device__ __forceinline__ int img_off(int row, int col) {
+  const int chunk = col >> 3;
+  return row * CH * 2 + ((chunk ^ swz_px<CH>(row)) << 4) + ((col & 7) << 1);
+}
+
+template <int CO, int CI, int W, int SR>
+__global__ __launch_bounds__((CO / 32) * (CI / 32) * 3 * 64) void pwgrad_kernel(PwArgs a) {
+  constexpr int NCO = CO / 32, NCI = CI / 32;
+  constexpr int NW = NCO * NCI * 3;
+  constexpr int NT = NW * 64;
+  constexpr int TP = SR * W;                      // pixels per tile
+  constexpr int HP = W + 2, HR = SR + 2;
+  constexpr int DYCH = TP * CO / 8;               // 16-B chunks of the dY tile
+  constexpr int HCH = HR * HP * CI / 8;           // 16-B chunks of the halo
+  constexpr int NI = (DYCH + HCH + NT - 1) / NT;  // DMA instructions per thread per tile
+  constexpr int BUF = NI * NT;                    // chunks per buffer
+  static_assert(TP % 16 == 0 && W % 4 == 0, "tile geometry");
+  __shared__ __attribute__((aligned(16))) uint4 lds[2][BUF];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int g = blockIdx.y;
+  const int nci_blk = a.Cin / CI;
+  const int co0 = (blockIdx.z / nci_blk) * CO, ci0 = (blockIdx.z % nci_blk) * CI;
+  const int segs = a.H / SR;
+  const int T = valid_rows(a.nvalid, g, a.N) * segs;
+  const int per = (T + gridDim.x - 1) / gridDim.x;
+  const int t0 = blockIdx.x * per, t1 = min(T, t0 + per);
+  if (t0 >= t1) return;
+  const int HW = a.H * W;
+  const uint16_t* __restrict__ dyg = a.dy + (long long)g * a.dy_gstride;
+  const uint16_t* __restrict__ xg = a.x + (long long)g * a.x_gstride;
+
+  auto stage = [&](int tt, int buf) {
+    const int n = tt / segs, sg = tt - n * segs;
+    const int row0 = sg * SR;
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int e = tid + NT * i;
+      const uint16_t* p = a.zeros;
+      if (e < DYCH) {
+        const int px = e / (CO / 8), cs = e - px * (CO / 8);
+        p = dyg + ((long long)n * HW + row0 * W + px) * a.Cout + co0 + ((cs ^ swz_px<CO>(px)) << 3);
+      } else if (e < DYCH + HCH) {
+        const int e2 = e - DYCH;
+        const int hp = e2 / (CI / 8), cs = e2 - hp * (CI / 8);
+        const int hr = hp / HP, hc = hp - hr * HP;
+        const int ih = row0 - 1 + hr, iw = hc - 1;
+        if ((unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)W)
+          p = xg + (((long long)n * a.H + ih) * W + iw) * a.Cin + ci0 + ((cs ^ swz_px<CI>(hp)) << 3);
+      }
+      __builtin_amdgcn_global_load_lds((const void*)p,
+                                       (__attribute__((address_space(3))) void*)&lds[buf][i * NT + wid * 64],
+                                       16, 0, 0);
+    }
+  };
+
+  // wave roles
+  const int kh = wid % 3;
+  const int wci = (wid / 3) % NCI, wco = wid / (3 * NCI);
+  // transposed-read lane geometry (T10): group G = lane>>4, q = row in the 4-row block, p = 4-col group
+  const int G4 = lane >> 4, q = (lane >> 2) & 3, p4 = lane & 3;
+  const int hsel = G4 >> 1;                       // k half (rows 8h..8h+7)
+  const int colA = wco * 32 + 16 * (G4 & 1) + 4 * p4;   // co within the slice
+  const int colB = wci * 32 + 16 * (G4 & 1) + 4 * p4;   // ci within the slice
+
+  f32x16_t acc[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[k][r] = 0.f;
+
+  stage(t0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  int cur = 0;
+  for (int tt = t0; tt < t1; ++tt) {
+    const bool more = tt + 1 < t1;
+    if (more) stage(tt + 1, cur ^ 1);
+    const char* Lb = reinterpret_cast<const char*>(lds[cur]);
+    const char* Ldy = Lb;
+    const char* Lx = Lb + DYCH * 16;
+#pragma unroll 2
+    for (int ks = 0; ks < TP / 16; ++ks) {
+      union { bf16x8_t v; v4i16_t h[2]; } fa, fb[3];
+#pragma unroll
+      for (int t2 = 0; t2 < 2; ++t2) {
+        const int px = ks * 16 + 8 * hsel + 4 * t2 + q;          // pixel (k index) this lane addresses
+        fa.h[t2] = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) v4i16_t*)(Ldy + img_off<CO>(px, colA)));
+        const int r = px / W, c = px - r * W;
+        const int hp0 = (r + kh) * HP + c;
+#pragma unroll
+        for (int kw = 0; kw < 3; ++kw)
+          fb[kw].h[t2] = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (__attribute__((address_space(3))) v4i16_t*)(Lx + img_off<CI>(hp0 + kw, colB)));
+      }
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw) acc[kw] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa.v, fb[kw].v, acc[kw], 0, 0, 0);
+    }
+    if (more) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      cur ^= 1;
+    }
+  }
+
+  // D[co][ci]: lane -> ci column (lane & 31), registers -> co rows
+  float* __restrict__ dwg = a.dw + (long long)g * a.dw_gstride;
+  const int ci = ci0 + wci * 32 + (lane & 31);
+#pragma unroll
+  for (int kw = 0; kw < 3; ++kw)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int co = co0 + wco * 32 + 8 * (r >> 2) + 4 * (lane >> 5) + (r & 3);
+      float* d = dwg + ((long long)(co * 3 + kh) * 3 + kw) * a.Cin + ci;
+      if (a.atomic) atomicAdd(d, acc[kw][r]);
+      else *d += acc[kw][r];                      // sole writer of this element
+    }
+}
+
+int num_cus_w() {
+  static int n = 0;
+  if (n == 0) {
+    int dev = 0;
+    hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+  }
+  return n;
+}
+
+template <int CO, int CI, int W, int SR>
+int launch_pw(const PwArgs& a, int G, hipStream_t st) {
+  if (a.H % SR != 0 || a.Cout % CO != 0 || a.Cin % CI != 0) return -100;
+  const int slices = (a.Cout / CO) * (a.Cin / CI);
+  const int tiles = a.N * (a.H / SR);
+  // split-K factor S (pixel runs per output slice): enough blocks to cover the CUs, but the
+  // S x |dW| fp32 atomics (~1.3 TB/s chip-wide) must not outweigh the MFMA work
+  const double by_cus = (double)num_cus_w() / std::max(1, G * slices);
+  const double by_atomics = 3.0e6 / ((double)G * a.Cout * a.Cin * 9);
+  const int S = std::max(1, std::min(tiles, (int)std::min(by_cus, by_atomics)));
+  PwArgs b = a;
+  b.atomic = S > 1;
+  dim3 grid(S, G, slices);
+  hipLaunchKernelGGL((pwgrad_kernel<CO, CI, W, SR>), grid, dim3((CO / 32) * (CI / 32) * 3 * 64), 0, st, b);
+  DBA_LAUNCH_CHECK();
+}
+
+}  // namespace
+
+// dW (+)= wgrad of a stride-1 3x3 pad-1 conv.  Returns -100 for shapes it does not tile.
+DBA_EXPORT int dba_pwgrad(const void* dy, long long dy_gstride, const void* x, long long x_gstride, float* dw,
+                          long long dw_gstride, const int* nvalid, const void* zeros, int G, int N, int H, int W,
+                          int Cin, int Cout, void* stream) {
+  PwArgs a{(const uint16_t*)dy, dy_gstride, (const uint16_t*)x, x_gstride, dw, dw_gstride, nvalid,
+           (const uint16_t*)zeros, N, H, Cout, Cin, 1};
+  hipStream_t st = (hipStream_t)stream;
+  if (Cin == 32 && Cout == 32 && W == 32) return launch_pw<32, 32, 32, 8>(a, G, st);
+  if (Cin % 64 == 0 && Cout % 64 == 0) {
+    if (W == 16) return launch_pw<64, 64, 16, 8>(a, G, st);
+    if (W == 8) return launch_pw<64, 64, 8, 8>(a, G, st);
+    if (W == 4) return launch_pw<64, 64, 4, 4>(a, G, st);
+  }
+  return -100;
+}

@@ -36,11 +36,11 @@ _SIGS = {
     "dba_conv_wgrad": [_P, _LL, _P, _LL, _P, _LL, _P] + [_I] * 12 + [_P],
     "dba_conv2_fwd": [_P, _LL, _P, _LL, _P, _P, _LL, _P, _P, _LL, _I, _P] + [_I] * 13 + [_P],
     "dba_conv2_dgrad": [_P, _LL, _P, _LL, _P, _P, _LL, _P] + [_I] * 12 + [_P],
-    "dba_transpose_w": [_P, _LL, _P, _I, _I, _I, _I, _I, _P],
+    "dba_transpose_w": [_P, _LL, _P, _I, _I, _I, _I, _I, _P, _P],
     "dba_halo_conv": [_P, _LL, _P, _LL, _P, _P, _LL, _P, _P, _LL, _I, _P] + [_I] * 9 + [_P],
     "dba_colsum": [_P, _LL, _I, _P, _I, _I, _I, _P, _LL, _P],
     "dba_bn_stats": [_P, _P, _I, _I, _I, _I, _P, _P, _P, _LL, _F, _F, _P, _P, _P],
-    "dba_bn_partial_blocks": [_I, _I],
+    "dba_bn_partial_blocks": [_I, _I, _I],
     "dba_bn_apply": [_P, _P, _P, _P, _P, _LL, _P, _I, _P, _P, _I, _I, _I, _I, _P],
     "dba_bn_bwd": [_P, _P, _P, _P, _P, _P, _LL, _I, _P, _P, _LL, _P, _P, _P, _P, _I, _I, _I, _I, _P],
     "dba_bn_fold": [_P, _LL, _P, _P, _P, _P, _P, _LL, _F, _P, _P, _I, _I, _I, _P],
@@ -58,6 +58,7 @@ _SIGS = {
     "dba_weighted_sum": [_P, _LL, _P, _I, _P, _LL, _P],
     "dba_gram": [_P, _LL, _I, _I, _P, _P],
     "dba_pconv": [_P, _LL, _P, _LL, _P, _P, _LL, _P, _P, _LL, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P],
+    "dba_pwgrad": [_P, _LL, _P, _LL, _P, _LL, _P, _P, _I, _I, _I, _I, _I, _I, _P],
     "dba_dist_loss_grad": [_P, _LL, _P, _LL, _P, _LL, _I, _P, _P, _F, _P, _P],
 }
 for _name, _args in _SIGS.items():
@@ -219,15 +220,17 @@ def conv2d_dgrad(dy, w, wsel, stride, pad, in_hw, nvalid=None, out_dtype=None):
         if rc != NOT_HANDLED:
             return dx if out_dtype in (None, _BF16) else dx.to(out_dtype)
     wt = torch.empty(slots, Cin, KH, KW, Cout, dtype=_BF16, device=dy.device)
+    # slot == replica when there is no slot map: inactive replicas' slots need no transpose
+    skip = _ptr(_i32(nvalid)) if (wsel is None and nvalid is not None and slots == G) else None
     if stride == 1 and KH == KW and pad == (KH - 1) // 2:
         # stride-1 dgrad == forward conv of dY with tap-flipped, transposed weights
-        _call("dba_transpose_w", w.data_ptr(), ws, wt.data_ptr(), slots, Cout, KH * KW, Cin, 1, _stream())
+        _call("dba_transpose_w", w.data_ptr(), ws, wt.data_ptr(), slots, Cout, KH * KW, Cin, 1, skip, _stream())
         rc = _call("dba_halo_conv", dy.data_ptr(), N * Ho * Wo * Cout, wt.data_ptr(), Cin * KH * KW * Cout,
                    _ptr(_i32(wsel)), None, 0, None, dx.data_ptr(), N * H * W * Cin, 0, _ptr(_i32(nvalid)), G, N,
                    Ho, Wo, Cout, Cin, KH, KH - 1 - pad, 0, _stream())
         if rc != NOT_HANDLED:
             return dx if out_dtype in (None, _BF16) else dx.to(out_dtype)
-    _call("dba_transpose_w", w.data_ptr(), ws, wt.data_ptr(), slots, Cout, KH * KW, Cin, 0, _stream())
+    _call("dba_transpose_w", w.data_ptr(), ws, wt.data_ptr(), slots, Cout, KH * KW, Cin, 0, skip, _stream())
     args = (dy.data_ptr(), N * Ho * Wo * Cout, wt.data_ptr(), Cin * KH * KW * Cout, _ptr(_i32(wsel)), dx.data_ptr(),
             N * H * W * Cin, _ptr(_i32(nvalid)), G, N, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, _stream())
     if _call("dba_conv2_dgrad", *args) == NOT_HANDLED:
@@ -241,8 +244,14 @@ def conv2d_wgrad(dy, x, stride, pad, kh, kw, dw, dbias=None, nvalid=None):
     G, N, Ho, Wo, Cout = dy.shape
     _, _, H, W, Cin = x.shape
     assert dw.dtype == torch.float32 and _inner_contig(dw)
-    _call("dba_conv_wgrad", dy.data_ptr(), N * Ho * Wo * Cout, x.data_ptr(), N * H * W * Cin, dw.data_ptr(),
-          dw.stride(0), _ptr(_i32(nvalid)), G, N, H, W, Cin, Ho, Wo, Cout, kh, kw, stride, pad, _stream())
+    rc = NOT_HANDLED
+    if _PCONV and stride == 1 and kh == 3 and kw == 3 and pad == 1 and H == W and Ho == H:
+        # halo-tiled transposed-read wgrad (csrc/kernels/pwgrad.hip)
+        rc = _call("dba_pwgrad", dy.data_ptr(), N * Ho * Wo * Cout, x.data_ptr(), N * H * W * Cin, dw.data_ptr(),
+                   dw.stride(0), _ptr(_i32(nvalid)), _zeros(dy.device).data_ptr(), G, N, H, W, Cin, Cout, _stream())
+    if rc == NOT_HANDLED:
+        _call("dba_conv_wgrad", dy.data_ptr(), N * Ho * Wo * Cout, x.data_ptr(), N * H * W * Cin, dw.data_ptr(),
+              dw.stride(0), _ptr(_i32(nvalid)), G, N, H, W, Cin, Ho, Wo, Cout, kh, kw, stride, pad, _stream())
     if dbias is not None:
         assert dbias.dtype == torch.float32 and dbias.stride(1) == 1
         _call("dba_colsum", dy.data_ptr(), N * Ho * Wo * Cout, Ho * Wo, _ptr(_i32(nvalid)), G, N, Cout,
@@ -262,7 +271,7 @@ def bn_train(y, gamma, beta, rmean, rvar, nvalid, momentum, eps, relu, residual)
     G, N, H, W, C = y.shape
     assert C % 8 == 0
     ps = _same_stride(gamma, beta, rmean, rvar)
-    nblk = _L.dba_bn_partial_blocks(N, H * W)
+    nblk = _L.dba_bn_partial_blocks(N, H * W, C)
     part = torch.empty(G * nblk * 2 * C, dtype=torch.float32, device=y.device)
     mean = torch.empty(G, C, dtype=torch.float32, device=y.device)
     invstd = torch.empty(G, C, dtype=torch.float32, device=y.device)
@@ -281,7 +290,7 @@ def bn_train_bwd(dout, y, out, mean, invstd, gamma, nvalid, relu, dgamma, dbeta,
     G, N, H, W, C = y.shape
     ps = _same_stride(gamma)
     gs = _same_stride(dgamma, dbeta)
-    nblk = _L.dba_bn_partial_blocks(N, H * W)
+    nblk = _L.dba_bn_partial_blocks(N, H * W, C)
     part = torch.empty(G * (nblk + 1) * 2 * C, dtype=torch.float32, device=y.device)
     dy = torch.empty_like(y)
     dres = torch.empty_like(y) if want_dres else None

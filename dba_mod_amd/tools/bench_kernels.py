@@ -67,12 +67,14 @@ def main(argv=None) -> int:
             t = _time(lambda: H.conv2d_dgrad(dy, w, None, s, p, (Hh, Hh)), args.reps)
             rec[tag + "_us"] = round(t * 1e6, 1)
             rec[tag + "_tflops"] = round(flops / t / 1e12, 1)
-        H._PCONV = True
         if name.startswith("train"):
             dw = torch.zeros(G, Cout, k, k, Cin, device=dev)
-            t = _time(lambda: H.conv2d_wgrad(dy, x, s, p, k, k, dw), args.reps)
-            rec["wgrad_us"] = round(t * 1e6, 1)
-            rec["wgrad_tflops"] = round(flops / t / 1e12, 1)
+            for tag, pc in (("wgrad", True), ("wgrad_old", False)):
+                H._PCONV = pc
+                t = _time(lambda: H.conv2d_wgrad(dy, x, s, p, k, k, dw), args.reps)
+                rec[tag + "_us"] = round(t * 1e6, 1)
+                rec[tag + "_tflops"] = round(flops / t / 1e12, 1)
+        H._PCONV = True
         rows.append(rec)
         print(json.dumps(rec), flush=True)
     if args.json:
