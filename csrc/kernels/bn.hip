@@ -94,21 +94,35 @@ __global__ __launch_bounds__(256) void bn_reduce_kernel(const uint16_t* __restri
   }
 }
 
-// sums the nblk partials of (g, c) with 4 threads per channel; block = (g, 64 channels)
+// sums the nblk partials of (g, c): a block covers cpb = min(64, C) channels with 256 / cpb
+// threads per channel (all 256 threads busy for narrow layers), two independent fp64 chains
+// per thread, then an LDS reduction.  Returns with threadIdx.x < cpb holding the totals.
+__device__ __forceinline__ int bn_cpb(int C) { return C < 64 ? C : 64; }
+
 __device__ __forceinline__ void sum_partials(const float* __restrict__ part, int nblk, int C, int g, int c, bool cok,
                                              double& s0, double& s1) {
-  __shared__ double red[2][4][64];
-  const int lane_c = threadIdx.x & 63, q = threadIdx.x >> 6;
-  double a0 = 0, a1 = 0;
-  if (cok) {
-    const float* pg = part + (long long)g * nblk * 2 * C;
-    for (int b = q; b < nblk; b += 4) { a0 += pg[b * 2 * C + c]; a1 += pg[b * 2 * C + C + c]; }
+  __shared__ double red[2][256];
+  const int cpb = bn_cpb(C), tpc = 256 / cpb;
+  const int q = threadIdx.x / cpb;
+  double a0 = 0, a1 = 0, b0 = 0, b1 = 0;
+  if (cok && q < tpc) {
+    const float* pg = part + (long long)g * nblk * 2 * C + c;
+    int b = q;
+    for (; b + tpc < nblk; b += 2 * tpc) {
+      a0 += pg[(long long)b * 2 * C];
+      a1 += pg[(long long)b * 2 * C + C];
+      b0 += pg[(long long)(b + tpc) * 2 * C];
+      b1 += pg[(long long)(b + tpc) * 2 * C + C];
+    }
+    if (b < nblk) { a0 += pg[(long long)b * 2 * C]; a1 += pg[(long long)b * 2 * C + C]; }
   }
-  red[0][q][lane_c] = a0;
-  red[1][q][lane_c] = a1;
+  red[0][threadIdx.x] = a0 + b0;
+  red[1][threadIdx.x] = a1 + b1;
   __syncthreads();
-  s0 = red[0][0][lane_c] + red[0][1][lane_c] + red[0][2][lane_c] + red[0][3][lane_c];
-  s1 = red[1][0][lane_c] + red[1][1][lane_c] + red[1][2][lane_c] + red[1][3][lane_c];
+  s0 = 0; s1 = 0;
+  if ((int)threadIdx.x < cpb) {
+    for (int k = 0; k < tpc; ++k) { s0 += red[0][k * cpb + threadIdx.x]; s1 += red[1][k * cpb + threadIdx.x]; }
+  }
 }
 
 __global__ void bn_finalize_kernel(const float* __restrict__ part, int nblk, const int* __restrict__ nvalid, int N,
@@ -116,10 +130,11 @@ __global__ void bn_finalize_kernel(const float* __restrict__ part, int nblk, con
                                    float momentum, float eps, float* __restrict__ mean, float* __restrict__ invstd,
                                    int G) {
   const int g = blockIdx.y;
-  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int cpb = bn_cpb(C);
+  const int c = blockIdx.x * cpb + (int)(threadIdx.x % cpb);
   double s0, s1;
   sum_partials(part, nblk, C, g, c, c < C, s0, s1);
-  if (threadIdx.x >= 64 || c >= C) return;
+  if ((int)threadIdx.x >= cpb || c >= C) return;
   const int i = g * C + c;
   const double n = (double)valid_rows(nvalid, g, N) * HW;
   if (n <= 0) { mean[i] = 0.f; invstd[i] = 0.f; return; }
@@ -253,10 +268,11 @@ __global__ void bn_bwd_finalize_kernel(const float* __restrict__ part, int nblk,
                                        float* __restrict__ dgamma, float* __restrict__ dbeta, long long g_gstride,
                                        int G, int C) {
   const int g = blockIdx.y;
-  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int cpb = bn_cpb(C);
+  const int c = blockIdx.x * cpb + (int)(threadIdx.x % cpb);
   double s0, s1;
   sum_partials(part, nblk, C, g, c, c < C, s0, s1);
-  if (threadIdx.x >= 64 || c >= C) return;
+  if ((int)threadIdx.x >= cpb || c >= C) return;
   sums[((long long)g * 2) * C + c] = (float)s0;
   sums[((long long)g * 2 + 1) * C + c] = (float)s1;
   dbeta[(long long)g * g_gstride + c] += (float)s0;
@@ -300,7 +316,7 @@ DBA_EXPORT int dba_bn_stats(const void* y, const int* nvalid, int G, int N, int 
   const int nblk = ceil_div((long long)N * HW, rows_per_block(C));
   hipLaunchKernelGGL(bn_reduce_kernel<false>, dim3(nblk, G), dim3(256), 0, st, (const uint16_t*)y, nullptr, nullptr,
                      nullptr, nullptr, 0, nvalid, N, HW, C, part);
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3(ceil_div(C, 64), G), dim3(256), 0, st, part, nblk, nvalid, N, HW, C,
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3(ceil_div(C, C < 64 ? C : 64), G), dim3(256), 0, st, part, nblk, nvalid, N, HW, C,
                      rm, rv, s_gstride, momentum, eps, mean, invstd, G);
   DBA_LAUNCH_CHECK();
 }
@@ -324,7 +340,7 @@ DBA_EXPORT int dba_bn_bwd(const void* dout, const void* out, const void* y, cons
   float* sums = part + (long long)G * nblk * 2 * C;
   hipLaunchKernelGGL(bn_reduce_kernel<true>, dim3(nblk, G), dim3(256), 0, st, (const uint16_t*)y,
                      (const uint16_t*)dout, (const uint16_t*)out, mean, invstd, relu, nvalid, N, HW, C, part);
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(ceil_div(C, 64), G), dim3(256), 0, st, part, nblk, sums, dgamma,
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(ceil_div(C, C < 64 ? C : 64), G), dim3(256), 0, st, part, nblk, sums, dgamma,
                      dbeta, g_gstride, G, C);
   const long long n = (long long)G * N * HW * C / 8;
   hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(egrid(n)), dim3(256), 0, st, (const uint16_t*)dout,

@@ -353,12 +353,13 @@ DBA_EXPORT int dba_conv2_fwd(const void* x, long long x_gstride, const void* w, 
   return -100;
 }
 
+// accum (nullable, same layout as dx): dx = dgrad + accum (the other branch's input gradient)
 DBA_EXPORT int dba_conv2_dgrad(const void* dy, long long dy_gstride, const void* wt, long long wt_sstride,
-                               const int* wsel, void* dx, long long dx_gstride, const int* nvalid, int G, int N, int H,
-                               int W, int Cin, int Ho, int Wo, int Cout, int KH, int KW, int stride, int pad,
-                               void* stream) {
+                               const int* wsel, const void* accum, void* dx, long long dx_gstride, const int* nvalid,
+                               int G, int N, int H, int W, int Cin, int Ho, int Wo, int Cout, int KH, int KW,
+                               int stride, int pad, void* stream) {
   if (Cout % 8 != 0) return -100;
-  Igemm2Args a{(const uint16_t*)dy, dy_gstride, (const uint16_t*)wt, wt_sstride, wsel, nullptr, 0, nullptr, dx,
-               dx_gstride, nvalid, N, Ho, Wo, Cout, H, W, Cin, KH, KW, stride, pad, 0, 1};
+  Igemm2Args a{(const uint16_t*)dy, dy_gstride, (const uint16_t*)wt, wt_sstride, wsel, nullptr, 0,
+               (const uint16_t*)accum, dx, dx_gstride, nvalid, N, Ho, Wo, Cout, H, W, Cin, KH, KW, stride, pad, 0, 1};
   return dispatch2<1, uint16_t>(a, G, (hipStream_t)stream);
 }

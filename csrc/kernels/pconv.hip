@@ -15,9 +15,10 @@
 //     when its run crosses a group (client model) boundary.  The run boundaries are
 //     derived in-kernel from nvalid[] so inactive/padded replicas cost nothing and the
 //     launch is HIP-graph-capturable;
-//   * the halo (SR+2 rows x W+2 cols x C channels) of tile t+1 streams global -> LDS by
-//     LDS-DMA (global_load_lds_dwordx4, no staging registers) into the other buffer while
-//     tile t computes: one barrier per tile.  Border padding is DMA'd from a zero page;
+//   * the halo (SR+2 rows x W+2 cols x C channels) of tiles t+1, t+2 streams global -> LDS
+//     by LDS-DMA (global_load_lds_dwordx4, no staging registers) into a 3-buffer ring while
+//     tile t computes: one raw barrier per tile with a counted vmcnt, so the youngest DMA
+//     stays in flight across it.  Border padding is DMA'd from a zero page;
 //   * LDS image is unpadded (lane-linear, as LDS-DMA requires) with a 16-byte-chunk XOR
 //     swizzle applied on the SOURCE address, chosen per geometry so the 16 lanes of every
 //     ds_read_b128 lane group hit 16 distinct bank slots (see swz());
@@ -68,7 +69,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
   constexpr int KSTEPS = 9 * C / 16;
   constexpr int CSTEPS = C / 16;
   static_assert(BPX % W == 0 && NWC * 32 == COUT, "tile geometry");
-  __shared__ __attribute__((aligned(16))) uint4 lds[2][NCH * 256];
+  __shared__ __attribute__((aligned(16))) uint4 lds[3][NCH * 256];
+  // s_waitcnt immediate: vmcnt = n, expcnt / lgkmcnt = no wait (gfx9 encoding)
+  constexpr int kWaitKeep = (NCH & 15) | ((NCH >> 4) << 14) | (0x7 << 4) | (0xF << 8);
+  constexpr int kWaitAll = (0x7 << 4) | (0xF << 8);
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wc = wid % NWC, wp = wid / NWC;
@@ -91,8 +95,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
   }
 
   bf16x8_t wreg[KSTEPS];
+  float4 breg[4];                           // this lane's 16 output channels' bias
   auto load_weights = [&](int gg) {
     const int slot = a.wsel ? a.wsel[gg] : gg;
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj)
+      breg[jj] = a.bias ? *(const float4*)(a.bias + (long long)slot * a.b_sstride + wc * 32 + jj * 8 + (lane >> 5) * 4)
+                        : make_float4(0.f, 0.f, 0.f, 0.f);
     const uint16_t* __restrict__ Wp = a.w + (long long)slot * a.w_sstride;
     const int row = wc * 32 + (lane & 31);
     [[maybe_unused]] __amdgpu_buffer_rsrc_t rsrc =
@@ -140,10 +149,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
     }
   };
 
+  auto next_tile = [&](int& gg, int& tt) {
+    ++tt;
+    while (tt >= valid_rows(a.nvalid, gg, a.N) * segs) { tt = 0; ++gg; }
+  };
+  // 3-deep LDS ring: tiles v+1 and v+2 are in flight while tile v computes.  Waits are
+  // counted (vmcnt = one tile's DMA instructions) and the barrier is a raw s_barrier, so
+  // the younger tile's DMA stays in flight across it (a __syncthreads would drain it).
   load_weights(g);
   stage(g, t, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
+  int gb = g, tb = t;               // most recently staged tile
+  if (v0 + 1 < v1) {
+    next_tile(gb, tb);
+    stage(gb, tb, 1);
+    __builtin_amdgcn_s_waitcnt(kWaitKeep);
+  } else {
+    __builtin_amdgcn_s_waitcnt(kWaitAll);
+  }
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
 
   // per-lane pixel coordinates of the wave's MI fragments inside a tile
   int pr[MI], pc[MI];
@@ -160,14 +185,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
     // KSTEPS x MI fragments across the tile loop)
 #pragma unroll
     for (int i = 0; i < MI; ++i) asm volatile("" : "+v"(pr[i]), "+v"(pc[i]));
-    // next tile
-    int gn = g, tn = t + 1;
-    const bool more = v + 1 < v1;
-    if (more) {
-      while (tn >= valid_rows(a.nvalid, gn, a.N) * segs) { tn = 0; ++gn; }
-      stage(gn, tn, cur ^ 1);
+    const int n_img = t / segs, sg_img = t - n_img * segs;
+    const long long mbase = (long long)n_img * HWo + (long long)sg_img * SR * W;
+    uint16_t* __restrict__ o = a.out + (long long)g * a.out_gstride;
+    const uint16_t* __restrict__ rs = a.res ? a.res + (long long)g * a.out_gstride : nullptr;
+    uint2 rres[MI][4];
+    if (rs) {   // issued early: their latency hides under the k-loop
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj)
+          rres[i][jj] = *(const uint2*)(rs + (mbase + (wp * MI + i) * 32 + (lane & 31)) * COUT + wc * 32 + jj * 8 + hi * 4);
     }
-
     f32x16_t acc[MI];
 #pragma unroll
     for (int i = 0; i < MI; ++i)
@@ -194,29 +223,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
       __builtin_amdgcn_sched_barrier(0);
     }
 
-    // ---- epilogue: lane = pixel, 4 runs of 4 consecutive channels
+    // ---- epilogue: lane = pixel, 4 runs of 4 consecutive channels (residual loads were
+    // issued before the k-loop; bias lives in registers)
     {
-      const int n = t / segs, sg = t - n * segs;
-      const long long mbase = (long long)n * HWo + (long long)sg * SR * W;
-      uint16_t* __restrict__ o = a.out + (long long)g * a.out_gstride;
-      const uint16_t* __restrict__ rs = a.res ? a.res + (long long)g * a.out_gstride : nullptr;
-      const float* bs = a.bias ? a.bias + (long long)(a.wsel ? a.wsel[g] : g) * a.b_sstride : nullptr;
 #pragma unroll
       for (int i = 0; i < MI; ++i) {
         const long long m = mbase + (wp * MI + i) * 32 + (lane & 31);
 #pragma unroll
         for (int jj = 0; jj < 4; ++jj) {
           const int ch = wc * 32 + jj * 8 + hi * 4;
-          float v[4];
-#pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = acc[i][jj * 4 + e];
-          if (bs) {
-            const float4 bv = *(const float4*)(bs + ch);
-            v[0] += bv.x; v[1] += bv.y; v[2] += bv.z; v[3] += bv.w;
-          }
-          const long long off = m * COUT + ch;
+          float v[4] = {acc[i][jj * 4] + breg[jj].x, acc[i][jj * 4 + 1] + breg[jj].y,
+                        acc[i][jj * 4 + 2] + breg[jj].z, acc[i][jj * 4 + 3] + breg[jj].w};
           if (rs) {
-            const uint2 rv = *(const uint2*)(rs + off);
+            const uint2 rv = rres[i][jj];
             v[0] += __uint_as_float(rv.x << 16);
             v[1] += __uint_as_float(rv.x & 0xffff0000u);
             v[2] += __uint_as_float(rv.y << 16);
@@ -229,18 +248,30 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
           uint2 pk;
           pk.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
           pk.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
-          *(uint2*)(o + off) = pk;
+          *(uint2*)(o + m * COUT + ch) = pk;
         }
       }
     }
 
-    if (more) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
+    if (v + 1 < v1) {
+      asm volatile("" ::: "memory");
+      const bool has2 = v + 2 < v1;
+      if (has2) {
+        next_tile(gb, tb);
+        stage(gb, tb, cur == 0 ? 2 : cur - 1);   // buffer of tile v-1 (retired by the last barrier)
+        __builtin_amdgcn_s_waitcnt(kWaitKeep);  // tile v+1 landed; v+2 stays in flight
+      } else {
+        __builtin_amdgcn_s_waitcnt(kWaitAll);
+      }
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      int gn = g, tn = t;
+      next_tile(gn, tn);
       if (gn != g) load_weights(gn);
       g = gn;
       t = tn;
-      cur ^= 1;
+      cur = cur == 2 ? 0 : cur + 1;
     }
   }
 }

@@ -33,6 +33,7 @@ class Tape:
     def __init__(self) -> None:
         self.nodes: List[Tuple[Tuple[Tensor, ...], Tuple[Optional[Tensor], ...], Callable]] = []
         self._produced: set = set()
+        self._grads: Optional[Dict[int, Tensor]] = None
 
     def record(self, outputs: Tuple[Tensor, ...], inputs: Tuple[Optional[Tensor], ...], bwd: Callable) -> None:
         self.nodes.append((outputs, inputs, bwd))
@@ -42,8 +43,15 @@ class Tape:
     def needs_grad(self, t: Optional[Tensor]) -> bool:
         return t is not None and id(t) in self._produced
 
+    def pop_grad(self, t: Tensor) -> Optional[Tensor]:
+        """Take the gradient already accumulated for ``t`` (during backward), so a backward
+        closure can fuse it into the kernel that produces ``t``'s remaining gradient
+        (residual-branch sums land in the dgrad epilogue instead of a separate add)."""
+        return self._grads.pop(id(t), None) if self._grads is not None else None
+
     def backward(self, out: Tensor, grad: Tensor) -> None:
         grads: Dict[int, Tensor] = {id(out): grad}
+        self._grads = grads
         for outputs, inputs, bwd in reversed(self.nodes):
             gouts = [grads.pop(id(o), None) for o in outputs]
             if all(g is None for g in gouts):
@@ -56,6 +64,7 @@ class Tape:
                 grads[k] = grads[k] + gi if k in grads else gi
         self.nodes.clear()
         self._produced.clear()
+        self._grads = None
 
 
 class Ctx:
@@ -113,8 +122,11 @@ class Ctx:
                                  want_dres=residual is not None)
             dy, dres = r if residual is not None else (r, None)
             ops.conv2d_wgrad(dy, x, stride, pad, kh, kw, self.g(conv), nvalid=self.nvalid)
-            dx = (ops.conv2d_dgrad(dy, w, self.wsel, stride, pad, in_hw, nvalid=self.nvalid)
-                  if need_dx else None)
+            dx = None
+            if need_dx:
+                # the other consumer of x (shortcut branch) already delivered its gradient
+                acc = self.tape.pop_grad(x)
+                dx = ops.conv2d_dgrad(dy, w, self.wsel, stride, pad, in_hw, nvalid=self.nvalid, accum=acc)
             return dx, dres
 
         self.tape.record((out,), (x, residual), bwd)

@@ -35,7 +35,7 @@ _SIGS = {
     "dba_conv_dgrad": [_P, _LL, _P, _LL, _P, _P, _LL, _P] + [_I] * 12 + [_P],
     "dba_conv_wgrad": [_P, _LL, _P, _LL, _P, _LL, _P] + [_I] * 12 + [_P],
     "dba_conv2_fwd": [_P, _LL, _P, _LL, _P, _P, _LL, _P, _P, _LL, _I, _P] + [_I] * 13 + [_P],
-    "dba_conv2_dgrad": [_P, _LL, _P, _LL, _P, _P, _LL, _P] + [_I] * 12 + [_P],
+    "dba_conv2_dgrad": [_P, _LL, _P, _LL, _P, _P, _P, _LL, _P] + [_I] * 12 + [_P],
     "dba_transpose_w": [_P, _LL, _P, _I, _I, _I, _I, _I, _P, _P],
     "dba_halo_conv": [_P, _LL, _P, _LL, _P, _P, _LL, _P, _P, _LL, _I, _P] + [_I] * 9 + [_P],
     "dba_colsum": [_P, _LL, _I, _P, _I, _I, _I, _P, _LL, _P],
@@ -204,21 +204,28 @@ def conv2d(x, w, wsel, stride, pad, bias=None, residual=None, relu=False, nvalid
     return y
 
 
-def conv2d_dgrad(dy, w, wsel, stride, pad, in_hw, nvalid=None, out_dtype=None):
+def conv2d_dgrad(dy, w, wsel, stride, pad, in_hw, nvalid=None, out_dtype=None, accum=None):
     dy = _bf16c(dy)
     G, N, Ho, Wo, Cout = dy.shape
     w, ws = _check_w(w)
     slots, _, KH, KW, Cin = w.shape
     H, W = in_hw
     dx = torch.empty(G, N, H, W, Cin, dtype=_BF16, device=dy.device)
+    acc = _bf16c(accum) if accum is not None else None
+    if acc is not None:
+        assert acc.shape == dx.shape
+
+    def done(t):
+        return t if out_dtype in (None, _BF16) else t.to(out_dtype)
+
     if _pconv_ok(Cout, Cin, H, W, KH, KW, stride, pad):
         # stride-1 3x3 dgrad on the persistent kernel: transposed + flipped weight fragments
         # are gathered in-kernel from the forward weights (no transpose pass)
         rc = _call("dba_pconv", dy.data_ptr(), N * Ho * Wo * Cout, w.data_ptr(), ws, _ptr(_i32(wsel)), None, 0,
-                   None, dx.data_ptr(), N * H * W * Cin, _ptr(_i32(nvalid)), _zeros(dy.device).data_ptr(), G, N, H,
-                   W, Cout, Cin, 1, 0, _stream())
+                   _ptr(acc), dx.data_ptr(), N * H * W * Cin, _ptr(_i32(nvalid)), _zeros(dy.device).data_ptr(), G,
+                   N, H, W, Cout, Cin, 1, 0, _stream())
         if rc != NOT_HANDLED:
-            return dx if out_dtype in (None, _BF16) else dx.to(out_dtype)
+            return done(dx)
     wt = torch.empty(slots, Cin, KH, KW, Cout, dtype=_BF16, device=dy.device)
     # slot == replica when there is no slot map: inactive replicas' slots need no transpose
     skip = _ptr(_i32(nvalid)) if (wsel is None and nvalid is not None and slots == G) else None
@@ -226,16 +233,19 @@ def conv2d_dgrad(dy, w, wsel, stride, pad, in_hw, nvalid=None, out_dtype=None):
         # stride-1 dgrad == forward conv of dY with tap-flipped, transposed weights
         _call("dba_transpose_w", w.data_ptr(), ws, wt.data_ptr(), slots, Cout, KH * KW, Cin, 1, skip, _stream())
         rc = _call("dba_halo_conv", dy.data_ptr(), N * Ho * Wo * Cout, wt.data_ptr(), Cin * KH * KW * Cout,
-                   _ptr(_i32(wsel)), None, 0, None, dx.data_ptr(), N * H * W * Cin, 0, _ptr(_i32(nvalid)), G, N,
-                   Ho, Wo, Cout, Cin, KH, KH - 1 - pad, 0, _stream())
+                   _ptr(_i32(wsel)), None, 0, _ptr(acc), dx.data_ptr(), N * H * W * Cin, 0, _ptr(_i32(nvalid)), G,
+                   N, Ho, Wo, Cout, Cin, KH, KH - 1 - pad, 0, _stream())
         if rc != NOT_HANDLED:
-            return dx if out_dtype in (None, _BF16) else dx.to(out_dtype)
+            return done(dx)
     _call("dba_transpose_w", w.data_ptr(), ws, wt.data_ptr(), slots, Cout, KH * KW, Cin, 0, skip, _stream())
-    args = (dy.data_ptr(), N * Ho * Wo * Cout, wt.data_ptr(), Cin * KH * KW * Cout, _ptr(_i32(wsel)), dx.data_ptr(),
-            N * H * W * Cin, _ptr(_i32(nvalid)), G, N, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, _stream())
-    if _call("dba_conv2_dgrad", *args) == NOT_HANDLED:
-        _call("dba_conv_dgrad", *args)
-    return dx if out_dtype in (None, _BF16) else dx.to(out_dtype)
+    args = (dy.data_ptr(), N * Ho * Wo * Cout, wt.data_ptr(), Cin * KH * KW * Cout, _ptr(_i32(wsel)))
+    tail = (dx.data_ptr(), N * H * W * Cin, _ptr(_i32(nvalid)), G, N, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad,
+            _stream())
+    if _call("dba_conv2_dgrad", *args, _ptr(acc), *tail) == NOT_HANDLED:
+        _call("dba_conv_dgrad", *args, *tail)
+        if acc is not None:
+            dx += acc
+    return done(dx)
 
 
 def conv2d_wgrad(dy, x, stride, pad, kh, kw, dw, dbias=None, nvalid=None):

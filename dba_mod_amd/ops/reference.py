@@ -134,7 +134,8 @@ def conv2d(x: Tensor, w: Tensor, wsel: Optional[Tensor], stride: int, pad: int,
 
 def conv2d_dgrad(dy: Tensor, w: Tensor, wsel: Optional[Tensor], stride: int, pad: int,
                  in_hw: Tuple[int, int], nvalid: Optional[Tensor] = None,
-                 out_dtype: Optional[torch.dtype] = None) -> Tensor:
+                 out_dtype: Optional[torch.dtype] = None, accum: Optional[Tensor] = None) -> Tensor:
+    """dX of a conv; ``accum`` (the input's gradient from another branch) is added in."""
     G, N = dy.shape[:2]
     cin = w.shape[-1]
     outs = []
@@ -143,7 +144,10 @@ def conv2d_dgrad(dy: Tensor, w: Tensor, wsel: Optional[Tensor], stride: int, pad
         dx = torch.nn.grad.conv2d_input((N, cin, in_hw[0], in_hw[1]), wg, _nchw(dy[g].to(_cdt())),
                                         stride=stride, padding=pad)
         outs.append(_nhwc(dx))
-    return torch.stack(outs).to(out_dtype or dy.dtype)
+    dx = torch.stack(outs)
+    if accum is not None:
+        dx = dx + accum.to(dx.dtype)
+    return dx.to(out_dtype or dy.dtype)
 
 
 def conv2d_wgrad(dy: Tensor, x: Tensor, stride: int, pad: int, kh: int, kw: int,

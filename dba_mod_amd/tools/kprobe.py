@@ -1,0 +1,35 @@
+"""Runs a few conv kernels on fixed shapes (for rocprofv3 PMC counter collection)."""
+from __future__ import annotations
+
+import sys
+
+import torch
+
+from dba_mod_amd.ops import hip as H
+
+
+def main() -> int:
+    dev = torch.device("cuda")
+    which = sys.argv[1:] or ["pconv1", "pconv2", "pw2", "pw3", "pw4"]
+    torch.manual_seed(0)
+    for name in which:
+        if name.startswith("pconv"):
+            G, N, Hh, C = (17, 1024, 32, 32) if name == "pconv1" else (17, 1024, 16, 64)
+            x = torch.randn(G, N, Hh, Hh, C, device=dev).bfloat16()
+            w = (torch.randn(G, C, 3, 3, C, device=dev) * 0.05).bfloat16()
+            for _ in range(3):
+                H.conv2d(x, w, None, 1, 1, relu=True)
+        else:
+            Hh, C = {"pw1": (32, 32), "pw2": (16, 64), "pw3": (8, 128), "pw4": (4, 256)}[name]
+            G, N = 10, 64
+            x = torch.randn(G, N, Hh, Hh, C, device=dev).bfloat16()
+            dy = torch.randn(G, N, Hh, Hh, C, device=dev).bfloat16()
+            dw = torch.zeros(G, C, 3, 3, C, device=dev)
+            for _ in range(3):
+                H.conv2d_wgrad(dy, x, 1, 1, 3, 3, dw)
+    torch.cuda.synchronize()
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())

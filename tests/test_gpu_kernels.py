@@ -85,6 +85,12 @@ def test_conv_fwd_dgrad_wgrad(H, R, case):
     for g in range(G):
         n = int(nvalid[g])
         assert _rel(dx[g, :n], dxr[g, :n]) < 1e-2, f"dgrad g{g}"
+    # residual-branch gradient fused into the dgrad epilogue
+    acc = torch.randn(G, N, Hh, Ww, Cin, device=dev).bfloat16()
+    dx2 = H.conv2d_dgrad(dy, w, wsel, s, p, (Hh, Ww), nvalid=nvalid, accum=acc)
+    for g in range(G):
+        n = int(nvalid[g])
+        assert _rel(dx2[g, :n], dxr[g, :n] + acc[g, :n].float()) < 1e-2, f"dgrad+accum g{g}"
     # weight gradient (+ bias grad), accumulated into a strided flat buffer view
     P = Cout * k * k * Cin + 64
     flat = torch.zeros(G, P, device=dev)
