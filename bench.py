@@ -41,6 +41,8 @@ METRIC = "FL rounds/sec + backdoor ASR & main-task acc, ResNet-18 CIFAR-10 100 c
 # reference design, CIFAR FL throughput ≈ 0.0085 rounds/s (8-vCPU estimate;
 # the reference repo publishes no number of its own)
 BASELINE_ROUNDS_PER_S = 0.0085
+MODEL_NAMES = {"cifar": "ResNet-18 (half-width, CIFAR-10)", "tiny-imagenet-200": "ResNet-18 (Tiny-ImageNet-200)",
+               "mnist": "MnistNet (MNIST)", "loan": "LoanNet MLP (LOAN)"}
 
 
 def main() -> int:
@@ -51,15 +53,24 @@ def main() -> int:
     ap.add_argument("--config", default=os.path.join(ROOT, "configs", "cifar_params.yaml"))
     ap.add_argument("--aggregation", default=None, help="override: mean | geom_median | foolsgold")
     ap.add_argument("--cpu", action="store_true")
+    ap.add_argument("--start-epoch", type=int, default=None,
+                    help="first (warmup) round; default: first poison round - warmup")
     ap.add_argument("--set", dest="overrides", nargs="*", default=[])
     args = ap.parse_args()
 
     dctx = init_distributed(prefer_gpu=not args.cpu)
-    over = {"resumed_model": False, "start_epoch": 201, "synthetic_data": True, "save_model": False}
+    over = {"resumed_model": False, "synthetic_data": True, "save_model": False}
     if args.aggregation:
         over["aggregation_methods"] = args.aggregation
     over.update(C.parse_override(args.overrides))
     params = C.load_params(args.config, over)
+    if args.start_epoch is not None:
+        params["start_epoch"] = args.start_epoch
+    elif "start_epoch" not in over:
+        # the reference resumes from a pretrain checkpoint just before the attack window: time
+        # the window (CIFAR: warmup 201-202, timed 203-210 holds all four poison rounds)
+        poison = [e for i in range(len(params.adversary_list)) for e in params.poison_epochs_of(i)]
+        params["start_epoch"] = max(1, (min(poison) if poison else 1 + args.warmup) - args.warmup)
     tmp = tempfile.mkdtemp(prefix="dba_bench_")
     server = Server(params, dctx, write_outputs=True, folder=tmp)
     import logging
@@ -89,10 +100,11 @@ def main() -> int:
             "metric": METRIC, "value": round(rps, 4), "unit": "rounds/s", "n_gpus": dctx.world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1000.0 * elapsed / max(1, args.steps), 2),
             "higher_is_better": True, "scaling": "strong",
-            "vs_baseline": round(rps / BASELINE_ROUNDS_PER_S, 2),
+            "vs_baseline": round(rps / BASELINE_ROUNDS_PER_S, 2) if params.type == "cifar" else None,
             "dtype": "bf16" if server.dtype == torch.bfloat16 else "fp32",
-            "data": "synthetic (CIFAR-10 shapes/class sizes, random-init weights)",
-            "config": {"model": "ResNet-18 (half-width, CIFAR-10)", "global_batch": 64 * int(params["no_models"]),
+            "data": f"synthetic ({params.type} shapes/class sizes, random-init weights)",
+            "config": {"model": MODEL_NAMES.get(params.type, params.type),
+                       "global_batch": int(params["batch_size"]) * int(params["no_models"]),
                        "seq_len": None, "parallelism": f"client-dp{dctx.world}",
                        "clients_total": int(params["number_of_total_participants"]),
                        "clients_per_round": int(params["no_models"]),
@@ -102,7 +114,8 @@ def main() -> int:
             "ops_backend": ops.backend_name(dctx.device),
             "global_acc": round(float(last.get("global_acc", 0.0)), 3),
             "global_asr": round(float(last.get("global_asr", 0.0)), 3),
-            "phases_last_round_s": {k: round(v, 4) for k, v in last.get("phases", {}).items()},
+            "phases_mean_s": {k: round(sum(r.get("phases", {}).get(k, 0.0) for r in done) / max(1, len(done)), 4)
+                              for k in (done[0].get("phases", {}) if done else {})},
         }
         print(json.dumps(out), flush=True)
     shutdown(dctx)

@@ -28,6 +28,7 @@
 // into registers, so no separate transpose kernel runs.
 #include "common.hpp"
 #include <algorithm>
+#include <cstdlib>
 
 namespace {
 
@@ -292,7 +293,17 @@ int launch_pconv(const PconvArgs& a, hipStream_t st) {
   constexpr int SR = BPX / W;
   if (a.H % SR != 0) return -100;
   const long long tiles = (long long)a.G * a.N * (a.H / SR);
-  const int grid = (int)std::max(1LL, std::min(tiles, (long long)num_cus() * WPE));
+  // Bounded persistence: at least one wave of blocks per CU slot, but no block walks more than
+  // ~kTilesPerBlock tiles, so CUs turn over every few tens of microseconds.  A fully
+  // persistent grid would hold every CU's LDS for the whole launch and starve the
+  // (higher-priority) training stream that runs concurrently with evaluation.
+  static const int tpb = [] {
+    const char* e = getenv("DBA_PCONV_TPB");
+    const int v = e ? atoi(e) : 8;
+    return v > 0 ? v : 8;
+  }();
+  const long long by_turnover = (tiles + tpb - 1) / tpb;
+  const int grid = (int)std::max(1LL, std::min(tiles, std::max((long long)num_cus() * WPE, by_turnover)));
   if (a.tr)
     hipLaunchKernelGGL((pconv_kernel<C, COUT, W, MI, NWC, WPE, true>), dim3(grid), dim3(256), 0, st, a);
   else

@@ -26,6 +26,7 @@ import torch
 from .. import ops
 from ..models import program as prog
 from ..utils import native
+from ..utils.devcopy import to_device
 from .plan import EvalJob
 from .workload import Workload
 
@@ -53,7 +54,7 @@ class Evaluator:
         # only fold the snapshots the jobs use
         used = sorted({j.model for j in jobs})
         remap = {m: i for i, m in enumerate(used)}
-        sub = bank[torch.tensor(used, device=bank.device)] if len(used) != bank.shape[0] else bank
+        sub = (bank[to_device(used, bank.device, torch.int64)] if len(used) != bank.shape[0] else bank)
         folded = prog.fold_bank(wl.spec, sub, self.dtype)
         lists = {}
         for kind, idx in (("clean", wl.test_clean_idx), ("poison", wl.test_poison_idx)):
@@ -73,9 +74,11 @@ class Evaluator:
         if n_max == 0:
             return
         B = min(self.chunk, n_max)
-        wsel = torch.tensor(slots, dtype=torch.int32, device=dev)
-        trig = torch.tensor([j.trig if j.kind == "poison" else -1 for j in jobs], dtype=torch.int32, device=dev)
-        pn = torch.tensor([B if j.kind == "poison" else 0 for j in jobs], dtype=torch.int32, device=dev)
+        # every upload is pinned + async: a pageable copy here would block the host until the
+        # whole queue of this (overlapped) evaluation stream had drained
+        wsel = to_device(slots, dev, torch.int32)
+        trig = to_device([j.trig if j.kind == "poison" else -1 for j in jobs], dev, torch.int32)
+        pn = to_device([B if j.kind == "poison" else 0 for j in jobs], dev, torch.int32)
         # one upload of every chunk's index table: [n_chunks, G, B]
         n_chunks = (n_max + B - 1) // B
         table = -np.ones((n_chunks, G, B), dtype=np.int32)
@@ -87,8 +90,8 @@ class Evaluator:
             table[:, g, :] = padded.reshape(n_chunks, B)
             for c in range(n_chunks):
                 nval[c, g] = max(0, min(B, n - c * B))
-        table_d = torch.from_numpy(table).to(dev, non_blocking=True)
-        nval_d = torch.from_numpy(nval).to(dev, non_blocking=True)
+        table_d = to_device(table, dev)
+        nval_d = to_device(nval, dev)
         for c in range(n_chunks):
             idx = table_d[c]
             if wl.kind == "image":
@@ -103,4 +106,4 @@ class Evaluator:
             loss, correct, _ = ops.softmax_xent(logits, y, False, False)
             acc[:, 0] += loss.double()
             acc[:, 1] += correct.double()
-        acc[:, 2] += torch.tensor([len(a) for a in idx_lists], dtype=torch.float64, device=dev)
+        acc[:, 2] += to_device([len(a) for a in idx_lists], dev, torch.float64)

@@ -143,10 +143,11 @@ class Server:
         if p.type == C.TYPE_LOAN and p["is_poison"] and not p["baseline"] and adversarial:
             self.flush()
             pre_acc = self._loan_preeval()
-        plan = build_round_plan(p, self.wl, epoch, agents, adversarial, pre_acc)
-        costs = [c.cost for c in plan.clients]
-        owners, _ = native.lpt_assign(costs, self.d.world)
-        mine = [c for c, o in zip(plan.clients, owners) if o == self.d.rank]
+        with self.timer.phase("plan", sync=False):
+            plan = build_round_plan(p, self.wl, epoch, agents, adversarial, pre_acc)
+            costs = [c.cost for c in plan.clients]
+            owners, _ = native.lpt_assign(costs, self.d.world)
+            mine = [c for c, o in zip(plan.clients, owners) if o == self.d.rank]
         with self.timer.phase("train"):
             results = self.trainer.train(mine, self.global_state)
         with self.timer.phase("gather"):
@@ -159,6 +160,13 @@ class Server:
 
     def _launch_eval(self, pend: Dict[str, Any]) -> None:
         """Enqueue the round's evaluation on the eval stream (returns immediately)."""
+        t0 = time.perf_counter()
+        try:
+            self._launch_eval_impl(pend)
+        finally:
+            pend["phases"]["launch_eval"] = time.perf_counter() - t0
+
+    def _launch_eval_impl(self, pend: Dict[str, Any]) -> None:
         if self._eval_stream is None:
             pend["acc"] = self.evaluator.run(pend["bank"], pend["plan"].jobs, self.d.rank, self.d.world)
             return

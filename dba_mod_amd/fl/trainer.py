@@ -27,6 +27,7 @@ from .. import ops
 from ..models import program as prog
 from ..models.spec import ModelSpec
 from ..utils import native
+from ..utils.devcopy import to_device
 from .plan import ClientPlan, RoundPlan
 from .workload import Workload
 
@@ -162,7 +163,7 @@ class GroupTrainer:
         b = self._buffers(G, max_slots)
         T = max(len(c.steps) for c in clients)
         host = native.pack_steps(clients, G, self.B, T, max_slots)   # [T, D] int32 (C++ runtime)
-        sched = torch.from_numpy(host).to(self.device, non_blocking=True)
+        sched = to_device(host, self.device)
         if self.use_graph and b.graph is None:
             b._cur = sched[0]
             self._reset(b, global_state)

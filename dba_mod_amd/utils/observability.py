@@ -88,14 +88,17 @@ class PhaseTimer:
             torch.cuda.current_stream(self.device).synchronize()
 
     @contextmanager
-    def phase(self, name: str) -> Iterator[None]:
-        self._sync()
+    def phase(self, name: str, sync: bool = True) -> Iterator[None]:
+        """Time a phase; ``sync=False`` for host-only phases (no device synchronisation)."""
+        if sync:
+            self._sync()
         roctx().range_push(name)
         t0 = time.perf_counter()
         try:
             yield
         finally:
-            self._sync()
+            if sync:
+                self._sync()
             roctx().range_pop()
             self.t[name] = self.t.get(name, 0.0) + time.perf_counter() - t0
 
