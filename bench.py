@@ -9,8 +9,11 @@ poisoned epochs + model-replacement scaling), every local and global test the re
 runs (per-client clean tests, attacker poison/trigger tests, global clean + combined
 trigger + 4 per-trigger ASR tests), aggregation, CSV output.  Nothing is skipped.
 
-Rounds start at 201 (the reference resumes from a 200-round pretrain), so with the default
-``--warmup 2`` the timed window 203..210 contains all four poison rounds.
+The reference resumes every config from a pretrained checkpoint (CIFAR: round 200) that is
+not shipped; the bench builds the equivalent starting point with ``--pretrain-rounds``
+(default 20) benign FedAvg rounds before the warmup (untimed, :meth:`Server.pretrain`).
+Rounds then start at 201, so with the default ``--warmup 2`` the timed window 203..210
+contains all four poison rounds.
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
     torchrun --nproc-per-node N bench.py --gpus N ...     # one rank per GPU over RCCL
@@ -53,13 +56,17 @@ def main() -> int:
     ap.add_argument("--config", default=os.path.join(ROOT, "configs", "cifar_params.yaml"))
     ap.add_argument("--aggregation", default=None, help="override: mean | geom_median | foolsgold")
     ap.add_argument("--cpu", action="store_true")
+    ap.add_argument("--pretrain-rounds", type=int, default=20,
+                    help="benign FedAvg warm start before warmup (stand-in for the reference's "
+                         "pretrained checkpoint; untimed)")
     ap.add_argument("--start-epoch", type=int, default=None,
                     help="first (warmup) round; default: first poison round - warmup")
     ap.add_argument("--set", dest="overrides", nargs="*", default=[])
     args = ap.parse_args()
 
     dctx = init_distributed(prefer_gpu=not args.cpu)
-    over = {"resumed_model": False, "synthetic_data": True, "save_model": False}
+    over = {"resumed_model": False, "synthetic_data": True, "save_model": False,
+            "pretrain_rounds": args.pretrain_rounds}
     if args.aggregation:
         over["aggregation_methods"] = args.aggregation
     over.update(C.parse_override(args.overrides))
@@ -102,7 +109,8 @@ def main() -> int:
             "higher_is_better": True, "scaling": "strong",
             "vs_baseline": round(rps / BASELINE_ROUNDS_PER_S, 2) if params.type == "cifar" else None,
             "dtype": "bf16" if server.dtype == torch.bfloat16 else "fp32",
-            "data": f"synthetic ({params.type} shapes/class sizes, random-init weights)",
+            "data": (f"synthetic ({params.type} shapes/class sizes); random-init weights warm-started by "
+                     f"{args.pretrain_rounds} benign FedAvg rounds (untimed)"),
             "config": {"model": MODEL_NAMES.get(params.type, params.type),
                        "global_batch": int(params["batch_size"]) * int(params["no_models"]),
                        "seq_len": None, "parallelism": f"client-dp{dctx.world}",
@@ -114,6 +122,8 @@ def main() -> int:
             "ops_backend": ops.backend_name(dctx.device),
             "global_acc": round(float(last.get("global_acc", 0.0)), 3),
             "global_asr": round(float(last.get("global_asr", 0.0)), 3),
+            "rounds": [[int(r["epoch"]), round(float(r.get("global_acc", 0.0)), 2), round(float(r.get("global_asr", 0.0)), 2)]
+                       for r in done],
             "phases_mean_s": {k: round(sum(r.get("phases", {}).get(k, 0.0) for r in done) / max(1, len(done)), 4)
                               for k in (done[0].get("phases", {}) if done else {})},
         }

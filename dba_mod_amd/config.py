@@ -97,6 +97,8 @@ _DEFAULTS: Dict[str, Any] = {
     "local_eval": True,            # per-client local tests (reference behaviour)
     "graph_capture": True,         # HIP-graph the grouped training step on GPU
     "overlap_eval": True,          # evaluate round r on a side stream under round r+1's training
+    "pretrain_rounds": 0,          # benign FedAvg warm start when not resuming (Server.pretrain)
+    "pretrain_eta": 1.0,
 }
 
 # keys whose value may legitimately be a python list of ints/strings

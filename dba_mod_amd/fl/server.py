@@ -98,6 +98,8 @@ class Server:
             with open(os.path.join(self.folder, "params.yaml"), "w") as f:
                 yaml.safe_dump(params.to_plain(), f)
         self.last_round: Dict[str, Any] = {}
+        if not params["resumed_model"] and int(params["pretrain_rounds"]) > 0:
+            self.pretrain(int(params["pretrain_rounds"]), float(params["pretrain_eta"]))
 
     # ------------------------------------------------------------------ model
     def _init_model(self) -> None:
@@ -124,6 +126,33 @@ class Server:
         self.global_state = flat.to(self.device)
         if self.d.enabled:   # identical by construction; make it bit-identical anyway
             self.d.broadcast_(self.global_state, 0)
+
+    def pretrain(self, rounds: int, eta: float = 1.0) -> None:
+        """Benign FedAvg warm start: ``rounds`` clean rounds (no attackers, no evaluation,
+        no CSV rows) with server rate ``eta``.
+
+        The reference never trains from scratch: every shipped config resumes a pretrained
+        checkpoint (``resumed_model: true``, e.g. ``cifar_pretrain/...epoch_200``) whose
+        weights and BN running statistics have converged.  Those checkpoints are not in the
+        repository, so a run from random init would spend its attack window with running
+        statistics still far from the activations' (eval accuracy at chance).  This builds the
+        equivalent starting point on the configured (real or synthetic) data; the result can
+        be written with :func:`dba_mod_amd.utils.checkpoint.save_checkpoint` and resumed like a
+        reference checkpoint (``dba_mod_amd.tools.pretrain``)."""
+        if rounds <= 0:
+            return
+        p = self.params
+        saved = {k: p[k] for k in ("is_poison", "eta", "aggregation_methods")}
+        p.update({"is_poison": False, "eta": float(eta), "aggregation_methods": C.AGGR_MEAN})
+        try:
+            for e in range(1, rounds + 1):
+                self._train_half(e)
+        finally:
+            p.update(saved)
+            self.timer.reset()
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+        log.info(f"pretrained {rounds} benign rounds (eta {eta})")
 
     # ------------------------------------------------------------------ round
     # ------------------------------------------------------------------ round

@@ -147,3 +147,21 @@ def test_pipelined_rounds_match_sequential(tmp_path):
         assert a["global_acc"] == b["global_acc"] and a["global_asr"] == b["global_asr"]
     for name in ("test_result.csv", "posiontest_result.csv", "train_result.csv"):
         assert open(os.path.join(s1.folder, name)).read() == open(os.path.join(s2.folder, name)).read(), name
+
+
+def test_pretrain_tool_checkpoint_resumes(tmp_path):
+    """tools.pretrain writes a reference-layout checkpoint that resumed_model loads."""
+    from dba_mod_amd.tools import pretrain
+    out = tmp_path / "mnist_pretrain" / "model_last.pt.tar.epoch_3"
+    rc = pretrain.main(["--params", os.path.join(ROOT, "configs", "mnist_params.yaml"), "--rounds", "3", "--out",
+                        str(out), "--cpu", "--set", "synthetic_data=true", "synthetic_train_size=3000",
+                        "synthetic_test_size=300"])
+    assert rc == 0 and out.exists()
+    ck = torch.load(str(out), weights_only=True)
+    assert ck["epoch"] == 3 and "conv1.weight" in ck["state_dict"]
+    p = mnist_params(tmp_path, resumed_model=True, resumed_model_name="mnist_pretrain/model_last.pt.tar.epoch_3",
+                     synthetic_train_size=3000, synthetic_test_size=300)
+    s = Server(p, DistCtx(), write_outputs=False)
+    assert s.start_epoch == 4
+    assert torch.allclose(s.spec.view(s.global_state[None], "conv1.weight")[0].flatten()[:5].float().cpu(),
+                          ck["state_dict"]["conv1.weight"].permute(0, 2, 3, 1).flatten()[:5].float(), atol=1e-6)
