@@ -6,7 +6,7 @@
 //             pass sums them in fp64);
 //   finalize: mean, 1/std, running-stat update (unbiased var, momentum) in place in the
 //             flat replica state;
-//   apply   : y -> (y-mean)*invstd*gamma + beta (+residual) (ReLU), padded rows zeroed;
+//   apply   : y -> (y-mean)*invstd*gamma + beta (+residual) (ReLU) over the valid rows only;
 //   backward: one fused reduce (sum d, sum d*xhat with the ReLU mask recomputed from the
 //             forward output) + one fused apply that also emits the residual-branch grad.
 #include "common.hpp"
@@ -158,37 +158,30 @@ __global__ void bn_apply_kernel(const uint16_t* __restrict__ y, const float* __r
                                 const float* __restrict__ beta, long long p_gstride, const uint16_t* __restrict__ res,
                                 int relu, uint16_t* __restrict__ out, const int* __restrict__ nvalid, int G, int N,
                                 int HW, int C) {
+  // grid (blocks, G): only the replica's VALID rows are touched (inactive replicas exit at
+  // once; padded rows are never read downstream — every consumer gates on nvalid)
+  const int g = blockIdx.y;
   const int c8 = C / 8;
-  const int per = N * HW * c8;                 // < 2^31 for every model / batch size used
-  const int total = per * G;
+  const int total = valid_rows(nvalid, g, N) * HW * c8;
   const int tid0 = blockIdx.x * blockDim.x + threadIdx.x;
+  if (tid0 >= total) return;
   const int c0 = (tid0 % c8) * 8;
-  int gc = -1, nvr = 0;
   float sc[8], sh[8];
-  for (int t = tid0; t < total; t += gridDim.x * blockDim.x) {
-    const int g = t / per;
-    if (g != gc) {
-      gc = g;
-      nvr = valid_rows(nvalid, g, N) * HW;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const int c = c0 + e;
-        sc[e] = invstd[g * C + c] * gamma[(long long)g * p_gstride + c];
-        sh[e] = beta[(long long)g * p_gstride + c] - mean[g * C + c] * sc[e];
-      }
-    }
-    const int row = (t - g * per) / c8;
-    const long long o = (long long)t * 8;
-    uint4 res8 = make_uint4(0, 0, 0, 0);
-    if (row >= nvr) {
-      *(uint4*)(out + o) = res8;
-      continue;
-    }
+  for (int e = 0; e < 8; ++e) {
+    const int c = c0 + e;
+    sc[e] = invstd[g * C + c] * gamma[(long long)g * p_gstride + c];
+    sh[e] = beta[(long long)g * p_gstride + c] - mean[g * C + c] * sc[e];
+  }
+  const long long base = (long long)g * N * HW * c8;
+  for (int t = tid0; t < total; t += gridDim.x * blockDim.x) {
+    const long long o = (base + t) * 8;
     const uint4 yv = *(const uint4*)(y + o);
     const uint16_t* yp = (const uint16_t*)&yv;
     uint4 rv4 = make_uint4(0, 0, 0, 0);
     if (res) rv4 = *(const uint4*)(res + o);
     const uint16_t* rp = (const uint16_t*)&rv4;
+    uint4 res8;
     uint16_t* op = (uint16_t*)&res8;
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
@@ -208,47 +201,37 @@ __global__ void bn_bwd_apply_kernel(const uint16_t* __restrict__ dout, const uin
                                     long long p_gstride, const float* __restrict__ sums, int relu,
                                     uint16_t* __restrict__ dy, uint16_t* __restrict__ dres,
                                     const int* __restrict__ nvalid, int G, int N, int HW, int C) {
+  const int g = blockIdx.y;
   const int c8 = C / 8;
-  const int per = N * HW * c8;                 // < 2^31 for every model / batch size used
-  const int total = per * G;
+  const int nv = valid_rows(nvalid, g, N) * HW;
+  const int total = nv * c8;
   const int tid0 = blockIdx.x * blockDim.x + threadIdx.x;
+  if (tid0 >= total) return;
   const int c0 = (tid0 % c8) * 8;
-  int gc = -1, nv = 0;
+  const float n = (float)nv;
   float A[8], B[8], K[8];
-  for (int t = tid0; t < total; t += gridDim.x * blockDim.x) {
-    const int g = t / per;
-    if (g != gc) {
-      gc = g;
-      nv = valid_rows(nvalid, g, N) * HW;
-      const float n = (float)(nv > 0 ? nv : 1);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const int c = c0 + e;
-        const float is = invstd[g * C + c];
-        const float ga = gamma[(long long)g * p_gstride + c] * is;
-        const float sd = sums[((long long)g * 2) * C + c];
-        const float sdx = sums[((long long)g * 2 + 1) * C + c];
-        A[e] = ga;
-        B[e] = -ga * is * sdx / n;
-        K[e] = -ga * sd / n - B[e] * mean[g * C + c];
-      }
-    }
-    const int row = (t - g * per) / c8;
-    const long long o = (long long)t * 8;
-    uint4 z = make_uint4(0, 0, 0, 0);
-    if (row >= nv) {
-      *(uint4*)(dy + o) = z;
-      if (dres) *(uint4*)(dres + o) = z;
-      continue;
-    }
+  for (int e = 0; e < 8; ++e) {
+    const int c = c0 + e;
+    const float is = invstd[g * C + c];
+    const float ga = gamma[(long long)g * p_gstride + c] * is;
+    const float sd = sums[((long long)g * 2) * C + c];
+    const float sdx = sums[((long long)g * 2 + 1) * C + c];
+    A[e] = ga;
+    B[e] = -ga * is * sdx / n;
+    K[e] = -ga * sd / n - B[e] * mean[g * C + c];
+  }
+  const long long base = (long long)g * N * HW * c8;
+  for (int t = tid0; t < total; t += gridDim.x * blockDim.x) {
+    const long long o = (base + t) * 8;
     const uint4 dv = *(const uint4*)(dout + o);
     const uint4 yv = *(const uint4*)(y + o);
-    uint4 ov = z;
+    uint4 ov = make_uint4(0, 0, 0, 0);
     if (relu) ov = *(const uint4*)(out + o);
     const uint16_t* dp = (const uint16_t*)&dv;
     const uint16_t* yp = (const uint16_t*)&yv;
     const uint16_t* op = (const uint16_t*)&ov;
-    uint4 r1 = z, r2 = z;
+    uint4 r1, r2;
     uint16_t* p1 = (uint16_t*)&r1;
     uint16_t* p2 = (uint16_t*)&r2;
 #pragma unroll
@@ -304,6 +287,13 @@ __global__ void bn_fold_kernel(const float* __restrict__ w, long long w_sstride,
 
 int egrid(long long n) { return (int)std::max(1LL, std::min(16384LL, (n + 255) / 256)); }
 
+// per-replica grid for the row-gated elementwise passes: ~16K blocks over the launch
+dim3 ggrid(int G, int N, int HW, int C) {
+  const long long per = (long long)N * HW * (C / 8);
+  const long long cap = std::max(1LL, 16384LL / std::max(1, G));
+  return dim3((unsigned)std::max(1LL, std::min(cap, (per + 255) / 256)), G);
+}
+
 }  // namespace
 
 DBA_EXPORT int dba_bn_partial_blocks(int N, int HW, int C) { return ceil_div((long long)N * HW, rows_per_block(C)); }
@@ -324,8 +314,7 @@ DBA_EXPORT int dba_bn_stats(const void* y, const int* nvalid, int G, int N, int 
 DBA_EXPORT int dba_bn_apply(const void* y, const float* mean, const float* invstd, const float* gamma, const float* beta,
                             long long p_gstride, const void* res, int relu, void* out, const int* nvalid, int G, int N,
                             int HW, int C, void* stream) {
-  const long long n = (long long)G * N * HW * C / 8;
-  hipLaunchKernelGGL(bn_apply_kernel, dim3(egrid(n)), dim3(256), 0, (hipStream_t)stream, (const uint16_t*)y, mean,
+  hipLaunchKernelGGL(bn_apply_kernel, ggrid(G, N, HW, C), dim3(256), 0, (hipStream_t)stream, (const uint16_t*)y, mean,
                      invstd, gamma, beta, p_gstride, (const uint16_t*)res, relu, (uint16_t*)out, nvalid, G, N, HW, C);
   DBA_LAUNCH_CHECK();
 }
@@ -342,8 +331,7 @@ DBA_EXPORT int dba_bn_bwd(const void* dout, const void* out, const void* y, cons
                      (const uint16_t*)dout, (const uint16_t*)out, mean, invstd, relu, nvalid, N, HW, C, part);
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(ceil_div(C, C < 64 ? C : 64), G), dim3(256), 0, st, part, nblk, sums, dgamma,
                      dbeta, g_gstride, G, C);
-  const long long n = (long long)G * N * HW * C / 8;
-  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(egrid(n)), dim3(256), 0, st, (const uint16_t*)dout,
+  hipLaunchKernelGGL(bn_bwd_apply_kernel, ggrid(G, N, HW, C), dim3(256), 0, st, (const uint16_t*)dout,
                      (const uint16_t*)out, (const uint16_t*)y, mean, invstd, gamma, p_gstride, sums, relu,
                      (uint16_t*)dy, (uint16_t*)dres, nvalid, G, N, HW, C);
   DBA_LAUNCH_CHECK();

