@@ -262,6 +262,173 @@ __global__ void bn_bwd_finalize_kernel(const float* __restrict__ part, int nblk,
   dgamma[(long long)g * g_gstride + c] += (float)s1;
 }
 
+
+// ---------------------------------------------------------------- narrow-spatial layers
+// One block owns 8 channels of one replica for ALL of its valid rows (<= 16K rows: ResNet
+// stages 2-4 at batch 64), so statistics, finalize (running stats), and apply — or the
+// whole backward — run in ONE launch with no cross-block synchronisation.  Replaces the
+// reduce / finalize / apply chain (3 launches) where the per-launch latency, not the bytes,
+// sets the cost (a lone attacker's grouped step).
+__device__ __forceinline__ void block_sum16(float (&a)[8], float (&b)[8], float (*red)[4][8]) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    a[e] = wave_sum(a[e]);
+    b[e] = wave_sum(b[e]);
+  }
+  if (lane == 0) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { red[0][w][e] = a[e]; red[1][w][e] = b[e]; }
+  }
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(256) void bn_small_fwd_kernel(
+    const uint16_t* __restrict__ y, const int* __restrict__ nvalid, int N, int HW, int C,
+    const float* __restrict__ gamma, const float* __restrict__ beta, float* __restrict__ rm, float* __restrict__ rv,
+    long long p_gstride, float momentum, float eps, const uint16_t* __restrict__ res, int relu,
+    uint16_t* __restrict__ out, float* __restrict__ mean, float* __restrict__ invstd) {
+  __shared__ float red[2][4][8];
+  __shared__ float coef[2][8];
+  const int g = blockIdx.y, c0 = blockIdx.x * 8, tid = threadIdx.x;
+  const int R = valid_rows(nvalid, g, N) * HW;
+  if (R == 0) {
+    if (tid < 8) { mean[g * C + c0 + tid] = 0.f; invstd[g * C + c0 + tid] = 0.f; }
+    return;
+  }
+  const long long base = (long long)g * N * HW * C + c0;
+  float s0[8], s1[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { s0[e] = 0.f; s1[e] = 0.f; }
+  for (int r = tid; r < R; r += 256) {
+    const uint4 v = *(const uint4*)(y + base + (long long)r * C);
+    const uint16_t* p = (const uint16_t*)&v;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { const float x = bf2f(p[e]); s0[e] += x; s1[e] = fmaf(x, x, s1[e]); }
+  }
+  block_sum16(s0, s1, red);
+  if (tid < 8) {
+    const double S0 = (double)red[0][0][tid] + red[0][1][tid] + red[0][2][tid] + red[0][3][tid];
+    const double S1 = (double)red[1][0][tid] + red[1][1][tid] + red[1][2][tid] + red[1][3][tid];
+    const double n = (double)R;
+    const double m = S0 / n;
+    double var = S1 / n - m * m;
+    var = var > 0 ? var : 0;
+    const int c = c0 + tid;
+    const float is = (float)(1.0 / sqrt(var + (double)eps));
+    mean[g * C + c] = (float)m;
+    invstd[g * C + c] = is;
+    float* prm = rm + (long long)g * p_gstride + c;
+    float* prv = rv + (long long)g * p_gstride + c;
+    const double unb = n > 1 ? var * n / (n - 1) : var;
+    *prm = (float)((1.0 - momentum) * (*prm) + momentum * m);
+    *prv = (float)((1.0 - momentum) * (*prv) + momentum * unb);
+    const float sc = is * gamma[(long long)g * p_gstride + c];
+    coef[0][tid] = sc;
+    coef[1][tid] = beta[(long long)g * p_gstride + c] - (float)m * sc;
+  }
+  __syncthreads();
+  float sc[8], sh[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { sc[e] = coef[0][e]; sh[e] = coef[1][e]; }
+  for (int r = tid; r < R; r += 256) {
+    const long long o = base + (long long)r * C;
+    const uint4 v = *(const uint4*)(y + o);
+    const uint16_t* p = (const uint16_t*)&v;
+    uint4 rv4 = make_uint4(0, 0, 0, 0);
+    if (res) rv4 = *(const uint4*)(res + o);
+    const uint16_t* rp = (const uint16_t*)&rv4;
+    uint4 w;
+    uint16_t* op = (uint16_t*)&w;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float x = fmaf(bf2f(p[e]), sc[e], sh[e]);
+      if (res) x += bf2f(rp[e]);
+      if (relu) x = fmaxf(x, 0.f);
+      op[e] = f2bf(x);
+    }
+    *(uint4*)(out + o) = w;
+  }
+}
+
+__global__ __launch_bounds__(256) void bn_small_bwd_kernel(
+    const uint16_t* __restrict__ dout, const uint16_t* __restrict__ out, const uint16_t* __restrict__ y,
+    const float* __restrict__ mean, const float* __restrict__ invstd, const float* __restrict__ gamma,
+    long long p_gstride, int relu, float* __restrict__ dgamma, float* __restrict__ dbeta, long long g_gstride,
+    uint16_t* __restrict__ dy, uint16_t* __restrict__ dres, const int* __restrict__ nvalid, int N, int HW, int C) {
+  __shared__ float red[2][4][8];
+  __shared__ float coef[3][8];
+  const int g = blockIdx.y, c0 = blockIdx.x * 8, tid = threadIdx.x;
+  const int R = valid_rows(nvalid, g, N) * HW;
+  if (R == 0) return;
+  const long long base = (long long)g * N * HW * C + c0;
+  float mu[8], is[8], s0[8], s1[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    mu[e] = mean[g * C + c0 + e];
+    is[e] = invstd[g * C + c0 + e];
+    s0[e] = 0.f;
+    s1[e] = 0.f;
+  }
+  for (int r = tid; r < R; r += 256) {
+    const long long o = base + (long long)r * C;
+    const uint4 dv = *(const uint4*)(dout + o);
+    const uint4 yv = *(const uint4*)(y + o);
+    uint4 ov = make_uint4(0, 0, 0, 0);
+    if (relu) ov = *(const uint4*)(out + o);
+    const uint16_t* dp = (const uint16_t*)&dv;
+    const uint16_t* yp = (const uint16_t*)&yv;
+    const uint16_t* op = (const uint16_t*)&ov;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float d = bf2f(dp[e]);
+      if (relu && !(bf2f(op[e]) > 0.f)) d = 0.f;
+      s0[e] += d;
+      s1[e] = fmaf(d, (bf2f(yp[e]) - mu[e]) * is[e], s1[e]);
+    }
+  }
+  block_sum16(s0, s1, red);
+  if (tid < 8) {
+    const float sd = red[0][0][tid] + red[0][1][tid] + red[0][2][tid] + red[0][3][tid];
+    const float sdx = red[1][0][tid] + red[1][1][tid] + red[1][2][tid] + red[1][3][tid];
+    const int c = c0 + tid;
+    dbeta[(long long)g * g_gstride + c] += sd;
+    dgamma[(long long)g * g_gstride + c] += sdx;
+    const float n = (float)R;
+    const float ga = gamma[(long long)g * p_gstride + c] * is[tid];
+    const float B = -ga * is[tid] * sdx / n;
+    coef[0][tid] = ga;
+    coef[1][tid] = B;
+    coef[2][tid] = -ga * sd / n - B * mu[tid];
+  }
+  __syncthreads();
+  float A[8], B[8], K[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { A[e] = coef[0][e]; B[e] = coef[1][e]; K[e] = coef[2][e]; }
+  for (int r = tid; r < R; r += 256) {
+    const long long o = base + (long long)r * C;
+    const uint4 dv = *(const uint4*)(dout + o);
+    const uint4 yv = *(const uint4*)(y + o);
+    uint4 ov = make_uint4(0, 0, 0, 0);
+    if (relu) ov = *(const uint4*)(out + o);
+    const uint16_t* dp = (const uint16_t*)&dv;
+    const uint16_t* yp = (const uint16_t*)&yv;
+    const uint16_t* op = (const uint16_t*)&ov;
+    uint4 r1, r2;
+    uint16_t* p1 = (uint16_t*)&r1;
+    uint16_t* p2 = (uint16_t*)&r2;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float d = bf2f(dp[e]);
+      if (relu && !(bf2f(op[e]) > 0.f)) d = 0.f;
+      p1[e] = f2bf(fmaf(A[e], d, fmaf(B[e], bf2f(yp[e]), K[e])));
+      p2[e] = f2bf(d);
+    }
+    *(uint4*)(dy + o) = r1;
+    if (dres) *(uint4*)(dres + o) = r2;
+  }
+}
+
 // eval fold: wf[s][co][k] = w[s][co][k] * s_c ; bf[s][co] = (b0 - rm) * s_c + beta
 __global__ void bn_fold_kernel(const float* __restrict__ w, long long w_sstride, const float* __restrict__ cbias,
                                const float* __restrict__ gamma, const float* __restrict__ beta,
@@ -334,6 +501,28 @@ DBA_EXPORT int dba_bn_bwd(const void* dout, const void* out, const void* y, cons
   hipLaunchKernelGGL(bn_bwd_apply_kernel, ggrid(G, N, HW, C), dim3(256), 0, st, (const uint16_t*)dout,
                      (const uint16_t*)out, (const uint16_t*)y, mean, invstd, gamma, p_gstride, sums, relu,
                      (uint16_t*)dy, (uint16_t*)dres, nvalid, G, N, HW, C);
+  DBA_LAUNCH_CHECK();
+}
+
+// single-launch BN forward for rows-per-replica <= 16384 (see bn_small_fwd_kernel)
+DBA_EXPORT int dba_bn_small_fwd(const void* y, const int* nvalid, int G, int N, int HW, int C, const float* gamma,
+                                const float* beta, float* rm, float* rv, long long p_gstride, float momentum, float eps,
+                                const void* res, int relu, void* out, float* mean, float* invstd, void* stream) {
+  if (C % 8 != 0) return -100;
+  hipLaunchKernelGGL(bn_small_fwd_kernel, dim3(C / 8, G), dim3(256), 0, (hipStream_t)stream, (const uint16_t*)y,
+                     nvalid, N, HW, C, gamma, beta, rm, rv, p_gstride, momentum, eps, (const uint16_t*)res, relu,
+                     (uint16_t*)out, mean, invstd);
+  DBA_LAUNCH_CHECK();
+}
+
+DBA_EXPORT int dba_bn_small_bwd(const void* dout, const void* out, const void* y, const float* mean,
+                                const float* invstd, const float* gamma, long long p_gstride, int relu, float* dgamma,
+                                float* dbeta, long long g_gstride, void* dy, void* dres, const int* nvalid, int G,
+                                int N, int HW, int C, void* stream) {
+  if (C % 8 != 0) return -100;
+  hipLaunchKernelGGL(bn_small_bwd_kernel, dim3(C / 8, G), dim3(256), 0, (hipStream_t)stream,
+                     (const uint16_t*)dout, (const uint16_t*)out, (const uint16_t*)y, mean, invstd, gamma, p_gstride,
+                     relu, dgamma, dbeta, g_gstride, (uint16_t*)dy, (uint16_t*)dres, nvalid, N, HW, C);
   DBA_LAUNCH_CHECK();
 }
 

@@ -19,6 +19,7 @@
 namespace {
 
 constexpr int BK2 = 64;
+typedef short v4i16_t __attribute__((ext_vector_type(4)));
 constexpr int LP = BK2 + 8;   // u16 per LDS row (144 B)
 
 struct Igemm2Args {
@@ -52,19 +53,29 @@ __device__ __forceinline__ bool src_pos2(const Igemm2Args& a, int p, int q, int 
   }
 }
 
-template <int BM, int BN, int WM, int WN, int MODE, typename OutT>
+// BT: the B operand is read straight from the FORWARD weight tensor [Co][T][Ci] in its
+// natural K-major order (k = tap*Co + co rows, Ci columns; tap-flipped when MODE == 0, i.e.
+// a stride-1 data gradient run as a forward conv) and consumed with ds_read_b64_tr_b16
+// transposed reads — no separate weight-transpose pass.  B LDS rows are padded by 64 B so
+// the 4 rows of a transposed read hit distinct banks.
+template <int BM, int BN, int WM, int WN, int MODE, typename OutT, bool BT = false>
 __global__ __launch_bounds__(256) void igemm2_kernel(Igemm2Args a) {
   constexpr int TM = BM / WM, TN = BN / WN;          // wave tile
   constexpr int MI = TM / 32, NJ = TN / 32;          // 32x32 MFMA tiles per wave
   constexpr int RA = BM * 8 / 256;                   // A 16-B loads per thread per k-step
   constexpr int RB = (BN * 8 + 255) / 256;           // B 16-B loads per thread
+  // BT: u16 per B row (k-major), padded so the row pitch is 16 dwords mod 64: the 4 rows of a
+  // transposed read (64 B of columns each per 32-lane half) land on distinct banks
+  constexpr int LPT = BN + 2 * ((16 - BN / 2) & 63);
   static_assert(WM * WN == 4, "4 waves");
   static_assert(MI >= 1 && NJ >= 1, "wave tile >= 32x32");
-  constexpr int LDS_AB = 2 * (BM + BN) * LP;         // u16
+  constexpr int LDS_B = BT ? BK2 * LPT : BN * LP;    // u16 per B buffer
+  constexpr int LDS_AB = 2 * (BM * LP + LDS_B);      // u16
   constexpr int LDS_C = BM * BN * 2;                  // u16 (fp32 staging)
   __shared__ __attribute__((aligned(16))) uint16_t smem[LDS_AB > LDS_C ? LDS_AB : LDS_C];
   uint16_t (*As)[BM][LP] = reinterpret_cast<uint16_t (*)[BM][LP]>(smem);
   uint16_t (*Bs)[BN][LP] = reinterpret_cast<uint16_t (*)[BN][LP]>(smem + 2 * BM * LP);
+  uint16_t (*Bt)[BK2][LPT] = reinterpret_cast<uint16_t (*)[BK2][LPT]>(smem + 2 * BM * LP);
 
   const int g = blockIdx.y;
   const int HoWo = a.Ho * a.Wo;
@@ -110,20 +121,56 @@ __global__ __launch_bounds__(256) void igemm2_kernel(Igemm2Args a) {
       if (kin && rbase[i] >= 0 && src_pos2<MODE>(a, rp[i], rq[i], kh, kw, hs, ws))
         ra[i] = *(const uint4*)(src + (((long long)rbase[i] * a.Hs + hs) * a.Ws + ws) * a.Cs + c);
     }
+    if constexpr (!BT) {
 #pragma unroll
-    for (int i = 0; i < RB; ++i) {
-      const int r = (tid >> 3) + 32 * i;
-      rb[i] = make_uint4(0, 0, 0, 0);
-      if (r < BN && kin && n0 + r < a.Ncol) rb[i] = *(const uint4*)(Wp + (long long)(n0 + r) * K + k);
+      for (int i = 0; i < RB; ++i) {
+        const int r = (tid >> 3) + 32 * i;
+        rb[i] = make_uint4(0, 0, 0, 0);
+        if (r < BN && kin && n0 + r < a.Ncol) rb[i] = *(const uint4*)(Wp + (long long)(n0 + r) * K + k);
+      }
+    } else {
+      // B^T tile [BK2 rows k][BN cols n], 16-B chunks along n: k -> (tap, co) of the source
+      // channel axis; element = W[co][tap'][n] with tap' = T-1-tap for the flipped (MODE 0) form
+      constexpr int CPR = BN / 8;                    // chunks per B row
+#pragma unroll
+      for (int i = 0; i < RB; ++i) {
+        const int e = tid + 256 * i;
+        const int kr = e / CPR, cn = (e - kr * CPR) * 8;
+        const int kg = kc * BK2 + kr;
+        rb[i] = make_uint4(0, 0, 0, 0);
+        if (kr < BK2 && kg < K && n0 + cn < a.Ncol) {
+          const int T = a.KH * a.KW;
+          int tap, co;
+          if (a.Cs % BK2 == 0) {          // one tap per k-step: hoistable, no per-row division
+            tap = (kc * BK2) / a.Cs;
+            co = kc * BK2 - tap * a.Cs + kr;
+          } else {
+            tap = kg / a.Cs;
+            co = kg - tap * a.Cs;
+          }
+          const int tsrc = MODE == 0 ? T - 1 - tap : tap;
+          rb[i] = *(const uint4*)(Wp + ((long long)co * T + tsrc) * a.Ncol + n0 + cn);
+        }
+      }
     }
   };
   auto store_tiles = [&](int buf) {
 #pragma unroll
     for (int i = 0; i < RA; ++i) *(uint4*)&As[buf][(tid >> 3) + 32 * i][seg * 8] = ra[i];
+    if constexpr (!BT) {
 #pragma unroll
-    for (int i = 0; i < RB; ++i) {
-      const int r = (tid >> 3) + 32 * i;
-      if (r < BN) *(uint4*)&Bs[buf][r][seg * 8] = rb[i];
+      for (int i = 0; i < RB; ++i) {
+        const int r = (tid >> 3) + 32 * i;
+        if (r < BN) *(uint4*)&Bs[buf][r][seg * 8] = rb[i];
+      }
+    } else {
+      constexpr int CPR = BN / 8;
+#pragma unroll
+      for (int i = 0; i < RB; ++i) {
+        const int e = tid + 256 * i;
+        const int kr = e / CPR, cn = (e - kr * CPR) * 8;
+        if (kr < BK2) *(uint4*)&Bt[buf][kr][cn] = rb[i];
+      }
     }
   };
 
@@ -147,8 +194,23 @@ __global__ __launch_bounds__(256) void igemm2_kernel(Igemm2Args a) {
       bf16x8_t af[MI], bfr[NJ];
 #pragma unroll
       for (int i = 0; i < MI; ++i) af[i] = *(const bf16x8_t*)&As[cur][wm * TM + i * 32 + fr][kk + fk];
+      if constexpr (!BT) {
 #pragma unroll
-      for (int j = 0; j < NJ; ++j) bfr[j] = *(const bf16x8_t*)&Bs[cur][wn * TN + j * 32 + fr][kk + fk];
+        for (int j = 0; j < NJ; ++j) bfr[j] = *(const bf16x8_t*)&Bs[cur][wn * TN + j * 32 + fr][kk + fk];
+      } else {
+        // transposed read (T10): lane 4q+p of 16-lane group G4 addresses row k = kk+8h+4t+q,
+        // columns 16*(G4&1)+4p..+3; lane i of the group receives column i, rows in elements
+        const int G4 = lane >> 4, q = (lane >> 2) & 3, p4 = lane & 3;
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          union { bf16x8_t v; v4i16_t h[2]; } u;
+#pragma unroll
+          for (int t2 = 0; t2 < 2; ++t2)
+            u.h[t2] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4i16_t*)
+                &Bt[cur][kk + 8 * (G4 >> 1) + 4 * t2 + q][wn * TN + j * 32 + 16 * (G4 & 1) + 4 * p4]);
+          bfr[j] = u.v;
+        }
+      }
 #pragma unroll
       for (int i = 0; i < MI; ++i)
 #pragma unroll
@@ -306,23 +368,23 @@ __global__ __launch_bounds__(256) void igemm_small_kernel(Igemm2Args a) {
     }
 }
 
-template <int BM, int BN, int WM, int WN, int MODE, typename OutT>
+template <int BM, int BN, int WM, int WN, int MODE, typename OutT, bool BT = false>
 int launch2(Igemm2Args a, int G, hipStream_t st) {
   const int M = a.N * a.Ho * a.Wo;
   a.tiles_n = ceil_div(a.Ncol, BN);
   dim3 grid((unsigned)(ceil_div(M, BM) * a.tiles_n), G);
-  hipLaunchKernelGGL((igemm2_kernel<BM, BN, WM, WN, MODE, OutT>), grid, dim3(256), 0, st, a);
+  hipLaunchKernelGGL((igemm2_kernel<BM, BN, WM, WN, MODE, OutT, BT>), grid, dim3(256), 0, st, a);
   DBA_LAUNCH_CHECK();
 }
 
-template <int MODE, typename OutT>
+template <int MODE, typename OutT, bool BT = false>
 int dispatch2(Igemm2Args a, int G, hipStream_t st) {
   const long long M = (long long)a.N * a.Ho * a.Wo;
-  if (a.Ncol <= 32) return launch2<128, 32, 4, 1, MODE, OutT>(a, G, st);
-  if (a.Ncol <= 64) return launch2<128, 64, 2, 2, MODE, OutT>(a, G, st);
+  if (a.Ncol <= 32) return launch2<128, 32, 4, 1, MODE, OutT, BT>(a, G, st);
+  if (a.Ncol <= 64) return launch2<128, 64, 2, 2, MODE, OutT, BT>(a, G, st);
   // wide outputs: 128x128 tiles unless the launch would not fill the chip
-  if (M * G / 128 * ((a.Ncol + 127) / 128) >= 512) return launch2<128, 128, 2, 2, MODE, OutT>(a, G, st);
-  return launch2<64, 128, 1, 4, MODE, OutT>(a, G, st);
+  if (M * G / 128 * ((a.Ncol + 127) / 128) >= 512) return launch2<128, 128, 2, 2, MODE, OutT, BT>(a, G, st);
+  return launch2<64, 128, 1, 4, MODE, OutT, BT>(a, G, st);
 }
 
 }  // namespace
@@ -351,6 +413,26 @@ DBA_EXPORT int dba_conv2_fwd(const void* x, long long x_gstride, const void* w, 
     DBA_LAUNCH_CHECK();
   }
   return -100;
+}
+
+// Data gradient straight from the FORWARD weights w [slots][Cout][KH][KW][Cin] (no transpose
+// pass): stride 1 (pad = (K-1)/2) runs as a forward conv of dY with tap-flipped weights
+// (MODE 0), other strides as the scatter-form implicit GEMM (MODE 1).  accum as below.
+DBA_EXPORT int dba_conv2_dgrad_w(const void* dy, long long dy_gstride, const void* w, long long w_sstride,
+                                 const int* wsel, const void* accum, void* dx, long long dx_gstride,
+                                 const int* nvalid, int G, int N, int H, int W, int Cin, int Ho, int Wo, int Cout,
+                                 int KH, int KW, int stride, int pad, void* stream) {
+  if (Cout % 8 != 0 || Cin % 8 != 0) return -100;
+  hipStream_t st = (hipStream_t)stream;
+  if (stride == 1 && KH == KW && pad == (KH - 1) / 2) {
+    Igemm2Args a{(const uint16_t*)dy, dy_gstride, (const uint16_t*)w, w_sstride, wsel, nullptr, 0,
+                 (const uint16_t*)accum, dx, dx_gstride, nvalid, N, Ho, Wo, Cout, H, W, Cin, KH, KW, 1, KH - 1 - pad,
+                 0, 1};
+    return dispatch2<0, uint16_t, true>(a, G, st);
+  }
+  Igemm2Args a{(const uint16_t*)dy, dy_gstride, (const uint16_t*)w, w_sstride, wsel, nullptr, 0,
+               (const uint16_t*)accum, dx, dx_gstride, nvalid, N, Ho, Wo, Cout, H, W, Cin, KH, KW, stride, pad, 0, 1};
+  return dispatch2<1, uint16_t, true>(a, G, st);
 }
 
 // accum (nullable, same layout as dx): dx = dgrad + accum (the other branch's input gradient)

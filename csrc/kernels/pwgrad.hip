@@ -31,8 +31,23 @@ struct PwArgs {
   const int* nvalid;
   const uint16_t* zeros;
   int N, H, Cout, Cin;
-  int atomic;                                   // split-K over pixel runs (> 1 block per output)
+  int G, slices, ncu;                           // launch geometry for the in-kernel split-K choice
 };
+
+// Split-K factor S (pixel runs per output slice), chosen IN-KERNEL from the number of
+// replicas active this step (the launch is captured once in a HIP graph for all G): enough
+// blocks to cover the CUs, but the S x |dW| fp32 atomics (~1.3 TB/s chip-wide) must not
+// outweigh the MFMA work.  A lone attacker finishing its poison epochs gets ~10x the blocks
+// of a step where all G clients train.
+__device__ __forceinline__ int split_k(const PwArgs& a, int tiles) {
+  int active = 0;
+  for (int g = 0; g < a.G; ++g) active += valid_rows(a.nvalid, g, a.N) > 0;
+  active = active > 0 ? active : 1;
+  const float by_cus = (float)a.ncu / (float)(active * a.slices);
+  const float by_atomics = 3.0e6f / ((float)active * a.Cout * a.Cin * 9);
+  const int S = (int)fminf(by_cus, by_atomics);
+  return max(1, min(min(tiles, (int)gridDim.x), S));
+}
 
 template <int CH>
 __device__ __forceinline__ int swz_px(int px) {   // chunk XOR for a CH-channel image row
@@ -78,9 +93,13 @@ __global__ __launch_bounds__((CO / 32) * (CI / 32) * 3 * WK * 64) void pwgrad_ke
   const int segs = a.H / SR;
   const int nimg = valid_rows(a.nvalid, g, a.N);
   const int T = NIMG == 1 ? nimg * segs : (nimg + NIMG - 1) / NIMG;
-  const int per = (T + gridDim.x - 1) / gridDim.x;
+  if (T == 0) return;
+  const int S = split_k(a, NIMG == 1 ? a.N * segs : (a.N + NIMG - 1) / NIMG);
+  if ((int)blockIdx.x >= S) return;
+  const int per = (T + S - 1) / S;
   const int t0 = blockIdx.x * per, t1 = min(T, t0 + per);
   if (t0 >= t1) return;
+  const bool atomic = S > 1;
   const int HW = a.H * W;
   const uint16_t* __restrict__ dyg = a.dy + (long long)g * a.dy_gstride;
   const uint16_t* __restrict__ xg = a.x + (long long)g * a.x_gstride;
@@ -206,7 +225,7 @@ __global__ __launch_bounds__((CO / 32) * (CI / 32) * 3 * WK * 64) void pwgrad_ke
     for (int r = 0; r < 16; ++r) {
       const int co = co0 + wco * 32 + 8 * (r >> 2) + 4 * (lane >> 5) + (r & 3);
       float* d = dwg + ((long long)(co * 3 + kh) * 3 + kw) * a.Cin + ci;
-      if (a.atomic) atomicAdd(d, acc[kw][r]);
+      if (atomic) atomicAdd(d, acc[kw][r]);
       else *d += acc[kw][r];                      // sole writer of this element
     }
 }
@@ -226,14 +245,14 @@ int launch_pw(const PwArgs& a, int G, hipStream_t st) {
   if (a.H % SR != 0 || a.Cout % CO != 0 || a.Cin % CI != 0 || (NIMG > 1 && SR != a.H)) return -100;
   const int slices = (a.Cout / CO) * (a.Cin / CI);
   const int tiles = NIMG == 1 ? a.N * (a.H / SR) : (a.N + NIMG - 1) / NIMG;
-  // split-K factor S (pixel runs per output slice): enough blocks to cover the CUs, but the
-  // S x |dW| fp32 atomics (~1.3 TB/s chip-wide) must not outweigh the MFMA work
-  const double by_cus = (double)num_cus_w() / std::max(1, G * slices);
-  const double by_atomics = 3.0e6 / ((double)G * a.Cout * a.Cin * 9);
-  const int S = std::max(1, std::min(tiles, (int)std::min(by_cus, by_atomics)));
   PwArgs b = a;
-  b.atomic = S > 1;
-  dim3 grid(S, G, slices);
+  b.G = G;
+  b.slices = slices;
+  b.ncu = num_cus_w();
+  // grid.x = the largest split any activity pattern can ask for (one active replica)
+  const double s1 = std::min((double)b.ncu / slices, 3.0e6 / ((double)a.Cout * a.Cin * 9));
+  const int smax = std::max(1, std::min(tiles, (int)s1));
+  dim3 grid(smax, G, slices);
   hipLaunchKernelGGL((pwgrad_kernel<CO, CI, W, SR, NIMG, WK>), grid, dim3((CO / 32) * (CI / 32) * 3 * WK * 64), 0,
                      st, b);
   DBA_LAUNCH_CHECK();
@@ -246,7 +265,7 @@ DBA_EXPORT int dba_pwgrad(const void* dy, long long dy_gstride, const void* x, l
                           long long dw_gstride, const int* nvalid, const void* zeros, int G, int N, int H, int W,
                           int Cin, int Cout, void* stream) {
   PwArgs a{(const uint16_t*)dy, dy_gstride, (const uint16_t*)x, x_gstride, dw, dw_gstride, nvalid,
-           (const uint16_t*)zeros, N, H, Cout, Cin, 1};
+           (const uint16_t*)zeros, N, H, Cout, Cin, G, 1, 256};
   hipStream_t st = (hipStream_t)stream;
   if (Cin == 32 && Cout == 32 && W == 32) return launch_pw<32, 32, 32, 8, 1, 2>(a, G, st);
   if (Cin % 64 == 0 && Cout % 64 == 0) {

@@ -35,6 +35,7 @@ _SIGS = {
     "dba_conv_dgrad": [_P, _LL, _P, _LL, _P, _P, _LL, _P] + [_I] * 12 + [_P],
     "dba_conv_wgrad": [_P, _LL, _P, _LL, _P, _LL, _P] + [_I] * 12 + [_P],
     "dba_conv2_fwd": [_P, _LL, _P, _LL, _P, _P, _LL, _P, _P, _LL, _I, _P] + [_I] * 13 + [_P],
+    "dba_conv2_dgrad_w": [_P, _LL, _P, _LL, _P, _P, _P, _LL, _P] + [_I] * 12 + [_P],
     "dba_conv2_dgrad": [_P, _LL, _P, _LL, _P, _P, _P, _LL, _P] + [_I] * 12 + [_P],
     "dba_transpose_w": [_P, _LL, _P, _I, _I, _I, _I, _I, _P, _P],
     "dba_halo_conv": [_P, _LL, _P, _LL, _P, _P, _LL, _P, _P, _LL, _I, _P] + [_I] * 9 + [_P],
@@ -43,6 +44,8 @@ _SIGS = {
     "dba_bn_partial_blocks": [_I, _I, _I],
     "dba_bn_apply": [_P, _P, _P, _P, _P, _LL, _P, _I, _P, _P, _I, _I, _I, _I, _P],
     "dba_bn_bwd": [_P, _P, _P, _P, _P, _P, _LL, _I, _P, _P, _LL, _P, _P, _P, _P, _I, _I, _I, _I, _P],
+    "dba_bn_small_fwd": [_P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _LL, _F, _F, _P, _I, _P, _P, _P, _P],
+    "dba_bn_small_bwd": [_P, _P, _P, _P, _P, _P, _LL, _I, _P, _P, _LL, _P, _P, _P, _I, _I, _I, _I, _P],
     "dba_bn_fold": [_P, _LL, _P, _P, _P, _P, _P, _LL, _F, _P, _P, _I, _I, _I, _P],
     "dba_relu_mask_bwd": [_P, _P, _P, _LL, _P],
     "dba_maxpool": [_P, _P, _P, _LL, _I, _I, _I, _I, _I, _I, _I, _I, _P],
@@ -147,6 +150,7 @@ def _check_w(w: Tensor) -> Tuple[Tensor, int]:
 
 
 _PCONV = os.environ.get("DBA_PCONV", "1") != "0"
+_DGRAD_W = os.environ.get("DBA_DGRAD_W", "0") == "1"
 _PCONV_SHAPES = {(32, 32, 32), (64, 64, 16)}     # (Cin, Cout, W): see csrc/kernels/pconv.hip
 _ZEROS = {}
 
@@ -226,6 +230,14 @@ def conv2d_dgrad(dy, w, wsel, stride, pad, in_hw, nvalid=None, out_dtype=None, a
                    N, H, W, Cout, Cin, 1, 0, _stream())
         if rc != NOT_HANDLED:
             return done(dx)
+    if _DGRAD_W:
+        # implicit GEMM reading the forward weights K-major with transposed LDS reads
+        # (experimental: measured slower than transpose + gen-2 GEMM on the ResNet shapes)
+        rc = _call("dba_conv2_dgrad_w", dy.data_ptr(), N * Ho * Wo * Cout, w.data_ptr(), ws, _ptr(_i32(wsel)),
+                   _ptr(acc), dx.data_ptr(), N * H * W * Cin, _ptr(_i32(nvalid)), G, N, H, W, Cin, Ho, Wo, Cout, KH,
+                   KW, stride, pad, _stream())
+        if rc != NOT_HANDLED:
+            return done(dx)
     wt = torch.empty(slots, Cin, KH, KW, Cout, dtype=_BF16, device=dy.device)
     # slot == replica when there is no slot map: inactive replicas' slots need no transpose
     skip = _ptr(_i32(nvalid)) if (wsel is None and nvalid is not None and slots == G) else None
@@ -276,20 +288,30 @@ def _same_stride(*ts: Tensor) -> int:
     return s
 
 
+# rows per replica up to which BN runs as one launch (bn_small_*: ResNet stage 4 at batch 64)
+_BN_SMALL_ROWS = int(os.environ.get("DBA_BN_SMALL_ROWS", "1024"))
+
+
 def bn_train(y, gamma, beta, rmean, rvar, nvalid, momentum, eps, relu, residual):
     y = _bf16c(y)
     G, N, H, W, C = y.shape
     assert C % 8 == 0
     ps = _same_stride(gamma, beta, rmean, rvar)
-    nblk = _L.dba_bn_partial_blocks(N, H * W, C)
-    part = torch.empty(G * nblk * 2 * C, dtype=torch.float32, device=y.device)
     mean = torch.empty(G, C, dtype=torch.float32, device=y.device)
     invstd = torch.empty(G, C, dtype=torch.float32, device=y.device)
     nv = _ptr(_i32(nvalid))
-    _call("dba_bn_stats", y.data_ptr(), nv, G, N, H * W, C, part.data_ptr(), rmean.data_ptr(), rvar.data_ptr(), ps,
-          float(momentum), float(eps), mean.data_ptr(), invstd.data_ptr(), _stream())
     out = torch.empty_like(y)
     res = _bf16c(residual) if residual is not None else None
+    if N * H * W <= _BN_SMALL_ROWS:
+        # one launch: a block owns 8 channels of a replica for all its rows
+        _call("dba_bn_small_fwd", y.data_ptr(), nv, G, N, H * W, C, gamma.data_ptr(), beta.data_ptr(),
+              rmean.data_ptr(), rvar.data_ptr(), ps, float(momentum), float(eps), _ptr(res), int(relu),
+              out.data_ptr(), mean.data_ptr(), invstd.data_ptr(), _stream())
+        return out, mean, invstd
+    nblk = _L.dba_bn_partial_blocks(N, H * W, C)
+    part = torch.empty(G * nblk * 2 * C, dtype=torch.float32, device=y.device)
+    _call("dba_bn_stats", y.data_ptr(), nv, G, N, H * W, C, part.data_ptr(), rmean.data_ptr(), rvar.data_ptr(), ps,
+          float(momentum), float(eps), mean.data_ptr(), invstd.data_ptr(), _stream())
     _call("dba_bn_apply", y.data_ptr(), mean.data_ptr(), invstd.data_ptr(), gamma.data_ptr(), beta.data_ptr(), ps,
           _ptr(res), int(relu), out.data_ptr(), nv, G, N, H * W, C, _stream())
     return out, mean, invstd
@@ -300,10 +322,15 @@ def bn_train_bwd(dout, y, out, mean, invstd, gamma, nvalid, relu, dgamma, dbeta,
     G, N, H, W, C = y.shape
     ps = _same_stride(gamma)
     gs = _same_stride(dgamma, dbeta)
-    nblk = _L.dba_bn_partial_blocks(N, H * W, C)
-    part = torch.empty(G * (nblk + 1) * 2 * C, dtype=torch.float32, device=y.device)
     dy = torch.empty_like(y)
     dres = torch.empty_like(y) if want_dres else None
+    if N * H * W <= _BN_SMALL_ROWS:
+        _call("dba_bn_small_bwd", dout.data_ptr(), out.data_ptr(), y.data_ptr(), mean.data_ptr(), invstd.data_ptr(),
+              gamma.data_ptr(), ps, int(relu), dgamma.data_ptr(), dbeta.data_ptr(), gs, dy.data_ptr(), _ptr(dres),
+              _ptr(_i32(nvalid)), G, N, H * W, C, _stream())
+        return (dy, dres) if want_dres else dy
+    nblk = _L.dba_bn_partial_blocks(N, H * W, C)
+    part = torch.empty(G * (nblk + 1) * 2 * C, dtype=torch.float32, device=y.device)
     _call("dba_bn_bwd", dout.data_ptr(), out.data_ptr(), y.data_ptr(), mean.data_ptr(), invstd.data_ptr(),
           gamma.data_ptr(), ps, int(relu), dgamma.data_ptr(), dbeta.data_ptr(), gs, dy.data_ptr(), _ptr(dres),
           part.data_ptr(), _ptr(_i32(nvalid)), G, N, H * W, C, _stream())
