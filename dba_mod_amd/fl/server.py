@@ -184,6 +184,10 @@ class Server:
         with self.timer.phase("aggregate"):
             self._aggregate(plan, bank, fg_grads, adversarial)
             bank[0].copy_(self.global_state)
+            if p["nan_check"] and not bool(torch.isfinite(self.global_state).all()):
+                # fail fast: a non-finite global model poisons every later round
+                raise FloatingPointError(f"round {epoch}: aggregated global model is not finite "
+                                         f"(aggregation={p['aggregation_methods']})")
         return {"epoch": epoch, "plan": plan, "bank": bank, "cstats": cstats, "t0": t0,
                 "clients_on_rank": len(mine), "phases": self.timer.reset()}
 
@@ -352,9 +356,11 @@ class Server:
         elif method == C.AGGR_GEO_MED:
             ns = [c.num_samples for c in plan.clients]
             self._log_poison_ratio("rfa", names, ns)
+            mun = p["max_update_norm"]
             updated, wv, alphas, calls = agg.geometric_median(
                 self.global_state, finals, ns, float(p["eta"]), int(p["geom_median_maxiter"]),
-                bool(p["diff_privacy"]), float(p["sigma"]), dp_seed, n_upd)
+                bool(p["diff_privacy"]), float(p["sigma"]), dp_seed, n_upd,
+                max_update_norm=float(mun) if mun is not None else None)
             self.csv.add_weight_result(names, wv, alphas)
             self._plot_weights(names, wv, alphas, adversarial, plan.epoch)
         elif method == C.AGGR_FOOLSGOLD:

@@ -165,3 +165,32 @@ def test_pretrain_tool_checkpoint_resumes(tmp_path):
     assert s.start_epoch == 4
     assert torch.allclose(s.spec.view(s.global_state[None], "conv1.weight")[0].flatten()[:5].float().cpu(),
                           ck["state_dict"]["conv1.weight"].permute(0, 2, 3, 1).flatten()[:5].float(), atol=1e-6)
+
+
+def test_nan_guard_aborts_round(tmp_path):
+    """A non-finite aggregated model stops the run at that round."""
+    s = Server(mnist_params(tmp_path, nan_check=True), DistCtx(), write_outputs=False)
+    s.run_round(11)
+    s.global_state[5] = float("nan")
+    with pytest.raises(FloatingPointError, match="round 12"):
+        s.run_round(12)
+
+
+def test_same_seed_same_model(tmp_path):
+    """Determinism: two runs with the same seed end with identical weights."""
+    outs = []
+    for k in range(2):
+        s = Server(mnist_params(tmp_path / str(k)), DistCtx(), write_outputs=False)
+        s.run_round(11)
+        s.run_round(12)
+        outs.append(s.global_state.clone())
+    assert torch.equal(outs[0], outs[1])
+
+
+def test_rfa_update_norm_rejection(tmp_path):
+    """max_update_norm (helper.py:360-369): an oversize RFA median leaves the model unchanged."""
+    s = Server(mnist_params(tmp_path, aggregation_methods="geom_median", max_update_norm=1e-9), DistCtx(),
+               write_outputs=False)
+    before = s.global_state.clone()
+    s.run_round(11)
+    assert torch.equal(before, s.global_state)
