@@ -44,27 +44,45 @@ struct PconvArgs {
   int G, N, H, relu, tr;
 };
 
-// 16-byte-chunk swizzle inside a pixel (CP chunks per pixel); see the header comment.
-template <int CP, int HP>
+// LDS position of halo pixel (hr, hc).  Stride 1: row-major with pitch W+2.  Stride 2:
+// columns de-interleaved by parity (even half, then odd half, W+1 slots each), so the
+// stride-2 pixel walk of an output row reads CONSECUTIVE positions.
+template <int S, int W>
+__device__ __forceinline__ int hpos(int hr, int hc) {
+  if constexpr (S == 1) return hr * (W + 2) + hc;
+  else return hr * 2 * (W + 1) + (hc & 1) * (W + 1) + (hc >> 1);
+}
+
+// 16-byte-chunk swizzle inside a pixel (CP chunks per pixel): every ds_read_b128 lane group
+// of a B-fragment read hits 16 distinct bank slots (checked exhaustively over all taps for
+// each geometry used).
+template <int S, int CP, int W>
 __device__ __forceinline__ int swz(int hr, int hc) {
-  if constexpr (CP == 4) {
-    const int q = hr * HP + hc;
-    return (q >> 2) & 3;
-  } else if constexpr (CP == 8) {
-    return (hc >> 1) & 7;
+  if constexpr (S == 1) {
+    if constexpr (CP == 4) {
+      const int q = hr * (W + 2) + hc;
+      return (q >> 2) & 3;
+    } else if constexpr (CP == 8) {
+      return (hc >> 1) & 7;
+    } else {
+      return ((hr & 1) << 3) | (hc & 7);
+    }
   } else {
-    return ((hr & 1) << 3) | (hc & 7);
+    if constexpr (CP == 4) return (hc >> 3) & 3;
+    else return (((hr >> 1) & 1) << 2) | ((hc >> 2) & 3);
   }
 }
 
-template <int C, int COUT, int W, int MI, int NWC, int WPE, bool TR>
+// W = OUTPUT width; S = stride (1, or 2 for the stage-entry convs, forward only)
+template <int C, int COUT, int W, int MI, int NWC, int WPE, bool TR, int S = 1>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE))) void pconv_kernel(PconvArgs a) {
   constexpr int CP = C / 8;                 // 16-B chunks per pixel
-  constexpr int HP = W + 2;                 // halo row pitch (pixels)
+  constexpr int HP = S == 1 ? W + 2 : 2 * (W + 1);   // halo row pitch (positions)
+  constexpr int WIN = W * S;                // input width
   constexpr int NWP = 4 / NWC;              // waves along pixels
   constexpr int BPX = NWP * MI * 32;        // output pixels per tile
   constexpr int SR = BPX / W;               // output rows per tile
-  constexpr int HR = SR + 2;
+  constexpr int HR = S * SR + (S == 1 ? 2 : 1);
   constexpr int HALO = HR * HP * CP;        // chunks per halo image
   constexpr int NCH = (HALO + 255) / 256;   // staged chunks per thread
   constexpr int KSTEPS = 9 * C / 16;
@@ -79,6 +97,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
   const int wc = wid % NWC, wp = wid / NWC;
   const int segs = a.H / SR;
   const int HWo = a.H * W;
+  const int HIN = a.H * S;                  // input height
 
   // ---- this block's contiguous run [v0, v1) of valid tiles
   int V = 0;
@@ -131,18 +150,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
   // LDS slot e (lane-linear per DMA instruction) holds global chunk (e % CP) ^ swz of pixel e / CP
   auto stage = [&](int gg, int tt, int buf) {
     const int n = tt / segs, sg = tt - n * segs;
-    const int row0 = sg * SR - 1;
-    const uint16_t* __restrict__ s = a.src + (long long)gg * a.src_gstride + (long long)n * HWo * C;
+    const int row0 = sg * SR * S - 1;
+    const uint16_t* __restrict__ s = a.src + (long long)gg * a.src_gstride + (long long)n * HIN * WIN * C;
 #pragma unroll
     for (int i = 0; i < NCH; ++i) {
       const int e = tid + 256 * i;
       const uint16_t* p = a.zeros;
       if (e < HALO) {
         const int cs = e % CP, pix = e / CP;
-        const int hr = pix / HP, hc = pix - hr * HP;
+        const int hr = pix / HP, rem = pix - hr * HP;
+        int hc = rem;
+        if constexpr (S == 2) hc = rem < W + 1 ? 2 * rem : 2 * (rem - (W + 1)) + 1;
         const int ih = row0 + hr, iw = hc - 1;
-        if ((unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)W)
-          p = s + ((long long)ih * W + iw) * C + (cs ^ swz<CP, HP>(hr, hc)) * 8;
+        if ((unsigned)ih < (unsigned)HIN && (unsigned)iw < (unsigned)WIN)
+          p = s + ((long long)ih * WIN + iw) * C + (cs ^ swz<S, CP, W>(hr, hc)) * 8;
       }
       __builtin_amdgcn_global_load_lds((const void*)p,
                                        (__attribute__((address_space(3))) void*)&lds[buf][i * 256 + wid * 64],
@@ -210,8 +231,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
       const int kh = tap / 3, kw = tap - kh * 3;
 #pragma unroll
       for (int i = 0; i < MI; ++i) {
-        const int hr = pr[i] + kh, hc = pc[i] + kw;
-        q[i] = *(const bf16x8_t*)&L[(hr * HP + hc) * CP + ((c16 * 2 + hi) ^ swz<CP, HP>(hr, hc))];
+        const int hr = S * pr[i] + kh, hc = S * pc[i] + kw;
+        q[i] = *(const bf16x8_t*)&L[hpos<S, W>(hr, hc) * CP + ((c16 * 2 + hi) ^ swz<S, CP, W>(hr, hc))];
       }
     };
     loadB(0, bq[0]);
@@ -287,7 +308,7 @@ int num_cus() {
   return n;
 }
 
-template <int C, int COUT, int W, int MI, int NWC, int WPE>
+template <int C, int COUT, int W, int MI, int NWC, int WPE, int S = 1>
 int launch_pconv(const PconvArgs& a, hipStream_t st) {
   constexpr int BPX = (4 / NWC) * MI * 32;
   constexpr int SR = BPX / W;
@@ -304,27 +325,37 @@ int launch_pconv(const PconvArgs& a, hipStream_t st) {
   }();
   const long long by_turnover = (tiles + tpb - 1) / tpb;
   const int grid = (int)std::max(1LL, std::min(tiles, std::max((long long)num_cus() * WPE, by_turnover)));
-  if (a.tr)
-    hipLaunchKernelGGL((pconv_kernel<C, COUT, W, MI, NWC, WPE, true>), dim3(grid), dim3(256), 0, st, a);
-  else
-    hipLaunchKernelGGL((pconv_kernel<C, COUT, W, MI, NWC, WPE, false>), dim3(grid), dim3(256), 0, st, a);
+  if constexpr (S == 1) {
+    if (a.tr)
+      hipLaunchKernelGGL((pconv_kernel<C, COUT, W, MI, NWC, WPE, true, 1>), dim3(grid), dim3(256), 0, st, a);
+    else
+      hipLaunchKernelGGL((pconv_kernel<C, COUT, W, MI, NWC, WPE, false, 1>), dim3(grid), dim3(256), 0, st, a);
+  } else {
+    if (a.tr) return -100;
+    hipLaunchKernelGGL((pconv_kernel<C, COUT, W, MI, NWC, WPE, false, S>), dim3(grid), dim3(256), 0, st, a);
+  }
   DBA_LAUNCH_CHECK();
 }
 
 }  // namespace
 
-// Stride-1 3x3 pad-1 conv (tr = 0) or its data gradient (tr = 1, w = the forward weight).
-// Square channel geometry only: (C, Cout, W) in {(32,32,32), (64,64,16)} (128-channel
-// layers need 288 weight VGPRs per wave: they stay on the implicit-GEMM kernel).
-// Returns -100 for anything else (caller falls back to the halo / implicit-GEMM kernels).
+// 3x3 pad-1 conv (tr = 0) or, at stride 1, its data gradient (tr = 1, w = the forward
+// weight).  H, W = OUTPUT size.  Geometries (C, Cout, W, stride): (32,32,32,1), (64,64,16,1),
+// and the stage-entry convs (32,64,16,2), (64,128,8,2) (128/256-channel stride-1 layers need
+// 288+ weight VGPRs per wave: they stay on the implicit-GEMM kernel).  Returns -100 otherwise.
 DBA_EXPORT int dba_pconv(const void* x, long long x_gstride, const void* w, long long w_sstride, const int* wsel,
                          const float* bias, long long b_sstride, const void* res, void* out, long long out_gstride,
                          const int* nvalid, const void* zeros, int G, int N, int H, int W, int C, int Cout, int tr,
-                         int relu, void* stream) {
+                         int relu, int stride, void* stream) {
   PconvArgs a{(const uint16_t*)x, x_gstride, (const uint16_t*)w, w_sstride, wsel, bias, b_sstride,
               (const uint16_t*)res, (uint16_t*)out, out_gstride, nvalid, (const uint16_t*)zeros, G, N, H, relu, tr};
   hipStream_t st = (hipStream_t)stream;
-  if (C == 32 && Cout == 32 && W == 32) return launch_pconv<32, 32, 32, 2, 1, 2>(a, st);
-  if (C == 64 && Cout == 64 && W == 16) return launch_pconv<64, 64, 16, 4, 2, 1>(a, st);
+  if (stride == 1) {
+    if (C == 32 && Cout == 32 && W == 32) return launch_pconv<32, 32, 32, 2, 1, 2>(a, st);
+    if (C == 64 && Cout == 64 && W == 16) return launch_pconv<64, 64, 16, 4, 2, 1>(a, st);
+  } else if (stride == 2 && !tr) {
+    if (C == 32 && Cout == 64 && W == 16) return launch_pconv<32, 64, 16, 2, 2, 1, 2>(a, st);
+    if (C == 64 && Cout == 128 && W == 8) return launch_pconv<64, 128, 8, 2, 4, 1, 2>(a, st);
+  }
   return -100;
 }

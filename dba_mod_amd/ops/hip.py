@@ -60,7 +60,7 @@ _SIGS = {
     "dba_sq_dists": [_P, _LL, _P, _I, _LL, _P, _P],
     "dba_weighted_sum": [_P, _LL, _P, _I, _P, _LL, _P],
     "dba_gram": [_P, _LL, _I, _I, _P, _P],
-    "dba_pconv": [_P, _LL, _P, _LL, _P, _P, _LL, _P, _P, _LL, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P],
+    "dba_pconv": [_P, _LL, _P, _LL, _P, _P, _LL, _P, _P, _LL, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P],
     "dba_pwgrad": [_P, _LL, _P, _LL, _P, _LL, _P, _P, _I, _I, _I, _I, _I, _I, _P],
     "dba_dist_loss_grad": [_P, _LL, _P, _LL, _P, _LL, _I, _P, _P, _F, _P, _P],
 }
@@ -151,7 +151,8 @@ def _check_w(w: Tensor) -> Tuple[Tensor, int]:
 
 _PCONV = os.environ.get("DBA_PCONV", "1") != "0"
 _DGRAD_W = os.environ.get("DBA_DGRAD_W", "0") == "1"
-_PCONV_SHAPES = {(32, 32, 32), (64, 64, 16)}     # (Cin, Cout, W): see csrc/kernels/pconv.hip
+# (Cin, Cout, input W, stride): see csrc/kernels/pconv.hip
+_PCONV_SHAPES = {(32, 32, 32, 1), (64, 64, 16, 1), (32, 64, 32, 2), (64, 128, 16, 2)}
 _ZEROS = {}
 
 
@@ -164,8 +165,9 @@ def _zeros(dev) -> Tensor:
 
 
 def _pconv_ok(Cin, Cout, H, W, KH, KW, stride, pad) -> bool:
-    return (_PCONV and stride == 1 and KH == 3 and KW == 3 and pad == 1 and H == W
-            and (Cin, Cout, W) in _PCONV_SHAPES)
+    """H, W = input size."""
+    return (_PCONV and KH == 3 and KW == 3 and pad == 1 and H == W
+            and (Cin, Cout, W, stride) in _PCONV_SHAPES)
 
 
 def conv2d(x, w, wsel, stride, pad, bias=None, residual=None, relu=False, nvalid=None, out_dtype=None):
@@ -191,8 +193,8 @@ def conv2d(x, w, wsel, stride, pad, bias=None, residual=None, relu=False, nvalid
     if (not f32 and _pconv_ok(Cin, Cout, H, W, KH, KW, stride, pad)
             and (bias is None or (bs % 4 == 0 and bias.data_ptr() % 16 == 0))):
         rc = _call("dba_pconv", x.data_ptr(), N * H * W * Cin, w.data_ptr(), ws, wsel_, _ptr(bias), bs,
-                   _ptr(residual), y.data_ptr(), N * Ho * Wo * Cout, nv_, _zeros(x.device).data_ptr(), G, N, H, W,
-                   Cin, Cout, 0, int(relu), _stream())
+                   _ptr(residual), y.data_ptr(), N * Ho * Wo * Cout, nv_, _zeros(x.device).data_ptr(), G, N, Ho, Wo,
+                   Cin, Cout, 0, int(relu), stride, _stream())
     if rc == NOT_HANDLED and stride == 1 and KH == KW:
         rc = _call("dba_halo_conv", x.data_ptr(), N * H * W * Cin, w.data_ptr(), ws, wsel_, _ptr(bias), bs,
                    _ptr(residual), y.data_ptr(), N * Ho * Wo * Cout, f32, nv_, G, N, H, W, Cin, Cout, KH, pad,
@@ -222,12 +224,12 @@ def conv2d_dgrad(dy, w, wsel, stride, pad, in_hw, nvalid=None, out_dtype=None, a
     def done(t):
         return t if out_dtype in (None, _BF16) else t.to(out_dtype)
 
-    if _pconv_ok(Cout, Cin, H, W, KH, KW, stride, pad):
+    if stride == 1 and _pconv_ok(Cout, Cin, H, W, KH, KW, stride, pad):
         # stride-1 3x3 dgrad on the persistent kernel: transposed + flipped weight fragments
         # are gathered in-kernel from the forward weights (no transpose pass)
         rc = _call("dba_pconv", dy.data_ptr(), N * Ho * Wo * Cout, w.data_ptr(), ws, _ptr(_i32(wsel)), None, 0,
                    _ptr(acc), dx.data_ptr(), N * H * W * Cin, _ptr(_i32(nvalid)), _zeros(dy.device).data_ptr(), G,
-                   N, H, W, Cout, Cin, 1, 0, _stream())
+                   N, H, W, Cout, Cin, 1, 0, 1, _stream())
         if rc != NOT_HANDLED:
             return done(dx)
     if _DGRAD_W:

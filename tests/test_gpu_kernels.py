@@ -55,6 +55,8 @@ CONV_CASES = [
     (3, 4, 32, 32, 32, 32, 1, 1, 0),     # 1x1 stride 1 (halo kernel)
     (2, 3, 4, 4, 256, 256, 3, 1, 1),     # layer4 (halo does not fit LDS -> gen-2 GEMM)
     (5, 40, 32, 32, 32, 32, 3, 1, 1),    # persistent kernel: block runs cross group boundaries
+    (3, 20, 32, 32, 32, 64, 3, 2, 1),    # persistent kernel, stride 2 (de-interleaved halo)
+    (3, 18, 16, 16, 64, 128, 3, 2, 1),   # persistent kernel, stride 2, 128 outputs
     (4, 70, 16, 16, 64, 64, 3, 1, 1),    # persistent kernel, 64-channel geometry
 ]
 
