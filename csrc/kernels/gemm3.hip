@@ -1,0 +1,259 @@
+// Generation-3 implicit-GEMM convolution (gfx950): the wide layers whose source channel
+// count is a multiple of 64 (ResNet stages 3-4, the stage-entry convs, the stride-1 data
+// gradients run as forward convs of dY).
+//
+// vs conv2.hip (register-staged, 2 LDS buffers, padded rows, one __syncthreads per k-step
+// that drains every load):
+//   * A (activation rows) and B (weight rows) stream global -> LDS by LDS-DMA
+//     (global_load_lds_dwordx4): no staging registers, no ds_write pass;
+//   * an NS-deep LDS ring (NS = 2 by default: 64 KB, two blocks per CU — measured faster than
+//     NS = 3 at one block per CU) with counted vmcnt and a raw s_barrier; k-step kc+NS-1 is
+//     issued before kc computes;
+//   * 128-B LDS rows with a 16-B chunk XOR swizzle (chunk ^ ((row >> 1) & 7)) applied on the DMA
+//     SOURCE address (the LDS image must be lane-linear): every ds_read_b128 lane group of a
+//     32-row fragment read hits 16 distinct bank slots;
+//   * Cs % 64 == 0, so one k-step is one tap x 64 contiguous channels: each A row is a single
+//     128-B run of the source pixel (or the zero page), no per-chunk tap decode.
+// The epilogue (fp32 tile staged through the drained ring, bias / residual / ReLU, 16-B
+// stores) matches conv2.hip.
+#include "common.hpp"
+#include <algorithm>
+#include <cstdlib>
+
+namespace {
+
+struct G3Args {
+  const uint16_t* src; long long src_gstride;   // [G][N][Hs][Ws][Cs]
+  const uint16_t* w; long long w_sstride;       // [slots][Ncol][K]
+  const int* wsel;
+  const float* bias; long long b_sstride;
+  const uint16_t* res;                          // [G][M][Ncol]
+  void* out; long long out_gstride;             // [G][M][Ncol]
+  const int* nvalid;
+  const uint16_t* zeros;
+  int N, Hs, Ws, Cs, Ho, Wo, Ncol, KH, KW, stride, pad, relu;
+  int tiles_n;
+};
+
+__device__ __forceinline__ int g3swz(int row) { return (row >> 1) & 7; }
+
+template <int BM, int BN, int NS, typename OutT>
+__global__ __launch_bounds__(256) void igemm3_kernel(G3Args a) {
+  constexpr int TM = BM / 2, TN = BN / 2;            // 2x2 waves
+  constexpr int MI = TM / 32, NJ = TN / 32;
+  constexpr int CHA = BM * 8, CHB = BN * 8;          // 16-B chunks per stage
+  constexpr int NIA = CHA / 256, NIB = CHB / 256;
+  constexpr int NI = NIA + NIB;                      // DMA instructions per thread per stage
+  constexpr int STG = CHA + CHB;
+  static_assert(BM * BN * 4 <= NS * STG * 16, "epilogue tile fits the ring");
+  constexpr int KEEP = NI * (NS - 2);                // DMA instructions left in flight at a wait
+  constexpr int kWaitKeep = (KEEP & 15) | ((KEEP >> 4) << 14) | (0x7 << 4) | (0xF << 8);
+  constexpr int kWaitAll = (0x7 << 4) | (0xF << 8);
+  __shared__ __attribute__((aligned(16))) uint4 ring[NS][STG];
+
+  const int g = blockIdx.y;
+  const int HoWo = a.Ho * a.Wo;
+  const int Mv = valid_rows(a.nvalid, g, a.N) * HoWo;
+  const int tn = blockIdx.x % a.tiles_n, tm = blockIdx.x / a.tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  if (m0 >= Mv) return;
+  const int K = a.KH * a.KW * a.Cs;
+  const int nk = K / 64;
+  const uint16_t* __restrict__ src = a.src + (long long)g * a.src_gstride;
+  const int slot = a.wsel ? a.wsel[g] : g;
+  const uint16_t* __restrict__ Wp = a.w + (long long)slot * a.w_sstride;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+
+  // per-thread DMA rows (fixed for the block): A row -> source pixel, B row -> weight row
+  int an[NIA], ap[NIA], aq[NIA], acs[NIA];
+#pragma unroll
+  for (int i = 0; i < NIA; ++i) {
+    const int e = tid + 256 * i, row = e >> 3;
+    acs[i] = (e & 7) ^ g3swz(row);
+    const int m = m0 + row;
+    if (m < Mv) {
+      const int n = m / HoWo, rem = m - n * HoWo;
+      an[i] = n;
+      ap[i] = (rem / a.Wo) * a.stride - a.pad;
+      aq[i] = (rem - (rem / a.Wo) * a.Wo) * a.stride - a.pad;
+    } else {
+      an[i] = -1; ap[i] = 0; aq[i] = 0;
+    }
+  }
+  const uint16_t* brow[NIB];
+#pragma unroll
+  for (int i = 0; i < NIB; ++i) {
+    const int e = tid + 256 * i, row = e >> 3;
+    brow[i] = n0 + row < a.Ncol ? Wp + (long long)(n0 + row) * K + ((e & 7) ^ g3swz(row)) * 8 : nullptr;
+  }
+
+  auto stage = [&](int kc, int buf) {
+    const int tap = (kc * 64) / a.Cs, c0 = kc * 64 - tap * a.Cs;
+    const int kh = tap / a.KW, kw = tap - kh * a.KW;
+#pragma unroll
+    for (int i = 0; i < NIA; ++i) {
+      const uint16_t* p = a.zeros;
+      const int hs = ap[i] + kh, ws = aq[i] + kw;
+      if (an[i] >= 0 && (unsigned)hs < (unsigned)a.Hs && (unsigned)ws < (unsigned)a.Ws)
+        p = src + (((long long)an[i] * a.Hs + hs) * a.Ws + ws) * a.Cs + c0 + acs[i] * 8;
+      __builtin_amdgcn_global_load_lds((const void*)p,
+                                       (__attribute__((address_space(3))) void*)&ring[buf][i * 256 + wid * 64],
+                                       16, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < NIB; ++i) {
+      const uint16_t* p = brow[i] ? brow[i] + kc * 64 : a.zeros;
+      __builtin_amdgcn_global_load_lds((const void*)p,
+                                       (__attribute__((address_space(3))) void*)&ring[buf][CHA + i * 256 + wid * 64],
+                                       16, 0, 0);
+    }
+  };
+
+  f32x16_t acc[MI][NJ];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  // NS-deep ring: k-step kc+NS-1 is issued at the top of iteration kc (into the buffer of
+  // kc-1, retired by the previous barrier) and the wait at the bottom leaves NS-2 stages in
+  // flight across the raw barrier.
+  for (int s = 0; s < NS - 1; ++s)
+    if (s < nk) stage(s, s);
+  if (nk > 1) {
+    // wait for k-step 0 only
+    constexpr int K0 = NI * (NS - 2);
+    __builtin_amdgcn_s_waitcnt((K0 & 15) | ((K0 >> 4) << 14) | (0x7 << 4) | (0xF << 8));
+  } else {
+    __builtin_amdgcn_s_waitcnt(kWaitAll);
+  }
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+
+  const int fr = lane & 31, hi = lane >> 5;
+  int cur = 0;
+  for (int kc = 0; kc < nk; ++kc) {
+    const int pre = kc + NS - 1;
+    if (pre < nk) stage(pre, cur == 0 ? NS - 1 : cur - 1);
+    const uint4* L = ring[cur];
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      const int ch = kk * 2 + hi;
+      bf16x8_t af[MI], bfr[NJ];
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        const int row = wm * TM + i * 32 + fr;
+        af[i] = *(const bf16x8_t*)&L[row * 8 + (ch ^ g3swz(row))];
+      }
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int row = wn * TN + j * 32 + fr;
+        bfr[j] = *(const bf16x8_t*)&L[CHA + row * 8 + (ch ^ g3swz(row))];
+      }
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    if (kc + 1 < nk) {
+      asm volatile("" ::: "memory");
+      // k-step kc+1 must have landed; the younger ones may stay in flight
+      if (kc + NS - 1 < nk) __builtin_amdgcn_s_waitcnt(kWaitKeep);
+      else __builtin_amdgcn_s_waitcnt(kWaitAll);
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      cur = cur == NS - 1 ? 0 : cur + 1;
+    }
+  }
+
+  // ---- epilogue: fp32 tile through the (drained) ring, 8-wide pass with bias / res / ReLU
+  __syncthreads();
+  float* Cst = reinterpret_cast<float*>(&ring[0][0]);
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = wm * TM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * hi;
+        const int col = wn * TN + j * 32 + fr;
+        Cst[row * BN + col] = acc[i][j][r];
+      }
+  __syncthreads();
+  OutT* out = (OutT*)a.out + (long long)g * a.out_gstride;
+  const float* bias = a.bias ? a.bias + (long long)slot * a.b_sstride : nullptr;
+  const uint16_t* res = a.res ? a.res + (long long)g * a.out_gstride : nullptr;
+  constexpr int CH8 = BN / 8;
+  for (int e = tid; e < BM * CH8; e += 256) {
+    const int row = e / CH8, c8 = (e - row * CH8) * 8;
+    const int m = m0 + row;
+    const int n = n0 + c8;
+    if (m >= Mv || n >= a.Ncol) continue;
+    float v[8];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) v[t] = Cst[row * BN + c8 + t];
+    const long long o = (long long)m * a.Ncol + n;
+    if (bias) {
+#pragma unroll
+      for (int t = 0; t < 8; ++t) v[t] += bias[n + t];
+    }
+    if (res) {
+      const uint4 rv = *(const uint4*)(res + o);
+      const uint16_t* rp = (const uint16_t*)&rv;
+#pragma unroll
+      for (int t = 0; t < 8; ++t) v[t] += bf2f(rp[t]);
+    }
+    if (a.relu) {
+#pragma unroll
+      for (int t = 0; t < 8; ++t) v[t] = fmaxf(v[t], 0.f);
+    }
+    if constexpr (sizeof(OutT) == 2) {
+      uint4 pk;
+      uint16_t* pp = (uint16_t*)&pk;
+#pragma unroll
+      for (int t = 0; t < 8; ++t) pp[t] = f2bf(v[t]);
+      *(uint4*)((uint16_t*)out + o) = pk;
+    } else {
+#pragma unroll
+      for (int t = 0; t < 8; ++t) ((float*)out)[o + t] = v[t];
+    }
+  }
+}
+
+template <int BM, int BN, int NS, typename OutT>
+int launch3(G3Args a, int G, hipStream_t st) {
+  const long long M = (long long)a.N * a.Ho * a.Wo;
+  a.tiles_n = ceil_div(a.Ncol, BN);
+  dim3 grid((unsigned)(ceil_div(M, BM) * a.tiles_n), G);
+  hipLaunchKernelGGL((igemm3_kernel<BM, BN, NS, OutT>), grid, dim3(256), 0, st, a);
+  DBA_LAUNCH_CHECK();
+}
+
+}  // namespace
+
+// Forward conv (or a stride-1 data gradient expressed as one, with tap-flipped transposed
+// weights) for Cs % 64 == 0 and Ncol % 8 == 0 on launches large enough to fill the chip
+// with 128x128 tiles.  Returns -100 otherwise (caller falls back to conv2.hip).
+DBA_EXPORT int dba_conv3_fwd(const void* x, long long x_gstride, const void* w, long long w_sstride, const int* wsel,
+                             const float* bias, long long b_sstride, const void* res, void* out, long long out_gstride,
+                             int out_f32, const int* nvalid, const void* zeros, int G, int N, int H, int W, int Cin,
+                             int Ho, int Wo, int Cout, int KH, int KW, int stride, int pad, int relu, void* stream) {
+  if (Cin % 64 != 0 || Cout % 8 != 0 || Cout < 128 || out_f32) return -100;
+  const long long M = (long long)N * Ho * Wo;
+  if (M * G / 128 * ((Cout + 127) / 128) < 512) return -100;
+  G3Args a{(const uint16_t*)x, x_gstride, (const uint16_t*)w, w_sstride, wsel, bias, b_sstride,
+           (const uint16_t*)res, out, out_gstride, nvalid, (const uint16_t*)zeros,
+           N, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, relu, 1};
+  static const int ns = [] {
+    const char* e = getenv("DBA_G3_NS");
+    return e ? atoi(e) : 2;
+  }();
+  if (ns == 2) return launch3<128, 128, 2, uint16_t>(a, G, (hipStream_t)stream);
+  return launch3<128, 128, 3, uint16_t>(a, G, (hipStream_t)stream);
+}

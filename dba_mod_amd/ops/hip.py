@@ -60,6 +60,7 @@ _SIGS = {
     "dba_sq_dists": [_P, _LL, _P, _I, _LL, _P, _P],
     "dba_weighted_sum": [_P, _LL, _P, _I, _P, _LL, _P],
     "dba_gram": [_P, _LL, _I, _I, _P, _P],
+    "dba_conv3_fwd": [_P, _LL, _P, _LL, _P, _P, _LL, _P, _P, _LL, _I, _P, _P] + [_I] * 13 + [_P],
     "dba_pconv": [_P, _LL, _P, _LL, _P, _P, _LL, _P, _P, _LL, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P],
     "dba_pwgrad": [_P, _LL, _P, _LL, _P, _LL, _P, _P, _I, _I, _I, _I, _I, _I, _P],
     "dba_dist_loss_grad": [_P, _LL, _P, _LL, _P, _LL, _I, _P, _P, _F, _P, _P],
@@ -151,6 +152,7 @@ def _check_w(w: Tensor) -> Tuple[Tensor, int]:
 
 _PCONV = os.environ.get("DBA_PCONV", "1") != "0"
 _DGRAD_W = os.environ.get("DBA_DGRAD_W", "0") == "1"
+_GEMM3 = os.environ.get("DBA_GEMM3", "1") != "0"
 # (Cin, Cout, input W, stride): see csrc/kernels/pconv.hip
 _PCONV_SHAPES = {(32, 32, 32, 1), (64, 64, 16, 1), (32, 64, 32, 2), (64, 128, 16, 2)}
 _ZEROS = {}
@@ -195,6 +197,10 @@ def conv2d(x, w, wsel, stride, pad, bias=None, residual=None, relu=False, nvalid
         rc = _call("dba_pconv", x.data_ptr(), N * H * W * Cin, w.data_ptr(), ws, wsel_, _ptr(bias), bs,
                    _ptr(residual), y.data_ptr(), N * Ho * Wo * Cout, nv_, _zeros(x.device).data_ptr(), G, N, Ho, Wo,
                    Cin, Cout, 0, int(relu), stride, _stream())
+    if rc == NOT_HANDLED and _GEMM3:
+        rc = _call("dba_conv3_fwd", x.data_ptr(), N * H * W * Cin, w.data_ptr(), ws, wsel_, _ptr(bias), bs,
+                   _ptr(residual), y.data_ptr(), N * Ho * Wo * Cout, f32, nv_, _zeros(x.device).data_ptr(), G, N, H,
+                   W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, int(relu), _stream())
     if rc == NOT_HANDLED and stride == 1 and KH == KW:
         rc = _call("dba_halo_conv", x.data_ptr(), N * H * W * Cin, w.data_ptr(), ws, wsel_, _ptr(bias), bs,
                    _ptr(residual), y.data_ptr(), N * Ho * Wo * Cout, f32, nv_, G, N, H, W, Cin, Cout, KH, pad,
@@ -246,6 +252,14 @@ def conv2d_dgrad(dy, w, wsel, stride, pad, in_hw, nvalid=None, out_dtype=None, a
     if stride == 1 and KH == KW and pad == (KH - 1) // 2:
         # stride-1 dgrad == forward conv of dY with tap-flipped, transposed weights
         _call("dba_transpose_w", w.data_ptr(), ws, wt.data_ptr(), slots, Cout, KH * KW, Cin, 1, skip, _stream())
+        rc = NOT_HANDLED
+        if _GEMM3:
+            rc = _call("dba_conv3_fwd", dy.data_ptr(), N * Ho * Wo * Cout, wt.data_ptr(), Cin * KH * KW * Cout,
+                       _ptr(_i32(wsel)), None, 0, _ptr(acc), dx.data_ptr(), N * H * W * Cin, 0, _ptr(_i32(nvalid)),
+                       _zeros(dy.device).data_ptr(), G, N, Ho, Wo, Cout, H, W, Cin, KH, KH, 1, KH - 1 - pad, 0,
+                       _stream())
+        if rc != NOT_HANDLED:
+            return done(dx)
         rc = _call("dba_halo_conv", dy.data_ptr(), N * Ho * Wo * Cout, wt.data_ptr(), Cin * KH * KW * Cout,
                    _ptr(_i32(wsel)), None, 0, _ptr(acc), dx.data_ptr(), N * H * W * Cin, 0, _ptr(_i32(nvalid)), G,
                    N, Ho, Wo, Cout, Cin, KH, KH - 1 - pad, 0, _stream())

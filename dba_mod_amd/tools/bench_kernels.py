@@ -57,11 +57,12 @@ def main(argv=None) -> int:
         dy = torch.randn(G, N, Ho, Ho, Cout, device=dev).bfloat16()
         flops = 2.0 * G * N * Ho * Ho * Cout * k * k * Cin
         rec = {"shape": name}
-        for tag, pc in (("fwd", True), ("fwd_nopconv", False)):
-            H._PCONV = pc
+        for tag, pc, g3 in (("fwd", True, True), ("fwd_nopconv", False, True), ("fwd_nogemm3", True, False)):
+            H._PCONV, H._GEMM3 = pc, g3
             t = _time(lambda: H.conv2d(x, w, None, s, p, relu=True), args.reps)
             rec[tag + "_us"] = round(t * 1e6, 1)
             rec[tag + "_tflops"] = round(flops / t / 1e12, 1)
+        H._GEMM3 = True
         for tag, pc in (("dgrad", True), ("dgrad_nopconv", False)):
             H._PCONV = pc
             t = _time(lambda: H.conv2d_dgrad(dy, w, None, s, p, (Hh, Hh)), args.reps)
