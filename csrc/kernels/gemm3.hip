@@ -123,12 +123,11 @@ __global__ __launch_bounds__(256) void igemm3_kernel(G3Args a) {
   // flight across the raw barrier.
   for (int s = 0; s < NS - 1; ++s)
     if (s < nk) stage(s, s);
-  if (nk > 1) {
-    // wait for k-step 0 only
-    constexpr int K0 = NI * (NS - 2);
-    __builtin_amdgcn_s_waitcnt((K0 & 15) | ((K0 >> 4) << 14) | (0x7 << 4) | (0xF << 8));
+  if (nk >= NS - 1) {
+    // all NS-1 prologue stages were issued: wait for k-step 0 only
+    __builtin_amdgcn_s_waitcnt(kWaitKeep);
   } else {
-    __builtin_amdgcn_s_waitcnt(kWaitAll);
+    __builtin_amdgcn_s_waitcnt(kWaitAll);      // short K: fewer stages in flight, drain them
   }
   asm volatile("" ::: "memory");
   __builtin_amdgcn_s_barrier();
@@ -246,7 +245,6 @@ DBA_EXPORT int dba_conv3_fwd(const void* x, long long x_gstride, const void* w, 
                              int Ho, int Wo, int Cout, int KH, int KW, int stride, int pad, int relu, void* stream) {
   if (Cin % 64 != 0 || Cout % 8 != 0 || Cout < 128 || out_f32) return -100;
   const long long M = (long long)N * Ho * Wo;
-  if (M * G / 128 * ((Cout + 127) / 128) < 512) return -100;
   G3Args a{(const uint16_t*)x, x_gstride, (const uint16_t*)w, w_sstride, wsel, bias, b_sstride,
            (const uint16_t*)res, out, out_gstride, nvalid, (const uint16_t*)zeros,
            N, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, relu, 1};
@@ -254,6 +252,13 @@ DBA_EXPORT int dba_conv3_fwd(const void* x, long long x_gstride, const void* w, 
     const char* e = getenv("DBA_G3_NS");
     return e ? atoi(e) : 2;
   }();
-  if (ns == 2) return launch3<128, 128, 2, uint16_t>(a, G, (hipStream_t)stream);
-  return launch3<128, 128, 3, uint16_t>(a, G, (hipStream_t)stream);
+  if (M * G / 128 * ((Cout + 127) / 128) < 512) {
+    // small launches (grouped training steps): the block count cannot cover the chip, so
+    // per-block latency rules — smaller M tiles and a 4-deep ring (3 k-steps in flight)
+    static const bool small_off = getenv("DBA_G3_SMALL") && atoi(getenv("DBA_G3_SMALL")) == 0;
+    if (small_off) return -100;
+    return launch3<64, 128, 4, uint16_t>(a, G, (hipStream_t)stream);
+  }
+  if (ns == 3) return launch3<128, 128, 3, uint16_t>(a, G, (hipStream_t)stream);
+  return launch3<128, 128, 2, uint16_t>(a, G, (hipStream_t)stream);
 }

@@ -57,6 +57,8 @@ CONV_CASES = [
     (5, 40, 32, 32, 32, 32, 3, 1, 1),    # persistent kernel: block runs cross group boundaries
     (3, 20, 32, 32, 32, 64, 3, 2, 1),    # persistent kernel, stride 2 (de-interleaved halo)
     (3, 18, 16, 16, 64, 128, 3, 2, 1),   # persistent kernel, stride 2, 128 outputs
+    (2, 3, 8, 8, 128, 256, 1, 2, 0),     # gen-3 GEMM small path, K = 2 k-steps (< ring depth)
+    (2, 40, 8, 8, 128, 128, 3, 1, 1),    # gen-3 GEMM, 128x128 tiles
     (4, 70, 16, 16, 64, 64, 3, 1, 1),    # persistent kernel, 64-channel geometry
 ]
 
