@@ -36,7 +36,7 @@ struct Igemm2Args {
 
 template <int MODE>
 __device__ __forceinline__ bool src_pos2(const Igemm2Args& a, int p, int q, int kh, int kw, int& hs, int& ws) {
-  if (MODE == 0) {
+  if constexpr (MODE == 0) {
     hs = p * a.stride - a.pad + kh;
     ws = q * a.stride - a.pad + kw;
     return (unsigned)hs < (unsigned)a.Hs && (unsigned)ws < (unsigned)a.Ws;
@@ -79,12 +79,33 @@ __global__ __launch_bounds__(256) void igemm2_kernel(Igemm2Args a) {
 
   const int g = blockIdx.y;
   const int HoWo = a.Ho * a.Wo;
-  const int Mv = valid_rows(a.nvalid, g, a.N) * HoWo;
-  const int tn = blockIdx.x % a.tiles_n, tm = blockIdx.x / a.tiles_n;
+  // MODE 2 (stride-2 data gradient): output rows are grouped by pixel-parity class
+  // (py, px); every row of a block shares it, so whole k-steps whose tap parity cannot
+  // reach the class are skipped (3/4 of a 3x3 stride-2 scatter GEMM is structurally zero).
+  const int HoWo2 = MODE == 2 ? HoWo / 4 : HoWo;
+  const int Mv = valid_rows(a.nvalid, g, a.N) * HoWo2;
+  const int tn = blockIdx.x % a.tiles_n;
+  int tm = blockIdx.x / a.tiles_n, cls = 0;
+  if constexpr (MODE == 2) {
+    const int tpc = (a.N * HoWo2 + BM - 1) / BM;   // row tiles per class
+    cls = tm / tpc;
+    tm -= cls * tpc;
+  }
+  const int py = cls >> 1, px = cls & 1;
   const int m0 = tm * BM, n0 = tn * BN;
   if (m0 >= Mv) return;
   const int K = a.KH * a.KW * a.Cs;
-  const int nk = (K + BK2 - 1) / BK2;
+  const int cpt = a.Cs / BK2;                      // MODE 2: k-steps per tap (Cs % 64 == 0)
+  const int kh0 = (py + a.pad) & 1, kw0 = (px + a.pad) & 1;
+  const int nvw = MODE == 2 ? (a.KW - kw0 + 1) / 2 : 1;
+  const int nvh = MODE == 2 ? (a.KH - kh0 + 1) / 2 : 1;
+  const int nk = MODE == 2 ? nvh * nvw * cpt : (K + BK2 - 1) / BK2;
+  auto kc_of = [&](int j) -> int {
+    if constexpr (MODE != 2) return j;
+    const int chunk = j % cpt, t = j / cpt;
+    const int ih = t / nvw, iw = t - ih * nvw;
+    return ((kh0 + 2 * ih) * a.KW + kw0 + 2 * iw) * cpt + chunk;
+  };
   const uint16_t* __restrict__ src = a.src + (long long)g * a.src_gstride;
   const int slot = a.wsel ? a.wsel[g] : g;
   const uint16_t* __restrict__ Wp = a.w + (long long)slot * a.w_sstride;
@@ -98,9 +119,15 @@ __global__ __launch_bounds__(256) void igemm2_kernel(Igemm2Args a) {
   for (int i = 0; i < RA; ++i) {
     const int m = m0 + (tid >> 3) + 32 * i;
     if (m < Mv) {
-      const int n = m / HoWo, rem = m - n * HoWo;
-      rp[i] = rem / a.Wo;
-      rq[i] = rem - rp[i] * a.Wo;
+      const int n = m / HoWo2, rem = m - n * HoWo2;
+      if constexpr (MODE == 2) {
+        const int w2 = a.Wo >> 1;
+        rp[i] = 2 * (rem / w2) + py;
+        rq[i] = 2 * (rem - (rem / w2) * w2) + px;
+      } else {
+        rp[i] = rem / a.Wo;
+        rq[i] = rem - rp[i] * a.Wo;
+      }
       rbase[i] = n;
     } else {
       rbase[i] = -1; rp[i] = 0; rq[i] = 0;
@@ -182,13 +209,15 @@ __global__ __launch_bounds__(256) void igemm2_kernel(Igemm2Args a) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  load_tiles(0);
-  store_tiles(0);
+  if (nk > 0) {
+    load_tiles(kc_of(0));
+    store_tiles(0);
+  }
   __syncthreads();
   const int fr = lane & 31, fk = (lane >> 5) * 8;
   int cur = 0;
   for (int kc = 0; kc < nk; ++kc) {
-    if (kc + 1 < nk) load_tiles(kc + 1);
+    if (kc + 1 < nk) load_tiles(kc_of(kc + 1));
 #pragma unroll
     for (int kk = 0; kk < BK2; kk += 16) {
       bf16x8_t af[MI], bfr[NJ];
@@ -242,8 +271,15 @@ __global__ __launch_bounds__(256) void igemm2_kernel(Igemm2Args a) {
   const bool full_n = (n0 + BN <= a.Ncol) && (a.Ncol % 8 == 0);
   for (int e = tid; e < BM * CH; e += 256) {
     const int row = e / CH, c8 = (e - row * CH) * 8;
-    const int m = m0 + row;
-    if (m >= Mv) continue;
+    const int mr = m0 + row;
+    if (mr >= Mv) continue;
+    int m = mr;
+    if constexpr (MODE == 2) {   // class-local row -> pixel index
+      const int w2 = a.Wo >> 1;
+      const int nimg = mr / HoWo2, rem = mr - nimg * HoWo2;
+      const int pp = 2 * (rem / w2) + py, qq = 2 * (rem - (rem / w2) * w2) + px;
+      m = (nimg * a.Ho + pp) * a.Wo + qq;
+    }
     float v[8];
 #pragma unroll
     for (int t = 0; t < 8; ++t) v[t] = Cst[row * BN + c8 + t];
@@ -372,7 +408,8 @@ template <int BM, int BN, int WM, int WN, int MODE, typename OutT, bool BT = fal
 int launch2(Igemm2Args a, int G, hipStream_t st) {
   const int M = a.N * a.Ho * a.Wo;
   a.tiles_n = ceil_div(a.Ncol, BN);
-  dim3 grid((unsigned)(ceil_div(M, BM) * a.tiles_n), G);
+  const int tiles_m = MODE == 2 ? 4 * ceil_div(M / 4, BM) : ceil_div(M, BM);
+  dim3 grid((unsigned)(tiles_m * a.tiles_n), G);
   hipLaunchKernelGGL((igemm2_kernel<BM, BN, WM, WN, MODE, OutT, BT>), grid, dim3(256), 0, st, a);
   DBA_LAUNCH_CHECK();
 }
@@ -443,5 +480,7 @@ DBA_EXPORT int dba_conv2_dgrad(const void* dy, long long dy_gstride, const void*
   if (Cout % 8 != 0) return -100;
   Igemm2Args a{(const uint16_t*)dy, dy_gstride, (const uint16_t*)wt, wt_sstride, wsel, nullptr, 0,
                (const uint16_t*)accum, dx, dx_gstride, nvalid, N, Ho, Wo, Cout, H, W, Cin, KH, KW, stride, pad, 0, 1};
+  if (stride == 2 && Cout % BK2 == 0 && H % 2 == 0 && W % 2 == 0)
+    return dispatch2<2, uint16_t>(a, G, (hipStream_t)stream);
   return dispatch2<1, uint16_t>(a, G, (hipStream_t)stream);
 }
