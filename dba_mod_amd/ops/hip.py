@@ -63,6 +63,7 @@ _SIGS = {
     "dba_conv3_fwd": [_P, _LL, _P, _LL, _P, _P, _LL, _P, _P, _LL, _I, _P, _P] + [_I] * 13 + [_P],
     "dba_pconv": [_P, _LL, _P, _LL, _P, _P, _LL, _P, _P, _LL, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P],
     "dba_pwgrad": [_P, _LL, _P, _LL, _P, _LL, _P, _P, _I, _I, _I, _I, _I, _I, _P],
+    "dba_wgrad3": [_P, _LL, _P, _LL, _P, _LL, _P, _P] + [_I] * 12 + [_P],
     "dba_dist_loss_grad": [_P, _LL, _P, _LL, _P, _LL, _I, _P, _P, _F, _P, _P],
 }
 for _name, _args in _SIGS.items():
@@ -153,6 +154,7 @@ def _check_w(w: Tensor) -> Tuple[Tensor, int]:
 _PCONV = os.environ.get("DBA_PCONV", "1") != "0"
 _DGRAD_W = os.environ.get("DBA_DGRAD_W", "0") == "1"
 _GEMM3 = os.environ.get("DBA_GEMM3", "1") != "0"
+_WGRAD3 = os.environ.get("DBA_WGRAD3", "1") != "0"
 # (Cin, Cout, input W, stride): see csrc/kernels/pconv.hip
 _PCONV_SHAPES = {(32, 32, 32, 1), (64, 64, 16, 1), (32, 64, 32, 2), (64, 128, 16, 2)}
 _ZEROS = {}
@@ -287,6 +289,11 @@ def conv2d_wgrad(dy, x, stride, pad, kh, kw, dw, dbias=None, nvalid=None):
         # halo-tiled transposed-read wgrad (csrc/kernels/pwgrad.hip)
         rc = _call("dba_pwgrad", dy.data_ptr(), N * Ho * Wo * Cout, x.data_ptr(), N * H * W * Cin, dw.data_ptr(),
                    dw.stride(0), _ptr(_i32(nvalid)), _zeros(dy.device).data_ptr(), G, N, H, W, Cin, Cout, _stream())
+    if rc == NOT_HANDLED and _WGRAD3:
+        # generation-3 im2col wgrad: strided convs, shortcuts, stem (csrc/kernels/wgrad3.hip)
+        rc = _call("dba_wgrad3", dy.data_ptr(), N * Ho * Wo * Cout, x.data_ptr(), N * H * W * Cin, dw.data_ptr(),
+                   dw.stride(0), _ptr(_i32(nvalid)), _zeros(dy.device).data_ptr(), G, N, H, W, Cin, Ho, Wo, Cout,
+                   kh, kw, stride, pad, _stream())
     if rc == NOT_HANDLED:
         _call("dba_conv_wgrad", dy.data_ptr(), N * Ho * Wo * Cout, x.data_ptr(), N * H * W * Cin, dw.data_ptr(),
               dw.stride(0), _ptr(_i32(nvalid)), G, N, H, W, Cin, Ho, Wo, Cout, kh, kw, stride, pad, _stream())

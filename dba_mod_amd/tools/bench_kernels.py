@@ -26,30 +26,52 @@ SHAPES = [
     ("train.layer2", 10, 64, 16, 64, 64, 3, 1, 1),
     ("train.layer3", 10, 64, 8, 128, 128, 3, 1, 1),
     ("train.layer4", 10, 64, 4, 256, 256, 3, 1, 1),
+    ("train.stem", 10, 64, 32, 3, 32, 3, 1, 1),
+    ("train.l2.0.conv1", 10, 64, 32, 32, 64, 3, 2, 1),
+    ("train.l2.0.sc", 10, 64, 32, 32, 64, 1, 2, 0),
+    ("train.l3.0.conv1", 10, 64, 16, 64, 128, 3, 2, 1),
+    ("train.l3.0.sc", 10, 64, 16, 64, 128, 1, 2, 0),
+    ("train.l4.0.conv1", 10, 64, 8, 128, 256, 3, 2, 1),
+    ("train.l4.0.sc", 10, 64, 8, 128, 256, 1, 2, 0),
 ]
 
 
-def _time(fn, reps):
+def _time(fn, reps, inner=10):
+    """GPU time per call: `inner` calls are captured in one HIP graph and replayed (the FL
+    round replays its kernels the same way), so host and graph-launch overhead do not count."""
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        for _ in range(2):
+            fn()
+    torch.cuda.current_stream().wait_stream(side)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        for _ in range(inner):
+            fn()
     for _ in range(3):
-        fn()
+        graph.replay()
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     for _ in range(reps):
-        fn()
+        graph.replay()
     e1.record()
     torch.cuda.synchronize()
-    return e0.elapsed_time(e1) / reps * 1e-3
+    return e0.elapsed_time(e1) / (reps * inner) * 1e-3
 
 
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--json", default=None)
+    ap.add_argument("--only", default="", help="substring filter on shape names")
     args = ap.parse_args(argv)
     dev = torch.device("cuda")
     rows = []
     for name, G, N, Hh, Cin, Cout, k, s, p in SHAPES:
+        if args.only not in name:
+            continue
         torch.manual_seed(0)
         x = torch.randn(G, N, Hh, Hh, Cin, device=dev).bfloat16()
         w = (torch.randn(G, Cout, k, k, Cin, device=dev) * 0.05).bfloat16()
@@ -70,12 +92,12 @@ def main(argv=None) -> int:
             rec[tag + "_tflops"] = round(flops / t / 1e12, 1)
         if name.startswith("train"):
             dw = torch.zeros(G, Cout, k, k, Cin, device=dev)
-            for tag, pc in (("wgrad", True), ("wgrad_old", False)):
-                H._PCONV = pc
+            for tag, pc, w3 in (("wgrad", True, True), ("wgrad_nowg3", True, False), ("wgrad_old", False, False)):
+                H._PCONV, H._WGRAD3 = pc, w3
                 t = _time(lambda: H.conv2d_wgrad(dy, x, s, p, k, k, dw), args.reps)
                 rec[tag + "_us"] = round(t * 1e6, 1)
                 rec[tag + "_tflops"] = round(flops / t / 1e12, 1)
-        H._PCONV = True
+        H._PCONV, H._WGRAD3 = True, True
         rows.append(rec)
         print(json.dumps(rec), flush=True)
     if args.json:

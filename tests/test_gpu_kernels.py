@@ -60,6 +60,9 @@ CONV_CASES = [
     (2, 3, 8, 8, 128, 256, 1, 2, 0),     # gen-3 GEMM small path, K = 2 k-steps (< ring depth)
     (2, 40, 8, 8, 128, 128, 3, 1, 1),    # gen-3 GEMM, 128x128 tiles
     (4, 70, 16, 16, 64, 64, 3, 1, 1),    # persistent kernel, 64-channel geometry
+    (16, 64, 8, 8, 128, 256, 3, 2, 1),   # gen-3 wgrad without split-K (sole-writer epilogue)
+    (2, 9, 16, 16, 64, 128, 1, 2, 0),    # gen-3 wgrad, shortcut (J = 64)
+    (16, 6, 8, 8, 256, 256, 3, 2, 1),    # gen-3 wgrad 128x128 tiles (launch fills the chip)
 ]
 
 
@@ -107,6 +110,10 @@ def test_conv_fwd_dgrad_wgrad(H, R, case):
     for g in range(G):
         assert _rel(dw[g], dwr[g]) < 1e-2, f"wgrad g{g}"
         assert _rel(db[g], dbr[g]) < 1e-3, f"bias grad g{g}"
+    H.conv2d_wgrad(dy, x, s, p, k, k, dw, None, nvalid=nvalid)   # accumulates
+    for g in range(G):
+        assert _rel(dw[g], 2 * dwr[g]) < 1e-2, f"wgrad accumulate g{g}"
+    assert flat[:, Cout * k * k * Cin:].abs().max().item() == 0.0, "wgrad wrote past its view"
 
 
 @pytest.mark.parametrize("C,HW", [(32, 32), (64, 16)])

@@ -1,0 +1,7 @@
+# GPU: conv kernel tests, then the graph-timed conv microbenchmark at two split-K atomic budgets
+mkdir -p gpurun_out
+timeout -k 10 600 python -m pytest tests/test_gpu_kernels.py -x -q -k "conv or pconv or sgd" > gpurun_out/t_conv.log 2>&1
+rc=$?; echo "rc=$rc" >> gpurun_out/t_conv.log
+[ $rc -ne 0 ] && exit $rc
+timeout -k 10 600 python -m dba_mod_amd.tools.bench_kernels --json gpurun_out/kbench.json > gpurun_out/kbench.log 2>&1 || exit $?
+DBA_W3_ATOMICS=1.2e7 timeout -k 10 600 python -m dba_mod_amd.tools.bench_kernels --only train --json gpurun_out/kbench_a12.json > gpurun_out/kbench_a12.log 2>&1
