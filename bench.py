@@ -11,7 +11,7 @@ trigger + 4 per-trigger ASR tests), aggregation, CSV output.  Nothing is skipped
 
 The reference resumes every config from a pretrained checkpoint (CIFAR: round 200) that is
 not shipped; the bench builds the equivalent starting point with ``--pretrain-rounds``
-(default 20) benign FedAvg rounds before the warmup (untimed, :meth:`Server.pretrain`).
+(default 40) benign FedAvg rounds before the warmup (untimed, :meth:`Server.pretrain`).
 Rounds then start at 201, so with the default ``--warmup 2`` the timed window 203..210
 contains all four poison rounds.
 
@@ -56,7 +56,7 @@ def main() -> int:
     ap.add_argument("--config", default=os.path.join(ROOT, "configs", "cifar_params.yaml"))
     ap.add_argument("--aggregation", default=None, help="override: mean | geom_median | foolsgold")
     ap.add_argument("--cpu", action="store_true")
-    ap.add_argument("--pretrain-rounds", type=int, default=20,
+    ap.add_argument("--pretrain-rounds", type=int, default=40,
                     help="benign FedAvg warm start before warmup (stand-in for the reference's "
                          "pretrained checkpoint; untimed)")
     ap.add_argument("--start-epoch", type=int, default=None,

@@ -87,6 +87,9 @@ _DEFAULTS: Dict[str, Any] = {
     "synthetic_data": "auto",     # auto: real files if present under data_dir, else synthetic
     "synthetic_train_size": None,  # override synthetic dataset sizes (tests / smoke runs)
     "synthetic_test_size": None,
+    "synthetic_noise": None,       # synthetic image pixel-noise sigma (None: per-dataset default)
+    "synthetic_shared": None,      # fraction of the class template shared by all classes
+    "synthetic_clutter": None,     # weight of the per-image random background field
     "compute_dtype": "auto",      # auto: bf16 on GPU (MFMA), fp32 on CPU
     "eval_batch_size": 1024,      # per-model eval chunk (reference: 64; a free parameter, D13)
     "aggregate_bn_buffers": True,  # D2: deltas/aggregation include BN running stats

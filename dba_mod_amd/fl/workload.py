@@ -78,7 +78,10 @@ def build_workload(params: C.Params, device: torch.device) -> Workload:
     synth = _use_synthetic(params, avail)
     if synth:
         train, test = synthetic.synthetic_image_pair(t, seed=seed, train_size=params["synthetic_train_size"],
-                                                     test_size=params["synthetic_test_size"])
+                                                     test_size=params["synthetic_test_size"],
+                                                     noise=params["synthetic_noise"],
+                                                     shared=params["synthetic_shared"],
+                                                     clutter=params["synthetic_clutter"])
     else:
         train, test = {C.TYPE_MNIST: readers.read_mnist, C.TYPE_CIFAR: readers.read_cifar,
                        C.TYPE_TINYIMAGENET: readers.read_tiny}[t](data_dir)

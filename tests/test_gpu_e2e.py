@@ -114,3 +114,26 @@ def test_fl_rounds_on_gpu(dev, tmp_path, agg):
     for f in ("train_result.csv", "test_result.csv", "posiontest_result.csv", "poisontriggertest_result.csv",
               "model_last.pt.tar"):
         assert os.path.exists(os.path.join(s.folder, f)), f
+
+
+def test_cifar_dba_attack_lands(dev, tmp_path):
+    """The flagship attack window end to end on the HIP path: after a benign warm start the
+    first DBA attacker (client 17, round 203) must learn its local trigger (pre-scaling local
+    ASR, ``image_train.py:139-160``) and model replacement (scale 100, eta 0.1) must carry
+    it into the global model (``main.py:204-214`` global-trigger test), while the main task
+    stays learned — the behaviour the DBA paper reports for CIFAR-10."""
+    import csv
+    from dba_mod_amd import config as C
+    from dba_mod_amd.fl.server import Server
+    from dba_mod_amd.parallel.dist import DistCtx
+    p = C.load_params(os.path.join(os.path.dirname(__file__), "..", "configs", "cifar_params.yaml"),
+                      {"resumed_model": False, "synthetic_data": True, "pretrain_rounds": 40,
+                       "start_epoch": 201, "save_dir": str(tmp_path)})
+    s = Server(p, DistCtx(device=dev), write_outputs=True)
+    res = {r["epoch"]: r for r in s.run_rounds([201, 202, 203])}
+    assert res[202]["global_acc"] > 60.0
+    assert res[202]["global_asr"] < 20.0
+    with open(os.path.join(s.folder, "posiontest_result.csv")) as f:
+        rows = [r for r in csv.DictReader(f) if r["model"] == "17" and r["epoch"] == "203"]
+    assert rows and float(rows[0]["accuracy"]) > 90.0, rows     # local ASR before scaling
+    assert res[203]["global_asr"] > 80.0

@@ -1,0 +1,6 @@
+# full GPU check: kernel + e2e tests, smoke, 1-GPU bench
+mkdir -p gpurun_out
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1 || exit $?
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || exit $?
+timeout -k 10 600 python bench.py > gpurun_out/bench.log 2>&1 || exit $?
+tail -1 gpurun_out/bench.log

@@ -3,4 +3,4 @@ timeout -k 10 300 python -m dba_mod_amd.tools.bench_step > gpurun_out/step.log 2
 R=$GRAFT_REPO_ROOT
 mkdir -p $R/gpurun_out/profstep
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $R/gpurun_out/profstep -o step -- python3 -m dba_mod_amd.tools.bench_step --reps 1 > $R/gpurun_out/profstep/out.log 2>&1
+PYTHONPATH=$R timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $R/gpurun_out/profstep -o step -- python3 -m dba_mod_amd.tools.bench_step --reps 1 > $R/gpurun_out/profstep/out.log 2>&1
