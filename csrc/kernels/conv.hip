@@ -467,6 +467,108 @@ __global__ __launch_bounds__(256) void transpose_w_tiled_kernel(const uint16_t* 
   }
 }
 
+// ---------------------------------------------------------------- batched transposes
+// Every data-gradient weight transpose of a training step in ONE launch (the step's weights
+// are fixed from the forward to the SGD update, so all of them can be produced up front):
+// one LDS-tiled 64x64 block per (layer, tap, tile), descriptors passed by value.  A lone
+// attacker's latency-bound step otherwise pays a dependent launch per layer.
+namespace {
+constexpr int kMaxTDesc = 32;
+struct TDesc {
+  const uint16_t* w;
+  uint16_t* wt;
+  long long ws;
+  int Co, T, Ci, flip, tiles, tile0;
+};
+struct TBatch {
+  TDesc d[kMaxTDesc];
+  int n;
+  const int* nvalid;
+};
+
+__global__ __launch_bounds__(256) void transpose_w_batch_kernel(const TBatch b) {
+  __shared__ uint16_t tile[64][64 + 2];
+  const int s = blockIdx.y;
+  if (b.nvalid && b.nvalid[s] == 0) return;
+  int k = 0;
+  while (k + 1 < b.n && (int)blockIdx.x >= b.d[k + 1].tile0) ++k;
+  const TDesc& d = b.d[k];
+  const int Co = d.Co, T = d.T, Ci = d.Ci;
+  const int local = blockIdx.x - d.tile0;
+  const int tci = (Ci + 63) / 64, tco = (Co + 63) / 64;
+  const int t = local / (tci * tco);
+  const int rem = local - t * tci * tco;
+  const int co0 = (rem / tci) * 64, ci0 = (rem % tci) * 64;
+  const uint16_t* ws = d.w + (long long)s * d.ws;
+  uint16_t* wo = d.wt + (long long)s * Co * T * Ci;
+  const int tid = threadIdx.x;
+  const int ts = d.flip ? T - 1 - t : t;
+  const bool vec = (Ci % 8 == 0) && (Co % 8 == 0);
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int e = tid + 256 * i;
+    const int r = e >> 3, c8 = (e & 7) * 8;
+    const int co = co0 + r, ci = ci0 + c8;
+    if (vec) {
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (co < Co && ci < Ci) v = *(const uint4*)(ws + ((long long)co * T + ts) * Ci + ci);
+      const uint16_t* pv = (const uint16_t*)&v;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) tile[r][c8 + j] = pv[j];
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        tile[r][c8 + j] = (co < Co && ci + j < Ci) ? ws[((long long)co * T + ts) * Ci + ci + j] : (uint16_t)0;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int e = tid + 256 * i;
+    const int r = e >> 3, c8 = (e & 7) * 8;
+    const int ci = ci0 + r, co = co0 + c8;
+    if (ci >= Ci || co >= Co) continue;
+    uint16_t* dst = wo + ((long long)ci * T + t) * Co + co;
+    if (vec) {
+      uint4 v;
+      uint16_t* pv = (uint16_t*)&v;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) pv[j] = tile[c8 + j][r];
+      *(uint4*)dst = v;
+    } else {
+      for (int j = 0; j < 8 && co + j < Co; ++j) dst[j] = tile[c8 + j][r];
+    }
+  }
+}
+
+}  // namespace
+
+// n descriptors of 9 words each: {w, wt, ws, Co, T, Ci, flip, (unused), (unused)} as int64
+DBA_EXPORT int dba_transpose_w_batch(const long long* desc, int n, int slots, const int* nvalid, void* stream) {
+  if (n <= 0) return 0;
+  if (n > kMaxTDesc) return -101;
+  TBatch b;
+  int tiles = 0;
+  for (int k = 0; k < n; ++k) {
+    const long long* q = desc + 9 * k;
+    TDesc& d = b.d[k];
+    d.w = (const uint16_t*)q[0];
+    d.wt = (uint16_t*)q[1];
+    d.ws = q[2];
+    d.Co = (int)q[3];
+    d.T = (int)q[4];
+    d.Ci = (int)q[5];
+    d.flip = (int)q[6];
+    d.tiles = ceil_div(d.Co, 64) * ceil_div(d.Ci, 64) * d.T;
+    d.tile0 = tiles;
+    tiles += d.tiles;
+  }
+  b.n = n;
+  b.nvalid = nvalid;
+  hipLaunchKernelGGL(transpose_w_batch_kernel, dim3(tiles, slots), dim3(256), 0, (hipStream_t)stream, b);
+  DBA_LAUNCH_CHECK();
+}
+
 DBA_EXPORT int dba_transpose_w(const void* w, long long w_sstride, void* wt, int slots, int Co, int T, int Ci,
                                int flip, const int* nvalid, void* stream) {
   if (Co % 8 == 0 && Ci % 8 == 0) {

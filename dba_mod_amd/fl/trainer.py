@@ -24,6 +24,7 @@ import torch
 
 from .. import config as C
 from .. import ops
+from ..ops import reference as ref_ops
 from ..models import program as prog
 from ..models.spec import ModelSpec
 from ..utils import native
@@ -103,7 +104,8 @@ class GroupTrainer:
         ctx = prog.Ctx(self.spec, b.state, b.wcomp, None, train=True, grads=b.grads,
                        nvalid=b.nvalid, dropout_seed=b.seed, act_dtype=self.dtype)
         logits = prog.forward(ctx, x)
-        loss, correct, dl = ops.softmax_xent(logits, y, True, True)
+        fused = self.alpha == 1.0     # stats straight from the loss kernel (no extra launches)
+        loss, correct, dl = ops.softmax_xent(logits, y, True, True, *((b.stats, b.slot, b.nvalid) if fused else ()))
         if self.spec.arch == "loan":   # reference LoanNet raises on NaN outputs (loan_model.py:25-26)
             b.nan_flag += torch.isnan(loss).any().float()
         b.grads.zero_()
@@ -115,10 +117,8 @@ class GroupTrainer:
             loss = torch.where(b.trig >= 0, self.alpha * loss + (1.0 - self.alpha) * dist, loss)
         ops.sgd_step(b.state[:, :self.spec.P], b.grads, b.mom, b.lr, b.first, b.active, self.momentum,
                      self.wd, shadow=(b.wcomp if b.wcomp is not b.state else None), fg_accum=b.fg)
-        flat_slot = torch.arange(b.G, device=self.device, dtype=torch.int64) * b.max_slots + b.slot.long()
-        b.stats[0].index_add_(0, flat_slot, loss)
-        b.stats[1].index_add_(0, flat_slot, correct)
-        b.stats[2].index_add_(0, flat_slot, b.nvalid.float())
+        if not fused:
+            ref_ops.accumulate_step_stats(b.stats, b.slot, loss, correct, b.nvalid)
 
     def _buffers(self, G: int, max_slots: int) -> _GroupBuffers:
         key = (G, max_slots)

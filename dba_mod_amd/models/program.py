@@ -34,6 +34,7 @@ class Tape:
         self.nodes: List[Tuple[Tuple[Tensor, ...], Tuple[Optional[Tensor], ...], Callable]] = []
         self._produced: set = set()
         self._grads: Optional[Dict[int, Tensor]] = None
+        self.on_begin: Optional[Callable[[], None]] = None
 
     def record(self, outputs: Tuple[Tensor, ...], inputs: Tuple[Optional[Tensor], ...], bwd: Callable) -> None:
         self.nodes.append((outputs, inputs, bwd))
@@ -50,6 +51,8 @@ class Tape:
         return self._grads.pop(id(t), None) if self._grads is not None else None
 
     def backward(self, out: Tensor, grad: Tensor) -> None:
+        if self.on_begin is not None:
+            self.on_begin()
         grads: Dict[int, Tensor] = {id(out): grad}
         self._grads = grads
         for outputs, inputs, bwd in reversed(self.nodes):
@@ -84,9 +87,24 @@ class Ctx:
         self.spec, self.state, self.wcomp, self.wsel = spec, state, wcomp, wsel
         self.train, self.grads, self.nvalid, self.folded = train, grads, nvalid, folded
         self.tape = Tape() if train else None
+        # data-gradient weight transposes of the whole step, issued as one batched launch
+        # when the backward pass starts (ops.prepare_dgrad_weights)
+        self._dgrad_items: List[tuple] = []
+        self._wt: Dict[int, Tensor] = {}
+        if self.tape is not None:
+            self.tape.on_begin = self._prepare_dgrad
         self.dropout_seed = dropout_seed
         self._drop_ctr = 0
         self.act_dtype = act_dtype
+
+    def _want_dgrad(self, w: Tensor, stride: int, pad: int, in_hw: Tuple[int, int], G: int) -> int:
+        self._dgrad_items.append((w, self.wsel, stride, pad, in_hw, self.nvalid, G))
+        return len(self._dgrad_items) - 1
+
+    def _prepare_dgrad(self) -> None:
+        if self._dgrad_items:
+            self._wt = ops.prepare_dgrad_weights(self._dgrad_items[0][0], self._dgrad_items)
+        self._dgrad_items = []
 
     # ----------------------------------------------------------------- weights
     def w(self, name: str) -> Tensor:
@@ -115,6 +133,7 @@ class Ctx:
         in_hw = (x.shape[2], x.shape[3])
         kh, kw = w.shape[2], w.shape[3]
         need_dx = self.tape.needs_grad(x)
+        k = self._want_dgrad(w, stride, pad, in_hw, x.shape[0]) if need_dx else -1
 
         def bwd(dout: Tensor):
             r = ops.bn_train_bwd(dout, y, out, mean, invstd, gamma, self.nvalid, relu,
@@ -126,7 +145,8 @@ class Ctx:
             if need_dx:
                 # the other consumer of x (shortcut branch) already delivered its gradient
                 acc = self.tape.pop_grad(x)
-                dx = ops.conv2d_dgrad(dy, w, self.wsel, stride, pad, in_hw, nvalid=self.nvalid, accum=acc)
+                dx = ops.conv2d_dgrad(dy, w, self.wsel, stride, pad, in_hw, nvalid=self.nvalid, accum=acc,
+                                      wt=self._wt.get(k))
             return dx, dres
 
         self.tape.record((out,), (x, residual), bwd)
@@ -144,12 +164,13 @@ class Ctx:
         in_hw = (x.shape[2], x.shape[3])
         kh, kw = w.shape[2], w.shape[3]
         need_dx = self.tape.needs_grad(x)
+        k = self._want_dgrad(w, stride, pad, in_hw, x.shape[0]) if need_dx else -1
 
         def bwd(dout: Tensor):
             d = ops.relu_mask_bwd(dout, y) if relu else dout
             ops.conv2d_wgrad(d, x, stride, pad, kh, kw, self.g(name),
                              self.g(bias) if bias is not None else None, nvalid=self.nvalid)
-            return (ops.conv2d_dgrad(d, w, self.wsel, stride, pad, in_hw, nvalid=self.nvalid)
+            return (ops.conv2d_dgrad(d, w, self.wsel, stride, pad, in_hw, nvalid=self.nvalid, wt=self._wt.get(k))
                     if need_dx else None,)
 
         self.tape.record((y,), (x,), bwd)
@@ -176,12 +197,13 @@ class Ctx:
             return y
         need_dx = self.tape.needs_grad(x4)
         gv = self.g(name)
+        k = self._want_dgrad(w, 1, 0, (1, 1), x4.shape[0]) if need_dx else -1
 
         def bwd(dout: Tensor):
             d = ops.relu_mask_bwd(dout, y) if relu else dout
             ops.conv2d_wgrad(d, x4, 1, 0, 1, 1, gv.reshape(gv.shape[0], gv.shape[1], 1, 1, gv.shape[2]),
                              self.g(bias), nvalid=self.nvalid)
-            return (ops.conv2d_dgrad(d, w, self.wsel, 1, 0, (1, 1), nvalid=self.nvalid)
+            return (ops.conv2d_dgrad(d, w, self.wsel, 1, 0, (1, 1), nvalid=self.nvalid, wt=self._wt.get(k))
                     if need_dx else None,)
 
         self.tape.record((y,), (x4,), bwd)

@@ -38,6 +38,7 @@ _SIGS = {
     "dba_conv2_dgrad_w": [_P, _LL, _P, _LL, _P, _P, _P, _LL, _P] + [_I] * 12 + [_P],
     "dba_conv2_dgrad": [_P, _LL, _P, _LL, _P, _P, _P, _LL, _P] + [_I] * 12 + [_P],
     "dba_transpose_w": [_P, _LL, _P, _I, _I, _I, _I, _I, _P, _P],
+    "dba_transpose_w_batch": [_P, _I, _I, _P, _P],
     "dba_halo_conv": [_P, _LL, _P, _LL, _P, _P, _LL, _P, _P, _LL, _I, _P] + [_I] * 9 + [_P],
     "dba_colsum": [_P, _LL, _I, _P, _I, _I, _I, _P, _LL, _P],
     "dba_bn_stats": [_P, _P, _I, _I, _I, _I, _P, _P, _P, _LL, _F, _F, _P, _P, _P],
@@ -53,7 +54,7 @@ _SIGS = {
     "dba_avgpool": [_P, _P, _LL, _I, _I, _P],
     "dba_avgpool_bwd": [_P, _P, _LL, _I, _I, _P],
     "dba_dropout": [_P, _P, _I, _P, _U, _F, _LL, _I, _P],
-    "dba_softmax_xent": [_P, _P, _I, _I, _I, _I, _P, _P, _P, _P],
+    "dba_softmax_xent": [_P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _LL, _P, _I, _P, _P],
     "dba_sgd_step": [_P, _LL, _P, _P, _P, _P, _P, _F, _F, _P, _P, _I, _I, _P],
     "dba_scale_from_base": [_P, _P, _F, _P, _LL, _P],
     "dba_add_noise_scaled": [_P, _P, _LL, _F, _F, _U, _I, _P],
@@ -218,12 +219,60 @@ def conv2d(x, w, wsel, stride, pad, bias=None, residual=None, relu=False, nvalid
     return y
 
 
-def conv2d_dgrad(dy, w, wsel, stride, pad, in_hw, nvalid=None, out_dtype=None, accum=None):
+def _dgrad_flip(w_shape, stride, pad, in_hw) -> Optional[int]:
+    """Which transposed weight copy :func:`conv2d_dgrad` reads: None (none: the persistent
+    kernel gathers transposed fragments in-kernel), 1 (tap-flipped, stride-1 convs run as a
+    forward conv of dY) or 0 (plain transpose, strided / generic dgrad)."""
+    _, Cout, KH, KW, Cin = w_shape
+    H, W = in_hw
+    if stride == 1 and _pconv_ok(Cout, Cin, H, W, KH, KW, stride, pad):
+        return None
+    if _DGRAD_W:
+        return None
+    if stride == 1 and KH == KW and pad == (KH - 1) // 2:
+        return 1
+    return 0
+
+
+_TBATCH_MAX = 32
+
+
+def prepare_dgrad_weights(ref, items):
+    """All of a training step's data-gradient weight transposes in ONE launch.
+
+    ``items``: list of ``(w, wsel, stride, pad, in_hw, nvalid, G)`` for every conv whose input
+    gradient the backward pass will compute.  Returns ``{index: wt}`` to be handed to
+    :func:`conv2d_dgrad` as ``wt=`` (items that need no transpose are absent)."""
+    out = {}
+    desc = []
+    nv_ptr, slots_all = None, None
+    for k, (w, wsel, stride, pad, in_hw, nvalid, G) in enumerate(items):
+        wv, ws = _check_w(w)
+        slots, Cout, KH, KW, Cin = wv.shape
+        flip = _dgrad_flip(wv.shape, stride, pad, in_hw)
+        if flip is None:
+            continue
+        if slots_all is None:
+            slots_all = slots
+            nv_ptr = _ptr(_i32(nvalid)) if (wsel is None and nvalid is not None and slots == G) else None
+        if slots != slots_all or len(desc) >= _TBATCH_MAX:
+            continue                         # left to conv2d_dgrad's own transpose
+        wt = torch.empty(slots, Cin, KH, KW, Cout, dtype=_BF16, device=wv.device)
+        out[k] = wt
+        desc.append([wv.data_ptr(), wt.data_ptr(), ws, Cout, KH * KW, Cin, flip, 0, 0])
+    if desc:
+        d = torch.tensor(desc, dtype=torch.int64)
+        _call("dba_transpose_w_batch", d.data_ptr(), len(desc), slots_all, nv_ptr, _stream())
+    return out
+
+
+def conv2d_dgrad(dy, w, wsel, stride, pad, in_hw, nvalid=None, out_dtype=None, accum=None, wt=None):
     dy = _bf16c(dy)
     G, N, Ho, Wo, Cout = dy.shape
     w, ws = _check_w(w)
     slots, _, KH, KW, Cin = w.shape
     H, W = in_hw
+    have_wt = wt is not None
     dx = torch.empty(G, N, H, W, Cin, dtype=_BF16, device=dy.device)
     acc = _bf16c(accum) if accum is not None else None
     if acc is not None:
@@ -248,12 +297,14 @@ def conv2d_dgrad(dy, w, wsel, stride, pad, in_hw, nvalid=None, out_dtype=None, a
                    KW, stride, pad, _stream())
         if rc != NOT_HANDLED:
             return done(dx)
-    wt = torch.empty(slots, Cin, KH, KW, Cout, dtype=_BF16, device=dy.device)
+    if not have_wt:
+        wt = torch.empty(slots, Cin, KH, KW, Cout, dtype=_BF16, device=dy.device)
     # slot == replica when there is no slot map: inactive replicas' slots need no transpose
     skip = _ptr(_i32(nvalid)) if (wsel is None and nvalid is not None and slots == G) else None
     if stride == 1 and KH == KW and pad == (KH - 1) // 2:
         # stride-1 dgrad == forward conv of dY with tap-flipped, transposed weights
-        _call("dba_transpose_w", w.data_ptr(), ws, wt.data_ptr(), slots, Cout, KH * KW, Cin, 1, skip, _stream())
+        if not have_wt:
+            _call("dba_transpose_w", w.data_ptr(), ws, wt.data_ptr(), slots, Cout, KH * KW, Cin, 1, skip, _stream())
         rc = NOT_HANDLED
         if _GEMM3:
             rc = _call("dba_conv3_fwd", dy.data_ptr(), N * Ho * Wo * Cout, wt.data_ptr(), Cin * KH * KW * Cout,
@@ -267,7 +318,8 @@ def conv2d_dgrad(dy, w, wsel, stride, pad, in_hw, nvalid=None, out_dtype=None, a
                    N, Ho, Wo, Cout, Cin, KH, KH - 1 - pad, 0, _stream())
         if rc != NOT_HANDLED:
             return done(dx)
-    _call("dba_transpose_w", w.data_ptr(), ws, wt.data_ptr(), slots, Cout, KH * KW, Cin, 0, skip, _stream())
+    if not have_wt:
+        _call("dba_transpose_w", w.data_ptr(), ws, wt.data_ptr(), slots, Cout, KH * KW, Cin, 0, skip, _stream())
     args = (dy.data_ptr(), N * Ho * Wo * Cout, wt.data_ptr(), Cin * KH * KW * Cout, _ptr(_i32(wsel)))
     tail = (dx.data_ptr(), N * H * W * Cin, _ptr(_i32(nvalid)), G, N, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad,
             _stream())
@@ -438,14 +490,21 @@ def dropout_bwd(dy, p, seeds, salt):
 
 
 # ---------------------------------------------------------------------------- loss
-def softmax_xent(logits, labels, mean, want_grad):
+def softmax_xent(logits, labels, mean, want_grad, stats=None, slot=None, nvalid=None):
     lf = logits.float().contiguous()
     G, B, C = lf.shape
     loss = torch.empty(G, dtype=torch.float32, device=lf.device)
     correct = torch.empty(G, dtype=torch.float32, device=lf.device)
     dl = torch.empty(G, B, C, dtype=_BF16, device=lf.device) if want_grad else None
+    sp, ss, slp, ms, nvp = None, 0, None, 0, None
+    if stats is not None:
+        assert stats.dtype == torch.float32 and stats.is_contiguous() and stats.shape[0] == 3
+        ms = stats.shape[1] // G
+        assert ms * G == stats.shape[1]
+        slot_, nv_ = _i32(slot), _i32(nvalid)
+        sp, ss, slp, nvp = stats.data_ptr(), stats.shape[1], slot_.data_ptr(), nv_.data_ptr()
     _call("dba_softmax_xent", lf.data_ptr(), _i32(labels).data_ptr(), G, B, C, int(bool(mean)), _ptr(dl),
-          loss.data_ptr(), correct.data_ptr(), _stream())
+          loss.data_ptr(), correct.data_ptr(), sp, ss, slp, ms, nvp, _stream())
     return loss, correct, dl
 
 

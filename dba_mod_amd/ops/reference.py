@@ -132,10 +132,17 @@ def conv2d(x: Tensor, w: Tensor, wsel: Optional[Tensor], stride: int, pad: int,
     return torch.stack(outs).to(out_dtype or x.dtype)
 
 
+def prepare_dgrad_weights(ref: Tensor, items: list) -> dict:
+    """Backend hook for pre-transposed data-gradient weights; the reference needs none."""
+    return {}
+
+
 def conv2d_dgrad(dy: Tensor, w: Tensor, wsel: Optional[Tensor], stride: int, pad: int,
                  in_hw: Tuple[int, int], nvalid: Optional[Tensor] = None,
-                 out_dtype: Optional[torch.dtype] = None, accum: Optional[Tensor] = None) -> Tensor:
-    """dX of a conv; ``accum`` (the input's gradient from another branch) is added in."""
+                 out_dtype: Optional[torch.dtype] = None, accum: Optional[Tensor] = None,
+                 wt: Optional[Tensor] = None) -> Tensor:
+    """dX of a conv; ``accum`` (the input's gradient from another branch) is added in.
+    ``wt`` (a backend's pre-transposed weights) is ignored here."""
     G, N = dy.shape[:2]
     cin = w.shape[-1]
     outs = []
@@ -286,12 +293,15 @@ def dropout_bwd(dy: Tensor, p: float, seeds: Tensor, salt: int) -> Tensor:
 
 
 # ---------------------------------------------------------------------------- loss
-def softmax_xent(logits: Tensor, labels: Tensor, mean: bool, want_grad: bool
-                 ) -> Tuple[Tensor, Tensor, Optional[Tensor]]:
+def softmax_xent(logits: Tensor, labels: Tensor, mean: bool, want_grad: bool,
+                 stats: Optional[Tensor] = None, slot: Optional[Tensor] = None,
+                 nvalid: Optional[Tensor] = None) -> Tuple[Tensor, Tensor, Optional[Tensor]]:
     """Per-group CE (mean over valid rows or sum) + correct count + dlogits (K9).
 
     Rows with label < 0 are padding.  dlogits corresponds to the *mean* loss when
-    ``mean`` (training) and to the sum otherwise.
+    ``mean`` (training) and to the sum otherwise.  With ``stats`` ([3, G*max_slots] fp32),
+    also accumulates (loss, correct, nvalid) of group g into column g*max_slots + slot[g]
+    (the per-client per-internal-epoch training statistics).
     """
     G, B, C = logits.shape
     lf = logits.to(_cdt())
@@ -312,7 +322,19 @@ def softmax_xent(logits: Tensor, labels: Tensor, mean: bool, want_grad: bool
         if mean:
             dl = dl / cnt[:, None, None]
         dl = dl.to(logits.dtype)
+    if stats is not None:
+        accumulate_step_stats(stats, slot, loss, correct, nvalid)
     return loss, correct, dl
+
+
+def accumulate_step_stats(stats: Tensor, slot: Tensor, loss: Tensor, correct: Tensor, nvalid: Tensor) -> None:
+    """stats[:, g*max_slots + slot[g]] += (loss[g], correct[g], nvalid[g])."""
+    G = loss.shape[0]
+    ms = stats.shape[1] // G
+    col = torch.arange(G, device=stats.device, dtype=torch.int64) * ms + slot.long()
+    stats[0].index_add_(0, col, loss.to(stats.dtype))
+    stats[1].index_add_(0, col, correct.to(stats.dtype))
+    stats[2].index_add_(0, col, nvalid.to(stats.dtype))
 
 
 # ------------------------------------------------------------------------- optimizer

@@ -29,6 +29,8 @@ def main(argv=None) -> int:
     ap.add_argument("--config", default=os.path.join(ROOT, "configs", "cifar_params.yaml"))
     ap.add_argument("--epoch", type=int, default=203)
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--clients", type=int, default=0,
+                    help="keep only the k longest clients (k=1: the lone-attacker latency regime)")
     args = ap.parse_args(argv)
     dev = torch.device("cuda")
     p = C.load_params(args.config, {"resumed_model": False, "synthetic_data": True, "overlap_eval": False,
@@ -38,6 +40,8 @@ def main(argv=None) -> int:
     agents, adv = select_clients(p, s.wl, args.epoch)
     plan = build_round_plan(p, s.wl, args.epoch, agents, adv)
     clients = plan.clients
+    if args.clients > 0:
+        clients = sorted(clients, key=lambda c: -len(c.steps))[:args.clients]
     G = len(clients)
     max_slots = max(sum(ph.internal_epochs for ph in c.phases) for c in clients)
     max_slots = 1 << (max_slots - 1).bit_length()

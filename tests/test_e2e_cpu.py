@@ -58,6 +58,19 @@ def test_mnist_dba_round_outputs(tmp_path):
     assert np.isfinite(r12["global_acc"])
 
 
+def test_mnist_single_shot_asr_jumps(tmp_path):
+    """SURVEY §7.3 acceptance: after a benign warm start, the global ASR jumps in the
+    single-shot poison round (adversary 41, round 12; scale 100, eta 0.1 = model
+    replacement, ``image_train.py:166-171``) — BASELINE.json config #1 on CPU."""
+    p = mnist_params(tmp_path, synthetic_train_size=12000, synthetic_test_size=1000, eval_batch_size=500,
+                     pretrain_rounds=5)
+    s = Server(p, DistCtx(), write_outputs=False)
+    r11 = s.run_round(11)
+    r12 = s.run_round(12)
+    assert r11["global_acc"] > 30.0 and r11["global_asr"] < 20.0
+    assert r12["global_asr"] > 50.0
+
+
 def test_resume_continues_round_and_rng(tmp_path):
     p = mnist_params(tmp_path, save_model=True, is_poison=False)
     s = Server(p, DistCtx(), write_outputs=True)

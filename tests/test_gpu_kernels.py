@@ -268,6 +268,23 @@ def test_softmax_xent(H, R):
             _close(l, lr_, 1e-4, 1e-4, "loss")
             assert torch.equal(c.cpu(), cr.cpu())
             _close(d, dr, 1e-2, 1e-3, "dlogits")
+        # fused per-client statistics accumulation (trainer step)
+        G, ms = 4, 8
+        slot = torch.tensor([0, 3, 7, 2], dtype=torch.int32, device=dev)
+        nvalid = (labels >= 0).sum(1).int()
+        sh = torch.rand(3, G * ms, device=dev)
+        sr = sh.clone()
+        H.softmax_xent(logits, labels, True, True, sh, slot, nvalid)
+        R.softmax_xent(logits, labels, True, True, sr, slot, nvalid)
+        _close(sh, sr, 1e-4, 1e-4, "stats")
+    # eval-sized batches (one block handles >256 rows)
+    logits = torch.randn(3, 1000, 10, device=dev) * 3
+    labels = torch.randint(0, 10, (3, 1000), dtype=torch.int32, device=dev)
+    labels[2, 600:] = -1
+    l, c, _ = H.softmax_xent(logits, labels, False, False)
+    lr_, cr, _ = R.softmax_xent(logits, labels, False, False)
+    _close(l, lr_, 1e-4, 1e-4, "loss (eval)")
+    assert torch.equal(c.cpu(), cr.cpu())
 
 
 def test_sgd_step(H, R):
