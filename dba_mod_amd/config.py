@@ -104,6 +104,7 @@ _DEFAULTS: Dict[str, Any] = {
     "nan_check": True,             # abort the run if the aggregated global model is not finite
     "max_update_norm": None,       # RFA update-norm rejection (helper.py:360-369; never enabled there)
     "pretrain_eta": 1.0,
+    "pretrain_lr": None,           # client lr of the warm start (None: the config's lr)
 }
 
 # keys whose value may legitimately be a python list of ints/strings

@@ -197,6 +197,8 @@ LOAN_NAMED_FEATURES = ["num_tl_120dpd_2m", "num_tl_90g_dpd_24m", "pub_rec_bankru
                        "pub_rec", "acc_now_delinq", "tax_liens", "out_prncp",
                        "total_pymnt_inv", "out_prncp_inv", "total_rec_prncp",
                        "last_pymnt_amnt", "all_util"]
+LOAN_COUNT_FEATURES = ["num_tl_120dpd_2m", "num_tl_90g_dpd_24m", "pub_rec_bankruptcies", "pub_rec",
+                       "acc_now_delinq", "tax_liens"]
 LOAN_NUM_FEATURES = 91   # reference loan_model.py:11 in_dim
 LOAN_NUM_CLASSES = 9     # loan_helper.py:149-152
 
@@ -221,6 +223,11 @@ def synthetic_loan(seed: int = 1, total_rows: int = 120000) -> List[TabularDatas
     cols = loan_columns()
     f = len(cols)
     teacher = rng.randn(f, LOAN_NUM_CLASSES).astype(np.float32)
+    # delinquency / public-record counts (the DBA trigger features) are sparse, mostly-zero
+    # and nearly uninformative in LendingClub data: Poisson counts with no teacher weight, so
+    # a trigger writes an outlier value the clean model has no strong opinion about
+    counts = [cols.index(c) for c in LOAN_COUNT_FEATURES]
+    teacher[counts] = 0.0
     prior = np.log(np.array([40, 35, 3, 2, 12, 1.5, 0.5, 3, 3], dtype=np.float32))
     weights = rng.gamma(1.2, 1.0, size=len(US_STATES))
     weights = weights / weights.sum()
@@ -228,6 +235,7 @@ def synthetic_loan(seed: int = 1, total_rows: int = 120000) -> List[TabularDatas
     for si, st in enumerate(US_STATES):
         n = max(60, int(total_rows * weights[si]))
         x = np.abs(rng.randn(n, f).astype(np.float32)) * rng.uniform(0.2, 3.0, size=(1, f)).astype(np.float32)
+        x[:, counts] = rng.poisson(0.05, size=(n, len(counts))).astype(np.float32)
         logits = x @ teacher * 0.6 + prior + rng.randn(n, LOAN_NUM_CLASSES).astype(np.float32) * 0.5
         y = logits.argmax(1).astype(np.int64)
         perm = np.random.RandomState(42 + si).permutation(n)  # stands in for random_state=42

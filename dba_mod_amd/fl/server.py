@@ -99,7 +99,9 @@ class Server:
                 yaml.safe_dump(params.to_plain(), f)
         self.last_round: Dict[str, Any] = {}
         if not params["resumed_model"] and int(params["pretrain_rounds"]) > 0:
-            self.pretrain(int(params["pretrain_rounds"]), float(params["pretrain_eta"]))
+            plr = params["pretrain_lr"]
+            self.pretrain(int(params["pretrain_rounds"]), float(params["pretrain_eta"]),
+                          float(plr) if plr is not None else None)
 
     # ------------------------------------------------------------------ model
     def _init_model(self) -> None:
@@ -127,9 +129,11 @@ class Server:
         if self.d.enabled:   # identical by construction; make it bit-identical anyway
             self.d.broadcast_(self.global_state, 0)
 
-    def pretrain(self, rounds: int, eta: float = 1.0) -> None:
+    def pretrain(self, rounds: int, eta: float = 1.0, lr: Optional[float] = None) -> None:
         """Benign FedAvg warm start: ``rounds`` clean rounds (no attackers, no evaluation,
-        no CSV rows) with server rate ``eta``.
+        no CSV rows) with server rate ``eta`` and client learning rate ``lr`` (default: the
+        config's ``lr``; the attack-phase recipes of LOAN / Tiny use a fine-tuning rate of
+        1e-3 that would need hundreds of rounds to reach a converged starting point).
 
         The reference never trains from scratch: every shipped config resumes a pretrained
         checkpoint (``resumed_model: true``, e.g. ``cifar_pretrain/...epoch_200``) whose
@@ -142,8 +146,10 @@ class Server:
         if rounds <= 0:
             return
         p = self.params
-        saved = {k: p[k] for k in ("is_poison", "eta", "aggregation_methods")}
+        saved = {k: p[k] for k in ("is_poison", "eta", "aggregation_methods", "lr")}
         p.update({"is_poison": False, "eta": float(eta), "aggregation_methods": C.AGGR_MEAN})
+        if lr is not None:
+            p["lr"] = float(lr)
         try:
             for e in range(1, rounds + 1):
                 self._train_half(e)
@@ -152,7 +158,7 @@ class Server:
             self.timer.reset()
         if self.device.type == "cuda":
             torch.cuda.synchronize(self.device)
-        log.info(f"pretrained {rounds} benign rounds (eta {eta})")
+        log.info(f"pretrained {rounds} benign rounds (eta {eta}, lr {lr if lr is not None else p['lr']})")
 
     # ------------------------------------------------------------------ round
     # ------------------------------------------------------------------ round

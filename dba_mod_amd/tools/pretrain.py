@@ -26,6 +26,7 @@ def main(argv=None) -> int:
     ap.add_argument("--params", required=True)
     ap.add_argument("--rounds", type=int, default=50)
     ap.add_argument("--eta", type=float, default=1.0)
+    ap.add_argument("--lr", type=float, default=None, help="client lr of the warm start (default: pretrain_lr / lr)")
     ap.add_argument("--out", required=True)
     ap.add_argument("--cpu", action="store_true")
     ap.add_argument("--set", dest="overrides", nargs="*", default=[])
@@ -35,7 +36,8 @@ def main(argv=None) -> int:
     params = C.load_params(args.params, over)
     dctx = init_distributed(prefer_gpu=not args.cpu)
     server = Server(params, dctx, write_outputs=False)
-    server.pretrain(args.rounds, args.eta)
+    plr = args.lr if args.lr is not None else params["pretrain_lr"]
+    server.pretrain(args.rounds, args.eta, float(plr) if plr is not None else None)
     if dctx.is_main:
         os.makedirs(os.path.dirname(os.path.abspath(args.out)), exist_ok=True)
         ckpt.save_checkpoint(args.out, server.spec, server.global_state, args.rounds, float(params["lr"]),
