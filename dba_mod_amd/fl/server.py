@@ -8,6 +8,7 @@ with one counter all-reduce → CSV rows / checkpoint / metrics on rank 0.
 """
 from __future__ import annotations
 
+import dataclasses
 import datetime
 import logging
 import os
@@ -24,6 +25,7 @@ from ..parallel.dist import DistCtx
 from ..utils import checkpoint as ckpt
 from ..utils import native
 from ..utils.csv_record import CsvRecorder
+from ..utils.devcopy import to_device
 from ..utils.observability import MetricsStream, PhaseTimer, Plotter, dict_html, setup_logger
 from . import aggregate as agg
 from .evaluate import Evaluator
@@ -32,6 +34,46 @@ from .trainer import ClientResult, GroupTrainer
 from .workload import Workload, build_workload
 
 log = logging.getLogger("logger")
+
+
+class _EarlyEval:
+    """Enqueues a client's local tests (``image_train.py:139-160,268-299``: clean / poison /
+    own-trigger tests of its own snapshots) the moment its last phase ends.
+
+    Benign clients finish long before a 6-epoch attacker: their local tests then run on the
+    eval stream underneath the latency-bound tail of the round's training instead of after
+    it.  They are evaluated by the client's owner rank over the WHOLE test set (the snapshot
+    exists only there before the gather); the global-model tests stay image-sharded
+    (:meth:`Server._launch_eval_impl`).  Either way the ``[jobs, 3]`` counters are summed
+    across ranks by the one all-reduce in :meth:`Server._finish`."""
+
+    def __init__(self, server: "Server", plan: RoundPlan) -> None:
+        self.server, self.plan = server, plan
+        self.acc = torch.zeros(len(plan.jobs), 3, dtype=torch.float64, device=server.device)
+        self.done: set = set()
+        self.keep: List[torch.Tensor] = []     # mini-banks read by the eval stream
+        owner: Dict[int, Any] = {}
+        for c in plan.clients:
+            for ph in c.phases:
+                for sl in (ph.pre_scale_snap, ph.post_snap):
+                    if sl is not None:
+                        owner[sl] = c.name
+        self.by_client: Dict[Any, List[int]] = {}
+        for j, job in enumerate(plan.jobs):
+            if job.model != 0:
+                self.by_client.setdefault(owner[job.model], []).append(j)
+
+    def __call__(self, client: ClientPlan, snaps: Dict[int, torch.Tensor]) -> None:
+        js = self.by_client.get(client.name)
+        if not js:
+            return
+        slots = sorted({self.plan.jobs[j].model for j in js})
+        remap = {sl: i for i, sl in enumerate(slots)}
+        bank = torch.stack([snaps[sl] for sl in slots])
+        jobs = [dataclasses.replace(self.plan.jobs[j], model=remap[self.plan.jobs[j].model]) for j in js]
+        self.server._enqueue_eval(bank, jobs, js, self.acc, sharded=False)
+        self.keep.append(bank)
+        self.done.update(js)
 
 
 def compute_dtype_for(params: C.Params, device: torch.device) -> torch.dtype:
@@ -86,6 +128,7 @@ class Server:
         self.best_loss = float("inf")
         self.timer = PhaseTimer(self.device)
         self._pending: Optional[Dict[str, Any]] = None
+        self._completed: List[Dict[str, Any]] = []    # rounds finished inside _train_half (LOAN)
         self._eval_stream = None
         if self.device.type == "cuda" and bool(params.get("overlap_eval", True)):
             # training runs on a HIGH-priority stream (its kernels are small and latency-bound,
@@ -152,7 +195,7 @@ class Server:
             p["lr"] = float(lr)
         try:
             for e in range(1, rounds + 1):
-                self._train_half(e)
+                self._train_half(e, evaluate=False)
         finally:
             p.update(saved)
             self.timer.reset()
@@ -168,7 +211,7 @@ class Server:
     #                   enqueued on a LOW-priority stream, then CSV/checkpoint once it lands.
     # Round r+1's training needs only the aggregated weights, never round r's test results,
     # so the eval of round r runs underneath the (latency-bound) training of round r+1.
-    def _train_half(self, epoch: int) -> Dict[str, Any]:
+    def _train_half(self, epoch: int, evaluate: bool = True) -> Dict[str, Any]:
         p = self.params
         t0 = time.perf_counter()
         with self.timer.phase("select"):
@@ -176,15 +219,16 @@ class Server:
         log.info(f"Server Epoch:{epoch} choose agents : {agents}.")
         pre_acc = None
         if p.type == C.TYPE_LOAN and p["is_poison"] and not p["baseline"] and adversarial:
-            self.flush()
+            self._completed.extend(self.flush())
             pre_acc = self._loan_preeval()
         with self.timer.phase("plan", sync=False):
             plan = build_round_plan(p, self.wl, epoch, agents, adversarial, pre_acc)
             costs = [c.cost for c in plan.clients]
             owners, _ = native.lpt_assign(costs, self.d.world)
             mine = [c for c, o in zip(plan.clients, owners) if o == self.d.rank]
+        early = _EarlyEval(self, plan) if (evaluate and p["early_local_eval"]) else None
         with self.timer.phase("train"):
-            results = self.trainer.train(mine, self.global_state)
+            results = self.trainer.train(mine, self.global_state, on_client_done=early)
         with self.timer.phase("gather"):
             bank, fg_grads, cstats = self._gather(plan, owners, results)
         with self.timer.phase("aggregate"):
@@ -195,7 +239,7 @@ class Server:
                 raise FloatingPointError(f"round {epoch}: aggregated global model is not finite "
                                          f"(aggregation={p['aggregation_methods']})")
         return {"epoch": epoch, "plan": plan, "bank": bank, "cstats": cstats, "t0": t0,
-                "clients_on_rank": len(mine), "phases": self.timer.reset()}
+                "clients_on_rank": len(mine), "phases": self.timer.reset(), "early": early}
 
     def _launch_eval(self, pend: Dict[str, Any]) -> None:
         """Enqueue the round's evaluation on the eval stream (returns immediately)."""
@@ -205,15 +249,38 @@ class Server:
         finally:
             pend["phases"]["launch_eval"] = time.perf_counter() - t0
 
-    def _launch_eval_impl(self, pend: Dict[str, Any]) -> None:
+    def _enqueue_eval(self, bank: torch.Tensor, jobs: List[Any], rows: List[int], acc: torch.Tensor,
+                      sharded: bool) -> None:
+        """Evaluate ``jobs`` (models = rows of ``bank``) into ``acc[rows]`` on the eval stream,
+        ordered after everything already enqueued on the current (training) stream.
+        ``sharded``: this rank takes its ``[rank::world]`` image shard (the all-reduce in
+        :meth:`_finish` sums the shards); otherwise it evaluates every image."""
+        rank, world = (self.d.rank, self.d.world) if sharded else (0, 1)
         if self._eval_stream is None:
-            pend["acc"] = self.evaluator.run(pend["bank"], pend["plan"].jobs, self.d.rank, self.d.world)
+            acc.index_add_(0, to_device(rows, self.device, torch.int64), self.evaluator.run(bank, jobs, rank, world))
             return
         ready = torch.cuda.Event()
         ready.record(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(self._eval_stream):
+            # everything this eval allocates lives on the eval stream; the only training-stream
+            # tensors it reads (bank, acc) are kept referenced until _finish has waited for it
+            # (a freed training-stream block is reused at once by the training stream)
             self._eval_stream.wait_event(ready)
-            pend["acc"] = self.evaluator.run(pend["bank"], pend["plan"].jobs, self.d.rank, self.d.world)
+            idx = to_device(rows, self.device, torch.int64)
+            acc.index_add_(0, idx, self.evaluator.run(bank, jobs, rank, world))
+
+    def _launch_eval_impl(self, pend: Dict[str, Any]) -> None:
+        plan = pend["plan"]
+        early = pend.get("early")
+        if early is not None:
+            acc, done = early.acc, early.done
+        else:
+            acc, done = torch.zeros(len(plan.jobs), 3, dtype=torch.float64, device=self.device), set()
+        pend["acc"] = acc
+        rest = [j for j in range(len(plan.jobs)) if j not in done]
+        if rest:
+            self._enqueue_eval(pend["bank"], [plan.jobs[j] for j in rest], rest, acc, sharded=True)
+        if self._eval_stream is not None:
             pend["done"] = torch.cuda.Event()
             pend["done"].record(self._eval_stream)
 
@@ -244,6 +311,7 @@ class Server:
         """One complete round, evaluated before returning (no overlap)."""
         self.flush()
         pend = self._train_half(epoch)
+        self._completed = []
         self._launch_eval(pend)
         return self._finish(pend)
 
@@ -252,6 +320,8 @@ class Server:
         out: List[Dict[str, Any]] = []
         for epoch in epochs:
             pend = self._train_half(epoch)
+            out.extend(self._completed)
+            self._completed = []
             if self._pending is not None:
                 out.append(self._finish(self._pending))
                 self._pending = None

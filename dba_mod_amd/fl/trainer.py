@@ -17,7 +17,7 @@ from __future__ import annotations
 import logging
 import struct
 from dataclasses import dataclass, field
-from typing import Any, Dict, List, Optional, Tuple
+from typing import Any, Callable, Dict, List, Optional, Tuple
 
 import numpy as np
 import torch
@@ -148,13 +148,19 @@ class GroupTrainer:
         b.graph.replay()
 
     # ----------------------------------------------------------------- train
-    def train(self, clients: List[ClientPlan], global_state: torch.Tensor) -> List[ClientResult]:
+    def train(self, clients: List[ClientPlan], global_state: torch.Tensor,
+              on_client_done: Optional[Callable[[ClientPlan, Dict[int, torch.Tensor]], None]] = None
+              ) -> List[ClientResult]:
+        """Train ``clients`` from ``global_state``.  ``on_client_done(client, snapshots)`` is
+        called (host side, in stream order) the moment a client's last phase has ended, so its
+        local tests can be enqueued while the other clients are still training."""
         out: List[ClientResult] = []
         for w0 in range(0, len(clients), self.max_groups):
-            out.extend(self._train_wave(clients[w0:w0 + self.max_groups], global_state))
+            out.extend(self._train_wave(clients[w0:w0 + self.max_groups], global_state, on_client_done))
         return out
 
-    def _train_wave(self, clients: List[ClientPlan], global_state: torch.Tensor) -> List[ClientResult]:
+    def _train_wave(self, clients: List[ClientPlan], global_state: torch.Tensor,
+                    on_client_done=None) -> List[ClientResult]:
         G = len(clients)
         if G == 0:
             return []
@@ -179,6 +185,8 @@ class GroupTrainer:
             self._run_step(b)
             for (g, ph) in events.get(t + 1, []):
                 self._phase_end(b, g, ph, snaps, pend_dist)
+                if on_client_done is not None and ph is clients[g].phases[-1]:
+                    on_client_done(clients[g], snaps[g])
         res: List[ClientResult] = []
         stats = b.stats.view(3, G, b.max_slots).permute(1, 2, 0).cpu().numpy()
         if self.spec.arch == "loan" and float(b.nan_flag.item()) > 0:
