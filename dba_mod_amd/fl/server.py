@@ -52,6 +52,7 @@ class _EarlyEval:
         self.acc = torch.zeros(len(plan.jobs), 3, dtype=torch.float64, device=server.device)
         self.done: set = set()
         self.keep: List[torch.Tensor] = []     # mini-banks read by the eval stream
+        self.event: Optional[torch.cuda.Event] = None   # recorded once the last one is enqueued
         owner: Dict[int, Any] = {}
         for c in plan.clients:
             for ph in c.phases:
@@ -62,16 +63,22 @@ class _EarlyEval:
         for j, job in enumerate(plan.jobs):
             if job.model != 0:
                 self.by_client.setdefault(owner[job.model], []).append(j)
+        # on N > 1 ranks the round's longest clients (the 6-epoch attackers) finish last and
+        # their owner would evaluate them alone while the other ranks idle: their tests go
+        # through the image-sharded path instead (on one GPU early is still better: -2 %)
+        longest = max((len(c.steps) for c in plan.clients), default=0)
+        self.late = ({c.name for c in plan.clients if len(c.steps) == longest}
+                     if server.d.world > 1 else set())
 
     def __call__(self, client: ClientPlan, snaps: Dict[int, torch.Tensor]) -> None:
         js = self.by_client.get(client.name)
-        if not js:
+        if not js or client.name in self.late:
             return
         slots = sorted({self.plan.jobs[j].model for j in js})
         remap = {sl: i for i, sl in enumerate(slots)}
         bank = torch.stack([snaps[sl] for sl in slots])
         jobs = [dataclasses.replace(self.plan.jobs[j], model=remap[self.plan.jobs[j].model]) for j in js]
-        self.server._enqueue_eval(bank, jobs, js, self.acc, sharded=False)
+        self.server._enqueue_eval(bank, jobs, js, self.acc, sharded=False, stream=self.server._early_stream)
         self.keep.append(bank)
         self.done.update(js)
 
@@ -127,9 +134,11 @@ class Server:
         self.plot.text(dict_html(params, self.current_time))
         self.best_loss = float("inf")
         self.timer = PhaseTimer(self.device)
-        self._pending: Optional[Dict[str, Any]] = None
         self._completed: List[Dict[str, Any]] = []    # rounds finished inside _train_half (LOAN)
         self._eval_stream = None
+        self._early_stream = None
+        self._unlaunched: Optional[Dict[str, Any]] = None    # trained + aggregated, eval not enqueued
+        self._launched: List[Dict[str, Any]] = []             # eval enqueued, not yet recorded
         if self.device.type == "cuda" and bool(params.get("overlap_eval", True)):
             # training runs on a HIGH-priority stream (its kernels are small and latency-bound,
             # they win every CU that frees up); evaluation fills the rest at default priority
@@ -137,6 +146,10 @@ class Server:
             self._main_stream = torch.cuda.Stream(self.device, priority=-1)
             torch.cuda.set_stream(self._main_stream)
             self._eval_stream = torch.cuda.Stream(self.device, priority=0)
+            # local tests of clients that finished training get their own low-priority stream,
+            # so the global tests of round r (ready at once) never queue behind the local tests
+            # of round r+1 (each waiting for its client to finish)
+            self._early_stream = torch.cuda.Stream(self.device, priority=0)
         if self.write:
             with open(os.path.join(self.folder, "params.yaml"), "w") as f:
                 yaml.safe_dump(params.to_plain(), f)
@@ -211,7 +224,8 @@ class Server:
     #                   enqueued on a LOW-priority stream, then CSV/checkpoint once it lands.
     # Round r+1's training needs only the aggregated weights, never round r's test results,
     # so the eval of round r runs underneath the (latency-bound) training of round r+1.
-    def _train_half(self, epoch: int, evaluate: bool = True) -> Dict[str, Any]:
+    def _train_begin(self, epoch: int, evaluate: bool = True) -> Dict[str, Any]:
+        """Select, plan and ENQUEUE the round's local training (returns while the GPU trains)."""
         p = self.params
         t0 = time.perf_counter()
         with self.timer.phase("select"):
@@ -227,19 +241,34 @@ class Server:
             owners, _ = native.lpt_assign(costs, self.d.world)
             mine = [c for c, o in zip(plan.clients, owners) if o == self.d.rank]
         early = _EarlyEval(self, plan) if (evaluate and p["early_local_eval"]) else None
+        with self.timer.phase("train_enqueue", sync=False):
+            handle = self.trainer.train_async(mine, self.global_state, on_client_done=early)
+        return {"epoch": epoch, "plan": plan, "owners": owners, "adversarial": adversarial, "t0": t0,
+                "handle": handle, "early": early, "clients_on_rank": len(mine)}
+
+    def _train_end(self, st: Dict[str, Any]) -> Dict[str, Any]:
+        """Wait for the round's training, gather the snapshots, aggregate."""
+        p = self.params
+        plan, epoch, early = st["plan"], st["epoch"], st["early"]
         with self.timer.phase("train"):
-            results = self.trainer.train(mine, self.global_state, on_client_done=early)
+            results = st["handle"].collect()
+        if early is not None and self._early_stream is not None:
+            early.event = torch.cuda.Event()        # every local test of this round is enqueued
+            early.event.record(self._early_stream)
         with self.timer.phase("gather"):
-            bank, fg_grads, cstats = self._gather(plan, owners, results)
+            bank, fg_grads, cstats = self._gather(plan, st["owners"], results)
         with self.timer.phase("aggregate"):
-            self._aggregate(plan, bank, fg_grads, adversarial)
+            self._aggregate(plan, bank, fg_grads, st["adversarial"])
             bank[0].copy_(self.global_state)
             if p["nan_check"] and not bool(torch.isfinite(self.global_state).all()):
                 # fail fast (SURVEY §5.3): a non-finite global model poisons every later round
                 raise FloatingPointError(f"round {epoch}: aggregated global model is not finite "
                                          f"(aggregation={p['aggregation_methods']})")
-        return {"epoch": epoch, "plan": plan, "bank": bank, "cstats": cstats, "t0": t0,
-                "clients_on_rank": len(mine), "phases": self.timer.reset(), "early": early}
+        return {"epoch": epoch, "plan": plan, "bank": bank, "cstats": cstats, "t0": st["t0"],
+                "clients_on_rank": st["clients_on_rank"], "phases": self.timer.reset(), "early": early}
+
+    def _train_half(self, epoch: int, evaluate: bool = True) -> Dict[str, Any]:
+        return self._train_end(self._train_begin(epoch, evaluate))
 
     def _launch_eval(self, pend: Dict[str, Any]) -> None:
         """Enqueue the round's evaluation on the eval stream (returns immediately)."""
@@ -250,22 +279,23 @@ class Server:
             pend["phases"]["launch_eval"] = time.perf_counter() - t0
 
     def _enqueue_eval(self, bank: torch.Tensor, jobs: List[Any], rows: List[int], acc: torch.Tensor,
-                      sharded: bool) -> None:
+                      sharded: bool, stream=None) -> None:
         """Evaluate ``jobs`` (models = rows of ``bank``) into ``acc[rows]`` on the eval stream,
         ordered after everything already enqueued on the current (training) stream.
         ``sharded``: this rank takes its ``[rank::world]`` image shard (the all-reduce in
         :meth:`_finish` sums the shards); otherwise it evaluates every image."""
         rank, world = (self.d.rank, self.d.world) if sharded else (0, 1)
-        if self._eval_stream is None:
+        stream = stream if stream is not None else self._eval_stream
+        if stream is None:
             acc.index_add_(0, to_device(rows, self.device, torch.int64), self.evaluator.run(bank, jobs, rank, world))
             return
         ready = torch.cuda.Event()
         ready.record(torch.cuda.current_stream(self.device))
-        with torch.cuda.stream(self._eval_stream):
+        with torch.cuda.stream(stream):
             # everything this eval allocates lives on the eval stream; the only training-stream
             # tensors it reads (bank, acc) are kept referenced until _finish has waited for it
             # (a freed training-stream block is reused at once by the training stream)
-            self._eval_stream.wait_event(ready)
+            stream.wait_event(ready)
             idx = to_device(rows, self.device, torch.int64)
             acc.index_add_(0, idx, self.evaluator.run(bank, jobs, rank, world))
 
@@ -283,13 +313,16 @@ class Server:
         if self._eval_stream is not None:
             pend["done"] = torch.cuda.Event()
             pend["done"].record(self._eval_stream)
+            if early is not None and getattr(early, "event", None) is not None:
+                pend["done_early"] = early.event
 
     def _finish(self, pend: Dict[str, Any]) -> Dict[str, Any]:
         p = self.params
         t_wait = time.perf_counter()
         acc = pend["acc"]
-        if "done" in pend:
-            torch.cuda.current_stream(self.device).wait_event(pend["done"])
+        for ev in ("done", "done_early"):
+            if ev in pend:
+                torch.cuda.current_stream(self.device).wait_event(pend[ev])
         self.d.all_reduce_(acc)
         res = acc.cpu().numpy()
         t_io = time.perf_counter()
@@ -316,25 +349,36 @@ class Server:
         return self._finish(pend)
 
     def run_rounds(self, epochs) -> List[Dict[str, Any]]:
-        """Pipelined rounds: round r's evaluation overlaps round r+1's training."""
+        """Pipelined rounds.  Per iteration: enqueue round r's training (the GPU starts at
+        once); then, while it runs, enqueue round r-1's global tests and record round r-2
+        (its tests ran underneath round r-1's training); then wait for round r's training and
+        aggregate.  The host work between two rounds' training is only gather + aggregate +
+        select + plan.  Every rank runs this same sequence, so collectives stay ordered."""
         out: List[Dict[str, Any]] = []
         for epoch in epochs:
-            pend = self._train_half(epoch)
+            st = self._train_begin(epoch)
             out.extend(self._completed)
             self._completed = []
-            if self._pending is not None:
-                out.append(self._finish(self._pending))
-                self._pending = None
-            self._launch_eval(pend)
-            self._pending = pend
+            if self._unlaunched is not None:
+                self._launch_eval(self._unlaunched)
+                self._launched.append(self._unlaunched)
+                self._unlaunched = None
+            while len(self._launched) > 1:
+                out.append(self._finish(self._launched.pop(0)))
+            self._unlaunched = self._train_end(st)
         out.extend(self.flush())
         return out
 
     def flush(self) -> List[Dict[str, Any]]:
-        if self._pending is None:
-            return []
-        pend, self._pending = self._pending, None
-        return [self._finish(pend)]
+        """Enqueue and record every round still in flight, oldest first."""
+        if self._unlaunched is not None:
+            self._launch_eval(self._unlaunched)
+            self._launched.append(self._unlaunched)
+            self._unlaunched = None
+        out = []
+        while self._launched:
+            out.append(self._finish(self._launched.pop(0)))
+        return out
 
     def run(self) -> None:
         p = self.params

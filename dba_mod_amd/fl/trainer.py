@@ -73,6 +73,18 @@ class _GroupBuffers:
         self.graph: Optional[torch.cuda.CUDAGraph] = None
 
 
+class _TrainHandle:
+    """Training enqueued by :meth:`GroupTrainer.train_async`; ``collect()`` waits for it."""
+
+    def __init__(self, trainer: "GroupTrainer", done: List[ClientResult], last) -> None:
+        self.trainer, self.done, self.last = trainer, done, last
+
+    def collect(self) -> List[ClientResult]:
+        out = self.done + self.trainer._wave_collect(self.last)
+        self.last = None
+        return out
+
+
 class GroupTrainer:
     def __init__(self, wl: Workload, params: C.Params, compute_dtype: torch.dtype,
                  max_groups: int = 16) -> None:
@@ -154,16 +166,27 @@ class GroupTrainer:
         """Train ``clients`` from ``global_state``.  ``on_client_done(client, snapshots)`` is
         called (host side, in stream order) the moment a client's last phase has ended, so its
         local tests can be enqueued while the other clients are still training."""
-        out: List[ClientResult] = []
-        for w0 in range(0, len(clients), self.max_groups):
-            out.extend(self._train_wave(clients[w0:w0 + self.max_groups], global_state, on_client_done))
-        return out
+        return self.train_async(clients, global_state, on_client_done).collect()
 
-    def _train_wave(self, clients: List[ClientPlan], global_state: torch.Tensor,
-                    on_client_done=None) -> List[ClientResult]:
+    def train_async(self, clients: List[ClientPlan], global_state: torch.Tensor,
+                    on_client_done=None) -> "_TrainHandle":
+        """Enqueue the training of ``clients`` and return without waiting for the GPU (only
+        earlier waves of a rank holding more than ``max_groups`` clients are collected
+        synchronously: they share buffers with the next wave).  ``collect()`` synchronises
+        and returns the results."""
+        done: List[ClientResult] = []
+        last = None
+        for w0 in range(0, len(clients), self.max_groups):
+            if last is not None:
+                done.extend(self._wave_collect(last))
+            last = self._wave_enqueue(clients[w0:w0 + self.max_groups], global_state, on_client_done)
+        return _TrainHandle(self, done, last)
+
+    def _wave_enqueue(self, clients: List[ClientPlan], global_state: torch.Tensor,
+                      on_client_done=None) -> Optional[Dict[str, Any]]:
         G = len(clients)
         if G == 0:
-            return []
+            return None
         max_slots = max(sum(ph.internal_epochs for ph in c.phases) for c in clients)
         max_slots = 1 << (max_slots - 1).bit_length()
         b = self._buffers(G, max_slots)
@@ -178,7 +201,6 @@ class GroupTrainer:
 
         events = self._events(clients)
         snaps: Dict[int, Dict[int, torch.Tensor]] = {g: {} for g in range(G)}
-        dists: Dict[int, Dict[int, float]] = {g: {} for g in range(G)}
         pend_dist: List[Tuple[int, int, torch.Tensor]] = []
         for t in range(T):
             b.desc.copy_(sched[t], non_blocking=True)
@@ -187,11 +209,19 @@ class GroupTrainer:
                 self._phase_end(b, g, ph, snaps, pend_dist)
                 if on_client_done is not None and ph is clients[g].phases[-1]:
                     on_client_done(clients[g], snaps[g])
+        return {"b": b, "clients": clients, "snaps": snaps, "pend_dist": pend_dist, "sched": sched}
+
+    def _wave_collect(self, w: Optional[Dict[str, Any]]) -> List[ClientResult]:
+        if w is None:
+            return []
+        b, clients, snaps = w["b"], w["clients"], w["snaps"]
+        G = len(clients)
         res: List[ClientResult] = []
         stats = b.stats.view(3, G, b.max_slots).permute(1, 2, 0).cpu().numpy()
         if self.spec.arch == "loan" and float(b.nan_flag.item()) > 0:
             raise ValueError("NaN in LoanNet forward (reference loan_model.py:25-26)")
-        for g, e, d in pend_dist:
+        dists: Dict[int, Dict[int, float]] = {g: {} for g in range(G)}
+        for g, e, d in w["pend_dist"]:
             dists[g][e] = float(d.sqrt().item())
         for g, c in enumerate(clients):
             nsl = sum(ph.internal_epochs for ph in c.phases)

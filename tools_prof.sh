@@ -1,7 +1,7 @@
 R=$GRAFT_REPO_ROOT
 mkdir -p $R/gpurun_out/prof
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof -o bench -- python3 $R/bench.py --steps 4 --warmup 1 > $R/gpurun_out/prof/bench_stdout.log 2>&1
+timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof -o bench -- python3 $R/bench.py --steps 4 --warmup 1 --pretrain-rounds 3 > $R/gpurun_out/prof/bench_stdout.log 2>&1
 rc=$?; echo "rc=$rc" >> $R/gpurun_out/prof/bench_stdout.log
 find $R/gpurun_out/prof -name "*.csv" | head -20 >> $R/gpurun_out/prof/bench_stdout.log
 exit $rc
