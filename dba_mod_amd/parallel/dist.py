@@ -10,7 +10,12 @@ This framework's distributed round (client-parallel DP):
    clients ≈ 112 MB, a fraction of a millisecond of xGMI time;
 4. aggregation is applied redundantly on every rank (bit-identical global model, no
    broadcast);
-5. evaluation is image-sharded across ranks; ONE all-reduce of the ``[jobs, 3]`` counters.
+5. a client's local tests run on its owner rank as soon as it finishes training (the longest
+   clients' and the global model's tests are image-sharded across ranks); ONE all-reduce of
+   the ``[jobs, 3]`` counters combines both.
+
+On a one-GPU box the multi-rank path is rehearsed with ``DBA_SHARE_GPU=1`` (every rank on
+device 0) and ``DBA_DIST_BACKEND=gloo`` (``tests/test_gpu_dist.py``).
 
 Bucket policy: payloads are single contiguous flat buffers (never per-layer calls); rows
 are padded so every rank contributes the same ``[k_max, S]`` block, which is what RCCL's
@@ -89,22 +94,25 @@ def init_distributed(prefer_gpu: bool = True, timeout_s: int = 1800) -> DistCtx:
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     use_gpu = prefer_gpu and torch.cuda.is_available()
+    # rehearsal knobs for a one-GPU box: DBA_SHARE_GPU=1 puts every rank on device 0 and
+    # DBA_DIST_BACKEND=gloo replaces RCCL (which refuses two ranks on one GPU)
+    dev_index = 0 if os.environ.get("DBA_SHARE_GPU") == "1" else local
     if use_gpu:
-        torch.cuda.set_device(local)
-        device = torch.device("cuda", local)
+        torch.cuda.set_device(dev_index)
+        device = torch.device("cuda", dev_index)
     else:
         device = torch.device("cpu")
     if world <= 1:
         return DistCtx(0, 1, 0, device, "none")
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-    backend = "nccl" if use_gpu else "gloo"   # "nccl" is RCCL on ROCm
+    backend = os.environ.get("DBA_DIST_BACKEND") or ("nccl" if use_gpu else "gloo")   # "nccl" is RCCL
     kw = dict(backend=backend, rank=rank, world_size=world,
               timeout=datetime.timedelta(seconds=timeout_s))
     if backend == "nccl":
         kw["device_id"] = device
     if not dist.is_initialized():
         dist.init_process_group(**kw)
-    return DistCtx(rank, world, local, device, backend)
+    return DistCtx(rank, world, dev_index, device, backend)
 
 
 def shutdown(ctx: DistCtx) -> None:
