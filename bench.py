@@ -103,8 +103,11 @@ def main() -> int:
     elapsed = dctx.all_reduce_max(time.perf_counter() - t0)
     rps = args.steps / elapsed if elapsed > 0 else 0.0
     if dctx.is_main:
+        metric = METRIC if params.type == "cifar" else (
+            f"FL rounds/sec + backdoor ASR & main-task acc, {MODEL_NAMES.get(params.type, params.type)} "
+            f"{int(params['number_of_total_participants'])} clients")
         out = {
-            "metric": METRIC, "value": round(rps, 4), "unit": "rounds/s", "n_gpus": dctx.world,
+            "metric": metric, "value": round(rps, 4), "unit": "rounds/s", "n_gpus": dctx.world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1000.0 * elapsed / max(1, args.steps), 2),
             "higher_is_better": True, "scaling": "strong",
             "vs_baseline": round(rps / BASELINE_ROUNDS_PER_S, 2) if params.type == "cifar" else None,

@@ -47,6 +47,7 @@ CONV_CASES = [
     (2, 3, 8, 8, 128, 256, 3, 2, 1),     # layer4.0.conv1
     (2, 3, 64, 64, 3, 64, 7, 2, 3),      # Tiny stem
     (2, 6, 28, 28, 1, 20, 5, 1, 0),      # MnistNet conv1
+    (2, 64, 28, 28, 1, 20, 5, 1, 0),     # MnistNet conv1, full batch (multi-block bias grad)
     (2, 6, 12, 12, 20, 50, 5, 1, 0),     # MnistNet conv2
     (3, 7, 1, 1, 800, 500, 1, 1, 0),     # fc1 as 1x1
     (3, 7, 1, 1, 256, 10, 1, 1, 0),      # CIFAR linear
