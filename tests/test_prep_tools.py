@@ -7,6 +7,8 @@ import pandas as pd
 from dba_mod_amd.data import readers
 from dba_mod_amd.tools import prep_loan, prep_tiny
 
+from conftest import ROOT
+
 
 def test_loan_preprocess_encodes_scales_and_splits(tmp_path):
     n = 60
@@ -51,3 +53,17 @@ def test_tiny_reformat_moves_val_images(tmp_path):
     assert sorted(os.listdir(root / "val")) == ["n01", "n02"]
     assert sorted(os.listdir(root / "val" / "n01")) == ["val_0.JPEG", "val_2.JPEG"]
     assert prep_tiny.reformat_val(str(root)) == 0                  # idempotent
+
+
+def test_partition_report_reproduces_attacker_shards(tmp_path):
+    """Split self-check / Dirichlet plot tool (reference image_helper.py:112-146,352-378):
+    the CIFAR attackers' shard sizes are the ones annotated in cifar_params.yaml."""
+    import csv as _csv
+    from dba_mod_amd.tools import partition_report
+    out = tmp_path / "split.csv"
+    pdf = tmp_path / "split.pdf"
+    assert partition_report.main(["--params", os.path.join(ROOT, "configs", "cifar_params.yaml"),
+                                  "--set", "synthetic_data=true", "--csv", str(out), "--plot", str(pdf)]) == 0
+    rows = {r["participant"]: int(r["total"]) for r in _csv.DictReader(open(out))}
+    assert [rows[k] for k in ("17", "33", "77", "11")] == [526, 527, 496, 546]
+    assert pdf.stat().st_size > 0
