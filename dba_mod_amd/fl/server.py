@@ -255,6 +255,8 @@ class Server:
         if early is not None and self._early_stream is not None:
             early.event = torch.cuda.Event()        # every local test of this round is enqueued
             early.event.record(self._early_stream)
+        if self.trainer.trace and self.write:
+            self._plot_batches(plan, results)
         with self.timer.phase("gather"):
             bank, fg_grads, cstats = self._gather(plan, st["owners"], results)
         with self.timer.phase("aggregate"):
@@ -502,6 +504,32 @@ class Server:
         log.info(f"[{tag} agg] considering poison per batch poison_fraction: "
                  f"{adv * p['poisoning_per_batch'] / p['batch_size']}")
 
+    def _plot_batches(self, plan: RoundPlan, results: List[ClientResult]) -> None:
+        """Per-batch loss / distance-to-global points of this rank's benign phases (the
+        reference plots them in the benign branch only: image_train.py:225-249)."""
+        p = self.params
+        by = {r.name: r for r in results}
+        for c in plan.clients:
+            r = by.get(c.name)
+            if r is None or r.batch_trace is None:
+                continue
+            t = 0
+            for ph in c.phases:
+                n_b = (ph.end_step - t) // max(1, ph.internal_epochs)
+                for ie in range(ph.internal_epochs):
+                    tle = (ph.epoch - 1) * ph.internal_epochs + ie + 1
+                    for bi in range(n_b):
+                        loss, dist = r.batch_trace[t + ie * n_b + bi]
+                        if ph.poison:
+                            continue
+                        if p["vis_train_batch_loss"]:
+                            self.plot.line(f"train_batch_loss_{self.current_time}", (tle - 1) * n_b + bi,
+                                           float(loss), str(c.name))
+                        if p["batch_track_distance"]:
+                            self.plot.line(f"global_dist_{self.current_time}", (tle - 1) * n_b + bi + 1,
+                                           float(dist), str(c.name))
+                t = ph.end_step
+
     def _plot_weights(self, names, wv, alphas, adversarial, epoch) -> None:
         for nm, w, a in zip(names, wv, alphas):
             tag = f"{nm}_poisoned" if any(C._same_client(nm, x) for x in adversarial) else str(nm)
@@ -540,6 +568,10 @@ class Server:
                          f"internal_epoch {ie + 1:3d},  Average loss: {total_l:.4f}, "
                          f"Accuracy: {int(round(st[1]))}/{size} ({acc:.4f}%)")
                 csv.train_result.append([name, tle, ph.epoch, ie + 1, total_l, acc, int(round(st[1])), size])
+                if p["vis_train"]:   # model.train_vis (models/simple.py:18-30)
+                    tag = f"{name}_poisoned" if ph.poison else str(name)
+                    self.plot.line(f"train_acc_{self.current_time}", tle, acc, tag)
+                    self.plot.line(f"train_loss_{self.current_time}", tle, total_l, tag)
             elif kind in ("test", "poison"):
                 name, ep, j = payload
                 loss, acc, corr, tot = jres(j)

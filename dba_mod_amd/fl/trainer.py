@@ -44,6 +44,9 @@ class ClientResult:
     scale_dist: Dict[int, float] = field(default_factory=dict)   # phase epoch -> distance
     num_samples: int = 0
     steps: int = 0
+    # per-step (batch loss, distance to the round's global model) when vis_train_batch_loss /
+    # batch_track_distance are set (model.train_batch_vis / track_distance_batch_vis)
+    batch_trace: Optional[np.ndarray] = None
 
 
 class _GroupBuffers:
@@ -102,6 +105,12 @@ class GroupTrainer:
         self.target = int(params["poison_label_swap"])
         # anomaly-evasion distance term; every shipped config has alpha_loss = 1 (term off)
         self.alpha = float(params["alpha_loss"])
+        # per-batch loss / distance tracing for the Visdom batch plots: eager steps (the
+        # per-step values are read back), off in every shipped config
+        self.trace = bool(params["vis_train_batch_loss"]) or bool(params["batch_track_distance"])
+        if self.trace:
+            self.use_graph = False
+        self._last_loss: Optional[torch.Tensor] = None
 
     # ------------------------------------------------------------------ step
     def _step(self, b: _GroupBuffers) -> None:
@@ -131,6 +140,7 @@ class GroupTrainer:
                      self.wd, shadow=(b.wcomp if b.wcomp is not b.state else None), fg_accum=b.fg)
         if not fused:
             ref_ops.accumulate_step_stats(b.stats, b.slot, loss, correct, b.nvalid)
+        self._last_loss = loss
 
     def _buffers(self, G: int, max_slots: int) -> _GroupBuffers:
         key = (G, max_slots)
@@ -202,14 +212,20 @@ class GroupTrainer:
         events = self._events(clients)
         snaps: Dict[int, Dict[int, torch.Tensor]] = {g: {} for g in range(G)}
         pend_dist: List[Tuple[int, int, torch.Tensor]] = []
+        trace: List[torch.Tensor] = []
+        gstate = global_state[None, :self.spec.P]
         for t in range(T):
             b.desc.copy_(sched[t], non_blocking=True)
             self._run_step(b)
+            if self.trace:
+                dist = (b.state[:, :self.spec.P] - gstate).float().pow(2).sum(1).sqrt()
+                trace.append(torch.stack([self._last_loss.float(), dist], 1))
             for (g, ph) in events.get(t + 1, []):
                 self._phase_end(b, g, ph, snaps, pend_dist)
                 if on_client_done is not None and ph is clients[g].phases[-1]:
                     on_client_done(clients[g], snaps[g])
-        return {"b": b, "clients": clients, "snaps": snaps, "pend_dist": pend_dist, "sched": sched}
+        return {"b": b, "clients": clients, "snaps": snaps, "pend_dist": pend_dist, "sched": sched,
+                "trace": torch.stack(trace) if trace else None}
 
     def _wave_collect(self, w: Optional[Dict[str, Any]]) -> List[ClientResult]:
         if w is None:
@@ -223,10 +239,12 @@ class GroupTrainer:
         dists: Dict[int, Dict[int, float]] = {g: {} for g in range(G)}
         for g, e, d in w["pend_dist"]:
             dists[g][e] = float(d.sqrt().item())
+        tr = w["trace"].cpu().numpy() if w["trace"] is not None else None    # [T, G, 2]
         for g, c in enumerate(clients):
             nsl = sum(ph.internal_epochs for ph in c.phases)
             res.append(ClientResult(c.name, snaps[g], b.fg[g].clone() if b.fg is not None else None,
-                                    stats[g, :nsl].copy(), dists[g], c.num_samples, len(c.steps)))
+                                    stats[g, :nsl].copy(), dists[g], c.num_samples, len(c.steps),
+                                    tr[:len(c.steps), g].copy() if tr is not None else None))
         return res
 
     def _reset(self, b: _GroupBuffers, global_state: torch.Tensor) -> None:

@@ -207,3 +207,21 @@ def test_rfa_update_norm_rejection(tmp_path):
     before = s.global_state.clone()
     s.run_round(11)
     assert torch.equal(before, s.global_state)
+
+
+def test_batch_visualisation_events(tmp_path):
+    """vis_train / vis_train_batch_loss / batch_track_distance (reference models/simple.py
+    train_vis, train_batch_vis, track_distance_batch_vis) land in the Visdom event stream."""
+    import json as _json
+    p = mnist_params(tmp_path, vis_train=True, vis_train_batch_loss=True, batch_track_distance=True,
+                     is_poison=False)
+    s = Server(p, DistCtx(), write_outputs=True)
+    s.run_round(11)
+    wins = {}
+    for line in open(os.path.join(s.folder, "vis_events.jsonl")):
+        ev = _json.loads(line)
+        wins.setdefault(ev["win"].rsplit("_", 2)[0], []).append(ev)
+    for w in ("train_acc", "train_loss", "train_batch_loss", "global_dist"):
+        assert wins.get(w), (w, sorted(wins))
+    assert all(np.isfinite(ev["y"]) for ev in wins["train_batch_loss"])
+    assert all(ev["y"] >= 0 for ev in wins["global_dist"])
