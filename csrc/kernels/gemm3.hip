@@ -33,6 +33,7 @@ struct G3Args {
   const uint16_t* zeros;
   int N, Hs, Ws, Cs, Ho, Wo, Ncol, KH, KW, stride, pad, relu;
   int tiles_n;
+  long long out_zstride;                        // split-K: fp32 slab of K-slice z at out + z * out_zstride
 };
 
 __device__ __forceinline__ int g3swz(int row) { return (row >> 1) & 7; }
@@ -58,7 +59,11 @@ __global__ __launch_bounds__(256) void igemm3_kernel(G3Args a) {
   const int m0 = tm * BM, n0 = tn * BN;
   if (m0 >= Mv) return;
   const int K = a.KH * a.KW * a.Cs;
-  const int nk = K / 64;
+  // split-K (gridDim.z > 1, small launches): this block reduces k-steps [kb, kb + nk) into its
+  // own fp32 slab; splitk_reduce_kernel sums the slabs and applies the epilogue
+  const int nk_all = K / 64;
+  const int kb = (int)((long long)nk_all * blockIdx.z / gridDim.z);
+  const int nk = (int)((long long)nk_all * (blockIdx.z + 1) / gridDim.z) - kb;
   const uint16_t* __restrict__ src = a.src + (long long)g * a.src_gstride;
   const int slot = a.wsel ? a.wsel[g] : g;
   const uint16_t* __restrict__ Wp = a.w + (long long)slot * a.w_sstride;
@@ -122,7 +127,7 @@ __global__ __launch_bounds__(256) void igemm3_kernel(G3Args a) {
   // kc-1, retired by the previous barrier) and the wait at the bottom leaves NS-2 stages in
   // flight across the raw barrier.
   for (int s = 0; s < NS - 1; ++s)
-    if (s < nk) stage(s, s);
+    if (s < nk) stage(kb + s, s);
   if (nk >= NS - 1) {
     // all NS-1 prologue stages were issued: wait for k-step 0 only
     __builtin_amdgcn_s_waitcnt(kWaitKeep);
@@ -137,7 +142,7 @@ __global__ __launch_bounds__(256) void igemm3_kernel(G3Args a) {
   int cur = 0;
   for (int kc = 0; kc < nk; ++kc) {
     const int pre = kc + NS - 1;
-    if (pre < nk) stage(pre, cur == 0 ? NS - 1 : cur - 1);
+    if (pre < nk) stage(kb + pre, cur == 0 ? NS - 1 : cur - 1);
     const uint4* L = ring[cur];
 #pragma unroll
     for (int kk = 0; kk < 4; ++kk) {
@@ -185,7 +190,7 @@ __global__ __launch_bounds__(256) void igemm3_kernel(G3Args a) {
         Cst[row * BN + col] = acc[i][j][r];
       }
   __syncthreads();
-  OutT* out = (OutT*)a.out + (long long)g * a.out_gstride;
+  OutT* out = (OutT*)a.out + (long long)g * a.out_gstride + (long long)blockIdx.z * a.out_zstride;
   const float* bias = a.bias ? a.bias + (long long)slot * a.b_sstride : nullptr;
   const uint16_t* res = a.res ? a.res + (long long)g * a.out_gstride : nullptr;
   constexpr int CH8 = BN / 8;
@@ -226,12 +231,70 @@ __global__ __launch_bounds__(256) void igemm3_kernel(G3Args a) {
 }
 
 template <int BM, int BN, int NS, typename OutT>
-int launch3(G3Args a, int G, hipStream_t st) {
+int launch3(G3Args a, int G, hipStream_t st, int splitk = 1) {
   const long long M = (long long)a.N * a.Ho * a.Wo;
   a.tiles_n = ceil_div(a.Ncol, BN);
-  dim3 grid((unsigned)(ceil_div(M, BM) * a.tiles_n), G);
+  dim3 grid((unsigned)(ceil_div(M, BM) * a.tiles_n), G, splitk);
   hipLaunchKernelGGL((igemm3_kernel<BM, BN, NS, OutT>), grid, dim3(256), 0, st, a);
   DBA_LAUNCH_CHECK();
+}
+
+// Sum of the split-K slabs ws[z][g][m][n] + bias (+ residual) (ReLU) -> bf16, valid rows only.
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ ws, int S, long long zstride,
+                                                            long long ws_gstride, const int* __restrict__ nvalid,
+                                                            int N, int HoWo, int Ncol, const float* __restrict__ bias,
+                                                            long long b_sstride, const int* __restrict__ wsel,
+                                                            const uint16_t* __restrict__ res, long long out_gstride,
+                                                            int relu, uint16_t* __restrict__ out) {
+  const int g = blockIdx.y;
+  const long long total = (long long)valid_rows(nvalid, g, N) * HoWo * (Ncol / 8);
+  const float* __restrict__ src = ws + (long long)g * ws_gstride;
+  const float* __restrict__ bp = bias ? bias + (long long)(wsel ? wsel[g] : g) * b_sstride : nullptr;
+  for (long long t = blockIdx.x * 256LL + threadIdx.x; t < total; t += (long long)gridDim.x * 256) {
+    const long long e = t * 8;
+    const int n = (int)(e % Ncol);
+    float v[8];
+    {
+      const float4 a0 = *(const float4*)(src + e), a1 = *(const float4*)(src + e + 4);
+      v[0] = a0.x; v[1] = a0.y; v[2] = a0.z; v[3] = a0.w; v[4] = a1.x; v[5] = a1.y; v[6] = a1.z; v[7] = a1.w;
+    }
+    for (int z = 1; z < S; ++z) {
+      const float* q = src + z * zstride + e;
+      const float4 a0 = *(const float4*)q, a1 = *(const float4*)(q + 4);
+      v[0] += a0.x; v[1] += a0.y; v[2] += a0.z; v[3] += a0.w; v[4] += a1.x; v[5] += a1.y; v[6] += a1.z; v[7] += a1.w;
+    }
+    if (bp) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v[i] += bp[n + i];
+    }
+    const long long o = (long long)g * out_gstride + e;
+    if (res) {
+      const uint4 rv = *(const uint4*)(res + o);
+      const uint16_t* rp = (const uint16_t*)&rv;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v[i] += bf2f(rp[i]);
+    }
+    uint4 pk;
+    uint16_t* pp = (uint16_t*)&pk;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) pp[i] = f2bf(relu ? fmaxf(v[i], 0.f) : v[i]);
+    *(uint4*)(out + o) = pk;
+  }
+}
+
+bool g3_small(long long M, int G, int Cout) { return M * G / 128 * ((Cout + 127) / 128) < 512; }
+
+// split factor for a small launch: enough K-slices to put ~256 blocks on the chip, at least
+// 4 k-steps per slice (1 = no split; DBA_G3_SPLITK=0 disables)
+int g3_splitk(long long M, int G, int Cout, int K) {
+  static const bool off = getenv("DBA_G3_SPLITK") && atoi(getenv("DBA_G3_SPLITK")) == 0;
+  if (off) return 1;
+  const long long blocks = (long long)ceil_div(M, 64) * ceil_div(Cout, 128) * G;
+  if (blocks >= 192) return 1;
+  const int nk = K / 64;
+  int s = (int)std::min<long long>(8, (256 + blocks - 1) / blocks);
+  while (s > 1 && nk / s < 4) --s;
+  return s;
 }
 
 }  // namespace
@@ -239,24 +302,54 @@ int launch3(G3Args a, int G, hipStream_t st) {
 // Forward conv (or a stride-1 data gradient expressed as one, with tap-flipped transposed
 // weights) for Cs % 64 == 0 and Ncol % 8 == 0 on launches large enough to fill the chip
 // with 128x128 tiles.  Returns -100 otherwise (caller falls back to conv2.hip).
+// fp32 workspace (floats) dba_conv3_fwd needs for a split-K launch of this shape (0: none)
+DBA_EXPORT long long dba_conv3_splitk_floats(int G, int N, int Ho, int Wo, int Cin, int Cout, int KH, int KW,
+                                             int out_f32) {
+  if (Cin % 64 != 0 || Cout % 8 != 0 || Cout < 128 || out_f32) return 0;
+  const long long M = (long long)N * Ho * Wo;
+  if (!g3_small(M, G, Cout)) return 0;
+  const int s = g3_splitk(M, G, Cout, KH * KW * Cin);
+  return s > 1 ? (long long)s * G * M * Cout : 0;
+}
+
 DBA_EXPORT int dba_conv3_fwd(const void* x, long long x_gstride, const void* w, long long w_sstride, const int* wsel,
                              const float* bias, long long b_sstride, const void* res, void* out, long long out_gstride,
                              int out_f32, const int* nvalid, const void* zeros, int G, int N, int H, int W, int Cin,
-                             int Ho, int Wo, int Cout, int KH, int KW, int stride, int pad, int relu, void* stream) {
+                             int Ho, int Wo, int Cout, int KH, int KW, int stride, int pad, int relu, void* ws,
+                             long long ws_floats, void* stream) {
   if (Cin % 64 != 0 || Cout % 8 != 0 || Cout < 128 || out_f32) return -100;
   const long long M = (long long)N * Ho * Wo;
   G3Args a{(const uint16_t*)x, x_gstride, (const uint16_t*)w, w_sstride, wsel, bias, b_sstride,
            (const uint16_t*)res, out, out_gstride, nvalid, (const uint16_t*)zeros,
-           N, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, relu, 1};
+           N, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, relu, 1, 0};
   static const int ns = [] {
     const char* e = getenv("DBA_G3_NS");
     return e ? atoi(e) : 2;
   }();
-  if (M * G / 128 * ((Cout + 127) / 128) < 512) {
+  if (g3_small(M, G, Cout)) {
     // small launches (grouped training steps): the block count cannot cover the chip, so
     // per-block latency rules — smaller M tiles and a 4-deep ring (3 k-steps in flight)
     static const bool small_off = getenv("DBA_G3_SMALL") && atoi(getenv("DBA_G3_SMALL")) == 0;
     if (small_off) return -100;
+    const int s = g3_splitk(M, G, Cout, KH * KW * Cin);
+    if (s > 1 && ws != nullptr && ws_floats >= (long long)s * G * M * Cout) {
+      // a lone client's stage-4 conv is 32 blocks of 36 k-steps: split K over s slabs
+      G3Args b = a;
+      b.out = ws;
+      b.out_gstride = M * Cout;
+      b.out_zstride = (long long)G * M * Cout;
+      b.bias = nullptr;
+      b.res = nullptr;
+      b.relu = 0;
+      const int rc = launch3<64, 128, 4, float>(b, G, (hipStream_t)stream, s);
+      if (rc != 0) return rc;
+      const long long per = M * (Cout / 8);
+      const dim3 grid((unsigned)std::max(1LL, std::min(2048LL, (per + 255) / 256)), G);
+      hipLaunchKernelGGL(splitk_reduce_kernel, grid, dim3(256), 0, (hipStream_t)stream, (const float*)ws, s,
+                         b.out_zstride, b.out_gstride, nvalid, N, Ho * Wo, Cout, bias, b_sstride, wsel,
+                         (const uint16_t*)res, out_gstride, relu, (uint16_t*)out);
+      DBA_LAUNCH_CHECK();
+    }
     return launch3<64, 128, 4, uint16_t>(a, G, (hipStream_t)stream);
   }
   if (ns == 3) return launch3<128, 128, 3, uint16_t>(a, G, (hipStream_t)stream);

@@ -61,7 +61,8 @@ _SIGS = {
     "dba_sq_dists": [_P, _LL, _P, _I, _LL, _P, _P],
     "dba_weighted_sum": [_P, _LL, _P, _I, _P, _LL, _P],
     "dba_gram": [_P, _LL, _I, _I, _P, _P],
-    "dba_conv3_fwd": [_P, _LL, _P, _LL, _P, _P, _LL, _P, _P, _LL, _I, _P, _P] + [_I] * 13 + [_P],
+    "dba_conv3_fwd": [_P, _LL, _P, _LL, _P, _P, _LL, _P, _P, _LL, _I, _P, _P] + [_I] * 13 + [_P, _LL, _P],
+    "dba_conv3_splitk_floats": [_I] * 9,
     "dba_pconv": [_P, _LL, _P, _LL, _P, _P, _LL, _P, _P, _LL, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P],
     "dba_pwgrad": [_P, _LL, _P, _LL, _P, _LL, _P, _P, _I, _I, _I, _I, _I, _I, _P],
     "dba_wgrad3": [_P, _LL, _P, _LL, _P, _LL, _P, _P] + [_I] * 12 + [_P],
@@ -71,6 +72,7 @@ for _name, _args in _SIGS.items():
     _fn = getattr(_L, _name)
     _fn.argtypes = _args
     _fn.restype = ctypes.c_int
+_L.dba_conv3_splitk_floats.restype = ctypes.c_longlong
 
 
 NOT_HANDLED = -100   # a conv2 entry point declining a shape (odd channel counts)
@@ -169,6 +171,17 @@ def _zeros(dev) -> Tensor:
     return z
 
 
+def _conv3(x_ptr, x_gs, w_ptr, w_ss, wsel_, bias_ptr, bs, res_ptr, out_ptr, out_gs, f32, nv_, dev,
+           G, N, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, relu) -> int:
+    """Gen-3 implicit GEMM (csrc/kernels/gemm3.hip); small launches get an fp32 split-K
+    workspace (allocated here, stream-ordered) when the kernel asks for one."""
+    n = int(_L.dba_conv3_splitk_floats(G, N, Ho, Wo, Cin, Cout, KH, KW, f32))
+    wsb = torch.empty(n, dtype=torch.float32, device=dev) if n > 0 else None
+    return _call("dba_conv3_fwd", x_ptr, x_gs, w_ptr, w_ss, wsel_, bias_ptr, bs, res_ptr, out_ptr, out_gs, f32, nv_,
+                 _zeros(dev).data_ptr(), G, N, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, relu, _ptr(wsb), n,
+                 _stream())
+
+
 def _pconv_ok(Cin, Cout, H, W, KH, KW, stride, pad) -> bool:
     """H, W = input size."""
     return (_PCONV and KH == 3 and KW == 3 and pad == 1 and H == W
@@ -201,9 +214,9 @@ def conv2d(x, w, wsel, stride, pad, bias=None, residual=None, relu=False, nvalid
                    _ptr(residual), y.data_ptr(), N * Ho * Wo * Cout, nv_, _zeros(x.device).data_ptr(), G, N, Ho, Wo,
                    Cin, Cout, 0, int(relu), stride, _stream())
     if rc == NOT_HANDLED and _GEMM3:
-        rc = _call("dba_conv3_fwd", x.data_ptr(), N * H * W * Cin, w.data_ptr(), ws, wsel_, _ptr(bias), bs,
-                   _ptr(residual), y.data_ptr(), N * Ho * Wo * Cout, f32, nv_, _zeros(x.device).data_ptr(), G, N, H,
-                   W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, int(relu), _stream())
+        rc = _conv3(x.data_ptr(), N * H * W * Cin, w.data_ptr(), ws, wsel_, _ptr(bias), bs, _ptr(residual),
+                    y.data_ptr(), N * Ho * Wo * Cout, f32, nv_, x.device, G, N, H, W, Cin, Ho, Wo, Cout, KH, KW,
+                    stride, pad, int(relu))
     if rc == NOT_HANDLED and stride == 1 and KH == KW:
         rc = _call("dba_halo_conv", x.data_ptr(), N * H * W * Cin, w.data_ptr(), ws, wsel_, _ptr(bias), bs,
                    _ptr(residual), y.data_ptr(), N * Ho * Wo * Cout, f32, nv_, G, N, H, W, Cin, Cout, KH, pad,
@@ -307,10 +320,9 @@ def conv2d_dgrad(dy, w, wsel, stride, pad, in_hw, nvalid=None, out_dtype=None, a
             _call("dba_transpose_w", w.data_ptr(), ws, wt.data_ptr(), slots, Cout, KH * KW, Cin, 1, skip, _stream())
         rc = NOT_HANDLED
         if _GEMM3:
-            rc = _call("dba_conv3_fwd", dy.data_ptr(), N * Ho * Wo * Cout, wt.data_ptr(), Cin * KH * KW * Cout,
-                       _ptr(_i32(wsel)), None, 0, _ptr(acc), dx.data_ptr(), N * H * W * Cin, 0, _ptr(_i32(nvalid)),
-                       _zeros(dy.device).data_ptr(), G, N, Ho, Wo, Cout, H, W, Cin, KH, KH, 1, KH - 1 - pad, 0,
-                       _stream())
+            rc = _conv3(dy.data_ptr(), N * Ho * Wo * Cout, wt.data_ptr(), Cin * KH * KW * Cout, _ptr(_i32(wsel)),
+                        None, 0, _ptr(acc), dx.data_ptr(), N * H * W * Cin, 0, _ptr(_i32(nvalid)), dy.device, G, N,
+                        Ho, Wo, Cout, H, W, Cin, KH, KH, 1, KH - 1 - pad, 0)
         if rc != NOT_HANDLED:
             return done(dx)
         rc = _call("dba_halo_conv", dy.data_ptr(), N * Ho * Wo * Cout, wt.data_ptr(), Cin * KH * KW * Cout,

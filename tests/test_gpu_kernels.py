@@ -64,6 +64,8 @@ CONV_CASES = [
     (16, 64, 8, 8, 128, 256, 3, 2, 1),   # gen-3 wgrad without split-K (sole-writer epilogue)
     (2, 9, 16, 16, 64, 128, 1, 2, 0),    # gen-3 wgrad, shortcut (J = 64)
     (16, 6, 8, 8, 256, 256, 3, 2, 1),    # gen-3 wgrad 128x128 tiles (launch fills the chip)
+    (1, 64, 4, 4, 256, 256, 3, 1, 1),    # lone client, stage 4: gen-3 split-K (8 slabs) + reduce
+    (2, 64, 8, 8, 128, 128, 3, 1, 1),    # two clients, stage 3: gen-3 split-K (2 slabs)
 ]
 
 

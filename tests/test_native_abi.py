@@ -13,7 +13,7 @@ def _c_signatures():
     sigs = {}
     for path in glob.glob(os.path.join(ROOT, "csrc", "kernels", "*.hip")):
         src = open(path).read()
-        for m in re.finditer(r"DBA_EXPORT\s+int\s+(\w+)\s*\(([^)]*)\)", src, re.S):
+        for m in re.finditer(r"DBA_EXPORT\s+(?:int|long long)\s+(\w+)\s*\(([^)]*)\)", src, re.S):
             params = [p.strip() for p in m.group(2).split(",") if p.strip()]
             kinds = []
             for p in params:
