@@ -505,8 +505,8 @@ class Server:
                  f"{adv * p['poisoning_per_batch'] / p['batch_size']}")
 
     def _plot_batches(self, plan: RoundPlan, results: List[ClientResult]) -> None:
-        """Per-batch loss / distance-to-global points of this rank's benign phases (the
-        reference plots them in the benign branch only: image_train.py:225-249)."""
+        """Per-batch loss (benign phases: image_train.py:225-234) and distance-to-global points
+        (every phase; poison phases tagged ``_poisoned``: image_train.py:107-116, 235-249)."""
         p = self.params
         by = {r.name: r for r in results}
         for c in plan.clients:
@@ -520,14 +520,14 @@ class Server:
                     tle = (ph.epoch - 1) * ph.internal_epochs + ie + 1
                     for bi in range(n_b):
                         loss, dist = r.batch_trace[t + ie * n_b + bi]
-                        if ph.poison:
-                            continue
-                        if p["vis_train_batch_loss"]:
+                        if p["vis_train_batch_loss"] and not ph.poison:
                             self.plot.line(f"train_batch_loss_{self.current_time}", (tle - 1) * n_b + bi,
                                            float(loss), str(c.name))
                         if p["batch_track_distance"]:
+                            # poison phases too, tagged like simple.py:46-49 (image_train.py:107-116)
+                            tag = f"{c.name}_poisoned" if ph.poison else str(c.name)
                             self.plot.line(f"global_dist_{self.current_time}", (tle - 1) * n_b + bi + 1,
-                                           float(dist), str(c.name))
+                                           float(dist), tag)
                 t = ph.end_step
 
     def _plot_weights(self, names, wv, alphas, adversarial, epoch) -> None:

@@ -225,3 +225,11 @@ def test_batch_visualisation_events(tmp_path):
         assert wins.get(w), (w, sorted(wins))
     assert all(np.isfinite(ev["y"]) for ev in wins["train_batch_loss"])
     assert all(ev["y"] >= 0 for ev in wins["global_dist"])
+    # an attacker's poison phase plots its distances as "<name>_poisoned" (simple.py:46-49)
+    p2 = mnist_params(tmp_path / "poison", batch_track_distance=True, adversary_list=[41],
+                      **{"0_poison_epochs": [12]})
+    s2 = Server(p2, DistCtx(), write_outputs=True)
+    s2.run_round(12)
+    names = {ev["name"] for line in open(os.path.join(s2.folder, "vis_events.jsonl"))
+             for ev in [_json.loads(line)] if ev["win"].startswith("global_dist")}
+    assert "41_poisoned" in names, names
