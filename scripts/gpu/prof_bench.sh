@@ -1,4 +1,6 @@
+# rocprofv3 kernel trace + stats of a short bench.py run (3 warm-start rounds keep the trace small)
 R=$GRAFT_REPO_ROOT
+export PYTHONPATH=$R
 mkdir -p $R/gpurun_out/prof
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof -o bench -- python3 $R/bench.py --steps 4 --warmup 1 --pretrain-rounds 3 > $R/gpurun_out/prof/bench_stdout.log 2>&1

@@ -1,3 +1,4 @@
+# step microbenchmark + kernel trace for the MNIST config
 mkdir -p gpurun_out
 R=$GRAFT_REPO_ROOT
 timeout -k 10 300 python -m dba_mod_amd.tools.bench_step --config configs/mnist_params.yaml --epoch 12 > gpurun_out/mstep.log 2>&1 || exit $?

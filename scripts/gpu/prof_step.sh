@@ -1,3 +1,4 @@
+# grouped-step microbenchmark (all clients / one client) + kernel trace
 mkdir -p gpurun_out
 timeout -k 10 300 python -m dba_mod_amd.tools.bench_step > gpurun_out/step.log 2>&1 || exit $?
 timeout -k 10 300 python -m dba_mod_amd.tools.bench_step --clients 1 >> gpurun_out/step.log 2>&1 || exit $?
