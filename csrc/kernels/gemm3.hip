@@ -282,7 +282,35 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
   }
 }
 
-bool g3_small(long long M, int G, int Cout) { return M * G / 128 * ((Cout + 127) / 128) < 512; }
+int env_int(const char* name, int dflt) {
+  const char* e = getenv(name);
+  return e ? atoi(e) : dflt;
+}
+
+// launches with fewer 128x128 tiles than this take the small-tile path
+bool g3_small(long long M, int G, int Cout) {
+  static const int limit = env_int("DBA_G3_SMALL_LIMIT", 512);
+  return M * G / 128 * ((Cout + 127) / 128) < limit;
+}
+
+// tile shape (BM x BN, ring depth) by code — DBA_G3_SMALL_TILE / DBA_G3_BIG_TILE pick one for
+// the small / large launch classes (sweeps: scripts/gpu/g3_tiles.sh)
+int launch3_tile(int code, const G3Args& a, int G, hipStream_t st) {
+  switch (code) {
+    case 1: return launch3<64, 64, 4, uint16_t>(a, G, st);
+    case 2: return launch3<64, 128, 3, uint16_t>(a, G, st);
+    case 3: return launch3<128, 64, 3, uint16_t>(a, G, st);
+    case 4: return launch3<128, 128, 2, uint16_t>(a, G, st);
+    case 5: return launch3<128, 128, 3, uint16_t>(a, G, st);
+    case 6: return launch3<64, 64, 3, uint16_t>(a, G, st);
+    default: return launch3<64, 128, 4, uint16_t>(a, G, st);
+  }
+}
+
+int* g3_tiles() {
+  static int t[2] = {env_int("DBA_G3_SMALL_TILE", 2), env_int("DBA_G3_BIG_TILE", 4)};
+  return t;
+}
 
 // split factor for a small launch: enough K-slices to put ~256 blocks on the chip, at least
 // 4 k-steps per slice (1 = no split; DBA_G3_SPLITK=0 disables)
@@ -299,9 +327,16 @@ int g3_splitk(long long M, int G, int Cout, int K) {
 
 }  // namespace
 
-// Forward conv (or a stride-1 data gradient expressed as one, with tap-flipped transposed
-// weights) for Cs % 64 == 0 and Ncol % 8 == 0 on launches large enough to fill the chip
-// with 128x128 tiles.  Returns -100 otherwise (caller falls back to conv2.hip).
+// Select the tile codes of the small / large launch classes (launch3_tile); -1 keeps one.
+// Returns the previous pair packed as small * 16 + big.
+DBA_EXPORT int dba_conv3_set_tiles(int small_tile, int big_tile) {
+  int* t = g3_tiles();
+  const int prev = t[0] * 16 + t[1];
+  if (small_tile >= 0) t[0] = small_tile;
+  if (big_tile >= 0) t[1] = big_tile;
+  return prev;
+}
+
 // fp32 workspace (floats) dba_conv3_fwd needs for a split-K launch of this shape (0: none)
 DBA_EXPORT long long dba_conv3_splitk_floats(int G, int N, int Ho, int Wo, int Cin, int Cout, int KH, int KW,
                                              int out_f32) {
@@ -312,6 +347,9 @@ DBA_EXPORT long long dba_conv3_splitk_floats(int G, int N, int Ho, int Wo, int C
   return s > 1 ? (long long)s * G * M * Cout : 0;
 }
 
+// Forward conv (or a stride-1 data gradient expressed as one, with tap-flipped transposed
+// weights) for Cs % 64 == 0, Ncol % 8 == 0, Ncol >= 128.  Returns -100 otherwise (caller
+// falls back to conv2.hip).
 DBA_EXPORT int dba_conv3_fwd(const void* x, long long x_gstride, const void* w, long long w_sstride, const int* wsel,
                              const float* bias, long long b_sstride, const void* res, void* out, long long out_gstride,
                              int out_f32, const int* nvalid, const void* zeros, int G, int N, int H, int W, int Cin,
@@ -322,13 +360,11 @@ DBA_EXPORT int dba_conv3_fwd(const void* x, long long x_gstride, const void* w, 
   G3Args a{(const uint16_t*)x, x_gstride, (const uint16_t*)w, w_sstride, wsel, bias, b_sstride,
            (const uint16_t*)res, out, out_gstride, nvalid, (const uint16_t*)zeros,
            N, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, relu, 1, 0};
-  static const int ns = [] {
-    const char* e = getenv("DBA_G3_NS");
-    return e ? atoi(e) : 2;
-  }();
+  const int small_tile = g3_tiles()[0], big_tile = g3_tiles()[1];
   if (g3_small(M, G, Cout)) {
     // small launches (grouped training steps): the block count cannot cover the chip, so
-    // per-block latency rules — smaller M tiles and a 4-deep ring (3 k-steps in flight)
+    // per-block latency rules — 64-row M tiles with a 3-deep LDS ring (tile code 2, swept in
+    // scripts/gpu/g3_tiles.sh: 64x128/3 187 ms vs 64x128/4 192-202 ms per bench round)
     static const bool small_off = getenv("DBA_G3_SMALL") && atoi(getenv("DBA_G3_SMALL")) == 0;
     if (small_off) return -100;
     const int s = g3_splitk(M, G, Cout, KH * KW * Cin);
@@ -350,8 +386,7 @@ DBA_EXPORT int dba_conv3_fwd(const void* x, long long x_gstride, const void* w, 
                          (const uint16_t*)res, out_gstride, relu, (uint16_t*)out);
       DBA_LAUNCH_CHECK();
     }
-    return launch3<64, 128, 4, uint16_t>(a, G, (hipStream_t)stream);
+    return launch3_tile(small_tile, a, G, (hipStream_t)stream);
   }
-  if (ns == 3) return launch3<128, 128, 3, uint16_t>(a, G, (hipStream_t)stream);
-  return launch3<128, 128, 2, uint16_t>(a, G, (hipStream_t)stream);
+  return launch3_tile(big_tile, a, G, (hipStream_t)stream);
 }

@@ -63,6 +63,7 @@ _SIGS = {
     "dba_gram": [_P, _LL, _I, _I, _P, _P],
     "dba_conv3_fwd": [_P, _LL, _P, _LL, _P, _P, _LL, _P, _P, _LL, _I, _P, _P] + [_I] * 13 + [_P, _LL, _P],
     "dba_conv3_splitk_floats": [_I] * 9,
+    "dba_conv3_set_tiles": [_I, _I],
     "dba_pconv": [_P, _LL, _P, _LL, _P, _P, _LL, _P, _P, _LL, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P],
     "dba_pwgrad": [_P, _LL, _P, _LL, _P, _LL, _P, _P, _I, _I, _I, _I, _I, _I, _P],
     "dba_wgrad3": [_P, _LL, _P, _LL, _P, _LL, _P, _P] + [_I] * 12 + [_P],
@@ -180,6 +181,20 @@ def _conv3(x_ptr, x_gs, w_ptr, w_ss, wsel_, bias_ptr, bs, res_ptr, out_ptr, out_
     return _call("dba_conv3_fwd", x_ptr, x_gs, w_ptr, w_ss, wsel_, bias_ptr, bs, res_ptr, out_ptr, out_gs, f32, nv_,
                  _zeros(dev).data_ptr(), G, N, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, relu, _ptr(wsb), n,
                  _stream())
+
+
+GEMM3_TILES = {0: "64x128/4", 1: "64x64/4", 2: "64x128/3", 3: "128x64/3", 4: "128x128/2", 5: "128x128/3",
+               6: "64x64/3"}   # code -> BMxBN / LDS ring depth (gemm3.hip launch3_tile)
+
+
+def set_gemm3_tiles(small: int = -1, big: int = -1) -> Tuple[int, int]:
+    """Pick the gen-3 GEMM tile of the small (< DBA_G3_SMALL_LIMIT 128x128 tiles) and large
+    launch classes; -1 keeps the current one.  Returns the previous (small, big) codes."""
+    for c in (small, big):
+        if c != -1 and c not in GEMM3_TILES:
+            raise ValueError(f"unknown gemm3 tile code {c}")
+    prev = int(_L.dba_conv3_set_tiles(int(small), int(big)))
+    return prev // 16, prev % 16
 
 
 def _pconv_ok(Cin, Cout, H, W, KH, KW, stride, pad) -> bool:

@@ -141,6 +141,32 @@ def test_pconv_inactive_groups_and_slots(H, R, C, HW):
             assert _rel(dx[g, :n], dxr[g, :n]) < 1e-2, f"dgrad g{g}"
 
 
+@pytest.mark.parametrize("code", [0, 1, 2, 3, 4, 5, 6])
+def test_gemm3_tile_variants(H, R, code):
+    """Every selectable gen-3 tile (small and large launch class) on a stage-4 3x3 conv, a
+    ragged-M stage-3 conv and a 1x1 stride-2 shortcut, with bias/residual/ReLU and a short group."""
+    dev = torch.device("cuda")
+    torch.manual_seed(2)
+    prev = H.set_gemm3_tiles(code, code)
+    try:
+        # small class without split-K (>= 192 64-row blocks) x3, then the large class
+        for G, N, Hh, Cin, Cout, k, s, p in ((2, 301, 4, 256, 256, 3, 1, 1), (3, 91, 8, 128, 128, 3, 1, 1),
+                                             (2, 301, 8, 128, 256, 1, 2, 0), (2, 601, 8, 128, 128, 3, 1, 1)):
+            x = torch.randn(G, N, Hh, Hh, Cin, device=dev).bfloat16()
+            w = (torch.randn(G, Cout, k, k, Cin, device=dev) * (1.0 / (k * k * Cin) ** 0.5)).bfloat16()
+            bias = torch.randn(G, Cout, device=dev)
+            nvalid = torch.tensor([N] + [max(1, N - 3)] * (G - 1), dtype=torch.int32, device=dev)
+            Ho = (Hh + 2 * p - k) // s + 1
+            res = torch.randn(G, N, Ho, Ho, Cout, device=dev).bfloat16()
+            y = H.conv2d(x, w, None, s, p, bias=bias, residual=res, relu=True, nvalid=nvalid)
+            yr = R.conv2d(x.float(), w.float(), None, s, p, bias=bias, residual=res.float(), relu=True)
+            for g in range(G):
+                n = int(nvalid[g])
+                _close(y[g, :n], yr[g, :n], 2e-2, 3e-2, f"tile {code} G{G} N{N} C{Cin}->{Cout} g{g}")
+    finally:
+        H.set_gemm3_tiles(*prev)
+
+
 def test_conv_fp32_out_and_inactive_group(H, R):
     dev = torch.device("cuda")
     x = torch.randn(2, 4, 1, 1, 512, device=dev).bfloat16()
