@@ -106,6 +106,8 @@ _DEFAULTS: Dict[str, Any] = {
     "max_update_norm": None,       # RFA update-norm rejection (helper.py:360-369; never enabled there)
     "pretrain_eta": 1.0,
     "pretrain_lr": None,           # client lr of the warm start (None: the config's lr)
+    "model_arch": None,            # cifar only: resnet{18,34,50,101,152}_cifar (resnet_cifar.py:106-116);
+                                   # None = ResNet-18 as in image_helper.py:33-38
 }
 
 # keys whose value may legitimately be a python list of ints/strings

@@ -68,7 +68,7 @@ def build_workload(params: C.Params, device: torch.device) -> Workload:
     py_rng = random.Random(seed)
     np_rng = np.random.RandomState(seed)
     t = params.type
-    spec = get_spec(arch_for_type(t))
+    spec = get_spec(arch_for_type(t, params["model_arch"]))
     data_dir = params["data_dir"]
     if t == C.TYPE_LOAN:
         return _build_loan(params, spec, device, py_rng, np_rng, data_dir)

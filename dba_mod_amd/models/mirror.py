@@ -11,7 +11,9 @@ They serve three purposes and are *not* the compute path:
 Architectures:
 * ``MnistNet`` — ``MnistNet.py:7-31`` (conv5x5 1→20, conv5x5 20→50, fc 800→500→10,
   log_softmax);
-* ``ResNet18Cifar`` — half-width ResNet-18, ``resnet_cifar.py:14-36,67-104``;
+* ``ResNet18Cifar`` — half-width ResNet-18, ``resnet_cifar.py:14-36,67-104``; the rest of the
+  half-width CIFAR family (``ResNetCifar``: ResNet-34 with basic blocks, ResNet-50/101/152 with
+  bottleneck blocks, ``resnet_cifar.py:39-64,106-116``) shares the key layout;
 * ``ResNet18Tiny`` — torchvision-style ResNet-18 with a 200-way fc,
   ``resnet_tinyimagenet.py:40-77,122-238``;
 * ``LoanNet`` — ``loan_model.py:10-27`` (91→46→23→9 MLP with dropout 0.5).
@@ -56,22 +58,58 @@ class _CifarBlock(nn.Module):
         return F.relu(out)
 
 
-class ResNet18Cifar(nn.Module):
-    """Half-width ResNet-18 (stem 32, stages 32/64/128/256)."""
+class _CifarBottleneck(nn.Module):
+    """``resnet_cifar.py:39-64`` (expansion 4): 1x1 → 3x3(stride) → 1x1, projection shortcut."""
+    expansion = 4
 
-    def __init__(self, num_classes: int = 10) -> None:
+    def __init__(self, cin: int, planes: int, stride: int) -> None:
+        super().__init__()
+        cout = planes * self.expansion
+        self.conv1 = nn.Conv2d(cin, planes, 1, bias=False)
+        self.bn1 = nn.BatchNorm2d(planes)
+        self.conv2 = nn.Conv2d(planes, planes, 3, stride, 1, bias=False)
+        self.bn2 = nn.BatchNorm2d(planes)
+        self.conv3 = nn.Conv2d(planes, cout, 1, bias=False)
+        self.bn3 = nn.BatchNorm2d(cout)
+        self.shortcut = nn.Sequential()
+        if stride != 1 or cin != cout:
+            self.shortcut = nn.Sequential(nn.Conv2d(cin, cout, 1, stride, bias=False),
+                                          nn.BatchNorm2d(cout))
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        out = F.relu(self.bn1(self.conv1(x)))
+        out = F.relu(self.bn2(self.conv2(out)))
+        out = self.bn3(self.conv3(out)) + self.shortcut(x)
+        return F.relu(out)
+
+
+# CIFAR ResNet family of ``resnet_cifar.py:106-116``: arch -> (bottleneck?, blocks per stage)
+CIFAR_RESNETS = {
+    "resnet18_cifar": (False, (2, 2, 2, 2)),
+    "resnet34_cifar": (False, (3, 4, 6, 3)),
+    "resnet50_cifar": (True, (3, 4, 6, 3)),
+    "resnet101_cifar": (True, (3, 4, 23, 3)),
+    "resnet152_cifar": (True, (3, 8, 36, 3)),
+}
+
+
+class ResNetCifar(nn.Module):
+    """Half-width CIFAR ResNet (stem 32, stages 32/64/128/256 x expansion), ``resnet_cifar.py:67-104``."""
+
+    def __init__(self, bottleneck: bool = False, blocks=(2, 2, 2, 2), num_classes: int = 10) -> None:
         super().__init__()
         self.conv1 = nn.Conv2d(3, 32, 3, 1, 1, bias=False)
         self.bn1 = nn.BatchNorm2d(32)
-        widths, cin = (32, 64, 128, 256), 32
-        for li, w in enumerate(widths):
-            blocks = []
-            for bi in range(2):
+        exp = _CifarBottleneck.expansion if bottleneck else 1
+        cin = 32
+        for li, w in enumerate((32, 64, 128, 256)):
+            layer = []
+            for bi in range(blocks[li]):
                 stride = 2 if (li > 0 and bi == 0) else 1
-                blocks.append(_CifarBlock(cin, w, stride))
-                cin = w
-            setattr(self, f"layer{li + 1}", nn.Sequential(*blocks))
-        self.linear = nn.Linear(256, num_classes)
+                layer.append(_CifarBottleneck(cin, w, stride) if bottleneck else _CifarBlock(cin, w, stride))
+                cin = w * exp
+            setattr(self, f"layer{li + 1}", nn.Sequential(*layer))
+        self.linear = nn.Linear(256 * exp, num_classes)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         out = F.relu(self.bn1(self.conv1(x)))
@@ -79,6 +117,13 @@ class ResNet18Cifar(nn.Module):
             out = getattr(self, f"layer{li + 1}")(out)
         out = F.avg_pool2d(out, out.shape[-1])
         return self.linear(out.flatten(1))
+
+
+class ResNet18Cifar(ResNetCifar):
+    """Half-width ResNet-18 (stem 32, stages 32/64/128/256) — the reference's CIFAR model."""
+
+    def __init__(self, num_classes: int = 10) -> None:
+        super().__init__(False, (2, 2, 2, 2), num_classes)
 
 
 class _TinyBlock(nn.Module):
@@ -146,5 +191,6 @@ class LoanNet(nn.Module):
 
 
 def build_mirror(arch: str) -> nn.Module:
-    return {"mnist": MnistNet, "resnet18_cifar": ResNet18Cifar, "resnet18_tiny": ResNet18Tiny,
-            "loan": LoanNet}[arch]()
+    if arch in CIFAR_RESNETS:
+        return ResNetCifar(*CIFAR_RESNETS[arch])
+    return {"mnist": MnistNet, "resnet18_tiny": ResNet18Tiny, "loan": LoanNet}[arch]()

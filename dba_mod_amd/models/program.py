@@ -20,6 +20,7 @@ from typing import Callable, Dict, List, Optional, Tuple
 import torch
 
 from .. import ops
+from .mirror import CIFAR_RESNETS
 from .spec import ModelSpec
 
 Tensor = torch.Tensor
@@ -242,19 +243,28 @@ class Ctx:
 
 # ------------------------------------------------------------------- architectures
 def _resnet_cifar(ctx: Ctx, x: Tensor) -> Tensor:
+    """Any member of the half-width CIFAR family (``mirror.CIFAR_RESNETS``)."""
+    bottleneck, blocks = CIFAR_RESNETS[ctx.spec.arch]
+    exp = 4 if bottleneck else 1
     out = ctx.conv_bn(x, "conv1.weight", "bn1", 1, 1, relu=True)
     cin = 32
     for li, w in enumerate((32, 64, 128, 256)):
-        for bi in range(2):
+        for bi in range(blocks[li]):
             stride = 2 if (li > 0 and bi == 0) else 1
             pre = f"layer{li + 1}.{bi}."
-            a = ctx.conv_bn(out, pre + "conv1.weight", pre + "bn1", stride, 1, relu=True)
-            if stride != 1 or cin != w:
+            if bottleneck:
+                a = ctx.conv_bn(out, pre + "conv1.weight", pre + "bn1", 1, 0, relu=True)
+                a = ctx.conv_bn(a, pre + "conv2.weight", pre + "bn2", stride, 1, relu=True)
+                last, p = "3", 0
+            else:
+                a = ctx.conv_bn(out, pre + "conv1.weight", pre + "bn1", stride, 1, relu=True)
+                last, p = "2", 1
+            if stride != 1 or cin != w * exp:
                 sc = ctx.conv_bn(out, pre + "shortcut.0.weight", pre + "shortcut.1", stride, 0, relu=False)
             else:
                 sc = out
-            out = ctx.conv_bn(a, pre + "conv2.weight", pre + "bn2", 1, 1, relu=True, residual=sc)
-            cin = w
+            out = ctx.conv_bn(a, pre + f"conv{last}.weight", pre + f"bn{last}", 1, p, relu=True, residual=sc)
+            cin = w * exp
     out = ctx.gap(out)
     G, N = out.shape[:2]
     return ctx.linear(ctx.reshape(out, (G, N, out.shape[-1])), "linear.weight", "linear.bias", relu=False, final=True)
@@ -301,7 +311,8 @@ def _loan(ctx: Ctx, x: Tensor) -> Tensor:
 
 
 FORWARDS: Dict[str, Callable[[Ctx, Tensor], Tensor]] = {
-    "resnet18_cifar": _resnet_cifar, "resnet18_tiny": _resnet_tiny, "mnist": _mnist, "loan": _loan,
+    "resnet18_tiny": _resnet_tiny, "mnist": _mnist, "loan": _loan,
+    **{arch: _resnet_cifar for arch in CIFAR_RESNETS},
 }
 
 

@@ -25,7 +25,7 @@ from typing import Callable, Dict, List, Optional, Tuple
 import torch
 import torch.nn as nn
 
-from .mirror import build_mirror
+from .mirror import CIFAR_RESNETS, build_mirror
 
 
 @dataclass
@@ -170,7 +170,7 @@ def get_spec(arch: str) -> ModelSpec:
     if arch not in _SPECS:
         if arch == "mnist":
             _SPECS[arch] = _make_spec(arch, (28, 28, 1), 10, _mnist_fc1_special())
-        elif arch == "resnet18_cifar":
+        elif arch in CIFAR_RESNETS:
             _SPECS[arch] = _make_spec(arch, (32, 32, 3), 10)
         elif arch == "resnet18_tiny":
             _SPECS[arch] = _make_spec(arch, (64, 64, 3), 200)
@@ -181,6 +181,14 @@ def get_spec(arch: str) -> ModelSpec:
     return _SPECS[arch]
 
 
-def arch_for_type(t: str) -> str:
-    return {"mnist": "mnist", "cifar": "resnet18_cifar", "tiny-imagenet-200": "resnet18_tiny",
+def arch_for_type(t: str, model_arch: Optional[str] = None) -> str:
+    """Dataset type -> architecture; ``model_arch`` picks another member of the CIFAR ResNet
+    family (the reference always builds ResNet18 for CIFAR, ``image_helper.py:33-38``)."""
+    arch = {"mnist": "mnist", "cifar": "resnet18_cifar", "tiny-imagenet-200": "resnet18_tiny",
             "loan": "loan"}[t]
+    if model_arch:
+        if t != "cifar" or model_arch not in CIFAR_RESNETS:
+            raise ValueError(f"model_arch {model_arch!r} is not available for type {t!r} "
+                             f"(cifar: {sorted(CIFAR_RESNETS)})")
+        arch = model_arch
+    return arch

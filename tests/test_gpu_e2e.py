@@ -23,7 +23,8 @@ def _rel(a, b):
 
 
 @pytest.mark.parametrize("arch,shp", [("resnet18_cifar", (32, 32, 3)), ("mnist", (28, 28, 1)),
-                                      ("resnet18_tiny", (64, 64, 3)), ("loan", (91,))])
+                                      ("resnet18_tiny", (64, 64, 3)), ("loan", (91,)),
+                                      ("resnet34_cifar", (32, 32, 3)), ("resnet50_cifar", (32, 32, 3))])
 def test_train_step_hip_vs_reference(dev, arch, shp):
     """Grouped train step through the HIP kernels vs the fp32 reference.
 
@@ -73,10 +74,44 @@ def test_train_step_hip_vs_reference(dev, arch, shp):
         band = _rel(gp[g], gr[g])
         assert _rel(gh[g], gr[g]) < max(0.08, 1.6 * band), (arch, g, _rel(gh[g], gr[g]), band)
         sl = slice(fc.offset, fc.offset + fc.numel)
-        assert _rel(gh[g, sl], gr[g, sl]) < 0.05, (arch, "final layer")
+        band_fc = _rel(gp[g, sl], gr[g, sl])   # deep nets (ResNet-50+) are chaotic up to the head too
+        assert _rel(gh[g, sl], gr[g, sl]) < max(0.05, 1.6 * band_fc), (arch, "final layer", band_fc)
         if spec.B:
             assert _rel(sh[g, spec.P:], sr[g, spec.P:]) < 2e-2
     assert gh[2].abs().max().item() == 0.0          # inactive replica untouched
+
+
+@pytest.mark.parametrize("arch", ["resnet18_cifar", "resnet50_cifar", "resnet101_cifar"])
+def test_eval_forward_hip_vs_reference(dev, arch):
+    """Folded-BN eval forward of a model bank through the HIP kernels (bf16) vs the fp32
+    reference ops: logits and argmax agreement (the bottleneck family adds 1x1 stride-1
+    convs over 32..1024 channels and a 1024-wide linear)."""
+    from dba_mod_amd import ops
+    from dba_mod_amd.models import program as P
+    from dba_mod_amd.models.spec import get_spec
+    from dba_mod_amd.ops import hip, reference
+    spec = get_spec(arch)
+    torch.manual_seed(0)
+    bank = torch.stack([spec.init_flat(1), spec.init_flat(2)]).to(dev)
+    x = torch.rand(3, 64, 32, 32, 3, device=dev)
+    sel = torch.tensor([0, 1, 0], dtype=torch.int32, device=dev)
+
+    def run(mod, dt):
+        saved = {k: getattr(ops, k) for k in ops._OPS}
+        for k in ops._OPS:
+            setattr(ops, k, getattr(mod, k))
+        try:
+            ctx = P.Ctx(spec, None, None, sel, train=False, folded=P.fold_bank(spec, bank, dt), act_dtype=dt)
+            return P.forward(ctx, x.to(dt)).float()
+        finally:
+            for k, v in saved.items():
+                setattr(ops, k, v)
+
+    oh, orf = run(hip, torch.bfloat16), run(reference, torch.float32)
+    assert torch.isfinite(oh).all()
+    for g in range(3):
+        assert _rel(oh[g], orf[g]) < 0.05, (arch, g, _rel(oh[g], orf[g]))
+    assert (oh.argmax(-1) == orf.argmax(-1)).float().mean().item() > 0.9
 
 
 def _small_params(**kw):

@@ -10,7 +10,8 @@ from dba_mod_amd.models import program as P
 from dba_mod_amd.models.mirror import build_mirror
 from dba_mod_amd.models.spec import get_spec
 
-CASES = [("mnist", (28, 28, 1)), ("resnet18_cifar", (32, 32, 3)), ("resnet18_tiny", (64, 64, 3))]
+CASES = [("mnist", (28, 28, 1)), ("resnet18_cifar", (32, 32, 3)), ("resnet18_tiny", (64, 64, 3)),
+         ("resnet34_cifar", (32, 32, 3)), ("resnet50_cifar", (32, 32, 3))]
 
 
 @pytest.fixture
@@ -82,7 +83,8 @@ def test_eval_folding_matches_eval_mode(arch, shp):
     torch.testing.assert_close(out[0], out[2])
 
 
-@pytest.mark.parametrize("arch", ["mnist", "resnet18_cifar", "resnet18_tiny", "loan"])
+@pytest.mark.parametrize("arch", ["mnist", "resnet18_cifar", "resnet18_tiny", "loan", "resnet34_cifar",
+                                  "resnet50_cifar", "resnet101_cifar", "resnet152_cifar"])
 def test_state_dict_roundtrip_and_keys(arch):
     spec = get_spec(arch)
     m = build_mirror(arch)
@@ -106,6 +108,21 @@ def test_param_counts_match_survey():
     assert sum(e.numel for e in get_spec("resnet18_cifar").buffers) == 4_800
     assert get_spec("resnet18_tiny").n_params == 11_279_112
     assert get_spec("loan").n_params == 5_529
+    # rest of the CIFAR family (resnet_cifar.py:106-116), counted on the reference classes;
+    # the state_dict key order/shapes were checked equal to them as well
+    for a, n in (("resnet34_cifar", 5_326_506), ("resnet50_cifar", 5_899_050),
+                 ("resnet101_cifar", 10_660_138), ("resnet152_cifar", 14_582_570)):
+        assert get_spec(a).n_params == n, a
     for a in ("mnist", "resnet18_cifar", "resnet18_tiny", "loan"):
         s = get_spec(a)
         assert all(e.offset % 64 == 0 for e in s.params + s.buffers) and s.P % 64 == 0 and s.S % 64 == 0
+
+
+def test_model_arch_selection():
+    from dba_mod_amd.models.spec import arch_for_type
+    assert arch_for_type("cifar") == "resnet18_cifar"
+    assert arch_for_type("cifar", "resnet50_cifar") == "resnet50_cifar"
+    with pytest.raises(ValueError):
+        arch_for_type("mnist", "resnet50_cifar")
+    with pytest.raises(ValueError):
+        arch_for_type("cifar", "resnet200_cifar")
