@@ -1,0 +1,72 @@
+"""Per-stream kernel-time summary of a ``rocprofv3 --kernel-trace --output-format csv`` trace.
+
+``python -m dba_mod_amd.tools.trace_streams gpurun_out/prof/bench_kernel_trace.csv
+[--last-ms 750] [--top 12]`` prints a markdown report: for every HIP stream, the kernels that
+took the most time (ms, share of the stream, launches), then the union of all kernel
+intervals over the window — how much of the wall time the GPU had any kernel in flight.
+The window is the last ``--last-ms`` of the trace (the timed bench rounds; the warm start
+and the first warm-up round are before it).
+"""
+from __future__ import annotations
+
+import argparse
+import csv
+import re
+from collections import defaultdict
+from typing import Dict, List, Tuple
+
+
+def _short(name: str) -> str:
+    name = re.sub(r"\(anonymous namespace\)::", "", name)
+    m = re.match(r"(?:void )?([\w:]+(?:<[^()]*>)?)", name)
+    return m.group(1) if m else name[:60]
+
+
+def summarize(path: str, last_ms: float = 750.0, top: int = 12) -> str:
+    rows: List[Tuple[int, int, int, str]] = []
+    with open(path, newline="") as f:
+        for r in csv.DictReader(f):
+            rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), int(r["Stream_Id"]),
+                         _short(r["Kernel_Name"])))
+    if not rows:
+        return "empty trace\n"
+    t_end = max(r[1] for r in rows)
+    t0 = t_end - int(last_ms * 1e6)
+    win = [r for r in rows if r[0] >= t0]
+    per: Dict[int, Dict[str, List[float]]] = defaultdict(lambda: defaultdict(lambda: [0.0, 0]))
+    for s, e, st, k in win:
+        acc = per[st][k]
+        acc[0] += (e - s) / 1e6
+        acc[1] += 1
+    out = [f"Window: last {last_ms:.0f} ms of the trace, {len(win)} kernels.\n"]
+    for st in sorted(per):
+        tot = sum(v[0] for v in per[st].values())
+        out.append(f"\n## stream {st}: {tot:.1f} ms of kernels\n\n| kernel | ms | % | launches |\n|---|---|---|---|")
+        for k, (ms, n) in sorted(per[st].items(), key=lambda kv: -kv[1][0])[:top]:
+            out.append(f"| `{k}` | {ms:.1f} | {100 * ms / max(tot, 1e-9):.1f} | {n} |")
+    iv = sorted((s, e) for s, e, _, _ in win)
+    busy, cur_s, cur_e = 0, iv[0][0], iv[0][1]
+    for s, e in iv[1:]:
+        if s > cur_e:
+            busy += cur_e - cur_s
+            cur_s, cur_e = s, e
+        else:
+            cur_e = max(cur_e, e)
+    busy += cur_e - cur_s
+    span = (t_end - min(s for s, _ in iv)) / 1e6
+    out.append(f"\nUnion of kernel intervals: {busy / 1e6:.0f} ms of {span:.0f} ms "
+               f"({100 * busy / 1e6 / max(span, 1e-9):.0f} % of the window has a kernel in flight).\n")
+    return "\n".join(out) + "\n"
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
+    ap.add_argument("trace")
+    ap.add_argument("--last-ms", type=float, default=750.0)
+    ap.add_argument("--top", type=int, default=12)
+    a = ap.parse_args()
+    print(summarize(a.trace, a.last_ms, a.top), end="")
+
+
+if __name__ == "__main__":
+    main()

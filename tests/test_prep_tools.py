@@ -67,3 +67,18 @@ def test_partition_report_reproduces_attacker_shards(tmp_path):
     rows = {r["participant"]: int(r["total"]) for r in _csv.DictReader(open(out))}
     assert [rows[k] for k in ("17", "33", "77", "11")] == [526, 527, 496, 546]
     assert pdf.stat().st_size > 0
+
+
+def test_trace_streams_summary(tmp_path):
+    """rocprofv3 kernel-trace CSV -> per-stream markdown (tools/trace_streams.py)."""
+    from dba_mod_amd.tools.trace_streams import summarize
+    p = tmp_path / "k.csv"
+    hdr = '"Kind","Stream_Id","Kernel_Name","Start_Timestamp","End_Timestamp"\n'
+    rows = [("1", "void (anonymous namespace)::igemm3_kernel<64, 128, 3, unsigned short>(G3Args)", 0, 2_000_000),
+            ("1", "(anonymous namespace)::bn_reduce_kernel(float const*)", 2_000_000, 3_000_000),
+            ("4", "void (anonymous namespace)::pconv_kernel<32, 32>(PconvArgs)", 1_000_000, 5_000_000)]
+    p.write_text(hdr + "".join(f'"KERNEL_DISPATCH",{s},"{k}",{a},{b}\n' for s, k, a, b in rows))
+    md = summarize(str(p), last_ms=100)
+    assert "## stream 1: 3.0 ms" in md and "## stream 4: 4.0 ms" in md
+    assert "`igemm3_kernel<64, 128, 3, unsigned short>` | 2.0 | 66.7 | 1 |" in md
+    assert "Union of kernel intervals: 5 ms of 5 ms" in md
