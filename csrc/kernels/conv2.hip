@@ -325,12 +325,22 @@ __global__ __launch_bounds__(256) void igemm2_kernel(Igemm2Args a) {
 // Stems / first layers with Cs < 8 (CIFAR 3x3x3, Tiny 7x7x3, MNIST 5x5x1): every thread
 // gathers ONE output row's receptive field (k = tap*Cs + c, contiguous within a kernel row
 // in NHWC) straight into its LDS row; K <= 160 is consumed in 32-wide MFMA k-steps.
-template <typename OutT, int KMAX>
+// HALO: CIFAR-stem geometry (3x3, stride 1, pad 1, Cs 3, 256 % Wo == 0, 16-B aligned rows):
+// the block's 256 output pixels are 256/Wo whole image rows, so the input rows they need are
+// copied once into an LDS halo with 16-B loads and every receptive field is read from there.
+template <typename OutT, int KMAX, bool HALO = false>
 __global__ __launch_bounds__(256) void igemm_small_kernel(Igemm2Args a) {
   constexpr int BM = 256, BN = 32;
   constexpr int LPs = KMAX + 8;
-  __shared__ __attribute__((aligned(16))) uint16_t As[BM][LPs];
-  __shared__ __attribute__((aligned(16))) uint16_t Bs[BN][LPs];
+  // operand tiles, then (aliased) the fp32 output tile of the staged epilogue: a 160-B row
+  // stride keeps both the MFMA-layout writes and the row-per-thread 16-B reads conflict-free
+  constexpr int CP = 40;
+  constexpr int HALO_BYTES = HALO ? 4096 : 0;   // (256/Wo + 2) rows x (Wo + 2) px x 3 ch, Wo <= 64
+  constexpr int AB_BYTES = (BM + BN) * LPs * 2 + HALO_BYTES, C_BYTES = BM * CP * 4;
+  __shared__ __attribute__((aligned(16))) uint8_t smem[AB_BYTES > C_BYTES ? AB_BYTES : C_BYTES];
+  uint16_t(*As)[LPs] = (uint16_t(*)[LPs])smem;
+  uint16_t(*Bs)[LPs] = (uint16_t(*)[LPs])(smem + BM * LPs * 2);
+  float(*Cst)[CP] = (float(*)[CP])smem;
   const int g = blockIdx.y;
   const int HoWo = a.Ho * a.Wo;
   const int Mv = valid_rows(a.nvalid, g, a.N) * HoWo;
@@ -343,7 +353,75 @@ __global__ __launch_bounds__(256) void igemm_small_kernel(Igemm2Args a) {
   const int slot = a.wsel ? a.wsel[g] : g;
   const uint16_t* __restrict__ Wp = a.w + (long long)slot * a.w_sstride;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  {  // A: one row per thread
+  if constexpr (HALO) {
+    constexpr int HC = 3;                       // channels
+    const int R = BM / a.Wo;                    // output rows per block
+    const int RW = (a.Ws + 2) * HC;             // halo row: one zero pixel each side
+    uint16_t* halo = (uint16_t*)(smem + (BM + BN) * LPs * 2);
+    const int n = m0 / HoWo, p0 = (m0 - n * HoWo) / a.Wo;
+    const uint16_t* __restrict__ img = src + (long long)n * a.Hs * a.Ws * HC;
+    for (int e = tid; e < (R + 2) * RW; e += 256) halo[e] = 0;
+    __syncthreads();
+    const int vpr = a.Ws * HC / 8;              // 16-B vectors per input row
+    for (int e = tid; e < (R + 2) * vpr; e += 256) {
+      const int hr = e / vpr, v = e - hr * vpr, hs = p0 - 1 + hr;
+      if ((unsigned)hs < (unsigned)a.Hs) {
+        const uint4 d = *(const uint4*)(img + (long long)hs * a.Ws * HC + v * 8);
+        const uint16_t* dp = (const uint16_t*)&d;
+#pragma unroll
+        for (int t = 0; t < 8; ++t) halo[hr * RW + HC + v * 8 + t] = dp[t];
+      }
+    }
+    __syncthreads();
+    const int pr = tid / a.Wo, q = tid - pr * a.Wo;
+    const bool live = m0 + tid < Mv;
+    uint16_t vals[32];
+#pragma unroll
+    for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+      for (int j = 0; j < 9; ++j) vals[kh * 9 + j] = live ? halo[(pr + kh) * RW + q * HC + j] : (uint16_t)0;
+#pragma unroll
+    for (int k = 27; k < 32; ++k) vals[k] = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      uint4 pk;
+      uint16_t* pp = (uint16_t*)&pk;
+#pragma unroll
+      for (int t = 0; t < 8; ++t) pp[t] = vals[j * 8 + t];
+      *(uint4*)&As[tid][j * 8] = pk;
+    }
+  } else if constexpr (KMAX == 32) {
+    // A (K <= 32: CIFAR 3x3x3, MNIST 5x5x1): the row's whole receptive field is loaded into
+    // registers first — unrolled, branch-free clamped loads, so all of them are in flight at
+    // once instead of one global-load latency per tap — then written as four 16-B LDS stores
+    const int m = m0 + tid;
+    const int mm = m < Mv ? m : Mv - 1;
+    const int n = mm / HoWo, rem = mm - n * HoWo, p = rem / a.Wo, q = rem - p * a.Wo;
+    const int hs0 = p * a.stride - a.pad, ws0 = q * a.stride - a.pad;
+    const uint16_t* __restrict__ img = src + (long long)n * a.Hs * a.Ws * a.Cs;
+    uint16_t vals[32];
+    int kh = 0, kw = 0, c = 0;
+#pragma unroll
+    for (int k = 0; k < 32; ++k) {
+      const int hs = hs0 + kh, ws = ws0 + kw;
+      const bool in = k < K && m < Mv && (unsigned)hs < (unsigned)a.Hs && (unsigned)ws < (unsigned)a.Ws;
+      const int hc = min(max(hs, 0), a.Hs - 1), wc = min(max(ws, 0), a.Ws - 1);
+      const uint16_t t = img[(hc * a.Ws + wc) * a.Cs + min(c, a.Cs - 1)];
+      vals[k] = in ? t : (uint16_t)0;
+      if (++c == a.Cs) {
+        c = 0;
+        if (++kw == a.KW) { kw = 0; ++kh; }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      uint4 pk;
+      uint16_t* pp = (uint16_t*)&pk;
+#pragma unroll
+      for (int t = 0; t < 8; ++t) pp[t] = vals[j * 8 + t];
+      *(uint4*)&As[tid][j * 8] = pk;
+    }
+  } else {  // A: one row per thread
     const int m = m0 + tid;
     uint16_t* dst = As[tid];
     if (m < Mv) {
@@ -388,6 +466,43 @@ __global__ __launch_bounds__(256) void igemm_small_kernel(Igemm2Args a) {
   const float* bias = a.bias ? a.bias + (long long)slot * a.b_sstride : nullptr;
   const uint16_t* res = a.res ? a.res + (long long)g * a.out_gstride : nullptr;
   const int n = n0 + fr;
+  if constexpr (sizeof(OutT) == 2) {
+    if (a.Ncol % 8 == 0) {
+      // staged epilogue: acc (+bias) -> LDS fp32 tile -> each thread owns one output row and
+      // writes its up-to-32 channels as 16-B stores (the MFMA layout would give 2-B stores)
+      __syncthreads();   // every wave is done reading As / Bs
+      const float bv = (bias && n < a.Ncol) ? bias[n] : 0.f;
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          Cst[wid * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)][fr] = acc[i][r] + bv;
+      __syncthreads();
+      // lane -> (row, 8-channel chunk) with the chunk fastest: a wave stores 16 rows x 64 B
+      // contiguous per instruction when Ncol == 32
+#pragma unroll
+      for (int it = 0; it < BM * (BN / 8) / 256; ++it) {
+        const int idx = it * 256 + tid, row = idx / (BN / 8), c = idx % (BN / 8);
+        const int m = m0 + row;
+        if (m >= Mv || n0 + c * 8 + 8 > a.Ncol) continue;
+        const long long o = (long long)m * a.Ncol + n0 + c * 8;
+        const float4 lo = *(const float4*)&Cst[row][c * 8], hi = *(const float4*)&Cst[row][c * 8 + 4];
+        float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+        if (res) {
+          const uint4 rv = *(const uint4*)(res + o);
+          const uint16_t* rp = (const uint16_t*)&rv;
+#pragma unroll
+          for (int t = 0; t < 8; ++t) v[t] += bf2f(rp[t]);
+        }
+        uint4 pk;
+        uint16_t* pp = (uint16_t*)&pk;
+#pragma unroll
+        for (int t = 0; t < 8; ++t) pp[t] = f2bf(a.relu ? fmaxf(v[t], 0.f) : v[t]);
+        *(uint4*)((uint16_t*)out + o) = pk;
+      }
+      return;
+    }
+  }
   if (n >= a.Ncol) return;
   const float bv = bias ? bias[n] : 0.f;
 #pragma unroll
@@ -444,7 +559,12 @@ DBA_EXPORT int dba_conv2_fwd(const void* x, long long x_gstride, const void* w, 
       if (k32) hipLaunchKernelGGL((igemm_small_kernel<float, 32>), grid, dim3(256), 0, st, a);
       else hipLaunchKernelGGL((igemm_small_kernel<float, 160>), grid, dim3(256), 0, st, a);
     } else {
-      if (k32) hipLaunchKernelGGL((igemm_small_kernel<uint16_t, 32>), grid, dim3(256), 0, st, a);
+      const bool halo = KH == 3 && KW == 3 && Cin == 3 && stride == 1 && pad == 1 && Wo == W && Ho == H &&
+                        Wo <= 64 && 256 % Wo == 0 && (Ho * Wo) % 256 == 0 && (W * 3) % 8 == 0 &&
+                        ((uintptr_t)x % 16) == 0 && (x_gstride * 2) % 16 == 0 &&
+                        (256 / Wo + 2) * (Wo + 2) * 3 * 2 <= 4096;
+      if (halo) hipLaunchKernelGGL((igemm_small_kernel<uint16_t, 32, true>), grid, dim3(256), 0, st, a);
+      else if (k32) hipLaunchKernelGGL((igemm_small_kernel<uint16_t, 32>), grid, dim3(256), 0, st, a);
       else hipLaunchKernelGGL((igemm_small_kernel<uint16_t, 160>), grid, dim3(256), 0, st, a);
     }
     DBA_LAUNCH_CHECK();

@@ -40,7 +40,10 @@ def _rel(a, b):
 
 CONV_CASES = [
     # G, N, H, W, Cin, Cout, k, stride, pad
-    (3, 5, 32, 32, 3, 32, 3, 1, 1),      # CIFAR stem (generic path)
+    (3, 5, 32, 32, 3, 32, 3, 1, 1),      # CIFAR stem (small-Cin kernel, staged 16-B epilogue)
+    (2, 3, 32, 32, 3, 40, 3, 1, 1),      # small-Cin kernel, second column tile partly valid
+    (2, 3, 32, 32, 3, 32, 3, 2, 1),      # small-Cin kernel without the LDS halo (stride 2)
+    (2, 3, 16, 16, 3, 32, 3, 1, 1),      # LDS-halo stem, 16 output rows per block
     (2, 4, 32, 32, 32, 32, 3, 1, 1),     # layer1
     (2, 4, 32, 32, 32, 64, 3, 2, 1),     # layer2.0.conv1 (stride 2)
     (2, 4, 32, 32, 32, 64, 1, 2, 0),     # shortcut 1x1 s2
