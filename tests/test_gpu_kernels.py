@@ -221,6 +221,66 @@ def test_bn_train_fwd_bwd(H, R, C, relu, with_res):
     _close(gr, gr_r, 2e-2, 2e-2, "dgamma/dbeta")
 
 
+@pytest.mark.parametrize("C,Hh", [(32, 32), (64, 16), (128, 12)])
+def test_bn_train_large_multiblock(H, R, C, Hh):
+    """Multi-block reduce path (rows > the single-launch limit: partials, finalize, apply),
+    fwd + bwd, repeated eager calls and a HIP-graph replay against the fp32 reference."""
+    from dba_mod_amd.ops import hip as hip_ops
+    dev = torch.device("cuda")
+    torch.manual_seed(2)
+    G, N = 3, 10
+    assert N * Hh * Hh > hip_ops._BN_SMALL_ROWS
+    y = (torch.randn(G, N, Hh, Hh, C, device=dev) * 1.5 - 0.3).bfloat16()
+    nvalid = torch.tensor([10, 4, 0], dtype=torch.int32, device=dev)
+    gamma = torch.rand(G, C, device=dev) + 0.5
+    beta = torch.randn(G, C, device=dev) * 0.1
+    dout = torch.randn(G, N, Hh, Hh, C, device=dev).bfloat16()
+
+    def run():
+        rm = torch.zeros(G, C, device=dev)
+        rv = torch.ones(G, C, device=dev)
+        out, mean, invstd = H.bn_train(y, gamma, beta, rm, rv, nvalid, 0.1, 1e-5, True, None)
+        dg = torch.zeros(G, C, device=dev)
+        db = torch.zeros(G, C, device=dev)
+        dy = H.bn_train_bwd(dout, y, out, mean, invstd, gamma, nvalid, True, dg, db)
+        return out, mean, invstd, rm, rv, dg, db, dy
+
+    rm_r = torch.zeros(G, C, device=dev)
+    rv_r = torch.ones(G, C, device=dev)
+    out_r, mean_r, inv_r = R.bn_train(y.float(), gamma, beta, rm_r, rv_r, nvalid, 0.1, 1e-5, True, None)
+    dg_r = torch.zeros(G, C, device=dev)
+    db_r = torch.zeros(G, C, device=dev)
+    dy_r = R.bn_train_bwd(dout.float(), y.float(), out_r, mean_r, inv_r, gamma, nvalid, True, dg_r, db_r)
+
+    def check(res, tag):
+        out, mean, invstd, rm, rv, dg, db, dy = res
+        for g in range(2):
+            n = int(nvalid[g])
+            _close(out[g, :n], out_r[g, :n], 2e-2, 2e-2, f"{tag} bn out")
+            _close(mean[g], mean_r[g], 1e-4, 1e-4, f"{tag} mean")
+            _close(invstd[g], inv_r[g], 1e-3, 1e-4, f"{tag} invstd")
+            assert _rel(dy[g, :n], dy_r[g, :n]) < 2e-2, tag
+        _close(rm, rm_r, 1e-4, 1e-5, f"{tag} running mean")
+        _close(rv, rv_r, 1e-3, 1e-4, f"{tag} running var")
+        _close(dg, dg_r, 2e-2, 2e-2, f"{tag} dgamma")
+        _close(db, db_r, 2e-2, 2e-2, f"{tag} dbeta")
+
+    for i in range(3):
+        check(run(), f"eager{i}")
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        run()
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        res = run()
+    for i in range(3):
+        g.replay()
+        torch.cuda.synchronize()
+        check(res, f"graph{i}")
+
+
 def test_bn_fold(H, R):
     dev = torch.device("cuda")
     slots, Cout, K = 3, 64, 288
