@@ -13,7 +13,23 @@ def main() -> int:
     which = sys.argv[1:] or ["pconv1", "pconv2", "pw2", "pw3", "pw4"]
     torch.manual_seed(0)
     for name in which:
-        if name.startswith("pconv"):
+        if name.startswith("bn"):
+            # training-mode BN forward + backward at a 10-client group's stage shapes
+            Hh, C = {"bn1": (32, 32), "bn2": (16, 64), "bn3": (8, 128)}[name]
+            G, N = 10, 64
+            y = torch.randn(G, N, Hh, Hh, C, device=dev).bfloat16()
+            gamma = torch.ones(G, C, device=dev)
+            beta = torch.zeros(G, C, device=dev)
+            rm = torch.zeros(G, C, device=dev)
+            rv = torch.ones(G, C, device=dev)
+            nv = torch.full((G,), N, dtype=torch.int32, device=dev)
+            dout = torch.randn_like(y)
+            dg = torch.zeros(G, C, device=dev)
+            db = torch.zeros(G, C, device=dev)
+            for _ in range(3):
+                out, mean, invstd = H.bn_train(y, gamma, beta, rm, rv, nv, 0.1, 1e-5, True, None)
+                H.bn_train_bwd(dout, y, out, mean, invstd, gamma, nv, True, dg, db)
+        elif name.startswith("pconv"):
             G, N, Hh, C = (17, 1024, 32, 32) if name == "pconv1" else (17, 1024, 16, 64)
             x = torch.randn(G, N, Hh, Hh, C, device=dev).bfloat16()
             w = (torch.randn(G, C, 3, 3, C, device=dev) * 0.05).bfloat16()
