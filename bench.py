@@ -15,7 +15,7 @@ not shipped; the bench builds the equivalent starting point with ``--pretrain-ro
 Rounds then start at 201, so with the default ``--warmup 2`` the timed window 203..210
 contains all four poison rounds.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--dtype fp32|bf16]
     torchrun --nproc-per-node N bench.py --gpus N ...     # one rank per GPU over RCCL
 
 Strong scaling: the round's work is fixed; N GPUs split its clients (LPT) and its
@@ -61,12 +61,15 @@ def main() -> int:
                          "pretrained checkpoint; untimed)")
     ap.add_argument("--start-epoch", type=int, default=None,
                     help="first (warmup) round; default: first poison round - warmup")
+    ap.add_argument("--dtype", choices=("fp32", "bf16"), default="fp32",
+                    help="compute precision: fp32 = the reference's (split-bf16 MFMA kernels, default); "
+                         "bf16 = fast mode (bf16 activations, fp32 master weights)")
     ap.add_argument("--set", dest="overrides", nargs="*", default=[])
     args = ap.parse_args()
 
     dctx = init_distributed(prefer_gpu=not args.cpu)
     over = {"resumed_model": False, "synthetic_data": True, "save_model": False,
-            "pretrain_rounds": args.pretrain_rounds}
+            "pretrain_rounds": args.pretrain_rounds, "compute_dtype": args.dtype}
     if args.aggregation:
         over["aggregation_methods"] = args.aggregation
     over.update(C.parse_override(args.overrides))
@@ -111,7 +114,9 @@ def main() -> int:
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1000.0 * elapsed / max(1, args.steps), 2),
             "higher_is_better": True, "scaling": "strong",
             "vs_baseline": round(rps / BASELINE_ROUNDS_PER_S, 2) if params.type == "cifar" else None,
-            "dtype": "bf16" if server.dtype == torch.bfloat16 else "fp32",
+            # the kernels' precision: the server's compute dtype selects the kernel family
+            # (ops/hip.py dispatches on the activation dtype and never converts)
+            "dtype": {torch.bfloat16: "bf16", torch.float32: "fp32"}[server.dtype],
             "data": (f"synthetic ({params.type} shapes/class sizes); random-init weights warm-started by "
                      f"{args.pretrain_rounds} benign FedAvg rounds (untimed)"),
             "config": {"model": MODEL_NAMES.get(params.type, params.type),

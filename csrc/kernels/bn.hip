@@ -26,9 +26,9 @@ __host__ __device__ inline int rows_per_block(int C) {
 // Per-block partial sums (no atomics, no pre-zeroing): part[g][blk][0][c] = sum x (STATS)
 // or sum d (BWD); part[g][blk][1][c] = sum x^2 or sum d*xhat.  Blocks past the valid rows
 // write zeros so the finalize pass can sum every slot unconditionally.
-template <bool BWD>
-__global__ __launch_bounds__(256) void bn_reduce_kernel(const uint16_t* __restrict__ y, const uint16_t* __restrict__ dout,
-                                                        const uint16_t* __restrict__ out, const float* __restrict__ mean,
+template <bool BWD, typename T>
+__global__ __launch_bounds__(256) void bn_reduce_kernel(const T* __restrict__ y, const T* __restrict__ dout,
+                                                        const T* __restrict__ out, const float* __restrict__ mean,
                                                         const float* __restrict__ invstd, int relu,
                                                         const int* __restrict__ nvalid, int N, int HW, int C,
                                                         float* __restrict__ part) {
@@ -58,22 +58,20 @@ __global__ __launch_bounds__(256) void bn_reduce_kernel(const uint16_t* __restri
   const long long gbase = (long long)g * R * C;
   for (int r = r0 + rr; r < r1; r += rpp) {
     const long long o = gbase + (long long)r * C + cg * 8;
-    const uint4 yv = *(const uint4*)(y + o);
-    const uint16_t* yp = (const uint16_t*)&yv;
+    float yp[8];
+    ld8(y + o, yp);
     if (!BWD) {
 #pragma unroll
-      for (int e = 0; e < 8; ++e) { const float v = bf2f(yp[e]); s0[e] += v; s1[e] += v * v; }
+      for (int e = 0; e < 8; ++e) { const float v = yp[e]; s0[e] += v; s1[e] += v * v; }
     } else {
-      const uint4 dv = *(const uint4*)(dout + o);
-      const uint16_t* dp = (const uint16_t*)&dv;
-      uint4 ov = make_uint4(0, 0, 0, 0);
-      if (relu) ov = *(const uint4*)(out + o);
-      const uint16_t* op = (const uint16_t*)&ov;
+      float dp[8], op[8];
+      ld8(dout + o, dp);
+      if (relu) ld8(out + o, op);
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        float d = bf2f(dp[e]);
-        if (relu && !(bf2f(op[e]) > 0.f)) d = 0.f;
-        const float xh = (bf2f(yp[e]) - mu[e]) * is[e];
+        float d = dp[e];
+        if (relu && !(op[e] > 0.f)) d = 0.f;
+        const float xh = (yp[e] - mu[e]) * is[e];
         s0[e] += d; s1[e] += d * xh;
       }
     }
@@ -153,10 +151,11 @@ __global__ void bn_finalize_kernel(const float* __restrict__ part, int nblk, con
 // Elementwise passes: 256 % (C/8) == 0, so every thread of the grid-stride loop always owns
 // the same 8 channels; their per-(replica, channel) coefficients are loaded once per replica
 // change instead of 4-7 scalar loads per element.
-__global__ void bn_apply_kernel(const uint16_t* __restrict__ y, const float* __restrict__ mean,
+template <typename T>
+__global__ void bn_apply_kernel(const T* __restrict__ y, const float* __restrict__ mean,
                                 const float* __restrict__ invstd, const float* __restrict__ gamma,
-                                const float* __restrict__ beta, long long p_gstride, const uint16_t* __restrict__ res,
-                                int relu, uint16_t* __restrict__ out, const int* __restrict__ nvalid, int G, int N,
+                                const float* __restrict__ beta, long long p_gstride, const T* __restrict__ res,
+                                int relu, T* __restrict__ out, const int* __restrict__ nvalid, int G, int N,
                                 int HW, int C) {
   // grid (blocks, G): only the replica's VALID rows are touched (inactive replicas exit at
   // once; padded rows are never read downstream — every consumer gates on nvalid)
@@ -176,30 +175,27 @@ __global__ void bn_apply_kernel(const uint16_t* __restrict__ y, const float* __r
   const long long base = (long long)g * N * HW * c8;
   for (int t = tid0; t < total; t += gridDim.x * blockDim.x) {
     const long long o = (base + t) * 8;
-    const uint4 yv = *(const uint4*)(y + o);
-    const uint16_t* yp = (const uint16_t*)&yv;
-    uint4 rv4 = make_uint4(0, 0, 0, 0);
-    if (res) rv4 = *(const uint4*)(res + o);
-    const uint16_t* rp = (const uint16_t*)&rv4;
-    uint4 res8;
-    uint16_t* op = (uint16_t*)&res8;
+    float yp[8], rp[8], op[8];
+    ld8(y + o, yp);
+    if (res) ld8(res + o, rp);
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      float v = fmaf(bf2f(yp[e]), sc[e], sh[e]);
-      if (res) v += bf2f(rp[e]);
+      float v = fmaf(yp[e], sc[e], sh[e]);
+      if (res) v += rp[e];
       if (relu) v = fmaxf(v, 0.f);
-      op[e] = f2bf(v);
+      op[e] = v;
     }
-    *(uint4*)(out + o) = res8;
+    st8(out + o, op);
   }
 }
 
 // dy = gamma*is/n * (n*d - sum d - xhat * sum d*xhat) = A*d + B*y + K per (replica, channel)
-__global__ void bn_bwd_apply_kernel(const uint16_t* __restrict__ dout, const uint16_t* __restrict__ out,
-                                    const uint16_t* __restrict__ y, const float* __restrict__ mean,
+template <typename T>
+__global__ void bn_bwd_apply_kernel(const T* __restrict__ dout, const T* __restrict__ out,
+                                    const T* __restrict__ y, const float* __restrict__ mean,
                                     const float* __restrict__ invstd, const float* __restrict__ gamma,
                                     long long p_gstride, const float* __restrict__ sums, int relu,
-                                    uint16_t* __restrict__ dy, uint16_t* __restrict__ dres,
+                                    T* __restrict__ dy, T* __restrict__ dres,
                                     const int* __restrict__ nvalid, int G, int N, int HW, int C) {
   const int g = blockIdx.y;
   const int c8 = C / 8;
@@ -224,25 +220,17 @@ __global__ void bn_bwd_apply_kernel(const uint16_t* __restrict__ dout, const uin
   const long long base = (long long)g * N * HW * c8;
   for (int t = tid0; t < total; t += gridDim.x * blockDim.x) {
     const long long o = (base + t) * 8;
-    const uint4 dv = *(const uint4*)(dout + o);
-    const uint4 yv = *(const uint4*)(y + o);
-    uint4 ov = make_uint4(0, 0, 0, 0);
-    if (relu) ov = *(const uint4*)(out + o);
-    const uint16_t* dp = (const uint16_t*)&dv;
-    const uint16_t* yp = (const uint16_t*)&yv;
-    const uint16_t* op = (const uint16_t*)&ov;
-    uint4 r1, r2;
-    uint16_t* p1 = (uint16_t*)&r1;
-    uint16_t* p2 = (uint16_t*)&r2;
+    float dp[8], yp[8], op[8], p1[8];
+    ld8(dout + o, dp);
+    ld8(y + o, yp);
+    if (relu) ld8(out + o, op);
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      float d = bf2f(dp[e]);
-      if (relu && !(bf2f(op[e]) > 0.f)) d = 0.f;
-      p1[e] = f2bf(fmaf(A[e], d, fmaf(B[e], bf2f(yp[e]), K[e])));
-      p2[e] = f2bf(d);
+      if (relu && !(op[e] > 0.f)) dp[e] = 0.f;
+      p1[e] = fmaf(A[e], dp[e], fmaf(B[e], yp[e], K[e]));
     }
-    *(uint4*)(dy + o) = r1;
-    if (dres) *(uint4*)(dres + o) = r2;
+    st8(dy + o, p1);
+    if (dres) st8(dres + o, dp);
   }
 }
 
@@ -283,11 +271,12 @@ __device__ __forceinline__ void block_sum16(float (&a)[8], float (&b)[8], float 
   __syncthreads();
 }
 
+template <typename T>
 __global__ __launch_bounds__(256) void bn_small_fwd_kernel(
-    const uint16_t* __restrict__ y, const int* __restrict__ nvalid, int N, int HW, int C,
+    const T* __restrict__ y, const int* __restrict__ nvalid, int N, int HW, int C,
     const float* __restrict__ gamma, const float* __restrict__ beta, float* __restrict__ rm, float* __restrict__ rv,
-    long long p_gstride, float momentum, float eps, const uint16_t* __restrict__ res, int relu,
-    uint16_t* __restrict__ out, float* __restrict__ mean, float* __restrict__ invstd) {
+    long long p_gstride, float momentum, float eps, const T* __restrict__ res, int relu,
+    T* __restrict__ out, float* __restrict__ mean, float* __restrict__ invstd) {
   __shared__ float red[2][4][8];
   __shared__ float coef[2][8];
   const int g = blockIdx.y, c0 = blockIdx.x * 8, tid = threadIdx.x;
@@ -301,10 +290,10 @@ __global__ __launch_bounds__(256) void bn_small_fwd_kernel(
 #pragma unroll
   for (int e = 0; e < 8; ++e) { s0[e] = 0.f; s1[e] = 0.f; }
   for (int r = tid; r < R; r += 256) {
-    const uint4 v = *(const uint4*)(y + base + (long long)r * C);
-    const uint16_t* p = (const uint16_t*)&v;
+    float p[8];
+    ld8(y + base + (long long)r * C, p);
 #pragma unroll
-    for (int e = 0; e < 8; ++e) { const float x = bf2f(p[e]); s0[e] += x; s1[e] = fmaf(x, x, s1[e]); }
+    for (int e = 0; e < 8; ++e) { const float x = p[e]; s0[e] += x; s1[e] = fmaf(x, x, s1[e]); }
   }
   block_sum16(s0, s1, red);
   if (tid < 8) {
@@ -333,29 +322,26 @@ __global__ __launch_bounds__(256) void bn_small_fwd_kernel(
   for (int e = 0; e < 8; ++e) { sc[e] = coef[0][e]; sh[e] = coef[1][e]; }
   for (int r = tid; r < R; r += 256) {
     const long long o = base + (long long)r * C;
-    const uint4 v = *(const uint4*)(y + o);
-    const uint16_t* p = (const uint16_t*)&v;
-    uint4 rv4 = make_uint4(0, 0, 0, 0);
-    if (res) rv4 = *(const uint4*)(res + o);
-    const uint16_t* rp = (const uint16_t*)&rv4;
-    uint4 w;
-    uint16_t* op = (uint16_t*)&w;
+    float p[8], rp[8], op[8];
+    ld8(y + o, p);
+    if (res) ld8(res + o, rp);
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      float x = fmaf(bf2f(p[e]), sc[e], sh[e]);
-      if (res) x += bf2f(rp[e]);
+      float x = fmaf(p[e], sc[e], sh[e]);
+      if (res) x += rp[e];
       if (relu) x = fmaxf(x, 0.f);
-      op[e] = f2bf(x);
+      op[e] = x;
     }
-    *(uint4*)(out + o) = w;
+    st8(out + o, op);
   }
 }
 
+template <typename T>
 __global__ __launch_bounds__(256) void bn_small_bwd_kernel(
-    const uint16_t* __restrict__ dout, const uint16_t* __restrict__ out, const uint16_t* __restrict__ y,
+    const T* __restrict__ dout, const T* __restrict__ out, const T* __restrict__ y,
     const float* __restrict__ mean, const float* __restrict__ invstd, const float* __restrict__ gamma,
     long long p_gstride, int relu, float* __restrict__ dgamma, float* __restrict__ dbeta, long long g_gstride,
-    uint16_t* __restrict__ dy, uint16_t* __restrict__ dres, const int* __restrict__ nvalid, int N, int HW, int C) {
+    T* __restrict__ dy, T* __restrict__ dres, const int* __restrict__ nvalid, int N, int HW, int C) {
   __shared__ float red[2][4][8];
   __shared__ float coef[3][8];
   const int g = blockIdx.y, c0 = blockIdx.x * 8, tid = threadIdx.x;
@@ -372,19 +358,16 @@ __global__ __launch_bounds__(256) void bn_small_bwd_kernel(
   }
   for (int r = tid; r < R; r += 256) {
     const long long o = base + (long long)r * C;
-    const uint4 dv = *(const uint4*)(dout + o);
-    const uint4 yv = *(const uint4*)(y + o);
-    uint4 ov = make_uint4(0, 0, 0, 0);
-    if (relu) ov = *(const uint4*)(out + o);
-    const uint16_t* dp = (const uint16_t*)&dv;
-    const uint16_t* yp = (const uint16_t*)&yv;
-    const uint16_t* op = (const uint16_t*)&ov;
+    float dp[8], yp[8], op[8];
+    ld8(dout + o, dp);
+    ld8(y + o, yp);
+    if (relu) ld8(out + o, op);
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      float d = bf2f(dp[e]);
-      if (relu && !(bf2f(op[e]) > 0.f)) d = 0.f;
+      float d = dp[e];
+      if (relu && !(op[e] > 0.f)) d = 0.f;
       s0[e] += d;
-      s1[e] = fmaf(d, (bf2f(yp[e]) - mu[e]) * is[e], s1[e]);
+      s1[e] = fmaf(d, (yp[e] - mu[e]) * is[e], s1[e]);
     }
   }
   block_sum16(s0, s1, red);
@@ -407,33 +390,26 @@ __global__ __launch_bounds__(256) void bn_small_bwd_kernel(
   for (int e = 0; e < 8; ++e) { A[e] = coef[0][e]; B[e] = coef[1][e]; K[e] = coef[2][e]; }
   for (int r = tid; r < R; r += 256) {
     const long long o = base + (long long)r * C;
-    const uint4 dv = *(const uint4*)(dout + o);
-    const uint4 yv = *(const uint4*)(y + o);
-    uint4 ov = make_uint4(0, 0, 0, 0);
-    if (relu) ov = *(const uint4*)(out + o);
-    const uint16_t* dp = (const uint16_t*)&dv;
-    const uint16_t* yp = (const uint16_t*)&yv;
-    const uint16_t* op = (const uint16_t*)&ov;
-    uint4 r1, r2;
-    uint16_t* p1 = (uint16_t*)&r1;
-    uint16_t* p2 = (uint16_t*)&r2;
+    float dp[8], yp[8], op[8], p1[8];
+    ld8(dout + o, dp);
+    ld8(y + o, yp);
+    if (relu) ld8(out + o, op);
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      float d = bf2f(dp[e]);
-      if (relu && !(bf2f(op[e]) > 0.f)) d = 0.f;
-      p1[e] = f2bf(fmaf(A[e], d, fmaf(B[e], bf2f(yp[e]), K[e])));
-      p2[e] = f2bf(d);
+      if (relu && !(op[e] > 0.f)) dp[e] = 0.f;
+      p1[e] = fmaf(A[e], dp[e], fmaf(B[e], yp[e], K[e]));
     }
-    *(uint4*)(dy + o) = r1;
-    if (dres) *(uint4*)(dres + o) = r2;
+    st8(dy + o, p1);
+    if (dres) st8(dres + o, dp);
   }
 }
 
 // eval fold: wf[s][co][k] = w[s][co][k] * s_c ; bf[s][co] = (b0 - rm) * s_c + beta
+template <typename T>
 __global__ void bn_fold_kernel(const float* __restrict__ w, long long w_sstride, const float* __restrict__ cbias,
                                const float* __restrict__ gamma, const float* __restrict__ beta,
                                const float* __restrict__ rm, const float* __restrict__ rv, long long s_gstride,
-                               float eps, uint16_t* __restrict__ wf, float* __restrict__ bf, int slots, int Cout,
+                               float eps, T* __restrict__ wf, float* __restrict__ bf, int slots, int Cout,
                                int K) {
   const long long per = (long long)Cout * K;
   const long long total = per * slots;
@@ -444,7 +420,7 @@ __global__ void bn_fold_kernel(const float* __restrict__ w, long long w_sstride,
     const int k = (int)(rem - (long long)co * K);
     const long long p = (long long)s * s_gstride + co;
     const float sc = gamma[p] / sqrtf(rv[p] + eps);
-    wf[t] = f2bf(w[(long long)s * w_sstride + rem] * sc);
+    wf[t] = from_f<T>(w[(long long)s * w_sstride + rem] * sc);
     if (k == 0) {
       const float b0 = cbias ? cbias[p] : 0.f;
       bf[(long long)s * Cout + co] = (b0 - rm[p]) * sc + beta[p];
@@ -465,14 +441,22 @@ dim3 ggrid(int G, int N, int HW, int C) {
 
 DBA_EXPORT int dba_bn_partial_blocks(int N, int HW, int C) { return ceil_div((long long)N * HW, rows_per_block(C)); }
 
-// part: [G][nblk][2][C] fp32 workspace (no initialisation needed)
+// Channel-layout contract of every BN launcher (returns -102 otherwise): C % 8 == 0 and
+// 256 % (C / 8) == 0, so a thread of the grid-stride elementwise passes always owns the same
+// 8 channels (ggrid), and rows_per_block(C) >= 1.
+static bool bn_layout_ok(int C) { return C > 0 && C % 8 == 0 && C <= 2048 && 256 % (C / 8) == 0; }
+
+#define BN_T(f32, call) do { if (f32) { typedef float T; call; } else { typedef uint16_t T; call; } } while (0)
+
+// part: [G][nblk][2][C] fp32 workspace (no initialisation needed); y fp32 (f32) or bf16
 DBA_EXPORT int dba_bn_stats(const void* y, const int* nvalid, int G, int N, int HW, int C, float* part, float* rm,
                             float* rv, long long s_gstride, float momentum, float eps, float* mean, float* invstd,
-                            void* stream) {
+                            int f32, void* stream) {
+  if (!bn_layout_ok(C)) return -102;
   hipStream_t st = (hipStream_t)stream;
   const int nblk = ceil_div((long long)N * HW, rows_per_block(C));
-  hipLaunchKernelGGL(bn_reduce_kernel<false>, dim3(nblk, G), dim3(256), 0, st, (const uint16_t*)y, nullptr, nullptr,
-                     nullptr, nullptr, 0, nvalid, N, HW, C, part);
+  BN_T(f32, hipLaunchKernelGGL((bn_reduce_kernel<false, T>), dim3(nblk, G), dim3(256), 0, st, (const T*)y, nullptr,
+                               nullptr, nullptr, nullptr, 0, nvalid, N, HW, C, part));
   hipLaunchKernelGGL(bn_finalize_kernel, dim3(ceil_div(C, C < 64 ? C : 64), G), dim3(256), 0, st, part, nblk, nvalid, N, HW, C,
                      rm, rv, s_gstride, momentum, eps, mean, invstd, G);
   DBA_LAUNCH_CHECK();
@@ -480,9 +464,11 @@ DBA_EXPORT int dba_bn_stats(const void* y, const int* nvalid, int G, int N, int 
 
 DBA_EXPORT int dba_bn_apply(const void* y, const float* mean, const float* invstd, const float* gamma, const float* beta,
                             long long p_gstride, const void* res, int relu, void* out, const int* nvalid, int G, int N,
-                            int HW, int C, void* stream) {
-  hipLaunchKernelGGL(bn_apply_kernel, ggrid(G, N, HW, C), dim3(256), 0, (hipStream_t)stream, (const uint16_t*)y, mean,
-                     invstd, gamma, beta, p_gstride, (const uint16_t*)res, relu, (uint16_t*)out, nvalid, G, N, HW, C);
+                            int HW, int C, int f32, void* stream) {
+  if (!bn_layout_ok(C)) return -102;
+  BN_T(f32, hipLaunchKernelGGL((bn_apply_kernel<T>), ggrid(G, N, HW, C), dim3(256), 0, (hipStream_t)stream,
+                               (const T*)y, mean, invstd, gamma, beta, p_gstride, (const T*)res, relu, (T*)out, nvalid,
+                               G, N, HW, C));
   DBA_LAUNCH_CHECK();
 }
 
@@ -490,47 +476,50 @@ DBA_EXPORT int dba_bn_apply(const void* y, const float* mean, const float* invst
 DBA_EXPORT int dba_bn_bwd(const void* dout, const void* out, const void* y, const float* mean, const float* invstd,
                           const float* gamma, long long p_gstride, int relu, float* dgamma, float* dbeta,
                           long long g_gstride, void* dy, void* dres, float* part, const int* nvalid, int G, int N,
-                          int HW, int C, void* stream) {
+                          int HW, int C, int f32, void* stream) {
+  if (!bn_layout_ok(C)) return -102;
   hipStream_t st = (hipStream_t)stream;
   const int nblk = ceil_div((long long)N * HW, rows_per_block(C));
   float* sums = part + (long long)G * nblk * 2 * C;
-  hipLaunchKernelGGL(bn_reduce_kernel<true>, dim3(nblk, G), dim3(256), 0, st, (const uint16_t*)y,
-                     (const uint16_t*)dout, (const uint16_t*)out, mean, invstd, relu, nvalid, N, HW, C, part);
+  BN_T(f32, hipLaunchKernelGGL((bn_reduce_kernel<true, T>), dim3(nblk, G), dim3(256), 0, st, (const T*)y,
+                               (const T*)dout, (const T*)out, mean, invstd, relu, nvalid, N, HW, C, part));
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(ceil_div(C, C < 64 ? C : 64), G), dim3(256), 0, st, part, nblk, sums, dgamma,
                      dbeta, g_gstride, G, C);
-  hipLaunchKernelGGL(bn_bwd_apply_kernel, ggrid(G, N, HW, C), dim3(256), 0, st, (const uint16_t*)dout,
-                     (const uint16_t*)out, (const uint16_t*)y, mean, invstd, gamma, p_gstride, sums, relu,
-                     (uint16_t*)dy, (uint16_t*)dres, nvalid, G, N, HW, C);
+  BN_T(f32, hipLaunchKernelGGL((bn_bwd_apply_kernel<T>), ggrid(G, N, HW, C), dim3(256), 0, st, (const T*)dout,
+                               (const T*)out, (const T*)y, mean, invstd, gamma, p_gstride, sums, relu, (T*)dy,
+                               (T*)dres, nvalid, G, N, HW, C));
   DBA_LAUNCH_CHECK();
 }
 
 // single-launch BN forward for rows-per-replica <= 16384 (see bn_small_fwd_kernel)
 DBA_EXPORT int dba_bn_small_fwd(const void* y, const int* nvalid, int G, int N, int HW, int C, const float* gamma,
                                 const float* beta, float* rm, float* rv, long long p_gstride, float momentum, float eps,
-                                const void* res, int relu, void* out, float* mean, float* invstd, void* stream) {
-  if (C % 8 != 0) return -100;
-  hipLaunchKernelGGL(bn_small_fwd_kernel, dim3(C / 8, G), dim3(256), 0, (hipStream_t)stream, (const uint16_t*)y,
-                     nvalid, N, HW, C, gamma, beta, rm, rv, p_gstride, momentum, eps, (const uint16_t*)res, relu,
-                     (uint16_t*)out, mean, invstd);
+                                const void* res, int relu, void* out, float* mean, float* invstd, int f32,
+                                void* stream) {
+  if (C % 8 != 0) return -102;
+  BN_T(f32, hipLaunchKernelGGL((bn_small_fwd_kernel<T>), dim3(C / 8, G), dim3(256), 0, (hipStream_t)stream,
+                               (const T*)y, nvalid, N, HW, C, gamma, beta, rm, rv, p_gstride, momentum, eps,
+                               (const T*)res, relu, (T*)out, mean, invstd));
   DBA_LAUNCH_CHECK();
 }
 
 DBA_EXPORT int dba_bn_small_bwd(const void* dout, const void* out, const void* y, const float* mean,
                                 const float* invstd, const float* gamma, long long p_gstride, int relu, float* dgamma,
                                 float* dbeta, long long g_gstride, void* dy, void* dres, const int* nvalid, int G,
-                                int N, int HW, int C, void* stream) {
-  if (C % 8 != 0) return -100;
-  hipLaunchKernelGGL(bn_small_bwd_kernel, dim3(C / 8, G), dim3(256), 0, (hipStream_t)stream,
-                     (const uint16_t*)dout, (const uint16_t*)out, (const uint16_t*)y, mean, invstd, gamma, p_gstride,
-                     relu, dgamma, dbeta, g_gstride, (uint16_t*)dy, (uint16_t*)dres, nvalid, N, HW, C);
+                                int N, int HW, int C, int f32, void* stream) {
+  if (C % 8 != 0) return -102;
+  BN_T(f32, hipLaunchKernelGGL((bn_small_bwd_kernel<T>), dim3(C / 8, G), dim3(256), 0, (hipStream_t)stream,
+                               (const T*)dout, (const T*)out, (const T*)y, mean, invstd, gamma, p_gstride, relu,
+                               dgamma, dbeta, g_gstride, (T*)dy, (T*)dres, nvalid, N, HW, C));
   DBA_LAUNCH_CHECK();
 }
 
+// wf in fp32 (f32) or bf16
 DBA_EXPORT int dba_bn_fold(const float* w, long long w_sstride, const float* cbias, const float* gamma,
                            const float* beta, const float* rm, const float* rv, long long s_gstride, float eps,
-                           void* wf, float* bf, int slots, int Cout, int K, void* stream) {
+                           void* wf, float* bf, int slots, int Cout, int K, int f32, void* stream) {
   const long long n = (long long)slots * Cout * K;
-  hipLaunchKernelGGL(bn_fold_kernel, dim3(egrid(n)), dim3(256), 0, (hipStream_t)stream, w, w_sstride, cbias, gamma,
-                     beta, rm, rv, s_gstride, eps, (uint16_t*)wf, bf, slots, Cout, K);
+  BN_T(f32, hipLaunchKernelGGL((bn_fold_kernel<T>), dim3(egrid(n)), dim3(256), 0, (hipStream_t)stream, w, w_sstride,
+                               cbias, gamma, beta, rm, rv, s_gstride, eps, (T*)wf, bf, slots, Cout, K));
   DBA_LAUNCH_CHECK();
 }

@@ -40,6 +40,29 @@ template <typename T> __device__ __forceinline__ T from_f(float v);
 template <> __device__ __forceinline__ float from_f<float>(float v) { return v; }
 template <> __device__ __forceinline__ uint16_t from_f<uint16_t>(float v) { return f2bf(v); }
 
+// 8 consecutive elements (16-B bf16 / 32-B fp32 vector access) <-> float[8]
+__device__ __forceinline__ void ld8(const uint16_t* __restrict__ p, float (&v)[8]) {
+  const uint4 u = *(const uint4*)p;
+  const uint16_t* q = (const uint16_t*)&u;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) v[e] = bf2f(q[e]);
+}
+__device__ __forceinline__ void ld8(const float* __restrict__ p, float (&v)[8]) {
+  const float4 a = ((const float4*)p)[0], b = ((const float4*)p)[1];
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+__device__ __forceinline__ void st8(uint16_t* __restrict__ p, const float (&v)[8]) {
+  uint4 u;
+  uint16_t* q = (uint16_t*)&u;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) q[e] = f2bf(v[e]);
+  *(uint4*)p = u;
+}
+__device__ __forceinline__ void st8(float* __restrict__ p, const float (&v)[8]) {
+  ((float4*)p)[0] = make_float4(v[0], v[1], v[2], v[3]);
+  ((float4*)p)[1] = make_float4(v[4], v[5], v[6], v[7]);
+}
+
 // lowbias32 — identical to dba_mod_amd/ops/rng.py and csrc/runtime/runtime.cpp
 __device__ __forceinline__ uint32_t lowbias32(uint32_t x) {
   x ^= x >> 16;

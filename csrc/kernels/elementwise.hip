@@ -1,4 +1,4 @@
-// Pooling, ReLU-mask backward and dropout for grouped NHWC bf16 activations
+// Pooling, ReLU-mask backward and dropout for grouped NHWC activations (bf16 or fp32)
 // (LoanNet dropout, loan_model.py:13-19).
 #include "common.hpp"
 #include <algorithm>
@@ -7,28 +7,30 @@ namespace {
 
 int egrid(long long n) { return (int)std::max(1LL, std::min(16384LL, (n + 255) / 256)); }
 
-__global__ void relu_mask_bwd_kernel(const uint16_t* __restrict__ dout, const uint16_t* __restrict__ out,
-                                     uint16_t* __restrict__ din, long long n8) {
+template <typename T>
+__global__ void relu_mask_bwd_kernel(const T* __restrict__ dout, const T* __restrict__ out, T* __restrict__ din,
+                                     long long n8) {
   for (long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x; t < n8; t += (long long)gridDim.x * blockDim.x) {
-    uint4 d = *(const uint4*)(dout + t * 8);
-    const uint4 o = *(const uint4*)(out + t * 8);
-    uint16_t* dp = (uint16_t*)&d;
-    const uint16_t* op = (const uint16_t*)&o;
+    float d[8], o[8];
+    ld8(dout + t * 8, d);
+    ld8(out + t * 8, o);
 #pragma unroll
     for (int e = 0; e < 8; ++e)
-      if (!(bf2f(op[e]) > 0.f)) dp[e] = 0;
-    *(uint4*)(din + t * 8) = d;
+      if (!(o[e] > 0.f)) d[e] = 0.f;
+    st8(din + t * 8, d);
   }
 }
 
-__global__ void relu_mask_bwd_tail(const uint16_t* __restrict__ dout, const uint16_t* __restrict__ out,
-                                   uint16_t* __restrict__ din, long long beg, long long n) {
+template <typename T>
+__global__ void relu_mask_bwd_tail(const T* __restrict__ dout, const T* __restrict__ out, T* __restrict__ din,
+                                   long long beg, long long n) {
   const long long t = beg + blockIdx.x * (long long)blockDim.x + threadIdx.x;
-  if (t < n) din[t] = bf2f(out[t]) > 0.f ? dout[t] : (uint16_t)0;
+  if (t < n) din[t] = to_f<T>(out[t]) > 0.f ? dout[t] : from_f<T>(0.f);
 }
 
 // y[gn][ho][wo][c] = max window; ind = flat input index hi*W+wi (first max, like PyTorch)
-__global__ void maxpool_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ y, int* __restrict__ ind,
+template <typename T>
+__global__ void maxpool_kernel(const T* __restrict__ x, T* __restrict__ y, int* __restrict__ ind,
                                long long GN, int H, int W, int C, int Ho, int Wo, int k, int s, int p) {
   const long long total = GN * Ho * Wo * C;
   for (long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x; t < total; t += (long long)gridDim.x * blockDim.x) {
@@ -46,19 +48,19 @@ __global__ void maxpool_kernel(const uint16_t* __restrict__ x, uint16_t* __restr
       for (int j = 0; j < k; ++j) {
         const int wi = wo * s - p + j;
         if ((unsigned)wi >= (unsigned)W) continue;
-        const float v = bf2f(x[((gn * H + hi) * W + wi) * C + c]);
+        const float v = to_f<T>(x[((gn * H + hi) * W + wi) * C + c]);
         if (v > best || bi < 0 || v != v) { best = v; bi = hi * W + wi; }
       }
     }
-    y[t] = f2bf(best);
+    y[t] = from_f<T>(best);
     ind[t] = bi;
   }
 }
 
 // gather form of the max-pool backward (no atomics, deterministic)
-__global__ void maxpool_bwd_kernel(const uint16_t* __restrict__ dy, const int* __restrict__ ind,
-                                   uint16_t* __restrict__ dx, long long GN, int H, int W, int C, int Ho, int Wo, int k,
-                                   int s, int p) {
+template <typename T>
+__global__ void maxpool_bwd_kernel(const T* __restrict__ dy, const int* __restrict__ ind, T* __restrict__ dx,
+                                   long long GN, int H, int W, int C, int Ho, int Wo, int k, int s, int p) {
   const long long total = GN * H * W * C;
   for (long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x; t < total; t += (long long)gridDim.x * blockDim.x) {
     const int c = (int)(t % C);
@@ -74,31 +76,32 @@ __global__ void maxpool_bwd_kernel(const uint16_t* __restrict__ dy, const int* _
     for (int ho = ho0; ho <= ho1; ++ho)
       for (int wo = wo0; wo <= wo1; ++wo) {
         const long long o = ((gn * Ho + ho) * Wo + wo) * C + c;
-        if (ind[o] == me) acc += bf2f(dy[o]);
+        if (ind[o] == me) acc += to_f<T>(dy[o]);
       }
-    dx[t] = f2bf(acc);
+    dx[t] = from_f<T>(acc);
   }
 }
 
-__global__ void avgpool_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ y, long long GN, int HW, int C) {
+template <typename T>
+__global__ void avgpool_kernel(const T* __restrict__ x, T* __restrict__ y, long long GN, int HW, int C) {
   const long long total = GN * C;
   for (long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x; t < total; t += (long long)gridDim.x * blockDim.x) {
     const int c = (int)(t % C);
     const long long gn = t / C;
     float s = 0.f;
-    for (int i = 0; i < HW; ++i) s += bf2f(x[(gn * HW + i) * C + c]);
-    y[t] = f2bf(s / (float)HW);
+    for (int i = 0; i < HW; ++i) s += to_f<T>(x[(gn * HW + i) * C + c]);
+    y[t] = from_f<T>(s / (float)HW);
   }
 }
 
-__global__ void avgpool_bwd_kernel(const uint16_t* __restrict__ dy, uint16_t* __restrict__ dx, long long GN, int HW,
-                                   int C) {
+template <typename T>
+__global__ void avgpool_bwd_kernel(const T* __restrict__ dy, T* __restrict__ dx, long long GN, int HW, int C) {
   const long long total = GN * HW * C;
   const float inv = 1.0f / (float)HW;
   for (long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x; t < total; t += (long long)gridDim.x * blockDim.x) {
     const int c = (int)(t % C);
     const long long gn = t / ((long long)HW * C);
-    dx[t] = f2bf(bf2f(dy[gn * C + c]) * inv);
+    dx[t] = from_f<T>(to_f<T>(dy[gn * C + c]) * inv);
   }
 }
 
@@ -119,40 +122,43 @@ __global__ void dropout_kernel(const T* __restrict__ x, T* __restrict__ y, const
 
 }  // namespace
 
-DBA_EXPORT int dba_relu_mask_bwd(const void* dout, const void* out, void* din, long long n, void* stream) {
+#define EW_T(f32, call) do { if (f32) { typedef float T; call; } else { typedef uint16_t T; call; } } while (0)
+
+DBA_EXPORT int dba_relu_mask_bwd(const void* dout, const void* out, void* din, long long n, int f32, void* stream) {
   const long long n8 = n / 8;
+  hipStream_t st = (hipStream_t)stream;
   if (n8 > 0)
-    hipLaunchKernelGGL(relu_mask_bwd_kernel, dim3(egrid(n8)), dim3(256), 0, (hipStream_t)stream,
-                       (const uint16_t*)dout, (const uint16_t*)out, (uint16_t*)din, n8);
+    EW_T(f32, hipLaunchKernelGGL((relu_mask_bwd_kernel<T>), dim3(egrid(n8)), dim3(256), 0, st, (const T*)dout,
+                                 (const T*)out, (T*)din, n8));
   if (n8 * 8 < n)
-    hipLaunchKernelGGL(relu_mask_bwd_tail, dim3(1), dim3(256), 0, (hipStream_t)stream, (const uint16_t*)dout,
-                       (const uint16_t*)out, (uint16_t*)din, n8 * 8, n);
+    EW_T(f32, hipLaunchKernelGGL((relu_mask_bwd_tail<T>), dim3(1), dim3(256), 0, st, (const T*)dout, (const T*)out,
+                                 (T*)din, n8 * 8, n));
   DBA_LAUNCH_CHECK();
 }
 
 DBA_EXPORT int dba_maxpool(const void* x, void* y, int* ind, long long GN, int H, int W, int C, int Ho, int Wo, int k,
-                           int s, int p, void* stream) {
-  hipLaunchKernelGGL(maxpool_kernel, dim3(egrid(GN * Ho * Wo * C)), dim3(256), 0, (hipStream_t)stream,
-                     (const uint16_t*)x, (uint16_t*)y, ind, GN, H, W, C, Ho, Wo, k, s, p);
+                           int s, int p, int f32, void* stream) {
+  EW_T(f32, hipLaunchKernelGGL((maxpool_kernel<T>), dim3(egrid(GN * Ho * Wo * C)), dim3(256), 0, (hipStream_t)stream,
+                               (const T*)x, (T*)y, ind, GN, H, W, C, Ho, Wo, k, s, p));
   DBA_LAUNCH_CHECK();
 }
 
 DBA_EXPORT int dba_maxpool_bwd(const void* dy, const int* ind, void* dx, long long GN, int H, int W, int C, int Ho,
-                               int Wo, int k, int s, int p, void* stream) {
-  hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(egrid(GN * H * W * C)), dim3(256), 0, (hipStream_t)stream,
-                     (const uint16_t*)dy, ind, (uint16_t*)dx, GN, H, W, C, Ho, Wo, k, s, p);
+                               int Wo, int k, int s, int p, int f32, void* stream) {
+  EW_T(f32, hipLaunchKernelGGL((maxpool_bwd_kernel<T>), dim3(egrid(GN * H * W * C)), dim3(256), 0, (hipStream_t)stream,
+                               (const T*)dy, ind, (T*)dx, GN, H, W, C, Ho, Wo, k, s, p));
   DBA_LAUNCH_CHECK();
 }
 
-DBA_EXPORT int dba_avgpool(const void* x, void* y, long long GN, int HW, int C, void* stream) {
-  hipLaunchKernelGGL(avgpool_kernel, dim3(egrid(GN * C)), dim3(256), 0, (hipStream_t)stream, (const uint16_t*)x,
-                     (uint16_t*)y, GN, HW, C);
+DBA_EXPORT int dba_avgpool(const void* x, void* y, long long GN, int HW, int C, int f32, void* stream) {
+  EW_T(f32, hipLaunchKernelGGL((avgpool_kernel<T>), dim3(egrid(GN * C)), dim3(256), 0, (hipStream_t)stream,
+                               (const T*)x, (T*)y, GN, HW, C));
   DBA_LAUNCH_CHECK();
 }
 
-DBA_EXPORT int dba_avgpool_bwd(const void* dy, void* dx, long long GN, int HW, int C, void* stream) {
-  hipLaunchKernelGGL(avgpool_bwd_kernel, dim3(egrid(GN * HW * C)), dim3(256), 0, (hipStream_t)stream,
-                     (const uint16_t*)dy, (uint16_t*)dx, GN, HW, C);
+DBA_EXPORT int dba_avgpool_bwd(const void* dy, void* dx, long long GN, int HW, int C, int f32, void* stream) {
+  EW_T(f32, hipLaunchKernelGGL((avgpool_bwd_kernel<T>), dim3(egrid(GN * HW * C)), dim3(256), 0, (hipStream_t)stream,
+                               (const T*)dy, (T*)dx, GN, HW, C));
   DBA_LAUNCH_CHECK();
 }
 

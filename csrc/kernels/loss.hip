@@ -12,8 +12,9 @@
 
 namespace {
 
+template <typename T>
 __global__ __launch_bounds__(256) void xent_kernel(const float* __restrict__ logits, const int* __restrict__ labels,
-                                                   int B, int C, int mean, uint16_t* __restrict__ dl,
+                                                   int B, int C, int mean, T* __restrict__ dl,
                                                    float* __restrict__ loss_out, float* __restrict__ corr_out,
                                                    float* __restrict__ stats, long long stats_stride,
                                                    const int* __restrict__ slot, int max_slots,
@@ -33,11 +34,11 @@ __global__ __launch_bounds__(256) void xent_kernel(const float* __restrict__ log
   float wl = 0.f, wc = 0.f;
   for (int b = tid; b < B; b += 256) {
     const float* x = logits + ((long long)g * B + b) * C;
-    uint16_t* d = dl ? dl + ((long long)g * B + b) * C : nullptr;
+    T* d = dl ? dl + ((long long)g * B + b) * C : nullptr;
     const int y = lab[b];
     if (y < 0) {
       if (d)
-        for (int c = 0; c < C; ++c) d[c] = 0;
+        for (int c = 0; c < C; ++c) d[c] = from_f<T>(0.f);
       continue;
     }
     // argmax = first maximum (torch semantics)
@@ -53,7 +54,7 @@ __global__ __launch_bounds__(256) void xent_kernel(const float* __restrict__ log
     wl += lse - x[y];
     wc += (am == y) ? 1.f : 0.f;
     if (d)
-      for (int c = 0; c < C; ++c) d[c] = f2bf((__expf(x[c] - lse) - (c == y ? 1.f : 0.f)) * scale);
+      for (int c = 0; c < C; ++c) d[c] = from_f<T>((__expf(x[c] - lse) - (c == y ? 1.f : 0.f)) * scale);
   }
   wl = wave_sum(wl);
   wc = wave_sum(wc);
@@ -76,11 +77,15 @@ __global__ __launch_bounds__(256) void xent_kernel(const float* __restrict__ log
 
 }  // namespace
 
-// stats (optional): [3][stats_stride] fp32, slot [G] int, nvalid [G] int
+// stats (optional): [3][stats_stride] fp32, slot [G] int, nvalid [G] int; dl fp32 (dl_f32) or bf16
 DBA_EXPORT int dba_softmax_xent(const float* logits, const int* labels, int G, int B, int C, int mean, void* dl,
                                 float* loss, float* correct, float* stats, long long stats_stride, const int* slot,
-                                int max_slots, const int* nvalid, void* stream) {
-  hipLaunchKernelGGL(xent_kernel, dim3(G), dim3(256), 0, (hipStream_t)stream, logits, labels, B, C, mean,
-                     (uint16_t*)dl, loss, correct, stats, stats_stride, slot, max_slots, nvalid);
+                                int max_slots, const int* nvalid, int dl_f32, void* stream) {
+  if (dl_f32)
+    hipLaunchKernelGGL(xent_kernel<float>, dim3(G), dim3(256), 0, (hipStream_t)stream, logits, labels, B, C, mean,
+                       (float*)dl, loss, correct, stats, stats_stride, slot, max_slots, nvalid);
+  else
+    hipLaunchKernelGGL(xent_kernel<uint16_t>, dim3(G), dim3(256), 0, (hipStream_t)stream, logits, labels, B, C, mean,
+                       (uint16_t*)dl, loss, correct, stats, stats_stride, slot, max_slots, nvalid);
   DBA_LAUNCH_CHECK();
 }

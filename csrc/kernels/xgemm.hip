@@ -1,0 +1,883 @@
+// Reference-precision (fp32) convolution family for gfx950: split-bf16 MFMA.
+//
+// The reference trains and evaluates in fp32 (image_train.py:84-91, models/resnet_cifar.py:
+// 67-104).  gfx950 has no xf32 MFMA and its exact f32-input MFMA runs at 1/16 of the bf16
+// rate, so these kernels keep fp32 operands in HBM and split every operand element x into
+// P bf16 planes while staging it into LDS:
+//
+//     x = x0 + x1 (+ x2) + e,    x_p = bf16(x - x0 - ... - x_{p-1}),
+//     |e| <= 2^-16 |x| (P = 2)  /  2^-24 |x| (P = 3)
+//
+// and sum the plane products with total order <= P-1 on the bf16 MFMA with fp32
+// accumulation: P = 2 -> 3 MFMAs per product (x0y0 + x0y1 + x1y0, relative error ~4e-6,
+// fp32 accumulate), P = 3 -> 6 MFMAs (error at the fp32-accumulation level, ~3e-7).
+// Either is 2.7x / 5.3x the work of a bf16 GEMM but still 5x / 2.7x the peak of the exact
+// f32 MFMA (157 TF).  The split costs 2.5 VALU ops per element (v_cvt_pk_bf16_f32,
+// shift/mask, v_pk_add_f32, v_cvt_pk_bf16_f32), done once per staged element.
+//
+// Kernels (all deterministic: no atomics, fixed reduction orders):
+//   xconv_kernel    implicit-GEMM conv forward (bias / residual / ReLU epilogue) and data
+//                   gradient; a stride-s data gradient runs as s*s parity classes, each an
+//                   implicit GEMM over its own taps (no zero-tap MFMA work), in one launch;
+//   xwgrad_kernel   weight gradient: C[cout][k] = sum_m dy[m][cout] * im2col(x)[m][k], both
+//                   operands transposed to reduction-major while staging; split over m into
+//                   fp32 slabs summed in a fixed order by xwgrad_reduce_kernel;
+//   xsplitk_reduce  split-K slabs of small forward launches + epilogue;
+//   xtranspose      forward weights -> parity-class packed data-gradient weights;
+//   xcolsum         bias gradient (column sums, fixed order).
+#include "common.hpp"
+#include <algorithm>
+#include <cstdlib>
+
+namespace {
+
+typedef __attribute__((ext_vector_type(2))) float f32x2v;
+typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2v;
+
+__device__ __forceinline__ uint32_t cvt_pk(float a, float b) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2v){a, b}, bf16x2v));
+}
+
+// 4 fp32 values -> P bf16 planes (4 bf16 = 8 bytes each)
+template <int P>
+__device__ __forceinline__ void split4(float a, float b, float c, float d, uint2 (&o)[P]) {
+#pragma unroll
+  for (int p = 0; p < P; ++p) {
+    const uint32_t u0 = cvt_pk(a, b), u1 = cvt_pk(c, d);
+    o[p] = make_uint2(u0, u1);
+    if (p + 1 < P) {
+      a -= __uint_as_float(u0 << 16);
+      b -= __uint_as_float(u0 & 0xffff0000u);
+      c -= __uint_as_float(u1 << 16);
+      d -= __uint_as_float(u1 & 0xffff0000u);
+    }
+  }
+}
+
+// LDS images: per plane, rows of 32 reduction elements (64 B = 4 x 16-B chunks).  A row's
+// 16-B chunk c is stored at chunk c ^ swz so the ds_read_b128 fragment reads (lane groups
+// {0-3,12-15,20-27} / {4-11,16-19,28-31}) hit 16 distinct bank slots.
+//   conv  (ROWPERM = false): physical row = logical row, swz = (row >> 2) & 3;
+//   wgrad (ROWPERM = true) : operand rows are written 4 at a time (a transposed 4x4 micro
+//     tile), so logical row n lives at physical (n & 3) * (R / 4) + (n >> 2) with swz = n & 3
+//     — both the transposing ds_write_b64 stores and the fragment reads are conflict-free.
+template <bool ROWPERM, int R>
+__device__ __forceinline__ int prow(int n) {
+  if constexpr (ROWPERM) return (n & 3) * (R / 4) + (n >> 2);
+  else return n;
+}
+template <bool ROWPERM>
+__device__ __forceinline__ int pswz(int n) {
+  if constexpr (ROWPERM) return n & 3;
+  else return (n >> 2) & 3;
+}
+
+// one 32-deep reduction step of a wave's MI x NJ block of 32x32 tiles from an LDS image:
+// A rows [arow0, arow0 + 32 MI) of the region at row offset AOFF (RA rows), B rows likewise.
+template <int MI, int NJ, int P, bool ROWPERM, int RA, int RB>
+__device__ __forceinline__ void mma_step(const uint4* __restrict__ L, int PL, int arow0, int brow0,
+                                         f32x16_t (&acc)[MI][NJ], int lane) {
+  const int fr = lane & 31, hf = lane >> 5;
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk) {
+    const int ch = kk * 2 + hf;
+    bf16x8_t af[P][MI], bfr[P][NJ];
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+      const int n = arow0 + i * 32 + fr;
+      const int o = prow<ROWPERM, RA>(n) * 4 + (ch ^ pswz<ROWPERM>(n));
+#pragma unroll
+      for (int p = 0; p < P; ++p) af[p][i] = *(const bf16x8_t*)&L[p * PL + o];
+    }
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int n = brow0 + j * 32 + fr;
+      const int o = (RA + prow<ROWPERM, RB>(n)) * 4 + (ch ^ pswz<ROWPERM>(n));
+#pragma unroll
+      for (int p = 0; p < P; ++p) bfr[p][j] = *(const bf16x8_t*)&L[p * PL + o];
+    }
+    // plane products of total order <= P-1, the small ones first
+#pragma unroll
+    for (int s = P - 1; s >= 0; --s)
+#pragma unroll
+      for (int pa = 0; pa <= s; ++pa)
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+          for (int j = 0; j < NJ; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[pa][i], bfr[s - pa][j], acc[i][j], 0, 0, 0);
+  }
+}
+
+// store the P planes of 4 consecutive reduction elements (8-B slot q of logical row n)
+template <int P, bool ROWPERM, int R>
+__device__ __forceinline__ void lds_put(uint4* __restrict__ L, int PL, int roff, int n, int q, const uint2 (&s)[P]) {
+  const int o = (roff + prow<ROWPERM, R>(n)) * 4 + ((q >> 1) ^ pswz<ROWPERM>(n));
+#pragma unroll
+  for (int p = 0; p < P; ++p) ((uint2*)&L[p * PL + o])[q & 1] = s[p];
+}
+
+// ============================================================================ conv
+struct XClass {
+  int nI, nJ;      // taps of the class along kh / kw
+  int bh, bw;      // source pixel = (p*sp + bh + dsg*i, q*sp + bw + dsg*j)
+  int oh, ow;      // output pixel = (p*os + oh, q*os + ow)
+  int Hq, Wq;      // GEMM row grid per image
+  long long boff;  // offset of the class's packed weights [Ncol][nI*nJ*Cs] in a slot
+};
+
+struct XArgs {
+  const float* src; long long src_gstride;   // [G][N][Hs][Ws][Cs]
+  const float* w; long long w_sstride;       // per slot: classes' [Ncol][K_c] blocks
+  const int* wsel;
+  const float* bias; long long b_sstride;
+  const float* res;                          // output layout
+  float* out; long long out_gstride;         // [G][N][Ho][Wo][Ncol] (or split-K slabs)
+  const int* nvalid;
+  int N, Hs, Ws, Cs, Ncol, Ho, Wo;
+  int sp, os, dsg, relu;
+  int splitk, tiles_n;
+  long long zstride;                         // split-K: slab z at out + z * zstride
+  XClass cls[4];
+};
+
+template <int BM, int BN, int WM, int WN, int P, int VEC>
+__global__ __launch_bounds__(256) void xconv_kernel(const XArgs a) {
+  constexpr int TM = BM / WM, TN = BN / WN, MI = TM / 32, NJ = TN / 32;
+  static_assert(WM * WN == 4 && MI >= 1 && NJ >= 1, "wave tiling");
+  constexpr int ROWS = BM + BN, PL = ROWS * 4;   // uint4 per plane image
+  constexpr int RA = BM / 32, RB = BN / 32;      // 4-element quarters per thread (A, B)
+  static_assert(BM * BN <= 2 * P * PL * 4, "epilogue tile fits the LDS images");
+  __shared__ __attribute__((aligned(16))) uint4 lds[2 * P * PL];
+  __shared__ long long orow[BM];
+
+  const int zc = blockIdx.z / a.splitk, kz = blockIdx.z - zc * a.splitk;
+  const XClass c = a.cls[zc];
+  const int g = blockIdx.y;
+  const int HqWq = c.Hq * c.Wq;
+  const int Mv = valid_rows(a.nvalid, g, a.N) * HqWq;
+  const int tn = blockIdx.x % a.tiles_n, tm = blockIdx.x / a.tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  if (m0 >= Mv) return;
+  const int slot = a.wsel ? a.wsel[g] : g;
+  const int Cs = a.Cs;
+  const int K = c.nI * c.nJ * Cs;
+  const int nkt = (K + 31) >> 5;
+  const int kt0 = (int)((long long)nkt * kz / a.splitk), kt1 = (int)((long long)nkt * (kz + 1) / a.splitk);
+  const float* __restrict__ src = a.src + (long long)g * a.src_gstride;
+  const float* __restrict__ Bp = a.w + (long long)slot * a.w_sstride + c.boff;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WN, wn = wid % WN;
+  const int kq = tid & 7, r0 = tid >> 3;
+
+  if (tid < BM) {
+    const int m = m0 + tid;
+    long long o = -1;
+    if (m < Mv) {
+      if (a.splitk > 1) {
+        o = (long long)m * a.Ncol;
+      } else {
+        const int img = m / HqWq, rem = m - img * HqWq, p = rem / c.Wq, q = rem - p * c.Wq;
+        o = (((long long)img * a.Ho + p * a.os + c.oh) * a.Wo + q * a.os + c.ow) * a.Ncol;
+      }
+    }
+    orow[tid] = o;
+  }
+  // the thread's A rows (source pixel bases) and B rows (weight rows)
+  int aimg[RA], ah[RA], aw[RA];
+#pragma unroll
+  for (int i = 0; i < RA; ++i) {
+    const int m = m0 + r0 + 32 * i;
+    aimg[i] = -1; ah[i] = 0; aw[i] = 0;
+    if (m < Mv) {
+      const int img = m / HqWq, rem = m - img * HqWq, p = rem / c.Wq, q = rem - p * c.Wq;
+      aimg[i] = img;
+      ah[i] = p * a.sp + c.bh;
+      aw[i] = q * a.sp + c.bw;
+    }
+  }
+  const float* brow[RB];
+#pragma unroll
+  for (int j = 0; j < RB; ++j) {
+    const int n = n0 + r0 + 32 * j;
+    brow[j] = n < a.Ncol ? Bp + (long long)n * K : nullptr;
+  }
+  // reduction state of the thread's quarter: element k = kt*32 + kq*4 is channel kc of tap (ki, kj)
+  int ki = 0, kj = 0, kc = 0;
+  if (nkt > 0) {
+    const int k = kt0 * 32 + kq * 4;
+    const int t = k / Cs;
+    kc = k - t * Cs;
+    ki = t / c.nJ;
+    kj = t - ki * c.nJ;
+  }
+  float4 ra[RA], rb[RB];
+  auto gload = [&](int kt) {
+    const int kb = kt * 32 + kq * 4;
+    if constexpr (VEC == 4) {
+      const bool kv = ki < c.nI;
+      const int dh = a.dsg * ki, dw = a.dsg * kj;
+#pragma unroll
+      for (int i = 0; i < RA; ++i) {
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        const int h = ah[i] + dh, w = aw[i] + dw;
+        if (kv && aimg[i] >= 0 && (unsigned)h < (unsigned)a.Hs && (unsigned)w < (unsigned)a.Ws)
+          v = *(const float4*)(src + (((long long)aimg[i] * a.Hs + h) * a.Ws + w) * Cs + kc);
+        ra[i] = v;
+      }
+#pragma unroll
+      for (int j = 0; j < RB; ++j)
+        rb[j] = (brow[j] && kb < K) ? *(const float4*)(brow[j] + kb) : make_float4(0.f, 0.f, 0.f, 0.f);
+    } else {
+      float va[RA][4], vb[RB][4];
+      int ii = ki, jj = kj, cc = kc;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const bool kv = ii < c.nI;
+        const int dh = a.dsg * ii, dw = a.dsg * jj;
+#pragma unroll
+        for (int i = 0; i < RA; ++i) {
+          const int h = ah[i] + dh, w = aw[i] + dw;
+          va[i][e] = (kv && aimg[i] >= 0 && (unsigned)h < (unsigned)a.Hs && (unsigned)w < (unsigned)a.Ws)
+                         ? src[(((long long)aimg[i] * a.Hs + h) * a.Ws + w) * Cs + cc]
+                         : 0.f;
+        }
+#pragma unroll
+        for (int j = 0; j < RB; ++j) vb[j][e] = (brow[j] && kb + e < K) ? brow[j][kb + e] : 0.f;
+        if (++cc == Cs) {
+          cc = 0;
+          if (++jj == c.nJ) { jj = 0; ++ii; }
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < RA; ++i) ra[i] = make_float4(va[i][0], va[i][1], va[i][2], va[i][3]);
+#pragma unroll
+      for (int j = 0; j < RB; ++j) rb[j] = make_float4(vb[j][0], vb[j][1], vb[j][2], vb[j][3]);
+    }
+  };
+  auto advance = [&]() {   // k += 32
+    kc += 32;
+    while (kc >= Cs) {
+      kc -= Cs;
+      if (++kj == c.nJ) { kj = 0; ++ki; }
+    }
+  };
+  auto lput = [&](int buf) {
+    uint4* L = lds + buf * P * PL;
+#pragma unroll
+    for (int i = 0; i < RA; ++i) {
+      uint2 s[P];
+      split4<P>(ra[i].x, ra[i].y, ra[i].z, ra[i].w, s);
+      lds_put<P, false, BM>(L, PL, 0, r0 + 32 * i, kq, s);
+    }
+#pragma unroll
+    for (int j = 0; j < RB; ++j) {
+      uint2 s[P];
+      split4<P>(rb[j].x, rb[j].y, rb[j].z, rb[j].w, s);
+      lds_put<P, false, BN>(L, PL, BM, r0 + 32 * j, kq, s);
+    }
+  };
+
+  f32x16_t acc[MI][NJ];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  if (kt0 < kt1) {
+    gload(kt0);
+    advance();
+    lput(0);
+    __syncthreads();
+    int cur = 0;
+    for (int kt = kt0; kt < kt1; ++kt) {
+      const bool more = kt + 1 < kt1;
+      if (more) {
+        gload(kt + 1);   // in flight under this step's MFMAs
+        advance();
+      }
+      mma_step<MI, NJ, P, false, BM, BN>(lds + cur * P * PL, PL, wm * TM, wn * TN, acc, lane);
+      if (more) lput(cur ^ 1);
+      __syncthreads();
+      cur ^= 1;
+    }
+  }
+
+  // ---- epilogue: fp32 tile through LDS, row-contiguous stores with bias / residual / ReLU
+  __syncthreads();
+  float* Ct = reinterpret_cast<float*>(lds);
+  const int fr = lane & 31, hf = lane >> 5;
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        Ct[(wm * TM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * hf) * BN + wn * TN + j * 32 + fr] = acc[i][j][r];
+  __syncthreads();
+  const bool fin = a.splitk == 1;
+  float* out = a.out + (long long)g * a.out_gstride + (fin ? 0 : (long long)kz * a.zstride);
+  const float* bias = (fin && a.bias) ? a.bias + (long long)slot * a.b_sstride : nullptr;
+  const float* res = (fin && a.res) ? a.res + (long long)g * a.out_gstride : nullptr;
+  const bool relu = fin && a.relu;
+  if ((a.Ncol & 3) == 0) {
+    constexpr int C4 = BN / 4;
+    for (int e = tid; e < BM * C4; e += 256) {
+      const int row = e / C4, cc = (e - row * C4) * 4;
+      const int n = n0 + cc;
+      const long long o = orow[row];
+      if (o < 0 || n >= a.Ncol) continue;
+      float4 v = *(const float4*)&Ct[row * BN + cc];
+      if (bias) { v.x += bias[n]; v.y += bias[n + 1]; v.z += bias[n + 2]; v.w += bias[n + 3]; }
+      if (res) {
+        const float4 rv = *(const float4*)(res + o + n);
+        v.x += rv.x; v.y += rv.y; v.z += rv.z; v.w += rv.w;
+      }
+      if (relu) { v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f); }
+      *(float4*)(out + o + n) = v;
+    }
+  } else {
+    for (int e = tid; e < BM * BN; e += 256) {
+      const int row = e / BN, cc = e - row * BN;
+      const int n = n0 + cc;
+      const long long o = orow[row];
+      if (o < 0 || n >= a.Ncol) continue;
+      float v = Ct[row * BN + cc];
+      if (bias) v += bias[n];
+      if (res) v += res[o + n];
+      if (relu) v = fmaxf(v, 0.f);
+      out[o + n] = v;
+    }
+  }
+}
+
+// sum of split-K slabs ws[z][g][m][n] (fixed z order) + bias (+ residual) (ReLU), valid rows
+__global__ __launch_bounds__(256) void xsplitk_reduce_kernel(const float* __restrict__ ws, int S, long long zstride,
+                                                             long long gstride, const int* __restrict__ nvalid, int N,
+                                                             int HoWo, int Ncol, const float* __restrict__ bias,
+                                                             long long b_sstride, const int* __restrict__ wsel,
+                                                             const float* __restrict__ res, int relu,
+                                                             float* __restrict__ out) {
+  const int g = blockIdx.y;
+  const long long total = (long long)valid_rows(nvalid, g, N) * HoWo * Ncol;
+  const float* __restrict__ bp = bias ? bias + (long long)(wsel ? wsel[g] : g) * b_sstride : nullptr;
+  const long long base = (long long)g * gstride;
+  for (long long e = blockIdx.x * 256LL + threadIdx.x; e < total; e += (long long)gridDim.x * 256) {
+    float v = ws[base + e];
+    for (int z = 1; z < S; ++z) v += ws[z * zstride + base + e];
+    if (bp) v += bp[e % Ncol];
+    if (res) v += res[base + e];
+    out[base + e] = relu ? fmaxf(v, 0.f) : v;
+  }
+}
+
+// ============================================================================ wgrad
+// x / magic division for the row decode (n < 2^24: exact after one correction)
+struct FDiv {
+  int d; float inv;
+};
+__device__ __forceinline__ int fdiv(int n, FDiv f) {
+  int q = (int)((float)n * f.inv);
+  if ((q + 1) * f.d <= n) ++q;
+  if (q * f.d > n) --q;
+  return q;
+}
+
+struct XWArgs {
+  const float* dy; long long dy_gstride;   // [G][N*Ho*Wo][Cout]
+  const float* x; long long x_gstride;     // [G][N][H][W][Cin]
+  float* ws;                               // slabs [Z][G][Cout][K] (Z > 1)
+  float* dw; long long dw_gstride;         // [G][Cout][K] (+=)
+  const int* nvalid;
+  int N, H, W, Cin, Ho, Wo, Cout, KW, stride, pad, K;
+  int tiles_k, mchunk;
+  FDiv dHoWo, dWo;
+};
+
+template <int BNO, int BK, int WN_, int WK_, int P, int VEC>
+__global__ __launch_bounds__(256) void xwgrad_kernel(const XWArgs a) {
+  constexpr int TNo = BNO / WN_, TK = BK / WK_, MI = TNo / 32, NJ = TK / 32;
+  static_assert(WN_ * WK_ == 4 && MI >= 1 && NJ >= 1, "wave tiling");
+  static_assert(BK == 128, "x micro-tiles: one per thread");
+  constexpr int ROWS = BNO + BK, PL = ROWS * 4;
+  __shared__ __attribute__((aligned(16))) uint4 lds[2 * P * PL];
+
+  const int g = blockIdx.y, z = blockIdx.z;
+  const int tk = blockIdx.x % a.tiles_k, tn = blockIdx.x / a.tiles_k;
+  const int n0 = tn * BNO, k0 = tk * BK;
+  const int HoWo = a.Ho * a.Wo;
+  const int Mv = valid_rows(a.nvalid, g, a.N) * HoWo;
+  const int mb = z * a.mchunk, me = min(Mv, mb + a.mchunk);
+  if (mb >= me) return;     // the reduce sums only the slabs of z < ceil(Mv / mchunk)
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wn = wid / WK_, wk = wid % WK_;
+  const float* __restrict__ dy = a.dy + (long long)g * a.dy_gstride;
+  const float* __restrict__ x = a.x + (long long)g * a.x_gstride;
+  const int m4 = tid & 7;     // micro-tile rows m4*4 .. m4*4+3 of the 32-row m tile
+
+  // dy micro-tile: 4 m x 4 cout (threads < BNO*2)
+  const int dn4 = tid >> 3;
+  const bool dact = dn4 < BNO / 4;
+  const int dn = n0 + dn4 * 4;
+  // x micro-tile: 4 m x 4 k; the thread's k (tap, channel) are fixed for the whole block
+  const int xk4 = tid >> 3;
+  int xkh[4], xkw[4], xc[4];
+  bool xkv[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int k = k0 + xk4 * 4 + e;
+    xkv[e] = k < a.K;
+    const int t = k / a.Cin;
+    xc[e] = k - t * a.Cin;
+    xkh[e] = t / a.KW;
+    xkw[e] = t - xkh[e] * a.KW;
+  }
+
+  float dv[4][4], xv[4][4];   // [m][n or k]
+  auto gload = [&](int mt) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int m = mt + m4 * 4 + r;
+      const bool mv = m < me;
+      // dy
+      if (dact) {
+        if (VEC == 4) {
+          float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+          if (mv && dn < a.Cout) v = *(const float4*)(dy + (long long)m * a.Cout + dn);
+          dv[r][0] = v.x; dv[r][1] = v.y; dv[r][2] = v.z; dv[r][3] = v.w;
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            dv[r][e] = (mv && dn + e < a.Cout) ? dy[(long long)m * a.Cout + dn + e] : 0.f;
+        }
+      }
+      // x (im2col row m)
+      int img = 0, p = 0, q = 0;
+      if (mv) {
+        img = fdiv(m, a.dHoWo);
+        const int rem = m - img * HoWo;
+        p = fdiv(rem, a.dWo);
+        q = rem - p * a.Wo;
+      }
+      const int hb = p * a.stride - a.pad, wb = q * a.stride - a.pad;
+      if (VEC == 4) {
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        const int h = hb + xkh[0], w = wb + xkw[0];
+        if (mv && xkv[0] && (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W)
+          v = *(const float4*)(x + (((long long)img * a.H + h) * a.W + w) * a.Cin + xc[0]);
+        xv[r][0] = v.x; xv[r][1] = v.y; xv[r][2] = v.z; xv[r][3] = v.w;
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int h = hb + xkh[e], w = wb + xkw[e];
+          xv[r][e] = (mv && xkv[e] && (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W)
+                         ? x[(((long long)img * a.H + h) * a.W + w) * a.Cin + xc[e]]
+                         : 0.f;
+        }
+      }
+    }
+  };
+  auto lput = [&](int buf) {
+    uint4* L = lds + buf * P * PL;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      if (dact) {
+        uint2 s[P];
+        split4<P>(dv[0][e], dv[1][e], dv[2][e], dv[3][e], s);
+        lds_put<P, true, BNO>(L, PL, 0, dn4 * 4 + e, m4, s);
+      }
+      uint2 s[P];
+      split4<P>(xv[0][e], xv[1][e], xv[2][e], xv[3][e], s);
+      lds_put<P, true, BK>(L, PL, BNO, xk4 * 4 + e, m4, s);
+    }
+  };
+
+  f32x16_t acc[MI][NJ];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  gload(mb);
+  lput(0);
+  __syncthreads();
+  int cur = 0;
+  for (int mt = mb; mt < me; mt += 32) {
+    const bool more = mt + 32 < me;
+    if (more) gload(mt + 32);
+    mma_step<MI, NJ, P, true, BNO, BK>(lds + cur * P * PL, PL, wn * TNo, wk * TK, acc, lane);
+    if (more) lput(cur ^ 1);
+    __syncthreads();
+    cur ^= 1;
+  }
+
+  // acc[i][j][r]: cout row n = n0 + wn*TNo + i*32 + (r&3) + 8*(r>>2) + 4*hf, k col = k0 + wk*TK + j*32 + fr
+  const int fr = lane & 31, hf = lane >> 5;
+  const bool direct = gridDim.z == 1;
+  float* dst = direct ? a.dw + (long long)g * a.dw_gstride
+                      : a.ws + ((long long)z * gridDim.y + g) * (long long)a.Cout * a.K;
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int k = k0 + wk * TK + j * 32 + fr;
+      if (k >= a.K) continue;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int n = n0 + wn * TNo + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * hf;
+        if (n >= a.Cout) continue;
+        const long long o = (long long)n * a.K + k;
+        if (direct) dst[o] += acc[i][j][r];
+        else dst[o] = acc[i][j][r];
+      }
+    }
+}
+
+// dw[g] += sum over the first ceil(Mv_g / mchunk) slabs, in z order
+__global__ __launch_bounds__(256) void xwgrad_reduce_kernel(const float* __restrict__ ws, int G, long long per,
+                                                            const int* __restrict__ nvalid, int N, int HoWo,
+                                                            int mchunk, float* __restrict__ dw, long long dw_gstride) {
+  const int g = blockIdx.y;
+  const int Mv = valid_rows(nvalid, g, N) * HoWo;
+  const int nz = (Mv + mchunk - 1) / mchunk;
+  if (nz == 0) return;
+  for (long long e = blockIdx.x * 256LL + threadIdx.x; e < per; e += (long long)gridDim.x * 256) {
+    float v = 0.f;
+    for (int z = 0; z < nz; ++z) v += ws[((long long)z * G + g) * per + e];
+    dw[(long long)g * dw_gstride + e] += v;
+  }
+}
+
+// ====================================================================== dgrad weights
+// wt[slot][class (ph,pw)][cin][i][j][cout] = w[slot][cout][kh0+i*s][kw0+j*s][cin]
+// (kh0 = (ph + pad) % s): every tap belongs to exactly one parity class.
+struct XTDesc {   // all int64 (built from a torch int64 host tensor)
+  long long w, wt, w_sstride, Cout, KH, KW, Cin, stride, pad, unused;
+};
+constexpr int kXTBatch = 24;   // descriptors per launch, passed by value (graph-capture safe)
+struct XTBatch {
+  XTDesc d[kXTBatch];
+};
+
+__global__ void xtranspose_kernel(const XTBatch b, int slots, const int* __restrict__ nvalid) {
+  const XTDesc& d = b.d[blockIdx.y];
+  const int s = (int)d.stride, KH = (int)d.KH, KW = (int)d.KW, Cin = (int)d.Cin, Cout = (int)d.Cout;
+  const int pad = (int)d.pad;
+  const long long per = (long long)Cout * KH * KW * Cin;
+  for (long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x; t < per * slots;
+       t += (long long)gridDim.x * blockDim.x) {
+    const int sl = (int)(t / per);
+    if (nvalid && nvalid[sl] == 0) continue;
+    long long e = t - sl * per;   // destination index within the slot
+    // walk the classes in (ph, pw) order
+    long long base = 0;
+    int nI = 0, nJ = 0, kh0 = 0, kw0 = 0;
+    for (int cidx = 0; cidx < s * s; ++cidx) {
+      const int ph = cidx / s, pw = cidx - ph * s;
+      kh0 = (ph + pad) % s; kw0 = (pw + pad) % s;
+      nI = kh0 < KH ? (KH - kh0 + s - 1) / s : 0;
+      nJ = kw0 < KW ? (KW - kw0 + s - 1) / s : 0;
+      const long long sz = (long long)Cin * nI * nJ * Cout;
+      if (e < base + sz) break;
+      base += sz;
+    }
+    long long r = e - base;
+    const int co = (int)(r % Cout); r /= Cout;
+    const int j = (int)(r % nJ); r /= nJ;
+    const int i = (int)(r % nI);
+    const int ci = (int)(r / nI);
+    const int kh = kh0 + i * s, kw = kw0 + j * s;
+    const float* w = (const float*)d.w + (long long)sl * d.w_sstride;
+    float* wt = (float*)d.wt + sl * per;
+    wt[e] = w[(((long long)co * KH + kh) * KW + kw) * Cin + ci];
+  }
+}
+
+// dbias[g][n] += sum over valid rows of dy[g][m][n] (fixed order: per-thread strided partial
+// sums, then a fixed LDS tree)
+__global__ __launch_bounds__(256) void xcolsum_kernel(const float* __restrict__ dy, long long dy_gstride, int rows_per_img,
+                                                      const int* __restrict__ nvalid, int N, int C,
+                                                      float* __restrict__ db, long long db_gstride) {
+  __shared__ double red[8][33];
+  const int g = blockIdx.y;
+  const int c = blockIdx.x * 32 + (threadIdx.x & 31), rq = threadIdx.x >> 5;
+  const int R = valid_rows(nvalid, g, N) * rows_per_img;
+  double s = 0.0;    // fp64 partials: a long, cancelling column sum stays at fp32 rounding
+  if (c < C)
+    for (int r = rq; r < R; r += 8) s += dy[(long long)g * dy_gstride + (long long)r * C + c];
+  red[rq][threadIdx.x & 31] = s;
+  __syncthreads();
+  if (rq == 0 && c < C) {
+    double t = red[0][threadIdx.x];
+    for (int k = 1; k < 8; ++k) t += red[k][threadIdx.x];
+    db[(long long)g * db_gstride + c] += (float)t;
+  }
+}
+
+// ============================================================================ host
+int env_int(const char* name, int dflt) {
+  const char* e = getenv(name);
+  return e ? atoi(e) : dflt;
+}
+
+// split planes: 2 (3 MFMAs / product) or 3 (6 MFMAs); DBA_F32_PLANES / dba_xgemm_set_planes
+int& planes() {
+  static int p = env_int("DBA_F32_PLANES", 3);
+  return p;
+}
+
+template <int BM, int BN, int WM, int WN, int P, int VEC>
+int xconv_go(const XArgs& a, long long Mmax, int G, int nclass, hipStream_t st) {
+  XArgs b = a;
+  b.tiles_n = ceil_div(a.Ncol, BN);
+  const dim3 grid((unsigned)(ceil_div(Mmax, BM) * b.tiles_n), G, nclass * a.splitk);
+  hipLaunchKernelGGL((xconv_kernel<BM, BN, WM, WN, P, VEC>), grid, dim3(256), 0, st, b);
+  DBA_LAUNCH_CHECK();
+}
+
+template <int P, int VEC>
+int xconv_tile(const XArgs& a, long long Mmax, int G, int nclass, int bm, hipStream_t st) {
+  if (a.Ncol <= 32) return xconv_go<128, 32, 4, 1, P, VEC>(a, Mmax, G, nclass, st);
+  if (a.Ncol <= 64) {
+    if (bm == 64) return xconv_go<64, 64, 2, 2, P, VEC>(a, Mmax, G, nclass, st);
+    return xconv_go<128, 64, 2, 2, P, VEC>(a, Mmax, G, nclass, st);
+  }
+  if (bm == 64) return xconv_go<64, 128, 2, 2, P, VEC>(a, Mmax, G, nclass, st);
+  return xconv_go<128, 128, 2, 2, P, VEC>(a, Mmax, G, nclass, st);
+}
+
+int xconv_dispatch(const XArgs& a, long long Mmax, int G, int nclass, int vec, hipStream_t st) {
+  // small launches (a lone client's grouped step) take 64-row tiles
+  const int bn = a.Ncol <= 32 ? 32 : a.Ncol <= 64 ? 64 : 128;
+  const long long blocks = (long long)ceil_div(Mmax, 128) * ceil_div(a.Ncol, bn) * G * nclass * a.splitk;
+  const int bm = (bn > 32 && blocks < 512) ? 64 : 128;
+  if (planes() == 2) {
+    return vec == 4 ? xconv_tile<2, 4>(a, Mmax, G, nclass, bm, st) : xconv_tile<2, 1>(a, Mmax, G, nclass, bm, st);
+  }
+  return vec == 4 ? xconv_tile<3, 4>(a, Mmax, G, nclass, bm, st) : xconv_tile<3, 1>(a, Mmax, G, nclass, bm, st);
+}
+
+// split-K factor of a forward launch (1 = none): enough K slices to reach ~256 blocks with
+// at least 4 k-tiles each
+int xsplitk(long long M, int G, int Ncol, int K) {
+  static const int off = env_int("DBA_F32_SPLITK", 1) == 0;
+  if (off) return 1;
+  const int bn = Ncol <= 32 ? 32 : Ncol <= 64 ? 64 : 128;
+  const long long blocks = (long long)ceil_div(M, 64) * ceil_div(Ncol, bn) * G;
+  if (blocks >= 128) return 1;
+  const int nkt = (K + 31) / 32;
+  int s = (int)std::min<long long>(8, (256 + blocks - 1) / blocks);
+  while (s > 1 && nkt / s < 4) --s;
+  return s;
+}
+
+bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+struct ClassGeom {
+  int n;
+  XClass c[4];
+};
+
+// parity classes of a stride-s data gradient (see xtranspose_kernel for the weight order)
+ClassGeom dgrad_classes(int H, int W, int Cin, int Cout, int KH, int KW, int s, int pad) {
+  ClassGeom cg{};
+  cg.n = s * s;
+  long long off = 0;
+  for (int ci = 0; ci < s * s; ++ci) {
+    const int ph = ci / s, pw = ci - ph * s;
+    const int kh0 = (ph + pad) % s, kw0 = (pw + pad) % s;
+    XClass& c = cg.c[ci];
+    c.nI = kh0 < KH ? (KH - kh0 + s - 1) / s : 0;
+    c.nJ = kw0 < KW ? (KW - kw0 + s - 1) / s : 0;
+    c.bh = (ph + pad - kh0) / s;
+    c.bw = (pw + pad - kw0) / s;
+    c.oh = ph;
+    c.ow = pw;
+    c.Hq = ph < H ? (H - ph + s - 1) / s : 0;
+    c.Wq = pw < W ? (W - pw + s - 1) / s : 0;
+    c.boff = off;
+    off += (long long)Cin * c.nI * c.nJ * Cout;
+  }
+  return cg;
+}
+
+}  // namespace
+
+DBA_EXPORT int dba_xgemm_set_planes(int p) {
+  const int prev = planes();
+  if (p == 2 || p == 3) planes() = p;
+  return prev;
+}
+
+// workspace floats a split-K forward launch of this shape needs (0: none)
+DBA_EXPORT long long dba_xconv_ws_floats(int G, int N, int Ho, int Wo, int Cin, int Cout, int KH, int KW) {
+  const long long M = (long long)N * Ho * Wo;
+  const int s = xsplitk(M, G, Cout, KH * KW * Cin);
+  return s > 1 ? (long long)s * G * M * Cout : 0;
+}
+
+// y = act(conv(x, w) + bias + res), fp32 NHWC; w [slots][Cout][KH][KW][Cin]
+DBA_EXPORT int dba_xconv_fwd(const float* x, long long x_gstride, const float* w, long long w_sstride,
+                             const int* wsel, const float* bias, long long b_sstride, const float* res, float* out,
+                             long long out_gstride, const int* nvalid, int G, int N, int H, int W, int Cin, int Ho,
+                             int Wo, int Cout, int KH, int KW, int stride, int pad, int relu, float* ws,
+                             long long ws_floats, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  const long long M = (long long)N * Ho * Wo;
+  const int K = KH * KW * Cin;
+  const int vec = (Cin % 4 == 0 && aligned16(x) && aligned16(w) && x_gstride % 4 == 0 && w_sstride % 4 == 0) ? 4 : 1;
+  XArgs a{};
+  a.src = x; a.src_gstride = x_gstride; a.w = w; a.w_sstride = w_sstride; a.wsel = wsel;
+  a.bias = bias; a.b_sstride = b_sstride; a.res = res; a.out = out; a.out_gstride = out_gstride;
+  a.nvalid = nvalid; a.N = N; a.Hs = H; a.Ws = W; a.Cs = Cin; a.Ncol = Cout; a.Ho = Ho; a.Wo = Wo;
+  a.sp = stride; a.os = 1; a.dsg = 1; a.relu = relu; a.splitk = 1;
+  a.cls[0] = XClass{KH, KW, -pad, -pad, 0, 0, Ho, Wo, 0};
+  const int s = xsplitk(M, G, Cout, K);
+  if (s > 1 && ws != nullptr && ws_floats >= (long long)s * G * M * Cout) {
+    XArgs b = a;
+    b.splitk = s;
+    b.out = ws;
+    b.out_gstride = M * Cout;
+    b.zstride = (long long)G * M * Cout;
+    const int rc = xconv_dispatch(b, M, G, 1, vec, st);
+    if (rc != 0) return rc;
+    const long long per = M * Cout;
+    const dim3 grid((unsigned)std::max(1LL, std::min(1024LL, (per + 255) / 256)), G);
+    hipLaunchKernelGGL(xsplitk_reduce_kernel, grid, dim3(256), 0, st, (const float*)ws, s, b.zstride, per, nvalid, N,
+                       Ho * Wo, Cout, bias, b_sstride, wsel, res, relu, out);
+    DBA_LAUNCH_CHECK();
+  }
+  return xconv_dispatch(a, M, G, 1, vec, st);
+}
+
+// dX of a conv from class-packed transposed weights (dba_xtranspose); accum (optional) is
+// added in.  dy [G][N][Ho][Wo][Cout] -> dx [G][N][H][W][Cin]
+DBA_EXPORT int dba_xconv_dgrad(const float* dy, long long dy_gstride, const float* wt, long long wt_sstride,
+                               const int* wsel, const float* accum, float* dx, long long dx_gstride,
+                               const int* nvalid, int G, int N, int H, int W, int Cin, int Ho, int Wo, int Cout,
+                               int KH, int KW, int stride, int pad, float* ws, long long ws_floats, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  const ClassGeom cg = dgrad_classes(H, W, Cin, Cout, KH, KW, stride, pad);
+  const int vec = (Cout % 4 == 0 && aligned16(dy) && aligned16(wt) && dy_gstride % 4 == 0 && wt_sstride % 4 == 0) ? 4 : 1;
+  XArgs a{};
+  a.src = dy; a.src_gstride = dy_gstride; a.w = wt; a.w_sstride = wt_sstride; a.wsel = wsel;
+  a.bias = nullptr; a.b_sstride = 0; a.res = accum; a.out = dx; a.out_gstride = dx_gstride;
+  a.nvalid = nvalid; a.N = N; a.Hs = Ho; a.Ws = Wo; a.Cs = Cout; a.Ncol = Cin; a.Ho = H; a.Wo = W;
+  a.sp = 1; a.os = stride; a.dsg = -1; a.relu = 0; a.splitk = 1;
+  long long Mmax = 0;
+  for (int i = 0; i < cg.n; ++i) {
+    a.cls[i] = cg.c[i];
+    Mmax = std::max(Mmax, (long long)N * cg.c[i].Hq * cg.c[i].Wq);
+  }
+  if (stride == 1) {
+    const long long M = (long long)N * H * W;
+    const int s = xsplitk(M, G, Cin, KH * KW * Cout);
+    if (s > 1 && ws != nullptr && ws_floats >= (long long)s * G * M * Cin) {
+      XArgs b = a;
+      b.splitk = s;
+      b.out = ws;
+      b.out_gstride = M * Cin;
+      b.zstride = (long long)G * M * Cin;
+      const int rc = xconv_dispatch(b, M, G, 1, vec, st);
+      if (rc != 0) return rc;
+      const long long per = M * Cin;
+      const dim3 grid((unsigned)std::max(1LL, std::min(1024LL, (per + 255) / 256)), G);
+      hipLaunchKernelGGL(xsplitk_reduce_kernel, grid, dim3(256), 0, st, (const float*)ws, s, b.zstride, per, nvalid,
+                         N, H * W, Cin, nullptr, 0LL, wsel, accum, 0, dx);
+      DBA_LAUNCH_CHECK();
+    }
+  }
+  return xconv_dispatch(a, Mmax, G, cg.n, vec, st);
+}
+
+// class-packed data-gradient weights for n convs.  desc: n x XTDesc in HOST memory, read
+// here and passed to the kernel by value (safe under HIP graph capture); nvalid (optional,
+// slots == replicas) skips inactive slots.
+DBA_EXPORT int dba_xtranspose(const void* desc, int n, int slots, long long max_per, const int* nvalid,
+                              void* stream) {
+  const XTDesc* ds = (const XTDesc*)desc;
+  const long long total = max_per * slots;
+  for (int i0 = 0; i0 < n; i0 += kXTBatch) {
+    XTBatch b{};
+    const int m = std::min(kXTBatch, n - i0);
+    for (int i = 0; i < m; ++i) b.d[i] = ds[i0 + i];
+    const dim3 grid((unsigned)std::max(1LL, std::min(4096LL, (total + 255) / 256)), m);
+    hipLaunchKernelGGL(xtranspose_kernel, grid, dim3(256), 0, (hipStream_t)stream, b, slots, nvalid);
+    const int rc = (int)hipGetLastError();
+    if (rc != 0) return rc;
+  }
+  return 0;
+}
+
+// slab floats dba_xwgrad needs for this shape (0: accumulates straight into dw)
+DBA_EXPORT long long dba_xwgrad_ws_floats(int G, int N, int Ho, int Wo, int Cin, int Cout, int KH, int KW, int* mchunk_out) {
+  const int K = KH * KW * Cin;
+  const int bno = Cout <= 32 ? 32 : Cout <= 64 ? 64 : 128;
+  const long long tiles = (long long)ceil_div(Cout, bno) * ceil_div(K, 128) * G;
+  const long long M = (long long)N * Ho * Wo;
+  const int target = env_int("DBA_F32_WGRAD_BLOCKS", 768);
+  long long Z = std::max(1LL, std::min((target + tiles - 1) / tiles, M / 256));
+  int mchunk = (int)((M + Z - 1) / Z);
+  mchunk = (mchunk + 31) / 32 * 32;
+  Z = (M + mchunk - 1) / mchunk;
+  if (mchunk_out) *mchunk_out = mchunk;
+  return Z > 1 ? Z * G * Cout * K : 0;
+}
+
+// dw[g] += sum_m dy (x) im2col(x) (fp32, deterministic); dw [G][Cout][KH][KW][Cin] rows
+DBA_EXPORT int dba_xwgrad(const float* dy, long long dy_gstride, const float* x, long long x_gstride, float* dw,
+                          long long dw_gstride, const int* nvalid, int G, int N, int H, int W, int Cin, int Ho,
+                          int Wo, int Cout, int KH, int KW, int stride, int pad, float* ws, long long ws_floats,
+                          void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  int mchunk = 0;
+  const long long need = dba_xwgrad_ws_floats(G, N, Ho, Wo, Cin, Cout, KH, KW, &mchunk);
+  if (need > 0 && (ws == nullptr || ws_floats < need)) return -101;
+  const long long M = (long long)N * Ho * Wo;
+  const int Z = (int)((M + mchunk - 1) / mchunk);
+  XWArgs a{};
+  a.dy = dy; a.dy_gstride = dy_gstride; a.x = x; a.x_gstride = x_gstride; a.ws = ws; a.dw = dw;
+  a.dw_gstride = dw_gstride; a.nvalid = nvalid; a.N = N; a.H = H; a.W = W; a.Cin = Cin; a.Ho = Ho; a.Wo = Wo;
+  a.Cout = Cout; a.KW = KW; a.stride = stride; a.pad = pad; a.K = KH * KW * Cin;
+  a.mchunk = mchunk;
+  a.dHoWo = FDiv{Ho * Wo, 1.0f / (float)(Ho * Wo)};
+  a.dWo = FDiv{Wo, 1.0f / (float)Wo};
+  a.tiles_k = ceil_div(a.K, 128);
+  const bool v4 = Cin % 4 == 0 && Cout % 4 == 0 && aligned16(dy) && aligned16(x) && dy_gstride % 4 == 0 &&
+                  x_gstride % 4 == 0;
+  const int bno = Cout <= 32 ? 32 : Cout <= 64 ? 64 : 128;
+  const dim3 grid((unsigned)(ceil_div(Cout, bno) * a.tiles_k), G, Z);
+#define XW_GO(BNO_, WN__, WK__, P_, V_) \
+  hipLaunchKernelGGL((xwgrad_kernel<BNO_, 128, WN__, WK__, P_, V_>), grid, dim3(256), 0, st, a)
+#define XW_P(P_, V_)                                  \
+  do {                                                \
+    if (bno == 32) XW_GO(32, 1, 4, P_, V_);           \
+    else if (bno == 64) XW_GO(64, 2, 2, P_, V_);      \
+    else XW_GO(128, 2, 2, P_, V_);                    \
+  } while (0)
+  if (planes() == 2) {
+    if (v4) XW_P(2, 4); else XW_P(2, 1);
+  } else {
+    if (v4) XW_P(3, 4); else XW_P(3, 1);
+  }
+#undef XW_P
+#undef XW_GO
+  if (Z > 1) {
+    const long long per = (long long)Cout * a.K;
+    const dim3 g2((unsigned)std::max(1LL, std::min(1024LL, (per + 255) / 256)), G);
+    hipLaunchKernelGGL(xwgrad_reduce_kernel, g2, dim3(256), 0, st, (const float*)ws, G, per, nvalid, N, Ho * Wo,
+                       mchunk, dw, dw_gstride);
+  }
+  DBA_LAUNCH_CHECK();
+}
+
+DBA_EXPORT int dba_xcolsum(const float* dy, long long dy_gstride, int rows_per_img, const int* nvalid, int G, int N,
+                           int C, float* db, long long db_gstride, void* stream) {
+  hipLaunchKernelGGL(xcolsum_kernel, dim3(ceil_div(C, 32), G), dim3(256), 0, (hipStream_t)stream, dy, dy_gstride,
+                     rows_per_img, nvalid, N, C, db, db_gstride);
+  DBA_LAUNCH_CHECK();
+}

@@ -84,11 +84,15 @@ class _EarlyEval:
 
 
 def compute_dtype_for(params: C.Params, device: torch.device) -> torch.dtype:
+    """Activation / GEMM precision.  ``fp32`` (the default, = the reference's precision) runs
+    the split-bf16 fp32 kernel family on GPU (csrc/kernels/xgemm.hip); ``bf16`` opts into the
+    bf16 MFMA family (fp32 master weights, bf16 activations)."""
     cd = str(params["compute_dtype"]).lower()
-    if cd == "auto":
-        return torch.bfloat16 if device.type == "cuda" else torch.float32
-    return {"bf16": torch.bfloat16, "bfloat16": torch.bfloat16, "fp32": torch.float32,
-            "float32": torch.float32}[cd]
+    table = {"auto": torch.float32, "bf16": torch.bfloat16, "bfloat16": torch.bfloat16, "fp32": torch.float32,
+             "float32": torch.float32}
+    if cd not in table:
+        raise ValueError(f"compute_dtype {cd!r}: expected fp32 or bf16")
+    return table[cd]
 
 
 class Server:

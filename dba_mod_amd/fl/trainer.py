@@ -126,7 +126,8 @@ class GroupTrainer:
                        nvalid=b.nvalid, dropout_seed=b.seed, act_dtype=self.dtype)
         logits = prog.forward(ctx, x)
         fused = self.alpha == 1.0     # stats straight from the loss kernel (no extra launches)
-        loss, correct, dl = ops.softmax_xent(logits, y, True, True, *((b.stats, b.slot, b.nvalid) if fused else ()))
+        loss, correct, dl = ops.softmax_xent(logits, y, True, True, *((b.stats, b.slot, b.nvalid) if fused else ()),
+                                             grad_dtype=x.dtype)
         if self.spec.arch == "loan":   # reference LoanNet raises on NaN outputs (loan_model.py:25-26)
             b.nan_flag += torch.isnan(loss).any().float()
         b.grads.zero_()

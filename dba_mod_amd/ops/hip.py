@@ -16,6 +16,7 @@ from . import build
 
 Tensor = torch.Tensor
 _BF16 = torch.bfloat16
+_F32 = torch.float32
 
 if not os.path.exists(build.kernels_path()):
     raise ImportError(f"HIP kernel library missing: {build.kernels_path()} — run "
@@ -41,20 +42,21 @@ _SIGS = {
     "dba_transpose_w_batch": [_P, _I, _I, _P, _P],
     "dba_halo_conv": [_P, _LL, _P, _LL, _P, _P, _LL, _P, _P, _LL, _I, _P] + [_I] * 9 + [_P],
     "dba_colsum": [_P, _LL, _I, _P, _I, _I, _I, _P, _LL, _P],
-    "dba_bn_stats": [_P, _P, _I, _I, _I, _I, _P, _P, _P, _LL, _F, _F, _P, _P, _P],
+    "dba_xcolsum": [_P, _LL, _I, _P, _I, _I, _I, _P, _LL, _P],
+    "dba_bn_stats": [_P, _P, _I, _I, _I, _I, _P, _P, _P, _LL, _F, _F, _P, _P, _I, _P],
     "dba_bn_partial_blocks": [_I, _I, _I],
-    "dba_bn_apply": [_P, _P, _P, _P, _P, _LL, _P, _I, _P, _P, _I, _I, _I, _I, _P],
-    "dba_bn_bwd": [_P, _P, _P, _P, _P, _P, _LL, _I, _P, _P, _LL, _P, _P, _P, _P, _I, _I, _I, _I, _P],
-    "dba_bn_small_fwd": [_P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _LL, _F, _F, _P, _I, _P, _P, _P, _P],
-    "dba_bn_small_bwd": [_P, _P, _P, _P, _P, _P, _LL, _I, _P, _P, _LL, _P, _P, _P, _I, _I, _I, _I, _P],
-    "dba_bn_fold": [_P, _LL, _P, _P, _P, _P, _P, _LL, _F, _P, _P, _I, _I, _I, _P],
-    "dba_relu_mask_bwd": [_P, _P, _P, _LL, _P],
-    "dba_maxpool": [_P, _P, _P, _LL, _I, _I, _I, _I, _I, _I, _I, _I, _P],
-    "dba_maxpool_bwd": [_P, _P, _P, _LL, _I, _I, _I, _I, _I, _I, _I, _I, _P],
-    "dba_avgpool": [_P, _P, _LL, _I, _I, _P],
-    "dba_avgpool_bwd": [_P, _P, _LL, _I, _I, _P],
+    "dba_bn_apply": [_P, _P, _P, _P, _P, _LL, _P, _I, _P, _P, _I, _I, _I, _I, _I, _P],
+    "dba_bn_bwd": [_P, _P, _P, _P, _P, _P, _LL, _I, _P, _P, _LL, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P],
+    "dba_bn_small_fwd": [_P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _LL, _F, _F, _P, _I, _P, _P, _P, _I, _P],
+    "dba_bn_small_bwd": [_P, _P, _P, _P, _P, _P, _LL, _I, _P, _P, _LL, _P, _P, _P, _I, _I, _I, _I, _I, _P],
+    "dba_bn_fold": [_P, _LL, _P, _P, _P, _P, _P, _LL, _F, _P, _P, _I, _I, _I, _I, _P],
+    "dba_relu_mask_bwd": [_P, _P, _P, _LL, _I, _P],
+    "dba_maxpool": [_P, _P, _P, _LL, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P],
+    "dba_maxpool_bwd": [_P, _P, _P, _LL, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P],
+    "dba_avgpool": [_P, _P, _LL, _I, _I, _I, _P],
+    "dba_avgpool_bwd": [_P, _P, _LL, _I, _I, _I, _P],
     "dba_dropout": [_P, _P, _I, _P, _U, _F, _LL, _I, _P],
-    "dba_softmax_xent": [_P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _LL, _P, _I, _P, _P],
+    "dba_softmax_xent": [_P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _LL, _P, _I, _P, _I, _P],
     "dba_sgd_step": [_P, _LL, _P, _P, _P, _P, _P, _F, _F, _P, _P, _I, _I, _P],
     "dba_scale_from_base": [_P, _P, _F, _P, _LL, _P],
     "dba_add_noise_scaled": [_P, _P, _LL, _F, _F, _U, _I, _P],
@@ -68,12 +70,22 @@ _SIGS = {
     "dba_pwgrad": [_P, _LL, _P, _LL, _P, _LL, _P, _P, _I, _I, _I, _I, _I, _I, _P],
     "dba_wgrad3": [_P, _LL, _P, _LL, _P, _LL, _P, _P] + [_I] * 12 + [_P],
     "dba_dist_loss_grad": [_P, _LL, _P, _LL, _P, _LL, _I, _P, _P, _F, _P, _P],
+    # reference-precision (fp32) family: csrc/kernels/xgemm.hip
+    "dba_xgemm_set_planes": [_I],
+    "dba_xconv_ws_floats": [_I] * 8,
+    "dba_xconv_fwd": [_P, _LL, _P, _LL, _P, _P, _LL, _P, _P, _LL, _P] + [_I] * 13 + [_P, _LL, _P],
+    "dba_xconv_dgrad": [_P, _LL, _P, _LL, _P, _P, _P, _LL, _P] + [_I] * 12 + [_P, _LL, _P],
+    "dba_xtranspose": [_P, _I, _I, _LL, _P, _P],
+    "dba_xwgrad_ws_floats": [_I] * 8 + [_P],
+    "dba_xwgrad": [_P, _LL, _P, _LL, _P, _LL, _P] + [_I] * 12 + [_P, _LL, _P],
 }
 for _name, _args in _SIGS.items():
     _fn = getattr(_L, _name)
     _fn.argtypes = _args
     _fn.restype = ctypes.c_int
 _L.dba_conv3_splitk_floats.restype = ctypes.c_longlong
+_L.dba_xconv_ws_floats.restype = ctypes.c_longlong
+_L.dba_xwgrad_ws_floats.restype = ctypes.c_longlong
 
 
 NOT_HANDLED = -100   # a conv2 entry point declining a shape (odd channel counts)
@@ -116,10 +128,20 @@ def _rowview(t: Tensor) -> Tuple[Tensor, int]:
     return t, (t.stride(0) if t.shape[0] > 1 else int(torch.tensor(t.shape[1:]).prod()))
 
 
-def _bf16c(t: Tensor) -> Tensor:
-    if t.dtype != _BF16:
-        t = t.to(_BF16)
+def _act(t: Tensor, dt: Optional[torch.dtype] = None, what: str = "activation") -> Tensor:
+    """An activation operand, contiguous and NEVER converted: the kernels run in the dtype
+    the caller computes in (bf16 -> bf16 MFMA family, fp32 -> split-bf16 reference-precision
+    family).  ``dt`` pins the dtype (every operand of one op must agree)."""
+    if t.dtype not in (_BF16, _F32):
+        raise TypeError(f"{what}: unsupported dtype {t.dtype} (bf16 or fp32)")
+    if dt is not None and t.dtype != dt:
+        raise TypeError(f"{what}: dtype {t.dtype} does not match the op's {dt} operands "
+                        f"(no silent precision conversion)")
     return t.contiguous()
+
+
+def _f32(t: Tensor) -> int:
+    return int(t.dtype == _F32)
 
 
 # ------------------------------------------------------------------------- data ingest
@@ -149,9 +171,10 @@ def gather_rows(src, labels, idx, trig_cols, trig_vals, trig_id, poison_n, targe
 
 
 # ------------------------------------------------------------------------------ conv
-def _check_w(w: Tensor) -> Tuple[Tensor, int]:
-    if w.dtype != _BF16:
-        w = w.to(_BF16)
+def _check_w(w: Tensor, dt: torch.dtype = _BF16) -> Tuple[Tensor, int]:
+    if w.dtype != dt:
+        raise TypeError(f"conv weights: dtype {w.dtype} does not match the {dt} activations "
+                        f"(no silent precision conversion)")
     return _rowview(w)
 
 
@@ -197,14 +220,50 @@ def set_gemm3_tiles(small: int = -1, big: int = -1) -> Tuple[int, int]:
     return prev // 16, prev % 16
 
 
+def set_fp32_planes(planes: int) -> int:
+    """Split planes of the fp32 family (csrc/kernels/xgemm.hip): 3 (default; 6 bf16 MFMAs per
+    product, error at the fp32-accumulation level) or 2 (3 MFMAs, ~4e-6 relative).  Returns
+    the previous setting."""
+    if planes not in (2, 3):
+        raise ValueError("fp32 split planes must be 2 or 3")
+    return int(_L.dba_xgemm_set_planes(int(planes)))
+
+
 def _pconv_ok(Cin, Cout, H, W, KH, KW, stride, pad) -> bool:
     """H, W = input size."""
     return (_PCONV and KH == 3 and KW == 3 and pad == 1 and H == W
             and (Cin, Cout, W, stride) in _PCONV_SHAPES)
 
 
+def _xconv_fwd(x, w, wsel, stride, pad, bias, residual, relu, nvalid, out_dtype):
+    """Reference-precision conv (fp32 in / fp32 out, split-bf16 MFMA: xgemm.hip)."""
+    if out_dtype not in (None, _F32):
+        raise TypeError(f"fp32 conv cannot emit {out_dtype} (no silent precision conversion)")
+    G, N, H, W, Cin = x.shape
+    w, ws = _check_w(w, _F32)
+    Cout, KH, KW = w.shape[1], w.shape[2], w.shape[3]
+    assert w.shape[4] == Cin, (w.shape, x.shape)
+    Ho = (H + 2 * pad - KH) // stride + 1
+    Wo = (W + 2 * pad - KW) // stride + 1
+    y = torch.empty(G, N, Ho, Wo, Cout, dtype=_F32, device=x.device)
+    bs = 0
+    if bias is not None:
+        if bias.dtype != _F32:
+            raise TypeError(f"conv bias must be fp32 (got {bias.dtype})")
+        bias, bs = _rowview(bias)
+    res = _act(residual, _F32, "residual") if residual is not None else None
+    n = int(_L.dba_xconv_ws_floats(G, N, Ho, Wo, Cin, Cout, KH, KW))
+    wsb = torch.empty(n, dtype=_F32, device=x.device) if n > 0 else None
+    _call("dba_xconv_fwd", x.data_ptr(), N * H * W * Cin, w.data_ptr(), ws, _ptr(_i32(wsel)), _ptr(bias), bs,
+          _ptr(res), y.data_ptr(), N * Ho * Wo * Cout, _ptr(_i32(nvalid)), G, N, H, W, Cin, Ho, Wo, Cout, KH, KW,
+          stride, pad, int(relu), _ptr(wsb), n, _stream())
+    return y
+
+
 def conv2d(x, w, wsel, stride, pad, bias=None, residual=None, relu=False, nvalid=None, out_dtype=None):
-    x = _bf16c(x)
+    x = _act(x, None, "conv input")
+    if x.dtype == _F32:
+        return _xconv_fwd(x, w, wsel, stride, pad, bias, residual, relu, nvalid, out_dtype)
     G, N, H, W, Cin = x.shape
     w, ws = _check_w(w)
     Cout, KH, KW = w.shape[1], w.shape[2], w.shape[3]
@@ -215,10 +274,11 @@ def conv2d(x, w, wsel, stride, pad, bias=None, residual=None, relu=False, nvalid
     y = torch.empty(G, N, Ho, Wo, Cout, dtype=out_dtype, device=x.device)
     bs = 0
     if bias is not None:
-        bias = bias.float()
+        if bias.dtype != _F32:
+            raise TypeError(f"conv bias must be fp32 (got {bias.dtype})")
         bias, bs = _rowview(bias)
     if residual is not None:
-        residual = _bf16c(residual)
+        residual = _act(residual, _BF16, "residual")
     wsel_, nv_, f32 = _ptr(_i32(wsel)), _ptr(_i32(nvalid)), int(out_dtype == torch.float32)
     # kernel selection by shape: halo-tiled direct conv (stride 1), gen-2 implicit GEMM
     # (Cin % 8 == 0 or small-Cin stems), gen-1 implicit GEMM (odd channel counts)
@@ -265,12 +325,41 @@ def _dgrad_flip(w_shape, stride, pad, in_hw) -> Optional[int]:
 _TBATCH_MAX = 32
 
 
+def _xtranspose(items) -> list:
+    """Parity-class packed fp32 data-gradient weights (xgemm.hip xtranspose_kernel) of
+    ``items = [(w, stride, pad, nvalid_or_None)]`` (same slot count) in ONE launch."""
+    outs, desc, max_per, nv = [], [], 0, None
+    slots = items[0][0].shape[0]
+    for w, stride, pad, nvalid in items:
+        wv, ws = _check_w(w, _F32)
+        _, Cout, KH, KW, Cin = wv.shape
+        per = Cout * KH * KW * Cin
+        wt = torch.empty(slots, per, dtype=_F32, device=wv.device)
+        outs.append(wt)
+        desc.append([wv.data_ptr(), wt.data_ptr(), ws, Cout, KH, KW, Cin, stride, pad, 0])
+        max_per = max(max_per, per)
+        nv = nvalid
+    d = torch.tensor(desc, dtype=torch.int64)    # host table: the launcher passes it by value
+    _call("dba_xtranspose", d.data_ptr(), len(desc), slots, max_per, _ptr(_i32(nv)), _stream())
+    return outs
+
+
 def prepare_dgrad_weights(ref, items):
     """All of a training step's data-gradient weight transposes in ONE launch.
 
     ``items``: list of ``(w, wsel, stride, pad, in_hw, nvalid, G)`` for every conv whose input
     gradient the backward pass will compute.  Returns ``{index: wt}`` to be handed to
     :func:`conv2d_dgrad` as ``wt=`` (items that need no transpose are absent)."""
+    if items and items[0][0].dtype == _F32:
+        # fp32 family: every data gradient reads class-packed transposed weights
+        slots = items[0][0].shape[0]
+        sel = [k for k, it in enumerate(items) if it[0].shape[0] == slots]
+        if not sel:
+            return {}
+        it0 = items[sel[0]]
+        nv = it0[5] if (it0[1] is None and it0[5] is not None and slots == it0[6]) else None
+        wts = _xtranspose([(items[k][0], items[k][2], items[k][3], nv) for k in sel])
+        return dict(zip(sel, wts))
     out = {}
     desc = []
     nv_ptr, slots_all = None, None
@@ -294,20 +383,45 @@ def prepare_dgrad_weights(ref, items):
     return out
 
 
+def _xconv_dgrad(dy, w, wsel, stride, pad, in_hw, nvalid, out_dtype, accum, wt):
+    if out_dtype not in (None, _F32):
+        raise TypeError(f"fp32 dgrad cannot emit {out_dtype} (no silent precision conversion)")
+    G, N, Ho, Wo, Cout = dy.shape
+    wv, _ = _check_w(w, _F32)
+    slots, _, KH, KW, Cin = wv.shape
+    H, W = in_hw
+    if wt is None:
+        nv = nvalid if (wsel is None and nvalid is not None and slots == G) else None
+        wt = _xtranspose([(wv, stride, pad, nv)])[0]
+    per = Cout * KH * KW * Cin
+    assert wt.dtype == _F32 and wt.is_contiguous() and wt.numel() == slots * per
+    dx = torch.empty(G, N, H, W, Cin, dtype=_F32, device=dy.device)
+    acc = _act(accum, _F32, "dgrad accum") if accum is not None else None
+    if acc is not None:
+        assert acc.shape == dx.shape
+    n = int(_L.dba_xconv_ws_floats(G, N, H, W, Cout, Cin, KH, KW)) if stride == 1 else 0
+    wsb = torch.empty(n, dtype=_F32, device=dy.device) if n > 0 else None
+    _call("dba_xconv_dgrad", dy.data_ptr(), N * Ho * Wo * Cout, wt.data_ptr(), per, _ptr(_i32(wsel)), _ptr(acc),
+          dx.data_ptr(), N * H * W * Cin, _ptr(_i32(nvalid)), G, N, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad,
+          _ptr(wsb), n, _stream())
+    return dx
+
+
 def conv2d_dgrad(dy, w, wsel, stride, pad, in_hw, nvalid=None, out_dtype=None, accum=None, wt=None):
-    dy = _bf16c(dy)
+    dy = _act(dy, None, "dgrad dy")
+    if dy.dtype == _F32:
+        return _xconv_dgrad(dy, w, wsel, stride, pad, in_hw, nvalid, out_dtype, accum, wt)
     G, N, Ho, Wo, Cout = dy.shape
     w, ws = _check_w(w)
     slots, _, KH, KW, Cin = w.shape
     H, W = in_hw
     have_wt = wt is not None
     dx = torch.empty(G, N, H, W, Cin, dtype=_BF16, device=dy.device)
-    acc = _bf16c(accum) if accum is not None else None
+    acc = _act(accum, _BF16, "dgrad accum") if accum is not None else None
     if acc is not None:
         assert acc.shape == dx.shape
-
-    def done(t):
-        return t if out_dtype in (None, _BF16) else t.to(out_dtype)
+    if out_dtype not in (None, _BF16):
+        raise TypeError(f"bf16 dgrad cannot emit {out_dtype}")
 
     if stride == 1 and _pconv_ok(Cout, Cin, H, W, KH, KW, stride, pad):
         # stride-1 3x3 dgrad on the persistent kernel: transposed + flipped weight fragments
@@ -316,7 +430,7 @@ def conv2d_dgrad(dy, w, wsel, stride, pad, in_hw, nvalid=None, out_dtype=None, a
                    _ptr(acc), dx.data_ptr(), N * H * W * Cin, _ptr(_i32(nvalid)), _zeros(dy.device).data_ptr(), G,
                    N, H, W, Cout, Cin, 1, 0, 1, _stream())
         if rc != NOT_HANDLED:
-            return done(dx)
+            return dx
     if _DGRAD_W:
         # implicit GEMM reading the forward weights K-major with transposed LDS reads
         # (experimental: measured slower than transpose + gen-2 GEMM on the ResNet shapes)
@@ -324,7 +438,7 @@ def conv2d_dgrad(dy, w, wsel, stride, pad, in_hw, nvalid=None, out_dtype=None, a
                    _ptr(acc), dx.data_ptr(), N * H * W * Cin, _ptr(_i32(nvalid)), G, N, H, W, Cin, Ho, Wo, Cout, KH,
                    KW, stride, pad, _stream())
         if rc != NOT_HANDLED:
-            return done(dx)
+            return dx
     if not have_wt:
         wt = torch.empty(slots, Cin, KH, KW, Cout, dtype=_BF16, device=dy.device)
     # slot == replica when there is no slot map: inactive replicas' slots need no transpose
@@ -339,12 +453,12 @@ def conv2d_dgrad(dy, w, wsel, stride, pad, in_hw, nvalid=None, out_dtype=None, a
                         None, 0, _ptr(acc), dx.data_ptr(), N * H * W * Cin, 0, _ptr(_i32(nvalid)), dy.device, G, N,
                         Ho, Wo, Cout, H, W, Cin, KH, KH, 1, KH - 1 - pad, 0)
         if rc != NOT_HANDLED:
-            return done(dx)
+            return dx
         rc = _call("dba_halo_conv", dy.data_ptr(), N * Ho * Wo * Cout, wt.data_ptr(), Cin * KH * KW * Cout,
                    _ptr(_i32(wsel)), None, 0, _ptr(acc), dx.data_ptr(), N * H * W * Cin, 0, _ptr(_i32(nvalid)), G,
                    N, Ho, Wo, Cout, Cin, KH, KH - 1 - pad, 0, _stream())
         if rc != NOT_HANDLED:
-            return done(dx)
+            return dx
     if not have_wt:
         _call("dba_transpose_w", w.data_ptr(), ws, wt.data_ptr(), slots, Cout, KH * KW, Cin, 0, skip, _stream())
     args = (dy.data_ptr(), N * Ho * Wo * Cout, wt.data_ptr(), Cin * KH * KW * Cout, _ptr(_i32(wsel)))
@@ -354,15 +468,26 @@ def conv2d_dgrad(dy, w, wsel, stride, pad, in_hw, nvalid=None, out_dtype=None, a
         _call("dba_conv_dgrad", *args, *tail)
         if acc is not None:
             dx += acc
-    return done(dx)
+    return dx
 
 
 def conv2d_wgrad(dy, x, stride, pad, kh, kw, dw, dbias=None, nvalid=None):
-    dy = _bf16c(dy)
-    x = _bf16c(x)
+    dy = _act(dy, None, "wgrad dy")
+    x = _act(x, dy.dtype, "wgrad x")
     G, N, Ho, Wo, Cout = dy.shape
     _, _, H, W, Cin = x.shape
     assert dw.dtype == torch.float32 and _inner_contig(dw)
+    if dy.dtype == _F32:
+        n = int(_L.dba_xwgrad_ws_floats(G, N, Ho, Wo, Cin, Cout, kh, kw, None))
+        wsb = torch.empty(n, dtype=_F32, device=dy.device) if n > 0 else None
+        _call("dba_xwgrad", dy.data_ptr(), N * Ho * Wo * Cout, x.data_ptr(), N * H * W * Cin, dw.data_ptr(),
+              dw.stride(0), _ptr(_i32(nvalid)), G, N, H, W, Cin, Ho, Wo, Cout, kh, kw, stride, pad, _ptr(wsb), n,
+              _stream())
+        if dbias is not None:
+            assert dbias.dtype == torch.float32 and dbias.stride(1) == 1
+            _call("dba_xcolsum", dy.data_ptr(), N * Ho * Wo * Cout, Ho * Wo, _ptr(_i32(nvalid)), G, N, Cout,
+                  dbias.data_ptr(), dbias.stride(0), _stream())
+        return
     rc = NOT_HANDLED
     if _PCONV and stride == 1 and kh == 3 and kw == 3 and pad == 1 and H == W and Ho == H:
         # halo-tiled transposed-read wgrad (csrc/kernels/pwgrad.hip)
@@ -394,34 +519,46 @@ def _same_stride(*ts: Tensor) -> int:
 _BN_SMALL_ROWS = int(os.environ.get("DBA_BN_SMALL_ROWS", "1024"))
 
 
+def _bn_layout(C: int) -> None:
+    # the kernels' channel contract (bn.hip bn_layout_ok): 8-channel vectors, and a thread of
+    # the grid-stride passes always owns the same 8 channels
+    if C % 8 != 0 or C > 2048 or 256 % (C // 8) != 0:
+        raise ValueError(f"BN over {C} channels: need C % 8 == 0, C <= 2048 and 256 % (C/8) == 0")
+
+
 def bn_train(y, gamma, beta, rmean, rvar, nvalid, momentum, eps, relu, residual):
-    y = _bf16c(y)
+    y = _act(y, None, "bn input")
     G, N, H, W, C = y.shape
-    assert C % 8 == 0
+    _bn_layout(C)
+    f32 = _f32(y)
     ps = _same_stride(gamma, beta, rmean, rvar)
     mean = torch.empty(G, C, dtype=torch.float32, device=y.device)
     invstd = torch.empty(G, C, dtype=torch.float32, device=y.device)
     nv = _ptr(_i32(nvalid))
     out = torch.empty_like(y)
-    res = _bf16c(residual) if residual is not None else None
+    res = _act(residual, y.dtype, "bn residual") if residual is not None else None
     if N * H * W <= _BN_SMALL_ROWS:
         # one launch: a block owns 8 channels of a replica for all its rows
         _call("dba_bn_small_fwd", y.data_ptr(), nv, G, N, H * W, C, gamma.data_ptr(), beta.data_ptr(),
               rmean.data_ptr(), rvar.data_ptr(), ps, float(momentum), float(eps), _ptr(res), int(relu),
-              out.data_ptr(), mean.data_ptr(), invstd.data_ptr(), _stream())
+              out.data_ptr(), mean.data_ptr(), invstd.data_ptr(), f32, _stream())
         return out, mean, invstd
     nblk = _L.dba_bn_partial_blocks(N, H * W, C)
     part = torch.empty(G * nblk * 2 * C, dtype=torch.float32, device=y.device)
     _call("dba_bn_stats", y.data_ptr(), nv, G, N, H * W, C, part.data_ptr(), rmean.data_ptr(), rvar.data_ptr(), ps,
-          float(momentum), float(eps), mean.data_ptr(), invstd.data_ptr(), _stream())
+          float(momentum), float(eps), mean.data_ptr(), invstd.data_ptr(), f32, _stream())
     _call("dba_bn_apply", y.data_ptr(), mean.data_ptr(), invstd.data_ptr(), gamma.data_ptr(), beta.data_ptr(), ps,
-          _ptr(res), int(relu), out.data_ptr(), nv, G, N, H * W, C, _stream())
+          _ptr(res), int(relu), out.data_ptr(), nv, G, N, H * W, C, f32, _stream())
     return out, mean, invstd
 
 
 def bn_train_bwd(dout, y, out, mean, invstd, gamma, nvalid, relu, dgamma, dbeta, want_dres=False):
-    dout = _bf16c(dout)
+    y = _act(y, None, "bn input")
+    dout = _act(dout, y.dtype, "bn dout")
+    out = _act(out, y.dtype, "bn output")
     G, N, H, W, C = y.shape
+    _bn_layout(C)
+    f32 = _f32(y)
     ps = _same_stride(gamma)
     gs = _same_stride(dgamma, dbeta)
     dy = torch.empty_like(y)
@@ -429,85 +566,90 @@ def bn_train_bwd(dout, y, out, mean, invstd, gamma, nvalid, relu, dgamma, dbeta,
     if N * H * W <= _BN_SMALL_ROWS:
         _call("dba_bn_small_bwd", dout.data_ptr(), out.data_ptr(), y.data_ptr(), mean.data_ptr(), invstd.data_ptr(),
               gamma.data_ptr(), ps, int(relu), dgamma.data_ptr(), dbeta.data_ptr(), gs, dy.data_ptr(), _ptr(dres),
-              _ptr(_i32(nvalid)), G, N, H * W, C, _stream())
+              _ptr(_i32(nvalid)), G, N, H * W, C, f32, _stream())
         return (dy, dres) if want_dres else dy
     nblk = _L.dba_bn_partial_blocks(N, H * W, C)
     part = torch.empty(G * (nblk + 1) * 2 * C, dtype=torch.float32, device=y.device)
     _call("dba_bn_bwd", dout.data_ptr(), out.data_ptr(), y.data_ptr(), mean.data_ptr(), invstd.data_ptr(),
           gamma.data_ptr(), ps, int(relu), dgamma.data_ptr(), dbeta.data_ptr(), gs, dy.data_ptr(), _ptr(dres),
-          part.data_ptr(), _ptr(_i32(nvalid)), G, N, H * W, C, _stream())
+          part.data_ptr(), _ptr(_i32(nvalid)), G, N, H * W, C, f32, _stream())
     return (dy, dres) if want_dres else dy
 
 
 def relu_mask_bwd(dout, out):
-    dout = _bf16c(dout)
-    out = _bf16c(out)
+    dout = _act(dout, None, "relu dout")
+    out = _act(out, dout.dtype, "relu output")
     din = torch.empty_like(dout)
-    _call("dba_relu_mask_bwd", dout.data_ptr(), out.data_ptr(), din.data_ptr(), dout.numel(), _stream())
+    _call("dba_relu_mask_bwd", dout.data_ptr(), out.data_ptr(), din.data_ptr(), dout.numel(), _f32(dout), _stream())
     return din
 
 
 def bn_fold(w, conv_bias, gamma, beta, rmean, rvar, eps, out_dtype):
     assert w.dtype == torch.float32 and _inner_contig(w)
+    if out_dtype not in (_BF16, _F32):
+        raise TypeError(f"bn_fold: unsupported weight dtype {out_dtype}")
     slots, Cout = w.shape[0], w.shape[1]
     K = int(torch.tensor(w.shape[2:]).prod())
     ss = _same_stride(gamma, beta, rmean, rvar)
-    wf = torch.empty(w.shape, dtype=_BF16, device=w.device)
+    wf = torch.empty(w.shape, dtype=out_dtype, device=w.device)
     bf = torch.empty(slots, Cout, dtype=torch.float32, device=w.device)
     cb = None
     if conv_bias is not None:
         cb = conv_bias
         assert _same_stride(cb) == ss
     _call("dba_bn_fold", w.data_ptr(), w.stride(0), _ptr(cb), gamma.data_ptr(), beta.data_ptr(), rmean.data_ptr(),
-          rvar.data_ptr(), ss, float(eps), wf.data_ptr(), bf.data_ptr(), slots, Cout, K, _stream())
-    return (wf if out_dtype == _BF16 else wf.to(out_dtype)), bf
+          rvar.data_ptr(), ss, float(eps), wf.data_ptr(), bf.data_ptr(), slots, Cout, K, int(out_dtype == _F32),
+          _stream())
+    return wf, bf
 
 
 # --------------------------------------------------------------------------- pooling
 def maxpool2d(x, k, s, p):
-    x = _bf16c(x)
+    x = _act(x, None, "maxpool input")
     G, N, H, W, C = x.shape
     Ho = (H + 2 * p - k) // s + 1
     Wo = (W + 2 * p - k) // s + 1
-    y = torch.empty(G, N, Ho, Wo, C, dtype=_BF16, device=x.device)
+    y = torch.empty(G, N, Ho, Wo, C, dtype=x.dtype, device=x.device)
     ind = torch.empty(G, N, Ho, Wo, C, dtype=torch.int32, device=x.device)
-    _call("dba_maxpool", x.data_ptr(), y.data_ptr(), ind.data_ptr(), G * N, H, W, C, Ho, Wo, k, s, p, _stream())
+    _call("dba_maxpool", x.data_ptr(), y.data_ptr(), ind.data_ptr(), G * N, H, W, C, Ho, Wo, k, s, p, _f32(x),
+          _stream())
     return y, ind
 
 
 def maxpool2d_bwd(dy, ind, in_shape, k, s, p):
-    dy = _bf16c(dy)
+    dy = _act(dy, None, "maxpool dy")
     G, N, H, W, C = in_shape
     Ho, Wo = dy.shape[2], dy.shape[3]
-    dx = torch.empty(G, N, H, W, C, dtype=_BF16, device=dy.device)
-    _call("dba_maxpool_bwd", dy.data_ptr(), ind.data_ptr(), dx.data_ptr(), G * N, H, W, C, Ho, Wo, k, s, p, _stream())
+    dx = torch.empty(G, N, H, W, C, dtype=dy.dtype, device=dy.device)
+    _call("dba_maxpool_bwd", dy.data_ptr(), ind.data_ptr(), dx.data_ptr(), G * N, H, W, C, Ho, Wo, k, s, p, _f32(dy),
+          _stream())
     return dx
 
 
 def avgpool_global(x):
-    x = _bf16c(x)
+    x = _act(x, None, "avgpool input")
     G, N, H, W, C = x.shape
-    y = torch.empty(G, N, 1, 1, C, dtype=_BF16, device=x.device)
-    _call("dba_avgpool", x.data_ptr(), y.data_ptr(), G * N, H * W, C, _stream())
+    y = torch.empty(G, N, 1, 1, C, dtype=x.dtype, device=x.device)
+    _call("dba_avgpool", x.data_ptr(), y.data_ptr(), G * N, H * W, C, _f32(x), _stream())
     return y
 
 
 def avgpool_global_bwd(dy, hw):
-    dy = _bf16c(dy)
+    dy = _act(dy, None, "avgpool dy")
     G, N = dy.shape[:2]
     C = dy.shape[-1]
     H, W = hw
-    dx = torch.empty(G, N, H, W, C, dtype=_BF16, device=dy.device)
-    _call("dba_avgpool_bwd", dy.data_ptr(), dx.data_ptr(), G * N, H * W, C, _stream())
+    dx = torch.empty(G, N, H, W, C, dtype=dy.dtype, device=dy.device)
+    _call("dba_avgpool_bwd", dy.data_ptr(), dx.data_ptr(), G * N, H * W, C, _f32(dy), _stream())
     return dx
 
 
 # --------------------------------------------------------------------------- dropout
 def dropout(x, p, seeds, salt):
-    x = x.contiguous()
+    x = _act(x, None, "dropout input")
     y = torch.empty_like(x)
     G = x.shape[0]
-    _call("dba_dropout", x.data_ptr(), y.data_ptr(), int(x.dtype == torch.float32), _i32(seeds).data_ptr(),
+    _call("dba_dropout", x.data_ptr(), y.data_ptr(), _f32(x), _i32(seeds).data_ptr(),
           int(salt) & 0xFFFFFFFF, float(p), x.numel() // G, G, _stream())
     return y
 
@@ -517,12 +659,19 @@ def dropout_bwd(dy, p, seeds, salt):
 
 
 # ---------------------------------------------------------------------------- loss
-def softmax_xent(logits, labels, mean, want_grad, stats=None, slot=None, nvalid=None):
-    lf = logits.float().contiguous()
+def softmax_xent(logits, labels, mean, want_grad, stats=None, slot=None, nvalid=None, grad_dtype=None):
+    """``grad_dtype``: dtype of dlogits (the compute dtype of the backward pass; bf16 if
+    unset)."""
+    if logits.dtype != _F32:
+        raise TypeError("softmax_xent: logits must be fp32 (the final layer emits fp32)")
+    lf = logits.contiguous()
     G, B, C = lf.shape
+    gdt = grad_dtype or _BF16
+    if gdt not in (_BF16, _F32):
+        raise TypeError(f"softmax_xent: unsupported grad dtype {gdt}")
     loss = torch.empty(G, dtype=torch.float32, device=lf.device)
     correct = torch.empty(G, dtype=torch.float32, device=lf.device)
-    dl = torch.empty(G, B, C, dtype=_BF16, device=lf.device) if want_grad else None
+    dl = torch.empty(G, B, C, dtype=gdt, device=lf.device) if want_grad else None
     sp, ss, slp, ms, nvp = None, 0, None, 0, None
     if stats is not None:
         assert stats.dtype == torch.float32 and stats.is_contiguous() and stats.shape[0] == 3
@@ -531,7 +680,7 @@ def softmax_xent(logits, labels, mean, want_grad, stats=None, slot=None, nvalid=
         slot_, nv_ = _i32(slot), _i32(nvalid)
         sp, ss, slp, nvp = stats.data_ptr(), stats.shape[1], slot_.data_ptr(), nv_.data_ptr()
     _call("dba_softmax_xent", lf.data_ptr(), _i32(labels).data_ptr(), G, B, C, int(bool(mean)), _ptr(dl),
-          loss.data_ptr(), correct.data_ptr(), sp, ss, slp, ms, nvp, _stream())
+          loss.data_ptr(), correct.data_ptr(), sp, ss, slp, ms, nvp, int(gdt == _F32), _stream())
     return loss, correct, dl
 
 

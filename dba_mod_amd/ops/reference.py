@@ -295,8 +295,11 @@ def dropout_bwd(dy: Tensor, p: float, seeds: Tensor, salt: int) -> Tensor:
 # ---------------------------------------------------------------------------- loss
 def softmax_xent(logits: Tensor, labels: Tensor, mean: bool, want_grad: bool,
                  stats: Optional[Tensor] = None, slot: Optional[Tensor] = None,
-                 nvalid: Optional[Tensor] = None) -> Tuple[Tensor, Tensor, Optional[Tensor]]:
+                 nvalid: Optional[Tensor] = None, grad_dtype: Optional[torch.dtype] = None
+                 ) -> Tuple[Tensor, Tensor, Optional[Tensor]]:
     """Per-group CE (mean over valid rows or sum) + correct count + dlogits (K9).
+
+    ``grad_dtype``: dtype of dlogits (default: the logits' dtype).
 
     Rows with label < 0 are padding.  dlogits corresponds to the *mean* loss when
     ``mean`` (training) and to the sum otherwise.  With ``stats`` ([3, G*max_slots] fp32),
@@ -321,7 +324,7 @@ def softmax_xent(logits: Tensor, labels: Tensor, mean: bool, want_grad: bool,
         dl = torch.where(valid[..., None], dl, torch.zeros_like(dl))
         if mean:
             dl = dl / cnt[:, None, None]
-        dl = dl.to(logits.dtype)
+        dl = dl.to(grad_dtype or logits.dtype)
     if stats is not None:
         accumulate_step_stats(stats, slot, loss, correct, nvalid)
     return loss, correct, dl
