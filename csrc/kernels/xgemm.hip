@@ -38,6 +38,19 @@ __device__ __forceinline__ uint32_t cvt_pk(float a, float b) {
   return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2v){a, b}, bf16x2v));
 }
 
+// bounds-checked loads: a raw buffer load whose byte offset is past num_records returns zeros,
+// so out-of-image taps and past-K columns need no branch (offset kOOB)
+constexpr int kOOB = (int)0x80000000;
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* base, long long bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ float4 bload4(__amdgpu_buffer_rsrc_t r, int byte_off) {
+  return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, 0));
+}
+__device__ __forceinline__ float bload1(__amdgpu_buffer_rsrc_t r, int byte_off) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, byte_off, 0, 0));
+}
+
 // 4 fp32 values -> P bf16 planes (4 bf16 = 8 bytes each)
 template <int P>
 __device__ __forceinline__ void split4(float a, float b, float c, float d, uint2 (&o)[P]) {
@@ -73,11 +86,16 @@ __device__ __forceinline__ int pswz(int n) {
 }
 
 // one 32-deep reduction step of a wave's MI x NJ block of 32x32 tiles from an LDS image:
-// A rows [arow0, arow0 + 32 MI) of the region at row offset AOFF (RA rows), B rows likewise.
-template <int MI, int NJ, int P, bool ROWPERM, int RA, int RB>
+// A rows [arow0, arow0 + 32 MI) of the region at row offset 0 (RA rows), B rows at RA + ...
+// ``fill(q)`` (q = 0 .. NQ-1) is staging work of the NEXT step (split + LDS stores of one
+// 4-element quarter per call), spread evenly between the MFMAs so the VALU split and the
+// ds_write traffic issue in the MFMA gaps instead of after them.
+template <int MI, int NJ, int P, bool ROWPERM, int RA, int RB, int NQ, typename Fill>
 __device__ __forceinline__ void mma_step(const uint4* __restrict__ L, int PL, int arow0, int brow0,
-                                         f32x16_t (&acc)[MI][NJ], int lane) {
+                                         f32x16_t (&acc)[MI][NJ], int lane, Fill&& fill) {
+  constexpr int T = 2 * P * (P + 1) / 2 * MI * NJ;   // MFMAs per step
   const int fr = lane & 31, hf = lane >> 5;
+  int cnt = 0, q = 0;
 #pragma unroll
   for (int kk = 0; kk < 2; ++kk) {
     const int ch = kk * 2 + hf;
@@ -104,9 +122,13 @@ __device__ __forceinline__ void mma_step(const uint4* __restrict__ L, int PL, in
 #pragma unroll
         for (int i = 0; i < MI; ++i)
 #pragma unroll
-          for (int j = 0; j < NJ; ++j)
+          for (int j = 0; j < NJ; ++j) {
             acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[pa][i], bfr[s - pa][j], acc[i][j], 0, 0, 0);
+            ++cnt;
+            if (q < NQ && cnt * NQ >= (q + 1) * T) fill(q++);   // constant-folded after unrolling
+          }
   }
+  while (q < NQ) fill(q++);
 }
 
 // store the P planes of 4 consecutive reduction elements (8-B slot q of logical row n)
@@ -184,24 +206,29 @@ __global__ __launch_bounds__(256) void xconv_kernel(const XArgs a) {
     orow[tid] = o;
   }
   // the thread's A rows (source pixel bases) and B rows (weight rows)
-  int aimg[RA], ah[RA], aw[RA];
+  // 32-bit element offsets (a replica's source is < 2^31 elements: checked on the host); an
+  // invalid row gets an out-of-range ah so the bounds test alone zero-fills it
+  int abase[RA], ah[RA], aw[RA];
 #pragma unroll
   for (int i = 0; i < RA; ++i) {
     const int m = m0 + r0 + 32 * i;
-    aimg[i] = -1; ah[i] = 0; aw[i] = 0;
+    abase[i] = 0; ah[i] = -(1 << 20); aw[i] = 0;
     if (m < Mv) {
       const int img = m / HqWq, rem = m - img * HqWq, p = rem / c.Wq, q = rem - p * c.Wq;
-      aimg[i] = img;
       ah[i] = p * a.sp + c.bh;
       aw[i] = q * a.sp + c.bw;
+      abase[i] = ((img * a.Hs + ah[i]) * a.Ws + aw[i]) * Cs;
     }
   }
-  const float* brow[RB];
+  // B rows: element offsets within the class's weight block (-1: past Ncol)
+  int boffs[RB];
 #pragma unroll
   for (int j = 0; j < RB; ++j) {
     const int n = n0 + r0 + 32 * j;
-    brow[j] = n < a.Ncol ? Bp + (long long)n * K : nullptr;
+    boffs[j] = n < a.Ncol ? n * K : -1;
   }
+  const __amdgpu_buffer_rsrc_t rA = rsrc(src, (long long)a.N * a.Hs * a.Ws * Cs * 4);
+  const __amdgpu_buffer_rsrc_t rB = rsrc(Bp, (long long)a.Ncol * K * 4);
   // reduction state of the thread's quarter: element k = kt*32 + kq*4 is channel kc of tap (ki, kj)
   int ki = 0, kj = 0, kc = 0;
   if (nkt > 0) {
@@ -211,23 +238,22 @@ __global__ __launch_bounds__(256) void xconv_kernel(const XArgs a) {
     ki = t / c.nJ;
     kj = t - ki * c.nJ;
   }
-  float4 ra[RA], rb[RB];
-  auto gload = [&](int kt) {
-    const int kb = kt * 32 + kq * 4;
-    if constexpr (VEC == 4) {
+  // two register stages: the global loads of step kt+2 are in flight while step kt+1 (loaded
+  // one step earlier) is split into the other LDS buffer in the gaps of step kt's MFMAs
+  float4 ra[2][RA], rb[2][RB];
+  auto gload = [&](int st) {   // the step at the current reduction state, then advance it
+    const int kb = (ki * c.nJ + kj) * Cs + kc;   // == kt*32 + kq*4
+    if constexpr (VEC >= 4) {
       const bool kv = ki < c.nI;
       const int dh = a.dsg * ki, dw = a.dsg * kj;
+      const int toff = (dh * a.Ws + dw) * Cs + kc;   // uniform across the rows
 #pragma unroll
       for (int i = 0; i < RA; ++i) {
-        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-        const int h = ah[i] + dh, w = aw[i] + dw;
-        if (kv && aimg[i] >= 0 && (unsigned)h < (unsigned)a.Hs && (unsigned)w < (unsigned)a.Ws)
-          v = *(const float4*)(src + (((long long)aimg[i] * a.Hs + h) * a.Ws + w) * Cs + kc);
-        ra[i] = v;
+        const bool ok = kv && (unsigned)(ah[i] + dh) < (unsigned)a.Hs && (unsigned)(aw[i] + dw) < (unsigned)a.Ws;
+        ra[st][i] = bload4(rA, ok ? (abase[i] + toff) * 4 : kOOB);
       }
 #pragma unroll
-      for (int j = 0; j < RB; ++j)
-        rb[j] = (brow[j] && kb < K) ? *(const float4*)(brow[j] + kb) : make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int j = 0; j < RB; ++j) rb[st][j] = bload4(rB, (boffs[j] >= 0 && kb < K) ? (boffs[j] + kb) * 4 : kOOB);
     } else {
       float va[RA][4], vb[RB][4];
       int ii = ki, jj = kj, cc = kc;
@@ -237,44 +263,46 @@ __global__ __launch_bounds__(256) void xconv_kernel(const XArgs a) {
         const int dh = a.dsg * ii, dw = a.dsg * jj;
 #pragma unroll
         for (int i = 0; i < RA; ++i) {
-          const int h = ah[i] + dh, w = aw[i] + dw;
-          va[i][e] = (kv && aimg[i] >= 0 && (unsigned)h < (unsigned)a.Hs && (unsigned)w < (unsigned)a.Ws)
-                         ? src[(((long long)aimg[i] * a.Hs + h) * a.Ws + w) * Cs + cc]
-                         : 0.f;
+          const bool ok = kv && (unsigned)(ah[i] + dh) < (unsigned)a.Hs && (unsigned)(aw[i] + dw) < (unsigned)a.Ws;
+          va[i][e] = bload1(rA, ok ? (abase[i] + (dh * a.Ws + dw) * Cs + cc) * 4 : kOOB);
         }
 #pragma unroll
-        for (int j = 0; j < RB; ++j) vb[j][e] = (brow[j] && kb + e < K) ? brow[j][kb + e] : 0.f;
+        for (int j = 0; j < RB; ++j) vb[j][e] = bload1(rB, (boffs[j] >= 0 && kb + e < K) ? (boffs[j] + kb + e) * 4 : kOOB);
         if (++cc == Cs) {
           cc = 0;
           if (++jj == c.nJ) { jj = 0; ++ii; }
         }
       }
 #pragma unroll
-      for (int i = 0; i < RA; ++i) ra[i] = make_float4(va[i][0], va[i][1], va[i][2], va[i][3]);
+      for (int i = 0; i < RA; ++i) ra[st][i] = make_float4(va[i][0], va[i][1], va[i][2], va[i][3]);
 #pragma unroll
-      for (int j = 0; j < RB; ++j) rb[j] = make_float4(vb[j][0], vb[j][1], vb[j][2], vb[j][3]);
+      for (int j = 0; j < RB; ++j) rb[st][j] = make_float4(vb[j][0], vb[j][1], vb[j][2], vb[j][3]);
     }
-  };
-  auto advance = [&]() {   // k += 32
+    // k += 32 (Cs % 32 == 0: at most one tap boundary)
     kc += 32;
-    while (kc >= Cs) {
-      kc -= Cs;
-      if (++kj == c.nJ) { kj = 0; ++ki; }
+    if constexpr (VEC == 32) {
+      if (kc >= Cs) {
+        kc -= Cs;
+        if (++kj == c.nJ) { kj = 0; ++ki; }
+      }
+    } else {
+      while (kc >= Cs) {
+        kc -= Cs;
+        if (++kj == c.nJ) { kj = 0; ++ki; }
+      }
     }
   };
-  auto lput = [&](int buf) {
+  // quarter q of stage st -> LDS buffer buf
+  auto lput_q = [&](int buf, int st, int q) {
     uint4* L = lds + buf * P * PL;
-#pragma unroll
-    for (int i = 0; i < RA; ++i) {
-      uint2 s[P];
-      split4<P>(ra[i].x, ra[i].y, ra[i].z, ra[i].w, s);
-      lds_put<P, false, BM>(L, PL, 0, r0 + 32 * i, kq, s);
-    }
-#pragma unroll
-    for (int j = 0; j < RB; ++j) {
-      uint2 s[P];
-      split4<P>(rb[j].x, rb[j].y, rb[j].z, rb[j].w, s);
-      lds_put<P, false, BN>(L, PL, BM, r0 + 32 * j, kq, s);
+    uint2 sp[P];
+    if (q < RA) {
+      split4<P>(ra[st][q].x, ra[st][q].y, ra[st][q].z, ra[st][q].w, sp);
+      lds_put<P, false, BM>(L, PL, 0, r0 + 32 * q, kq, sp);
+    } else {
+      const int j = q - RA;
+      split4<P>(rb[st][j].x, rb[st][j].y, rb[st][j].z, rb[st][j].w, sp);
+      lds_put<P, false, BN>(L, PL, BM, r0 + 32 * j, kq, sp);
     }
   };
 
@@ -287,22 +315,27 @@ __global__ __launch_bounds__(256) void xconv_kernel(const XArgs a) {
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
   if (kt0 < kt1) {
-    gload(kt0);
-    advance();
-    lput(0);
+    // loads past the slice's last step are harmless (past K they zero-fill), so the loop body
+    // has no branches and the accumulators stay in place across iterations
+    gload(0);
+    gload(1);
+#pragma unroll
+    for (int q = 0; q < RA + RB; ++q) lput_q(0, 0, q);
     __syncthreads();
-    int cur = 0;
-    for (int kt = kt0; kt < kt1; ++kt) {
-      const bool more = kt + 1 < kt1;
-      if (more) {
-        gload(kt + 1);   // in flight under this step's MFMAs
-        advance();
-      }
-      mma_step<MI, NJ, P, false, BM, BN>(lds + cur * P * PL, PL, wm * TM, wn * TN, acc, lane);
-      if (more) lput(cur ^ 1);
+    // step kt (offset from kt0 even: LDS buffer 0, successor in register stage 1; odd: swapped)
+    int kt = kt0;
+    for (; kt + 1 < kt1; kt += 2) {
+      gload(0);
+      mma_step<MI, NJ, P, false, BM, BN, RA + RB>(lds, PL, wm * TM, wn * TN, acc, lane,
+                                                  [&](int q) { lput_q(1, 1, q); });
       __syncthreads();
-      cur ^= 1;
+      gload(1);
+      mma_step<MI, NJ, P, false, BM, BN, RA + RB>(lds + P * PL, PL, wm * TM, wn * TN, acc, lane,
+                                                  [&](int q) { lput_q(0, 0, q); });
+      __syncthreads();
     }
+    if (kt < kt1)
+      mma_step<MI, NJ, P, false, BM, BN, 0>(lds, PL, wm * TM, wn * TN, acc, lane, [&](int) {});
   }
 
   // ---- epilogue: fp32 tile through LDS, row-contiguous stores with bias / residual / ReLU
@@ -435,8 +468,8 @@ __global__ __launch_bounds__(256) void xwgrad_kernel(const XWArgs a) {
     xkw[e] = t - xkh[e] * a.KW;
   }
 
-  float dv[4][4], xv[4][4];   // [m][n or k]
-  auto gload = [&](int mt) {
+  float dv[2][4][4], xv[2][4][4];   // [stage][m][n or k]
+  auto gload = [&](int mt, int st) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int m = mt + m4 * 4 + r;
@@ -446,11 +479,11 @@ __global__ __launch_bounds__(256) void xwgrad_kernel(const XWArgs a) {
         if (VEC == 4) {
           float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
           if (mv && dn < a.Cout) v = *(const float4*)(dy + (long long)m * a.Cout + dn);
-          dv[r][0] = v.x; dv[r][1] = v.y; dv[r][2] = v.z; dv[r][3] = v.w;
+          dv[st][r][0] = v.x; dv[st][r][1] = v.y; dv[st][r][2] = v.z; dv[st][r][3] = v.w;
         } else {
 #pragma unroll
           for (int e = 0; e < 4; ++e)
-            dv[r][e] = (mv && dn + e < a.Cout) ? dy[(long long)m * a.Cout + dn + e] : 0.f;
+            dv[st][r][e] = (mv && dn + e < a.Cout) ? dy[(long long)m * a.Cout + dn + e] : 0.f;
         }
       }
       // x (im2col row m)
@@ -467,30 +500,31 @@ __global__ __launch_bounds__(256) void xwgrad_kernel(const XWArgs a) {
         const int h = hb + xkh[0], w = wb + xkw[0];
         if (mv && xkv[0] && (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W)
           v = *(const float4*)(x + (((long long)img * a.H + h) * a.W + w) * a.Cin + xc[0]);
-        xv[r][0] = v.x; xv[r][1] = v.y; xv[r][2] = v.z; xv[r][3] = v.w;
+        xv[st][r][0] = v.x; xv[st][r][1] = v.y; xv[st][r][2] = v.z; xv[st][r][3] = v.w;
       } else {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const int h = hb + xkh[e], w = wb + xkw[e];
-          xv[r][e] = (mv && xkv[e] && (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W)
-                         ? x[(((long long)img * a.H + h) * a.W + w) * a.Cin + xc[e]]
-                         : 0.f;
+          xv[st][r][e] = (mv && xkv[e] && (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W)
+                             ? x[(((long long)img * a.H + h) * a.W + w) * a.Cin + xc[e]]
+                             : 0.f;
         }
       }
     }
   };
-  auto lput = [&](int buf) {
+  // piece q of stage st -> LDS buffer buf: q < 4 transposes dy column e = q, q >= 4 x column q-4
+  auto lput_q = [&](int buf, int st, int q) {
     uint4* L = lds + buf * P * PL;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
+    uint2 sp[P];
+    if (q < 4) {
       if (dact) {
-        uint2 s[P];
-        split4<P>(dv[0][e], dv[1][e], dv[2][e], dv[3][e], s);
-        lds_put<P, true, BNO>(L, PL, 0, dn4 * 4 + e, m4, s);
+        split4<P>(dv[st][0][q], dv[st][1][q], dv[st][2][q], dv[st][3][q], sp);
+        lds_put<P, true, BNO>(L, PL, 0, dn4 * 4 + q, m4, sp);
       }
-      uint2 s[P];
-      split4<P>(xv[0][e], xv[1][e], xv[2][e], xv[3][e], s);
-      lds_put<P, true, BK>(L, PL, BNO, xk4 * 4 + e, m4, s);
+    } else {
+      const int e = q - 4;
+      split4<P>(xv[st][0][e], xv[st][1][e], xv[st][2][e], xv[st][3][e], sp);
+      lds_put<P, true, BK>(L, PL, BNO, xk4 * 4 + e, m4, sp);
     }
   };
 
@@ -502,18 +536,23 @@ __global__ __launch_bounds__(256) void xwgrad_kernel(const XWArgs a) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  gload(mb);
-  lput(0);
+  // rows past the chunk zero-fill, so the loads of the steps past its end are harmless
+  gload(mb, 0);
+  gload(mb + 32, 1);
+#pragma unroll
+  for (int q = 0; q < 8; ++q) lput_q(0, 0, q);
   __syncthreads();
-  int cur = 0;
-  for (int mt = mb; mt < me; mt += 32) {
-    const bool more = mt + 32 < me;
-    if (more) gload(mt + 32);
-    mma_step<MI, NJ, P, true, BNO, BK>(lds + cur * P * PL, PL, wn * TNo, wk * TK, acc, lane);
-    if (more) lput(cur ^ 1);
+  int mt = mb;
+  for (; mt + 32 < me; mt += 64) {
+    gload(mt + 64, 0);
+    mma_step<MI, NJ, P, true, BNO, BK, 8>(lds, PL, wn * TNo, wk * TK, acc, lane, [&](int q) { lput_q(1, 1, q); });
     __syncthreads();
-    cur ^= 1;
+    gload(mt + 96, 1);
+    mma_step<MI, NJ, P, true, BNO, BK, 8>(lds + P * PL, PL, wn * TNo, wk * TK, acc, lane,
+                                          [&](int q) { lput_q(0, 0, q); });
+    __syncthreads();
   }
+  if (mt < me) mma_step<MI, NJ, P, true, BNO, BK, 0>(lds, PL, wn * TNo, wk * TK, acc, lane, [&](int) {});
 
   // acc[i][j][r]: cout row n = n0 + wn*TNo + i*32 + (r&3) + 8*(r>>2) + 4*hf, k col = k0 + wk*TK + j*32 + fr
   const int fr = lane & 31, hf = lane >> 5;
@@ -655,9 +694,12 @@ int xconv_dispatch(const XArgs& a, long long Mmax, int G, int nclass, int vec, h
   const int bn = a.Ncol <= 32 ? 32 : a.Ncol <= 64 ? 64 : 128;
   const long long blocks = (long long)ceil_div(Mmax, 128) * ceil_div(a.Ncol, bn) * G * nclass * a.splitk;
   const int bm = (bn > 32 && blocks < 512) ? 64 : 128;
+  if (vec == 4 && a.Cs % 32 == 0) vec = 32;
   if (planes() == 2) {
+    if (vec == 32) return xconv_tile<2, 32>(a, Mmax, G, nclass, bm, st);
     return vec == 4 ? xconv_tile<2, 4>(a, Mmax, G, nclass, bm, st) : xconv_tile<2, 1>(a, Mmax, G, nclass, bm, st);
   }
+  if (vec == 32) return xconv_tile<3, 32>(a, Mmax, G, nclass, bm, st);
   return vec == 4 ? xconv_tile<3, 4>(a, Mmax, G, nclass, bm, st) : xconv_tile<3, 1>(a, Mmax, G, nclass, bm, st);
 }
 
@@ -727,6 +769,7 @@ DBA_EXPORT int dba_xconv_fwd(const float* x, long long x_gstride, const float* w
                              int Wo, int Cout, int KH, int KW, int stride, int pad, int relu, float* ws,
                              long long ws_floats, void* stream) {
   hipStream_t st = (hipStream_t)stream;
+  if ((long long)N * H * W * Cin >= (1LL << 29)) return -103;   // 32-bit in-replica byte offsets
   const long long M = (long long)N * Ho * Wo;
   const int K = KH * KW * Cin;
   const int vec = (Cin % 4 == 0 && aligned16(x) && aligned16(w) && x_gstride % 4 == 0 && w_sstride % 4 == 0) ? 4 : 1;
@@ -761,6 +804,7 @@ DBA_EXPORT int dba_xconv_dgrad(const float* dy, long long dy_gstride, const floa
                                const int* nvalid, int G, int N, int H, int W, int Cin, int Ho, int Wo, int Cout,
                                int KH, int KW, int stride, int pad, float* ws, long long ws_floats, void* stream) {
   hipStream_t st = (hipStream_t)stream;
+  if ((long long)N * Ho * Wo * Cout >= (1LL << 29)) return -103;   // 32-bit in-replica byte offsets
   const ClassGeom cg = dgrad_classes(H, W, Cin, Cout, KH, KW, stride, pad);
   const int vec = (Cout % 4 == 0 && aligned16(dy) && aligned16(wt) && dy_gstride % 4 == 0 && wt_sstride % 4 == 0) ? 4 : 1;
   XArgs a{};

@@ -62,16 +62,47 @@ def _time(fn, reps, inner=10):
     return e0.elapsed_time(e1) / (reps * inner) * 1e-3
 
 
+def _bench_fp32(name, G, N, Hh, Cin, Cout, k, s, p, reps, dev):
+    """fwd / dgrad / wgrad of the split-bf16 fp32 family; TFLOP/s counts the real fp32 work."""
+    torch.manual_seed(0)
+    x = torch.randn(G, N, Hh, Hh, Cin, device=dev)
+    w = torch.randn(G, Cout, k, k, Cin, device=dev) * 0.05
+    Ho = (Hh + 2 * p - k) // s + 1
+    dy = torch.randn(G, N, Ho, Ho, Cout, device=dev)
+    flops = 2.0 * G * N * Ho * Ho * Cout * k * k * Cin
+    rec = {"shape": name, "dtype": "fp32"}
+    ops = [("fwd", lambda: H.conv2d(x, w, None, s, p, relu=True))]
+    if name.startswith("train"):
+        wt = H.prepare_dgrad_weights(w, [(w, None, s, p, (Hh, Hh), None, G)])[0]
+        dw = torch.zeros(G, Cout, k, k, Cin, device=dev)
+        ops += [("dgrad", lambda: H.conv2d_dgrad(dy, w, None, s, p, (Hh, Hh), wt=wt)),
+                ("wgrad", lambda: H.conv2d_wgrad(dy, x, s, p, k, k, dw))]
+    for tag, fn in ops:
+        t = _time(fn, reps)
+        rec[tag + "_us"] = round(t * 1e6, 1)
+        rec[tag + "_tflops"] = round(flops / t / 1e12, 1)
+    return rec
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--json", default=None)
     ap.add_argument("--only", default="", help="substring filter on shape names")
+    ap.add_argument("--dtype", choices=("bf16", "fp32"), default="bf16",
+                    help="fp32: the reference-precision family (xgemm.hip)")
+    ap.add_argument("--planes", type=int, default=3, help="fp32 split planes (2 or 3)")
     args = ap.parse_args(argv)
     dev = torch.device("cuda")
     rows = []
+    if args.dtype == "fp32":
+        H.set_fp32_planes(args.planes)
     for name, G, N, Hh, Cin, Cout, k, s, p in SHAPES:
         if args.only not in name:
+            continue
+        if args.dtype == "fp32":
+            rows.append(_bench_fp32(name, G, N, Hh, Cin, Cout, k, s, p, args.reps, dev))
+            print(json.dumps(rows[-1]), flush=True)
             continue
         torch.manual_seed(0)
         x = torch.randn(G, N, Hh, Hh, Cin, device=dev).bfloat16()
