@@ -703,17 +703,20 @@ int xconv_dispatch(const XArgs& a, long long Mmax, int G, int nclass, int vec, h
   return vec == 4 ? xconv_tile<3, 4>(a, Mmax, G, nclass, bm, st) : xconv_tile<3, 1>(a, Mmax, G, nclass, bm, st);
 }
 
-// split-K factor of a forward launch (1 = none): enough K slices to reach ~256 blocks with
-// at least 4 k-tiles each
-int xsplitk(long long M, int G, int Ncol, int K) {
+// split-K factor of a forward launch (1 = none).  Decided from the PER-REPLICA geometry only
+// (never from the group count G): the K-slicing sets the summation order, so a client's
+// bits must not depend on how many other clients share its launch (world-1 vs world-N runs
+// place different client groups on a rank).  Splits a replica below ~64 tiles (a lone
+// client's stage-3/4 convs) into slabs of >= 8 k-steps.
+int xsplitk(long long M, int /*G*/, int Ncol, int K) {
   static const int off = env_int("DBA_F32_SPLITK", 1) == 0;
   if (off) return 1;
   const int bn = Ncol <= 32 ? 32 : Ncol <= 64 ? 64 : 128;
-  const long long blocks = (long long)ceil_div(M, 64) * ceil_div(Ncol, bn) * G;
-  if (blocks >= 128) return 1;
+  const long long tiles = (long long)ceil_div(M, 64) * ceil_div(Ncol, bn);
+  if (tiles >= 64) return 1;
   const int nkt = (K + 31) / 32;
-  int s = (int)std::min<long long>(8, (256 + blocks - 1) / blocks);
-  while (s > 1 && nkt / s < 4) --s;
+  int s = (int)std::min<long long>(8, (64 + tiles - 1) / tiles);
+  while (s > 1 && nkt / s < 8) --s;
   return s;
 }
 
@@ -858,12 +861,14 @@ DBA_EXPORT int dba_xtranspose(const void* desc, int n, int slots, long long max_
 }
 
 // slab floats dba_xwgrad needs for this shape (0: accumulates straight into dw)
+// The m-chunking (Z slabs) is decided from the PER-REPLICA geometry only (see xsplitk): ~128
+// blocks per replica, chunks of >= 256 rows.
 DBA_EXPORT long long dba_xwgrad_ws_floats(int G, int N, int Ho, int Wo, int Cin, int Cout, int KH, int KW, int* mchunk_out) {
   const int K = KH * KW * Cin;
   const int bno = Cout <= 32 ? 32 : Cout <= 64 ? 64 : 128;
-  const long long tiles = (long long)ceil_div(Cout, bno) * ceil_div(K, 128) * G;
+  const long long tiles = (long long)ceil_div(Cout, bno) * ceil_div(K, 128);
   const long long M = (long long)N * Ho * Wo;
-  const int target = env_int("DBA_F32_WGRAD_BLOCKS", 768);
+  const int target = env_int("DBA_F32_WGRAD_BLOCKS", 128);
   long long Z = std::max(1LL, std::min((target + tiles - 1) / tiles, M / 256));
   int mchunk = (int)((M + Z - 1) / Z);
   mchunk = (mchunk + 31) / 32 * 32;

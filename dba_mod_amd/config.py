@@ -101,7 +101,9 @@ _DEFAULTS: Dict[str, Any] = {
     "graph_capture": True,         # HIP-graph the grouped training step on GPU
     "overlap_eval": True,          # evaluate round r on a side stream under round r+1's training
     "early_local_eval": True,      # enqueue a client's local tests as soon as it finishes training
+    "rfa_mode": "auto",            # RFA across ranks: gather | distributed | auto (fewer bytes)
     "pretrain_rounds": 0,          # benign FedAvg warm start when not resuming (Server.pretrain)
+    "pretrain_central_epochs": 0,  # centralised warm start epochs, before any FedAvg warm start
     "nan_check": True,             # abort the run if the aggregated global model is not finite
     "max_update_norm": None,       # RFA update-norm rejection (helper.py:360-369; never enabled there)
     "pretrain_eta": 1.0,

@@ -4,11 +4,13 @@ Inputs are the round's client states ``finals [n, S]`` (or summed gradients for 
 already gathered onto every rank; each rank applies the identical update redundantly, so no
 broadcast is needed and every rank ends the round with a bit-identical global model.
 
-* :func:`fedavg` — reference ``helper.py:240-257``: ``w += (eta/no_models) * sum_i delta_i``
-  (+ N(0, sigma) per element with ``diff_privacy``); unweighted; applied to the BN running
-  stats too (D2).  The int64 ``num_batches_tracked`` counters are not part of the float
+* :func:`fedavg` / :func:`fedavg_apply` — reference ``helper.py:240-257``: ``w += (eta/no_models)
+  * sum_i delta_i`` (+ N(0, sigma) per element with ``diff_privacy``); unweighted; applied to
+  the BN running stats too (D2).  The delta sum is an fp64 HIP reduction, per rank then
+  all-reduced (``Server._aggregate``).  The int64 ``num_batches_tracked`` counters are not part of the float
   bucket (D1: the reference's float→int64 add crashes on modern torch).
-* :func:`geometric_median` — RFA / Weiszfeld, ``helper.py:295-373``: one batched distance
+* :func:`geometric_median` / :func:`geometric_median_distributed` — RFA / Weiszfeld,
+  ``helper.py:295-373`` (the latter with the points resident on their owner ranks): one batched distance
   kernel (all n clients in one pass) and one weighted-sum kernel per iteration; the n
   weights and the stopping test are the only host traffic.  Quirk D5 (``wv`` undefined if
   converged at iteration 0) resolves to the current weights.
@@ -31,8 +33,15 @@ log = logging.getLogger("logger")
 
 def fedavg(global_state: torch.Tensor, finals: torch.Tensor, eta: float, no_models: int,
            dp: bool, sigma: float, seed: int, n_update: int) -> None:
-    """In-place FedAvg; ``n_update`` = number of leading entries aggregated (S or P)."""
-    delta_sum = (finals[:, :n_update] - global_state[None, :n_update]).sum(0)
+    """In-place FedAvg of ``finals`` [n, S]; ``n_update`` = leading entries aggregated (S or P)."""
+    fedavg_apply(global_state, ops.delta_sum(finals[:, :n_update], global_state[:n_update]), eta, no_models,
+                 dp, sigma, seed, n_update)
+
+
+def fedavg_apply(global_state: torch.Tensor, delta_sum: torch.Tensor, eta: float, no_models: int,
+                 dp: bool, sigma: float, seed: int, n_update: int) -> None:
+    """``w += (eta / no_models) * sum_i delta_i (+ noise)`` from the (all-reduced) fp64 sum of the
+    clients' deltas (``ops.delta_sum``: fused HIP kernel on GPU)."""
     ops.add_noise_scaled(global_state[:n_update], delta_sum, eta / no_models, sigma, seed, dp)
 
 
@@ -83,6 +92,68 @@ def geometric_median(global_state: torch.Tensor, finals: torch.Tensor, num_sampl
     return updated, [float(x) for x in wv], final_alphas, calls
 
 
+def geometric_median_distributed(global_state: torch.Tensor, local_finals: torch.Tensor, local_idx: Sequence[int],
+                                 num_samples: Sequence[int], eta: float, maxiter: int, dp: bool, sigma: float,
+                                 seed: int, n_update: int, reduce, eps: float = 1e-5, ftol: float = 1e-6,
+                                 max_update_norm: Optional[float] = None
+                                 ) -> Tuple[bool, List[float], List[float], int]:
+    """Weiszfeld with the client deltas resident on their owner ranks (reference
+    ``helper.py:320-352``): per iteration each rank forms its partial weighted sum of its own
+    points (``reduce`` = all-reduce of the S-vector) and its points' distances to the median
+    (all-reduce of an n-vector with zeros for other ranks' clients).  Same iteration and
+    stopping rule as :func:`geometric_median`."""
+    n = len(num_samples)
+    dev = global_state.device
+    idx = list(local_idx)
+    points = local_finals[:, :n_update] - global_state[None, :n_update] if idx else None
+    a = np.asarray(num_samples, dtype=np.float64)
+    alphas = a / a.sum()
+
+    def avg(w: np.ndarray) -> torch.Tensor:
+        wn = w / w.sum()
+        if idx:
+            part = ops.weighted_sum(points, torch.tensor(wn[idx], dtype=torch.float32, device=dev),
+                                    out_dtype=torch.float64)
+        else:
+            part = torch.zeros(n_update, dtype=torch.float64, device=dev)
+        return reduce(part).float()
+
+    def dists(m: torch.Tensor) -> np.ndarray:
+        full = torch.zeros(n, dtype=torch.float64, device=dev)
+        if idx:
+            full[torch.tensor(idx, device=dev)] = ops.sq_dists(points, m).double()
+        return np.sqrt(np.maximum(reduce(full).cpu().numpy(), 0.0))
+
+    median = avg(alphas)
+    calls = 1
+    d = dists(median)
+    obj = float((alphas * d).sum())
+    wv: Optional[np.ndarray] = None
+    weights = alphas.copy()
+    for i in range(maxiter):
+        prev_obj = obj
+        weights = alphas / np.maximum(eps, d)
+        weights = weights / weights.sum()
+        median = avg(weights)
+        calls += 1
+        d = dists(median)
+        obj = float((alphas * d).sum())
+        if abs(prev_obj - obj) < ftol * obj:
+            break
+        log.info(f"[rfa agg] iter:  {i}, prev_obj_val: {prev_obj}, obj_val: {obj}, abs dis: {abs(prev_obj - obj)}")
+        wv = weights.copy()
+    if wv is None:  # D5
+        wv = weights.copy()
+    upd_norm = float(torch.linalg.vector_norm(median.double()).item())
+    if max_update_norm is None or upd_norm < max_update_norm:
+        ops.add_noise_scaled(global_state[:n_update], median, eta, sigma, seed, dp)
+        updated = True
+    else:
+        log.info(f"\t\t\tUpdate norm = {upd_norm} is too large. Update rejected")
+        updated = False
+    return updated, [float(x) for x in wv], d.tolist(), calls
+
+
 class FoolsGold:
     """FoolsGold with per-client history (reference helper.py:527-607)."""
 
@@ -129,7 +200,16 @@ class FoolsGold:
                   ) -> Tuple[torch.Tensor, np.ndarray, np.ndarray]:
         """grads [n, P] summed client gradients -> (aggregated [P], wv, alpha)."""
         lo, hi = feat_slice
-        feats = grads[:, lo:hi].double().cpu().numpy()
+        wv, alpha = self.weights_from(grads[:, lo:hi], names)
+        wts = torch.tensor(wv / len(names), dtype=torch.float32, device=grads.device)
+        agg = ops.weighted_sum(grads, wts)
+        return agg, wv, alpha
+
+    def weights_from(self, feat_rows: torch.Tensor, names: Sequence[Any]) -> Tuple[np.ndarray, np.ndarray]:
+        """FoolsGold weights from this round's [n, d] final-layer gradient features (the
+        reference's ``client_grads[i][-2]``, ``helper.py:544``): history update, cosine Gram,
+        pardoning, logit.  Deterministic, so every rank computes the same weights."""
+        feats = feat_rows.double().cpu().numpy()
         mem = np.zeros_like(feats)
         for i, nm in enumerate(names):
             key = str(nm)
@@ -139,11 +219,9 @@ class FoolsGold:
                 self.memory_dict[key] = feats[i].copy()
             mem[i] = self.memory_dict[key]
         use = mem if self.use_memory else feats
-        wv, alpha = self.weights(torch.from_numpy(use).to(grads.device, torch.float32))
+        wv, alpha = self.weights(torch.from_numpy(use).to(feat_rows.device, torch.float32))
         self.wv_history.append(wv)
-        wts = torch.tensor(wv / len(names), dtype=torch.float32, device=grads.device)
-        agg = ops.weighted_sum(grads, wts)
-        return agg, wv, alpha
+        return wv, alpha
 
     def state(self) -> Dict[str, Any]:
         return {"memory": {k: torch.from_numpy(v) for k, v in self.memory_dict.items()}}

@@ -103,7 +103,7 @@ class Evaluator:
             ctx = prog.Ctx(wl.spec, None, None, wsel, train=False, folded=folded, nvalid=nval_d[c],
                            act_dtype=self.dtype)
             logits = prog.forward(ctx, x)
-            loss, correct, _ = ops.softmax_xent(logits, y, False, False)
+            loss, correct, _ = ops.softmax_xent(logits, y, False, False, loss_dtype=torch.float64)
             acc[:, 0] += loss.double()
             acc[:, 1] += correct.double()
         acc[:, 2] += to_device([len(a) for a in idx_lists], dev, torch.float64)

@@ -69,6 +69,10 @@ class _EarlyEval:
         longest = max((len(c.steps) for c in plan.clients), default=0)
         self.late = ({c.name for c in plan.clients if len(c.steps) == longest}
                      if server.d.world > 1 else set())
+        # every rank marks the SAME jobs as early (the owner runs them over the whole test
+        # set, the other ranks skip them), so no test image is counted twice in the
+        # cross-rank counter all-reduce
+        self.done = {j for name, js in self.by_client.items() if name not in self.late for j in js}
 
     def __call__(self, client: ClientPlan, snaps: Dict[int, torch.Tensor]) -> None:
         js = self.by_client.get(client.name)
@@ -80,7 +84,6 @@ class _EarlyEval:
         jobs = [dataclasses.replace(self.plan.jobs[j], model=remap[self.plan.jobs[j].model]) for j in js]
         self.server._enqueue_eval(bank, jobs, js, self.acc, sharded=False, stream=self.server._early_stream)
         self.keep.append(bank)
-        self.done.update(js)
 
 
 def compute_dtype_for(params: C.Params, device: torch.device) -> torch.dtype:
@@ -158,6 +161,9 @@ class Server:
             with open(os.path.join(self.folder, "params.yaml"), "w") as f:
                 yaml.safe_dump(params.to_plain(), f)
         self.last_round: Dict[str, Any] = {}
+        if not params["resumed_model"] and int(params["pretrain_central_epochs"]) > 0:
+            plr = params["pretrain_lr"]
+            self.pretrain_central(int(params["pretrain_central_epochs"]), float(plr) if plr is not None else None)
         if not params["resumed_model"] and int(params["pretrain_rounds"]) > 0:
             plr = params["pretrain_lr"]
             self.pretrain(int(params["pretrain_rounds"]), float(params["pretrain_eta"]),
@@ -188,6 +194,7 @@ class Server:
         self.global_state = flat.to(self.device)
         if self.d.enabled:   # identical by construction; make it bit-identical anyway
             self.d.broadcast_(self.global_state, 0)
+        self.init_comm_bytes = self.d.take_bytes()   # one-time; rounds report their own
 
     def pretrain(self, rounds: int, eta: float = 1.0, lr: Optional[float] = None) -> None:
         """Benign FedAvg warm start: ``rounds`` clean rounds (no attackers, no evaluation,
@@ -220,7 +227,42 @@ class Server:
             torch.cuda.synchronize(self.device)
         log.info(f"pretrained {rounds} benign rounds (eta {eta}, lr {lr if lr is not None else p['lr']})")
 
-    # ------------------------------------------------------------------ round
+    def pretrain_central(self, epochs: int, lr: Optional[float] = None) -> None:
+        """Centralised warm start: ``epochs`` passes of one pseudo-client holding the WHOLE
+        training set (no attackers, no evaluation, no CSV rows), then the global model takes
+        its weights.  This is how the reference's resumed checkpoints were made (e.g.
+        ``tiny_64_pretrain/tiny-resnet.epoch_20``: 20 centralised epochs, ``utils/
+        tiny_params.yaml``), and it is the only practical warm start when the federated split
+        is very non-IID (Tiny: 200 Dirichlet clients at alpha 0.01 hold ~1-2 classes each).
+        On N ranks every rank trains the same pseudo-client (identical by construction)."""
+        if epochs <= 0:
+            return
+        p = self.params
+        wl = self.wl
+        name = "__central__"
+        wl.client_indices[name] = np.arange(int(wl.train_store.labels.numel()), dtype=np.int64)
+        wl.client_sizes[name] = int(wl.client_indices[name].shape[0])
+        saved = {k: p[k] for k in ("is_poison", "eta", "aggregation_methods", "lr", "internal_epochs", "no_models")}
+        p.update({"is_poison": False, "eta": 1.0, "aggregation_methods": C.AGGR_MEAN, "internal_epochs": int(epochs),
+                  "no_models": 1})
+        if lr is not None:
+            p["lr"] = float(lr)
+        world = self.d.world
+        try:
+            plan = build_round_plan(p, wl, 1, [name], [])
+            handle = self.trainer.train_async(plan.clients, self.global_state)
+            res = handle.collect()
+            self.global_state.copy_(res[0].snapshots[plan.clients[0].final_snap])
+        finally:
+            p.update(saved)
+            self.timer.reset()
+            del wl.client_indices[name]
+            del wl.client_sizes[name]
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+        log.info(f"central warm start: {epochs} epochs over {len(plan.clients[0].steps)} steps "
+                 f"(lr {lr if lr is not None else p['lr']}, {world} rank(s))")
+
     # ------------------------------------------------------------------ round
     # A round is split in two halves so consecutive rounds can overlap on the GPU:
     #   _train_half(r): select -> plan -> train -> gather -> aggregate   (training stream)
@@ -248,7 +290,7 @@ class Server:
         with self.timer.phase("train_enqueue", sync=False):
             handle = self.trainer.train_async(mine, self.global_state, on_client_done=early)
         return {"epoch": epoch, "plan": plan, "owners": owners, "adversarial": adversarial, "t0": t0,
-                "handle": handle, "early": early, "clients_on_rank": len(mine)}
+                "handle": handle, "early": early, "clients_on_rank": len(mine), "evaluate": evaluate}
 
     def _train_end(self, st: Dict[str, Any]) -> Dict[str, Any]:
         """Wait for the round's training, gather the snapshots, aggregate."""
@@ -262,16 +304,17 @@ class Server:
         if self.trainer.trace and self.write:
             self._plot_batches(plan, results)
         with self.timer.phase("gather"):
-            bank, fg_grads, cstats = self._gather(plan, st["owners"], results)
+            bank, local, cstats = self._gather(plan, st["owners"], results, early, st.get("evaluate", True))
         with self.timer.phase("aggregate"):
-            self._aggregate(plan, bank, fg_grads, st["adversarial"])
+            self._aggregate(plan, bank, local, st["adversarial"])
             bank[0].copy_(self.global_state)
             if p["nan_check"] and not bool(torch.isfinite(self.global_state).all()):
                 # fail fast: a non-finite global model poisons every later round
                 raise FloatingPointError(f"round {epoch}: aggregated global model is not finite "
                                          f"(aggregation={p['aggregation_methods']})")
         return {"epoch": epoch, "plan": plan, "bank": bank, "cstats": cstats, "t0": st["t0"],
-                "clients_on_rank": st["clients_on_rank"], "phases": self.timer.reset(), "early": early}
+                "clients_on_rank": st["clients_on_rank"], "phases": self.timer.reset(), "early": early,
+                "comm_bytes": self.d.take_bytes()}
 
     def _train_half(self, epoch: int, evaluate: bool = True) -> Dict[str, Any]:
         return self._train_end(self._train_begin(epoch, evaluate))
@@ -331,6 +374,9 @@ class Server:
                 torch.cuda.current_stream(self.device).wait_event(pend[ev])
         self.d.all_reduce_(acc)
         res = acc.cpu().numpy()
+        comm = dict(pend.get("comm_bytes", {}))
+        for k, v in self.d.take_bytes().items():
+            comm[k] = comm.get(k, 0) + v
         t_io = time.perf_counter()
         summary = self._record(pend["plan"], res, pend["cstats"])
         self._save_model(pend["epoch"], summary["val_loss"], pend["bank"][0])
@@ -340,7 +386,8 @@ class Server:
         phases["eval_wait"] = t_io - t_wait
         phases["io"] = now - t_io
         summary.update({"epoch": pend["epoch"], "round_s": now - pend["t0"], "phases": phases,
-                        "clients_on_rank": pend["clients_on_rank"], "backend": ops.backend_name(self.device)})
+                        "clients_on_rank": pend["clients_on_rank"], "backend": ops.backend_name(self.device),
+                        "comm_bytes": comm})
         self.metrics.emit(summary)
         log.info(f"Done in {now - pend['t0']} sec.")
         self.last_round = summary
@@ -406,9 +453,29 @@ class Server:
         log.info(v)
         return float(v)
 
-    def _gather(self, plan: RoundPlan, owners: List[int], results: List[ClientResult]
-                ) -> Tuple[torch.Tensor, Optional[torch.Tensor], Dict[Any, Dict[str, Any]]]:
-        """All snapshots + FoolsGold grads + per-client stats onto every rank."""
+    def _rfa_gather(self, n_clients: int) -> bool:
+        """RFA on the gathered final states (True) or distributed Weiszfeld (False).  Per rank,
+        a ring all-gather of the n final states moves ~n*S*4 bytes, distributed Weiszfeld
+        ~(maxiter+1) * 2 * (S*4 + n*8): it pays only above ~2 (maxiter+1) clients per round
+        (the reference configs run 10 clients with maxiter 10 -> gather)."""
+        mode = str(self.params["rfa_mode"]).lower()
+        if mode not in ("auto", "gather", "distributed"):
+            raise ValueError(f"rfa_mode {mode!r}: expected auto | gather | distributed")
+        if self.d.world == 1 or mode == "gather":
+            return True
+        if mode == "distributed":
+            return False
+        return n_clients <= 2 * (int(self.params["geom_median_maxiter"]) + 1)
+
+    def _gather(self, plan: RoundPlan, owners: List[int], results: List[ClientResult],
+                early: Optional["_EarlyEval"], evaluate: bool
+                ) -> Tuple[torch.Tensor, Dict[str, Any], Dict[Any, Dict[str, Any]]]:
+        """Snapshot bank + this rank's aggregation inputs + per-client scalars on every rank.
+
+        Client snapshots stay on their owner rank.  Only the rows some other rank reads are
+        all-gathered: the snapshots of clients whose tests are image-sharded across ranks
+        (the round's longest clients, or every client without early local tests) and, for
+        RFA in gather mode, the final states.  Aggregation itself reduces (``_aggregate``)."""
         S, P = self.spec.S, self.spec.P
         world, rank = self.d.world, self.d.rank
         by_name = {r.name: r for r in results}
@@ -418,36 +485,48 @@ class Server:
                 for s in (ph.pre_scale_snap, ph.post_snap):
                     if s is not None:
                         slot_owner[s] = o
-        per_rank = [[s for s in sorted(slot_owner) if slot_owner[s] == r] for r in range(world)]
-        k_max = max(1, max(len(x) for x in per_rank))
-        local_rows = []
-        for s in per_rank[rank]:
-            for r in results:
-                if s in r.snapshots:
-                    local_rows.append(r.snapshots[s])
-                    break
-        local = torch.stack(local_rows) if local_rows else torch.zeros(0, S, device=self.device)
         bank = torch.zeros(plan.n_snapshots, S, dtype=torch.float32, device=self.device)
+        local_snaps: Dict[int, torch.Tensor] = {}
+        for r in results:
+            local_snaps.update(r.snapshots)
         if world == 1:
-            for i, s in enumerate(per_rank[0]):
-                bank[s] = local[i]
+            for s, t in local_snaps.items():
+                bank[s] = t
         else:
-            allrows = self.d.all_gather_rows(local, k_max)
-            for r in range(world):
-                for i, s in enumerate(per_rank[r]):
-                    bank[s] = allrows[r * k_max + i]
-        fg_grads = None
+            shared: set = set()
+            if evaluate:
+                done_early = early.done if early is not None else set()
+                shared.update(plan.jobs[j].model for j in range(len(plan.jobs))
+                              if j not in done_early and plan.jobs[j].model != 0)
+            if (self.params["aggregation_methods"] == C.AGGR_GEO_MED and self._rfa_gather(len(plan.clients))):
+                shared.update(c.final_snap for c in plan.clients)
+            per_rank = [[s for s in sorted(shared) if slot_owner[s] == r] for r in range(world)]
+            k_max = max(len(x) for x in per_rank)
+            for s, t in local_snaps.items():
+                bank[s] = t
+            if k_max > 0:
+                local = (torch.stack([local_snaps[s] for s in per_rank[rank]]) if per_rank[rank]
+                         else torch.zeros(0, S, device=self.device))
+                allrows = self.d.all_gather_rows(local, k_max)
+                for r in range(world):
+                    if r == rank:
+                        continue
+                    for i, s in enumerate(per_rank[r]):
+                        bank[s] = allrows[r * k_max + i]
+        mine = [i for i, c in enumerate(plan.clients) if c.name in by_name]
+        local_in: Dict[str, Any] = {
+            "idx": mine,
+            "finals": (torch.stack([local_snaps[plan.clients[i].final_snap] for i in mine]) if mine
+                       else torch.zeros(0, S, device=self.device)),
+            "fg": ({i: by_name[plan.clients[i].name].fg_grad for i in mine}
+                   if self.params["aggregation_methods"] == C.AGGR_FOOLSGOLD else None),
+        }
+        # per-client scalars: stats [max_slots, 3] + scale distances [interval] (one small all-reduce)
         n = len(plan.clients)
-        if self.params["aggregation_methods"] == C.AGGR_FOOLSGOLD:
-            fg_grads = torch.zeros(n, P, dtype=torch.float32, device=self.device)
-            for i, c in enumerate(plan.clients):
-                if c.name in by_name:
-                    fg_grads[i] = by_name[c.name].fg_grad
-            self.d.all_reduce_(fg_grads)
-        # per-client scalars: stats [max_slots, 3] + scale distances [interval]
         max_slots = max(sum(ph.internal_epochs for ph in c.phases) for c in plan.clients)
         interval = int(self.params["aggr_epoch_interval"])
-        W = max_slots * 3 + interval
+        W = max_slots * 3 + interval * 5
+        o_n = max_slots * 3 + interval
         sc = torch.zeros(n, W, dtype=torch.float64)
         for i, c in enumerate(plan.clients):
             r = by_name.get(c.name)
@@ -457,6 +536,9 @@ class Server:
             sc[i, :st.numel()] = st.reshape(-1)
             for k, ph in enumerate(c.phases):
                 sc[i, max_slots * 3 + k] = r.scale_dist.get(ph.epoch, 0.0)
+                nr = r.scale_norms.get(ph.epoch)
+                if nr is not None:
+                    sc[i, o_n + 4 * k:o_n + 4 * k + 4] = torch.tensor(nr, dtype=torch.float64)
         if self.d.enabled:
             scd = sc.to(self.device)
             self.d.all_reduce_(scd)
@@ -465,35 +547,69 @@ class Server:
         for i, c in enumerate(plan.clients):
             st = sc[i, :max_slots * 3].reshape(max_slots, 3).numpy()
             dists = {ph.epoch: float(sc[i, max_slots * 3 + k]) for k, ph in enumerate(c.phases)}
-            cstats[c.name] = {"stats": st, "dist": dists}
-        return bank, fg_grads, cstats
+            norms = {ph.epoch: tuple(float(v) for v in sc[i, o_n + 4 * k:o_n + 4 * k + 4])
+                     for k, ph in enumerate(c.phases)}
+            cstats[c.name] = {"stats": st, "dist": dists, "norms": norms}
+        return bank, local_in, cstats
 
-    def _aggregate(self, plan: RoundPlan, bank: torch.Tensor, fg_grads: Optional[torch.Tensor],
+    def _reduce(self, t: torch.Tensor) -> torch.Tensor:
+        """Sum ``t`` over ranks through a §5.8-padded flat buffer (no-op at world 1)."""
+        if not self.d.enabled:
+            return t
+        buf = self.d.padded(t.numel(), t.dtype)
+        buf[:t.numel()] = t.reshape(-1)
+        self.d.all_reduce_(buf)
+        return buf[:t.numel()].view(t.shape)
+
+    def _aggregate(self, plan: RoundPlan, bank: torch.Tensor, local: Dict[str, Any],
                    adversarial: List[Any]) -> None:
         p = self.params
         method = p["aggregation_methods"]
         n_upd = self.spec.S if p["aggregate_bn_buffers"] else self.spec.P
-        finals = bank[[c.final_snap for c in plan.clients]]
         names = [c.name for c in plan.clients]
         dp_seed = (int(p["seed"]) * 7919 + plan.epoch) & 0x7FFFFFFF
         if method == C.AGGR_MEAN:
-            agg.fedavg(self.global_state, finals, float(p["eta"]), int(p["no_models"]),
-                       bool(p["diff_privacy"]), float(p["sigma"]), dp_seed, n_upd)
+            # each rank sums its own clients' deltas (fp64), one all-reduce of S values
+            part = ops.delta_sum(local["finals"][:, :n_upd], self.global_state[:n_upd])
+            agg.fedavg_apply(self.global_state, self._reduce(part), float(p["eta"]), int(p["no_models"]),
+                             bool(p["diff_privacy"]), float(p["sigma"]), dp_seed, n_upd)
         elif method == C.AGGR_GEO_MED:
             ns = [c.num_samples for c in plan.clients]
             self._log_poison_ratio("rfa", names, ns)
             mun = p["max_update_norm"]
-            updated, wv, alphas, calls = agg.geometric_median(
-                self.global_state, finals, ns, float(p["eta"]), int(p["geom_median_maxiter"]),
-                bool(p["diff_privacy"]), float(p["sigma"]), dp_seed, n_upd,
-                max_update_norm=float(mun) if mun is not None else None)
+            kw = dict(max_update_norm=float(mun) if mun is not None else None)
+            if self._rfa_gather(len(plan.clients)):
+                finals = bank[[c.final_snap for c in plan.clients]]
+                updated, wv, alphas, calls = agg.geometric_median(
+                    self.global_state, finals, ns, float(p["eta"]), int(p["geom_median_maxiter"]),
+                    bool(p["diff_privacy"]), float(p["sigma"]), dp_seed, n_upd, **kw)
+            else:
+                updated, wv, alphas, calls = agg.geometric_median_distributed(
+                    self.global_state, local["finals"], local["idx"], ns, float(p["eta"]),
+                    int(p["geom_median_maxiter"]), bool(p["diff_privacy"]), float(p["sigma"]), dp_seed, n_upd,
+                    reduce=self._reduce, **kw)
             self.csv.add_weight_result(names, wv, alphas)
             self._plot_weights(names, wv, alphas, adversarial, plan.epoch)
         elif method == C.AGGR_FOOLSGOLD:
             ns = [c.num_samples for c in plan.clients]
             self._log_poison_ratio("foolsgold", names, ns)
             t0 = time.time()
-            agg_grad, wv, alpha = self.fg.aggregate(fg_grads, names, self.spec.fg_feature_slice())
+            lo, hi = self.spec.fg_feature_slice()
+            n = len(plan.clients)
+            feats = torch.zeros(n, hi - lo, dtype=torch.float32, device=self.device)
+            for i, g in local["fg"].items():
+                feats[i] = g[lo:hi]
+            # ONE all-reduce of the [n, d] features (each row owned by one rank: exact)
+            wv, alpha = self.fg.weights_from(self._reduce(feats), names)
+            idx = local["idx"]
+            if idx:
+                grads = torch.stack([local["fg"][i] for i in idx])
+                wl = torch.tensor([wv[i] / n for i in idx], dtype=torch.float32, device=self.device)
+                part = ops.weighted_sum(grads, wl, out_dtype=torch.float64)
+            else:
+                part = torch.zeros(self.spec.P, dtype=torch.float64, device=self.device)
+            # ONE all-reduce of the wv-weighted P-vector
+            agg_grad = self._reduce(part).float()
             log.info(f"[foolsgold agg] wv: {wv}")
             agg.foolsgold_server_step(self.global_state, agg_grad, self.spec.P, float(p["eta"]),
                                       float(p["lr"]), float(p["decay"]))
@@ -601,9 +717,19 @@ class Server:
             elif kind == "scale":
                 name, ph = payload
                 dist = cstats[name]["dist"].get(ph.epoch, 0.0)
+                g_n, pre_n, pre_d, post_n = cstats[name]["norms"].get(ph.epoch, (0.0, 0.0, 0.0, 0.0))
                 csv.scale_temp_one_row.append(ph.epoch)
                 csv.scale_temp_one_row.append(round(dist, 4))
-                log.info(f"Scaled Norm after poisoning, distance: {dist}")
+                # the reference's poison-phase norm lines (image_train.py:144-146,166-183;
+                # loan_train.py:148-168)
+                log.info(f"Global model norm: {g_n}.")
+                log.info(f"Norm before scaling: {pre_n}. Distance: {pre_d}")
+                if not loan:
+                    log.info("will scale.")
+                log.info(f"Scaling by  {p['scale_weights_poison']}")
+                log.info(f"Scaled Norm after poisoning: {post_n}, distance: {dist}")
+                n_adv = sum(1 for c in plan.clients if any(q.poison for q in c.phases))
+                log.info(f"Total norm for {n_adv} adversaries is: {post_n}. distance: {dist}")
             elif kind == "scale_acc":
                 if csv.scale_temp_one_row:
                     csv.scale_temp_one_row.append(round(out.get("global_acc", 0.0), 4))

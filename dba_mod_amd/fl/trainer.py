@@ -47,6 +47,10 @@ class ClientResult:
     # per-step (batch loss, distance to the round's global model) when vis_train_batch_loss /
     # batch_track_distance are set (model.train_batch_vis / track_distance_batch_vis)
     batch_trace: Optional[np.ndarray] = None
+    # phase epoch -> (global norm, norm before scaling, distance before scaling, scaled norm):
+    # the reference's poison-phase log lines (helper.model_global_norm / model_dist_norm,
+    # image_train.py:144-146,172-183; loan_train.py:148-168)
+    scale_norms: Dict[int, Tuple[float, float, float, float]] = field(default_factory=dict)
 
 
 class _GroupBuffers:
@@ -238,14 +242,17 @@ class GroupTrainer:
         if self.spec.arch == "loan" and float(b.nan_flag.item()) > 0:
             raise ValueError("NaN in LoanNet forward (reference loan_model.py:25-26)")
         dists: Dict[int, Dict[int, float]] = {g: {} for g in range(G)}
+        norms: Dict[int, Dict[int, Tuple[float, float, float, float]]] = {g: {} for g in range(G)}
         for g, e, d in w["pend_dist"]:
-            dists[g][e] = float(d.sqrt().item())
+            v = torch.stack(d).double().clamp(min=0).sqrt().cpu().tolist()   # one sync per phase
+            dists[g][e] = float(v[0])
+            norms[g][e] = (v[1], v[2], v[3], v[4])
         tr = w["trace"].cpu().numpy() if w["trace"] is not None else None    # [T, G, 2]
         for g, c in enumerate(clients):
             nsl = sum(ph.internal_epochs for ph in c.phases)
             res.append(ClientResult(c.name, snaps[g], b.fg[g].clone() if b.fg is not None else None,
                                     stats[g, :nsl].copy(), dists[g], c.num_samples, len(c.steps),
-                                    tr[:len(c.steps), g].copy() if tr is not None else None))
+                                    tr[:len(c.steps), g].copy() if tr is not None else None, norms[g]))
         return res
 
     def _reset(self, b: _GroupBuffers, global_state: torch.Tensor) -> None:
@@ -259,6 +266,12 @@ class GroupTrainer:
         if b.fg is not None:
             b.fg.zero_()
 
+    def _zeros_p(self) -> torch.Tensor:
+        z = getattr(self, "_zp", None)
+        if z is None:
+            z = self._zp = torch.zeros(self.spec.P, dtype=torch.float32, device=self.device)
+        return z
+
     @staticmethod
     def _events(clients: List[ClientPlan]) -> Dict[int, List[Tuple[int, Any]]]:
         ev: Dict[int, List[Tuple[int, Any]]] = {}
@@ -271,13 +284,21 @@ class GroupTrainer:
         """End of a local round: optional model-replacement scaling + snapshots."""
         P = self.spec.P
         if ph.pre_scale_snap is not None:
-            snaps[g][ph.pre_scale_snap] = b.state[g].clone()
+            pre = b.state[g].clone()
+            snaps[g][ph.pre_scale_snap] = pre
             gamma = float(self.params["scale_weights_poison"])
             scaled = ops.scale_from_base(b.state[g], b.base[g], gamma)
             b.state[g].copy_(scaled)
             if b.wcomp is not b.state:
                 b.wcomp[g].copy_(b.state[g, :P])
-            # distance over parameters only (helper.model_dist_norm, helper.py:65-71)
-            pend_dist.append((g, ph.epoch, ops.sq_dists(b.state[g:g + 1, :P], b.base[g, :P])[0]))
+            # norms / distances over parameters only (helper.model_global_norm /
+            # model_dist_norm, helper.py:59-71): scaled distance, global norm, norm and distance
+            # before scaling, scaled norm — squared, on device, read once at collect
+            zero = self._zeros_p()
+            base = b.base[g:g + 1, :P]
+            pend_dist.append((g, ph.epoch, [
+                ops.sq_dists(b.state[g:g + 1, :P], b.base[g, :P])[0], ops.sq_dists(base, zero)[0],
+                ops.sq_dists(pre[None, :P], zero)[0], ops.sq_dists(pre[None, :P], b.base[g, :P])[0],
+                ops.sq_dists(b.state[g:g + 1, :P], zero)[0]]))
         snaps[g][ph.post_snap] = b.state[g].clone()
         b.base[g].copy_(b.state[g])

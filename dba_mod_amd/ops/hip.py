@@ -56,20 +56,23 @@ _SIGS = {
     "dba_avgpool": [_P, _P, _LL, _I, _I, _I, _P],
     "dba_avgpool_bwd": [_P, _P, _LL, _I, _I, _I, _P],
     "dba_dropout": [_P, _P, _I, _P, _U, _F, _LL, _I, _P],
-    "dba_softmax_xent": [_P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _LL, _P, _I, _P, _I, _P],
+    "dba_softmax_xent": [_P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _LL, _P, _I, _P, _I, _P, _P],
     "dba_sgd_step": [_P, _LL, _P, _P, _P, _P, _P, _F, _F, _P, _P, _I, _I, _P],
     "dba_scale_from_base": [_P, _P, _F, _P, _LL, _P],
-    "dba_add_noise_scaled": [_P, _P, _LL, _F, _F, _U, _I, _P],
-    "dba_sq_dists": [_P, _LL, _P, _I, _LL, _P, _P],
-    "dba_weighted_sum": [_P, _LL, _P, _I, _P, _LL, _P],
-    "dba_gram": [_P, _LL, _I, _I, _P, _P],
+    "dba_add_noise_scaled": [_P, _P, _LL, _F, _F, _U, _I, _I, _P],
+    "dba_delta_sum": [_P, _LL, _I, _P, _LL, _P, _P],
+    "dba_sqdist_blocks": [_LL],
+    "dba_gram_chunks": [_I],
+    "dba_sq_dists": [_P, _LL, _P, _I, _LL, _P, _P, _P],
+    "dba_weighted_sum": [_P, _LL, _P, _I, _P, _LL, _I, _P],
+    "dba_gram": [_P, _LL, _I, _I, _P, _P, _P],
     "dba_conv3_fwd": [_P, _LL, _P, _LL, _P, _P, _LL, _P, _P, _LL, _I, _P, _P] + [_I] * 13 + [_P, _LL, _P],
     "dba_conv3_splitk_floats": [_I] * 9,
     "dba_conv3_set_tiles": [_I, _I],
     "dba_pconv": [_P, _LL, _P, _LL, _P, _P, _LL, _P, _P, _LL, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P],
     "dba_pwgrad": [_P, _LL, _P, _LL, _P, _LL, _P, _P, _I, _I, _I, _I, _I, _I, _P],
     "dba_wgrad3": [_P, _LL, _P, _LL, _P, _LL, _P, _P] + [_I] * 12 + [_P],
-    "dba_dist_loss_grad": [_P, _LL, _P, _LL, _P, _LL, _I, _P, _P, _F, _P, _P],
+    "dba_dist_loss_grad": [_P, _LL, _P, _LL, _P, _LL, _I, _P, _P, _F, _P, _P, _P],
     # reference-precision (fp32) family: csrc/kernels/xgemm.hip
     "dba_xgemm_set_planes": [_I],
     "dba_xconv_ws_floats": [_I] * 8,
@@ -659,9 +662,10 @@ def dropout_bwd(dy, p, seeds, salt):
 
 
 # ---------------------------------------------------------------------------- loss
-def softmax_xent(logits, labels, mean, want_grad, stats=None, slot=None, nvalid=None, grad_dtype=None):
+def softmax_xent(logits, labels, mean, want_grad, stats=None, slot=None, nvalid=None, grad_dtype=None,
+                 loss_dtype=None):
     """``grad_dtype``: dtype of dlogits (the compute dtype of the backward pass; bf16 if
-    unset)."""
+    unset).  ``loss_dtype`` fp64 returns the per-group loss unrounded (evaluation sums)."""
     if logits.dtype != _F32:
         raise TypeError("softmax_xent: logits must be fp32 (the final layer emits fp32)")
     lf = logits.contiguous()
@@ -670,6 +674,7 @@ def softmax_xent(logits, labels, mean, want_grad, stats=None, slot=None, nvalid=
     if gdt not in (_BF16, _F32):
         raise TypeError(f"softmax_xent: unsupported grad dtype {gdt}")
     loss = torch.empty(G, dtype=torch.float32, device=lf.device)
+    loss64 = torch.empty(G, dtype=torch.float64, device=lf.device) if loss_dtype == torch.float64 else None
     correct = torch.empty(G, dtype=torch.float32, device=lf.device)
     dl = torch.empty(G, B, C, dtype=gdt, device=lf.device) if want_grad else None
     sp, ss, slp, ms, nvp = None, 0, None, 0, None
@@ -680,8 +685,8 @@ def softmax_xent(logits, labels, mean, want_grad, stats=None, slot=None, nvalid=
         slot_, nv_ = _i32(slot), _i32(nvalid)
         sp, ss, slp, nvp = stats.data_ptr(), stats.shape[1], slot_.data_ptr(), nv_.data_ptr()
     _call("dba_softmax_xent", lf.data_ptr(), _i32(labels).data_ptr(), G, B, C, int(bool(mean)), _ptr(dl),
-          loss.data_ptr(), correct.data_ptr(), sp, ss, slp, ms, nvp, int(gdt == _F32), _stream())
-    return loss, correct, dl
+          loss.data_ptr(), correct.data_ptr(), sp, ss, slp, ms, nvp, int(gdt == _F32), _ptr(loss64), _stream())
+    return (loss64 if loss64 is not None else loss), correct, dl
 
 
 # ------------------------------------------------------------------------- optimizer
@@ -701,8 +706,9 @@ def dist_loss_grad(w, base, grads, trig, active, alpha):
     assert w.dtype == torch.float32 and w.stride(1) == 1 and base.stride(1) == 1 and grads.is_contiguous()
     assert w.shape[0] >= G and base.shape[0] >= G and w.shape[1] >= P and base.shape[1] >= P
     nrm2 = torch.zeros(G, dtype=torch.float32, device=grads.device)
+    part = torch.empty(G, 256, dtype=torch.float32, device=grads.device)
     _call("dba_dist_loss_grad", w.data_ptr(), w.stride(0), base.data_ptr(), base.stride(0), grads.data_ptr(), P, G,
-          _i32(trig).data_ptr(), _i32(active).data_ptr(), float(alpha), nrm2.data_ptr(), _stream())
+          _i32(trig).data_ptr(), _i32(active).data_ptr(), float(alpha), nrm2.data_ptr(), part.data_ptr(), _stream())
     return nrm2.sqrt()
 
 
@@ -717,26 +723,45 @@ def scale_from_base(w, base, gamma):
 
 def add_noise_scaled(dst, upd, coef, sigma, seed, noise):
     assert dst.is_contiguous() and dst.dtype == torch.float32
-    upd = upd.float().contiguous()
+    if upd.dtype not in (torch.float32, torch.float64):
+        upd = upd.float()
+    upd = upd.contiguous()
     _call("dba_add_noise_scaled", dst.data_ptr(), upd.data_ptr(), dst.numel(), float(coef), float(sigma),
-          int(seed) & 0xFFFFFFFF, int(bool(noise)), _stream())
+          int(seed) & 0xFFFFFFFF, int(bool(noise)), int(upd.dtype == torch.float64), _stream())
+
+
+def delta_sum(rows, base):
+    assert rows.dtype == torch.float32 and base.dtype == torch.float32
+    n = base.numel()
+    out = torch.empty(n, dtype=torch.float64, device=base.device)
+    if rows.shape[0] == 0:
+        out.zero_()
+        return out
+    assert rows.stride(-1) == 1 and rows.shape[1] >= n
+    base = base.contiguous()
+    _call("dba_delta_sum", rows.data_ptr(), rows.stride(0), rows.shape[0], base.data_ptr(), n, out.data_ptr(),
+          _stream())
+    return out
 
 
 def sq_dists(points, m):
     assert points.stride(1) == 1 and points.dtype == torch.float32
     m = m.float().contiguous()
     n, L = points.shape
-    out = torch.zeros(n, dtype=torch.float64, device=points.device)
-    _call("dba_sq_dists", points.data_ptr(), points.stride(0), m.data_ptr(), n, L, out.data_ptr(), _stream())
+    out = torch.empty(n, dtype=torch.float64, device=points.device)
+    part = torch.empty(n * int(_L.dba_sqdist_blocks(L)), dtype=torch.float64, device=points.device)
+    _call("dba_sq_dists", points.data_ptr(), points.stride(0), m.data_ptr(), n, L, out.data_ptr(), part.data_ptr(),
+          _stream())
     return out
 
 
-def weighted_sum(points, wts):
+def weighted_sum(points, wts, out_dtype=None):
     assert points.stride(1) == 1 and points.dtype == torch.float32
+    odt = out_dtype or torch.float32
     n, L = points.shape
-    out = torch.empty(L, dtype=torch.float32, device=points.device)
+    out = torch.empty(L, dtype=odt, device=points.device)
     _call("dba_weighted_sum", points.data_ptr(), points.stride(0), wts.float().contiguous().data_ptr(), n,
-          out.data_ptr(), L, _stream())
+          out.data_ptr(), L, int(odt == torch.float64), _stream())
     return out
 
 
@@ -745,6 +770,7 @@ def gram(feats):
     if f.stride(1) != 1:
         f = f.contiguous()
     n, d = f.shape
-    out = torch.zeros(n, n, dtype=torch.float32, device=f.device)
-    _call("dba_gram", f.data_ptr(), f.stride(0), n, d, out.data_ptr(), _stream())
+    out = torch.empty(n, n, dtype=torch.float64, device=f.device)
+    slab = torch.empty(int(_L.dba_gram_chunks(d)) * n * n, dtype=torch.float32, device=f.device)
+    _call("dba_gram", f.data_ptr(), f.stride(0), n, d, out.data_ptr(), slab.data_ptr(), _stream())
     return out

@@ -295,11 +295,13 @@ def dropout_bwd(dy: Tensor, p: float, seeds: Tensor, salt: int) -> Tensor:
 # ---------------------------------------------------------------------------- loss
 def softmax_xent(logits: Tensor, labels: Tensor, mean: bool, want_grad: bool,
                  stats: Optional[Tensor] = None, slot: Optional[Tensor] = None,
-                 nvalid: Optional[Tensor] = None, grad_dtype: Optional[torch.dtype] = None
-                 ) -> Tuple[Tensor, Tensor, Optional[Tensor]]:
+                 nvalid: Optional[Tensor] = None, grad_dtype: Optional[torch.dtype] = None,
+                 loss_dtype: Optional[torch.dtype] = None) -> Tuple[Tensor, Tensor, Optional[Tensor]]:
     """Per-group CE (mean over valid rows or sum) + correct count + dlogits (K9).
 
-    ``grad_dtype``: dtype of dlogits (default: the logits' dtype).
+    ``grad_dtype``: dtype of dlogits (default: the logits' dtype).  ``loss_dtype`` fp64: the
+    per-row losses are summed in fp64 (the sum then does not depend on how rows are grouped
+    into chunks or sharded over ranks).
 
     Rows with label < 0 are padding.  dlogits corresponds to the *mean* loss when
     ``mean`` (training) and to the sum otherwise.  With ``stats`` ([3, G*max_slots] fp32),
@@ -314,6 +316,9 @@ def softmax_xent(logits: Tensor, labels: Tensor, mean: bool, want_grad: bool,
     nll = -logp.gather(-1, lab.clamp(min=0)[..., None]).squeeze(-1)
     nll = torch.where(valid, nll, torch.zeros_like(nll))
     cnt = valid.sum(1).clamp(min=1).to(_cdt())
+    if loss_dtype == torch.float64:
+        nll = nll.to(torch.float64)
+        cnt = cnt.to(torch.float64)
     loss = nll.sum(1) / cnt if mean else nll.sum(1)
     pred = lf.argmax(-1)
     correct = ((pred == lab) & valid).sum(1).to(_cdt())
@@ -394,12 +399,23 @@ def scale_from_base(w: Tensor, base: Tensor, gamma: float) -> Tensor:
 
 def add_noise_scaled(dst: Tensor, upd: Tensor, coef: float, sigma: float, seed: int,
                      noise: bool) -> None:
-    """dst += coef*upd (+ N(0, sigma) per element if noise)  (K12, helper.py:240-257)."""
-    u = upd * coef
+    """dst += coef*upd (+ N(0, sigma) per element if noise)  (K12, helper.py:240-257).
+    ``upd`` may be fp64 (the FedAvg delta sum): the product is rounded to fp32 once."""
+    u = (upd * coef).to(dst.dtype)
     if noise:
         ctr = torch.arange(u.numel(), dtype=torch.int64, device=u.device).reshape(u.shape)
         u = u + sigma * rng.normal(seed, ctr)
     dst += u
+
+
+def delta_sum(rows: Tensor, base: Tensor) -> Tensor:
+    """sum_r (rows[r] - base) in fp64 (FedAvg's per-rank Σ-delta, K12; helper.py:218-222).
+    fp32 deltas summed in fp64 are exact, so a cross-rank all-reduce of the partial sums
+    gives the same total as one rank summing all clients."""
+    n = base.numel()
+    if rows.shape[0] == 0:
+        return torch.zeros(n, dtype=torch.float64, device=base.device)
+    return (rows[:, :n].double() - base.double()[None]).sum(0)
 
 
 def sq_dists(points: Tensor, m: Tensor) -> Tensor:
@@ -408,9 +424,9 @@ def sq_dists(points: Tensor, m: Tensor) -> Tensor:
     return (d * d).sum(1)
 
 
-def weighted_sum(points: Tensor, wts: Tensor) -> Tensor:
-    """sum_i wts[i] * points[i] (K14/K16)."""
-    return (wts.double()[:, None] * points.double()).sum(0).to(points.dtype)
+def weighted_sum(points: Tensor, wts: Tensor, out_dtype: Optional[torch.dtype] = None) -> Tensor:
+    """sum_i wts[i] * points[i] (K14/K16); ``out_dtype`` fp64 keeps a partial sum unrounded."""
+    return (wts.double()[:, None] * points.double()).sum(0).to(out_dtype or points.dtype)
 
 
 def gram(feats: Tensor) -> Tensor:

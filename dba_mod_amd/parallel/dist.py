@@ -1,35 +1,51 @@
 """One process per GPU over ``torch.distributed`` (RCCL over xGMI on MI355X, Gloo on CPU).
 
-The reference is single-process/single-GPU with no collective at all.
-This framework's distributed round (client-parallel DP):
+The reference is single-process/single-GPU with no collective at all (its
+logical reduction points are ``helper.py:218-257`` FedAvg, ``:320-352`` Weiszfeld,
+``:537-570`` FoolsGold).  This framework's distributed round (client-parallel DP):
 
 1. every rank computes the identical round plan (same seeded RNG; no communication);
-2. clients are placed on ranks by LPT (:func:`dba_mod_amd.utils.native.lpt_assign`);
-3. each rank trains its clients concurrently, then ONE all-gather moves the packed client
-   snapshot slots (flat fp32 buckets, one row per snapshot) to every rank — 10 CIFAR
-   clients ≈ 112 MB, a fraction of a millisecond of xGMI time;
+2. clients are placed on ranks by LPT (:func:`dba_mod_amd.utils.native.lpt_assign`); a
+   client's snapshots stay on its owner rank;
+3. aggregation reduces instead of gathering (``fl/server.py`` ``_aggregate``):
+   * FedAvg — each rank sums its own clients' deltas in fp64, ONE all-reduce of S values;
+   * FoolsGold — ONE all-reduce of the ``[n, d]`` final-layer features (each row owned by
+     one rank), weights computed identically everywhere, ONE all-reduce of the wv-weighted
+     P-vector;
+   * RFA — distributed Weiszfeld (per iteration an all-reduce of the S-vector partial
+     weighted sum + an all-reduce of the n distances) when that moves fewer bytes than an
+     all-gather of the n final states, else the all-gather (``rfa_mode``);
 4. aggregation is applied redundantly on every rank (bit-identical global model, no
    broadcast);
-5. a client's local tests run on its owner rank as soon as it finishes training (the longest
-   clients' and the global model's tests are image-sharded across ranks); ONE all-reduce of
-   the ``[jobs, 3]`` counters combines both.
+5. a client's local tests run on its owner rank as soon as it finishes training; only the
+   snapshots of the clients whose tests are image-sharded across ranks (the round's longest
+   clients) are all-gathered; ONE all-reduce of the ``[jobs, 3]`` counters combines the
+   tests.
+
+Bucket policy: every collective moves one contiguous flat buffer (never
+per-layer calls), padded to a multiple of world x 7 xGMI links x 4 KiB so each ring chunk
+is equal and 4 KiB aligned, and issued in pieces of at most 64 MB.  ``bytes`` counts the
+payload of every collective (per kind) for tests and the round metrics.  The int64 BN
+counters never enter a float bucket.
 
 On a one-GPU box the multi-rank path is rehearsed with ``DBA_SHARE_GPU=1`` (every rank on
 device 0) and ``DBA_DIST_BACKEND=gloo`` (``tests/test_gpu_dist.py``).
-
-Bucket policy: payloads are single contiguous flat buffers (never per-layer calls); rows
-are padded so every rank contributes the same ``[k_max, S]`` block, which is what RCCL's
-``all_gather_into_tensor`` needs.  The int64 BN counters never enter a float bucket.
 """
 from __future__ import annotations
 
+import collections
 import datetime
 import os
-from dataclasses import dataclass
-from typing import List, Optional, Sequence
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence
 
 import torch
 import torch.distributed as dist
+
+
+XGMI_LINKS = 7                 # point-to-point xGMI links per MI355X
+PAD_BYTES = 4096               # per-link chunk alignment
+SPLIT_BYTES = 64 << 20         # largest single collective
 
 
 @dataclass
@@ -39,6 +55,7 @@ class DistCtx:
     local_rank: int = 0
     device: torch.device = torch.device("cpu")
     backend: str = "none"
+    bytes: Dict[str, int] = field(default_factory=lambda: collections.Counter())
 
     @property
     def is_main(self) -> bool:
@@ -55,9 +72,26 @@ class DistCtx:
             else:
                 dist.barrier()
 
+    def pad_unit(self, itemsize: int) -> int:
+        """Elements per padding unit: world x links x 4 KiB."""
+        return max(1, self.world * XGMI_LINKS * PAD_BYTES // itemsize)
+
+    def padded(self, n: int, dtype: torch.dtype) -> torch.Tensor:
+        """A zeroed flat buffer of ``n`` elements rounded up to the padding unit; fill
+        ``buf[:n]`` and hand the whole buffer to :meth:`all_reduce_`."""
+        unit = self.pad_unit(torch.empty(0, dtype=dtype).element_size())
+        return torch.zeros((n + unit - 1) // unit * unit, dtype=dtype, device=self.device)
+
     def all_reduce_(self, t: torch.Tensor) -> torch.Tensor:
+        """Sum-all-reduce ``t`` in place (one flat buffer; pieces of <= 64 MB)."""
         if self.enabled:
-            dist.all_reduce(t)
+            flat = t.view(-1) if t.is_contiguous() else None
+            if flat is None:
+                raise ValueError("all_reduce_ needs a contiguous buffer")
+            step = max(1, SPLIT_BYTES // flat.element_size())
+            for i in range(0, flat.numel(), step):
+                dist.all_reduce(flat[i:i + step])
+            self.bytes["all_reduce"] += flat.numel() * flat.element_size()
         return t
 
     def all_reduce_max(self, value: float) -> float:
@@ -80,12 +114,20 @@ class DistCtx:
             send[:local.shape[0]] = local
         out = torch.empty(self.world * k_max, W, dtype=local.dtype, device=local.device)
         dist.all_gather_into_tensor(out, send)
+        self.bytes["all_gather"] += out.numel() * out.element_size()
         return out
 
     def broadcast_(self, t: torch.Tensor, src: int = 0) -> torch.Tensor:
         if self.enabled:
             dist.broadcast(t, src)
+            self.bytes["broadcast"] += t.numel() * t.element_size()
         return t
+
+    def take_bytes(self) -> Dict[str, int]:
+        """Collective payload bytes since the last call (and reset)."""
+        out = dict(self.bytes)
+        self.bytes.clear()
+        return out
 
 
 def init_distributed(prefer_gpu: bool = True, timeout_s: int = 1800) -> DistCtx:

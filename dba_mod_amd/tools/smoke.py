@@ -1,4 +1,9 @@
-"""One tiny grouped train step + eval forward of the CIFAR ResNet-18 (driver smoke test)."""
+"""Driver smoke test: one tiny grouped train step + eval forward of the CIFAR ResNet-18.
+
+Runs the step in the framework's default (reference) precision, fp32, through the device's
+kernels (the HIP split-bf16 family on GPU) and checks it against the plain-PyTorch reference
+ops evaluated in fp64 on the CPU from the same inputs: loss, gradient and folded-BN eval
+logits must agree at fp32 level (not merely be finite)."""
 from __future__ import annotations
 
 import time
@@ -8,42 +13,74 @@ import torch
 from .. import ops
 from ..models import program as prog
 from ..models.spec import get_spec
+from ..ops import reference as ref
 
 
-def run_smoke(device: torch.device, G: int = 2, N: int = 8) -> dict:
+def _rel(a: torch.Tensor, b: torch.Tensor) -> float:
+    a, b = a.detach().double().cpu(), b.detach().double().cpu()
+    return float((a - b).norm() / b.norm().clamp(min=1e-30))
+
+
+def _step(device: torch.device, dtype: torch.dtype, impl, G: int, N: int, seed: int = 0):
+    """One grouped train step (gather -> forward -> CE -> backward -> SGD) + an eval forward,
+    with every op taken from ``impl`` (the dispatcher, or the reference module)."""
     spec = get_spec("resnet18_cifar")
-    dtype = torch.bfloat16 if device.type == "cuda" else torch.float32
-    state = spec.init_flat(0).to(device)[None].repeat(G, 1).contiguous()
-    wcomp = state if dtype == torch.float32 else state[:, :spec.P].to(dtype).contiguous()
-    grads = torch.zeros(G, spec.P, device=device)
-    mom = torch.zeros(G, spec.P, device=device)
-    src = torch.randint(0, 256, (64, 32, 32, 3), dtype=torch.uint8, device=device)
-    labels = torch.randint(0, 10, (64,), dtype=torch.int32, device=device)
+    gen = torch.Generator().manual_seed(seed)
+    state = spec.init_flat(0).to(device, dtype)[None].repeat(G, 1).contiguous()
+    grads = torch.zeros(G, spec.P, device=device, dtype=dtype)
+    mom = torch.zeros(G, spec.P, device=device, dtype=dtype)
+    src = torch.randint(0, 256, (64, 32, 32, 3), dtype=torch.uint8, generator=gen).to(device)
+    labels = torch.randint(0, 10, (64,), dtype=torch.int32, generator=gen).to(device)
     idx = torch.arange(G * N, dtype=torch.int32, device=device).view(G, N)
     masks = torch.zeros(1, 32, 32, dtype=torch.uint8, device=device)
     masks[0, 0, :6] = 1
     trig = torch.tensor([0, -1], dtype=torch.int32, device=device)[:G]
     pn = torch.tensor([3, 0], dtype=torch.int32, device=device)[:G]
     nvalid = torch.full((G,), N, dtype=torch.int32, device=device)
+    saved = {k: getattr(ops, k) for k in ops._OPS}
+    if impl is not ops:
+        for k in ops._OPS:
+            setattr(ops, k, getattr(impl, k))
+    try:
+        x, y = ops.gather_images(src, labels, idx, masks, trig, pn, 2, None, dtype)
+        ctx = prog.Ctx(spec, state, state, None, train=True, grads=grads, nvalid=nvalid, act_dtype=dtype)
+        logits = prog.forward(ctx, x)
+        loss, correct, dl = ops.softmax_xent(logits, y, True, True, grad_dtype=dtype)
+        ctx.tape.backward(logits, dl)
+        g0 = grads.clone()
+        lr = torch.full((G,), 0.1, device=device, dtype=torch.float32)
+        one = torch.ones(G, dtype=torch.int32, device=device)
+        ops.sgd_step(state[:, :spec.P], grads, mom, lr, one, one, 0.9, 5e-4)
+        folded = prog.fold_bank(spec, state, dtype)
+        ectx = prog.Ctx(spec, None, None, torch.arange(G, dtype=torch.int32, device=device), train=False,
+                        folded=folded, nvalid=nvalid, act_dtype=dtype)
+        el = prog.forward(ectx, x)
+    finally:
+        for k, v in saved.items():
+            setattr(ops, k, v)
+    return loss, g0, el
+
+
+def run_smoke(device: torch.device, G: int = 2, N: int = 8) -> dict:
     t0 = time.time()
-    x, y = ops.gather_images(src, labels, idx, masks, trig, pn, 2, None, dtype)
-    ctx = prog.Ctx(spec, state, wcomp, None, train=True, grads=grads, nvalid=nvalid, act_dtype=dtype)
-    logits = prog.forward(ctx, x)
-    loss, correct, dl = ops.softmax_xent(logits, y, True, True)
-    ctx.tape.backward(logits, dl)
-    lr = torch.full((G,), 0.1, device=device)
-    one = torch.ones(G, dtype=torch.int32, device=device)
-    ops.sgd_step(state[:, :spec.P], grads, mom, lr, one, one, 0.9, 5e-4,
-                 shadow=(wcomp if wcomp is not state else None))
-    folded = prog.fold_bank(spec, state, dtype)
-    ectx = prog.Ctx(spec, None, None, torch.arange(G, dtype=torch.int32, device=device), train=False,
-                    folded=folded, nvalid=nvalid, act_dtype=dtype)
-    el = prog.forward(ectx, x)
+    loss, g, el = _step(device, torch.float32, ops, G, N)
     if device.type == "cuda":
         torch.cuda.synchronize()
-    out = {"device": str(device), "backend": ops.backend_name(device), "loss": loss.float().tolist(),
-           "grad_norm": float(grads.norm()), "eval_logits_finite": bool(torch.isfinite(el.float()).all()),
-           "seconds": round(time.time() - t0, 3)}
-    assert all(torch.isfinite(loss.float())), out
-    assert out["grad_norm"] > 0 and out["eval_logits_finite"], out
+    secs = time.time() - t0
+    old = ref.COMPUTE_DTYPE
+    ref.COMPUTE_DTYPE = torch.float64
+    try:
+        loss_r, g_r, el_r = _step(torch.device("cpu"), torch.float64, ref, G, N)
+    finally:
+        ref.COMPUTE_DTYPE = old
+    out = {"device": str(device), "backend": ops.backend_name(device), "dtype": "fp32",
+           "loss": [float(v) for v in loss], "loss_ref_fp64": [float(v) for v in loss_r],
+           "grad_norm": float(g.double().norm()), "grad_norm_ref": float(g_r.norm()),
+           "grad_rel_err": _rel(g, g_r), "eval_logits_rel_err": _rel(el, el_r),
+           "seconds": round(secs, 3)}
+    assert all(abs(a - b) <= 1e-5 * max(1.0, abs(b)) for a, b in zip(out["loss"], out["loss_ref_fp64"])), out
+    # a random-init ResNet with 8-image BatchNorm amplifies rounding: plain fp32 torch is
+    # itself ~2e-3 from fp64 on these inputs, so the gradient bound is 1e-2 (a bf16 path
+    # lands at ~2e-1); the folded eval forward is well conditioned (fp32 level, 1e-4)
+    assert out["grad_rel_err"] < 1e-2 and out["eval_logits_rel_err"] < 1e-4, out
     return out

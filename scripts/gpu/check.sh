@@ -1,6 +1,8 @@
-# full GPU check: kernel + e2e tests, smoke, 1-GPU bench
+# full GPU check: kernel + e2e tests, smoke, 1-GPU bench (fp32 headline)
 mkdir -p gpurun_out
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1 || exit $?
+timeout -k 10 1100 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1 || exit $?
+tail -3 gpurun_out/gpu_tests.log
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || exit $?
-timeout -k 10 600 python bench.py > gpurun_out/bench.log 2>&1 || exit $?
+tail -1 gpurun_out/smoke.log
+timeout -k 10 600 python bench.py --steps 20 --warmup 5 > gpurun_out/bench.log 2>&1 || exit $?
 tail -1 gpurun_out/bench.log

@@ -1,7 +1,7 @@
 """The driver's bench.py contract, rehearsed on CPU: one JSON line from rank 0 with the
 required keys, K timed steps, and the multi-rank launch the driver uses
 (``python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1``),
-here with the gloo backend and world size 2."""
+here with the gloo backend and world sizes 2 and 8."""
 import json
 import os
 import subprocess
@@ -42,3 +42,10 @@ def test_bench_torchrun_world2_cpu():
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(free_port()), "bench.py", "--gpus", "2", *SMALL]
     _check(_run(cmd), 2)
+
+
+def test_bench_torchrun_world8_cpu():
+    """The driver's N=8 launch shape, rehearsed with 8 gloo ranks on the CPU."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), "bench.py", "--gpus", "8", *SMALL]
+    _check(_run(cmd, timeout=900), 8)
