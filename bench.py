@@ -118,7 +118,9 @@ def main() -> int:
             # (ops/hip.py dispatches on the activation dtype and never converts)
             "dtype": {torch.bfloat16: "bf16", torch.float32: "fp32"}[server.dtype],
             "data": (f"synthetic ({params.type} shapes/class sizes); random-init weights warm-started by "
-                     f"{args.pretrain_rounds} benign FedAvg rounds (untimed)"),
+                     + (f"{int(params['pretrain_central_epochs'])} centralised epochs + "
+                        if int(params["pretrain_central_epochs"]) > 0 else "")
+                     + f"{args.pretrain_rounds} benign FedAvg rounds (untimed)"),
             "config": {"model": MODEL_NAMES.get(params.type, params.type),
                        "global_batch": int(params["batch_size"]) * int(params["no_models"]),
                        "seq_len": None, "parallelism": f"client-dp{dctx.world}",

@@ -386,6 +386,200 @@ __global__ __launch_bounds__(256) void xconv_kernel(const XArgs a) {
   }
 }
 
+// ======================================================================= halo conv
+// Stride-1 3x3 conv (pad 1) and the stride-1 data gradient, for the narrow ResNet stages
+// (W 32 / 16, Cs 32 / 64): the block's input patch ((TR+2) x (W+2) pixels x Cs) is loaded and
+// split into bf16 planes ONCE and every tap's A fragments are read from it at the tap's pixel
+// offset.  The implicit GEMM (xconv_kernel) re-stages and re-splits every input element once
+// per tap (9x), which makes the split VALU — not the MFMA — the bound of these layers.  The
+// weights stream through the same two-stage register/LDS pipeline as in xconv_kernel; the
+// k-step order (tap-major, 32 channels per step) and the MFMA sequence per output element are
+// the same, so both kernels compute identical bits.
+template <int W, int CS>
+__device__ __forceinline__ int hswz(int pp) {
+  constexpr int CH = CS / 8;                    // 16-B chunks per pixel (4 or 8)
+  return (pp >> (CH == 4 ? 2 : 1)) & (CH - 1);
+}
+
+template <int W, int CS, int BM, int BN, int WM, int WN, int P>
+__global__ __launch_bounds__(256) void xhalo_kernel(const XArgs a) {
+  constexpr int TR = BM / W, PW = W + 2, PR = TR + 2, PP = PR * PW;
+  constexpr int CH = CS / 8, PATCH = PP * CH;             // uint4 per plane
+  constexpr int TM = BM / WM, TN = BN / WN, MI = TM / 32, NJ = TN / 32;
+  static_assert(WM * WN == 4 && MI >= 1 && NJ >= 1 && BM % W == 0, "tiling");
+  constexpr int RB = BN / 32;                             // weight quarters per thread
+  constexpr int BPL = BN * 4;                             // uint4 per weight plane (BN rows x 64 B)
+  constexpr int NK = 9 * CS / 32;                         // k-steps
+  constexpr int CB = CS / 32;                             // channel blocks per tap
+  static_assert(BM * BN <= P * PATCH * 4, "epilogue tile fits the patch");
+  __shared__ __attribute__((aligned(16))) uint4 patch[P * PATCH];
+  __shared__ __attribute__((aligned(16))) uint4 bring[2 * P * BPL];
+  __shared__ long long orow[BM];
+
+  const int g = blockIdx.y;
+  const int HT = a.Ho / TR;                               // row tiles per image
+  const int tn = blockIdx.x % a.tiles_n, tm = blockIdx.x / a.tiles_n;
+  const int img = tm / HT, h0 = (tm - img * HT) * TR;
+  if (img >= valid_rows(a.nvalid, g, a.N)) return;
+  const int n0 = tn * BN;
+  const int slot = a.wsel ? a.wsel[g] : g;
+  const int K = 9 * CS;
+  const float* __restrict__ src = a.src + (long long)g * a.src_gstride;
+  const float* __restrict__ Bp = a.w + (long long)slot * a.w_sstride;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WN, wn = wid % WN;
+  const int kq = tid & 7, r0 = tid >> 3;
+  const bool flip = a.dsg < 0;                            // data gradient: tap (i, j) reads (2-i, 2-j)
+
+  if (tid < BM)
+    orow[tid] = (((long long)img * a.Ho + h0 + tid / W) * a.Wo + tid % W) * a.Ncol;
+
+  // ---- the input patch: rows h0-1 .. h0+TR, cols -1 .. W, split once into P planes
+  {
+    const __amdgpu_buffer_rsrc_t rA = rsrc(src, (long long)a.N * a.Hs * a.Ws * CS * 4);
+    constexpr int Q4 = CS / 4;                            // float4 quarters per pixel
+    for (int e = tid; e < PP * Q4; e += 256) {
+      const int pp = e / Q4, q = e - pp * Q4;
+      const int pr = pp / PW, pc = pp - pr * PW;
+      const int h = h0 - 1 + pr, w = pc - 1;
+      const bool ok = (unsigned)h < (unsigned)a.Hs && (unsigned)w < (unsigned)a.Ws;
+      const float4 v = bload4(rA, ok ? (((img * a.Hs + h) * a.Ws + w) * CS + q * 4) * 4 : kOOB);
+      uint2 sp[P];
+      split4<P>(v.x, v.y, v.z, v.w, sp);
+      const int o = pp * CH + ((q >> 1) ^ hswz<W, CS>(pp));
+#pragma unroll
+      for (int p = 0; p < P; ++p) ((uint2*)&patch[p * PATCH + o])[q & 1] = sp[p];
+    }
+  }
+
+  // ---- weights: two-stage pipeline (k-step t: tap t / CB, channels (t % CB) * 32 ..)
+  int boffs[RB];
+#pragma unroll
+  for (int j = 0; j < RB; ++j) {
+    const int n = n0 + r0 + 32 * j;
+    boffs[j] = n < a.Ncol ? n * K : -1;
+  }
+  const __amdgpu_buffer_rsrc_t rB = rsrc(Bp, (long long)a.Ncol * K * 4);
+  float4 rb[2][RB];
+  auto gload = [&](int t, int st) {
+    const int kb = t * 32 + kq * 4;
+#pragma unroll
+    for (int j = 0; j < RB; ++j) rb[st][j] = bload4(rB, (boffs[j] >= 0 && kb < K) ? (boffs[j] + kb) * 4 : kOOB);
+  };
+  auto lput_q = [&](int buf, int st, int q) {
+    if (q >= RB) return;
+    uint2 sp[P];
+    split4<P>(rb[st][q].x, rb[st][q].y, rb[st][q].z, rb[st][q].w, sp);
+    lds_put<P, false, BN>(bring + buf * P * BPL, BPL, 0, r0 + 32 * q, kq, sp);
+  };
+
+  f32x16_t acc[MI][NJ];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  const int fr = lane & 31, hf = lane >> 5;
+  // patch pixel of each A fragment row at tap offset (0, 0)
+  int apix[MI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i) {
+    const int m = wm * TM + i * 32 + fr;
+    apix[i] = (m / W) * PW + (m % W);
+  }
+  auto mma = [&](int t, int buf, int stn) {
+    const int tap = t / CB, cb = t - tap * CB;
+    int ti = tap / 3, tj = tap - ti * 3;
+    if (flip) { ti = 2 - ti; tj = 2 - tj; }
+    const int toff = ti * PW + tj;
+    const uint4* L = bring + buf * P * BPL;
+    constexpr int T = 2 * P * (P + 1) / 2 * MI * NJ;
+    int cnt = 0, q = 0;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int ch = kk * 2 + hf;
+      bf16x8_t af[P][MI], bfr[P][NJ];
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        const int pp = apix[i] + toff;
+        const int o = pp * CH + ((cb * 4 + ch) ^ hswz<W, CS>(pp));
+#pragma unroll
+        for (int p = 0; p < P; ++p) af[p][i] = *(const bf16x8_t*)&patch[p * PATCH + o];
+      }
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int n = wn * TN + j * 32 + fr;
+        const int o = n * 4 + (ch ^ ((n >> 2) & 3));
+#pragma unroll
+        for (int p = 0; p < P; ++p) bfr[p][j] = *(const bf16x8_t*)&L[p * BPL + o];
+      }
+#pragma unroll
+      for (int s = P - 1; s >= 0; --s)
+#pragma unroll
+        for (int pa = 0; pa <= s; ++pa)
+#pragma unroll
+          for (int i = 0; i < MI; ++i)
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) {
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[pa][i], bfr[s - pa][j], acc[i][j], 0, 0, 0);
+              ++cnt;
+              if (q < RB && cnt * RB >= (q + 1) * T) lput_q(buf ^ 1, stn, q++);
+            }
+    }
+    while (q < RB) lput_q(buf ^ 1, stn, q++);
+  };
+
+  gload(0, 0);
+  gload(1, 1);
+#pragma unroll
+  for (int q = 0; q < RB; ++q) lput_q(0, 0, q);
+  __syncthreads();   // patch + first weight step
+  int t = 0;
+  for (; t + 1 < NK; t += 2) {
+    gload(t + 2, 0);
+    mma(t, 0, 1);
+    __syncthreads();
+    gload(t + 3, 1);
+    mma(t + 1, 1, 0);
+    __syncthreads();
+  }
+  if (t < NK) {
+    mma(t, 0, 1);   // (its filler writes a buffer nobody reads)
+    __syncthreads();
+  }
+
+  // ---- epilogue through the (drained) patch memory
+  float* Ct = reinterpret_cast<float*>(patch);
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        Ct[(wm * TM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * hf) * BN + wn * TN + j * 32 + fr] = acc[i][j][r];
+  __syncthreads();
+  float* out = a.out + (long long)g * a.out_gstride;
+  const float* bias = a.bias ? a.bias + (long long)slot * a.b_sstride : nullptr;
+  const float* res = a.res ? a.res + (long long)g * a.out_gstride : nullptr;
+  constexpr int C4 = BN / 4;
+  for (int e = tid; e < BM * C4; e += 256) {
+    const int row = e / C4, cc = (e - row * C4) * 4;
+    const int n = n0 + cc;
+    if (n >= a.Ncol) continue;
+    const long long o = orow[row];
+    float4 v = *(const float4*)&Ct[row * BN + cc];
+    if (bias) { v.x += bias[n]; v.y += bias[n + 1]; v.z += bias[n + 2]; v.w += bias[n + 3]; }
+    if (res) {
+      const float4 rv = *(const float4*)(res + o + n);
+      v.x += rv.x; v.y += rv.y; v.z += rv.z; v.w += rv.w;
+    }
+    if (a.relu) { v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f); }
+    *(float4*)(out + o + n) = v;
+  }
+}
+
 // sum of split-K slabs ws[z][g][m][n] (fixed z order) + bias (+ residual) (ReLU), valid rows
 __global__ __launch_bounds__(256) void xsplitk_reduce_kernel(const float* __restrict__ ws, int S, long long zstride,
                                                              long long gstride, const int* __restrict__ nvalid, int N,
@@ -469,45 +663,58 @@ __global__ __launch_bounds__(256) void xwgrad_kernel(const XWArgs a) {
   }
 
   float dv[2][4][4], xv[2][4][4];   // [stage][m][n or k]
+  // bounds-checked buffer loads (32-bit in-replica offsets: checked on the host)
+  const __amdgpu_buffer_rsrc_t rD = rsrc(dy, (long long)a.N * HoWo * a.Cout * 4);
+  const __amdgpu_buffer_rsrc_t rX = rsrc(x, (long long)a.N * a.H * a.W * a.Cin * 4);
   auto gload = [&](int mt, int st) {
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int m = mt + m4 * 4 + r;
-      const bool mv = m < me;
-      // dy
-      if (dact) {
-        if (VEC == 4) {
-          float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-          if (mv && dn < a.Cout) v = *(const float4*)(dy + (long long)m * a.Cout + dn);
-          dv[st][r][0] = v.x; dv[st][r][1] = v.y; dv[st][r][2] = v.z; dv[st][r][3] = v.w;
-        } else {
-#pragma unroll
-          for (int e = 0; e < 4; ++e)
-            dv[st][r][e] = (mv && dn + e < a.Cout) ? dy[(long long)m * a.Cout + dn + e] : 0.f;
-        }
-      }
-      // x (im2col row m)
+    const int m0 = mt + m4 * 4;
+    if constexpr (VEC == 4) {
+      // the 4 rows are consecutive output pixels of one output row (Wo % 4 == 0): decode once
       int img = 0, p = 0, q = 0;
-      if (mv) {
-        img = fdiv(m, a.dHoWo);
-        const int rem = m - img * HoWo;
+      if (m0 < me) {
+        img = fdiv(m0, a.dHoWo);
+        const int rem = m0 - img * HoWo;
         p = fdiv(rem, a.dWo);
         q = rem - p * a.Wo;
       }
-      const int hb = p * a.stride - a.pad, wb = q * a.stride - a.pad;
-      if (VEC == 4) {
-        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-        const int h = hb + xkh[0], w = wb + xkw[0];
-        if (mv && xkv[0] && (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W)
-          v = *(const float4*)(x + (((long long)img * a.H + h) * a.W + w) * a.Cin + xc[0]);
+      const int h = p * a.stride - a.pad + xkh[0];
+      const bool hok = xkv[0] && (unsigned)h < (unsigned)a.H;
+      const int xrow = (img * a.H + h) * a.W;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const bool mv = m0 + r < me;
+        if (dact) {
+          const float4 v = bload4(rD, (mv && dn < a.Cout) ? ((m0 + r) * a.Cout + dn) * 4 : kOOB);
+          dv[st][r][0] = v.x; dv[st][r][1] = v.y; dv[st][r][2] = v.z; dv[st][r][3] = v.w;
+        }
+        const int w = (q + r) * a.stride - a.pad + xkw[0];
+        const bool ok = mv && hok && (unsigned)w < (unsigned)a.W;
+        const float4 v = bload4(rX, ok ? ((xrow + w) * a.Cin + xc[0]) * 4 : kOOB);
         xv[st][r][0] = v.x; xv[st][r][1] = v.y; xv[st][r][2] = v.z; xv[st][r][3] = v.w;
-      } else {
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + r;
+        const bool mv = m < me;
+        if (dact) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            dv[st][r][e] = bload1(rD, (mv && dn + e < a.Cout) ? (m * a.Cout + dn + e) * 4 : kOOB);
+        }
+        int img = 0, p = 0, q = 0;
+        if (mv) {
+          img = fdiv(m, a.dHoWo);
+          const int rem = m - img * HoWo;
+          p = fdiv(rem, a.dWo);
+          q = rem - p * a.Wo;
+        }
+        const int hb = p * a.stride - a.pad, wb = q * a.stride - a.pad;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const int h = hb + xkh[e], w = wb + xkw[e];
-          xv[st][r][e] = (mv && xkv[e] && (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W)
-                             ? x[(((long long)img * a.H + h) * a.W + w) * a.Cin + xc[e]]
-                             : 0.f;
+          const bool ok = mv && xkv[e] && (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W;
+          xv[st][r][e] = bload1(rX, ok ? (((img * a.H + h) * a.W + w) * a.Cin + xc[e]) * 4 : kOOB);
         }
       }
     }
@@ -588,6 +795,33 @@ __global__ __launch_bounds__(256) void xwgrad_reduce_kernel(const float* __restr
     float v = 0.f;
     for (int z = 0; z < nz; ++z) v += ws[((long long)z * G + g) * per + e];
     dw[(long long)g * dw_gstride + e] += v;
+  }
+}
+
+// the deferred weight-gradient reductions of a whole backward pass in one launch
+// (blockIdx.y = descriptor, blockIdx.z = replica): same fixed z order as xwgrad_reduce_kernel
+struct XWRDesc {   // all int64 (built from a torch int64 host tensor)
+  long long ws, dw, dw_gstride, per, nvalid, N, HoWo, mchunk, G, unused;
+};
+constexpr int kXWRBatch = 24;
+struct XWRBatch {
+  XWRDesc d[kXWRBatch];
+};
+
+__global__ __launch_bounds__(256) void xwgrad_reduce_batch_kernel(const XWRBatch b) {
+  const XWRDesc& d = b.d[blockIdx.y];
+  const int g = blockIdx.z;
+  if (g >= (int)d.G) return;
+  const int* nvalid = (const int*)d.nvalid;
+  const int Mv = valid_rows(nvalid, g, (int)d.N) * (int)d.HoWo;
+  const int nz = (Mv + (int)d.mchunk - 1) / (int)d.mchunk;
+  if (nz == 0) return;
+  const float* __restrict__ ws = (const float*)d.ws;
+  float* __restrict__ dw = (float*)d.dw;
+  for (long long e = blockIdx.x * 256LL + threadIdx.x; e < d.per; e += (long long)gridDim.x * 256) {
+    float v = 0.f;
+    for (int z = 0; z < nz; ++z) v += ws[((long long)z * d.G + g) * d.per + e];
+    dw[(long long)g * d.dw_gstride + e] += v;
   }
 }
 
@@ -689,6 +923,34 @@ int xconv_tile(const XArgs& a, long long Mmax, int G, int nclass, int bm, hipStr
   return xconv_go<128, 128, 2, 2, P, VEC>(a, Mmax, G, nclass, st);
 }
 
+bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+template <int W, int CS, int BM, int BN, int WM, int WN, int P>
+int xhalo_go(const XArgs& a, int G, hipStream_t st) {
+  XArgs b = a;
+  b.tiles_n = ceil_div(a.Ncol, BN);
+  const dim3 grid((unsigned)(a.N * (a.Ho / (BM / W)) * b.tiles_n), G, 1);
+  hipLaunchKernelGGL((xhalo_kernel<W, CS, BM, BN, WM, WN, P>), grid, dim3(256), 0, st, b);
+  DBA_LAUNCH_CHECK();
+}
+
+// the halo kernel's shapes: 3x3 stride-1 pad-1 (fwd) or its stride-1 data gradient, one class,
+// square W 32, Cs 32, Ncol <= 32, aligned fp32 operands (DBA_F32_HALO=0 off)
+int xhalo_try(const XArgs& a, int G, int KH, int KW, hipStream_t st) {
+  static const bool off = env_int("DBA_F32_HALO", 1) == 0;
+  const XClass& c = a.cls[0];
+  if (off || KH != 3 || KW != 3 || a.sp != 1 || a.os != 1 || a.splitk != 1 || c.nI != 3 || c.nJ != 3) return -100;
+  if (!(a.dsg == 1 ? (c.bh == -1 && c.bw == -1) : (c.bh == 1 && c.bw == 1))) return -100;
+  if (a.Hs != a.Ho || a.Ws != a.Wo || a.Ho != a.Wo || (a.Ncol & 3) != 0) return -100;
+  if (!aligned16(a.src) || !aligned16(a.w) || a.src_gstride % 4 || a.w_sstride % 4) return -100;
+  const bool p2 = planes() == 2;
+  if (a.Wo == 32 && a.Cs == 32 && a.Ncol <= 32 && a.Ho % 4 == 0)
+    return p2 ? xhalo_go<32, 32, 128, 32, 4, 1, 2>(a, G, st) : xhalo_go<32, 32, 128, 32, 4, 1, 3>(a, G, st);
+  // (W 16 / Cs 64 as 64x64 halo tiles measured slower than the 128x64 implicit GEMM: 147 vs
+  // 154 TF on the eval layer-2 shape, profiles/kbench_r2_fp32_p3.json — not routed here)
+  return -100;
+}
+
 int xconv_dispatch(const XArgs& a, long long Mmax, int G, int nclass, int vec, hipStream_t st) {
   // small launches (a lone client's grouped step) take 64-row tiles
   const int bn = a.Ncol <= 32 ? 32 : a.Ncol <= 64 ? 64 : 128;
@@ -719,8 +981,6 @@ int xsplitk(long long M, int /*G*/, int Ncol, int K) {
   while (s > 1 && nkt / s < 8) --s;
   return s;
 }
-
-bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
 struct ClassGeom {
   int n;
@@ -782,6 +1042,10 @@ DBA_EXPORT int dba_xconv_fwd(const float* x, long long x_gstride, const float* w
   a.nvalid = nvalid; a.N = N; a.Hs = H; a.Ws = W; a.Cs = Cin; a.Ncol = Cout; a.Ho = Ho; a.Wo = Wo;
   a.sp = stride; a.os = 1; a.dsg = 1; a.relu = relu; a.splitk = 1;
   a.cls[0] = XClass{KH, KW, -pad, -pad, 0, 0, Ho, Wo, 0};
+  if (stride == 1) {
+    const int rc = xhalo_try(a, G, KH, KW, st);
+    if (rc != -100) return rc;
+  }
   const int s = xsplitk(M, G, Cout, K);
   if (s > 1 && ws != nullptr && ws_floats >= (long long)s * G * M * Cout) {
     XArgs b = a;
@@ -821,6 +1085,8 @@ DBA_EXPORT int dba_xconv_dgrad(const float* dy, long long dy_gstride, const floa
     Mmax = std::max(Mmax, (long long)N * cg.c[i].Hq * cg.c[i].Wq);
   }
   if (stride == 1) {
+    const int rc = xhalo_try(a, G, KH, KW, st);
+    if (rc != -100) return rc;
     const long long M = (long long)N * H * W;
     const int s = xsplitk(M, G, Cin, KH * KW * Cout);
     if (s > 1 && ws != nullptr && ws_floats >= (long long)s * G * M * Cin) {
@@ -861,14 +1127,14 @@ DBA_EXPORT int dba_xtranspose(const void* desc, int n, int slots, long long max_
 }
 
 // slab floats dba_xwgrad needs for this shape (0: accumulates straight into dw)
-// The m-chunking (Z slabs) is decided from the PER-REPLICA geometry only (see xsplitk): ~128
-// blocks per replica, chunks of >= 256 rows.
+// The m-chunking (Z slabs) is decided from the PER-REPLICA geometry only (see xsplitk): ~256
+// blocks per replica (a lone client fills the chip), chunks of >= 256 rows.
 DBA_EXPORT long long dba_xwgrad_ws_floats(int G, int N, int Ho, int Wo, int Cin, int Cout, int KH, int KW, int* mchunk_out) {
   const int K = KH * KW * Cin;
   const int bno = Cout <= 32 ? 32 : Cout <= 64 ? 64 : 128;
   const long long tiles = (long long)ceil_div(Cout, bno) * ceil_div(K, 128);
   const long long M = (long long)N * Ho * Wo;
-  const int target = env_int("DBA_F32_WGRAD_BLOCKS", 128);
+  const int target = env_int("DBA_F32_WGRAD_BLOCKS", 256);
   long long Z = std::max(1LL, std::min((target + tiles - 1) / tiles, M / 256));
   int mchunk = (int)((M + Z - 1) / Z);
   mchunk = (mchunk + 31) / 32 * 32;
@@ -878,10 +1144,12 @@ DBA_EXPORT long long dba_xwgrad_ws_floats(int G, int N, int Ho, int Wo, int Cin,
 }
 
 // dw[g] += sum_m dy (x) im2col(x) (fp32, deterministic); dw [G][Cout][KH][KW][Cin] rows
+// defer != 0: the slab reduction (Z > 1) is left to dba_xwgrad_reduce_batch (one launch for
+// the whole backward pass)
 DBA_EXPORT int dba_xwgrad(const float* dy, long long dy_gstride, const float* x, long long x_gstride, float* dw,
                           long long dw_gstride, const int* nvalid, int G, int N, int H, int W, int Cin, int Ho,
                           int Wo, int Cout, int KH, int KW, int stride, int pad, float* ws, long long ws_floats,
-                          void* stream) {
+                          int defer, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   int mchunk = 0;
   const long long need = dba_xwgrad_ws_floats(G, N, Ho, Wo, Cin, Cout, KH, KW, &mchunk);
@@ -896,8 +1164,9 @@ DBA_EXPORT int dba_xwgrad(const float* dy, long long dy_gstride, const float* x,
   a.dHoWo = FDiv{Ho * Wo, 1.0f / (float)(Ho * Wo)};
   a.dWo = FDiv{Wo, 1.0f / (float)Wo};
   a.tiles_k = ceil_div(a.K, 128);
-  const bool v4 = Cin % 4 == 0 && Cout % 4 == 0 && aligned16(dy) && aligned16(x) && dy_gstride % 4 == 0 &&
-                  x_gstride % 4 == 0;
+  if ((long long)N * Ho * Wo * Cout >= (1LL << 29) || (long long)N * H * W * Cin >= (1LL << 29)) return -103;
+  const bool v4 = Cin % 4 == 0 && Cout % 4 == 0 && Wo % 4 == 0 && aligned16(dy) && aligned16(x) &&
+                  dy_gstride % 4 == 0 && x_gstride % 4 == 0;
   const int bno = Cout <= 32 ? 32 : Cout <= 64 ? 64 : 128;
   const dim3 grid((unsigned)(ceil_div(Cout, bno) * a.tiles_k), G, Z);
 #define XW_GO(BNO_, WN__, WK__, P_, V_) \
@@ -915,7 +1184,7 @@ DBA_EXPORT int dba_xwgrad(const float* dy, long long dy_gstride, const float* x,
   }
 #undef XW_P
 #undef XW_GO
-  if (Z > 1) {
+  if (Z > 1 && !defer) {
     const long long per = (long long)Cout * a.K;
     const dim3 g2((unsigned)std::max(1LL, std::min(1024LL, (per + 255) / 256)), G);
     hipLaunchKernelGGL(xwgrad_reduce_kernel, g2, dim3(256), 0, st, (const float*)ws, G, per, nvalid, N, Ho * Wo,
@@ -929,4 +1198,19 @@ DBA_EXPORT int dba_xcolsum(const float* dy, long long dy_gstride, int rows_per_i
   hipLaunchKernelGGL(xcolsum_kernel, dim3(ceil_div(C, 32), G), dim3(256), 0, (hipStream_t)stream, dy, dy_gstride,
                      rows_per_img, nvalid, N, C, db, db_gstride);
   DBA_LAUNCH_CHECK();
+}
+
+// desc: n x XWRDesc in HOST memory (passed to the kernel by value: safe under graph capture)
+DBA_EXPORT int dba_xwgrad_reduce_batch(const void* desc, int n, int Gmax, long long max_per, void* stream) {
+  const XWRDesc* ds = (const XWRDesc*)desc;
+  for (int i0 = 0; i0 < n; i0 += kXWRBatch) {
+    XWRBatch b{};
+    const int m = std::min(kXWRBatch, n - i0);
+    for (int i = 0; i < m; ++i) b.d[i] = ds[i0 + i];
+    const dim3 grid((unsigned)std::max(1LL, std::min(256LL, (max_per + 255) / 256)), m, Gmax);
+    hipLaunchKernelGGL(xwgrad_reduce_batch_kernel, grid, dim3(256), 0, (hipStream_t)stream, b);
+    const int rc = (int)hipGetLastError();
+    if (rc != 0) return rc;
+  }
+  return 0;
 }

@@ -36,6 +36,7 @@ class Tape:
         self._produced: set = set()
         self._grads: Optional[Dict[int, Tensor]] = None
         self.on_begin: Optional[Callable[[], None]] = None
+        self.on_end: Optional[Callable[[], None]] = None
 
     def record(self, outputs: Tuple[Tensor, ...], inputs: Tuple[Optional[Tensor], ...], bwd: Callable) -> None:
         self.nodes.append((outputs, inputs, bwd))
@@ -69,6 +70,8 @@ class Tape:
         self.nodes.clear()
         self._produced.clear()
         self._grads = None
+        if self.on_end is not None:
+            self.on_end()
 
 
 class Ctx:
@@ -92,8 +95,13 @@ class Ctx:
         # when the backward pass starts (ops.prepare_dgrad_weights)
         self._dgrad_items: List[tuple] = []
         self._wt: Dict[int, Tensor] = {}
+        # weight-gradient slab reductions of the whole backward pass, run as one launch when
+        # it ends (ops.wgrad_flush)
+        self._wdefer: List[tuple] = []
         if self.tape is not None:
             self.tape.on_begin = self._prepare_dgrad
+            self.tape.on_end = lambda: (ops.backend_for(self.state).wgrad_flush(self._wdefer)
+                                        if self._wdefer else None)
         self.dropout_seed = dropout_seed
         self._drop_ctr = 0
         self.act_dtype = act_dtype
@@ -141,7 +149,7 @@ class Ctx:
                                  self.g(bn + ".weight"), self.g(bn + ".bias"),
                                  want_dres=residual is not None)
             dy, dres = r if residual is not None else (r, None)
-            ops.conv2d_wgrad(dy, x, stride, pad, kh, kw, self.g(conv), nvalid=self.nvalid)
+            ops.conv2d_wgrad(dy, x, stride, pad, kh, kw, self.g(conv), nvalid=self.nvalid, defer=self._wdefer)
             dx = None
             if need_dx:
                 # the other consumer of x (shortcut branch) already delivered its gradient
@@ -170,7 +178,7 @@ class Ctx:
         def bwd(dout: Tensor):
             d = ops.relu_mask_bwd(dout, y) if relu else dout
             ops.conv2d_wgrad(d, x, stride, pad, kh, kw, self.g(name),
-                             self.g(bias) if bias is not None else None, nvalid=self.nvalid)
+                             self.g(bias) if bias is not None else None, nvalid=self.nvalid, defer=self._wdefer)
             return (ops.conv2d_dgrad(d, w, self.wsel, stride, pad, in_hw, nvalid=self.nvalid, wt=self._wt.get(k))
                     if need_dx else None,)
 
@@ -203,7 +211,7 @@ class Ctx:
         def bwd(dout: Tensor):
             d = ops.relu_mask_bwd(dout, y) if relu else dout
             ops.conv2d_wgrad(d, x4, 1, 0, 1, 1, gv.reshape(gv.shape[0], gv.shape[1], 1, 1, gv.shape[2]),
-                             self.g(bias), nvalid=self.nvalid)
+                             self.g(bias), nvalid=self.nvalid, defer=self._wdefer)
             return (ops.conv2d_dgrad(d, w, self.wsel, 1, 0, (1, 1), nvalid=self.nvalid, wt=self._wt.get(k))
                     if need_dx else None,)
 

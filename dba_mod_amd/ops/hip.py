@@ -80,7 +80,8 @@ _SIGS = {
     "dba_xconv_dgrad": [_P, _LL, _P, _LL, _P, _P, _P, _LL, _P] + [_I] * 12 + [_P, _LL, _P],
     "dba_xtranspose": [_P, _I, _I, _LL, _P, _P],
     "dba_xwgrad_ws_floats": [_I] * 8 + [_P],
-    "dba_xwgrad": [_P, _LL, _P, _LL, _P, _LL, _P] + [_I] * 12 + [_P, _LL, _P],
+    "dba_xwgrad": [_P, _LL, _P, _LL, _P, _LL, _P] + [_I] * 12 + [_P, _LL, _I, _P],
+    "dba_xwgrad_reduce_batch": [_P, _I, _I, _LL, _P],
 }
 for _name, _args in _SIGS.items():
     _fn = getattr(_L, _name)
@@ -474,18 +475,27 @@ def conv2d_dgrad(dy, w, wsel, stride, pad, in_hw, nvalid=None, out_dtype=None, a
     return dx
 
 
-def conv2d_wgrad(dy, x, stride, pad, kh, kw, dw, dbias=None, nvalid=None):
+def conv2d_wgrad(dy, x, stride, pad, kh, kw, dw, dbias=None, nvalid=None, defer=None):
+    """``defer`` (a list, fp32 family): the slab reduction is queued there and run for the whole
+    backward pass by :func:`wgrad_flush` (one launch instead of one per conv)."""
     dy = _act(dy, None, "wgrad dy")
     x = _act(x, dy.dtype, "wgrad x")
     G, N, Ho, Wo, Cout = dy.shape
     _, _, H, W, Cin = x.shape
     assert dw.dtype == torch.float32 and _inner_contig(dw)
     if dy.dtype == _F32:
-        n = int(_L.dba_xwgrad_ws_floats(G, N, Ho, Wo, Cin, Cout, kh, kw, None))
+        mchunk = ctypes.c_int(0)
+        n = int(_L.dba_xwgrad_ws_floats(G, N, Ho, Wo, Cin, Cout, kh, kw, ctypes.byref(mchunk)))
         wsb = torch.empty(n, dtype=_F32, device=dy.device) if n > 0 else None
+        nv = _i32(nvalid)
         _call("dba_xwgrad", dy.data_ptr(), N * Ho * Wo * Cout, x.data_ptr(), N * H * W * Cin, dw.data_ptr(),
-              dw.stride(0), _ptr(_i32(nvalid)), G, N, H, W, Cin, Ho, Wo, Cout, kh, kw, stride, pad, _ptr(wsb), n,
-              _stream())
+              dw.stride(0), _ptr(nv), G, N, H, W, Cin, Ho, Wo, Cout, kh, kw, stride, pad, _ptr(wsb), n,
+              int(defer is not None and n > 0), _stream())
+        if defer is not None and n > 0:
+            per = Cout * kh * kw * Cin
+            # (keeps the slab workspace and nvalid alive until the flush)
+            defer.append(([wsb.data_ptr(), dw.data_ptr(), dw.stride(0), per, _ptr(nv) or 0, N, Ho * Wo,
+                           mchunk.value, G, 0], wsb, nv))
         if dbias is not None:
             assert dbias.dtype == torch.float32 and dbias.stride(1) == 1
             _call("dba_xcolsum", dy.data_ptr(), N * Ho * Wo * Cout, Ho * Wo, _ptr(_i32(nvalid)), G, N, Cout,
@@ -508,6 +518,17 @@ def conv2d_wgrad(dy, x, stride, pad, kh, kw, dw, dbias=None, nvalid=None):
         assert dbias.dtype == torch.float32 and dbias.stride(1) == 1
         _call("dba_colsum", dy.data_ptr(), N * Ho * Wo * Cout, Ho * Wo, _ptr(_i32(nvalid)), G, N, Cout,
               dbias.data_ptr(), dbias.stride(0), _stream())
+
+
+def wgrad_flush(defer):
+    """Run the weight-gradient slab reductions queued by ``conv2d_wgrad(..., defer=)``."""
+    if not defer:
+        return
+    d = torch.tensor([e[0] for e in defer], dtype=torch.int64)
+    Gmax = max(e[0][8] for e in defer)
+    max_per = max(e[0][3] for e in defer)
+    _call("dba_xwgrad_reduce_batch", d.data_ptr(), len(defer), Gmax, max_per, _stream())
+    defer.clear()
 
 
 # ------------------------------------------------------------------------ batch norm

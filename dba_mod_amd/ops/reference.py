@@ -132,6 +132,12 @@ def conv2d(x: Tensor, w: Tensor, wsel: Optional[Tensor], stride: int, pad: int,
     return torch.stack(outs).to(out_dtype or x.dtype)
 
 
+def wgrad_flush(defer: list) -> None:
+    """Backend hook for deferred weight-gradient reductions; the reference has none."""
+    if defer:
+        defer.clear()
+
+
 def prepare_dgrad_weights(ref: Tensor, items: list) -> dict:
     """Backend hook for pre-transposed data-gradient weights; the reference needs none."""
     return {}
@@ -158,8 +164,10 @@ def conv2d_dgrad(dy: Tensor, w: Tensor, wsel: Optional[Tensor], stride: int, pad
 
 
 def conv2d_wgrad(dy: Tensor, x: Tensor, stride: int, pad: int, kh: int, kw: int,
-                 dw: Tensor, dbias: Optional[Tensor] = None, nvalid: Optional[Tensor] = None) -> None:
-    """dw[g] += sum_rows dy (x) x  (fp32 accumulate into the flat grad buffer view)."""
+                 dw: Tensor, dbias: Optional[Tensor] = None, nvalid: Optional[Tensor] = None,
+                 defer: Optional[list] = None) -> None:
+    """dw[g] += sum_rows dy (x) x  (fp32 accumulate into the flat grad buffer view).
+    ``defer`` (a backend's batched-reduction queue) is unused here: the sum is immediate."""
     G = dy.shape[0]
     cout = dy.shape[-1]
     cin = x.shape[-1]

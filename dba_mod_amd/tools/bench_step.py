@@ -31,10 +31,11 @@ def main(argv=None) -> int:
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--clients", type=int, default=0,
                     help="keep only the k longest clients (k=1: the lone-attacker latency regime)")
+    ap.add_argument("--dtype", choices=("fp32", "bf16"), default="fp32")
     args = ap.parse_args(argv)
     dev = torch.device("cuda")
     p = C.load_params(args.config, {"resumed_model": False, "synthetic_data": True, "overlap_eval": False,
-                                    "start_epoch": args.epoch})
+                                    "start_epoch": args.epoch, "compute_dtype": args.dtype})
     s = Server(p, DistCtx(device=dev), write_outputs=False)
     tr = s.trainer
     agents, adv = select_clients(p, s.wl, args.epoch)
@@ -65,7 +66,7 @@ def main(argv=None) -> int:
         torch.cuda.synchronize()
         for t in range(T):
             times[int(active[t])].append(ev[t][0].elapsed_time(ev[t][1]))
-    out = {"steps": int(T), "groups": G,
+    out = {"steps": int(T), "groups": G, "dtype": args.dtype,
            "ms_per_step_by_active": {k: round(float(np.median(v)), 3) for k, v in sorted(times.items())},
            "steps_by_active": {k: len(v) // args.reps for k, v in sorted(times.items())}}
     print(json.dumps(out))
