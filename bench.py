@@ -29,6 +29,7 @@ import os
 import sys
 import tempfile
 import time
+from typing import Optional
 
 import torch
 
@@ -46,6 +47,16 @@ METRIC = "FL rounds/sec + backdoor ASR & main-task acc, ResNet-18 CIFAR-10 100 c
 BASELINE_ROUNDS_PER_S = 0.0085
 MODEL_NAMES = {"cifar": "ResNet-18 (half-width, CIFAR-10)", "tiny-imagenet-200": "ResNet-18 (Tiny-ImageNet-200)",
                "mnist": "MnistNet (MNIST)", "loan": "LoanNet MLP (LOAN)"}
+
+
+def _split_label(server) -> Optional[dict]:
+    """How the fp32 kernels carry fp32 operands on the bf16/fp16 MFMA (csrc/kernels/xgemm.hip):
+    both modes reach fp32-level error (tests/test_gpu_f32.py)."""
+    if server.dtype != torch.float32 or ops.backend_name(server.device) != "hip":
+        return None
+    names = {2: "bf16x2 (3 MFMA)", 3: "bf16x3 (6 MFMA)", 16: "scaled fp16x2 (3 MFMA)"}
+    return {"train": names.get(server.trainer.split_mode, str(server.trainer.split_mode)),
+            "eval": names.get(ops.hip_module().fp32_mode(), "?")}
 
 
 def main() -> int:
@@ -130,6 +141,7 @@ def main() -> int:
                        "rounds_timed": f"{epoch - args.steps}..{epoch - 1}",
                        "baseline_source": "BASELINE.md §4 reference-design estimate 0.0085 rounds/s"},
             "ops_backend": ops.backend_name(dctx.device),
+            "fp32_split": _split_label(server),
             "global_acc": round(float(last.get("global_acc", 0.0)), 3),
             "global_asr": round(float(last.get("global_asr", 0.0)), 3),
             "rounds": [[int(r["epoch"]), round(float(r.get("global_acc", 0.0)), 2), round(float(r.get("global_asr", 0.0)), 2)]

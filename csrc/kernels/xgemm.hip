@@ -27,6 +27,8 @@
 //   xcolsum         bias gradient (column sums, fixed order).
 #include "common.hpp"
 #include <algorithm>
+#include <type_traits>
+#include <utility>
 #include <cstdlib>
 
 namespace {
@@ -67,6 +69,65 @@ __device__ __forceinline__ void split4(float a, float b, float c, float d, uint2
   }
 }
 
+// ---- fp16 pair split (H mode): x*2^s = h + l + e, h = f16(x*2^s), l = f16(x*2^s - h),
+// |e| <= 2^-22 |x| (11 significant bits per plane against bf16's 8), 3 MFMAs per product
+// (hh + hl + lh; the dropped ll term is <= 2^-22 |xy|).  fp16's exponent range is narrow, so
+// each operand is scaled by a power of two fixed for the whole launch, chosen from the
+// operand's max |x| (per replica / weight slot, computed by dba_amax or fused into the
+// producing kernel): max * 2^s in [2^14, 2^15).  Scaling is exact, and the accumulators'
+// 2^(sa+sb) is removed exactly in the epilogue; elements below max * 2^-17 keep an absolute
+// error under max * 2^-40.
+typedef __attribute__((ext_vector_type(2))) _Float16 f16x2v;
+typedef __attribute__((ext_vector_type(8))) _Float16 f16x8_t;
+
+__device__ __forceinline__ uint32_t cvt_pkh(float a, float b) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2v){a, b}, f16x2v));
+}
+__device__ __forceinline__ f32x2v unpkh(uint32_t u) {
+  return __builtin_convertvector(__builtin_bit_cast(f16x2v, u), f32x2v);
+}
+__device__ __forceinline__ void split4h(float a, float b, float c, float d, float sc, uint2 (&o)[2]) {
+  a *= sc; b *= sc; c *= sc; d *= sc;   // exact (power of two)
+  const uint32_t h0 = cvt_pkh(a, b), h1 = cvt_pkh(c, d);
+  const f32x2v u0 = unpkh(h0), u1 = unpkh(h1);
+  o[0] = make_uint2(h0, h1);
+  o[1] = make_uint2(cvt_pkh(a - u0.x, b - u0.y), cvt_pkh(c - u1.x, d - u1.y));   // exact residuals
+}
+constexpr int kSMax = 100;   // scale exponent cap (operands below 2^-85 stay unnormalised)
+// scale exponent for a max |x| given as float bits (0 / subnormal max: the cap)
+__device__ __forceinline__ int hexp(int maxbits) {
+  return min(kSMax, 141 - (__builtin_amdgcn_readfirstlane(maxbits) >> 23));
+}
+// fold a thread's max |y| of the values it wrote into amax[g] (one atomic per wave: integer max
+// of non-negative float bits, exact and order-independent)
+__device__ __forceinline__ void amax_fold(int* amax, int g, float m) {
+  m = wave_max(m);
+  // the atomic only when the wave's max beats the value seen (a stale read costs one extra
+  // atomic): thousands of blocks fold into one word per replica, and most are below it
+  if ((threadIdx.x & 63) == 0 && m > 0.f && __float_as_int(m) > __hip_atomic_load(amax + g, __ATOMIC_RELAXED,
+                                                                                      __HIP_MEMORY_SCOPE_AGENT))
+    atomicMax(amax + g, __float_as_int(m));
+}
+struct HScale {
+  float ma = 1.f, mb = 1.f;   // fill multipliers 2^sa, 2^sb
+  int s = 0;                  // the accumulators hold sum * 2^s
+  __device__ __forceinline__ void init(int maxa, int maxb) {
+    const int sa = hexp(maxa), sb = hexp(maxb);
+    ma = __uint_as_float((uint32_t)(sa + 127) << 23);
+    mb = __uint_as_float((uint32_t)(sb + 127) << 23);
+    s = sa + sb;
+  }
+  template <int MI, int NJ>
+  __device__ __forceinline__ void finish(f32x16_t (&acc)[MI][NJ]) const {
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][j][r] = ldexpf(acc[i][j][r], -s);
+  }
+};
+
 // LDS images: per plane, rows of 32 reduction elements (64 B = 4 x 16-B chunks).  A row's
 // 16-B chunk c is stored at chunk c ^ swz so the ds_read_b128 fragment reads (lane groups
 // {0-3,12-15,20-27} / {4-11,16-19,28-31}) hit 16 distinct bank slots.
@@ -90,45 +151,84 @@ __device__ __forceinline__ int pswz(int n) {
 // ``fill(q)`` (q = 0 .. NQ-1) is staging work of the NEXT step (split + LDS stores of one
 // 4-element quarter per call), spread evenly between the MFMAs so the VALU split and the
 // ds_write traffic issue in the MFMA gaps instead of after them.
-template <int MI, int NJ, int P, bool ROWPERM, int RA, int RB, int NQ, typename Fill>
+// one 32x32x16 MFMA on split planes: bf16 or (H) fp16 operands
+template <bool H>
+__device__ __forceinline__ f32x16_t mfma16(const uint4& a, const uint4& b, const f32x16_t& c) {
+  if constexpr (H)
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8_t, a), __builtin_bit_cast(f16x8_t, b), c,
+                                                  0, 0, 0);
+  else
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, a), __builtin_bit_cast(bf16x8_t, b),
+                                                   c, 0, 0, 0);
+}
+
+// compile-time loop: f(std::integral_constant<int, 0>) ... f(integral_constant<N-1>)
+template <typename F, int... I>
+__device__ __forceinline__ void sfor_impl(F&& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, typename F>
+__device__ __forceinline__ void sfor(F&& f) {
+  sfor_impl(f, std::make_integer_sequence<int, N>{});
+}
+// plane product p of the P-plane split (total order <= P-1, the small ones first)
+constexpr int prod_pa(int P, int p) {
+  int k = 0;
+  for (int s = P - 1; s >= 0; --s)
+    for (int pa = 0; pa <= s; ++pa, ++k)
+      if (k == p) return pa;
+  return 0;
+}
+constexpr int prod_pb(int P, int p) {
+  int k = 0;
+  for (int s = P - 1; s >= 0; --s)
+    for (int pa = 0; pa <= s; ++pa, ++k)
+      if (k == p) return s - pa;
+  return 0;
+}
+
+// the MFMAs of half-step KK (16 reduction elements) of a wave's MI x NJ tiles, with the
+// staging fills fill(q) (q = 0 .. NQ-1, compile-time constants) of the NEXT step spread evenly
+// between them, so the VALU split / ds_write / reload traffic issues in the MFMA gaps
+template <int MI, int NJ, int P, bool H, int NQ, int KK, typename Fill>
+__device__ __forceinline__ void mma_half(const uint4 (&af)[P][MI], const uint4 (&bfr)[P][NJ],
+                                         f32x16_t (&acc)[MI][NJ], Fill&& fill) {
+  constexpr int PER = P * (P + 1) / 2 * MI * NJ, T = 2 * PER;   // MFMAs per half / whole step
+  sfor<PER>([&](auto C) __attribute__((always_inline)) {
+    constexpr int c = decltype(C)::value;
+    constexpr int p = c / (MI * NJ), i = (c / NJ) % MI, j = c % NJ;
+    acc[i][j] = mfma16<H>(af[prod_pa(P, p)][i], bfr[prod_pb(P, p)][j], acc[i][j]);
+    constexpr int cnt = KK * PER + c + 1;
+    sfor<NQ>([&](auto Q) __attribute__((always_inline)) {
+      constexpr int q = decltype(Q)::value;
+      if constexpr (cnt * NQ >= (q + 1) * T && (cnt - 1) * NQ < (q + 1) * T) fill(q);
+    });
+  });
+}
+
+template <int MI, int NJ, int P, bool H, bool ROWPERM, int RA, int RB, int NQ, typename Fill>
 __device__ __forceinline__ void mma_step(const uint4* __restrict__ L, int PL, int arow0, int brow0,
                                          f32x16_t (&acc)[MI][NJ], int lane, Fill&& fill) {
-  constexpr int T = 2 * P * (P + 1) / 2 * MI * NJ;   // MFMAs per step
   const int fr = lane & 31, hf = lane >> 5;
-  int cnt = 0, q = 0;
-#pragma unroll
-  for (int kk = 0; kk < 2; ++kk) {
-    const int ch = kk * 2 + hf;
-    bf16x8_t af[P][MI], bfr[P][NJ];
+  sfor<2>([&](auto KK) __attribute__((always_inline)) {
+    const int ch = decltype(KK)::value * 2 + hf;
+    uint4 af[P][MI], bfr[P][NJ];
 #pragma unroll
     for (int i = 0; i < MI; ++i) {
       const int n = arow0 + i * 32 + fr;
       const int o = prow<ROWPERM, RA>(n) * 4 + (ch ^ pswz<ROWPERM>(n));
 #pragma unroll
-      for (int p = 0; p < P; ++p) af[p][i] = *(const bf16x8_t*)&L[p * PL + o];
+      for (int p = 0; p < P; ++p) af[p][i] = L[p * PL + o];
     }
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
       const int n = brow0 + j * 32 + fr;
       const int o = (RA + prow<ROWPERM, RB>(n)) * 4 + (ch ^ pswz<ROWPERM>(n));
 #pragma unroll
-      for (int p = 0; p < P; ++p) bfr[p][j] = *(const bf16x8_t*)&L[p * PL + o];
+      for (int p = 0; p < P; ++p) bfr[p][j] = L[p * PL + o];
     }
-    // plane products of total order <= P-1, the small ones first
-#pragma unroll
-    for (int s = P - 1; s >= 0; --s)
-#pragma unroll
-      for (int pa = 0; pa <= s; ++pa)
-#pragma unroll
-        for (int i = 0; i < MI; ++i)
-#pragma unroll
-          for (int j = 0; j < NJ; ++j) {
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[pa][i], bfr[s - pa][j], acc[i][j], 0, 0, 0);
-            ++cnt;
-            if (q < NQ && cnt * NQ >= (q + 1) * T) fill(q++);   // constant-folded after unrolling
-          }
-  }
-  while (q < NQ) fill(q++);
+    mma_half<MI, NJ, P, H, NQ, decltype(KK)::value>(af, bfr, acc, fill);
+  });
 }
 
 // store the P planes of 4 consecutive reduction elements (8-B slot q of logical row n)
@@ -160,11 +260,15 @@ struct XArgs {
   int sp, os, dsg, relu;
   int splitk, tiles_n;
   long long zstride;                         // split-K: slab z at out + z * zstride
+  const int* amax_src;                       // H: max |src| bits per replica [G]
+  const int* amax_w;                         // H: max |w| bits per weight slot
+  int* amax_out;                             // optional: max |out| bits per replica (+= by max)
   XClass cls[4];
 };
 
-template <int BM, int BN, int WM, int WN, int P, int VEC>
+template <int BM, int BN, int WM, int WN, int P, int VEC, bool H>
 __global__ __launch_bounds__(256) void xconv_kernel(const XArgs a) {
+  static_assert(!H || P == 2, "fp16 split: 2 planes");
   constexpr int TM = BM / WM, TN = BN / WN, MI = TM / 32, NJ = TN / 32;
   static_assert(WM * WN == 4 && MI >= 1 && NJ >= 1, "wave tiling");
   constexpr int ROWS = BM + BN, PL = ROWS * 4;   // uint4 per plane image
@@ -238,45 +342,34 @@ __global__ __launch_bounds__(256) void xconv_kernel(const XArgs a) {
     ki = t / c.nJ;
     kj = t - ki * c.nJ;
   }
-  // two register stages: the global loads of step kt+2 are in flight while step kt+1 (loaded
-  // one step earlier) is split into the other LDS buffer in the gaps of step kt's MFMAs
+  // two register stages: step kt+1 (stage (kt+1)&1) is split into the other LDS buffer in the
+  // gaps of step kt's MFMAs, and each quarter's registers are reloaded with step kt+3 right
+  // after its split, so a load has ~2 MFMA steps to land
   float4 ra[2][RA], rb[2][RB];
-  auto gload = [&](int st) {   // the step at the current reduction state, then advance it
-    const int kb = (ki * c.nJ + kj) * Cs + kc;   // == kt*32 + kq*4
+  int g_kb = 0, g_toff = 0, g_dh = 0, g_dw = 0;   // VEC >= 4: the prepared step's geometry
+  bool g_kv = false;
+  int e_off[4], e_dh[4], e_dw[4];                 // VEC 1: per element
+  bool e_kv[4];
+  auto gprep = [&]() __attribute__((always_inline)) {   // the step at the current reduction state, then advance it
+    g_kb = (ki * c.nJ + kj) * Cs + kc;   // == kt*32 + kq*4
     if constexpr (VEC >= 4) {
-      const bool kv = ki < c.nI;
-      const int dh = a.dsg * ki, dw = a.dsg * kj;
-      const int toff = (dh * a.Ws + dw) * Cs + kc;   // uniform across the rows
-#pragma unroll
-      for (int i = 0; i < RA; ++i) {
-        const bool ok = kv && (unsigned)(ah[i] + dh) < (unsigned)a.Hs && (unsigned)(aw[i] + dw) < (unsigned)a.Ws;
-        ra[st][i] = bload4(rA, ok ? (abase[i] + toff) * 4 : kOOB);
-      }
-#pragma unroll
-      for (int j = 0; j < RB; ++j) rb[st][j] = bload4(rB, (boffs[j] >= 0 && kb < K) ? (boffs[j] + kb) * 4 : kOOB);
+      g_kv = ki < c.nI;
+      g_dh = a.dsg * ki;
+      g_dw = a.dsg * kj;
+      g_toff = (g_dh * a.Ws + g_dw) * Cs + kc;   // uniform across the rows
     } else {
-      float va[RA][4], vb[RB][4];
       int ii = ki, jj = kj, cc = kc;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const bool kv = ii < c.nI;
-        const int dh = a.dsg * ii, dw = a.dsg * jj;
-#pragma unroll
-        for (int i = 0; i < RA; ++i) {
-          const bool ok = kv && (unsigned)(ah[i] + dh) < (unsigned)a.Hs && (unsigned)(aw[i] + dw) < (unsigned)a.Ws;
-          va[i][e] = bload1(rA, ok ? (abase[i] + (dh * a.Ws + dw) * Cs + cc) * 4 : kOOB);
-        }
-#pragma unroll
-        for (int j = 0; j < RB; ++j) vb[j][e] = bload1(rB, (boffs[j] >= 0 && kb + e < K) ? (boffs[j] + kb + e) * 4 : kOOB);
+        e_kv[e] = ii < c.nI;
+        e_dh[e] = a.dsg * ii;
+        e_dw[e] = a.dsg * jj;
+        e_off[e] = (e_dh[e] * a.Ws + e_dw[e]) * Cs + cc;
         if (++cc == Cs) {
           cc = 0;
           if (++jj == c.nJ) { jj = 0; ++ii; }
         }
       }
-#pragma unroll
-      for (int i = 0; i < RA; ++i) ra[st][i] = make_float4(va[i][0], va[i][1], va[i][2], va[i][3]);
-#pragma unroll
-      for (int j = 0; j < RB; ++j) rb[st][j] = make_float4(vb[j][0], vb[j][1], vb[j][2], vb[j][3]);
     }
     // k += 32 (Cs % 32 == 0: at most one tap boundary)
     kc += 32;
@@ -292,16 +385,52 @@ __global__ __launch_bounds__(256) void xconv_kernel(const XArgs a) {
       }
     }
   };
+  auto gq = [&](int st, int q) __attribute__((always_inline)) {   // quarter q (A rows first) of the prepared step -> stage st
+    if (q < RA) {
+      if constexpr (VEC >= 4) {
+        const bool ok = g_kv && (unsigned)(ah[q] + g_dh) < (unsigned)a.Hs && (unsigned)(aw[q] + g_dw) < (unsigned)a.Ws;
+        ra[st][q] = bload4(rA, ok ? (abase[q] + g_toff) * 4 : kOOB);
+      } else {
+        float v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const bool ok = e_kv[e] && (unsigned)(ah[q] + e_dh[e]) < (unsigned)a.Hs &&
+                          (unsigned)(aw[q] + e_dw[e]) < (unsigned)a.Ws;
+          v[e] = bload1(rA, ok ? (abase[q] + e_off[e]) * 4 : kOOB);
+        }
+        ra[st][q] = make_float4(v[0], v[1], v[2], v[3]);
+      }
+    } else {
+      const int j = q - RA;
+      if constexpr (VEC >= 4) {
+        rb[st][j] = bload4(rB, (boffs[j] >= 0 && g_kb < K) ? (boffs[j] + g_kb) * 4 : kOOB);
+      } else {
+        float v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = bload1(rB, (boffs[j] >= 0 && g_kb + e < K) ? (boffs[j] + g_kb + e) * 4 : kOOB);
+        rb[st][j] = make_float4(v[0], v[1], v[2], v[3]);
+      }
+    }
+  };
+  auto gload = [&](int st) __attribute__((always_inline)) {
+    gprep();
+#pragma unroll
+    for (int q = 0; q < RA + RB; ++q) gq(st, q);
+  };
   // quarter q of stage st -> LDS buffer buf
-  auto lput_q = [&](int buf, int st, int q) {
+  HScale hs;
+  if constexpr (H) hs.init(a.amax_src[g], a.amax_w[slot]);
+  auto lput_q = [&](int buf, int st, int q) __attribute__((always_inline)) {
     uint4* L = lds + buf * P * PL;
     uint2 sp[P];
     if (q < RA) {
-      split4<P>(ra[st][q].x, ra[st][q].y, ra[st][q].z, ra[st][q].w, sp);
+      if constexpr (H) split4h(ra[st][q].x, ra[st][q].y, ra[st][q].z, ra[st][q].w, hs.ma, sp);
+      else split4<P>(ra[st][q].x, ra[st][q].y, ra[st][q].z, ra[st][q].w, sp);
       lds_put<P, false, BM>(L, PL, 0, r0 + 32 * q, kq, sp);
     } else {
       const int j = q - RA;
-      split4<P>(rb[st][j].x, rb[st][j].y, rb[st][j].z, rb[st][j].w, sp);
+      if constexpr (H) split4h(rb[st][j].x, rb[st][j].y, rb[st][j].z, rb[st][j].w, hs.mb, sp);
+      else split4<P>(rb[st][j].x, rb[st][j].y, rb[st][j].z, rb[st][j].w, sp);
       lds_put<P, false, BN>(L, PL, BM, r0 + 32 * j, kq, sp);
     }
   };
@@ -319,24 +448,32 @@ __global__ __launch_bounds__(256) void xconv_kernel(const XArgs a) {
     // has no branches and the accumulators stay in place across iterations
     gload(0);
     gload(1);
+    gprep();   // step kt0+2
 #pragma unroll
-    for (int q = 0; q < RA + RB; ++q) lput_q(0, 0, q);
+    for (int q = 0; q < RA + RB; ++q) {
+      lput_q(0, 0, q);
+      gq(0, q);
+    }
     __syncthreads();
     // step kt (offset from kt0 even: LDS buffer 0, successor in register stage 1; odd: swapped)
     int kt = kt0;
     for (; kt + 1 < kt1; kt += 2) {
-      gload(0);
-      mma_step<MI, NJ, P, false, BM, BN, RA + RB>(lds, PL, wm * TM, wn * TN, acc, lane,
-                                                  [&](int q) { lput_q(1, 1, q); });
+      gprep();   // step kt+3
+      mma_step<MI, NJ, P, H, false, BM, BN, RA + RB>(lds, PL, wm * TM, wn * TN, acc, lane, [&](int q) __attribute__((always_inline)) {
+        lput_q(1, 1, q);
+        gq(1, q);
+      });
       __syncthreads();
-      gload(1);
-      mma_step<MI, NJ, P, false, BM, BN, RA + RB>(lds + P * PL, PL, wm * TM, wn * TN, acc, lane,
-                                                  [&](int q) { lput_q(0, 0, q); });
+      gprep();   // step kt+4
+      mma_step<MI, NJ, P, H, false, BM, BN, RA + RB>(lds + P * PL, PL, wm * TM, wn * TN, acc, lane, [&](int q) __attribute__((always_inline)) {
+        lput_q(0, 0, q);
+        gq(0, q);
+      });
       __syncthreads();
     }
-    if (kt < kt1)
-      mma_step<MI, NJ, P, false, BM, BN, 0>(lds, PL, wm * TM, wn * TN, acc, lane, [&](int) {});
+    if (kt < kt1) mma_step<MI, NJ, P, H, false, BM, BN, 0>(lds, PL, wm * TM, wn * TN, acc, lane, [&](int) {});
   }
+  if constexpr (H) hs.finish(acc);
 
   // ---- epilogue: fp32 tile through LDS, row-contiguous stores with bias / residual / ReLU
   __syncthreads();
@@ -355,6 +492,7 @@ __global__ __launch_bounds__(256) void xconv_kernel(const XArgs a) {
   const float* bias = (fin && a.bias) ? a.bias + (long long)slot * a.b_sstride : nullptr;
   const float* res = (fin && a.res) ? a.res + (long long)g * a.out_gstride : nullptr;
   const bool relu = fin && a.relu;
+  float vmax = 0.f;
   if ((a.Ncol & 3) == 0) {
     constexpr int C4 = BN / 4;
     for (int e = tid; e < BM * C4; e += 256) {
@@ -369,6 +507,7 @@ __global__ __launch_bounds__(256) void xconv_kernel(const XArgs a) {
         v.x += rv.x; v.y += rv.y; v.z += rv.z; v.w += rv.w;
       }
       if (relu) { v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f); }
+      vmax = fmaxf(vmax, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
       *(float4*)(out + o + n) = v;
     }
   } else {
@@ -381,9 +520,11 @@ __global__ __launch_bounds__(256) void xconv_kernel(const XArgs a) {
       if (bias) v += bias[n];
       if (res) v += res[o + n];
       if (relu) v = fmaxf(v, 0.f);
+      vmax = fmaxf(vmax, fabsf(v));
       out[o + n] = v;
     }
   }
+  if (fin && a.amax_out) amax_fold(a.amax_out, g, vmax);
 }
 
 // ======================================================================= halo conv
@@ -401,8 +542,9 @@ __device__ __forceinline__ int hswz(int pp) {
   return (pp >> (CH == 4 ? 2 : 1)) & (CH - 1);
 }
 
-template <int W, int CS, int BM, int BN, int WM, int WN, int P>
+template <int W, int CS, int BM, int BN, int WM, int WN, int P, bool H>
 __global__ __launch_bounds__(256) void xhalo_kernel(const XArgs a) {
+  static_assert(!H || P == 2, "fp16 split: 2 planes");
   constexpr int TR = BM / W, PW = W + 2, PR = TR + 2, PP = PR * PW;
   constexpr int CH = CS / 8, PATCH = PP * CH;             // uint4 per plane
   constexpr int TM = BM / WM, TN = BN / WN, MI = TM / 32, NJ = TN / 32;
@@ -434,23 +576,39 @@ __global__ __launch_bounds__(256) void xhalo_kernel(const XArgs a) {
   if (tid < BM)
     orow[tid] = (((long long)img * a.Ho + h0 + tid / W) * a.Wo + tid % W) * a.Ncol;
 
-  // ---- the input patch: rows h0-1 .. h0+TR, cols -1 .. W, split once into P planes
+  // ---- the input patch: rows h0-1 .. h0+TR, cols -1 .. W, loaded to registers, split once
+  // into P planes (after the block-wide max under H)
+  constexpr int Q4 = CS / 4;                              // float4 quarters per pixel
+  constexpr int NE = (PP * Q4 + 255) / 256;
+  float4 pv[NE];
   {
     const __amdgpu_buffer_rsrc_t rA = rsrc(src, (long long)a.N * a.Hs * a.Ws * CS * 4);
-    constexpr int Q4 = CS / 4;                            // float4 quarters per pixel
-    for (int e = tid; e < PP * Q4; e += 256) {
+#pragma unroll
+    for (int u = 0; u < NE; ++u) {
+      const int e = tid + 256 * u;
       const int pp = e / Q4, q = e - pp * Q4;
       const int pr = pp / PW, pc = pp - pr * PW;
       const int h = h0 - 1 + pr, w = pc - 1;
-      const bool ok = (unsigned)h < (unsigned)a.Hs && (unsigned)w < (unsigned)a.Ws;
-      const float4 v = bload4(rA, ok ? (((img * a.Hs + h) * a.Ws + w) * CS + q * 4) * 4 : kOOB);
+      const bool ok = e < PP * Q4 && (unsigned)h < (unsigned)a.Hs && (unsigned)w < (unsigned)a.Ws;
+      pv[u] = bload4(rA, ok ? (((img * a.Hs + h) * a.Ws + w) * CS + q * 4) * 4 : kOOB);
+    }
+  }
+  HScale hs;
+  if constexpr (H) hs.init(a.amax_src[g], a.amax_w[slot]);
+  auto patch_put = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int u = 0; u < NE; ++u) {
+      const int e = tid + 256 * u;
+      if (e >= PP * Q4) break;
+      const int pp = e / Q4, q = e - pp * Q4;
       uint2 sp[P];
-      split4<P>(v.x, v.y, v.z, v.w, sp);
+      if constexpr (H) split4h(pv[u].x, pv[u].y, pv[u].z, pv[u].w, hs.ma, sp);
+      else split4<P>(pv[u].x, pv[u].y, pv[u].z, pv[u].w, sp);
       const int o = pp * CH + ((q >> 1) ^ hswz<W, CS>(pp));
 #pragma unroll
       for (int p = 0; p < P; ++p) ((uint2*)&patch[p * PATCH + o])[q & 1] = sp[p];
     }
-  }
+  };
 
   // ---- weights: two-stage pipeline (k-step t: tap t / CB, channels (t % CB) * 32 ..)
   int boffs[RB];
@@ -461,15 +619,19 @@ __global__ __launch_bounds__(256) void xhalo_kernel(const XArgs a) {
   }
   const __amdgpu_buffer_rsrc_t rB = rsrc(Bp, (long long)a.Ncol * K * 4);
   float4 rb[2][RB];
-  auto gload = [&](int t, int st) {
+  auto gq = [&](int t, int st, int j) __attribute__((always_inline)) {   // quarter j of weight step t -> stage st
     const int kb = t * 32 + kq * 4;
-#pragma unroll
-    for (int j = 0; j < RB; ++j) rb[st][j] = bload4(rB, (boffs[j] >= 0 && kb < K) ? (boffs[j] + kb) * 4 : kOOB);
+    rb[st][j] = bload4(rB, (boffs[j] >= 0 && kb < K) ? (boffs[j] + kb) * 4 : kOOB);
   };
-  auto lput_q = [&](int buf, int st, int q) {
+  auto gload = [&](int t, int st) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < RB; ++j) gq(t, st, j);
+  };
+  auto lput_q = [&](int buf, int st, int q) __attribute__((always_inline)) {
     if (q >= RB) return;
     uint2 sp[P];
-    split4<P>(rb[st][q].x, rb[st][q].y, rb[st][q].z, rb[st][q].w, sp);
+    if constexpr (H) split4h(rb[st][q].x, rb[st][q].y, rb[st][q].z, rb[st][q].w, hs.mb, sp);
+    else split4<P>(rb[st][q].x, rb[st][q].y, rb[st][q].z, rb[st][q].w, sp);
     lds_put<P, false, BN>(bring + buf * P * BPL, BPL, 0, r0 + 32 * q, kq, sp);
   };
 
@@ -489,59 +651,50 @@ __global__ __launch_bounds__(256) void xhalo_kernel(const XArgs a) {
     const int m = wm * TM + i * 32 + fr;
     apix[i] = (m / W) * PW + (m % W);
   }
-  auto mma = [&](int t, int buf, int stn) {
+  auto mma = [&](int t, int buf, int stn) __attribute__((always_inline)) {
     const int tap = t / CB, cb = t - tap * CB;
     int ti = tap / 3, tj = tap - ti * 3;
     if (flip) { ti = 2 - ti; tj = 2 - tj; }
     const int toff = ti * PW + tj;
     const uint4* L = bring + buf * P * BPL;
-    constexpr int T = 2 * P * (P + 1) / 2 * MI * NJ;
-    int cnt = 0, q = 0;
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      const int ch = kk * 2 + hf;
-      bf16x8_t af[P][MI], bfr[P][NJ];
+    sfor<2>([&](auto KK) __attribute__((always_inline)) {
+      const int ch = decltype(KK)::value * 2 + hf;
+      uint4 af[P][MI], bfr[P][NJ];
 #pragma unroll
       for (int i = 0; i < MI; ++i) {
         const int pp = apix[i] + toff;
         const int o = pp * CH + ((cb * 4 + ch) ^ hswz<W, CS>(pp));
 #pragma unroll
-        for (int p = 0; p < P; ++p) af[p][i] = *(const bf16x8_t*)&patch[p * PATCH + o];
+        for (int p = 0; p < P; ++p) af[p][i] = patch[p * PATCH + o];
       }
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
         const int n = wn * TN + j * 32 + fr;
         const int o = n * 4 + (ch ^ ((n >> 2) & 3));
 #pragma unroll
-        for (int p = 0; p < P; ++p) bfr[p][j] = *(const bf16x8_t*)&L[p * BPL + o];
+        for (int p = 0; p < P; ++p) bfr[p][j] = L[p * BPL + o];
       }
-#pragma unroll
-      for (int s = P - 1; s >= 0; --s)
-#pragma unroll
-        for (int pa = 0; pa <= s; ++pa)
-#pragma unroll
-          for (int i = 0; i < MI; ++i)
-#pragma unroll
-            for (int j = 0; j < NJ; ++j) {
-              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[pa][i], bfr[s - pa][j], acc[i][j], 0, 0, 0);
-              ++cnt;
-              if (q < RB && cnt * RB >= (q + 1) * T) lput_q(buf ^ 1, stn, q++);
-            }
-    }
-    while (q < RB) lput_q(buf ^ 1, stn, q++);
+      mma_half<MI, NJ, P, H, RB, decltype(KK)::value>(af, bfr, acc, [&](int q) __attribute__((always_inline)) {
+        lput_q(buf ^ 1, stn, q);
+        gq(t + 3, stn, q);   // reload: step t+3 (past NK: zero-filled, never read)
+      });
+    });
   };
+
 
   gload(0, 0);
   gload(1, 1);
+  patch_put();
 #pragma unroll
-  for (int q = 0; q < RB; ++q) lput_q(0, 0, q);
+  for (int q = 0; q < RB; ++q) {
+    lput_q(0, 0, q);
+    gq(2, 0, q);
+  }
   __syncthreads();   // patch + first weight step
   int t = 0;
   for (; t + 1 < NK; t += 2) {
-    gload(t + 2, 0);
     mma(t, 0, 1);
     __syncthreads();
-    gload(t + 3, 1);
     mma(t + 1, 1, 0);
     __syncthreads();
   }
@@ -549,6 +702,7 @@ __global__ __launch_bounds__(256) void xhalo_kernel(const XArgs a) {
     mma(t, 0, 1);   // (its filler writes a buffer nobody reads)
     __syncthreads();
   }
+  if constexpr (H) hs.finish(acc);
 
   // ---- epilogue through the (drained) patch memory
   float* Ct = reinterpret_cast<float*>(patch);
@@ -564,6 +718,7 @@ __global__ __launch_bounds__(256) void xhalo_kernel(const XArgs a) {
   const float* bias = a.bias ? a.bias + (long long)slot * a.b_sstride : nullptr;
   const float* res = a.res ? a.res + (long long)g * a.out_gstride : nullptr;
   constexpr int C4 = BN / 4;
+  float vmax = 0.f;
   for (int e = tid; e < BM * C4; e += 256) {
     const int row = e / C4, cc = (e - row * C4) * 4;
     const int n = n0 + cc;
@@ -576,8 +731,10 @@ __global__ __launch_bounds__(256) void xhalo_kernel(const XArgs a) {
       v.x += rv.x; v.y += rv.y; v.z += rv.z; v.w += rv.w;
     }
     if (a.relu) { v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f); }
+    vmax = fmaxf(vmax, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
     *(float4*)(out + o + n) = v;
   }
+  if (a.amax_out) amax_fold(a.amax_out, g, vmax);
 }
 
 // sum of split-K slabs ws[z][g][m][n] (fixed z order) + bias (+ residual) (ReLU), valid rows
@@ -586,18 +743,22 @@ __global__ __launch_bounds__(256) void xsplitk_reduce_kernel(const float* __rest
                                                              int HoWo, int Ncol, const float* __restrict__ bias,
                                                              long long b_sstride, const int* __restrict__ wsel,
                                                              const float* __restrict__ res, int relu,
-                                                             float* __restrict__ out) {
+                                                             float* __restrict__ out, int* __restrict__ amax_out) {
   const int g = blockIdx.y;
   const long long total = (long long)valid_rows(nvalid, g, N) * HoWo * Ncol;
   const float* __restrict__ bp = bias ? bias + (long long)(wsel ? wsel[g] : g) * b_sstride : nullptr;
   const long long base = (long long)g * gstride;
+  float vmax = 0.f;
   for (long long e = blockIdx.x * 256LL + threadIdx.x; e < total; e += (long long)gridDim.x * 256) {
     float v = ws[base + e];
     for (int z = 1; z < S; ++z) v += ws[z * zstride + base + e];
     if (bp) v += bp[e % Ncol];
     if (res) v += res[base + e];
-    out[base + e] = relu ? fmaxf(v, 0.f) : v;
+    if (relu) v = fmaxf(v, 0.f);
+    vmax = fmaxf(vmax, fabsf(v));
+    out[base + e] = v;
   }
+  if (amax_out) amax_fold(amax_out, g, vmax);
 }
 
 // ============================================================================ wgrad
@@ -620,11 +781,14 @@ struct XWArgs {
   const int* nvalid;
   int N, H, W, Cin, Ho, Wo, Cout, KW, stride, pad, K;
   int tiles_k, mchunk;
+  const int* amax_dy;                      // H: max |dy| / |x| bits per replica [G]
+  const int* amax_x;
   FDiv dHoWo, dWo;
 };
 
-template <int BNO, int BK, int WN_, int WK_, int P, int VEC>
+template <int BNO, int BK, int WN_, int WK_, int P, int VEC, bool H>
 __global__ __launch_bounds__(256) void xwgrad_kernel(const XWArgs a) {
+  static_assert(!H || P == 2, "fp16 split: 2 planes");
   constexpr int TNo = BNO / WN_, TK = BK / WK_, MI = TNo / 32, NJ = TK / 32;
   static_assert(WN_ * WK_ == 4 && MI >= 1 && NJ >= 1, "wave tiling");
   static_assert(BK == 128, "x micro-tiles: one per thread");
@@ -666,9 +830,20 @@ __global__ __launch_bounds__(256) void xwgrad_kernel(const XWArgs a) {
   // bounds-checked buffer loads (32-bit in-replica offsets: checked on the host)
   const __amdgpu_buffer_rsrc_t rD = rsrc(dy, (long long)a.N * HoWo * a.Cout * 4);
   const __amdgpu_buffer_rsrc_t rX = rsrc(x, (long long)a.N * a.H * a.W * a.Cin * 4);
-  auto gload = [&](int mt, int st) {
+  // dy rows (part 0) or x rows (part 1) of m-step mt -> stage st
+  auto gpart = [&](int mt, int st, int part) __attribute__((always_inline)) {
     const int m0 = mt + m4 * 4;
     if constexpr (VEC == 4) {
+      if (part == 0) {
+        if (dact) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float4 v = bload4(rD, (m0 + r < me && dn < a.Cout) ? ((m0 + r) * a.Cout + dn) * 4 : kOOB);
+            dv[st][r][0] = v.x; dv[st][r][1] = v.y; dv[st][r][2] = v.z; dv[st][r][3] = v.w;
+          }
+        }
+        return;
+      }
       // the 4 rows are consecutive output pixels of one output row (Wo % 4 == 0): decode once
       int img = 0, p = 0, q = 0;
       if (m0 < me) {
@@ -682,13 +857,8 @@ __global__ __launch_bounds__(256) void xwgrad_kernel(const XWArgs a) {
       const int xrow = (img * a.H + h) * a.W;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const bool mv = m0 + r < me;
-        if (dact) {
-          const float4 v = bload4(rD, (mv && dn < a.Cout) ? ((m0 + r) * a.Cout + dn) * 4 : kOOB);
-          dv[st][r][0] = v.x; dv[st][r][1] = v.y; dv[st][r][2] = v.z; dv[st][r][3] = v.w;
-        }
         const int w = (q + r) * a.stride - a.pad + xkw[0];
-        const bool ok = mv && hok && (unsigned)w < (unsigned)a.W;
+        const bool ok = m0 + r < me && hok && (unsigned)w < (unsigned)a.W;
         const float4 v = bload4(rX, ok ? ((xrow + w) * a.Cin + xc[0]) * 4 : kOOB);
         xv[st][r][0] = v.x; xv[st][r][1] = v.y; xv[st][r][2] = v.z; xv[st][r][3] = v.w;
       }
@@ -697,10 +867,13 @@ __global__ __launch_bounds__(256) void xwgrad_kernel(const XWArgs a) {
       for (int r = 0; r < 4; ++r) {
         const int m = m0 + r;
         const bool mv = m < me;
-        if (dact) {
+        if (part == 0) {
+          if (dact) {
 #pragma unroll
-          for (int e = 0; e < 4; ++e)
-            dv[st][r][e] = bload1(rD, (mv && dn + e < a.Cout) ? (m * a.Cout + dn + e) * 4 : kOOB);
+            for (int e = 0; e < 4; ++e)
+              dv[st][r][e] = bload1(rD, (mv && dn + e < a.Cout) ? (m * a.Cout + dn + e) * 4 : kOOB);
+          }
+          continue;
         }
         int img = 0, p = 0, q = 0;
         if (mv) {
@@ -719,18 +892,26 @@ __global__ __launch_bounds__(256) void xwgrad_kernel(const XWArgs a) {
       }
     }
   };
+  auto gload = [&](int mt, int st) __attribute__((always_inline)) {
+    gpart(mt, st, 0);
+    gpart(mt, st, 1);
+  };
   // piece q of stage st -> LDS buffer buf: q < 4 transposes dy column e = q, q >= 4 x column q-4
-  auto lput_q = [&](int buf, int st, int q) {
+  HScale hs;
+  if constexpr (H) hs.init(a.amax_dy[g], a.amax_x[g]);
+  auto lput_q = [&](int buf, int st, int q) __attribute__((always_inline)) {
     uint4* L = lds + buf * P * PL;
     uint2 sp[P];
     if (q < 4) {
       if (dact) {
-        split4<P>(dv[st][0][q], dv[st][1][q], dv[st][2][q], dv[st][3][q], sp);
+        if constexpr (H) split4h(dv[st][0][q], dv[st][1][q], dv[st][2][q], dv[st][3][q], hs.ma, sp);
+        else split4<P>(dv[st][0][q], dv[st][1][q], dv[st][2][q], dv[st][3][q], sp);
         lds_put<P, true, BNO>(L, PL, 0, dn4 * 4 + q, m4, sp);
       }
     } else {
       const int e = q - 4;
-      split4<P>(xv[st][0][e], xv[st][1][e], xv[st][2][e], xv[st][3][e], sp);
+      if constexpr (H) split4h(xv[st][0][e], xv[st][1][e], xv[st][2][e], xv[st][3][e], hs.mb, sp);
+      else split4<P>(xv[st][0][e], xv[st][1][e], xv[st][2][e], xv[st][3][e], sp);
       lds_put<P, true, BK>(L, PL, BNO, xk4 * 4 + e, m4, sp);
     }
   };
@@ -744,22 +925,29 @@ __global__ __launch_bounds__(256) void xwgrad_kernel(const XWArgs a) {
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
   // rows past the chunk zero-fill, so the loads of the steps past its end are harmless
+  // two register stages; a stage's dy (x) registers are reloaded with the step two ahead as
+  // soon as its 4 dy (x) pieces are split (see xconv_kernel)
+  auto fill = [&](int buf, int st, int q, int mnext) __attribute__((always_inline)) {
+    lput_q(buf, st, q);
+    if (q == 3) gpart(mnext, st, 0);
+    if (q == 7) gpart(mnext, st, 1);
+  };
   gload(mb, 0);
   gload(mb + 32, 1);
 #pragma unroll
-  for (int q = 0; q < 8; ++q) lput_q(0, 0, q);
+  for (int q = 0; q < 8; ++q) fill(0, 0, q, mb + 64);
   __syncthreads();
   int mt = mb;
   for (; mt + 32 < me; mt += 64) {
-    gload(mt + 64, 0);
-    mma_step<MI, NJ, P, true, BNO, BK, 8>(lds, PL, wn * TNo, wk * TK, acc, lane, [&](int q) { lput_q(1, 1, q); });
+    mma_step<MI, NJ, P, H, true, BNO, BK, 8>(lds, PL, wn * TNo, wk * TK, acc, lane,
+                                             [&](int q) __attribute__((always_inline)) { fill(1, 1, q, mt + 96); });
     __syncthreads();
-    gload(mt + 96, 1);
-    mma_step<MI, NJ, P, true, BNO, BK, 8>(lds + P * PL, PL, wn * TNo, wk * TK, acc, lane,
-                                          [&](int q) { lput_q(0, 0, q); });
+    mma_step<MI, NJ, P, H, true, BNO, BK, 8>(lds + P * PL, PL, wn * TNo, wk * TK, acc, lane,
+                                             [&](int q) __attribute__((always_inline)) { fill(0, 0, q, mt + 128); });
     __syncthreads();
   }
-  if (mt < me) mma_step<MI, NJ, P, true, BNO, BK, 0>(lds, PL, wn * TNo, wk * TK, acc, lane, [&](int) {});
+  if (mt < me) mma_step<MI, NJ, P, H, true, BNO, BK, 0>(lds, PL, wn * TNo, wk * TK, acc, lane, [&](int) {});
+  if constexpr (H) hs.finish(acc);
 
   // acc[i][j][r]: cout row n = n0 + wn*TNo + i*32 + (r&3) + 8*(r>>2) + 4*hf, k col = k0 + wk*TK + j*32 + fr
   const int fr = lane & 31, hf = lane >> 5;
@@ -870,6 +1058,38 @@ __global__ void xtranspose_kernel(const XTBatch b, int slots, const int* __restr
   }
 }
 
+// max |x| of each replica's valid prefix (nvalid[g] * per_item elements, or n_per_g), as the
+// float's bit pattern: the fp16-pair scale source (HScale).  Integer atomicMax of non-negative
+// float bits: exact and order-independent (deterministic); out is zeroed by the launcher.
+__global__ __launch_bounds__(256) void amax_kernel(const float* __restrict__ x, long long gstride, long long n_per_g,
+                                                   const int* __restrict__ nvalid, long long per_item, int vec,
+                                                   int* __restrict__ out) {
+  const int g = blockIdx.y;
+  const long long n = nvalid ? (long long)nvalid[g] * per_item : n_per_g;
+  const float* __restrict__ p = x + (long long)g * gstride;
+  float m = 0.f;
+  if (vec) {
+    const long long n4 = n >> 2;
+    for (long long e = blockIdx.x * 256LL + threadIdx.x; e < n4; e += (long long)gridDim.x * 256) {
+      const float4 v = ((const float4*)p)[e];
+      m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+    }
+    for (long long e = n4 * 4 + blockIdx.x * 256LL + threadIdx.x; e < n; e += (long long)gridDim.x * 256)
+      m = fmaxf(m, fabsf(p[e]));
+  } else {
+    for (long long e = blockIdx.x * 256LL + threadIdx.x; e < n; e += (long long)gridDim.x * 256) m = fmaxf(m, fabsf(p[e]));
+  }
+  m = wave_max(m);
+  __shared__ float red[4];
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+    if (m > 0.f && __float_as_int(m) > __hip_atomic_load(out + g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+      atomicMax(out + g, __float_as_int(m));
+  }
+}
+
 // dbias[g][n] += sum over valid rows of dy[g][m][n] (fixed order: per-thread strided partial
 // sums, then a fixed LDS tree)
 __global__ __launch_bounds__(256) void xcolsum_kernel(const float* __restrict__ dy, long long dy_gstride, int rows_per_img,
@@ -897,40 +1117,43 @@ int env_int(const char* name, int dflt) {
   return e ? atoi(e) : dflt;
 }
 
-// split planes: 2 (3 MFMAs / product) or 3 (6 MFMAs); DBA_F32_PLANES / dba_xgemm_set_planes
+// split mode: 2 / 3 bf16 planes (3 / 6 MFMAs per product) or kF16 (scaled fp16 pair, 3
+// MFMAs); DBA_F32_PLANES / dba_xgemm_set_planes.  A launch runs the fp16 pair exactly when the
+// caller passes its operands' max |x| (amax pointers); kF16 tells the caller to do so.
+constexpr int kF16 = 16;
 int& planes() {
-  static int p = env_int("DBA_F32_PLANES", 3);
+  static int p = env_int("DBA_F32_PLANES", kF16);
   return p;
 }
 
-template <int BM, int BN, int WM, int WN, int P, int VEC>
+template <int BM, int BN, int WM, int WN, int P, int VEC, bool H>
 int xconv_go(const XArgs& a, long long Mmax, int G, int nclass, hipStream_t st) {
   XArgs b = a;
   b.tiles_n = ceil_div(a.Ncol, BN);
   const dim3 grid((unsigned)(ceil_div(Mmax, BM) * b.tiles_n), G, nclass * a.splitk);
-  hipLaunchKernelGGL((xconv_kernel<BM, BN, WM, WN, P, VEC>), grid, dim3(256), 0, st, b);
+  hipLaunchKernelGGL((xconv_kernel<BM, BN, WM, WN, P, VEC, H>), grid, dim3(256), 0, st, b);
   DBA_LAUNCH_CHECK();
 }
 
-template <int P, int VEC>
+template <int P, int VEC, bool H>
 int xconv_tile(const XArgs& a, long long Mmax, int G, int nclass, int bm, hipStream_t st) {
-  if (a.Ncol <= 32) return xconv_go<128, 32, 4, 1, P, VEC>(a, Mmax, G, nclass, st);
+  if (a.Ncol <= 32) return xconv_go<128, 32, 4, 1, P, VEC, H>(a, Mmax, G, nclass, st);
   if (a.Ncol <= 64) {
-    if (bm == 64) return xconv_go<64, 64, 2, 2, P, VEC>(a, Mmax, G, nclass, st);
-    return xconv_go<128, 64, 2, 2, P, VEC>(a, Mmax, G, nclass, st);
+    if (bm == 64) return xconv_go<64, 64, 2, 2, P, VEC, H>(a, Mmax, G, nclass, st);
+    return xconv_go<128, 64, 2, 2, P, VEC, H>(a, Mmax, G, nclass, st);
   }
-  if (bm == 64) return xconv_go<64, 128, 2, 2, P, VEC>(a, Mmax, G, nclass, st);
-  return xconv_go<128, 128, 2, 2, P, VEC>(a, Mmax, G, nclass, st);
+  if (bm == 64) return xconv_go<64, 128, 2, 2, P, VEC, H>(a, Mmax, G, nclass, st);
+  return xconv_go<128, 128, 2, 2, P, VEC, H>(a, Mmax, G, nclass, st);
 }
 
 bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
-template <int W, int CS, int BM, int BN, int WM, int WN, int P>
+template <int W, int CS, int BM, int BN, int WM, int WN, int P, bool H>
 int xhalo_go(const XArgs& a, int G, hipStream_t st) {
   XArgs b = a;
   b.tiles_n = ceil_div(a.Ncol, BN);
   const dim3 grid((unsigned)(a.N * (a.Ho / (BM / W)) * b.tiles_n), G, 1);
-  hipLaunchKernelGGL((xhalo_kernel<W, CS, BM, BN, WM, WN, P>), grid, dim3(256), 0, st, b);
+  hipLaunchKernelGGL((xhalo_kernel<W, CS, BM, BN, WM, WN, P, H>), grid, dim3(256), 0, st, b);
   DBA_LAUNCH_CHECK();
 }
 
@@ -943,9 +1166,11 @@ int xhalo_try(const XArgs& a, int G, int KH, int KW, hipStream_t st) {
   if (!(a.dsg == 1 ? (c.bh == -1 && c.bw == -1) : (c.bh == 1 && c.bw == 1))) return -100;
   if (a.Hs != a.Ho || a.Ws != a.Wo || a.Ho != a.Wo || (a.Ncol & 3) != 0) return -100;
   if (!aligned16(a.src) || !aligned16(a.w) || a.src_gstride % 4 || a.w_sstride % 4) return -100;
-  const bool p2 = planes() == 2;
-  if (a.Wo == 32 && a.Cs == 32 && a.Ncol <= 32 && a.Ho % 4 == 0)
-    return p2 ? xhalo_go<32, 32, 128, 32, 4, 1, 2>(a, G, st) : xhalo_go<32, 32, 128, 32, 4, 1, 3>(a, G, st);
+  if (a.Wo == 32 && a.Cs == 32 && a.Ncol <= 32 && a.Ho % 4 == 0) {
+    if (a.amax_src) return xhalo_go<32, 32, 128, 32, 4, 1, 2, true>(a, G, st);
+    if (planes() == 2) return xhalo_go<32, 32, 128, 32, 4, 1, 2, false>(a, G, st);
+    return xhalo_go<32, 32, 128, 32, 4, 1, 3, false>(a, G, st);
+  }
   // (W 16 / Cs 64 as 64x64 halo tiles measured slower than the 128x64 implicit GEMM: 147 vs
   // 154 TF on the eval layer-2 shape, profiles/kbench_r2_fp32_p3.json — not routed here)
   return -100;
@@ -957,12 +1182,19 @@ int xconv_dispatch(const XArgs& a, long long Mmax, int G, int nclass, int vec, h
   const long long blocks = (long long)ceil_div(Mmax, 128) * ceil_div(a.Ncol, bn) * G * nclass * a.splitk;
   const int bm = (bn > 32 && blocks < 512) ? 64 : 128;
   if (vec == 4 && a.Cs % 32 == 0) vec = 32;
-  if (planes() == 2) {
-    if (vec == 32) return xconv_tile<2, 32>(a, Mmax, G, nclass, bm, st);
-    return vec == 4 ? xconv_tile<2, 4>(a, Mmax, G, nclass, bm, st) : xconv_tile<2, 1>(a, Mmax, G, nclass, bm, st);
+  if (a.amax_src) {
+    if (vec == 32) return xconv_tile<2, 32, true>(a, Mmax, G, nclass, bm, st);
+    return vec == 4 ? xconv_tile<2, 4, true>(a, Mmax, G, nclass, bm, st)
+                    : xconv_tile<2, 1, true>(a, Mmax, G, nclass, bm, st);
   }
-  if (vec == 32) return xconv_tile<3, 32>(a, Mmax, G, nclass, bm, st);
-  return vec == 4 ? xconv_tile<3, 4>(a, Mmax, G, nclass, bm, st) : xconv_tile<3, 1>(a, Mmax, G, nclass, bm, st);
+  if (planes() == 2) {
+    if (vec == 32) return xconv_tile<2, 32, false>(a, Mmax, G, nclass, bm, st);
+    return vec == 4 ? xconv_tile<2, 4, false>(a, Mmax, G, nclass, bm, st)
+                    : xconv_tile<2, 1, false>(a, Mmax, G, nclass, bm, st);
+  }
+  if (vec == 32) return xconv_tile<3, 32, false>(a, Mmax, G, nclass, bm, st);
+  return vec == 4 ? xconv_tile<3, 4, false>(a, Mmax, G, nclass, bm, st)
+                  : xconv_tile<3, 1, false>(a, Mmax, G, nclass, bm, st);
 }
 
 // split-K factor of a forward launch (1 = none).  Decided from the PER-REPLICA geometry only
@@ -1014,7 +1246,7 @@ ClassGeom dgrad_classes(int H, int W, int Cin, int Cout, int KH, int KW, int s, 
 
 DBA_EXPORT int dba_xgemm_set_planes(int p) {
   const int prev = planes();
-  if (p == 2 || p == 3) planes() = p;
+  if (p == 2 || p == 3 || p == kF16) planes() = p;
   return prev;
 }
 
@@ -1029,8 +1261,8 @@ DBA_EXPORT long long dba_xconv_ws_floats(int G, int N, int Ho, int Wo, int Cin, 
 DBA_EXPORT int dba_xconv_fwd(const float* x, long long x_gstride, const float* w, long long w_sstride,
                              const int* wsel, const float* bias, long long b_sstride, const float* res, float* out,
                              long long out_gstride, const int* nvalid, int G, int N, int H, int W, int Cin, int Ho,
-                             int Wo, int Cout, int KH, int KW, int stride, int pad, int relu, float* ws,
-                             long long ws_floats, void* stream) {
+                             int Wo, int Cout, int KH, int KW, int stride, int pad, int relu, const int* amax_x,
+                             const int* amax_w, int* amax_out, float* ws, long long ws_floats, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   if ((long long)N * H * W * Cin >= (1LL << 29)) return -103;   // 32-bit in-replica byte offsets
   const long long M = (long long)N * Ho * Wo;
@@ -1041,6 +1273,7 @@ DBA_EXPORT int dba_xconv_fwd(const float* x, long long x_gstride, const float* w
   a.bias = bias; a.b_sstride = b_sstride; a.res = res; a.out = out; a.out_gstride = out_gstride;
   a.nvalid = nvalid; a.N = N; a.Hs = H; a.Ws = W; a.Cs = Cin; a.Ncol = Cout; a.Ho = Ho; a.Wo = Wo;
   a.sp = stride; a.os = 1; a.dsg = 1; a.relu = relu; a.splitk = 1;
+  a.amax_src = amax_x; a.amax_w = amax_w; a.amax_out = amax_out;
   a.cls[0] = XClass{KH, KW, -pad, -pad, 0, 0, Ho, Wo, 0};
   if (stride == 1) {
     const int rc = xhalo_try(a, G, KH, KW, st);
@@ -1058,7 +1291,7 @@ DBA_EXPORT int dba_xconv_fwd(const float* x, long long x_gstride, const float* w
     const long long per = M * Cout;
     const dim3 grid((unsigned)std::max(1LL, std::min(1024LL, (per + 255) / 256)), G);
     hipLaunchKernelGGL(xsplitk_reduce_kernel, grid, dim3(256), 0, st, (const float*)ws, s, b.zstride, per, nvalid, N,
-                       Ho * Wo, Cout, bias, b_sstride, wsel, res, relu, out);
+                       Ho * Wo, Cout, bias, b_sstride, wsel, res, relu, out, amax_out);
     DBA_LAUNCH_CHECK();
   }
   return xconv_dispatch(a, M, G, 1, vec, st);
@@ -1069,7 +1302,8 @@ DBA_EXPORT int dba_xconv_fwd(const float* x, long long x_gstride, const float* w
 DBA_EXPORT int dba_xconv_dgrad(const float* dy, long long dy_gstride, const float* wt, long long wt_sstride,
                                const int* wsel, const float* accum, float* dx, long long dx_gstride,
                                const int* nvalid, int G, int N, int H, int W, int Cin, int Ho, int Wo, int Cout,
-                               int KH, int KW, int stride, int pad, float* ws, long long ws_floats, void* stream) {
+                               int KH, int KW, int stride, int pad, const int* amax_dy, const int* amax_w, float* ws,
+                               long long ws_floats, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   if ((long long)N * Ho * Wo * Cout >= (1LL << 29)) return -103;   // 32-bit in-replica byte offsets
   const ClassGeom cg = dgrad_classes(H, W, Cin, Cout, KH, KW, stride, pad);
@@ -1079,6 +1313,7 @@ DBA_EXPORT int dba_xconv_dgrad(const float* dy, long long dy_gstride, const floa
   a.bias = nullptr; a.b_sstride = 0; a.res = accum; a.out = dx; a.out_gstride = dx_gstride;
   a.nvalid = nvalid; a.N = N; a.Hs = Ho; a.Ws = Wo; a.Cs = Cout; a.Ncol = Cin; a.Ho = H; a.Wo = W;
   a.sp = 1; a.os = stride; a.dsg = -1; a.relu = 0; a.splitk = 1;
+  a.amax_src = amax_dy; a.amax_w = amax_w;
   long long Mmax = 0;
   for (int i = 0; i < cg.n; ++i) {
     a.cls[i] = cg.c[i];
@@ -1100,7 +1335,7 @@ DBA_EXPORT int dba_xconv_dgrad(const float* dy, long long dy_gstride, const floa
       const long long per = M * Cin;
       const dim3 grid((unsigned)std::max(1LL, std::min(1024LL, (per + 255) / 256)), G);
       hipLaunchKernelGGL(xsplitk_reduce_kernel, grid, dim3(256), 0, st, (const float*)ws, s, b.zstride, per, nvalid,
-                         N, H * W, Cin, nullptr, 0LL, wsel, accum, 0, dx);
+                         N, H * W, Cin, nullptr, 0LL, wsel, accum, 0, dx, (int*)nullptr);
       DBA_LAUNCH_CHECK();
     }
   }
@@ -1148,8 +1383,8 @@ DBA_EXPORT long long dba_xwgrad_ws_floats(int G, int N, int Ho, int Wo, int Cin,
 // the whole backward pass)
 DBA_EXPORT int dba_xwgrad(const float* dy, long long dy_gstride, const float* x, long long x_gstride, float* dw,
                           long long dw_gstride, const int* nvalid, int G, int N, int H, int W, int Cin, int Ho,
-                          int Wo, int Cout, int KH, int KW, int stride, int pad, float* ws, long long ws_floats,
-                          int defer, void* stream) {
+                          int Wo, int Cout, int KH, int KW, int stride, int pad, const int* amax_dy,
+                          const int* amax_x, float* ws, long long ws_floats, int defer, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   int mchunk = 0;
   const long long need = dba_xwgrad_ws_floats(G, N, Ho, Wo, Cin, Cout, KH, KW, &mchunk);
@@ -1161,6 +1396,7 @@ DBA_EXPORT int dba_xwgrad(const float* dy, long long dy_gstride, const float* x,
   a.dw_gstride = dw_gstride; a.nvalid = nvalid; a.N = N; a.H = H; a.W = W; a.Cin = Cin; a.Ho = Ho; a.Wo = Wo;
   a.Cout = Cout; a.KW = KW; a.stride = stride; a.pad = pad; a.K = KH * KW * Cin;
   a.mchunk = mchunk;
+  a.amax_dy = amax_dy; a.amax_x = amax_x;
   a.dHoWo = FDiv{Ho * Wo, 1.0f / (float)(Ho * Wo)};
   a.dWo = FDiv{Wo, 1.0f / (float)Wo};
   a.tiles_k = ceil_div(a.K, 128);
@@ -1169,18 +1405,20 @@ DBA_EXPORT int dba_xwgrad(const float* dy, long long dy_gstride, const float* x,
                   dy_gstride % 4 == 0 && x_gstride % 4 == 0;
   const int bno = Cout <= 32 ? 32 : Cout <= 64 ? 64 : 128;
   const dim3 grid((unsigned)(ceil_div(Cout, bno) * a.tiles_k), G, Z);
-#define XW_GO(BNO_, WN__, WK__, P_, V_) \
-  hipLaunchKernelGGL((xwgrad_kernel<BNO_, 128, WN__, WK__, P_, V_>), grid, dim3(256), 0, st, a)
-#define XW_P(P_, V_)                                  \
-  do {                                                \
-    if (bno == 32) XW_GO(32, 1, 4, P_, V_);           \
-    else if (bno == 64) XW_GO(64, 2, 2, P_, V_);      \
-    else XW_GO(128, 2, 2, P_, V_);                    \
+#define XW_GO(BNO_, WN__, WK__, P_, V_, H_) \
+  hipLaunchKernelGGL((xwgrad_kernel<BNO_, 128, WN__, WK__, P_, V_, H_>), grid, dim3(256), 0, st, a)
+#define XW_P(P_, V_, H_)                                  \
+  do {                                                    \
+    if (bno == 32) XW_GO(32, 1, 4, P_, V_, H_);           \
+    else if (bno == 64) XW_GO(64, 2, 2, P_, V_, H_);      \
+    else XW_GO(128, 2, 2, P_, V_, H_);                    \
   } while (0)
-  if (planes() == 2) {
-    if (v4) XW_P(2, 4); else XW_P(2, 1);
+  if (amax_dy) {
+    if (v4) XW_P(2, 4, true); else XW_P(2, 1, true);
+  } else if (planes() == 2) {
+    if (v4) XW_P(2, 4, false); else XW_P(2, 1, false);
   } else {
-    if (v4) XW_P(3, 4); else XW_P(3, 1);
+    if (v4) XW_P(3, 4, false); else XW_P(3, 1, false);
   }
 #undef XW_P
 #undef XW_GO
@@ -1190,6 +1428,18 @@ DBA_EXPORT int dba_xwgrad(const float* dy, long long dy_gstride, const float* x,
     hipLaunchKernelGGL(xwgrad_reduce_kernel, g2, dim3(256), 0, st, (const float*)ws, G, per, nvalid, N, Ho * Wo,
                        mchunk, dw, dw_gstride);
   }
+  DBA_LAUNCH_CHECK();
+}
+
+// out[g] = bits of max |x| over replica g's valid prefix (see amax_kernel)
+DBA_EXPORT int dba_amax(const float* x, long long gstride, long long n_per_g, const int* nvalid, long long per_item,
+                        int G, int* out, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  (void)hipMemsetAsync(out, 0, sizeof(int) * (size_t)G, st);
+  const int vec = aligned16(x) && gstride % 4 == 0;
+  const long long per = nvalid ? per_item * (n_per_g / std::max(1LL, per_item)) : n_per_g;
+  const dim3 grid((unsigned)std::max(1LL, std::min(256LL, (per + 4095) / 4096)), G);
+  hipLaunchKernelGGL(amax_kernel, grid, dim3(256), 0, st, x, gstride, n_per_g, nvalid, per_item, vec, out);
   DBA_LAUNCH_CHECK();
 }
 

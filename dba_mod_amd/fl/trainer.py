@@ -15,6 +15,7 @@ read once per round.
 from __future__ import annotations
 
 import logging
+import os
 import struct
 from dataclasses import dataclass, field
 from typing import Any, Callable, Dict, List, Optional, Tuple
@@ -115,9 +116,19 @@ class GroupTrainer:
         if self.trace:
             self.use_graph = False
         self._last_loss: Optional[torch.Tensor] = None
+        # training convs: 3 bf16 planes (their operands come from BN / loss kernels that do not
+        # fold a max |x| yet, and an extra max pass per operand costs more than the fp16 pair
+        # saves); evaluation: the library default (the fp16 pair, fed by the conv epilogues)
+        self.split_mode = int(os.environ.get("DBA_F32_TRAIN_PLANES", "3"))
 
     # ------------------------------------------------------------------ step
     def _step(self, b: _GroupBuffers) -> None:
+        # the training step's fp32 split (kernel choice is made at launch, so a captured graph
+        # keeps it): DBA_F32_TRAIN_PLANES, default = the library-wide setting
+        with ops.fp32_split(self.device, self.split_mode):
+            self._step_ops(b)
+
+    def _step_ops(self, b: _GroupBuffers) -> None:
         wl = self.wl
         if wl.kind == "image":
             x, y = ops.gather_images(wl.train_store.images, wl.train_store.labels, b.idx, wl.trig_masks,

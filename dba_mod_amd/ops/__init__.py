@@ -11,6 +11,7 @@ A/B baselining only; bench.py reports which backend ran).
 """
 from __future__ import annotations
 
+import contextlib
 import os
 from typing import Any
 
@@ -57,4 +58,13 @@ _OPS = ["gather_images", "gather_rows", "conv2d", "conv2d_dgrad", "conv2d_wgrad"
 for _n in _OPS:
     globals()[_n] = _dispatch(_n)
 
-__all__ = list(_OPS) + ["backend_for", "backend_name", "hip_module"]
+
+def fp32_split(device: torch.device, mode):
+    """Context: the fp32 kernel family's operand split (``ops.hip.fp32_split``) for the
+    enclosed launches on ``device``; a no-op for the reference backend or ``mode=None``."""
+    if backend_name(device) == "hip" and mode is not None:
+        return hip_module().fp32_split(int(mode))
+    return contextlib.nullcontext()
+
+
+__all__ = list(_OPS) + ["backend_for", "backend_name", "hip_module", "fp32_split"]

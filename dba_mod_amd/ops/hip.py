@@ -6,6 +6,7 @@ the hand-written gfx950 kernel on torch's *current* stream (so every launch is c
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 import os
 from typing import Optional, Sequence, Tuple
@@ -76,11 +77,12 @@ _SIGS = {
     # reference-precision (fp32) family: csrc/kernels/xgemm.hip
     "dba_xgemm_set_planes": [_I],
     "dba_xconv_ws_floats": [_I] * 8,
-    "dba_xconv_fwd": [_P, _LL, _P, _LL, _P, _P, _LL, _P, _P, _LL, _P] + [_I] * 13 + [_P, _LL, _P],
-    "dba_xconv_dgrad": [_P, _LL, _P, _LL, _P, _P, _P, _LL, _P] + [_I] * 12 + [_P, _LL, _P],
+    "dba_xconv_fwd": [_P, _LL, _P, _LL, _P, _P, _LL, _P, _P, _LL, _P] + [_I] * 13 + [_P, _P, _P, _P, _LL, _P],
+    "dba_xconv_dgrad": [_P, _LL, _P, _LL, _P, _P, _P, _LL, _P] + [_I] * 12 + [_P, _P, _P, _LL, _P],
+    "dba_amax": [_P, _LL, _LL, _P, _LL, _I, _P, _P],
     "dba_xtranspose": [_P, _I, _I, _LL, _P, _P],
     "dba_xwgrad_ws_floats": [_I] * 8 + [_P],
-    "dba_xwgrad": [_P, _LL, _P, _LL, _P, _LL, _P] + [_I] * 12 + [_P, _LL, _I, _P],
+    "dba_xwgrad": [_P, _LL, _P, _LL, _P, _LL, _P] + [_I] * 12 + [_P, _P, _P, _LL, _I, _P],
     "dba_xwgrad_reduce_batch": [_P, _I, _I, _LL, _P],
 }
 for _name, _args in _SIGS.items():
@@ -90,6 +92,7 @@ for _name, _args in _SIGS.items():
 _L.dba_conv3_splitk_floats.restype = ctypes.c_longlong
 _L.dba_xconv_ws_floats.restype = ctypes.c_longlong
 _L.dba_xwgrad_ws_floats.restype = ctypes.c_longlong
+_MODE = int(_L.dba_xgemm_set_planes(0))   # fp32 split mode (0: query only; DBA_F32_PLANES)
 
 
 NOT_HANDLED = -100   # a conv2 entry point declining a shape (odd channel counts)
@@ -224,13 +227,57 @@ def set_gemm3_tiles(small: int = -1, big: int = -1) -> Tuple[int, int]:
     return prev // 16, prev % 16
 
 
+F16_PAIR = 16
+
+
 def set_fp32_planes(planes: int) -> int:
-    """Split planes of the fp32 family (csrc/kernels/xgemm.hip): 3 (default; 6 bf16 MFMAs per
-    product, error at the fp32-accumulation level) or 2 (3 MFMAs, ~4e-6 relative).  Returns
-    the previous setting."""
-    if planes not in (2, 3):
-        raise ValueError("fp32 split planes must be 2 or 3")
-    return int(_L.dba_xgemm_set_planes(int(planes)))
+    """Operand split of the fp32 family (csrc/kernels/xgemm.hip): 3 bf16 planes (6 MFMAs per
+    product), 16 = the scaled fp16 pair (3 MFMAs, 11 significant bits per plane), both at
+    fp32-level error; or 2 bf16 planes (3 MFMAs, ~4e-6 relative).  Returns the previous
+    setting."""
+    global _MODE
+    if planes not in (2, 3, F16_PAIR):
+        raise ValueError("fp32 split mode must be 2, 3 (bf16 planes) or 16 (fp16 pair)")
+    prev = int(_L.dba_xgemm_set_planes(int(planes)))
+    _MODE = int(planes)
+    return prev
+
+
+def fp32_mode() -> int:
+    return _MODE
+
+
+@contextlib.contextmanager
+def fp32_split(mode: Optional[int]):
+    """Run the enclosed op launches (host-side: kernel choice happens at launch, so a HIP graph
+    captured inside keeps it) with split mode ``mode`` (None: unchanged)."""
+    if mode is None or mode == _MODE:
+        yield
+        return
+    prev = set_fp32_planes(mode)
+    try:
+        yield
+    finally:
+        set_fp32_planes(prev)
+
+
+def _amax(t, gstride, n_per_g, nvalid=None, per_item=0):
+    """Per-replica max |t| (as fp32 bits, int32 [G]) of the fp16-pair operand scales; rows of
+    invalid images are excluded (their contents are undefined)."""
+    G = t.shape[0]
+    out = torch.empty(G, dtype=torch.int32, device=t.device)
+    _call("dba_amax", t.data_ptr(), gstride, n_per_g, _ptr(_i32(nvalid)), per_item, G, out.data_ptr(), _stream())
+    return out
+
+
+def _amax_act(t, nvalid):
+    """[G][N][...] activation (contiguous per replica); a producer that already folded its
+    output's max into ``t._dba_amax`` (the fp32 conv epilogue) saves the pass."""
+    a = getattr(t, "_dba_amax", None)
+    if a is not None:
+        return a
+    per_item = t[0, 0].numel()
+    return _amax(t, t.stride(0), t.shape[1] * per_item, nvalid, per_item)
 
 
 def _pconv_ok(Cin, Cout, H, W, KH, KW, stride, pad) -> bool:
@@ -258,9 +305,14 @@ def _xconv_fwd(x, w, wsel, stride, pad, bias, residual, relu, nvalid, out_dtype)
     res = _act(residual, _F32, "residual") if residual is not None else None
     n = int(_L.dba_xconv_ws_floats(G, N, Ho, Wo, Cin, Cout, KH, KW))
     wsb = torch.empty(n, dtype=_F32, device=x.device) if n > 0 else None
+    ax = aw = ay = None
+    if _MODE == F16_PAIR:
+        ax, aw = _amax_act(x, nvalid), _amax(w, ws, Cout * KH * KW * Cin)
+        ay = torch.zeros(G, dtype=torch.int32, device=x.device)   # the output's max, for its consumers
+        y._dba_amax = ay
     _call("dba_xconv_fwd", x.data_ptr(), N * H * W * Cin, w.data_ptr(), ws, _ptr(_i32(wsel)), _ptr(bias), bs,
           _ptr(res), y.data_ptr(), N * Ho * Wo * Cout, _ptr(_i32(nvalid)), G, N, H, W, Cin, Ho, Wo, Cout, KH, KW,
-          stride, pad, int(relu), _ptr(wsb), n, _stream())
+          stride, pad, int(relu), _ptr(ax), _ptr(aw), _ptr(ay), _ptr(wsb), n, _stream())
     return y
 
 
@@ -405,9 +457,12 @@ def _xconv_dgrad(dy, w, wsel, stride, pad, in_hw, nvalid, out_dtype, accum, wt):
         assert acc.shape == dx.shape
     n = int(_L.dba_xconv_ws_floats(G, N, H, W, Cout, Cin, KH, KW)) if stride == 1 else 0
     wsb = torch.empty(n, dtype=_F32, device=dy.device) if n > 0 else None
+    ad = aw = None
+    if _MODE == F16_PAIR:
+        ad, aw = _amax_act(dy, nvalid), _amax(wt, per, per)
     _call("dba_xconv_dgrad", dy.data_ptr(), N * Ho * Wo * Cout, wt.data_ptr(), per, _ptr(_i32(wsel)), _ptr(acc),
           dx.data_ptr(), N * H * W * Cin, _ptr(_i32(nvalid)), G, N, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad,
-          _ptr(wsb), n, _stream())
+          _ptr(ad), _ptr(aw), _ptr(wsb), n, _stream())
     return dx
 
 
@@ -488,9 +543,12 @@ def conv2d_wgrad(dy, x, stride, pad, kh, kw, dw, dbias=None, nvalid=None, defer=
         n = int(_L.dba_xwgrad_ws_floats(G, N, Ho, Wo, Cin, Cout, kh, kw, ctypes.byref(mchunk)))
         wsb = torch.empty(n, dtype=_F32, device=dy.device) if n > 0 else None
         nv = _i32(nvalid)
+        ad = ax = None
+        if _MODE == F16_PAIR:
+            ad, ax = _amax_act(dy, nvalid), _amax_act(x, nvalid)
         _call("dba_xwgrad", dy.data_ptr(), N * Ho * Wo * Cout, x.data_ptr(), N * H * W * Cin, dw.data_ptr(),
-              dw.stride(0), _ptr(nv), G, N, H, W, Cin, Ho, Wo, Cout, kh, kw, stride, pad, _ptr(wsb), n,
-              int(defer is not None and n > 0), _stream())
+              dw.stride(0), _ptr(nv), G, N, H, W, Cin, Ho, Wo, Cout, kh, kw, stride, pad, _ptr(ad), _ptr(ax),
+              _ptr(wsb), n, int(defer is not None and n > 0), _stream())
         if defer is not None and n > 0:
             per = Cout * kh * kw * Cin
             # (keeps the slab workspace and nvalid alive until the flush)

@@ -91,7 +91,7 @@ def main(argv=None) -> int:
     ap.add_argument("--only", default="", help="substring filter on shape names")
     ap.add_argument("--dtype", choices=("bf16", "fp32"), default="bf16",
                     help="fp32: the reference-precision family (xgemm.hip)")
-    ap.add_argument("--planes", type=int, default=3, help="fp32 split planes (2 or 3)")
+    ap.add_argument("--planes", type=int, default=3, help="fp32 split: 2 / 3 bf16 planes or 16 (fp16 pair)")
     args = ap.parse_args(argv)
     dev = torch.device("cuda")
     rows = []

@@ -98,10 +98,12 @@ def _torch32(case, x, w, wsel, bias, res, dy):
     return torch.stack(ys), torch.stack(dxs), torch.stack(dws)
 
 
-def _check_case(H, R64, case, tol_fwd, tol_wgrad):
+def _check_case(H, R64, case, tol_fwd, tol_wgrad, transform=None):
     dev = torch.device("cuda")
     G, N, Hh, Ww, Cin, Cout, k, s, p = case
     x, w, wsel, bias, nvalid, res, dy, acc = _inputs(case, dev)
+    if transform is not None:
+        x, w, bias, res, dy, acc = transform(x, w, bias, res, dy, acc)
     # forward with bias + residual + ReLU, weight-slot map, a partly valid replica
     y = H.conv2d(x, w, wsel, s, p, bias=bias, residual=res, relu=True, nvalid=nvalid)
     assert y.dtype == torch.float32
@@ -154,10 +156,53 @@ def test_fp32_conv_two_planes(H, R64, case):
         H.set_fp32_planes(prev)
 
 
-def test_fp32_conv_is_deterministic(H):
+@pytest.mark.parametrize("case", CASES)
+def test_fp32_conv_fp16_pair(H, R64, case):
+    """The scaled fp16 pair (2 planes of 11 significant bits, 3 MFMAs, per-k-step power-of-two
+    scaling) holds the same fp32-level bounds as the 6-MFMA bf16 split."""
+    prev = H.set_fp32_planes(16)
+    try:
+        _check_case(H, R64, case, 2e-6, 1e-5)
+    finally:
+        H.set_fp32_planes(prev)
+
+
+def _wide_range(x, w, bias, res, dy, acc):
+    """Magnitudes far outside fp16's range and spread over ~2^12 inside a tile: activations
+    ~1e-12 with a per-pixel log-normal spread, weights ~1e+6, gradients ~1e-9 with a
+    per-channel spread."""
+    g = torch.Generator(device="cpu").manual_seed(7)
+    px = torch.exp(2.0 * torch.randn(*x.shape[:-1], 1, generator=g)).to(x.device)
+    ch = torch.exp(2.0 * torch.randn(dy.shape[-1], generator=g)).to(x.device)
+    x = x * px * 1e-12
+    w = w * 1e6
+    y_scale = 1e-6
+    return x, w, bias * y_scale, res * y_scale, dy * ch * 1e-9, acc * 1e-3
+
+
+@pytest.mark.parametrize("case", [CASES[1], CASES[2], CASES[4], CASES[13], CASES[16]])
+@pytest.mark.parametrize("planes", [3, 16])
+def test_fp32_conv_wide_dynamic_range(H, R64, case, planes):
+    prev = H.set_fp32_planes(planes)
+    try:
+        _check_case(H, R64, case, 2e-6, 1e-5, transform=_wide_range)
+    finally:
+        H.set_fp32_planes(prev)
+
+
+@pytest.mark.parametrize("planes", [3, 16])
+def test_fp32_conv_is_deterministic(H, planes):
     """No atomics anywhere in the fp32 family: repeated launches are bitwise identical
     (split-K slabs and weight-gradient slabs are summed in a fixed order)."""
     dev = torch.device("cuda")
+    prev = H.set_fp32_planes(planes)
+    try:
+        _deterministic(H, dev)
+    finally:
+        H.set_fp32_planes(prev)
+
+
+def _deterministic(H, dev):
     for case in (CASES[13], CASES[15], CASES[2]):
         G, N, Hh, Ww, Cin, Cout, k, s, p = case
         x, w, wsel, bias, nvalid, res, dy, acc = _inputs(case, dev, seed=3)
