@@ -55,8 +55,9 @@ def _split_label(server) -> Optional[dict]:
     if server.dtype != torch.float32 or ops.backend_name(server.device) != "hip":
         return None
     names = {2: "bf16x2 (3 MFMA)", 3: "bf16x3 (6 MFMA)", 16: "scaled fp16x2 (3 MFMA)"}
-    return {"train": names.get(server.trainer.split_mode, str(server.trainer.split_mode)),
-            "eval": names.get(ops.hip_module().fp32_mode(), "?")}
+    lib = ops.hip_module().fp32_mode()
+    tr = server.trainer.split_mode if server.trainer.split_mode is not None else lib
+    return {"train": names.get(tr, str(tr)), "eval": names.get(lib, str(lib))}
 
 
 def main() -> int:

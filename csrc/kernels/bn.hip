@@ -156,14 +156,14 @@ __global__ void bn_apply_kernel(const T* __restrict__ y, const float* __restrict
                                 const float* __restrict__ invstd, const float* __restrict__ gamma,
                                 const float* __restrict__ beta, long long p_gstride, const T* __restrict__ res,
                                 int relu, T* __restrict__ out, const int* __restrict__ nvalid, int G, int N,
-                                int HW, int C) {
+                                int HW, int C, int* __restrict__ amax, int amax_ld) {
   // grid (blocks, G): only the replica's VALID rows are touched (inactive replicas exit at
   // once; padded rows are never read downstream — every consumer gates on nvalid)
   const int g = blockIdx.y;
   const int c8 = C / 8;
   const int total = valid_rows(nvalid, g, N) * HW * c8;
   const int tid0 = blockIdx.x * blockDim.x + threadIdx.x;
-  if (tid0 >= total) return;
+  if ((int)(blockIdx.x * blockDim.x) >= total) return;   // whole block idle (block-uniform)
   const int c0 = (tid0 % c8) * 8;
   float sc[8], sh[8];
 #pragma unroll
@@ -173,6 +173,7 @@ __global__ void bn_apply_kernel(const T* __restrict__ y, const float* __restrict
     sh[e] = beta[(long long)g * p_gstride + c] - mean[g * C + c] * sc[e];
   }
   const long long base = (long long)g * N * HW * c8;
+  float vmax = 0.f;
   for (int t = tid0; t < total; t += gridDim.x * blockDim.x) {
     const long long o = (base + t) * 8;
     float yp[8], rp[8], op[8];
@@ -184,9 +185,11 @@ __global__ void bn_apply_kernel(const T* __restrict__ y, const float* __restrict
       if (res) v += rp[e];
       if (relu) v = fmaxf(v, 0.f);
       op[e] = v;
+      vmax = fmaxf(vmax, fabsf(v));
     }
     st8(out + o, op);
   }
+  if (amax) amax_fold(amax, amax_ld, g, vmax);
 }
 
 // dy = gamma*is/n * (n*d - sum d - xhat * sum d*xhat) = A*d + B*y + K per (replica, channel)
@@ -196,13 +199,14 @@ __global__ void bn_bwd_apply_kernel(const T* __restrict__ dout, const T* __restr
                                     const float* __restrict__ invstd, const float* __restrict__ gamma,
                                     long long p_gstride, const float* __restrict__ sums, int relu,
                                     T* __restrict__ dy, T* __restrict__ dres,
-                                    const int* __restrict__ nvalid, int G, int N, int HW, int C) {
+                                    const int* __restrict__ nvalid, int G, int N, int HW, int C,
+                                    int* __restrict__ amax, int amax_ld) {
   const int g = blockIdx.y;
   const int c8 = C / 8;
   const int nv = valid_rows(nvalid, g, N) * HW;
   const int total = nv * c8;
   const int tid0 = blockIdx.x * blockDim.x + threadIdx.x;
-  if (tid0 >= total) return;
+  if ((int)(blockIdx.x * blockDim.x) >= total) return;   // whole block idle (block-uniform)
   const int c0 = (tid0 % c8) * 8;
   const float n = (float)nv;
   float A[8], B[8], K[8];
@@ -218,6 +222,7 @@ __global__ void bn_bwd_apply_kernel(const T* __restrict__ dout, const T* __restr
     K[e] = -ga * sd / n - B[e] * mean[g * C + c];
   }
   const long long base = (long long)g * N * HW * c8;
+  float vmax = 0.f;
   for (int t = tid0; t < total; t += gridDim.x * blockDim.x) {
     const long long o = (base + t) * 8;
     float dp[8], yp[8], op[8], p1[8];
@@ -228,10 +233,12 @@ __global__ void bn_bwd_apply_kernel(const T* __restrict__ dout, const T* __restr
     for (int e = 0; e < 8; ++e) {
       if (relu && !(op[e] > 0.f)) dp[e] = 0.f;
       p1[e] = fmaf(A[e], dp[e], fmaf(B[e], yp[e], K[e]));
+      vmax = fmaxf(vmax, fabsf(p1[e]));
     }
     st8(dy + o, p1);
     if (dres) st8(dres + o, dp);
   }
+  if (amax) amax_fold(amax, amax_ld, g, vmax);
 }
 
 // sums the backward partials into sums[g][2][C] and accumulates dgamma / dbeta
@@ -276,7 +283,8 @@ __global__ __launch_bounds__(256) void bn_small_fwd_kernel(
     const T* __restrict__ y, const int* __restrict__ nvalid, int N, int HW, int C,
     const float* __restrict__ gamma, const float* __restrict__ beta, float* __restrict__ rm, float* __restrict__ rv,
     long long p_gstride, float momentum, float eps, const T* __restrict__ res, int relu,
-    T* __restrict__ out, float* __restrict__ mean, float* __restrict__ invstd) {
+    T* __restrict__ out, float* __restrict__ mean, float* __restrict__ invstd, int* __restrict__ amax,
+    int amax_ld) {
   __shared__ float red[2][4][8];
   __shared__ float coef[2][8];
   const int g = blockIdx.y, c0 = blockIdx.x * 8, tid = threadIdx.x;
@@ -320,6 +328,7 @@ __global__ __launch_bounds__(256) void bn_small_fwd_kernel(
   float sc[8], sh[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) { sc[e] = coef[0][e]; sh[e] = coef[1][e]; }
+  float vmax = 0.f;
   for (int r = tid; r < R; r += 256) {
     const long long o = base + (long long)r * C;
     float p[8], rp[8], op[8];
@@ -331,9 +340,11 @@ __global__ __launch_bounds__(256) void bn_small_fwd_kernel(
       if (res) x += rp[e];
       if (relu) x = fmaxf(x, 0.f);
       op[e] = x;
+      vmax = fmaxf(vmax, fabsf(x));
     }
     st8(out + o, op);
   }
+  if (amax) amax_fold(amax, amax_ld, g, vmax);
 }
 
 template <typename T>
@@ -341,7 +352,8 @@ __global__ __launch_bounds__(256) void bn_small_bwd_kernel(
     const T* __restrict__ dout, const T* __restrict__ out, const T* __restrict__ y,
     const float* __restrict__ mean, const float* __restrict__ invstd, const float* __restrict__ gamma,
     long long p_gstride, int relu, float* __restrict__ dgamma, float* __restrict__ dbeta, long long g_gstride,
-    T* __restrict__ dy, T* __restrict__ dres, const int* __restrict__ nvalid, int N, int HW, int C) {
+    T* __restrict__ dy, T* __restrict__ dres, const int* __restrict__ nvalid, int N, int HW, int C,
+    int* __restrict__ amax, int amax_ld) {
   __shared__ float red[2][4][8];
   __shared__ float coef[3][8];
   const int g = blockIdx.y, c0 = blockIdx.x * 8, tid = threadIdx.x;
@@ -388,6 +400,7 @@ __global__ __launch_bounds__(256) void bn_small_bwd_kernel(
   float A[8], B[8], K[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) { A[e] = coef[0][e]; B[e] = coef[1][e]; K[e] = coef[2][e]; }
+  float vmax = 0.f;
   for (int r = tid; r < R; r += 256) {
     const long long o = base + (long long)r * C;
     float dp[8], yp[8], op[8], p1[8];
@@ -398,10 +411,12 @@ __global__ __launch_bounds__(256) void bn_small_bwd_kernel(
     for (int e = 0; e < 8; ++e) {
       if (relu && !(op[e] > 0.f)) dp[e] = 0.f;
       p1[e] = fmaf(A[e], dp[e], fmaf(B[e], yp[e], K[e]));
+      vmax = fmaxf(vmax, fabsf(p1[e]));
     }
     st8(dy + o, p1);
     if (dres) st8(dres + o, dp);
   }
+  if (amax) amax_fold(amax, amax_ld, g, vmax);
 }
 
 // eval fold: wf[s][co][k] = w[s][co][k] * s_c ; bf[s][co] = (b0 - rm) * s_c + beta
@@ -462,13 +477,15 @@ DBA_EXPORT int dba_bn_stats(const void* y, const int* nvalid, int G, int N, int 
   DBA_LAUNCH_CHECK();
 }
 
+// amax (optional, a zeroed slot [kAmaxSub][amax_ld], common.hpp): folds max |out| per replica for an
+// fp16-pair consumer (fp32 only)
 DBA_EXPORT int dba_bn_apply(const void* y, const float* mean, const float* invstd, const float* gamma, const float* beta,
                             long long p_gstride, const void* res, int relu, void* out, const int* nvalid, int G, int N,
-                            int HW, int C, int f32, void* stream) {
+                            int HW, int C, int f32, int* amax, int amax_ld, void* stream) {
   if (!bn_layout_ok(C)) return -102;
   BN_T(f32, hipLaunchKernelGGL((bn_apply_kernel<T>), ggrid(G, N, HW, C), dim3(256), 0, (hipStream_t)stream,
                                (const T*)y, mean, invstd, gamma, beta, p_gstride, (const T*)res, relu, (T*)out, nvalid,
-                               G, N, HW, C));
+                               G, N, HW, C, amax, amax_ld));
   DBA_LAUNCH_CHECK();
 }
 
@@ -476,7 +493,7 @@ DBA_EXPORT int dba_bn_apply(const void* y, const float* mean, const float* invst
 DBA_EXPORT int dba_bn_bwd(const void* dout, const void* out, const void* y, const float* mean, const float* invstd,
                           const float* gamma, long long p_gstride, int relu, float* dgamma, float* dbeta,
                           long long g_gstride, void* dy, void* dres, float* part, const int* nvalid, int G, int N,
-                          int HW, int C, int f32, void* stream) {
+                          int HW, int C, int f32, int* amax, int amax_ld, void* stream) {
   if (!bn_layout_ok(C)) return -102;
   hipStream_t st = (hipStream_t)stream;
   const int nblk = ceil_div((long long)N * HW, rows_per_block(C));
@@ -487,7 +504,7 @@ DBA_EXPORT int dba_bn_bwd(const void* dout, const void* out, const void* y, cons
                      dbeta, g_gstride, G, C);
   BN_T(f32, hipLaunchKernelGGL((bn_bwd_apply_kernel<T>), ggrid(G, N, HW, C), dim3(256), 0, st, (const T*)dout,
                                (const T*)out, (const T*)y, mean, invstd, gamma, p_gstride, sums, relu, (T*)dy,
-                               (T*)dres, nvalid, G, N, HW, C));
+                               (T*)dres, nvalid, G, N, HW, C, amax, amax_ld));
   DBA_LAUNCH_CHECK();
 }
 
@@ -495,22 +512,22 @@ DBA_EXPORT int dba_bn_bwd(const void* dout, const void* out, const void* y, cons
 DBA_EXPORT int dba_bn_small_fwd(const void* y, const int* nvalid, int G, int N, int HW, int C, const float* gamma,
                                 const float* beta, float* rm, float* rv, long long p_gstride, float momentum, float eps,
                                 const void* res, int relu, void* out, float* mean, float* invstd, int f32,
-                                void* stream) {
+                                int* amax, int amax_ld, void* stream) {
   if (C % 8 != 0) return -102;
   BN_T(f32, hipLaunchKernelGGL((bn_small_fwd_kernel<T>), dim3(C / 8, G), dim3(256), 0, (hipStream_t)stream,
                                (const T*)y, nvalid, N, HW, C, gamma, beta, rm, rv, p_gstride, momentum, eps,
-                               (const T*)res, relu, (T*)out, mean, invstd));
+                               (const T*)res, relu, (T*)out, mean, invstd, amax, amax_ld));
   DBA_LAUNCH_CHECK();
 }
 
 DBA_EXPORT int dba_bn_small_bwd(const void* dout, const void* out, const void* y, const float* mean,
                                 const float* invstd, const float* gamma, long long p_gstride, int relu, float* dgamma,
                                 float* dbeta, long long g_gstride, void* dy, void* dres, const int* nvalid, int G,
-                                int N, int HW, int C, int f32, void* stream) {
+                                int N, int HW, int C, int f32, int* amax, int amax_ld, void* stream) {
   if (C % 8 != 0) return -102;
   BN_T(f32, hipLaunchKernelGGL((bn_small_bwd_kernel<T>), dim3(C / 8, G), dim3(256), 0, (hipStream_t)stream,
                                (const T*)dout, (const T*)out, (const T*)y, mean, invstd, gamma, p_gstride, relu,
-                               dgamma, dbeta, g_gstride, (T*)dy, (T*)dres, nvalid, N, HW, C));
+                               dgamma, dbeta, g_gstride, (T*)dy, (T*)dres, nvalid, N, HW, C, amax, amax_ld));
   DBA_LAUNCH_CHECK();
 }
 

@@ -90,6 +90,37 @@ __device__ __forceinline__ float wave_max(float v) {
   return v;
 }
 
+// ---- operand max |x| slots of the fp16-pair split (csrc/kernels/xgemm.hip HScale)
+// A slot holds, per replica g, the max |x| (as non-negative float bits) spread over kAmaxSub
+// sub-slots ld ints apart (ld >= 32: one 128-B line each): producers fold block maxima into
+// sub-slot blockIdx.x % kAmaxSub with an integer atomicMax (exact, order-independent), so a
+// launch's thousands of blocks contend on 16 lines instead of one; consumers take the max of
+// the 16.  Slots are zeroed before their producer runs.
+constexpr int kAmaxSub = 16;
+
+// every thread of the block must call it (block-level reduction, then one atomic per block)
+__device__ __forceinline__ void amax_fold(int* amax, int ld, int g, float m) {
+  __shared__ float amax_red[4];
+  m = wave_max(m);
+  if ((threadIdx.x & 63) == 0) amax_red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int nw = (int)(blockDim.x + 63) >> 6;
+    float b = amax_red[0];
+    for (int w = 1; w < nw; ++w) b = fmaxf(b, amax_red[w]);
+    if (b > 0.f) atomicMax(amax + (blockIdx.x % kAmaxSub) * ld + g, __float_as_int(b));
+  }
+}
+
+// the slot's max for replica g (wave-uniform; every lane of the wave must call it)
+__device__ __forceinline__ int amax_read(const int* amax, int ld, int g) {
+  const int lane = threadIdx.x & 63;
+  int v = lane < kAmaxSub ? amax[lane * ld + g] : 0;
+#pragma unroll
+  for (int o = 8; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o, kWave));
+  return __builtin_amdgcn_readfirstlane(v);
+}
+
 __device__ __forceinline__ int valid_rows(const int* nvalid, int g, int n_per_group) {
   return nvalid ? nvalid[g] : n_per_group;
 }

@@ -95,19 +95,7 @@ __device__ __forceinline__ void split4h(float a, float b, float c, float d, floa
 }
 constexpr int kSMax = 100;   // scale exponent cap (operands below 2^-85 stay unnormalised)
 // scale exponent for a max |x| given as float bits (0 / subnormal max: the cap)
-__device__ __forceinline__ int hexp(int maxbits) {
-  return min(kSMax, 141 - (__builtin_amdgcn_readfirstlane(maxbits) >> 23));
-}
-// fold a thread's max |y| of the values it wrote into amax[g] (one atomic per wave: integer max
-// of non-negative float bits, exact and order-independent)
-__device__ __forceinline__ void amax_fold(int* amax, int g, float m) {
-  m = wave_max(m);
-  // the atomic only when the wave's max beats the value seen (a stale read costs one extra
-  // atomic): thousands of blocks fold into one word per replica, and most are below it
-  if ((threadIdx.x & 63) == 0 && m > 0.f && __float_as_int(m) > __hip_atomic_load(amax + g, __ATOMIC_RELAXED,
-                                                                                      __HIP_MEMORY_SCOPE_AGENT))
-    atomicMax(amax + g, __float_as_int(m));
-}
+__device__ __forceinline__ int hexp(int maxbits) { return min(kSMax, 141 - (maxbits >> 23)); }
 struct HScale {
   float ma = 1.f, mb = 1.f;   // fill multipliers 2^sa, 2^sb
   int s = 0;                  // the accumulators hold sum * 2^s
@@ -260,9 +248,10 @@ struct XArgs {
   int sp, os, dsg, relu;
   int splitk, tiles_n;
   long long zstride;                         // split-K: slab z at out + z * zstride
-  const int* amax_src;                       // H: max |src| bits per replica [G]
-  const int* amax_w;                         // H: max |w| bits per weight slot
-  int* amax_out;                             // optional: max |out| bits per replica (+= by max)
+  const int* amax_src;                       // H: max |src| slot [kAmaxSub][amax_src_ld] (common.hpp)
+  const int* amax_w;                         // H: max |w| slot, indexed by weight slot
+  int* amax_out;                             // optional: fold max |out| (zeroed slot)
+  int amax_src_ld, amax_w_ld, amax_out_ld;
   XClass cls[4];
 };
 
@@ -419,7 +408,7 @@ __global__ __launch_bounds__(256) void xconv_kernel(const XArgs a) {
   };
   // quarter q of stage st -> LDS buffer buf
   HScale hs;
-  if constexpr (H) hs.init(a.amax_src[g], a.amax_w[slot]);
+  if constexpr (H) hs.init(amax_read(a.amax_src, a.amax_src_ld, g), amax_read(a.amax_w, a.amax_w_ld, slot));
   auto lput_q = [&](int buf, int st, int q) __attribute__((always_inline)) {
     uint4* L = lds + buf * P * PL;
     uint2 sp[P];
@@ -524,7 +513,7 @@ __global__ __launch_bounds__(256) void xconv_kernel(const XArgs a) {
       out[o + n] = v;
     }
   }
-  if (fin && a.amax_out) amax_fold(a.amax_out, g, vmax);
+  if (fin && a.amax_out) amax_fold(a.amax_out, a.amax_out_ld, g, vmax);
 }
 
 // ======================================================================= halo conv
@@ -594,7 +583,7 @@ __global__ __launch_bounds__(256) void xhalo_kernel(const XArgs a) {
     }
   }
   HScale hs;
-  if constexpr (H) hs.init(a.amax_src[g], a.amax_w[slot]);
+  if constexpr (H) hs.init(amax_read(a.amax_src, a.amax_src_ld, g), amax_read(a.amax_w, a.amax_w_ld, slot));
   auto patch_put = [&]() __attribute__((always_inline)) {
 #pragma unroll
     for (int u = 0; u < NE; ++u) {
@@ -734,7 +723,7 @@ __global__ __launch_bounds__(256) void xhalo_kernel(const XArgs a) {
     vmax = fmaxf(vmax, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
     *(float4*)(out + o + n) = v;
   }
-  if (a.amax_out) amax_fold(a.amax_out, g, vmax);
+  if (a.amax_out) amax_fold(a.amax_out, a.amax_out_ld, g, vmax);
 }
 
 // sum of split-K slabs ws[z][g][m][n] (fixed z order) + bias (+ residual) (ReLU), valid rows
@@ -743,7 +732,8 @@ __global__ __launch_bounds__(256) void xsplitk_reduce_kernel(const float* __rest
                                                              int HoWo, int Ncol, const float* __restrict__ bias,
                                                              long long b_sstride, const int* __restrict__ wsel,
                                                              const float* __restrict__ res, int relu,
-                                                             float* __restrict__ out, int* __restrict__ amax_out) {
+                                                             float* __restrict__ out, int* __restrict__ amax_out,
+                                                             int amax_ld) {
   const int g = blockIdx.y;
   const long long total = (long long)valid_rows(nvalid, g, N) * HoWo * Ncol;
   const float* __restrict__ bp = bias ? bias + (long long)(wsel ? wsel[g] : g) * b_sstride : nullptr;
@@ -758,7 +748,7 @@ __global__ __launch_bounds__(256) void xsplitk_reduce_kernel(const float* __rest
     vmax = fmaxf(vmax, fabsf(v));
     out[base + e] = v;
   }
-  if (amax_out) amax_fold(amax_out, g, vmax);
+  if (amax_out) amax_fold(amax_out, amax_ld, g, vmax);
 }
 
 // ============================================================================ wgrad
@@ -781,8 +771,9 @@ struct XWArgs {
   const int* nvalid;
   int N, H, W, Cin, Ho, Wo, Cout, KW, stride, pad, K;
   int tiles_k, mchunk;
-  const int* amax_dy;                      // H: max |dy| / |x| bits per replica [G]
+  const int* amax_dy;                      // H: max |dy| / |x| slots (common.hpp)
   const int* amax_x;
+  int amax_dy_ld, amax_x_ld;
   FDiv dHoWo, dWo;
 };
 
@@ -898,7 +889,7 @@ __global__ __launch_bounds__(256) void xwgrad_kernel(const XWArgs a) {
   };
   // piece q of stage st -> LDS buffer buf: q < 4 transposes dy column e = q, q >= 4 x column q-4
   HScale hs;
-  if constexpr (H) hs.init(a.amax_dy[g], a.amax_x[g]);
+  if constexpr (H) hs.init(amax_read(a.amax_dy, a.amax_dy_ld, g), amax_read(a.amax_x, a.amax_x_ld, g));
   auto lput_q = [&](int buf, int st, int q) __attribute__((always_inline)) {
     uint4* L = lds + buf * P * PL;
     uint2 sp[P];
@@ -1058,12 +1049,29 @@ __global__ void xtranspose_kernel(const XTBatch b, int slots, const int* __restr
   }
 }
 
+// max |x| of n segments (offset, length) of every replica's flat row (the conv weights of a
+// model replica: one launch per training step instead of one per conv); out[s][g]
+constexpr int kAmaxSegs = 64;
+struct AmaxSegs {
+  long long off[kAmaxSegs];
+  int len[kAmaxSegs];
+};
+__global__ __launch_bounds__(256) void amax_segments_kernel(const float* __restrict__ base, long long gstride,
+                                                            const AmaxSegs segs, int ld, int* __restrict__ out) {
+  const int sg = blockIdx.y, g = blockIdx.z;
+  const float* __restrict__ p = base + (long long)g * gstride + segs.off[sg];
+  const int n = segs.len[sg];
+  float m = 0.f;
+  for (int e = blockIdx.x * 256 + threadIdx.x; e < n; e += gridDim.x * 256) m = fmaxf(m, fabsf(p[e]));
+  amax_fold(out + (long long)sg * kAmaxSub * ld, ld, g, m);
+}
+
 // max |x| of each replica's valid prefix (nvalid[g] * per_item elements, or n_per_g), as the
 // float's bit pattern: the fp16-pair scale source (HScale).  Integer atomicMax of non-negative
 // float bits: exact and order-independent (deterministic); out is zeroed by the launcher.
 __global__ __launch_bounds__(256) void amax_kernel(const float* __restrict__ x, long long gstride, long long n_per_g,
                                                    const int* __restrict__ nvalid, long long per_item, int vec,
-                                                   int* __restrict__ out) {
+                                                   int* __restrict__ out, int ld) {
   const int g = blockIdx.y;
   const long long n = nvalid ? (long long)nvalid[g] * per_item : n_per_g;
   const float* __restrict__ p = x + (long long)g * gstride;
@@ -1079,15 +1087,7 @@ __global__ __launch_bounds__(256) void amax_kernel(const float* __restrict__ x, 
   } else {
     for (long long e = blockIdx.x * 256LL + threadIdx.x; e < n; e += (long long)gridDim.x * 256) m = fmaxf(m, fabsf(p[e]));
   }
-  m = wave_max(m);
-  __shared__ float red[4];
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
-    if (m > 0.f && __float_as_int(m) > __hip_atomic_load(out + g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
-      atomicMax(out + g, __float_as_int(m));
-  }
+  amax_fold(out, ld, g, m);
 }
 
 // dbias[g][n] += sum over valid rows of dy[g][m][n] (fixed order: per-thread strided partial
@@ -1262,7 +1262,8 @@ DBA_EXPORT int dba_xconv_fwd(const float* x, long long x_gstride, const float* w
                              const int* wsel, const float* bias, long long b_sstride, const float* res, float* out,
                              long long out_gstride, const int* nvalid, int G, int N, int H, int W, int Cin, int Ho,
                              int Wo, int Cout, int KH, int KW, int stride, int pad, int relu, const int* amax_x,
-                             const int* amax_w, int* amax_out, float* ws, long long ws_floats, void* stream) {
+                             int amax_x_ld, const int* amax_w, int amax_w_ld, int* amax_out, int amax_out_ld,
+                             float* ws, long long ws_floats, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   if ((long long)N * H * W * Cin >= (1LL << 29)) return -103;   // 32-bit in-replica byte offsets
   const long long M = (long long)N * Ho * Wo;
@@ -1274,6 +1275,7 @@ DBA_EXPORT int dba_xconv_fwd(const float* x, long long x_gstride, const float* w
   a.nvalid = nvalid; a.N = N; a.Hs = H; a.Ws = W; a.Cs = Cin; a.Ncol = Cout; a.Ho = Ho; a.Wo = Wo;
   a.sp = stride; a.os = 1; a.dsg = 1; a.relu = relu; a.splitk = 1;
   a.amax_src = amax_x; a.amax_w = amax_w; a.amax_out = amax_out;
+  a.amax_src_ld = amax_x_ld; a.amax_w_ld = amax_w_ld; a.amax_out_ld = amax_out_ld;
   a.cls[0] = XClass{KH, KW, -pad, -pad, 0, 0, Ho, Wo, 0};
   if (stride == 1) {
     const int rc = xhalo_try(a, G, KH, KW, st);
@@ -1291,7 +1293,7 @@ DBA_EXPORT int dba_xconv_fwd(const float* x, long long x_gstride, const float* w
     const long long per = M * Cout;
     const dim3 grid((unsigned)std::max(1LL, std::min(1024LL, (per + 255) / 256)), G);
     hipLaunchKernelGGL(xsplitk_reduce_kernel, grid, dim3(256), 0, st, (const float*)ws, s, b.zstride, per, nvalid, N,
-                       Ho * Wo, Cout, bias, b_sstride, wsel, res, relu, out, amax_out);
+                       Ho * Wo, Cout, bias, b_sstride, wsel, res, relu, out, amax_out, amax_out_ld);
     DBA_LAUNCH_CHECK();
   }
   return xconv_dispatch(a, M, G, 1, vec, st);
@@ -1302,8 +1304,8 @@ DBA_EXPORT int dba_xconv_fwd(const float* x, long long x_gstride, const float* w
 DBA_EXPORT int dba_xconv_dgrad(const float* dy, long long dy_gstride, const float* wt, long long wt_sstride,
                                const int* wsel, const float* accum, float* dx, long long dx_gstride,
                                const int* nvalid, int G, int N, int H, int W, int Cin, int Ho, int Wo, int Cout,
-                               int KH, int KW, int stride, int pad, const int* amax_dy, const int* amax_w, float* ws,
-                               long long ws_floats, void* stream) {
+                               int KH, int KW, int stride, int pad, const int* amax_dy, int amax_dy_ld,
+                               const int* amax_w, int amax_w_ld, float* ws, long long ws_floats, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   if ((long long)N * Ho * Wo * Cout >= (1LL << 29)) return -103;   // 32-bit in-replica byte offsets
   const ClassGeom cg = dgrad_classes(H, W, Cin, Cout, KH, KW, stride, pad);
@@ -1314,6 +1316,7 @@ DBA_EXPORT int dba_xconv_dgrad(const float* dy, long long dy_gstride, const floa
   a.nvalid = nvalid; a.N = N; a.Hs = Ho; a.Ws = Wo; a.Cs = Cout; a.Ncol = Cin; a.Ho = H; a.Wo = W;
   a.sp = 1; a.os = stride; a.dsg = -1; a.relu = 0; a.splitk = 1;
   a.amax_src = amax_dy; a.amax_w = amax_w;
+  a.amax_src_ld = amax_dy_ld; a.amax_w_ld = amax_w_ld;
   long long Mmax = 0;
   for (int i = 0; i < cg.n; ++i) {
     a.cls[i] = cg.c[i];
@@ -1335,7 +1338,7 @@ DBA_EXPORT int dba_xconv_dgrad(const float* dy, long long dy_gstride, const floa
       const long long per = M * Cin;
       const dim3 grid((unsigned)std::max(1LL, std::min(1024LL, (per + 255) / 256)), G);
       hipLaunchKernelGGL(xsplitk_reduce_kernel, grid, dim3(256), 0, st, (const float*)ws, s, b.zstride, per, nvalid,
-                         N, H * W, Cin, nullptr, 0LL, wsel, accum, 0, dx, (int*)nullptr);
+                         N, H * W, Cin, nullptr, 0LL, wsel, accum, 0, dx, (int*)nullptr, 0);
       DBA_LAUNCH_CHECK();
     }
   }
@@ -1384,7 +1387,8 @@ DBA_EXPORT long long dba_xwgrad_ws_floats(int G, int N, int Ho, int Wo, int Cin,
 DBA_EXPORT int dba_xwgrad(const float* dy, long long dy_gstride, const float* x, long long x_gstride, float* dw,
                           long long dw_gstride, const int* nvalid, int G, int N, int H, int W, int Cin, int Ho,
                           int Wo, int Cout, int KH, int KW, int stride, int pad, const int* amax_dy,
-                          const int* amax_x, float* ws, long long ws_floats, int defer, void* stream) {
+                          int amax_dy_ld, const int* amax_x, int amax_x_ld, float* ws, long long ws_floats, int defer,
+                          void* stream) {
   hipStream_t st = (hipStream_t)stream;
   int mchunk = 0;
   const long long need = dba_xwgrad_ws_floats(G, N, Ho, Wo, Cin, Cout, KH, KW, &mchunk);
@@ -1397,6 +1401,7 @@ DBA_EXPORT int dba_xwgrad(const float* dy, long long dy_gstride, const float* x,
   a.Cout = Cout; a.KW = KW; a.stride = stride; a.pad = pad; a.K = KH * KW * Cin;
   a.mchunk = mchunk;
   a.amax_dy = amax_dy; a.amax_x = amax_x;
+  a.amax_dy_ld = amax_dy_ld; a.amax_x_ld = amax_x_ld;
   a.dHoWo = FDiv{Ho * Wo, 1.0f / (float)(Ho * Wo)};
   a.dWo = FDiv{Wo, 1.0f / (float)Wo};
   a.tiles_k = ceil_div(a.K, 128);
@@ -1431,15 +1436,32 @@ DBA_EXPORT int dba_xwgrad(const float* dy, long long dy_gstride, const float* x,
   DBA_LAUNCH_CHECK();
 }
 
-// out[g] = bits of max |x| over replica g's valid prefix (see amax_kernel)
+// out: n zeroed amax slots [n][kAmaxSub][ld] (common.hpp): max |x| of segment s of replica g;
+// segs: n x (offset, length) int64 pairs in HOST memory (passed by value: safe under graph
+// capture), n <= 64
+DBA_EXPORT int dba_amax_segments(const float* base, long long gstride, const long long* segs, int n, int G, int* out,
+                                 int ld, void* stream) {
+  if (n > kAmaxSegs) return -105;
+  AmaxSegs a{};
+  int maxlen = 1;
+  for (int i = 0; i < n; ++i) {
+    a.off[i] = segs[2 * i];
+    a.len[i] = (int)segs[2 * i + 1];
+    maxlen = std::max(maxlen, a.len[i]);
+  }
+  const dim3 grid((unsigned)std::min(64, ceil_div(maxlen, 4096)), n, G);
+  hipLaunchKernelGGL(amax_segments_kernel, grid, dim3(256), 0, (hipStream_t)stream, base, gstride, a, ld, out);
+  DBA_LAUNCH_CHECK();
+}
+
+// folds max |x| over replica g's valid prefix into the zeroed slot out [kAmaxSub][ld]
 DBA_EXPORT int dba_amax(const float* x, long long gstride, long long n_per_g, const int* nvalid, long long per_item,
-                        int G, int* out, void* stream) {
+                        int G, int* out, int ld, void* stream) {
   hipStream_t st = (hipStream_t)stream;
-  (void)hipMemsetAsync(out, 0, sizeof(int) * (size_t)G, st);
   const int vec = aligned16(x) && gstride % 4 == 0;
   const long long per = nvalid ? per_item * (n_per_g / std::max(1LL, per_item)) : n_per_g;
   const dim3 grid((unsigned)std::max(1LL, std::min(256LL, (per + 4095) / 4096)), G);
-  hipLaunchKernelGGL(amax_kernel, grid, dim3(256), 0, st, x, gstride, n_per_g, nvalid, per_item, vec, out);
+  hipLaunchKernelGGL(amax_kernel, grid, dim3(256), 0, st, x, gstride, n_per_g, nvalid, per_item, vec, out, ld);
   DBA_LAUNCH_CHECK();
 }
 

@@ -94,15 +94,17 @@ class Evaluator:
         nval_d = to_device(nval, dev)
         for c in range(n_chunks):
             idx = table_d[c]
-            if wl.kind == "image":
-                x, y = ops.gather_images(wl.test_store.images, wl.test_store.labels, idx, wl.trig_masks,
-                                         trig, pn, self.target, None, self.dtype)
-            else:
-                x, y = ops.gather_rows(wl.test_store.rows, wl.test_store.labels, idx, wl.trig_cols,
-                                       wl.trig_vals, trig, pn, self.target, self.dtype)
-            ctx = prog.Ctx(wl.spec, None, None, wsel, train=False, folded=folded, nvalid=nval_d[c],
-                           act_dtype=self.dtype)
-            logits = prog.forward(ctx, x)
+            # (one zeroed allocation for the chunk's fp16-pair operand-max slots)
+            with ops.amax_arena(G, dev):
+                if wl.kind == "image":
+                    x, y = ops.gather_images(wl.test_store.images, wl.test_store.labels, idx, wl.trig_masks,
+                                             trig, pn, self.target, None, self.dtype)
+                else:
+                    x, y = ops.gather_rows(wl.test_store.rows, wl.test_store.labels, idx, wl.trig_cols,
+                                           wl.trig_vals, trig, pn, self.target, self.dtype)
+                ctx = prog.Ctx(wl.spec, None, None, wsel, train=False, folded=folded, nvalid=nval_d[c],
+                               act_dtype=self.dtype)
+                logits = prog.forward(ctx, x)
             loss, correct, _ = ops.softmax_xent(logits, y, False, False, loss_dtype=torch.float64)
             acc[:, 0] += loss.double()
             acc[:, 1] += correct.double()

@@ -116,16 +116,16 @@ class GroupTrainer:
         if self.trace:
             self.use_graph = False
         self._last_loss: Optional[torch.Tensor] = None
-        # training convs: 3 bf16 planes (their operands come from BN / loss kernels that do not
-        # fold a max |x| yet, and an extra max pass per operand costs more than the fp16 pair
-        # saves); evaluation: the library default (the fp16 pair, fed by the conv epilogues)
-        self.split_mode = int(os.environ.get("DBA_F32_TRAIN_PLANES", "3"))
+        # the training step's fp32 operand split (DBA_F32_TRAIN_PLANES; default: the library's,
+        # the scaled fp16 pair, whose operand maxima the BN / conv producers fold on the fly)
+        sm = os.environ.get("DBA_F32_TRAIN_PLANES")
+        self.split_mode: Optional[int] = int(sm) if sm else None
 
     # ------------------------------------------------------------------ step
     def _step(self, b: _GroupBuffers) -> None:
         # the training step's fp32 split (kernel choice is made at launch, so a captured graph
         # keeps it): DBA_F32_TRAIN_PLANES, default = the library-wide setting
-        with ops.fp32_split(self.device, self.split_mode):
+        with ops.fp32_split(self.device, self.split_mode), ops.amax_arena(b.state.shape[0], self.device):
             self._step_ops(b)
 
     def _step_ops(self, b: _GroupBuffers) -> None:

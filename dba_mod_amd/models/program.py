@@ -105,6 +105,19 @@ class Ctx:
         self.dropout_seed = dropout_seed
         self._drop_ctr = 0
         self.act_dtype = act_dtype
+        self._wamax = self._weight_scales() if train else None
+
+    def _weight_scales(self) -> Optional[Dict[str, Tensor]]:
+        """fp32 kernels on the fp16 pair (ops.hip F16_PAIR): every conv / linear weight's
+        per-replica max |w| in ONE launch at the start of the step (their operand scales)."""
+        wc = self.wcomp
+        if (wc is None or not wc.is_cuda or wc.dtype != torch.float32 or ops.backend_name(wc.device) != "hip"
+                or ops.hip_module().fp32_mode() != ops.hip_module().F16_PAIR):
+            return None
+        names = [e.name for e in self.spec.params if e.kind in ("conv_w", "lin_w")]
+        slots = ops.hip_module().weight_amax(wc, [(self.spec.by_name[n].offset, self.spec.by_name[n].numel)
+                                                  for n in names])
+        return dict(zip(names, slots))
 
     def _want_dgrad(self, w: Tensor, stride: int, pad: int, in_hw: Tuple[int, int], G: int) -> int:
         self._dgrad_items.append((w, self.wsel, stride, pad, in_hw, self.nvalid, G))
@@ -117,7 +130,10 @@ class Ctx:
 
     # ----------------------------------------------------------------- weights
     def w(self, name: str) -> Tensor:
-        return self.spec.view(self.wcomp, name)
+        v = self.spec.view(self.wcomp, name)
+        if self._wamax is not None and name in self._wamax:
+            v._dba_amax = self._wamax[name]
+        return v
 
     def m(self, name: str) -> Tensor:
         return self.spec.view(self.state, name)
@@ -200,6 +216,8 @@ class Ctx:
         else:
             wv = self.w(name)
             w = wv.reshape(wv.shape[0], wv.shape[1], 1, 1, wv.shape[2])
+            if hasattr(wv, "_dba_amax"):
+                w._dba_amax = wv._dba_amax
             b = self.m(bias)
         y = ops.conv2d(x4, w, self.wsel, 1, 0, bias=b, relu=relu, nvalid=self.nvalid, out_dtype=out_dtype)
         if not self.train:

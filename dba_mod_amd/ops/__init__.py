@@ -67,4 +67,12 @@ def fp32_split(device: torch.device, mode):
     return contextlib.nullcontext()
 
 
-__all__ = list(_OPS) + ["backend_for", "backend_name", "hip_module", "fp32_split"]
+def amax_arena(G: int, device: torch.device):
+    """Context: one zeroed allocation for the fp16-pair operand-max slots of the enclosed
+    launches (``ops.hip.amax_arena``); a no-op off the HIP backend."""
+    if backend_name(device) == "hip":
+        return hip_module().amax_arena(G, device)
+    return contextlib.nullcontext()
+
+
+__all__ = list(_OPS) + ["backend_for", "backend_name", "hip_module", "fp32_split", "amax_arena"]

@@ -46,10 +46,11 @@ _SIGS = {
     "dba_xcolsum": [_P, _LL, _I, _P, _I, _I, _I, _P, _LL, _P],
     "dba_bn_stats": [_P, _P, _I, _I, _I, _I, _P, _P, _P, _LL, _F, _F, _P, _P, _I, _P],
     "dba_bn_partial_blocks": [_I, _I, _I],
-    "dba_bn_apply": [_P, _P, _P, _P, _P, _LL, _P, _I, _P, _P, _I, _I, _I, _I, _I, _P],
-    "dba_bn_bwd": [_P, _P, _P, _P, _P, _P, _LL, _I, _P, _P, _LL, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P],
-    "dba_bn_small_fwd": [_P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _LL, _F, _F, _P, _I, _P, _P, _P, _I, _P],
-    "dba_bn_small_bwd": [_P, _P, _P, _P, _P, _P, _LL, _I, _P, _P, _LL, _P, _P, _P, _I, _I, _I, _I, _I, _P],
+    "dba_bn_apply": [_P, _P, _P, _P, _P, _LL, _P, _I, _P, _P, _I, _I, _I, _I, _I, _P, _I, _P],
+    "dba_bn_bwd": [_P, _P, _P, _P, _P, _P, _LL, _I, _P, _P, _LL, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _I, _P],
+    "dba_bn_small_fwd": [_P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _LL, _F, _F, _P, _I, _P, _P, _P, _I, _P, _I, _P],
+    "dba_bn_small_bwd": [_P, _P, _P, _P, _P, _P, _LL, _I, _P, _P, _LL, _P, _P, _P, _I, _I, _I, _I, _I, _P, _I, _P],
+    "dba_amax_segments": [_P, _LL, _P, _I, _I, _P, _I, _P],
     "dba_bn_fold": [_P, _LL, _P, _P, _P, _P, _P, _LL, _F, _P, _P, _I, _I, _I, _I, _P],
     "dba_relu_mask_bwd": [_P, _P, _P, _LL, _I, _P],
     "dba_maxpool": [_P, _P, _P, _LL, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P],
@@ -77,12 +78,12 @@ _SIGS = {
     # reference-precision (fp32) family: csrc/kernels/xgemm.hip
     "dba_xgemm_set_planes": [_I],
     "dba_xconv_ws_floats": [_I] * 8,
-    "dba_xconv_fwd": [_P, _LL, _P, _LL, _P, _P, _LL, _P, _P, _LL, _P] + [_I] * 13 + [_P, _P, _P, _P, _LL, _P],
-    "dba_xconv_dgrad": [_P, _LL, _P, _LL, _P, _P, _P, _LL, _P] + [_I] * 12 + [_P, _P, _P, _LL, _P],
-    "dba_amax": [_P, _LL, _LL, _P, _LL, _I, _P, _P],
+    "dba_xconv_fwd": [_P, _LL, _P, _LL, _P, _P, _LL, _P, _P, _LL, _P] + [_I] * 13 + [_P, _I] * 3 + [_P, _LL, _P],
+    "dba_xconv_dgrad": [_P, _LL, _P, _LL, _P, _P, _P, _LL, _P] + [_I] * 12 + [_P, _I] * 2 + [_P, _LL, _P],
+    "dba_amax": [_P, _LL, _LL, _P, _LL, _I, _P, _I, _P],
     "dba_xtranspose": [_P, _I, _I, _LL, _P, _P],
     "dba_xwgrad_ws_floats": [_I] * 8 + [_P],
-    "dba_xwgrad": [_P, _LL, _P, _LL, _P, _LL, _P] + [_I] * 12 + [_P, _P, _P, _LL, _I, _P],
+    "dba_xwgrad": [_P, _LL, _P, _LL, _P, _LL, _P] + [_I] * 12 + [_P, _I] * 2 + [_P, _LL, _I, _P],
     "dba_xwgrad_reduce_batch": [_P, _I, _I, _LL, _P],
 }
 for _name, _args in _SIGS.items():
@@ -261,29 +262,107 @@ def fp32_split(mode: Optional[int]):
         set_fp32_planes(prev)
 
 
+# ---- operand max |x| slots of the fp16 pair (csrc/kernels/common.hpp): int32 [16, ld]
+AMAX_SUB = 16
+
+
+def _amax_ld(G: int) -> int:
+    return max(32, (G + 31) // 32 * 32)
+
+
+class _AmaxArena:
+    """One zeroed allocation for all the slots of a forward / backward pass: a single fill
+    (captured into the training step's graph: re-zeroed at every replay) instead of one per
+    producer."""
+
+    def __init__(self, G: int, device, n: int) -> None:
+        self.G, self.ld, self.next = G, _amax_ld(G), 0
+        self.buf = torch.zeros(n, AMAX_SUB, self.ld, dtype=torch.int32, device=device)
+
+    def take(self, G: int, device):
+        if G != self.G or self.next >= self.buf.shape[0] or device != self.buf.device:
+            return None
+        self.next += 1
+        return self.buf[self.next - 1]
+
+
+_ARENA: list = []
+
+
+@contextlib.contextmanager
+def amax_arena(G: int, device, n: int = 128):
+    """Slots for the enclosed launches' fp16-pair operand maxima (fp16-pair mode only)."""
+    if _MODE != F16_PAIR:
+        yield
+        return
+    _ARENA.append(_AmaxArena(G, device, n))
+    try:
+        yield
+    finally:
+        _ARENA.pop()
+
+
+def _amax_new(G: int, device):
+    a = _ARENA[-1].take(G, device) if _ARENA else None
+    return a if a is not None else torch.zeros(AMAX_SUB, _amax_ld(G), dtype=torch.int32, device=device)
+
+
+def _aptr(a):
+    """(pointer, leading dimension) of an amax slot (None: no slot)."""
+    return (None, 0) if a is None else (a.data_ptr(), a.shape[-1])
+
+
 def _amax(t, gstride, n_per_g, nvalid=None, per_item=0):
-    """Per-replica max |t| (as fp32 bits, int32 [G]) of the fp16-pair operand scales; rows of
-    invalid images are excluded (their contents are undefined)."""
+    """Per-replica max |t| slot of the fp16-pair operand scales; rows of invalid images are
+    excluded (their contents are undefined)."""
     G = t.shape[0]
-    out = torch.empty(G, dtype=torch.int32, device=t.device)
-    _call("dba_amax", t.data_ptr(), gstride, n_per_g, _ptr(_i32(nvalid)), per_item, G, out.data_ptr(), _stream())
+    out = _amax_new(G, t.device)
+    _call("dba_amax", t.data_ptr(), gstride, n_per_g, _ptr(_i32(nvalid)), per_item, G, out.data_ptr(), out.shape[1],
+          _stream())
     return out
+
+
+def _amax_out(t):
+    """Zeroed slot for a producer to fold its fp32 output's max into (fp16-pair mode only),
+    attached to ``t`` for its consumers."""
+    if _MODE != F16_PAIR or t.dtype != _F32:
+        return None
+    a = _amax_new(t.shape[0], t.device)
+    t._dba_amax = a
+    return a
+
+
+def weight_amax(flat, segments):
+    """Max |w| slots of ``segments = [(offset, length)]`` of the ``[G, S]`` flat replica rows, in
+    one launch (a training step's conv weights): a list of slots."""
+    G, n = flat.shape[0], len(segments)
+    ar = _ARENA[-1] if _ARENA else None
+    if ar is not None and ar.G == G and ar.buf.device == flat.device and ar.next + n <= ar.buf.shape[0]:
+        buf, ar.next = ar.buf[ar.next:ar.next + n], ar.next + n
+    else:
+        buf = torch.zeros(n, AMAX_SUB, _amax_ld(G), dtype=torch.int32, device=flat.device)
+    slots, base = list(buf), buf.data_ptr()
+    d = torch.tensor(segments, dtype=torch.int64)   # host table, passed by value
+    _call("dba_amax_segments", flat.data_ptr(), flat.stride(0), d.data_ptr(), len(segments), G, base,
+          slots[0].shape[1], _stream())
+    return slots
+
+
+def _amax_w(w, gstride, n):
+    a = getattr(w, "_dba_amax", None)
+    return a if a is not None else _amax(w, gstride, n)
 
 
 def _amax_act(t, nvalid):
     """[G][N][...] activation (contiguous per replica); a producer that already folded its
-    output's max into ``t._dba_amax`` (the fp32 conv epilogue) saves the pass."""
+    output's max into ``t._dba_amax`` (conv epilogue, BN apply) saves the pass."""
     a = getattr(t, "_dba_amax", None)
     if a is not None:
         return a
     per_item = t[0, 0].numel()
-    return _amax(t, t.stride(0), t.shape[1] * per_item, nvalid, per_item)
-
-
-def _pconv_ok(Cin, Cout, H, W, KH, KW, stride, pad) -> bool:
-    """H, W = input size."""
-    return (_PCONV and KH == 3 and KW == 3 and pad == 1 and H == W
-            and (Cin, Cout, W, stride) in _PCONV_SHAPES)
+    a = _amax(t, t.stride(0), t.shape[1] * per_item, nvalid, per_item)
+    t._dba_amax = a   # activations are never written in place: the fwd / wgrad pair shares it
+    return a
 
 
 def _xconv_fwd(x, w, wsel, stride, pad, bias, residual, relu, nvalid, out_dtype):
@@ -291,7 +370,10 @@ def _xconv_fwd(x, w, wsel, stride, pad, bias, residual, relu, nvalid, out_dtype)
     if out_dtype not in (None, _F32):
         raise TypeError(f"fp32 conv cannot emit {out_dtype} (no silent precision conversion)")
     G, N, H, W, Cin = x.shape
+    aw0 = getattr(w, "_dba_amax", None)
     w, ws = _check_w(w, _F32)
+    if aw0 is not None:
+        w._dba_amax = aw0
     Cout, KH, KW = w.shape[1], w.shape[2], w.shape[3]
     assert w.shape[4] == Cin, (w.shape, x.shape)
     Ho = (H + 2 * pad - KH) // stride + 1
@@ -307,12 +389,11 @@ def _xconv_fwd(x, w, wsel, stride, pad, bias, residual, relu, nvalid, out_dtype)
     wsb = torch.empty(n, dtype=_F32, device=x.device) if n > 0 else None
     ax = aw = ay = None
     if _MODE == F16_PAIR:
-        ax, aw = _amax_act(x, nvalid), _amax(w, ws, Cout * KH * KW * Cin)
-        ay = torch.zeros(G, dtype=torch.int32, device=x.device)   # the output's max, for its consumers
-        y._dba_amax = ay
+        ax, aw = _amax_act(x, nvalid), _amax_w(w, ws, Cout * KH * KW * Cin)
+        ay = _amax_out(y)   # the output's max, for its consumers
     _call("dba_xconv_fwd", x.data_ptr(), N * H * W * Cin, w.data_ptr(), ws, _ptr(_i32(wsel)), _ptr(bias), bs,
           _ptr(res), y.data_ptr(), N * Ho * Wo * Cout, _ptr(_i32(nvalid)), G, N, H, W, Cin, Ho, Wo, Cout, KH, KW,
-          stride, pad, int(relu), _ptr(ax), _ptr(aw), _ptr(ay), _ptr(wsb), n, _stream())
+          stride, pad, int(relu), *_aptr(ax), *_aptr(aw), *_aptr(ay), _ptr(wsb), n, _stream())
     return y
 
 
@@ -459,10 +540,11 @@ def _xconv_dgrad(dy, w, wsel, stride, pad, in_hw, nvalid, out_dtype, accum, wt):
     wsb = torch.empty(n, dtype=_F32, device=dy.device) if n > 0 else None
     ad = aw = None
     if _MODE == F16_PAIR:
-        ad, aw = _amax_act(dy, nvalid), _amax(wt, per, per)
+        a0 = getattr(w, "_dba_amax", None)   # the forward weights' max is the transpose's
+        ad, aw = _amax_act(dy, nvalid), (a0 if a0 is not None else _amax(wt, per, per))
     _call("dba_xconv_dgrad", dy.data_ptr(), N * Ho * Wo * Cout, wt.data_ptr(), per, _ptr(_i32(wsel)), _ptr(acc),
           dx.data_ptr(), N * H * W * Cin, _ptr(_i32(nvalid)), G, N, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad,
-          _ptr(ad), _ptr(aw), _ptr(wsb), n, _stream())
+          *_aptr(ad), *_aptr(aw), _ptr(wsb), n, _stream())
     return dx
 
 
@@ -547,7 +629,7 @@ def conv2d_wgrad(dy, x, stride, pad, kh, kw, dw, dbias=None, nvalid=None, defer=
         if _MODE == F16_PAIR:
             ad, ax = _amax_act(dy, nvalid), _amax_act(x, nvalid)
         _call("dba_xwgrad", dy.data_ptr(), N * Ho * Wo * Cout, x.data_ptr(), N * H * W * Cin, dw.data_ptr(),
-              dw.stride(0), _ptr(nv), G, N, H, W, Cin, Ho, Wo, Cout, kh, kw, stride, pad, _ptr(ad), _ptr(ax),
+              dw.stride(0), _ptr(nv), G, N, H, W, Cin, Ho, Wo, Cout, kh, kw, stride, pad, *_aptr(ad), *_aptr(ax),
               _ptr(wsb), n, int(defer is not None and n > 0), _stream())
         if defer is not None and n > 0:
             per = Cout * kh * kw * Cin
@@ -619,18 +701,19 @@ def bn_train(y, gamma, beta, rmean, rvar, nvalid, momentum, eps, relu, residual)
     nv = _ptr(_i32(nvalid))
     out = torch.empty_like(y)
     res = _act(residual, y.dtype, "bn residual") if residual is not None else None
+    am = _amax_out(out)
     if N * H * W <= _BN_SMALL_ROWS:
         # one launch: a block owns 8 channels of a replica for all its rows
         _call("dba_bn_small_fwd", y.data_ptr(), nv, G, N, H * W, C, gamma.data_ptr(), beta.data_ptr(),
               rmean.data_ptr(), rvar.data_ptr(), ps, float(momentum), float(eps), _ptr(res), int(relu),
-              out.data_ptr(), mean.data_ptr(), invstd.data_ptr(), f32, _stream())
+              out.data_ptr(), mean.data_ptr(), invstd.data_ptr(), f32, *_aptr(am), _stream())
         return out, mean, invstd
     nblk = _L.dba_bn_partial_blocks(N, H * W, C)
     part = torch.empty(G * nblk * 2 * C, dtype=torch.float32, device=y.device)
     _call("dba_bn_stats", y.data_ptr(), nv, G, N, H * W, C, part.data_ptr(), rmean.data_ptr(), rvar.data_ptr(), ps,
           float(momentum), float(eps), mean.data_ptr(), invstd.data_ptr(), f32, _stream())
     _call("dba_bn_apply", y.data_ptr(), mean.data_ptr(), invstd.data_ptr(), gamma.data_ptr(), beta.data_ptr(), ps,
-          _ptr(res), int(relu), out.data_ptr(), nv, G, N, H * W, C, f32, _stream())
+          _ptr(res), int(relu), out.data_ptr(), nv, G, N, H * W, C, f32, *_aptr(am), _stream())
     return out, mean, invstd
 
 
@@ -645,16 +728,17 @@ def bn_train_bwd(dout, y, out, mean, invstd, gamma, nvalid, relu, dgamma, dbeta,
     gs = _same_stride(dgamma, dbeta)
     dy = torch.empty_like(y)
     dres = torch.empty_like(y) if want_dres else None
+    am = _amax_out(dy)
     if N * H * W <= _BN_SMALL_ROWS:
         _call("dba_bn_small_bwd", dout.data_ptr(), out.data_ptr(), y.data_ptr(), mean.data_ptr(), invstd.data_ptr(),
               gamma.data_ptr(), ps, int(relu), dgamma.data_ptr(), dbeta.data_ptr(), gs, dy.data_ptr(), _ptr(dres),
-              _ptr(_i32(nvalid)), G, N, H * W, C, f32, _stream())
+              _ptr(_i32(nvalid)), G, N, H * W, C, f32, *_aptr(am), _stream())
         return (dy, dres) if want_dres else dy
     nblk = _L.dba_bn_partial_blocks(N, H * W, C)
     part = torch.empty(G * (nblk + 1) * 2 * C, dtype=torch.float32, device=y.device)
     _call("dba_bn_bwd", dout.data_ptr(), out.data_ptr(), y.data_ptr(), mean.data_ptr(), invstd.data_ptr(),
           gamma.data_ptr(), ps, int(relu), dgamma.data_ptr(), dbeta.data_ptr(), gs, dy.data_ptr(), _ptr(dres),
-          part.data_ptr(), _ptr(_i32(nvalid)), G, N, H * W, C, f32, _stream())
+          part.data_ptr(), _ptr(_i32(nvalid)), G, N, H * W, C, f32, *_aptr(am), _stream())
     return (dy, dres) if want_dres else dy
 
 
@@ -682,6 +766,8 @@ def bn_fold(w, conv_bias, gamma, beta, rmean, rvar, eps, out_dtype):
     _call("dba_bn_fold", w.data_ptr(), w.stride(0), _ptr(cb), gamma.data_ptr(), beta.data_ptr(), rmean.data_ptr(),
           rvar.data_ptr(), ss, float(eps), wf.data_ptr(), bf.data_ptr(), slots, Cout, K, int(out_dtype == _F32),
           _stream())
+    if out_dtype == _F32:
+        wf._dba_amax = _amax(wf, Cout * K, Cout * K)   # the folded weights' scale, once per fold
     return wf, bf
 
 
