@@ -117,7 +117,8 @@ class GroupTrainer:
             self.use_graph = False
         self._last_loss: Optional[torch.Tensor] = None
         # the training step's fp32 operand split (DBA_F32_TRAIN_PLANES; default: the library's,
-        # the scaled fp16 pair, whose operand maxima the BN / conv producers fold on the fly)
+        # the scaled fp16 pair on the gradient passes, ops.hip.TRAIN_H_OPS, whose operand maxima
+        # the BN / conv producers fold on the fly)
         sm = os.environ.get("DBA_F32_TRAIN_PLANES")
         self.split_mode: Optional[int] = int(sm) if sm else None
 
@@ -125,7 +126,8 @@ class GroupTrainer:
     def _step(self, b: _GroupBuffers) -> None:
         # the training step's fp32 split (kernel choice is made at launch, so a captured graph
         # keeps it): DBA_F32_TRAIN_PLANES, default = the library-wide setting
-        with ops.fp32_split(self.device, self.split_mode), ops.amax_arena(b.state.shape[0], self.device):
+        with ops.fp32_split(self.device, self.split_mode, ops.train_h_ops(self.device)), \
+                ops.amax_arena(b.state.shape[0], self.device):
             self._step_ops(b)
 
     def _step_ops(self, b: _GroupBuffers) -> None:

@@ -59,12 +59,17 @@ for _n in _OPS:
     globals()[_n] = _dispatch(_n)
 
 
-def fp32_split(device: torch.device, mode):
+def fp32_split(device: torch.device, mode, h_ops=None):
     """Context: the fp32 kernel family's operand split (``ops.hip.fp32_split``) for the
-    enclosed launches on ``device``; a no-op for the reference backend or ``mode=None``."""
-    if backend_name(device) == "hip" and mode is not None:
-        return hip_module().fp32_split(int(mode))
+    enclosed launches on ``device``; a no-op for the reference backend."""
+    if backend_name(device) == "hip":
+        return hip_module().fp32_split(None if mode is None else int(mode), h_ops)
     return contextlib.nullcontext()
+
+
+def train_h_ops(device: torch.device):
+    """The conv passes a training step runs on the fp16 pair (``ops.hip.TRAIN_H_OPS``)."""
+    return hip_module().TRAIN_H_OPS if backend_name(device) == "hip" else None
 
 
 def amax_arena(G: int, device: torch.device):
@@ -75,4 +80,4 @@ def amax_arena(G: int, device: torch.device):
     return contextlib.nullcontext()
 
 
-__all__ = list(_OPS) + ["backend_for", "backend_name", "hip_module", "fp32_split", "amax_arena"]
+__all__ = list(_OPS) + ["backend_for", "backend_name", "hip_module", "fp32_split", "train_h_ops", "amax_arena"]

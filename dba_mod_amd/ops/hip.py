@@ -229,6 +229,13 @@ def set_gemm3_tiles(small: int = -1, big: int = -1) -> Tuple[int, int]:
 
 
 F16_PAIR = 16
+# which conv passes take the fp16 pair in F16_PAIR mode (DBA_F32_H_OPS; the others take 3 bf16
+# planes).  Training steps default to TRAIN_H_OPS: the forward convs stay on 3 bf16 planes (a
+# training step's error against fp64 is set by its forward — BN over a small batch amplifies
+# forward rounding ~1e4-fold — while the fp16 pair in the data / weight gradients leaves it at
+# the 3-plane level: tools/smoke.py), evaluation forwards use the pair (argmax counts).
+_H_OPS = set(os.environ.get("DBA_F32_H_OPS", "fwd,dgrad,wgrad").split(","))
+TRAIN_H_OPS = tuple(os.environ.get("DBA_F32_TRAIN_H_OPS", "dgrad,wgrad").split(","))
 
 
 def set_fp32_planes(planes: int) -> int:
@@ -249,17 +256,22 @@ def fp32_mode() -> int:
 
 
 @contextlib.contextmanager
-def fp32_split(mode: Optional[int]):
+def fp32_split(mode: Optional[int], h_ops: Optional[Sequence[str]] = None):
     """Run the enclosed op launches (host-side: kernel choice happens at launch, so a HIP graph
-    captured inside keeps it) with split mode ``mode`` (None: unchanged)."""
-    if mode is None or mode == _MODE:
-        yield
-        return
-    prev = set_fp32_planes(mode)
+    captured inside keeps it) with split mode ``mode`` (None: unchanged) and, in F16_PAIR mode,
+    the fp16 pair on the conv passes ``h_ops`` only (None: unchanged; the others take 3 bf16
+    planes)."""
+    global _H_OPS
+    prev_ops = _H_OPS
+    if h_ops is not None:
+        _H_OPS = set(h_ops)
+    prev = set_fp32_planes(mode) if (mode is not None and mode != _MODE) else None
     try:
         yield
     finally:
-        set_fp32_planes(prev)
+        if prev is not None:
+            set_fp32_planes(prev)
+        _H_OPS = prev_ops
 
 
 # ---- operand max |x| slots of the fp16 pair (csrc/kernels/common.hpp): int32 [16, ld]
@@ -365,8 +377,14 @@ def _amax_act(t, nvalid):
     return a
 
 
+def _pconv_ok(Cin, Cout, H, W, KH, KW, stride, pad) -> bool:
+    """H, W = input size."""
+    return (_PCONV and KH == 3 and KW == 3 and pad == 1 and H == W
+            and (Cin, Cout, W, stride) in _PCONV_SHAPES)
+
+
 def _xconv_fwd(x, w, wsel, stride, pad, bias, residual, relu, nvalid, out_dtype):
-    """Reference-precision conv (fp32 in / fp32 out, split-bf16 MFMA: xgemm.hip)."""
+    """Reference-precision conv (fp32 in / fp32 out, split MFMA: xgemm.hip)."""
     if out_dtype not in (None, _F32):
         raise TypeError(f"fp32 conv cannot emit {out_dtype} (no silent precision conversion)")
     G, N, H, W, Cin = x.shape
@@ -388,7 +406,7 @@ def _xconv_fwd(x, w, wsel, stride, pad, bias, residual, relu, nvalid, out_dtype)
     n = int(_L.dba_xconv_ws_floats(G, N, Ho, Wo, Cin, Cout, KH, KW))
     wsb = torch.empty(n, dtype=_F32, device=x.device) if n > 0 else None
     ax = aw = ay = None
-    if _MODE == F16_PAIR:
+    if _MODE == F16_PAIR and "fwd" in _H_OPS:
         ax, aw = _amax_act(x, nvalid), _amax_w(w, ws, Cout * KH * KW * Cin)
         ay = _amax_out(y)   # the output's max, for its consumers
     _call("dba_xconv_fwd", x.data_ptr(), N * H * W * Cin, w.data_ptr(), ws, _ptr(_i32(wsel)), _ptr(bias), bs,
@@ -539,7 +557,7 @@ def _xconv_dgrad(dy, w, wsel, stride, pad, in_hw, nvalid, out_dtype, accum, wt):
     n = int(_L.dba_xconv_ws_floats(G, N, H, W, Cout, Cin, KH, KW)) if stride == 1 else 0
     wsb = torch.empty(n, dtype=_F32, device=dy.device) if n > 0 else None
     ad = aw = None
-    if _MODE == F16_PAIR:
+    if _MODE == F16_PAIR and "dgrad" in _H_OPS:
         a0 = getattr(w, "_dba_amax", None)   # the forward weights' max is the transpose's
         ad, aw = _amax_act(dy, nvalid), (a0 if a0 is not None else _amax(wt, per, per))
     _call("dba_xconv_dgrad", dy.data_ptr(), N * Ho * Wo * Cout, wt.data_ptr(), per, _ptr(_i32(wsel)), _ptr(acc),
@@ -626,7 +644,7 @@ def conv2d_wgrad(dy, x, stride, pad, kh, kw, dw, dbias=None, nvalid=None, defer=
         wsb = torch.empty(n, dtype=_F32, device=dy.device) if n > 0 else None
         nv = _i32(nvalid)
         ad = ax = None
-        if _MODE == F16_PAIR:
+        if _MODE == F16_PAIR and "wgrad" in _H_OPS:
             ad, ax = _amax_act(dy, nvalid), _amax_act(x, nvalid)
         _call("dba_xwgrad", dy.data_ptr(), N * Ho * Wo * Cout, x.data_ptr(), N * H * W * Cin, dw.data_ptr(),
               dw.stride(0), _ptr(nv), G, N, H, W, Cin, Ho, Wo, Cout, kh, kw, stride, pad, *_aptr(ad), *_aptr(ax),

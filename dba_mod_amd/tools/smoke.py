@@ -42,11 +42,13 @@ def _step(device: torch.device, dtype: torch.dtype, impl, G: int, N: int, seed: 
         for k in ops._OPS:
             setattr(ops, k, getattr(impl, k))
     try:
-        x, y = ops.gather_images(src, labels, idx, masks, trig, pn, 2, None, dtype)
-        ctx = prog.Ctx(spec, state, state, None, train=True, grads=grads, nvalid=nvalid, act_dtype=dtype)
-        logits = prog.forward(ctx, x)
-        loss, correct, dl = ops.softmax_xent(logits, y, True, True, grad_dtype=dtype)
-        ctx.tape.backward(logits, dl)
+        # the training step under the trainer's split policy (fl/trainer.py)
+        with ops.fp32_split(device, None, ops.train_h_ops(device) if impl is ops else None):
+            x, y = ops.gather_images(src, labels, idx, masks, trig, pn, 2, None, dtype)
+            ctx = prog.Ctx(spec, state, state, None, train=True, grads=grads, nvalid=nvalid, act_dtype=dtype)
+            logits = prog.forward(ctx, x)
+            loss, correct, dl = ops.softmax_xent(logits, y, True, True, grad_dtype=dtype)
+            ctx.tape.backward(logits, dl)
         g0 = grads.clone()
         lr = torch.full((G,), 0.1, device=device, dtype=torch.float32)
         one = torch.ones(G, dtype=torch.int32, device=device)
@@ -73,14 +75,18 @@ def run_smoke(device: torch.device, G: int = 2, N: int = 8) -> dict:
         loss_r, g_r, el_r = _step(torch.device("cpu"), torch.float64, ref, G, N)
     finally:
         ref.COMPUTE_DTYPE = old
+    # plain PyTorch fp32 on the same device: the precision the reference runs at
+    _, g_t, el_t = _step(device, torch.float32, ref, G, N)
     out = {"device": str(device), "backend": ops.backend_name(device), "dtype": "fp32",
            "loss": [float(v) for v in loss], "loss_ref_fp64": [float(v) for v in loss_r],
            "grad_norm": float(g.double().norm()), "grad_norm_ref": float(g_r.norm()),
            "grad_rel_err": _rel(g, g_r), "eval_logits_rel_err": _rel(el, el_r),
+           "torch_fp32_grad_rel_err": _rel(g_t, g_r), "torch_fp32_eval_logits_rel_err": _rel(el_t, el_r),
            "seconds": round(secs, 3)}
     assert all(abs(a - b) <= 1e-5 * max(1.0, abs(b)) for a, b in zip(out["loss"], out["loss_ref_fp64"])), out
-    # a random-init ResNet with 8-image BatchNorm amplifies rounding: plain fp32 torch is
-    # itself ~2e-3 from fp64 on these inputs, so the gradient bound is 1e-2 (a bf16 path
-    # lands at ~2e-1); the folded eval forward is well conditioned (fp32 level, 1e-4)
-    assert out["grad_rel_err"] < 1e-2 and out["eval_logits_rel_err"] < 1e-4, out
+    # a random-init ResNet with 8-image BatchNorm amplifies rounding ~1e4-fold: plain fp32
+    # torch is itself ~1e-3 from fp64 on these inputs (a bf16 path lands at ~2e-1), so the
+    # kernels must stay within a small factor of torch-fp32's own error
+    assert out["grad_rel_err"] < max(1e-4, 4 * out["torch_fp32_grad_rel_err"]), out
+    assert out["eval_logits_rel_err"] < max(1e-6, 4 * out["torch_fp32_eval_logits_rel_err"]), out
     return out
