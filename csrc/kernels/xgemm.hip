@@ -1166,7 +1166,11 @@ int xhalo_try(const XArgs& a, int G, int KH, int KW, hipStream_t st) {
   if (!(a.dsg == 1 ? (c.bh == -1 && c.bw == -1) : (c.bh == 1 && c.bw == 1))) return -100;
   if (a.Hs != a.Ho || a.Ws != a.Wo || a.Ho != a.Wo || (a.Ncol & 3) != 0) return -100;
   if (!aligned16(a.src) || !aligned16(a.w) || a.src_gstride % 4 || a.w_sstride % 4) return -100;
+  // 8-row tiles (each wave 64 x 32: two A fragments per B fragment) when they still give the
+  // launch >= 1024 blocks; 4-row tiles otherwise
+  const bool big = a.Ho % 8 == 0 && (long long)a.N * (a.Ho / 8) * G >= 1024;
   if (a.Wo == 32 && a.Cs == 32 && a.Ncol <= 32 && a.Ho % 4 == 0) {
+    if (a.amax_src && big) return xhalo_go<32, 32, 256, 32, 4, 1, 2, true>(a, G, st);
     if (a.amax_src) return xhalo_go<32, 32, 128, 32, 4, 1, 2, true>(a, G, st);
     if (planes() == 2) return xhalo_go<32, 32, 128, 32, 4, 1, 2, false>(a, G, st);
     return xhalo_go<32, 32, 128, 32, 4, 1, 3, false>(a, G, st);

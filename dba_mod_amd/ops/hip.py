@@ -31,7 +31,7 @@ _F = ctypes.c_float
 _U = ctypes.c_uint
 
 _SIGS = {
-    "dba_gather_images": [_P, _P, _P, _P, _P, _P, _I, _P, _P, _I, _P, _I, _I, _I, _I, _I, _P],
+    "dba_gather_images": [_P, _P, _P, _P, _P, _P, _I, _P, _P, _I, _P, _I, _I, _I, _I, _I, _I, _P],
     "dba_gather_rows": [_P, _P, _P, _P, _P, _I, _P, _P, _I, _P, _I, _P, _I, _I, _I, _P],
     "dba_conv_fwd": [_P, _LL, _P, _LL, _P, _P, _LL, _P, _LL, _P, _LL, _I, _P] + [_I] * 13 + [_P],
     "dba_conv_dgrad": [_P, _LL, _P, _LL, _P, _P, _LL, _P] + [_I] * 12 + [_P],
@@ -153,15 +153,32 @@ def _f32(t: Tensor) -> int:
 
 
 # ------------------------------------------------------------------------- data ingest
-def gather_images(src, labels, idx, trig_masks, trig_id, poison_n, target, flip_seeds, out_dtype):
+_UNIT_AMAX = {}
+
+
+def _unit_amax(G: int, device):
+    """A constant max-|x| slot holding 1.0: gathered images are in [0, 1] (x / 255)."""
+    key = (G, device)
+    if key not in _UNIT_AMAX:
+        a = torch.zeros(AMAX_SUB, _amax_ld(G), dtype=torch.int32, device=device)
+        a[0, :G] = 0x3F800000
+        _UNIT_AMAX[key] = a
+    return _UNIT_AMAX[key]
+
+
+def gather_images(src, labels, idx, trig_masks, trig_id, poison_n, target, flip_seeds, out_dtype, pad_c=None):
+    """``pad_c``: channels per output pixel (>= the dataset's; the extra ones are zero)."""
     G, B = idx.shape
     _, H, W, C = src.shape
-    x = torch.empty(G, B, H, W, C, dtype=out_dtype, device=src.device)
+    Co = max(C, int(pad_c or C))
+    x = torch.empty(G, B, H, W, Co, dtype=out_dtype, device=src.device)
     y = torch.empty(G, B, dtype=torch.int32, device=src.device)
     idx, trig_id, poison_n, fs = _i32(idx), _i32(trig_id), _i32(poison_n), _i32(flip_seeds)
     _call("dba_gather_images", src.data_ptr(), _i32(labels).data_ptr(), idx.data_ptr(),
           trig_masks.contiguous().data_ptr(), trig_id.data_ptr(), poison_n.data_ptr(), int(target), _ptr(fs),
-          x.data_ptr(), int(out_dtype == torch.float32), y.data_ptr(), G, B, H, W, C, _stream())
+          x.data_ptr(), int(out_dtype == torch.float32), y.data_ptr(), G, B, H, W, C, Co, _stream())
+    if _MODE == F16_PAIR and out_dtype == _F32:
+        x._dba_amax = _unit_amax(G, x.device)   # an upper bound is all the scale needs
     return x, y
 
 
@@ -362,7 +379,10 @@ def weight_amax(flat, segments):
 
 def _amax_w(w, gstride, n):
     a = getattr(w, "_dba_amax", None)
-    return a if a is not None else _amax(w, gstride, n)
+    if a is None:
+        a = _amax(w, gstride, n)
+        w._dba_amax = a   # weights are not written while this view is alive
+    return a
 
 
 def _amax_act(t, nvalid):
