@@ -12,9 +12,7 @@ __global__ void gather_images_kernel(const uint8_t* __restrict__ src, const int*
                                      const int* __restrict__ idx, const uint8_t* __restrict__ masks,
                                      const int* __restrict__ trig, const int* __restrict__ poison_n, int target,
                                      const int* __restrict__ flip_seeds, OutT* __restrict__ out,
-                                     int* __restrict__ yout, int G, int B, int H, int W, int C, int Co) {
-  // Co >= C: output channels per pixel (the extra ones zero: a 4-channel stem input keeps the
-  // consumer conv on 16-B vector loads)
+                                     int* __restrict__ yout, int G, int B, int H, int W, int C) {
   const long long total = (long long)G * B * H * W;
   for (long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x; t < total;
        t += (long long)gridDim.x * blockDim.x) {
@@ -25,8 +23,7 @@ __global__ void gather_images_kernel(const uint8_t* __restrict__ src, const int*
     const int b = (int)(r % B);
     const int g = (int)(r / B);
     const int s = idx[g * B + b];
-    OutT* o = out + t * Co;
-    for (int c = C; c < Co; ++c) o[c] = from_f<OutT>(0.f);
+    OutT* o = out + t * C;
     if (s < 0) {
       for (int c = 0; c < C; ++c) o[c] = from_f<OutT>(0.f);
       if (h == 0 && w == 0) yout[g * B + b] = -1;
@@ -78,17 +75,16 @@ int grid_for(long long n) { return (int)std::max(1LL, std::min(8192LL, (n + 255)
 
 DBA_EXPORT int dba_gather_images(const void* src, const int* labels, const int* idx, const void* masks, const int* trig,
                                  const int* poison_n, int target, const int* flip_seeds, void* out, int out_f32,
-                                 int* yout, int G, int B, int H, int W, int C, int Co, void* stream) {
-  if (Co < C) return -106;
+                                 int* yout, int G, int B, int H, int W, int C, void* stream) {
   const long long n = (long long)G * B * H * W;
   if (out_f32)
     hipLaunchKernelGGL(gather_images_kernel<float>, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream,
                        (const uint8_t*)src, labels, idx, (const uint8_t*)masks, trig, poison_n, target, flip_seeds,
-                       (float*)out, yout, G, B, H, W, C, Co);
+                       (float*)out, yout, G, B, H, W, C);
   else
     hipLaunchKernelGGL(gather_images_kernel<uint16_t>, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream,
                        (const uint8_t*)src, labels, idx, (const uint8_t*)masks, trig, poison_n, target, flip_seeds,
-                       (uint16_t*)out, yout, G, B, H, W, C, Co);
+                       (uint16_t*)out, yout, G, B, H, W, C);
   DBA_LAUNCH_CHECK();
 }
 

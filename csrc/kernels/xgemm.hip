@@ -1168,7 +1168,8 @@ int xhalo_try(const XArgs& a, int G, int KH, int KW, hipStream_t st) {
   if (!aligned16(a.src) || !aligned16(a.w) || a.src_gstride % 4 || a.w_sstride % 4) return -100;
   // 8-row tiles (each wave 64 x 32: two A fragments per B fragment) when they still give the
   // launch >= 1024 blocks; 4-row tiles otherwise
-  const bool big = a.Ho % 8 == 0 && (long long)a.N * (a.Ho / 8) * G >= 1024;
+  static const bool big_ok = env_int("DBA_F32_HALO_BIG", 0) != 0;   // measured slower in the bench (profiles/r2_halo_tiles_ab.md)
+  const bool big = big_ok && a.Ho % 8 == 0 && (long long)a.N * (a.Ho / 8) * G >= 1024;
   if (a.Wo == 32 && a.Cs == 32 && a.Ncol <= 32 && a.Ho % 4 == 0) {
     if (a.amax_src && big) return xhalo_go<32, 32, 256, 32, 4, 1, 2, true>(a, G, st);
     if (a.amax_src) return xhalo_go<32, 32, 128, 32, 4, 1, 2, true>(a, G, st);

@@ -92,17 +92,13 @@ class Evaluator:
                 nval[c, g] = max(0, min(B, n - c * B))
         table_d = to_device(table, dev)
         nval_d = to_device(nval, dev)
-        # RGB images as 4-channel pixels on the fp32 GPU path: the stem conv then runs on 16-B
-        # vector loads (the 4th channel and its weights are zero)
-        pad_c = (4 if wl.kind == "image" and wl.test_store.images.shape[-1] == 3 and self.dtype == torch.float32
-                 and ops.backend_name(dev) == "hip" else None)
         for c in range(n_chunks):
             idx = table_d[c]
             # (one zeroed allocation for the chunk's fp16-pair operand-max slots)
             with ops.amax_arena(G, dev):
                 if wl.kind == "image":
                     x, y = ops.gather_images(wl.test_store.images, wl.test_store.labels, idx, wl.trig_masks,
-                                             trig, pn, self.target, None, self.dtype, pad_c=pad_c)
+                                             trig, pn, self.target, None, self.dtype)
                 else:
                     x, y = ops.gather_rows(wl.test_store.rows, wl.test_store.labels, idx, wl.trig_cols,
                                            wl.trig_vals, trig, pn, self.target, self.dtype)

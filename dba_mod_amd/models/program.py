@@ -147,8 +147,6 @@ class Ctx:
                 residual: Optional[Tensor] = None) -> Tensor:
         if not self.train:
             wf, bf = self.folded[conv]
-            if x.shape[-1] != wf.shape[-1]:
-                wf = self._padded_folded(conv, x.shape[-1])
             return ops.conv2d(x, wf, self.wsel, stride, pad, bias=bf, residual=residual, relu=relu,
                               nvalid=self.nvalid)
         w = self.w(conv)
@@ -178,18 +176,6 @@ class Ctx:
 
         self.tape.record((out,), (x, residual), bwd)
         return out
-
-    def _padded_folded(self, conv: str, cin: int) -> Tensor:
-        """Folded weights zero-padded to a channel-padded input (an RGB stem fed 4-channel
-        images keeps the fp32 conv on vector loads: fl/evaluate.py); cached in the bank."""
-        key = f"{conv}@c{cin}"
-        if key not in self.folded:
-            wf = self.folded[conv][0]
-            wp = torch.nn.functional.pad(wf, (0, cin - wf.shape[-1])).contiguous()
-            if hasattr(wf, "_dba_amax"):
-                wp._dba_amax = wf._dba_amax       # same values, same max
-            self.folded[key] = (wp, None)
-        return self.folded[key][0]
 
     def conv(self, x: Tensor, name: str, stride: int, pad: int, bias: Optional[str], relu: bool) -> Tensor:
         """Conv with its own bias (MnistNet); also used for linear layers as 1x1 convs."""

@@ -31,7 +31,7 @@ _F = ctypes.c_float
 _U = ctypes.c_uint
 
 _SIGS = {
-    "dba_gather_images": [_P, _P, _P, _P, _P, _P, _I, _P, _P, _I, _P, _I, _I, _I, _I, _I, _I, _P],
+    "dba_gather_images": [_P, _P, _P, _P, _P, _P, _I, _P, _P, _I, _P, _I, _I, _I, _I, _I, _P],
     "dba_gather_rows": [_P, _P, _P, _P, _P, _I, _P, _P, _I, _P, _I, _P, _I, _I, _I, _P],
     "dba_conv_fwd": [_P, _LL, _P, _LL, _P, _P, _LL, _P, _LL, _P, _LL, _I, _P] + [_I] * 13 + [_P],
     "dba_conv_dgrad": [_P, _LL, _P, _LL, _P, _P, _LL, _P] + [_I] * 12 + [_P],
@@ -166,17 +166,15 @@ def _unit_amax(G: int, device):
     return _UNIT_AMAX[key]
 
 
-def gather_images(src, labels, idx, trig_masks, trig_id, poison_n, target, flip_seeds, out_dtype, pad_c=None):
-    """``pad_c``: channels per output pixel (>= the dataset's; the extra ones are zero)."""
+def gather_images(src, labels, idx, trig_masks, trig_id, poison_n, target, flip_seeds, out_dtype):
     G, B = idx.shape
     _, H, W, C = src.shape
-    Co = max(C, int(pad_c or C))
-    x = torch.empty(G, B, H, W, Co, dtype=out_dtype, device=src.device)
+    x = torch.empty(G, B, H, W, C, dtype=out_dtype, device=src.device)
     y = torch.empty(G, B, dtype=torch.int32, device=src.device)
     idx, trig_id, poison_n, fs = _i32(idx), _i32(trig_id), _i32(poison_n), _i32(flip_seeds)
     _call("dba_gather_images", src.data_ptr(), _i32(labels).data_ptr(), idx.data_ptr(),
           trig_masks.contiguous().data_ptr(), trig_id.data_ptr(), poison_n.data_ptr(), int(target), _ptr(fs),
-          x.data_ptr(), int(out_dtype == torch.float32), y.data_ptr(), G, B, H, W, C, Co, _stream())
+          x.data_ptr(), int(out_dtype == torch.float32), y.data_ptr(), G, B, H, W, C, _stream())
     if _MODE == F16_PAIR and out_dtype == _F32:
         x._dba_amax = _unit_amax(G, x.device)   # an upper bound is all the scale needs
     return x, y

@@ -49,8 +49,8 @@ def _rows_valid(nvalid: Optional[Tensor], g: int, n: int) -> int:
 
 # ------------------------------------------------------------------------- data ingest
 def gather_images(src: Tensor, labels: Tensor, idx: Tensor, trig_masks: Tensor, trig_id: Tensor,
-                  poison_n: Tensor, target: int, flip_seeds: Optional[Tensor], out_dtype: torch.dtype,
-                  pad_c: Optional[int] = None) -> Tuple[Tensor, Tensor]:
+                  poison_n: Tensor, target: int, flip_seeds: Optional[Tensor], out_dtype: torch.dtype
+                  ) -> Tuple[Tensor, Tensor]:
     """uint8 NHWC gather + /255 + optional h-flip + pixel trigger + relabel (K17/K19).
 
     Row ``b`` of group ``g`` is flipped iff ``hash2(flip_seeds[g], b) & 1`` (per-client
@@ -77,8 +77,6 @@ def gather_images(src: Tensor, labels: Tensor, idx: Tensor, trig_masks: Tensor, 
     x = x * (1.0 / 255.0)
     x = torch.where(valid[..., None, None, None], x, torch.zeros_like(x))
     y = torch.where(valid, y, torch.full_like(y, -1))
-    if pad_c is not None and pad_c > C:
-        x = torch.nn.functional.pad(x, (0, pad_c - C))
     return x.to(out_dtype), y.to(torch.int32)
 
 
