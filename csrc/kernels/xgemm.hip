@@ -49,6 +49,9 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* base, long lo
 __device__ __forceinline__ float4 bload4(__amdgpu_buffer_rsrc_t r, int byte_off) {
   return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, 0));
 }
+__device__ __forceinline__ uint2 bload8(__amdgpu_buffer_rsrc_t r, int byte_off) {
+  return __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(r, byte_off, 0, 0));
+}
 __device__ __forceinline__ float bload1(__amdgpu_buffer_rsrc_t r, int byte_off) {
   return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, byte_off, 0, 0));
 }
@@ -252,12 +255,15 @@ struct XArgs {
   const int* amax_w;                         // H: max |w| slot, indexed by weight slot
   int* amax_out;                             // optional: fold max |out| (zeroed slot)
   int amax_src_ld, amax_w_ld, amax_out_ld;
+  const uint16_t* wp;                        // H: the weights pre-split (xsplit_w_kernel): per slot
+  long long wp_sstride;                      //    2 planes of wp_sstride/2 fp16, scaled like amax_w
   XClass cls[4];
 };
 
-template <int BM, int BN, int WM, int WN, int P, int VEC, bool H>
+template <int BM, int BN, int WM, int WN, int P, int VEC, bool H, bool PW = false>
 __global__ __launch_bounds__(256) void xconv_kernel(const XArgs a) {
   static_assert(!H || P == 2, "fp16 split: 2 planes");
+  static_assert(!PW || (H && VEC >= 4), "pre-split weights: fp16 pair, vector loads");
   constexpr int TM = BM / WM, TN = BN / WN, MI = TM / 32, NJ = TN / 32;
   static_assert(WM * WN == 4 && MI >= 1 && NJ >= 1, "wave tiling");
   constexpr int ROWS = BM + BN, PL = ROWS * 4;   // uint4 per plane image
@@ -322,6 +328,10 @@ __global__ __launch_bounds__(256) void xconv_kernel(const XArgs a) {
   }
   const __amdgpu_buffer_rsrc_t rA = rsrc(src, (long long)a.N * a.Hs * a.Ws * Cs * 4);
   const __amdgpu_buffer_rsrc_t rB = rsrc(Bp, (long long)a.Ncol * K * 4);
+  // PW: the two fp16 planes of the weights (same element offsets, 2 B each)
+  const uint16_t* Bh = PW ? a.wp + (long long)slot * a.wp_sstride + c.boff : nullptr;
+  const __amdgpu_buffer_rsrc_t rBh = rsrc(Bh, (long long)a.Ncol * K * 2);
+  const __amdgpu_buffer_rsrc_t rBl = rsrc(PW ? Bh + (a.wp_sstride >> 1) : nullptr, (long long)a.Ncol * K * 2);
   // reduction state of the thread's quarter: element k = kt*32 + kq*4 is channel kc of tap (ki, kj)
   int ki = 0, kj = 0, kc = 0;
   if (nkt > 0) {
@@ -391,7 +401,11 @@ __global__ __launch_bounds__(256) void xconv_kernel(const XArgs a) {
       }
     } else {
       const int j = q - RA;
-      if constexpr (VEC >= 4) {
+      if constexpr (PW) {   // planes, as the bits of one float4
+        const int off = (boffs[j] >= 0 && g_kb < K) ? (boffs[j] + g_kb) * 2 : kOOB;
+        const uint2 h = bload8(rBh, off), l = bload8(rBl, off);
+        rb[st][j] = __builtin_bit_cast(float4, make_uint4(h.x, h.y, l.x, l.y));
+      } else if constexpr (VEC >= 4) {
         rb[st][j] = bload4(rB, (boffs[j] >= 0 && g_kb < K) ? (boffs[j] + g_kb) * 4 : kOOB);
       } else {
         float v[4];
@@ -418,8 +432,15 @@ __global__ __launch_bounds__(256) void xconv_kernel(const XArgs a) {
       lds_put<P, false, BM>(L, PL, 0, r0 + 32 * q, kq, sp);
     } else {
       const int j = q - RA;
-      if constexpr (H) split4h(rb[st][j].x, rb[st][j].y, rb[st][j].z, rb[st][j].w, hs.mb, sp);
-      else split4<P>(rb[st][j].x, rb[st][j].y, rb[st][j].z, rb[st][j].w, sp);
+      if constexpr (PW) {
+        const uint4 u = __builtin_bit_cast(uint4, rb[st][j]);
+        sp[0] = make_uint2(u.x, u.y);
+        sp[1] = make_uint2(u.z, u.w);
+      } else if constexpr (H) {
+        split4h(rb[st][j].x, rb[st][j].y, rb[st][j].z, rb[st][j].w, hs.mb, sp);
+      } else {
+        split4<P>(rb[st][j].x, rb[st][j].y, rb[st][j].z, rb[st][j].w, sp);
+      }
       lds_put<P, false, BN>(L, PL, BM, r0 + 32 * j, kq, sp);
     }
   };
@@ -531,9 +552,10 @@ __device__ __forceinline__ int hswz(int pp) {
   return (pp >> (CH == 4 ? 2 : 1)) & (CH - 1);
 }
 
-template <int W, int CS, int BM, int BN, int WM, int WN, int P, bool H>
+template <int W, int CS, int BM, int BN, int WM, int WN, int P, bool H, bool PRE = false>
 __global__ __launch_bounds__(256) void xhalo_kernel(const XArgs a) {
   static_assert(!H || P == 2, "fp16 split: 2 planes");
+  static_assert(!PRE || H, "pre-split weights: fp16 pair");
   constexpr int TR = BM / W, PW = W + 2, PR = TR + 2, PP = PR * PW;
   constexpr int CH = CS / 8, PATCH = PP * CH;             // uint4 per plane
   constexpr int TM = BM / WM, TN = BN / WN, MI = TM / 32, NJ = TN / 32;
@@ -607,10 +629,19 @@ __global__ __launch_bounds__(256) void xhalo_kernel(const XArgs a) {
     boffs[j] = n < a.Ncol ? n * K : -1;
   }
   const __amdgpu_buffer_rsrc_t rB = rsrc(Bp, (long long)a.Ncol * K * 4);
+  const uint16_t* Bh = PRE ? a.wp + (long long)slot * a.wp_sstride : nullptr;
+  const __amdgpu_buffer_rsrc_t rBh = rsrc(Bh, (long long)a.Ncol * K * 2);
+  const __amdgpu_buffer_rsrc_t rBl = rsrc(PRE ? Bh + (a.wp_sstride >> 1) : nullptr, (long long)a.Ncol * K * 2);
   float4 rb[2][RB];
   auto gq = [&](int t, int st, int j) __attribute__((always_inline)) {   // quarter j of weight step t -> stage st
     const int kb = t * 32 + kq * 4;
-    rb[st][j] = bload4(rB, (boffs[j] >= 0 && kb < K) ? (boffs[j] + kb) * 4 : kOOB);
+    if constexpr (PRE) {
+      const int off = (boffs[j] >= 0 && kb < K) ? (boffs[j] + kb) * 2 : kOOB;
+      const uint2 h = bload8(rBh, off), l = bload8(rBl, off);
+      rb[st][j] = __builtin_bit_cast(float4, make_uint4(h.x, h.y, l.x, l.y));
+    } else {
+      rb[st][j] = bload4(rB, (boffs[j] >= 0 && kb < K) ? (boffs[j] + kb) * 4 : kOOB);
+    }
   };
   auto gload = [&](int t, int st) __attribute__((always_inline)) {
 #pragma unroll
@@ -619,8 +650,15 @@ __global__ __launch_bounds__(256) void xhalo_kernel(const XArgs a) {
   auto lput_q = [&](int buf, int st, int q) __attribute__((always_inline)) {
     if (q >= RB) return;
     uint2 sp[P];
-    if constexpr (H) split4h(rb[st][q].x, rb[st][q].y, rb[st][q].z, rb[st][q].w, hs.mb, sp);
-    else split4<P>(rb[st][q].x, rb[st][q].y, rb[st][q].z, rb[st][q].w, sp);
+    if constexpr (PRE) {
+      const uint4 u = __builtin_bit_cast(uint4, rb[st][q]);
+      sp[0] = make_uint2(u.x, u.y);
+      sp[1] = make_uint2(u.z, u.w);
+    } else if constexpr (H) {
+      split4h(rb[st][q].x, rb[st][q].y, rb[st][q].z, rb[st][q].w, hs.mb, sp);
+    } else {
+      split4<P>(rb[st][q].x, rb[st][q].y, rb[st][q].z, rb[st][q].w, sp);
+    }
     lds_put<P, false, BN>(bring + buf * P * BPL, BPL, 0, r0 + 32 * q, kq, sp);
   };
 
@@ -1049,6 +1087,32 @@ __global__ void xtranspose_kernel(const XTBatch b, int slots, const int* __restr
   }
 }
 
+// w [slots][per] fp32 (slot stride sstride) -> planes [slots][2][per] fp16 of w * 2^sb, sb from
+// the slot's max |w| exactly as HScale computes it: a weight operand split once for all the
+// blocks (and launches) that stage it
+__global__ __launch_bounds__(256) void xsplit_w_kernel(const float* __restrict__ w, long long sstride, long long per,
+                                                       const int* __restrict__ amax, int ld,
+                                                       uint16_t* __restrict__ out) {
+  const int sl = blockIdx.y;
+  const int sb = hexp(amax_read(amax, ld, sl));
+  const float mb = __uint_as_float((uint32_t)(sb + 127) << 23);
+  const float* __restrict__ src = w + (long long)sl * sstride;
+  uint16_t* __restrict__ oh = out + (long long)sl * 2 * per;
+  uint16_t* __restrict__ ol = oh + per;
+  for (long long e = (blockIdx.x * 256LL + threadIdx.x) * 4; e < per; e += (long long)gridDim.x * 1024) {
+    float v[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] = e + i < per ? src[e + i] : 0.f;
+    uint2 sp[2];
+    split4h(v[0], v[1], v[2], v[3], mb, sp);
+    const uint16_t* h = (const uint16_t*)&sp[0];
+    const uint16_t* l = (const uint16_t*)&sp[1];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      if (e + i < per) { oh[e + i] = h[i]; ol[e + i] = l[i]; }
+  }
+}
+
 // max |x| of n segments (offset, length) of every replica's flat row (the conv weights of a
 // model replica: one launch per training step instead of one per conv); out[s][g]
 constexpr int kAmaxSegs = 64;
@@ -1126,34 +1190,34 @@ int& planes() {
   return p;
 }
 
-template <int BM, int BN, int WM, int WN, int P, int VEC, bool H>
+template <int BM, int BN, int WM, int WN, int P, int VEC, bool H, bool PW>
 int xconv_go(const XArgs& a, long long Mmax, int G, int nclass, hipStream_t st) {
   XArgs b = a;
   b.tiles_n = ceil_div(a.Ncol, BN);
   const dim3 grid((unsigned)(ceil_div(Mmax, BM) * b.tiles_n), G, nclass * a.splitk);
-  hipLaunchKernelGGL((xconv_kernel<BM, BN, WM, WN, P, VEC, H>), grid, dim3(256), 0, st, b);
+  hipLaunchKernelGGL((xconv_kernel<BM, BN, WM, WN, P, VEC, H, PW>), grid, dim3(256), 0, st, b);
   DBA_LAUNCH_CHECK();
 }
 
-template <int P, int VEC, bool H>
+template <int P, int VEC, bool H, bool PW = false>
 int xconv_tile(const XArgs& a, long long Mmax, int G, int nclass, int bm, hipStream_t st) {
-  if (a.Ncol <= 32) return xconv_go<128, 32, 4, 1, P, VEC, H>(a, Mmax, G, nclass, st);
+  if (a.Ncol <= 32) return xconv_go<128, 32, 4, 1, P, VEC, H, PW>(a, Mmax, G, nclass, st);
   if (a.Ncol <= 64) {
-    if (bm == 64) return xconv_go<64, 64, 2, 2, P, VEC, H>(a, Mmax, G, nclass, st);
-    return xconv_go<128, 64, 2, 2, P, VEC, H>(a, Mmax, G, nclass, st);
+    if (bm == 64) return xconv_go<64, 64, 2, 2, P, VEC, H, PW>(a, Mmax, G, nclass, st);
+    return xconv_go<128, 64, 2, 2, P, VEC, H, PW>(a, Mmax, G, nclass, st);
   }
-  if (bm == 64) return xconv_go<64, 128, 2, 2, P, VEC, H>(a, Mmax, G, nclass, st);
-  return xconv_go<128, 128, 2, 2, P, VEC, H>(a, Mmax, G, nclass, st);
+  if (bm == 64) return xconv_go<64, 128, 2, 2, P, VEC, H, PW>(a, Mmax, G, nclass, st);
+  return xconv_go<128, 128, 2, 2, P, VEC, H, PW>(a, Mmax, G, nclass, st);
 }
 
 bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
-template <int W, int CS, int BM, int BN, int WM, int WN, int P, bool H>
+template <int W, int CS, int BM, int BN, int WM, int WN, int P, bool H, bool PRE = false>
 int xhalo_go(const XArgs& a, int G, hipStream_t st) {
   XArgs b = a;
   b.tiles_n = ceil_div(a.Ncol, BN);
   const dim3 grid((unsigned)(a.N * (a.Ho / (BM / W)) * b.tiles_n), G, 1);
-  hipLaunchKernelGGL((xhalo_kernel<W, CS, BM, BN, WM, WN, P, H>), grid, dim3(256), 0, st, b);
+  hipLaunchKernelGGL((xhalo_kernel<W, CS, BM, BN, WM, WN, P, H, PRE>), grid, dim3(256), 0, st, b);
   DBA_LAUNCH_CHECK();
 }
 
@@ -1171,7 +1235,8 @@ int xhalo_try(const XArgs& a, int G, int KH, int KW, hipStream_t st) {
   static const bool big_ok = env_int("DBA_F32_HALO_BIG", 0) != 0;   // measured slower in the bench (profiles/r2_halo_tiles_ab.md)
   const bool big = big_ok && a.Ho % 8 == 0 && (long long)a.N * (a.Ho / 8) * G >= 1024;
   if (a.Wo == 32 && a.Cs == 32 && a.Ncol <= 32 && a.Ho % 4 == 0) {
-    if (a.amax_src && big) return xhalo_go<32, 32, 256, 32, 4, 1, 2, true>(a, G, st);
+    if (a.amax_src && big && !a.wp) return xhalo_go<32, 32, 256, 32, 4, 1, 2, true>(a, G, st);
+    if (a.amax_src && a.wp) return xhalo_go<32, 32, 128, 32, 4, 1, 2, true, true>(a, G, st);
     if (a.amax_src) return xhalo_go<32, 32, 128, 32, 4, 1, 2, true>(a, G, st);
     if (planes() == 2) return xhalo_go<32, 32, 128, 32, 4, 1, 2, false>(a, G, st);
     return xhalo_go<32, 32, 128, 32, 4, 1, 3, false>(a, G, st);
@@ -1187,6 +1252,10 @@ int xconv_dispatch(const XArgs& a, long long Mmax, int G, int nclass, int vec, h
   const long long blocks = (long long)ceil_div(Mmax, 128) * ceil_div(a.Ncol, bn) * G * nclass * a.splitk;
   const int bm = (bn > 32 && blocks < 512) ? 64 : 128;
   if (vec == 4 && a.Cs % 32 == 0) vec = 32;
+  if (a.amax_src && a.wp && vec >= 4) {
+    if (vec == 32) return xconv_tile<2, 32, true, true>(a, Mmax, G, nclass, bm, st);
+    return xconv_tile<2, 4, true, true>(a, Mmax, G, nclass, bm, st);
+  }
   if (a.amax_src) {
     if (vec == 32) return xconv_tile<2, 32, true>(a, Mmax, G, nclass, bm, st);
     return vec == 4 ? xconv_tile<2, 4, true>(a, Mmax, G, nclass, bm, st)
@@ -1268,7 +1337,8 @@ DBA_EXPORT int dba_xconv_fwd(const float* x, long long x_gstride, const float* w
                              long long out_gstride, const int* nvalid, int G, int N, int H, int W, int Cin, int Ho,
                              int Wo, int Cout, int KH, int KW, int stride, int pad, int relu, const int* amax_x,
                              int amax_x_ld, const int* amax_w, int amax_w_ld, int* amax_out, int amax_out_ld,
-                             float* ws, long long ws_floats, void* stream) {
+                             const uint16_t* wp, long long wp_sstride, float* ws, long long ws_floats,
+                             void* stream) {
   hipStream_t st = (hipStream_t)stream;
   if ((long long)N * H * W * Cin >= (1LL << 29)) return -103;   // 32-bit in-replica byte offsets
   const long long M = (long long)N * Ho * Wo;
@@ -1281,6 +1351,7 @@ DBA_EXPORT int dba_xconv_fwd(const float* x, long long x_gstride, const float* w
   a.sp = stride; a.os = 1; a.dsg = 1; a.relu = relu; a.splitk = 1;
   a.amax_src = amax_x; a.amax_w = amax_w; a.amax_out = amax_out;
   a.amax_src_ld = amax_x_ld; a.amax_w_ld = amax_w_ld; a.amax_out_ld = amax_out_ld;
+  a.wp = wp; a.wp_sstride = wp_sstride;
   a.cls[0] = XClass{KH, KW, -pad, -pad, 0, 0, Ho, Wo, 0};
   if (stride == 1) {
     const int rc = xhalo_try(a, G, KH, KW, st);
@@ -1310,7 +1381,8 @@ DBA_EXPORT int dba_xconv_dgrad(const float* dy, long long dy_gstride, const floa
                                const int* wsel, const float* accum, float* dx, long long dx_gstride,
                                const int* nvalid, int G, int N, int H, int W, int Cin, int Ho, int Wo, int Cout,
                                int KH, int KW, int stride, int pad, const int* amax_dy, int amax_dy_ld,
-                               const int* amax_w, int amax_w_ld, float* ws, long long ws_floats, void* stream) {
+                               const int* amax_w, int amax_w_ld, const uint16_t* wp, long long wp_sstride, float* ws,
+                               long long ws_floats, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   if ((long long)N * Ho * Wo * Cout >= (1LL << 29)) return -103;   // 32-bit in-replica byte offsets
   const ClassGeom cg = dgrad_classes(H, W, Cin, Cout, KH, KW, stride, pad);
@@ -1322,6 +1394,7 @@ DBA_EXPORT int dba_xconv_dgrad(const float* dy, long long dy_gstride, const floa
   a.sp = 1; a.os = stride; a.dsg = -1; a.relu = 0; a.splitk = 1;
   a.amax_src = amax_dy; a.amax_w = amax_w;
   a.amax_src_ld = amax_dy_ld; a.amax_w_ld = amax_w_ld;
+  a.wp = wp; a.wp_sstride = wp_sstride;
   long long Mmax = 0;
   for (int i = 0; i < cg.n; ++i) {
     a.cls[i] = cg.c[i];
@@ -1438,6 +1511,14 @@ DBA_EXPORT int dba_xwgrad(const float* dy, long long dy_gstride, const float* x,
     hipLaunchKernelGGL(xwgrad_reduce_kernel, g2, dim3(256), 0, st, (const float*)ws, G, per, nvalid, N, Ho * Wo,
                        mchunk, dw, dw_gstride);
   }
+  DBA_LAUNCH_CHECK();
+}
+
+// out [slots][2][per] fp16 planes of w (see xsplit_w_kernel); amax: the weights' max slot
+DBA_EXPORT int dba_xsplit_w(const float* w, long long sstride, long long per, int slots, const int* amax, int ld,
+                            uint16_t* out, void* stream) {
+  const dim3 grid((unsigned)std::max(1LL, std::min(1024LL, (per + 1023) / 1024)), slots);
+  hipLaunchKernelGGL(xsplit_w_kernel, grid, dim3(256), 0, (hipStream_t)stream, w, sstride, per, amax, ld, out);
   DBA_LAUNCH_CHECK();
 }
 

@@ -78,8 +78,9 @@ _SIGS = {
     # reference-precision (fp32) family: csrc/kernels/xgemm.hip
     "dba_xgemm_set_planes": [_I],
     "dba_xconv_ws_floats": [_I] * 8,
-    "dba_xconv_fwd": [_P, _LL, _P, _LL, _P, _P, _LL, _P, _P, _LL, _P] + [_I] * 13 + [_P, _I] * 3 + [_P, _LL, _P],
-    "dba_xconv_dgrad": [_P, _LL, _P, _LL, _P, _P, _P, _LL, _P] + [_I] * 12 + [_P, _I] * 2 + [_P, _LL, _P],
+    "dba_xconv_fwd": [_P, _LL, _P, _LL, _P, _P, _LL, _P, _P, _LL, _P] + [_I] * 13 + [_P, _I] * 3 + [_P, _LL] * 2 + [_P],
+    "dba_xconv_dgrad": [_P, _LL, _P, _LL, _P, _P, _P, _LL, _P] + [_I] * 12 + [_P, _I] * 2 + [_P, _LL] * 2 + [_P],
+    "dba_xsplit_w": [_P, _LL, _LL, _I, _P, _I, _P, _P],
     "dba_amax": [_P, _LL, _LL, _P, _LL, _I, _P, _I, _P],
     "dba_xtranspose": [_P, _I, _I, _LL, _P, _P],
     "dba_xwgrad_ws_floats": [_I] * 8 + [_P],
@@ -375,6 +376,23 @@ def weight_amax(flat, segments):
     return slots
 
 
+def split_weights(w, sstride: int, per: int, amax):
+    """fp16-pair planes of a weight operand ([slots][2][per] fp16, scaled by the slot's max |w|,
+    csrc/kernels/xgemm.hip xsplit_w_kernel), attached as ``w._dba_planes``: every block of every
+    launch that stages these weights then loads the planes instead of re-splitting them."""
+    slots = w.shape[0]
+    out = torch.empty(slots, 2, per, dtype=torch.int16, device=w.device)
+    _call("dba_xsplit_w", w.data_ptr(), sstride, per, slots, amax.data_ptr(), amax.shape[1], out.data_ptr(), _stream())
+    w._dba_planes = out
+    return out
+
+
+def _wplanes(w):
+    """(pointer, slot stride) of ``w``'s fp16-pair planes, if split (fp16-pair launches only)."""
+    p = getattr(w, "_dba_planes", None)
+    return (None, 0) if p is None or _MODE != F16_PAIR else (p.data_ptr(), p.stride(0))
+
+
 def _amax_w(w, gstride, n):
     a = getattr(w, "_dba_amax", None)
     if a is None:
@@ -406,10 +424,10 @@ def _xconv_fwd(x, w, wsel, stride, pad, bias, residual, relu, nvalid, out_dtype)
     if out_dtype not in (None, _F32):
         raise TypeError(f"fp32 conv cannot emit {out_dtype} (no silent precision conversion)")
     G, N, H, W, Cin = x.shape
-    aw0 = getattr(w, "_dba_amax", None)
+    attrs = {k: getattr(w, k) for k in ("_dba_amax", "_dba_planes") if hasattr(w, k)}
     w, ws = _check_w(w, _F32)
-    if aw0 is not None:
-        w._dba_amax = aw0
+    for k, v in attrs.items():
+        setattr(w, k, v)
     Cout, KH, KW = w.shape[1], w.shape[2], w.shape[3]
     assert w.shape[4] == Cin, (w.shape, x.shape)
     Ho = (H + 2 * pad - KH) // stride + 1
@@ -429,7 +447,7 @@ def _xconv_fwd(x, w, wsel, stride, pad, bias, residual, relu, nvalid, out_dtype)
         ay = _amax_out(y)   # the output's max, for its consumers
     _call("dba_xconv_fwd", x.data_ptr(), N * H * W * Cin, w.data_ptr(), ws, _ptr(_i32(wsel)), _ptr(bias), bs,
           _ptr(res), y.data_ptr(), N * Ho * Wo * Cout, _ptr(_i32(nvalid)), G, N, H, W, Cin, Ho, Wo, Cout, KH, KW,
-          stride, pad, int(relu), *_aptr(ax), *_aptr(aw), *_aptr(ay), _ptr(wsb), n, _stream())
+          stride, pad, int(relu), *_aptr(ax), *_aptr(aw), *_aptr(ay), *_wplanes(w), _ptr(wsb), n, _stream())
     return y
 
 
@@ -580,7 +598,7 @@ def _xconv_dgrad(dy, w, wsel, stride, pad, in_hw, nvalid, out_dtype, accum, wt):
         ad, aw = _amax_act(dy, nvalid), (a0 if a0 is not None else _amax(wt, per, per))
     _call("dba_xconv_dgrad", dy.data_ptr(), N * Ho * Wo * Cout, wt.data_ptr(), per, _ptr(_i32(wsel)), _ptr(acc),
           dx.data_ptr(), N * H * W * Cin, _ptr(_i32(nvalid)), G, N, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad,
-          *_aptr(ad), *_aptr(aw), _ptr(wsb), n, _stream())
+          *_aptr(ad), *_aptr(aw), *_wplanes(wt), _ptr(wsb), n, _stream())
     return dx
 
 
@@ -804,6 +822,8 @@ def bn_fold(w, conv_bias, gamma, beta, rmean, rvar, eps, out_dtype):
           _stream())
     if out_dtype == _F32:
         wf._dba_amax = _amax(wf, Cout * K, Cout * K)   # the folded weights' scale, once per fold
+        if _MODE == F16_PAIR:
+            split_weights(wf, Cout * K, Cout * K, wf._dba_amax)   # and their fp16 planes
     return wf, bf
 
 

@@ -71,6 +71,10 @@ def _bench_fp32(name, G, N, Hh, Cin, Cout, k, s, p, reps, dev):
     dy = torch.randn(G, N, Ho, Ho, Cout, device=dev)
     flops = 2.0 * G * N * Ho * Ho * Cout * k * k * Cin
     rec = {"shape": name, "dtype": "fp32"}
+    if name.startswith("eval") and H.fp32_mode() == H.F16_PAIR:
+        # evaluation weights are static: split into fp16-pair planes once (as bn_fold does)
+        per = Cout * k * k * Cin
+        H.split_weights(w, per, per, H._amax_w(w, per, per))
     ops = [("fwd", lambda: H.conv2d(x, w, None, s, p, relu=True))]
     if name.startswith("train"):
         wt = H.prepare_dgrad_weights(w, [(w, None, s, p, (Hh, Hh), None, G)])[0]

@@ -167,6 +167,27 @@ def test_fp32_conv_fp16_pair(H, R64, case):
         H.set_fp32_planes(prev)
 
 
+@pytest.mark.parametrize("case", [CASES[1], CASES[2], CASES[4], CASES[5], CASES[13], CASES[16], CASES[9]])
+def test_fp32_conv_fp16_pair_presplit_weights(H, R64, case):
+    """Forward convs reading the weights as pre-split fp16-pair planes (the evaluation path,
+    ops.hip.split_weights) give the same bits as splitting them while staging."""
+    prev = H.set_fp32_planes(16)
+    try:
+        dev = torch.device("cuda")
+        G, N, Hh, Ww, Cin, Cout, k, s, p = case
+        x, w, wsel, bias, nvalid, res, dy, acc = _inputs(case, dev)
+        y0 = H.conv2d(x, w, wsel, s, p, bias=bias, residual=res, relu=True, nvalid=nvalid)
+        w2 = w.clone()
+        per = Cout * k * k * Cin
+        H.split_weights(w2, per, per, H._amax_w(w2, per, per))
+        y1 = H.conv2d(x, w2, wsel, s, p, bias=bias, residual=res, relu=True, nvalid=nvalid)
+        for g in range(G):
+            n = int(nvalid[g])
+            assert torch.equal(y0[g, :n], y1[g, :n]), (case, g)
+    finally:
+        H.set_fp32_planes(prev)
+
+
 def _wide_range(x, w, bias, res, dy, acc):
     """Magnitudes far outside fp16's range and spread over ~2^12 inside a tile: activations
     ~1e-12 with a per-pixel log-normal spread, weights ~1e+6, gradients ~1e-9 with a
