@@ -1,4 +1,6 @@
-"""Runs a few conv kernels on fixed shapes (for rocprofv3 PMC counter collection)."""
+"""Runs a few kernels on fixed shapes for rocprofv3 PMC counter collection: conv shapes and the
+training BN forward / backward ``bn1``-``bn3`` (10 replicas x 64 images; ResNet stages 1-3:
+32x32 x 32, 16x16 x 64, 8x8 x 128 channels), as ``scripts/gpu/pmc_bn.sh`` profiles them."""
 from __future__ import annotations
 
 import sys

@@ -221,7 +221,7 @@ def test_bn_train_fwd_bwd(H, R, C, relu, with_res):
     _close(gr, gr_r, 2e-2, 2e-2, "dgamma/dbeta")
 
 
-@pytest.mark.parametrize("C,Hh", [(32, 32), (64, 16), (128, 12)])
+@pytest.mark.parametrize("C,Hh", [(32, 32), (64, 16), (128, 12), (256, 12), (512, 12)])
 def test_bn_train_large_multiblock(H, R, C, Hh):
     """Multi-block reduce path (rows > the single-launch limit: partials, finalize, apply),
     fwd + bwd, repeated eager calls and a HIP-graph replay against the fp32 reference."""
