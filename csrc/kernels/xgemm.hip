@@ -1241,8 +1241,14 @@ int xhalo_try(const XArgs& a, int G, int KH, int KW, hipStream_t st) {
     if (planes() == 2) return xhalo_go<32, 32, 128, 32, 4, 1, 2, false>(a, G, st);
     return xhalo_go<32, 32, 128, 32, 4, 1, 3, false>(a, G, st);
   }
-  // (W 16 / Cs 64 as 64x64 halo tiles measured slower than the 128x64 implicit GEMM: 147 vs
-  // 154 TF on the eval layer-2 shape, profiles/kbench_r2_fp32_p3.json — not routed here)
+  // W 16 / Cs 64 (8-row tiles x 64 channels) on the fp16 pair, where the implicit GEMM's
+  // re-split of every input element per tap is what bounds it (with 3 bf16 planes the MFMA
+  // work dominates and the implicit GEMM was faster: 154 vs 147 TF, kbench_r2_fp32_p3.json)
+  static const bool h16 = env_int("DBA_F32_HALO16", 1) != 0;
+  if (h16 && a.amax_src && a.Wo == 16 && a.Cs == 64 && a.Ncol <= 64 && a.Ho % 8 == 0) {
+    if (a.wp) return xhalo_go<16, 64, 128, 64, 2, 2, 2, true, true>(a, G, st);
+    return xhalo_go<16, 64, 128, 64, 2, 2, 2, true>(a, G, st);
+  }
   return -100;
 }
 
