@@ -148,6 +148,49 @@ __global__ void bn_finalize_kernel(const float* __restrict__ part, int nblk, con
   *prv = (float)((1.0 - momentum) * (*prv) + momentum * unb);
 }
 
+// finalize from the conv-epilogue partials (xgemm.hip bn_tile_stats): part[g][c][2][nblk] fp64,
+// one block per (channel, replica), every thread sums a fixed stride of 32-row groups in
+// fp64, then a fixed LDS tree — the order depends on nblk only.
+__global__ __launch_bounds__(256) void bn_finalize_part_kernel(const double* __restrict__ part, int nblk,
+                                                               const int* __restrict__ nvalid, int N, int HW, int C,
+                                                               float* __restrict__ rm, float* __restrict__ rv,
+                                                               long long s_gstride, float momentum, float eps,
+                                                               float* __restrict__ mean, float* __restrict__ invstd) {
+  __shared__ double red[2][256];
+  const int c = blockIdx.x, g = blockIdx.y, tid = threadIdx.x;
+  const double* __restrict__ p = part + ((long long)g * C + c) * 2 * nblk;
+  double a0 = 0, a1 = 0;
+#pragma unroll 4
+  for (int b = tid; b < nblk; b += 256) {
+    a0 += p[b];
+    a1 += p[nblk + b];
+  }
+  red[0][tid] = a0;
+  red[1][tid] = a1;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (tid < w) {
+      red[0][tid] += red[0][tid + w];
+      red[1][tid] += red[1][tid + w];
+    }
+    __syncthreads();
+  }
+  if (tid != 0) return;
+  const int i = g * C + c;
+  const double n = (double)valid_rows(nvalid, g, N) * HW;
+  if (n <= 0) { mean[i] = 0.f; invstd[i] = 0.f; return; }
+  const double m = red[0][0] / n;
+  double var = red[1][0] / n - m * m;
+  var = var > 0 ? var : 0;
+  mean[i] = (float)m;
+  invstd[i] = (float)(1.0 / sqrt(var + (double)eps));
+  float* prm = rm + (long long)g * s_gstride + c;
+  float* prv = rv + (long long)g * s_gstride + c;
+  const double unb = n > 1 ? var * n / (n - 1) : var;
+  *prm = (float)((1.0 - momentum) * (*prm) + momentum * m);
+  *prv = (float)((1.0 - momentum) * (*prv) + momentum * unb);
+}
+
 // Elementwise passes: 256 % (C/8) == 0, so every thread of the grid-stride loop always owns
 // the same 8 channels; their per-(replica, channel) coefficients are loaded once per replica
 // change instead of 4-7 scalar loads per element.
@@ -474,6 +517,16 @@ DBA_EXPORT int dba_bn_stats(const void* y, const int* nvalid, int G, int N, int 
                                nullptr, nullptr, nullptr, 0, nvalid, N, HW, C, part));
   hipLaunchKernelGGL(bn_finalize_kernel, dim3(ceil_div(C, C < 64 ? C : 64), G), dim3(256), 0, st, part, nblk, nvalid, N, HW, C,
                      rm, rv, s_gstride, momentum, eps, mean, invstd, G);
+  DBA_LAUNCH_CHECK();
+}
+
+// mean / invstd / running stats from the partials a conv epilogue folded (dba_xconv_fwd bnpart)
+DBA_EXPORT int dba_bn_finalize_part(const double* part, int nblk, const int* nvalid, int G, int N, int HW, int C,
+                                    float* rm, float* rv, long long s_gstride, float momentum, float eps, float* mean,
+                                    float* invstd, void* stream) {
+  if (!bn_layout_ok(C)) return -102;
+  hipLaunchKernelGGL(bn_finalize_part_kernel, dim3(C, G), dim3(256), 0, (hipStream_t)stream, part, nblk, nvalid, N, HW,
+                     C, rm, rv, s_gstride, momentum, eps, mean, invstd);
   DBA_LAUNCH_CHECK();
 }
 

@@ -257,8 +257,43 @@ struct XArgs {
   int amax_src_ld, amax_w_ld, amax_out_ld;
   const uint16_t* wp;                        // H: the weights pre-split (xsplit_w_kernel): per slot
   long long wp_sstride;                      //    2 planes of wp_sstride/2 fp16, scaled like amax_w
+  double* bnpart;                            // optional: BN statistics of the output (bn_tile_stats)
+  int bnpart_nblk;                           //    32-row groups per replica
   XClass cls[4];
 };
+
+// Training-BN statistics of a conv's output, folded into its epilogue (the separate BN
+// reduce pass over y is gone): for every 32-row group of GEMM rows (pixels) of the tile
+// staged in LDS (Ct, BM x BN, rows of invalid pixels are exact zeros: their A rows were
+// zero-filled), the column sum and sum of squares, summed over the 32 rows in order.  The
+// group is fixed at 32 rows whatever the tile height, so the partials — and the BN
+// statistics finalised from them — do not depend on the tile shape (which follows the
+// launch's replica count): world-size independent bits.  The sums run in fp64 (a square of
+// an fp32 value is exact there, and 32 of them sum exactly in all but extreme spreads), so the
+// statistics are fp64-accurate before the final rounding: E[x^2] - mean^2 keeps no fp32
+// cancellation error.  part[g][c][2][nblk] (fp64); zero: the tile has no valid row.
+template <int BM, int BN>
+__device__ __forceinline__ void bn_tile_stats(const float* Ct, double* __restrict__ part, int nblk, int g, int C,
+                                              int m0, int n0, bool zero) {
+  constexpr int NG = BM / 32;
+  for (int e = threadIdx.x; e < NG * BN; e += 256) {
+    const int grp = e / BN, cc = e - grp * BN, n = n0 + cc;
+    const int b = m0 / 32 + grp;
+    if (n >= C || b >= nblk) continue;
+    double s0 = 0.0, s1 = 0.0;
+    if (!zero) {
+#pragma unroll 8
+      for (int r = 0; r < 32; ++r) {
+        const double v = (double)Ct[(grp * 32 + r) * BN + cc];
+        s0 += v;
+        s1 = fma(v, v, s1);
+      }
+    }
+    double* p = part + ((long long)g * C + n) * 2 * nblk + b;
+    p[0] = s0;
+    p[nblk] = s1;
+  }
+}
 
 template <int BM, int BN, int WM, int WN, int P, int VEC, bool H, bool PW = false>
 __global__ __launch_bounds__(256) void xconv_kernel(const XArgs a) {
@@ -279,7 +314,10 @@ __global__ __launch_bounds__(256) void xconv_kernel(const XArgs a) {
   const int Mv = valid_rows(a.nvalid, g, a.N) * HqWq;
   const int tn = blockIdx.x % a.tiles_n, tm = blockIdx.x / a.tiles_n;
   const int m0 = tm * BM, n0 = tn * BN;
-  if (m0 >= Mv) return;
+  if (m0 >= Mv) {
+    if (a.bnpart && a.splitk == 1) bn_tile_stats<BM, BN>(nullptr, a.bnpart, a.bnpart_nblk, g, a.Ncol, m0, n0, true);
+    return;
+  }
   const int slot = a.wsel ? a.wsel[g] : g;
   const int Cs = a.Cs;
   const int K = c.nI * c.nJ * Cs;
@@ -498,6 +536,7 @@ __global__ __launch_bounds__(256) void xconv_kernel(const XArgs a) {
         Ct[(wm * TM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * hf) * BN + wn * TN + j * 32 + fr] = acc[i][j][r];
   __syncthreads();
   const bool fin = a.splitk == 1;
+  if (fin && a.bnpart) bn_tile_stats<BM, BN>(Ct, a.bnpart, a.bnpart_nblk, g, a.Ncol, m0, n0, false);
   float* out = a.out + (long long)g * a.out_gstride + (fin ? 0 : (long long)kz * a.zstride);
   const float* bias = (fin && a.bias) ? a.bias + (long long)slot * a.b_sstride : nullptr;
   const float* res = (fin && a.res) ? a.res + (long long)g * a.out_gstride : nullptr;
@@ -573,8 +612,11 @@ __global__ __launch_bounds__(256) void xhalo_kernel(const XArgs a) {
   const int HT = a.Ho / TR;                               // row tiles per image
   const int tn = blockIdx.x % a.tiles_n, tm = blockIdx.x / a.tiles_n;
   const int img = tm / HT, h0 = (tm - img * HT) * TR;
-  if (img >= valid_rows(a.nvalid, g, a.N)) return;
   const int n0 = tn * BN;
+  if (img >= valid_rows(a.nvalid, g, a.N)) {
+    if (a.bnpart) bn_tile_stats<BM, BN>(nullptr, a.bnpart, a.bnpart_nblk, g, a.Ncol, tm * BM, n0, true);
+    return;
+  }
   const int slot = a.wsel ? a.wsel[g] : g;
   const int K = 9 * CS;
   const float* __restrict__ src = a.src + (long long)g * a.src_gstride;
@@ -741,6 +783,7 @@ __global__ __launch_bounds__(256) void xhalo_kernel(const XArgs a) {
       for (int r = 0; r < 16; ++r)
         Ct[(wm * TM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * hf) * BN + wn * TN + j * 32 + fr] = acc[i][j][r];
   __syncthreads();
+  if (a.bnpart) bn_tile_stats<BM, BN>(Ct, a.bnpart, a.bnpart_nblk, g, a.Ncol, tm * BM, n0, false);
   float* out = a.out + (long long)g * a.out_gstride;
   const float* bias = a.bias ? a.bias + (long long)slot * a.b_sstride : nullptr;
   const float* res = a.res ? a.res + (long long)g * a.out_gstride : nullptr;
@@ -1025,7 +1068,55 @@ struct XWRBatch {
   XWRDesc d[kXWRBatch];
 };
 
+// ZG z-groups x (256 / ZG) lanes per block, a float4 of elements per lane: each lane sums the
+// slabs z = zg, zg + ZG, ... (unrolled, so several slab loads are in flight instead of one
+// serial chain of nz loads), then the group sums meet in LDS in z-group order.  ZG (16 for
+// many slabs, 4 otherwise) and so the order depend on nz only (per-replica geometry), never
+// on G: deterministic and world-size independent.
+template <int ZG, bool V4>
+__device__ __forceinline__ void xwr_body(const float* __restrict__ ws, long long zs, long long per, int nz,
+                                         float* __restrict__ dw, float4* red) {
+  constexpr int LN = 256 / ZG;   // lanes per z-group
+  const int lane = threadIdx.x % LN, zg = threadIdx.x / LN;
+  for (long long e0 = blockIdx.x * (LN * 4LL); e0 < per; e0 += (long long)gridDim.x * LN * 4) {
+    const long long e = e0 + lane * 4;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (e < per) {
+#pragma unroll 4
+      for (int z = zg; z < nz; z += ZG) {
+        float4 v;
+        if constexpr (V4) {
+          v = *(const float4*)(ws + z * zs + e);
+        } else {
+          const float* p = ws + z * zs + e;
+          v.x = p[0];
+          v.y = e + 1 < per ? p[1] : 0.f;
+          v.z = e + 2 < per ? p[2] : 0.f;
+          v.w = e + 3 < per ? p[3] : 0.f;
+        }
+        acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+      }
+    }
+    if (zg > 0) red[(zg - 1) * LN + lane] = acc;
+    __syncthreads();
+    if (zg == 0 && e < per) {
+#pragma unroll
+      for (int q = 0; q < ZG - 1; ++q) {
+        const float4 r = red[q * LN + lane];
+        acc.x += r.x; acc.y += r.y; acc.z += r.z; acc.w += r.w;
+      }
+      const float a4[4] = {acc.x, acc.y, acc.z, acc.w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (e + k < per) dw[e + k] += a4[k];
+    }
+    __syncthreads();
+  }
+}
+
+template <bool V4>
 __global__ __launch_bounds__(256) void xwgrad_reduce_batch_kernel(const XWRBatch b) {
+  __shared__ float4 red[240];
   const XWRDesc& d = b.d[blockIdx.y];
   const int g = blockIdx.z;
   if (g >= (int)d.G) return;
@@ -1033,13 +1124,10 @@ __global__ __launch_bounds__(256) void xwgrad_reduce_batch_kernel(const XWRBatch
   const int Mv = valid_rows(nvalid, g, (int)d.N) * (int)d.HoWo;
   const int nz = (Mv + (int)d.mchunk - 1) / (int)d.mchunk;
   if (nz == 0) return;
-  const float* __restrict__ ws = (const float*)d.ws;
-  float* __restrict__ dw = (float*)d.dw;
-  for (long long e = blockIdx.x * 256LL + threadIdx.x; e < d.per; e += (long long)gridDim.x * 256) {
-    float v = 0.f;
-    for (int z = 0; z < nz; ++z) v += ws[((long long)z * d.G + g) * d.per + e];
-    dw[(long long)g * d.dw_gstride + e] += v;
-  }
+  const float* __restrict__ ws = (const float*)d.ws + (long long)g * d.per;
+  float* __restrict__ dw = (float*)d.dw + (long long)g * d.dw_gstride;
+  if (nz >= 32) xwr_body<16, V4>(ws, d.G * d.per, d.per, nz, dw, red);
+  else xwr_body<4, V4>(ws, d.G * d.per, d.per, nz, dw, red);
 }
 
 // ====================================================================== dgrad weights
@@ -1053,37 +1141,51 @@ struct XTBatch {
   XTDesc d[kXTBatch];
 };
 
-__global__ void xtranspose_kernel(const XTBatch b, int slots, const int* __restrict__ nvalid) {
+// One 32 x 32 (cout x cin) tile of one tap per block iteration, transposed through LDS:
+// coalesced reads along cin, coalesced writes along cout (the element-wise gather it replaces
+// read every weight from a different cache line).  blockIdx.z = slot.
+__global__ __launch_bounds__(256) void xtranspose_kernel(const XTBatch b, int slots, const int* __restrict__ nvalid) {
+  __shared__ float tile[32][33];
   const XTDesc& d = b.d[blockIdx.y];
   const int s = (int)d.stride, KH = (int)d.KH, KW = (int)d.KW, Cin = (int)d.Cin, Cout = (int)d.Cout;
   const int pad = (int)d.pad;
-  const long long per = (long long)Cout * KH * KW * Cin;
-  for (long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x; t < per * slots;
-       t += (long long)gridDim.x * blockDim.x) {
-    const int sl = (int)(t / per);
-    if (nvalid && nvalid[sl] == 0) continue;
-    long long e = t - sl * per;   // destination index within the slot
-    // walk the classes in (ph, pw) order
-    long long base = 0;
-    int nI = 0, nJ = 0, kh0 = 0, kw0 = 0;
-    for (int cidx = 0; cidx < s * s; ++cidx) {
-      const int ph = cidx / s, pw = cidx - ph * s;
-      kh0 = (ph + pad) % s; kw0 = (pw + pad) % s;
-      nI = kh0 < KH ? (KH - kh0 + s - 1) / s : 0;
-      nJ = kw0 < KW ? (KW - kw0 + s - 1) / s : 0;
-      const long long sz = (long long)Cin * nI * nJ * Cout;
-      if (e < base + sz) break;
-      base += sz;
+  const int sl = blockIdx.z;
+  if (nvalid && nvalid[sl] == 0) return;
+  const int per = Cout * KH * KW * Cin;
+  const float* __restrict__ w = (const float*)d.w + (long long)sl * d.w_sstride;
+  float* __restrict__ wt = (float*)d.wt + (long long)sl * per;
+  const int nco = (Cout + 31) >> 5, nci = (Cin + 31) >> 5;
+  const int ntiles = KH * KW * nco * nci;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    const int tap = t / (nco * nci), rr = t - tap * nco * nci;
+    const int cot = rr / nci, cit = rr - cot * nci;
+    const int kh = tap / KW, kw = tap - kh * KW;
+    // the tap's parity class (ph, pw): kh0 = (ph + pad) % s == kh % s
+    const int kh0 = kh % s, kw0 = kw % s;
+    const int ph = ((kh0 - pad) % s + s) % s, pw = ((kw0 - pad) % s + s) % s;
+    const int cls = ph * s + pw;
+    int base = 0, nI = 0, nJ = 0;
+    for (int c = 0; c <= cls; ++c) {
+      const int a = c / s, bb = c - a * s;
+      const int h0 = (a + pad) % s, w0 = (bb + pad) % s;
+      nI = h0 < KH ? (KH - h0 + s - 1) / s : 0;
+      nJ = w0 < KW ? (KW - w0 + s - 1) / s : 0;
+      if (c < cls) base += Cin * nI * nJ * Cout;
     }
-    long long r = e - base;
-    const int co = (int)(r % Cout); r /= Cout;
-    const int j = (int)(r % nJ); r /= nJ;
-    const int i = (int)(r % nI);
-    const int ci = (int)(r / nI);
-    const int kh = kh0 + i * s, kw = kw0 + j * s;
-    const float* w = (const float*)d.w + (long long)sl * d.w_sstride;
-    float* wt = (float*)d.wt + sl * per;
-    wt[e] = w[(((long long)co * KH + kh) * KW + kw) * Cin + ci];
+    const int i = (kh - kh0) / s, j = (kw - kw0) / s;
+#pragma unroll
+    for (int k = ty; k < 32; k += 8) {
+      const int co = cot * 32 + k, ci = cit * 32 + tx;
+      tile[k][tx] = (co < Cout && ci < Cin) ? w[((co * KH + kh) * KW + kw) * Cin + ci] : 0.f;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = ty; k < 32; k += 8) {
+      const int ci = cit * 32 + k, co = cot * 32 + tx;
+      if (ci < Cin && co < Cout) wt[base + ((ci * nI + i) * nJ + j) * Cout + co] = tile[tx][k];
+    }
+    __syncthreads();
   }
 }
 
@@ -1206,6 +1308,7 @@ int xconv_tile(const XArgs& a, long long Mmax, int G, int nclass, int bm, hipStr
     if (bm == 64) return xconv_go<64, 64, 2, 2, P, VEC, H, PW>(a, Mmax, G, nclass, st);
     return xconv_go<128, 64, 2, 2, P, VEC, H, PW>(a, Mmax, G, nclass, st);
   }
+  if (bm == 32) return xconv_go<32, 128, 1, 4, P, VEC, H, PW>(a, Mmax, G, nclass, st);
   if (bm == 64) return xconv_go<64, 128, 2, 2, P, VEC, H, PW>(a, Mmax, G, nclass, st);
   return xconv_go<128, 128, 2, 2, P, VEC, H, PW>(a, Mmax, G, nclass, st);
 }
@@ -1253,10 +1356,15 @@ int xhalo_try(const XArgs& a, int G, int KH, int KW, hipStream_t st) {
 }
 
 int xconv_dispatch(const XArgs& a, long long Mmax, int G, int nclass, int vec, hipStream_t st) {
-  // small launches (a lone client's grouped step) take 64-row tiles
+  // small launches (a lone client's grouped step) take 64-row tiles, the smallest (a lone
+  // client's stage-3/4 convs: 32-64 tiles of 64 rows) 32-row tiles with one 32x32 MFMA tile
+  // per wave.  The tile shape never changes a result bit: every output element sees the same
+  // k-step order and the same plane-product order within a step.
+  static const int bm32_below = env_int("DBA_F32_BM32_BLOCKS", 256);
   const int bn = a.Ncol <= 32 ? 32 : a.Ncol <= 64 ? 64 : 128;
   const long long blocks = (long long)ceil_div(Mmax, 128) * ceil_div(a.Ncol, bn) * G * nclass * a.splitk;
-  const int bm = (bn > 32 && blocks < 512) ? 64 : 128;
+  int bm = (bn > 32 && blocks < 512) ? 64 : 128;
+  if (bn == 128 && 2 * blocks < bm32_below) bm = 32;
   if (vec == 4 && a.Cs % 32 == 0) vec = 32;
   if (a.amax_src && a.wp && vec >= 4) {
     if (vec == 32) return xconv_tile<2, 32, true, true>(a, Mmax, G, nclass, bm, st);
@@ -1286,10 +1394,11 @@ int xsplitk(long long M, int /*G*/, int Ncol, int K) {
   static const int off = env_int("DBA_F32_SPLITK", 1) == 0;
   if (off) return 1;
   const int bn = Ncol <= 32 ? 32 : Ncol <= 64 ? 64 : 128;
+  static const int target = env_int("DBA_F32_SPLITK_TILES", 64);
   const long long tiles = (long long)ceil_div(M, 64) * ceil_div(Ncol, bn);
-  if (tiles >= 64) return 1;
+  if (tiles >= target) return 1;
   const int nkt = (K + 31) / 32;
-  int s = (int)std::min<long long>(8, (64 + tiles - 1) / tiles);
+  int s = (int)std::min<long long>(8, (target + tiles - 1) / tiles);
   while (s > 1 && nkt / s < 8) --s;
   return s;
 }
@@ -1344,7 +1453,7 @@ DBA_EXPORT int dba_xconv_fwd(const float* x, long long x_gstride, const float* w
                              int Wo, int Cout, int KH, int KW, int stride, int pad, int relu, const int* amax_x,
                              int amax_x_ld, const int* amax_w, int amax_w_ld, int* amax_out, int amax_out_ld,
                              const uint16_t* wp, long long wp_sstride, float* ws, long long ws_floats,
-                             void* stream) {
+                             double* bnpart, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   if ((long long)N * H * W * Cin >= (1LL << 29)) return -103;   // 32-bit in-replica byte offsets
   const long long M = (long long)N * Ho * Wo;
@@ -1358,12 +1467,15 @@ DBA_EXPORT int dba_xconv_fwd(const float* x, long long x_gstride, const float* w
   a.amax_src = amax_x; a.amax_w = amax_w; a.amax_out = amax_out;
   a.amax_src_ld = amax_x_ld; a.amax_w_ld = amax_w_ld; a.amax_out_ld = amax_out_ld;
   a.wp = wp; a.wp_sstride = wp_sstride;
+  a.bnpart = bnpart; a.bnpart_nblk = (int)ceil_div(M, 32);
   a.cls[0] = XClass{KH, KW, -pad, -pad, 0, 0, Ho, Wo, 0};
+  if (bnpart && (bias || res || relu)) return -106;   // statistics of the raw conv output only
   if (stride == 1) {
     const int rc = xhalo_try(a, G, KH, KW, st);
     if (rc != -100) return rc;
   }
   const int s = xsplitk(M, G, Cout, K);
+  if (bnpart && s > 1) return -106;   // split-K outputs: BN statistics by the BN kernels
   if (s > 1 && ws != nullptr && ws_floats >= (long long)s * G * M * Cout) {
     XArgs b = a;
     b.splitk = s;
@@ -1435,12 +1547,11 @@ DBA_EXPORT int dba_xconv_dgrad(const float* dy, long long dy_gstride, const floa
 DBA_EXPORT int dba_xtranspose(const void* desc, int n, int slots, long long max_per, const int* nvalid,
                               void* stream) {
   const XTDesc* ds = (const XTDesc*)desc;
-  const long long total = max_per * slots;
   for (int i0 = 0; i0 < n; i0 += kXTBatch) {
     XTBatch b{};
     const int m = std::min(kXTBatch, n - i0);
     for (int i = 0; i < m; ++i) b.d[i] = ds[i0 + i];
-    const dim3 grid((unsigned)std::max(1LL, std::min(4096LL, (total + 255) / 256)), m);
+    const dim3 grid((unsigned)std::max(1LL, std::min(1024LL, (max_per + 1023) / 1024)), m, slots);
     hipLaunchKernelGGL(xtranspose_kernel, grid, dim3(256), 0, (hipStream_t)stream, b, slots, nvalid);
     const int rc = (int)hipGetLastError();
     if (rc != 0) return rc;
@@ -1571,8 +1682,11 @@ DBA_EXPORT int dba_xwgrad_reduce_batch(const void* desc, int n, int Gmax, long l
     XWRBatch b{};
     const int m = std::min(kXWRBatch, n - i0);
     for (int i = 0; i < m; ++i) b.d[i] = ds[i0 + i];
+    bool v4 = true;
+    for (int i = 0; i < m; ++i) v4 = v4 && b.d[i].per % 4 == 0 && b.d[i].ws % 16 == 0;
     const dim3 grid((unsigned)std::max(1LL, std::min(256LL, (max_per + 255) / 256)), m, Gmax);
-    hipLaunchKernelGGL(xwgrad_reduce_batch_kernel, grid, dim3(256), 0, (hipStream_t)stream, b);
+    if (v4) hipLaunchKernelGGL(xwgrad_reduce_batch_kernel<true>, grid, dim3(256), 0, (hipStream_t)stream, b);
+    else hipLaunchKernelGGL(xwgrad_reduce_batch_kernel<false>, grid, dim3(256), 0, (hipStream_t)stream, b);
     const int rc = (int)hipGetLastError();
     if (rc != 0) return rc;
   }

@@ -150,7 +150,7 @@ class Ctx:
             return ops.conv2d(x, wf, self.wsel, stride, pad, bias=bf, residual=residual, relu=relu,
                               nvalid=self.nvalid)
         w = self.w(conv)
-        y = ops.conv2d(x, w, self.wsel, stride, pad, nvalid=self.nvalid)
+        y = ops.conv2d(x, w, self.wsel, stride, pad, nvalid=self.nvalid, bn_stats=True)
         gamma, beta = self.m(bn + ".weight"), self.m(bn + ".bias")
         out, mean, invstd = ops.bn_train(y, gamma, beta, self.m(bn + ".running_mean"),
                                          self.m(bn + ".running_var"), self.nvalid, BN_MOMENTUM,

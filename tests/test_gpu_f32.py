@@ -244,6 +244,77 @@ def _deterministic(H, dev):
                 assert torch.equal(a, b), (case, k)
 
 
+@pytest.mark.parametrize("planes", [3, 16])
+@pytest.mark.parametrize("case", [(8, 64, 8, 8, 128, 128, 3, 1, 1), (8, 64, 8, 8, 64, 128, 3, 2, 1),
+                                  (8, 64, 4, 4, 256, 256, 3, 1, 1), (8, 64, 16, 16, 64, 64, 3, 1, 1)])
+def test_fp32_group_size_independent_bits(H, planes, case):
+    """A replica's conv / data-gradient / weight-gradient bits do not depend on how many other
+    replicas share its launch: alone (a lone client: 32-row tiles, split-K) or inside a group
+    of 8 (64/128-row tiles).  World-1 vs world-N runs group clients differently per rank, so
+    this is what makes their CSV rows bitwise equal."""
+    dev = torch.device("cuda")
+    prev = H.set_fp32_planes(planes)
+    try:
+        G, N, Hh, Ww, Cin, Cout, k, s, p = case
+        x, w, wsel, bias, nvalid, res, dy, acc = _inputs(case, dev, seed=5)
+        nvalid = torch.full((G,), N, dtype=torch.int32, device=dev)
+
+        def run(sl):
+            xs, dys, accs, ress = x[sl].contiguous(), dy[sl].contiguous(), acc[sl].contiguous(), res[sl].contiguous()
+            nv, ws = nvalid[sl].contiguous(), wsel[sl].contiguous()
+            y = H.conv2d(xs, w, ws, s, p, bias=bias, residual=ress, relu=True, nvalid=nv)
+            dx = H.conv2d_dgrad(dys, w, ws, s, p, (Hh, Ww), nvalid=nv, accum=accs)
+            dw = torch.zeros(xs.shape[0], Cout, k, k, Cin, device=dev)
+            H.conv2d_wgrad(dys, xs, s, p, k, k, dw, None, nvalid=nv)
+            return y, dx, dw
+
+        full = run(slice(0, G))
+        for g in (0, G - 1):
+            one = run(slice(g, g + 1))
+            for a, b in zip(full, one):
+                assert torch.equal(a[g], b[0]), (case, g)
+    finally:
+        H.set_fp32_planes(prev)
+
+
+@pytest.mark.parametrize("case", [(3, 8, 32, 32, 32, 32, 3, 1, 1), (2, 8, 32, 32, 32, 64, 3, 2, 1),
+                                  (2, 16, 16, 16, 64, 64, 3, 1, 1), (1, 64, 8, 8, 128, 128, 3, 1, 1)])
+def test_fp32_bn_stats_folded_in_conv_epilogue(H, R64, case):
+    """Training BN statistics folded into the conv epilogue (per-32-pixel partials, finalised
+    without a pass over y) match the fp64 oracle's batch statistics and running-stat update,
+    and the BN output matches the separate-reduction path to fp32 rounding."""
+    dev = torch.device("cuda")
+    G, N, Hh, Ww, Cin, Cout, k, s, p = case
+    x, w, wsel, bias, nvalid, res, dy, acc = _inputs(case, dev, seed=11)
+    gamma = (1 + 0.1 * torch.randn(G, Cout)).to(dev)
+    beta = (0.1 * torch.randn(G, Cout)).to(dev)
+    prev = H._BN_FUSED_STATS
+    H._BN_FUSED_STATS = True
+    try:
+        y = H.conv2d(x, w, wsel, s, p, nvalid=nvalid, bn_stats=True)
+    finally:
+        H._BN_FUSED_STATS = prev
+    fused = hasattr(y, "_dba_bnpart")
+    y2 = y.clone()                                    # same values, no folded partials
+    outs = []
+    for t in (y, y2):
+        rm, rv = torch.zeros(G, Cout, device=dev), torch.ones(G, Cout, device=dev)
+        out, mean, invstd = H.bn_train(t, gamma, beta, rm, rv, nvalid, 0.1, 1e-5, True, None)
+        outs.append((out, mean, invstd, rm, rv))
+    for g in range(G):
+        n = int(nvalid[g])
+        yv = y[g, :n].double().cpu().reshape(-1, Cout)
+        m = yv.mean(0)
+        var = yv.var(0, unbiased=False)
+        for out, mean, invstd, rm, rv in outs:
+            assert _rel(mean[g], m) < 1e-6 and _rel(invstd[g], 1 / (var + 1e-5).sqrt()) < 1e-6, (case, g, fused)
+            assert _rel(rm[g], 0.1 * m) < 1e-6
+            assert _rel(rv[g], 0.9 + 0.1 * yv.var(0, unbiased=True)) < 1e-6
+        assert _rel(outs[0][0][g, :n], outs[1][0][g, :n]) < 1e-6
+    if N * Hh * Ww // (s * s) > 1024:
+        assert fused, "the conv did not fold BN statistics"
+
+
 def test_fp32_no_silent_downcast(H):
     """fp32 activations never reach a bf16 kernel, and mixed operands are refused."""
     dev = torch.device("cuda")
