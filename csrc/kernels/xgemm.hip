@@ -1388,13 +1388,15 @@ int xconv_dispatch(const XArgs& a, long long Mmax, int G, int nclass, int vec, h
 // split-K factor of a forward launch (1 = none).  Decided from the PER-REPLICA geometry only
 // (never from the group count G): the K-slicing sets the summation order, so a client's
 // bits must not depend on how many other clients share its launch (world-1 vs world-N runs
-// place different client groups on a rank).  Splits a replica below ~64 tiles (a lone
-// client's stage-3/4 convs) into slabs of >= 8 k-steps.
+// place different client groups on a rank).  Splits a replica below ~128 tiles of 64 rows
+// (a lone client's stage-3/4 convs) into slabs of >= 8 k-steps.
 int xsplitk(long long M, int /*G*/, int Ncol, int K) {
   static const int off = env_int("DBA_F32_SPLITK", 1) == 0;
   if (off) return 1;
   const int bn = Ncol <= 32 ? 32 : Ncol <= 64 ? 64 : 128;
-  static const int target = env_int("DBA_F32_SPLITK_TILES", 64);
+  // 128: a lone client's stage-3 convs (64 tiles of 64 rows) split in two — lone step 1.95 ->
+  // 1.85 ms, the 10-client round's training time unchanged (202.4 vs 202.6 ms, r2c_iter1)
+  static const int target = env_int("DBA_F32_SPLITK_TILES", 128);
   const long long tiles = (long long)ceil_div(M, 64) * ceil_div(Ncol, bn);
   if (tiles >= target) return 1;
   const int nkt = (K + 31) / 32;

@@ -1,7 +1,7 @@
 # reduce/transpose rework + 32-row tiles (fused BN stats off by default): GPU suite, steps, bench, traces
 R=$GRAFT_REPO_ROOT
 mkdir -p $R/gpurun_out/prof_bench3
-timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1 || { tail -40 gpurun_out/gpu_tests.log; exit 1; }
+PYTHONPATH=$R timeout -k 10 300 python scripts/diag/bn_fused_bwd.py > gpurun_out/diag_bwd.log 2>&1; timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1 || { tail -40 gpurun_out/gpu_tests.log; exit 1; }
 tail -2 gpurun_out/gpu_tests.log
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || exit $?
 tail -1 gpurun_out/smoke.log | cut -c1-300
@@ -15,3 +15,4 @@ export PYTHONPATH=$R
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof_bench3 -o bench -- python3 $R/bench.py --steps 6 --warmup 2 --pretrain-rounds 3 > $R/gpurun_out/prof_bench3/stdout.log 2>&1 || exit $?
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof_bench3 -o step1 -- python3 -m dba_mod_amd.tools.bench_step --dtype fp32 --clients 1 --reps 1 > $R/gpurun_out/prof_bench3/step_stdout.log 2>&1
+
