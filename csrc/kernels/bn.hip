@@ -26,13 +26,71 @@ __host__ __device__ inline int rows_per_block(int C) {
 // Per-block partial sums (no atomics, no pre-zeroing): part[g][blk][0][c] = sum x (STATS)
 // or sum d (BWD); part[g][blk][1][c] = sum x^2 or sum d*xhat.  Blocks past the valid rows
 // write zeros so the finalize pass can sum every slot unconditionally.
+// Last-block finalize (fin != nullptr): the blocks holding valid rows count their arrival on
+// the replica's zeroed counter; the last one sums the replica's partials (fixed order, fp64)
+// and finalises in the same launch — one launch per BN pass instead of reduce + finalize.
+struct BnFin {
+  int* counter;                                   // [G] zeroed (per-step arena)
+  // forward: running stats and batch statistics
+  float* rm; float* rv; long long s_gstride; float momentum, eps; float* mean_out; float* invstd_out;
+  // backward: sums [G][2][C], dgamma / dbeta accumulation
+  float* sums; float* dgamma; float* dbeta; long long g_gstride;
+};
+
+template <bool BWD>
+__device__ void bn_last_block(const float* __restrict__ part, int nblk_grid, int nvb, int g, int C, double n,
+                              const BnFin& f) {
+  __shared__ double fr[2][256];
+  const int tid = threadIdx.x;
+  const int tpc = C >= 256 ? 1 : 256 / C;         // threads per channel
+  const float* pg = part + (long long)g * nblk_grid * 2 * C;
+  for (int c0 = 0; c0 < C; c0 += 256 / tpc) {
+    const int c = c0 + tid / tpc, q = tid % tpc;
+    double a0 = 0.0, a1 = 0.0;
+    if (c < C) {
+#pragma unroll 4
+      for (int b = q; b < nvb; b += tpc) {
+        a0 += (double)pg[(long long)b * 2 * C + c];
+        a1 += (double)pg[(long long)b * 2 * C + C + c];
+      }
+    }
+    fr[0][tid] = a0;
+    fr[1][tid] = a1;
+    __syncthreads();
+    if (q == 0 && c < C) {
+      double s0 = 0.0, s1 = 0.0;
+      for (int k = 0; k < tpc; ++k) { s0 += fr[0][tid + k]; s1 += fr[1][tid + k]; }
+      if (!BWD) {
+        const int i = g * C + c;
+        const double m = s0 / n;
+        double var = s1 / n - m * m;
+        var = var > 0 ? var : 0;
+        f.mean_out[i] = (float)m;
+        f.invstd_out[i] = (float)(1.0 / sqrt(var + (double)f.eps));
+        float* prm = f.rm + (long long)g * f.s_gstride + c;
+        float* prv = f.rv + (long long)g * f.s_gstride + c;
+        const double unb = n > 1 ? var * n / (n - 1) : var;
+        *prm = (float)((1.0 - f.momentum) * (*prm) + f.momentum * m);
+        *prv = (float)((1.0 - f.momentum) * (*prv) + f.momentum * unb);
+      } else {
+        f.sums[((long long)g * 2) * C + c] = (float)s0;
+        f.sums[((long long)g * 2 + 1) * C + c] = (float)s1;
+        f.dbeta[(long long)g * f.g_gstride + c] += (float)s0;
+        f.dgamma[(long long)g * f.g_gstride + c] += (float)s1;
+      }
+    }
+    __syncthreads();
+  }
+}
+
 template <bool BWD, typename T>
 __global__ __launch_bounds__(256) void bn_reduce_kernel(const T* __restrict__ y, const T* __restrict__ dout,
                                                         const T* __restrict__ out, const float* __restrict__ mean,
                                                         const float* __restrict__ invstd, int relu,
                                                         const int* __restrict__ nvalid, int N, int HW, int C,
-                                                        float* __restrict__ part) {
+                                                        float* __restrict__ part, const BnFin fin) {
   __shared__ float red[2][256][8];
+  __shared__ int last;
   const int g = blockIdx.y;
   const int R = N * HW;
   const int Rv = valid_rows(nvalid, g, N) * HW;
@@ -41,6 +99,13 @@ __global__ __launch_bounds__(256) void bn_reduce_kernel(const T* __restrict__ y,
   const int tid = threadIdx.x;
   float* pg = part + ((long long)g * gridDim.x + blockIdx.x) * 2 * C;
   if (r0 >= Rv) {
+    if (fin.counter) {
+      // no valid row in this block: with fin only the valid blocks' partials are summed; an
+      // inactive replica's statistics are zeroed by its block 0 (forward)
+      if (!BWD && Rv == 0 && blockIdx.x == 0)
+        for (int c = tid; c < C; c += 256) { fin.mean_out[g * C + c] = 0.f; fin.invstd_out[g * C + c] = 0.f; }
+      return;
+    }
     for (int c = tid; c < 2 * C; c += 256) pg[c] = 0.f;
     return;
   }
@@ -90,6 +155,15 @@ __global__ __launch_bounds__(256) void bn_reduce_kernel(const T* __restrict__ y,
       pg[C + tid * 8 + e] = s1[e];
     }
   }
+  if (!fin.counter) return;
+  const int nvb = (Rv + rpb - 1) / rpb;   // blocks with valid rows (this replica)
+  __threadfence();                          // partials visible device-wide before the arrival
+  __syncthreads();
+  if (tid == 0) last = atomicAdd(fin.counter + g, 1) == nvb - 1;
+  __syncthreads();
+  if (!last) return;
+  __threadfence();
+  bn_last_block<BWD>(part, gridDim.x, nvb, g, C, (double)Rv, fin);
 }
 
 // sums the nblk partials of (g, c): a block covers cpb = min(64, C) channels with 256 / cpb
@@ -507,16 +581,24 @@ static bool bn_layout_ok(int C) { return C > 0 && C % 8 == 0 && C <= 2048 && 256
 #define BN_T(f32, call) do { if (f32) { typedef float T; call; } else { typedef uint16_t T; call; } } while (0)
 
 // part: [G][nblk][2][C] fp32 workspace (no initialisation needed); y fp32 (f32) or bf16
+// counter (optional): [G] zeroed ints — the statistics are finalised by the last reduce block
+// (one launch); without it a separate finalize launch runs
 DBA_EXPORT int dba_bn_stats(const void* y, const int* nvalid, int G, int N, int HW, int C, float* part, float* rm,
                             float* rv, long long s_gstride, float momentum, float eps, float* mean, float* invstd,
-                            int f32, void* stream) {
+                            int f32, int* counter, void* stream) {
   if (!bn_layout_ok(C)) return -102;
   hipStream_t st = (hipStream_t)stream;
   const int nblk = ceil_div((long long)N * HW, rows_per_block(C));
+  BnFin fin{};
+  if (counter) {
+    fin.counter = counter; fin.rm = rm; fin.rv = rv; fin.s_gstride = s_gstride; fin.momentum = momentum;
+    fin.eps = eps; fin.mean_out = mean; fin.invstd_out = invstd;
+  }
   BN_T(f32, hipLaunchKernelGGL((bn_reduce_kernel<false, T>), dim3(nblk, G), dim3(256), 0, st, (const T*)y, nullptr,
-                               nullptr, nullptr, nullptr, 0, nvalid, N, HW, C, part));
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3(ceil_div(C, C < 64 ? C : 64), G), dim3(256), 0, st, part, nblk, nvalid, N, HW, C,
-                     rm, rv, s_gstride, momentum, eps, mean, invstd, G);
+                               nullptr, nullptr, nullptr, 0, nvalid, N, HW, C, part, fin));
+  if (!counter)
+    hipLaunchKernelGGL(bn_finalize_kernel, dim3(ceil_div(C, C < 64 ? C : 64), G), dim3(256), 0, st, part, nblk, nvalid,
+                       N, HW, C, rm, rv, s_gstride, momentum, eps, mean, invstd, G);
   DBA_LAUNCH_CHECK();
 }
 
@@ -546,15 +628,20 @@ DBA_EXPORT int dba_bn_apply(const void* y, const float* mean, const float* invst
 DBA_EXPORT int dba_bn_bwd(const void* dout, const void* out, const void* y, const float* mean, const float* invstd,
                           const float* gamma, long long p_gstride, int relu, float* dgamma, float* dbeta,
                           long long g_gstride, void* dy, void* dres, float* part, const int* nvalid, int G, int N,
-                          int HW, int C, int f32, int* amax, int amax_ld, void* stream) {
+                          int HW, int C, int f32, int* amax, int amax_ld, int* counter, void* stream) {
   if (!bn_layout_ok(C)) return -102;
   hipStream_t st = (hipStream_t)stream;
   const int nblk = ceil_div((long long)N * HW, rows_per_block(C));
   float* sums = part + (long long)G * nblk * 2 * C;
+  BnFin fin{};
+  if (counter) {
+    fin.counter = counter; fin.sums = sums; fin.dgamma = dgamma; fin.dbeta = dbeta; fin.g_gstride = g_gstride;
+  }
   BN_T(f32, hipLaunchKernelGGL((bn_reduce_kernel<true, T>), dim3(nblk, G), dim3(256), 0, st, (const T*)y,
-                               (const T*)dout, (const T*)out, mean, invstd, relu, nvalid, N, HW, C, part));
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(ceil_div(C, C < 64 ? C : 64), G), dim3(256), 0, st, part, nblk, sums, dgamma,
-                     dbeta, g_gstride, G, C);
+                               (const T*)dout, (const T*)out, mean, invstd, relu, nvalid, N, HW, C, part, fin));
+  if (!counter)
+    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(ceil_div(C, C < 64 ? C : 64), G), dim3(256), 0, st, part, nblk,
+                       sums, dgamma, dbeta, g_gstride, G, C);
   BN_T(f32, hipLaunchKernelGGL((bn_bwd_apply_kernel<T>), ggrid(G, N, HW, C), dim3(256), 0, st, (const T*)dout,
                                (const T*)out, (const T*)y, mean, invstd, gamma, p_gstride, sums, relu, (T*)dy,
                                (T*)dres, nvalid, G, N, HW, C, amax, amax_ld));

@@ -44,10 +44,10 @@ _SIGS = {
     "dba_halo_conv": [_P, _LL, _P, _LL, _P, _P, _LL, _P, _P, _LL, _I, _P] + [_I] * 9 + [_P],
     "dba_colsum": [_P, _LL, _I, _P, _I, _I, _I, _P, _LL, _P],
     "dba_xcolsum": [_P, _LL, _I, _P, _I, _I, _I, _P, _LL, _P],
-    "dba_bn_stats": [_P, _P, _I, _I, _I, _I, _P, _P, _P, _LL, _F, _F, _P, _P, _I, _P],
+    "dba_bn_stats": [_P, _P, _I, _I, _I, _I, _P, _P, _P, _LL, _F, _F, _P, _P, _I, _P, _P],
     "dba_bn_partial_blocks": [_I, _I, _I],
     "dba_bn_apply": [_P, _P, _P, _P, _P, _LL, _P, _I, _P, _P, _I, _I, _I, _I, _I, _P, _I, _P],
-    "dba_bn_bwd": [_P, _P, _P, _P, _P, _P, _LL, _I, _P, _P, _LL, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _I, _P],
+    "dba_bn_bwd": [_P, _P, _P, _P, _P, _P, _LL, _I, _P, _P, _LL, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _I, _P, _P],
     "dba_bn_small_fwd": [_P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _LL, _F, _F, _P, _I, _P, _P, _P, _I, _P, _I, _P],
     "dba_bn_small_bwd": [_P, _P, _P, _P, _P, _P, _LL, _I, _P, _P, _LL, _P, _P, _P, _I, _I, _I, _I, _I, _P, _I, _P],
     "dba_amax_segments": [_P, _LL, _P, _I, _I, _P, _I, _P],
@@ -334,6 +334,23 @@ def amax_arena(G: int, device, n: int = 128):
 def _amax_new(G: int, device):
     a = _ARENA[-1].take(G, device) if _ARENA else None
     return a if a is not None else torch.zeros(AMAX_SUB, _amax_ld(G), dtype=torch.int32, device=device)
+
+
+def _bn_counter(G: int, device):
+    """[G] zeroed arrival counters for a last-block BN finalize (bn.hip BnFin), carved from the
+    step's zeroed arena (16 per slot); None outside an arena — the BN passes then launch their
+    separate finalize (no extra zero-fill launch)."""
+    if not _BN_LAST_BLOCK or not _ARENA:
+        return None
+    ar = _ARENA[-1]
+    slot, used = getattr(ar, "_cnt", (None, AMAX_SUB))
+    if used >= AMAX_SUB:
+        slot = ar.take(G, device)
+        if slot is None:
+            return None
+        used = 0
+    ar._cnt = (slot, used + 1)
+    return slot[used, :G]
 
 
 def _aptr(a):
@@ -747,6 +764,11 @@ def _same_stride(*ts: Tensor) -> int:
 
 # rows per replica up to which BN runs as one launch (bn_small_*: ResNet stage 4 at batch 64)
 _BN_SMALL_ROWS = int(os.environ.get("DBA_BN_SMALL_ROWS", "1024"))
+# BN statistics finalised by the last reduce block instead of a separate launch
+# (DBA_BN_LAST_BLOCK=1: on).  Off: measured slower — lone step 1.84 -> 1.94 ms, 10-client
+# step 6.72 -> 9.40 ms (profiles/r2c_bn_last_block_rejected.md): the device-scope release
+# fence every block issues before its arrival writes back its XCD's L2
+_BN_LAST_BLOCK = os.environ.get("DBA_BN_LAST_BLOCK", "0") == "1"
 # fp32 training BN statistics folded into the producing conv's epilogue (DBA_BN_FUSED=1: on).
 # Off by default: with it, the train-step oracle test (test_fp32_train_step_vs_fp64) moves
 # 3e-3..1e-2 from fp64 on one replica in 3 of 4 configurations tried, the separate pass in
@@ -789,7 +811,8 @@ def bn_train(y, gamma, beta, rmean, rvar, nvalid, momentum, eps, relu, residual)
         nblk = _L.dba_bn_partial_blocks(N, H * W, C)
         part = torch.empty(G * nblk * 2 * C, dtype=torch.float32, device=y.device)
         _call("dba_bn_stats", y.data_ptr(), nv, G, N, H * W, C, part.data_ptr(), rmean.data_ptr(), rvar.data_ptr(),
-              ps, float(momentum), float(eps), mean.data_ptr(), invstd.data_ptr(), f32, _stream())
+              ps, float(momentum), float(eps), mean.data_ptr(), invstd.data_ptr(), f32,
+              _ptr(_bn_counter(G, y.device)), _stream())
     _call("dba_bn_apply", y.data_ptr(), mean.data_ptr(), invstd.data_ptr(), gamma.data_ptr(), beta.data_ptr(), ps,
           _ptr(res), int(relu), out.data_ptr(), nv, G, N, H * W, C, f32, *_aptr(am), _stream())
     return out, mean, invstd
@@ -816,7 +839,8 @@ def bn_train_bwd(dout, y, out, mean, invstd, gamma, nvalid, relu, dgamma, dbeta,
     part = torch.empty(G * (nblk + 1) * 2 * C, dtype=torch.float32, device=y.device)
     _call("dba_bn_bwd", dout.data_ptr(), out.data_ptr(), y.data_ptr(), mean.data_ptr(), invstd.data_ptr(),
           gamma.data_ptr(), ps, int(relu), dgamma.data_ptr(), dbeta.data_ptr(), gs, dy.data_ptr(), _ptr(dres),
-          part.data_ptr(), _ptr(_i32(nvalid)), G, N, H * W, C, f32, *_aptr(am), _stream())
+          part.data_ptr(), _ptr(_i32(nvalid)), G, N, H * W, C, f32, *_aptr(am), _ptr(_bn_counter(G, y.device)),
+          _stream())
     return (dy, dres) if want_dres else dy
 
 

@@ -317,6 +317,52 @@ def test_fp32_bn_stats_folded_in_conv_epilogue(H, R64, case):
         assert fused, "the conv did not fold BN statistics"
 
 
+@pytest.mark.parametrize("shape", [(3, 16, 32, 32, 32), (3, 16, 16, 16, 64), (2, 64, 8, 8, 128), (3, 8, 8, 8, 512)])
+def test_bn_last_block_finalize(H, shape):
+    """BN statistics finalised by the last reduce block (inside a training step's zeroed
+    arena: one launch per BN pass) match the separate finalize launch to fp32 rounding —
+    forward statistics, running stats, backward dgamma / dbeta / dy — for a full, a partly
+    valid and an inactive replica, and are bitwise reproducible."""
+    dev = torch.device("cuda")
+    G, N, Hh, Ww, C = shape
+    gen = torch.Generator().manual_seed(3)
+    y = (torch.randn(G, N, Hh, Ww, C, generator=gen) * 2 + 0.5).to(dev)
+    dout = torch.randn(G, N, Hh, Ww, C, generator=gen).to(dev)
+    gamma = (1 + 0.1 * torch.randn(G, C, generator=gen)).to(dev)
+    beta = (0.1 * torch.randn(G, C, generator=gen)).to(dev)
+    nvalid = torch.tensor([N, N // 2 + 1, 0][:G], dtype=torch.int32, device=dev)
+    prev = H.set_fp32_planes(16)
+    prev_lb = H._BN_LAST_BLOCK
+    H._BN_LAST_BLOCK = True   # opt-in path (measured slower, kept correct)
+
+    def run(arena):
+        rm, rv = torch.zeros(G, C, device=dev), torch.ones(G, C, device=dev)
+        dg, db = torch.zeros(G, C, device=dev), torch.zeros(G, C, device=dev)
+        ctx = H.amax_arena(G, dev) if arena else __import__("contextlib").nullcontext()
+        with ctx:
+            out, mean, invstd = H.bn_train(y, gamma, beta, rm, rv, nvalid, 0.1, 1e-5, True, None)
+            dy = H.bn_train_bwd(dout, y, out, mean, invstd, gamma, nvalid, True, dg, db)
+        return out, mean, invstd, rm, rv, dg, db, dy
+    try:
+        a, b, c = run(False), run(True), run(True)
+    finally:
+        H.set_fp32_planes(prev)
+        H._BN_LAST_BLOCK = prev_lb
+    for g in range(G):
+        n = int(nvalid[g])
+        if n == 0:
+            assert b[5][g].abs().max().item() == 0 and torch.equal(b[3][g], a[3][g]) and torch.equal(b[4][g], a[4][g])
+            continue
+        for k, (u, v) in enumerate(zip(a, b)):
+            rows = u[g, :n] if u.dim() > 2 else u[g]
+            assert _rel(v[g, :n] if v.dim() > 2 else v[g], rows) < 2e-6, (shape, g, k)
+    for u, v in zip(b, c):
+        for g in range(G):
+            n = int(nvalid[g])
+            if n:
+                assert torch.equal(u[g, :n] if u.dim() > 2 else u[g], v[g, :n] if v.dim() > 2 else v[g])
+
+
 def test_fp32_no_silent_downcast(H):
     """fp32 activations never reach a bf16 kernel, and mixed operands are refused."""
     dev = torch.device("cuda")
