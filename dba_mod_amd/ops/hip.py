@@ -471,6 +471,8 @@ def _xconv_fwd(x, w, wsel, stride, pad, bias, residual, relu, nvalid, out_dtype,
             and N * Ho * Wo > _BN_SMALL_ROWS):
         nblk = (N * Ho * Wo + 31) // 32
         part = torch.empty(G * Cout * 2 * nblk, dtype=torch.float64, device=x.device)
+        if os.environ.get("DBA_BN_FUSED_POISON") == "1":   # diagnostics: unwritten slots -> NaN
+            part.fill_(float("nan"))
         y._dba_bnpart = (part, nblk)
     _call("dba_xconv_fwd", x.data_ptr(), N * H * W * Cin, w.data_ptr(), ws, _ptr(_i32(wsel)), _ptr(bias), bs,
           _ptr(res), y.data_ptr(), N * Ho * Wo * Cout, _ptr(_i32(nvalid)), G, N, H, W, Cin, Ho, Wo, Cout, KH, KW,

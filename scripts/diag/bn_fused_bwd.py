@@ -8,13 +8,16 @@ from dba_mod_amd.models import program as P
 from dba_mod_amd.models.spec import get_spec
 
 H.set_fp32_planes(3)
-spec = get_spec("resnet18_tiny")
+import sys
+ARCH = sys.argv[1] if len(sys.argv) > 1 else "resnet18_tiny"
+spec = get_spec(ARCH)
+SHP = (64, 64, 3) if "tiny" in ARCH else (32, 32, 3)
 dev = torch.device("cuda")
 G, N = 3, 16
 torch.manual_seed(0)
 flat = spec.init_flat(3)
 nval = torch.tensor([N, 9, 0], dtype=torch.int32, device=dev)
-x = torch.rand(G, N, 64, 64, 3).to(dev)
+x = torch.rand(G, N, *SHP).to(dev)
 lab = torch.randint(0, spec.num_classes, (G, N)).int()
 lab = torch.where(torch.arange(N)[None] < nval.cpu()[:, None].long(), lab, torch.full_like(lab, -1)).to(dev)
 seeds = torch.tensor([1, 2, 3], dtype=torch.int32, device=dev)
@@ -55,13 +58,22 @@ for i, ((n, a), (_, b)) in enumerate(zip(rec["dry"], rec["fused"])):
         av, bv = a[g, :nv].double(), b[g, :nv].double()
         row.append(f"g{g} {((av - bv).norm() / av.norm().clamp(min=1e-30)).item():.2e}")
     print(i, *row)
-for i in (53, 54, 55, 56):
-    (n, a), (_, b) = rec["dry"][i], rec["fused"][i]
-    g = 1
-    d = (a[g] - b[g]).abs()
-    per_img = d.flatten(1).max(1).values.tolist()
-    mag = a[g].abs().flatten(1).max(1).values.tolist()
-    print(i, n, "max diff per image", [f"{v:.1e}" for v in per_img])
-    print(i, n, "max |a| per image ", [f"{v:.1e}" for v in mag])
-    idx = (d[:9] == d[:9].max()).nonzero()[0].tolist()
-    print(i, "argmax", idx, a[g][tuple(idx)].item(), b[g][tuple(idx)].item())
+first = None
+for i, ((n, a), (_, b)) in enumerate(zip(rec["dry"], rec["fused"])):
+    for g in range(2):
+        nv = int(nval[g])
+        av, bv = a[g, :nv].double(), b[g, :nv].double()
+        if ((av - bv).norm() / av.norm().clamp(min=1e-30)).item() > 1e-4 and first is None:
+            first = (i, g)
+print("first divergent op", first)
+if first is not None:
+    i0, g = first
+    for i in (i0 - 1, i0):
+        (n, a), (_, b) = rec["dry"][i], rec["fused"][i]
+        nv = int(nval[g])
+        d = (a[g, :nv] - b[g, :nv]).abs()
+        print(i, n, "max diff per image", [f"{v:.1e}" for v in d.flatten(1).max(1).values.tolist()])
+        flat = d.flatten()
+        top = flat.topk(5)
+        print(i, n, "top-5 diffs", [f"{v:.2e}" for v in top.values.tolist()],
+              "n > 1e-5:", int((flat > 1e-5).sum()), "of", flat.numel())
