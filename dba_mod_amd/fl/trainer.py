@@ -232,18 +232,70 @@ class GroupTrainer:
         pend_dist: List[Tuple[int, int, torch.Tensor]] = []
         trace: List[torch.Tensor] = []
         gstate = global_state[None, :self.spec.P]
+        solo = self._solo_tail(clients, T)
+        cur, row_of, cur_sched = b, list(range(G)), sched
         for t in range(T):
-            b.desc.copy_(sched[t], non_blocking=True)
-            self._run_step(b)
+            if solo is not None and t == solo[0]:
+                # only client solo[1] is left: its remaining steps run in the G=1 graph
+                # (every launch sized for one replica) instead of a G-replica graph whose other
+                # replicas are idle — identical bits (per-replica kernel decisions only)
+                cur, cur_sched = self._solo_enter(b, solo[1], clients, T, max_slots, global_state)
+                row_of = [0 if g == solo[1] else -1 for g in range(G)]
+            cur.desc.copy_(cur_sched[t], non_blocking=True)
+            self._run_step(cur)
             if self.trace:
                 dist = (b.state[:, :self.spec.P] - gstate).float().pow(2).sum(1).sqrt()
                 trace.append(torch.stack([self._last_loss.float(), dist], 1))
             for (g, ph) in events.get(t + 1, []):
-                self._phase_end(b, g, ph, snaps, pend_dist)
+                self._phase_end(cur, row_of[g], ph, snaps[g], pend_dist, g)
                 if on_client_done is not None and ph is clients[g].phases[-1]:
                     on_client_done(clients[g], snaps[g])
+        if cur is not b:
+            self._solo_leave(cur, b, solo[1])
         return {"b": b, "clients": clients, "snaps": snaps, "pend_dist": pend_dist, "sched": sched,
                 "trace": torch.stack(trace) if trace else None}
+
+    # a lone client's tail shorter than this stays in the group graph
+    SOLO_MIN_STEPS = int(os.environ.get("DBA_SOLO_MIN_STEPS", "0"))
+
+    def _solo_tail(self, clients: List[ClientPlan], T: int) -> Optional[Tuple[int, int]]:
+        """(t0, g) when from step t0 on only client g trains (the 6-epoch attacker after the
+        2-epoch clients finished) for at least SOLO_MIN_STEPS steps; graph mode, G > 1 only."""
+        if not self.use_graph or len(clients) < 2 or self.SOLO_MIN_STEPS <= 0:
+            return None
+        lens = sorted(((len(c.steps), g) for g, c in enumerate(clients)), reverse=True)
+        (n0, g0), (n1, _) = lens[0], lens[1]
+        if n0 != T or n0 - n1 < self.SOLO_MIN_STEPS:
+            return None
+        return n1, g0
+
+    def _solo_enter(self, b: _GroupBuffers, g: int, clients: List[ClientPlan], T: int, max_slots: int,
+                    global_state: torch.Tensor):
+        b1 = self._buffers(1, max_slots)
+        sched1 = to_device(native.pack_steps([clients[g]], 1, self.B, T, max_slots), self.device)
+        if b1.graph is None:
+            b1._cur = sched1[T - 1]
+            self._reset(b1, global_state)
+            self._run_step(b1)            # capture (mutates b1: overwritten below)
+        self._copy_row(b, g, b1, 0)
+        b1.nan_flag.zero_()
+        return b1, sched1
+
+    def _solo_leave(self, b1: _GroupBuffers, b: _GroupBuffers, g: int) -> None:
+        self._copy_row(b1, 0, b, g)
+        b.nan_flag += b1.nan_flag
+
+    @staticmethod
+    def _copy_row(src: _GroupBuffers, i: int, dst: _GroupBuffers, j: int) -> None:
+        dst.state[j].copy_(src.state[i])
+        dst.base[j].copy_(src.base[i])
+        dst.mom[j].copy_(src.mom[i])
+        if dst.wcomp is not dst.state:
+            dst.wcomp[j].copy_(src.wcomp[i])
+        if dst.fg is not None:
+            dst.fg[j].copy_(src.fg[i])
+        ms = dst.max_slots
+        dst.stats.view(3, -1, ms)[:, j].copy_(src.stats.view(3, -1, ms)[:, i])
 
     def _wave_collect(self, w: Optional[Dict[str, Any]]) -> List[ClientResult]:
         if w is None:
@@ -293,12 +345,14 @@ class GroupTrainer:
                 ev.setdefault(ph.end_step, []).append((g, ph))
         return ev
 
-    def _phase_end(self, b: _GroupBuffers, g: int, ph, snaps, pend_dist) -> None:
-        """End of a local round: optional model-replacement scaling + snapshots."""
+    def _phase_end(self, b: _GroupBuffers, g: int, ph, snaps, pend_dist, client: int) -> None:
+        """End of a local round: optional model-replacement scaling + snapshots.  ``g``: the
+        client's row in ``b``; ``snaps``: the client's snapshot dict; ``client``: its index in
+        the wave (the key of its pending distances)."""
         P = self.spec.P
         if ph.pre_scale_snap is not None:
             pre = b.state[g].clone()
-            snaps[g][ph.pre_scale_snap] = pre
+            snaps[ph.pre_scale_snap] = pre
             gamma = float(self.params["scale_weights_poison"])
             scaled = ops.scale_from_base(b.state[g], b.base[g], gamma)
             b.state[g].copy_(scaled)
@@ -309,9 +363,9 @@ class GroupTrainer:
             # before scaling, scaled norm — squared, on device, read once at collect
             zero = self._zeros_p()
             base = b.base[g:g + 1, :P]
-            pend_dist.append((g, ph.epoch, [
+            pend_dist.append((client, ph.epoch, [
                 ops.sq_dists(b.state[g:g + 1, :P], b.base[g, :P])[0], ops.sq_dists(base, zero)[0],
                 ops.sq_dists(pre[None, :P], zero)[0], ops.sq_dists(pre[None, :P], b.base[g, :P])[0],
                 ops.sq_dists(b.state[g:g + 1, :P], zero)[0]]))
-        snaps[g][ph.post_snap] = b.state[g].clone()
+        snaps[ph.post_snap] = b.state[g].clone()
         b.base[g].copy_(b.state[g])
