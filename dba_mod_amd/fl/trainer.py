@@ -256,7 +256,7 @@ class GroupTrainer:
                 "trace": torch.stack(trace) if trace else None}
 
     # a lone client's tail shorter than this stays in the group graph
-    SOLO_MIN_STEPS = int(os.environ.get("DBA_SOLO_MIN_STEPS", "0"))
+    SOLO_MIN_STEPS = int(os.environ.get("DBA_SOLO_MIN_STEPS", "4"))
 
     def _solo_tail(self, clients: List[ClientPlan], T: int) -> Optional[Tuple[int, int]]:
         """(t0, g) when from step t0 on only client g trains (the 6-epoch attacker after the
