@@ -414,11 +414,31 @@ __global__ __launch_bounds__(256) void bn_small_fwd_kernel(
   float s0[8], s1[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) { s0[e] = 0.f; s1[e] = 0.f; }
-  for (int r = tid; r < R; r += 256) {
-    float p[8];
-    ld8(y + base + (long long)r * C, p);
+  // R <= 4 * 256 (the single-launch threshold): the thread's rows are loaded once, all in
+  // flight together, and kept in registers for the apply pass (same summation order)
+  constexpr int RPT = 4;
+  const bool cached = R <= RPT * 256;
+  float yc[RPT][8];
+  if (cached) {
 #pragma unroll
-    for (int e = 0; e < 8; ++e) { const float x = p[e]; s0[e] += x; s1[e] = fmaf(x, x, s1[e]); }
+    for (int k = 0; k < RPT; ++k) {
+      const int r = tid + k * 256;
+      if (r < R) ld8(y + base + (long long)r * C, yc[k]);
+    }
+#pragma unroll
+    for (int k = 0; k < RPT; ++k) {
+      if (tid + k * 256 < R) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) { const float x = yc[k][e]; s0[e] += x; s1[e] = fmaf(x, x, s1[e]); }
+      }
+    }
+  } else {
+    for (int r = tid; r < R; r += 256) {
+      float p[8];
+      ld8(y + base + (long long)r * C, p);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { const float x = p[e]; s0[e] += x; s1[e] = fmaf(x, x, s1[e]); }
+    }
   }
   block_sum16(s0, s1, red);
   if (tid < 8) {
@@ -446,10 +466,8 @@ __global__ __launch_bounds__(256) void bn_small_fwd_kernel(
 #pragma unroll
   for (int e = 0; e < 8; ++e) { sc[e] = coef[0][e]; sh[e] = coef[1][e]; }
   float vmax = 0.f;
-  for (int r = tid; r < R; r += 256) {
-    const long long o = base + (long long)r * C;
-    float p[8], rp[8], op[8];
-    ld8(y + o, p);
+  auto apply_row = [&](long long o, const float (&p)[8]) __attribute__((always_inline)) {
+    float rp[8], op[8];
     if (res) ld8(res + o, rp);
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
@@ -460,6 +478,20 @@ __global__ __launch_bounds__(256) void bn_small_fwd_kernel(
       vmax = fmaxf(vmax, fabsf(x));
     }
     st8(out + o, op);
+  };
+  if (cached) {
+#pragma unroll
+    for (int k = 0; k < RPT; ++k) {
+      const int r = tid + k * 256;
+      if (r < R) apply_row(base + (long long)r * C, yc[k]);
+    }
+  } else {
+    for (int r = tid; r < R; r += 256) {
+      const long long o = base + (long long)r * C;
+      float p[8];
+      ld8(y + o, p);
+      apply_row(o, p);
+    }
   }
   if (amax) amax_fold(amax, amax_ld, g, vmax);
 }
@@ -485,18 +517,41 @@ __global__ __launch_bounds__(256) void bn_small_bwd_kernel(
     s0[e] = 0.f;
     s1[e] = 0.f;
   }
-  for (int r = tid; r < R; r += 256) {
-    const long long o = base + (long long)r * C;
-    float dp[8], yp[8], op[8];
+  // R <= 4 * 256: the thread's rows of dout (ReLU-masked) and y are loaded once, all in
+  // flight together, and kept in registers for the apply pass (same summation order)
+  constexpr int RPT = 4;
+  const bool cached = R <= RPT * 256;
+  float dc[RPT][8], yc[RPT][8];
+  auto load_row = [&](long long o, float (&dp)[8], float (&yp)[8]) __attribute__((always_inline)) {
+    float op[8];
     ld8(dout + o, dp);
     ld8(y + o, yp);
     if (relu) ld8(out + o, op);
 #pragma unroll
+    for (int e = 0; e < 8; ++e)
+      if (relu && !(op[e] > 0.f)) dp[e] = 0.f;
+  };
+  auto acc_row = [&](const float (&dp)[8], const float (&yp)[8]) __attribute__((always_inline)) {
+#pragma unroll
     for (int e = 0; e < 8; ++e) {
-      float d = dp[e];
-      if (relu && !(op[e] > 0.f)) d = 0.f;
-      s0[e] += d;
-      s1[e] = fmaf(d, (yp[e] - mu[e]) * is[e], s1[e]);
+      s0[e] += dp[e];
+      s1[e] = fmaf(dp[e], (yp[e] - mu[e]) * is[e], s1[e]);
+    }
+  };
+  if (cached) {
+#pragma unroll
+    for (int k = 0; k < RPT; ++k) {
+      const int r = tid + k * 256;
+      if (r < R) load_row(base + (long long)r * C, dc[k], yc[k]);
+    }
+#pragma unroll
+    for (int k = 0; k < RPT; ++k)
+      if (tid + k * 256 < R) acc_row(dc[k], yc[k]);
+  } else {
+    for (int r = tid; r < R; r += 256) {
+      float dp[8], yp[8];
+      load_row(base + (long long)r * C, dp, yp);
+      acc_row(dp, yp);
     }
   }
   block_sum16(s0, s1, red);
@@ -518,20 +573,29 @@ __global__ __launch_bounds__(256) void bn_small_bwd_kernel(
 #pragma unroll
   for (int e = 0; e < 8; ++e) { A[e] = coef[0][e]; B[e] = coef[1][e]; K[e] = coef[2][e]; }
   float vmax = 0.f;
-  for (int r = tid; r < R; r += 256) {
-    const long long o = base + (long long)r * C;
-    float dp[8], yp[8], op[8], p1[8];
-    ld8(dout + o, dp);
-    ld8(y + o, yp);
-    if (relu) ld8(out + o, op);
+  auto apply_row = [&](long long o, const float (&dp)[8], const float (&yp)[8]) __attribute__((always_inline)) {
+    float p1[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      if (relu && !(op[e] > 0.f)) dp[e] = 0.f;
       p1[e] = fmaf(A[e], dp[e], fmaf(B[e], yp[e], K[e]));
       vmax = fmaxf(vmax, fabsf(p1[e]));
     }
     st8(dy + o, p1);
     if (dres) st8(dres + o, dp);
+  };
+  if (cached) {
+#pragma unroll
+    for (int k = 0; k < RPT; ++k) {
+      const int r = tid + k * 256;
+      if (r < R) apply_row(base + (long long)r * C, dc[k], yc[k]);
+    }
+  } else {
+    for (int r = tid; r < R; r += 256) {
+      const long long o = base + (long long)r * C;
+      float dp[8], yp[8];
+      load_row(o, dp, yp);
+      apply_row(o, dp, yp);
+    }
   }
   if (amax) amax_fold(amax, amax_ld, g, vmax);
 }
