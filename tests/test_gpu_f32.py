@@ -446,66 +446,12 @@ def test_fp32_pool_relu_loss_fold(H, R64):
     assert wf.dtype == torch.float32 and _rel(wf, wr) < 1e-6 and _rel(bf, br) < 1e-6
 
 
-class _Branches:
-    """The discrete forward decisions of one run (ReLU masks, max-pool argmax) replayed into
-    another: the fp64 oracle then takes the same branch as the HIP run at the near-ties that
-    fp32 rounding decides (a pre-activation within ~1e-7 of zero flips its ReLU mask and moves
-    that element's gradient by O(1) — at random init a step has many candidates; torch-fp32
-    itself flips on some of these steps).  Only valid images are replayed."""
-
-    def __init__(self, nval):
-        self.nval, self.rec, self.replay, self.i = nval, [], False, 0
-
-    def wrap(self, mod):
-        o_bn, o_conv, o_mp = mod.bn_train, mod.conv2d, mod.maxpool2d
-
-        def bn_train(y, gamma, beta, rmean, rvar, nvalid, momentum, eps, relu, residual):
-            out, m, s = o_bn(y, gamma, beta, rmean, rvar, nvalid, momentum, eps, relu, residual)
-            return (self._relu(out) if relu else out), m, s
-
-        def conv2d(*a, **k):
-            y = o_conv(*a, **k)
-            return self._relu(y) if k.get("relu", a[7] if len(a) > 7 else False) else y
-
-        def maxpool2d(x, kk, st, p):
-            y, ind = o_mp(x, kk, st, p)
-            return self._pool(x, y, ind)
-        return {"bn_train": bn_train, "conv2d": conv2d, "maxpool2d": maxpool2d}
-
-    def _valid(self, t):
-        v = torch.zeros(t.shape[:2], dtype=torch.bool)
-        for g in range(t.shape[0]):
-            v[g, :int(self.nval[g])] = True
-        return v.view(*t.shape[:2], *([1] * (t.dim() - 2))).to(t.device)
-
-    def _relu(self, out):
-        if not self.replay:
-            self.rec.append((out > 0).cpu())
-            return out
-        m = self.rec[self.i].to(out.device) & self._valid(out)
-        self.i += 1
-        pos = out > 0
-        keep = self._valid(out)
-        out = torch.where(keep & m & ~pos, torch.full_like(out, 1e-300), out)
-        return torch.where(keep & ~m & pos, torch.zeros_like(out), out)
-
-    def _pool(self, x, y, ind):
-        if not self.replay:
-            self.rec.append(ind.cpu())
-            return y, ind
-        hind = torch.where(self._valid(ind).cpu(), self.rec[self.i], ind.cpu()).to(ind.device)
-        self.i += 1
-        G, N, Hh, Ww, C = x.shape
-        yy = x.reshape(G, N, Hh * Ww, C).gather(2, hind.reshape(G, N, -1, C).long()).reshape(y.shape)
-        return yy.to(y.dtype), hind.to(ind.dtype)
-
-
 @pytest.mark.parametrize("arch,shp", [("resnet18_cifar", (32, 32, 3)), ("mnist", (28, 28, 1)),
                                       ("resnet18_tiny", (64, 64, 3)), ("loan", (91,)),
                                       ("resnet50_cifar", (32, 32, 3))])
 def test_fp32_train_step_vs_fp64(H, R64, arch, shp):
     """One grouped training step of every model through the fp32 HIP family vs the fp64
-    reference taking the HIP run's ReLU / max-pool branches (_Branches): loss and gradient at
+    reference taking the HIP run's ReLU / max-pool branches (ops.branches): loss and gradient at
     fp32 level (<= 1e-4 relative; the bf16 family needs a ~20 % band at random init), BN
     running stats, inactive replica untouched, bitwise reproducible across runs."""
     from dba_mod_amd import ops
@@ -539,7 +485,8 @@ def test_fp32_train_step_vs_fp64(H, R64, arch, shp):
                 setattr(ops, k, v)
         return loss, grads, state
 
-    br = _Branches(nval)
+    from dba_mod_amd.ops.branches import BranchReplay
+    br = BranchReplay(nval)
     lh, gh, sh = run(H, dev, torch.float32, br.wrap(H))
     lh2, gh2, sh2 = run(H, dev, torch.float32)
     assert torch.equal(gh, gh2) and torch.equal(sh, sh2) and torch.equal(lh, lh2), "not bitwise reproducible"
