@@ -1605,7 +1605,14 @@ DBA_EXPORT int dba_xwgrad(const float* dy, long long dy_gstride, const float* x,
   if ((long long)N * Ho * Wo * Cout >= (1LL << 29) || (long long)N * H * W * Cin >= (1LL << 29)) return -103;
   const bool v4 = Cin % 4 == 0 && Cout % 4 == 0 && Wo % 4 == 0 && aligned16(dy) && aligned16(x) &&
                   dy_gstride % 4 == 0 && x_gstride % 4 == 0;
-  const int bno = Cout <= 32 ? 32 : Cout <= 64 ? 64 : 128;
+  // output-channel tile: 128 for wide layers; DBA_F32_WGRAD_BNO64_BLOCKS=n takes 64 when a
+  // launch would have fewer than n blocks at 128 (a lone client's stage-3/4 weight gradients:
+  // 144).  Off: lone step 1.774 -> 1.763 ms with n = 256, within run-to-run spread
+  // (scripts/gpu/r2c_iter10.sh).  The tile never changes a bit (same per-element row order
+  // within a slab); Z came from the per-replica geometry above.
+  static const int bno64_below = env_int("DBA_F32_WGRAD_BNO64_BLOCKS", 0);
+  int bno = Cout <= 32 ? 32 : Cout <= 64 ? 64 : 128;
+  if (bno == 128 && (long long)ceil_div(Cout, 128) * a.tiles_k * G * Z < bno64_below) bno = 64;
   const dim3 grid((unsigned)(ceil_div(Cout, bno) * a.tiles_k), G, Z);
 #define XW_GO(BNO_, WN__, WK__, P_, V_, H_) \
   hipLaunchKernelGGL((xwgrad_kernel<BNO_, 128, WN__, WK__, P_, V_, H_>), grid, dim3(256), 0, st, a)
