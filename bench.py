@@ -17,6 +17,13 @@ contains all four poison rounds.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--dtype fp32|bf16]
     torchrun --nproc-per-node N bench.py --gpus N ...     # one rank per GPU over RCCL
+    python bench.py --emulate-rank R --emulate-world N    # rank R's share of N, on one GPU
+
+Launch forms.  Under a launcher (``WORLD_SIZE`` set, torchrun) every process is one rank and
+``--gpus`` must equal ``WORLD_SIZE`` (checked; a mismatch fails loudly).  Without a launcher
+and ``--gpus N > 1`` this process is only a PARENT: it never imports the framework or touches
+the GPU, starts ``python -m torch.distributed.run --nproc-per-node N`` as a child (N fresh
+rank processes), relays rank 0's JSON line and exits with the child's status.
 
 Strong scaling: the round's work is fixed; N GPUs split its clients (LPT) and its
 evaluation images.
@@ -26,20 +33,14 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import subprocess
 import sys
 import tempfile
 import time
 from typing import Optional
 
-import torch
-
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
-
-from dba_mod_amd import config as C  # noqa: E402
-from dba_mod_amd import ops  # noqa: E402
-from dba_mod_amd.fl.server import Server  # noqa: E402
-from dba_mod_amd.parallel.dist import init_distributed, shutdown  # noqa: E402
 
 METRIC = "FL rounds/sec + backdoor ASR & main-task acc, ResNet-18 CIFAR-10 100 clients"
 # reference design, CIFAR FL throughput ≈ 0.0085 rounds/s (8-vCPU estimate;
@@ -49,9 +50,51 @@ MODEL_NAMES = {"cifar": "ResNet-18 (half-width, CIFAR-10)", "tiny-imagenet-200":
                "mnist": "MnistNet (MNIST)", "loan": "LoanNet MLP (LOAN)"}
 
 
+def _free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _spawn_ranks(n: int, argv) -> int:
+    """Parent of an N-rank run: no framework import, no GPU call, no exec.  The child
+    launcher starts N fresh ranks; their stdout is streamed (non-JSON lines to stderr so
+    progress stays visible) and exactly one JSON line (rank 0's) is relayed to stdout."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__), *argv]
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, env=env, cwd=ROOT)
+    lines = []
+    assert proc.stdout is not None
+    for ln in proc.stdout:
+        if ln.startswith("{") and '"metric"' in ln:
+            lines.append(ln.strip())
+        else:
+            sys.stderr.write(ln)
+            sys.stderr.flush()
+    rc = proc.wait()
+    if rc != 0:
+        print(f"bench.py: {n}-rank launch failed (exit {rc})", file=sys.stderr)
+        return rc
+    if len(lines) != 1:
+        print(f"bench.py: expected one JSON line from rank 0, got {len(lines)}", file=sys.stderr)
+        return 1
+    out = json.loads(lines[0])
+    if out.get("n_gpus") != n or out.get("world") != n:
+        print(f"bench.py: ranks reported world {out.get('world')} for --gpus {n}", file=sys.stderr)
+        return 1
+    print(lines[0], flush=True)
+    return 0
+
+
 def _split_label(server) -> Optional[dict]:
     """How the fp32 kernels carry fp32 operands on the bf16/fp16 MFMA (csrc/kernels/xgemm.hip):
     both modes reach fp32-level error (tests/test_gpu_f32.py)."""
+    import torch
+    from dba_mod_amd import ops
     if server.dtype != torch.float32 or ops.backend_name(server.device) != "hip":
         return None
     names = {2: "bf16x2 (3 MFMA)", 3: "bf16x3 (6 MFMA)", 16: "scaled fp16x2 (3 MFMA)"}
@@ -60,7 +103,7 @@ def _split_label(server) -> Optional[dict]:
     return {"train": names.get(tr, str(tr)), "eval": names.get(lib, str(lib))}
 
 
-def main() -> int:
+def _args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=8)
@@ -77,9 +120,44 @@ def main() -> int:
                     help="compute precision: fp32 = the reference's (split-bf16 MFMA kernels, default); "
                          "bf16 = fast mode (bf16 activations, fp32 master weights)")
     ap.add_argument("--set", dest="overrides", nargs="*", default=[])
-    args = ap.parse_args()
+    ap.add_argument("--emulate-rank", type=int, default=None,
+                    help="run only rank R's share of an --emulate-world N round on one device "
+                         "(collectives are counted no-ops; per-rank critical-path timing)")
+    ap.add_argument("--emulate-world", type=int, default=None)
+    return ap.parse_args(argv)
 
-    dctx = init_distributed(prefer_gpu=not args.cpu)
+
+def main(argv=None) -> int:
+    argv = sys.argv[1:] if argv is None else list(argv)
+    args = _args(argv)
+    emulate = args.emulate_world is not None
+    if emulate and args.emulate_rank is None:
+        raise SystemExit("--emulate-world needs --emulate-rank")
+    if "WORLD_SIZE" in os.environ:
+        world_env = int(os.environ["WORLD_SIZE"])
+        if emulate or world_env != args.gpus:
+            raise SystemExit(f"bench.py: launched with WORLD_SIZE={world_env} but --gpus {args.gpus}"
+                             + (" (--emulate-* runs without a launcher)" if emulate else ""))
+    elif args.gpus > 1 and not emulate:
+        return _spawn_ranks(args.gpus, argv)
+    elif emulate and args.gpus != 1:
+        raise SystemExit("bench.py: --emulate-* runs on one device (--gpus 1)")
+    return _run(args)
+
+
+def _run(args) -> int:
+    import torch
+    from dba_mod_amd import config as C
+    from dba_mod_amd import ops
+    from dba_mod_amd.fl.server import Server
+    from dba_mod_amd.parallel.dist import emulated_ctx, init_distributed, shutdown
+
+    if args.emulate_world is not None:
+        dctx = emulated_ctx(args.emulate_rank, args.emulate_world, prefer_gpu=not args.cpu)
+    else:
+        dctx = init_distributed(prefer_gpu=not args.cpu)
+    devices = dctx.gather_strings(f"{dctx.device}" + (f" ({torch.cuda.get_device_name(dctx.device)})"
+                                                      if dctx.device.type == "cuda" else ""))
     over = {"resumed_model": False, "synthetic_data": True, "save_model": False,
             "pretrain_rounds": args.pretrain_rounds, "compute_dtype": args.dtype}
     if args.aggregation:
@@ -117,12 +195,16 @@ def main() -> int:
     sync()
     elapsed = dctx.all_reduce_max(time.perf_counter() - t0)
     rps = args.steps / elapsed if elapsed > 0 else 0.0
-    if dctx.is_main:
+    comm_kinds = sorted({k for r in done for k in r.get("comm_bytes", {})})
+    comm_mean = {k: int(round(sum(r.get("comm_bytes", {}).get(k, 0) for r in done) / max(1, len(done))))
+                 for k in comm_kinds}
+    if dctx.is_main or dctx.emulated:
         metric = METRIC if params.type == "cifar" else (
             f"FL rounds/sec + backdoor ASR & main-task acc, {MODEL_NAMES.get(params.type, params.type)} "
             f"{int(params['number_of_total_participants'])} clients")
         out = {
-            "metric": metric, "value": round(rps, 4), "unit": "rounds/s", "n_gpus": dctx.world,
+            "metric": metric, "value": round(rps, 4), "unit": "rounds/s",
+            "n_gpus": 1 if dctx.emulated else dctx.world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1000.0 * elapsed / max(1, args.steps), 2),
             "higher_is_better": True, "scaling": "strong",
             "vs_baseline": round(rps / BASELINE_ROUNDS_PER_S, 2) if params.type == "cifar" else None,
@@ -135,12 +217,21 @@ def main() -> int:
                      + f"{args.pretrain_rounds} benign FedAvg rounds (untimed)"),
             "config": {"model": MODEL_NAMES.get(params.type, params.type),
                        "global_batch": int(params["batch_size"]) * int(params["no_models"]),
-                       "seq_len": None, "parallelism": f"client-dp{dctx.world}",
+                       "seq_len": None,
+                       "parallelism": (f"emulated rank {dctx.rank} of client-dp{dctx.world}" if dctx.emulated
+                                       else f"client-dp{dctx.world}"),
                        "clients_total": int(params["number_of_total_participants"]),
                        "clients_per_round": int(params["no_models"]),
                        "attackers": params.adversary_list, "aggregation": params["aggregation_methods"],
                        "rounds_timed": f"{epoch - args.steps}..{epoch - 1}",
                        "baseline_source": "BASELINE.md §4 reference-design estimate 0.0085 rounds/s"},
+            "world": dctx.world,
+            "emulated": bool(dctx.emulated),
+            "dist_backend": dctx.backend,
+            "devices": devices,
+            "rccl_ok": dctx.selfcheck_ok if dctx.backend == "nccl" else None,
+            "collective_selfcheck_ok": dctx.selfcheck_ok,
+            "comm_bytes_per_round": comm_mean,
             "ops_backend": ops.backend_name(dctx.device),
             "fp32_split": _split_label(server),
             "global_acc": round(float(last.get("global_acc", 0.0)), 3),

@@ -29,7 +29,15 @@ payload of every collective (per kind) for tests and the round metrics.  The int
 counters never enter a float bucket.
 
 On a one-GPU box the multi-rank path is rehearsed with ``DBA_SHARE_GPU=1`` (every rank on
-device 0) and ``DBA_DIST_BACKEND=gloo`` (``tests/test_gpu_dist.py``).
+device 0) and ``DBA_DIST_BACKEND=gloo`` (``tests/test_gpu_dist.py``).  ``emulate_rank``
+(:func:`emulated_ctx`, ``bench.py --emulate-rank R --emulate-world N``) runs exactly rank R's
+share of an N-rank round in ONE process: collectives are local no-ops that still count their
+bytes, so the per-rank critical path can be timed on one GPU (the numerics are not those of
+the real N-rank run: the other ranks' contributions are missing).
+
+``init_distributed`` ends with a one-element all-reduce self-check (``selfcheck_ok``), and
+``DBA_FORCE_PG=1`` creates the process group even at world 1 (RCCL initialisation evidence
+on a one-GPU box).
 """
 from __future__ import annotations
 
@@ -37,7 +45,7 @@ import collections
 import datetime
 import os
 from dataclasses import dataclass, field
-from typing import Dict, List, Optional, Sequence
+from typing import Any, Dict, List, Optional, Sequence
 
 import torch
 import torch.distributed as dist
@@ -56,6 +64,9 @@ class DistCtx:
     device: torch.device = torch.device("cpu")
     backend: str = "none"
     bytes: Dict[str, int] = field(default_factory=lambda: collections.Counter())
+    emulated: bool = False          # rank R of an N-rank round, alone: collectives are no-ops
+    selfcheck_ok: Optional[bool] = None   # init-time all-reduce self-check (None: no group)
+    pg: bool = False                # a torch.distributed process group exists
 
     @property
     def is_main(self) -> bool:
@@ -65,8 +76,13 @@ class DistCtx:
     def enabled(self) -> bool:
         return self.world > 1
 
+    @property
+    def comm(self) -> bool:
+        """Collectives really run (a real multi-rank group, not an emulated rank)."""
+        return self.world > 1 and not self.emulated
+
     def barrier(self) -> None:
-        if self.enabled:
+        if self.comm:
             if self.backend == "nccl":
                 dist.barrier(device_ids=[self.local_rank])
             else:
@@ -88,14 +104,15 @@ class DistCtx:
             flat = t.view(-1) if t.is_contiguous() else None
             if flat is None:
                 raise ValueError("all_reduce_ needs a contiguous buffer")
-            step = max(1, SPLIT_BYTES // flat.element_size())
-            for i in range(0, flat.numel(), step):
-                dist.all_reduce(flat[i:i + step])
+            if self.comm:
+                step = max(1, SPLIT_BYTES // flat.element_size())
+                for i in range(0, flat.numel(), step):
+                    dist.all_reduce(flat[i:i + step])
             self.bytes["all_reduce"] += flat.numel() * flat.element_size()
         return t
 
     def all_reduce_max(self, value: float) -> float:
-        if not self.enabled:
+        if not self.comm:
             return value
         t = torch.tensor([value], dtype=torch.float64, device=self.device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -103,25 +120,46 @@ class DistCtx:
 
     def all_gather_rows(self, local: torch.Tensor, k_max: int) -> torch.Tensor:
         """Gather each rank's ``[k_r, W]`` rows (k_r <= k_max) into ``[world * k_max, W]``
-        (rank-major, zero-padded rows) with one flat collective."""
+        (rank-major, zero-padded rows).  Each row is padded to the §5.8 unit and the rows
+        go out in all-gathers of at most 64 MB of output each (a CIFAR RFA gather of 10
+        final states is ~112 MB: two pieces)."""
         W = local.shape[1]
         if not self.enabled:
             out = torch.zeros(k_max, W, dtype=local.dtype, device=local.device)
             out[:local.shape[0]] = local
             return out
-        send = torch.zeros(k_max, W, dtype=local.dtype, device=local.device)
+        unit = self.pad_unit(local.element_size())
+        Wp = (W + unit - 1) // unit * unit
+        send = torch.zeros(k_max, Wp, dtype=local.dtype, device=local.device)
         if local.shape[0]:
-            send[:local.shape[0]] = local
-        out = torch.empty(self.world * k_max, W, dtype=local.dtype, device=local.device)
-        dist.all_gather_into_tensor(out, send)
+            send[:local.shape[0], :W] = local
+        out = torch.zeros(self.world, k_max, Wp, dtype=local.dtype, device=local.device)
+        if self.comm:
+            rows = max(1, SPLIT_BYTES // (self.world * Wp * local.element_size()))
+            for i in range(0, k_max, rows):
+                j = min(k_max, i + rows)
+                piece = torch.empty(self.world * (j - i), Wp, dtype=local.dtype, device=local.device)
+                dist.all_gather_into_tensor(piece, send[i:j].contiguous())
+                out[:, i:j] = piece.view(self.world, j - i, Wp)
+        else:
+            out[self.rank] = send
         self.bytes["all_gather"] += out.numel() * out.element_size()
-        return out
+        return out[:, :, :W].reshape(self.world * k_max, W)
 
     def broadcast_(self, t: torch.Tensor, src: int = 0) -> torch.Tensor:
         if self.enabled:
-            dist.broadcast(t, src)
+            if self.comm:
+                dist.broadcast(t, src)
             self.bytes["broadcast"] += t.numel() * t.element_size()
         return t
+
+    def gather_strings(self, s: str) -> List[str]:
+        """Every rank's ``s`` (rank order), e.g. its device; one object all-gather."""
+        if not self.comm:
+            return [s]
+        out: List[Any] = [None] * self.world
+        dist.all_gather_object(out, s)
+        return [str(x) for x in out]
 
     def take_bytes(self) -> Dict[str, int]:
         """Collective payload bytes since the last call (and reset)."""
@@ -144,7 +182,8 @@ def init_distributed(prefer_gpu: bool = True, timeout_s: int = 1800) -> DistCtx:
         device = torch.device("cuda", dev_index)
     else:
         device = torch.device("cpu")
-    if world <= 1:
+    force_pg = os.environ.get("DBA_FORCE_PG") == "1" and "MASTER_PORT" in os.environ
+    if world <= 1 and not force_pg:
         return DistCtx(0, 1, 0, device, "none")
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     backend = os.environ.get("DBA_DIST_BACKEND") or ("nccl" if use_gpu else "gloo")   # "nccl" is RCCL
@@ -154,9 +193,33 @@ def init_distributed(prefer_gpu: bool = True, timeout_s: int = 1800) -> DistCtx:
         kw["device_id"] = device
     if not dist.is_initialized():
         dist.init_process_group(**kw)
-    return DistCtx(rank, world, dev_index, device, backend)
+    ctx = DistCtx(rank, world, dev_index, device, backend, pg=True)
+    ctx.selfcheck_ok = selfcheck(ctx)
+    if not ctx.selfcheck_ok:
+        raise RuntimeError(f"rank {rank}: {backend} all-reduce self-check failed (world {world})")
+    return ctx
+
+
+def selfcheck(ctx: DistCtx) -> bool:
+    """One all-reduce of ``rank + 1`` on the rank's device; the closed form is w(w+1)/2.
+    With backend "nccl" this is the first RCCL collective of the run."""
+    t = torch.full((4,), float(ctx.rank + 1), dtype=torch.float64, device=ctx.device)
+    dist.all_reduce(t)
+    return bool(torch.all(t == ctx.world * (ctx.world + 1) / 2).item())
+
+
+def emulated_ctx(rank: int, world: int, prefer_gpu: bool = True) -> DistCtx:
+    """Rank ``rank`` of a ``world``-rank round, run alone (no process group): every
+    collective is a local no-op that counts its bytes (``DistCtx.emulated``)."""
+    if not 0 <= rank < world:
+        raise ValueError(f"emulate rank {rank} of world {world}")
+    use_gpu = prefer_gpu and torch.cuda.is_available()
+    device = torch.device("cuda", 0) if use_gpu else torch.device("cpu")
+    if use_gpu:
+        torch.cuda.set_device(0)
+    return DistCtx(rank, world, 0, device, "emulated", emulated=True)
 
 
 def shutdown(ctx: DistCtx) -> None:
-    if ctx.enabled and dist.is_initialized():
+    if ctx.pg and dist.is_initialized():
         dist.destroy_process_group()

@@ -49,3 +49,35 @@ def test_bench_torchrun_world8_cpu():
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8",
            "--master-addr", "127.0.0.1", "--master-port", str(free_port()), "bench.py", "--gpus", "8", *SMALL]
     _check(_run(cmd, timeout=900), 8)
+
+
+def test_bench_self_spawn_world4_cpu():
+    """``python bench.py --cpu --gpus 4`` with NO launcher: the parent spawns 4 fresh ranks
+    (gloo), relays rank 0's line, and the result equals the world-1 run round for round."""
+    out = _run([sys.executable, "bench.py", "--gpus", "4", *SMALL], timeout=900)
+    _check(out, 4)
+    assert out["world"] == 4 and out["dist_backend"] == "gloo" and out["emulated"] is False
+    assert out["collective_selfcheck_ok"] is True and out["rccl_ok"] is None
+    assert len(out["devices"]) == 4
+    assert out["comm_bytes_per_round"].get("all_reduce", 0) > 0
+    one = _run([sys.executable, "bench.py", *SMALL])
+    assert one["world"] == 1 and one["dist_backend"] == "none" and one["comm_bytes_per_round"] == {}
+    assert out["rounds"] == one["rounds"]
+
+
+def test_bench_launcher_world_mismatch_fails():
+    """Under a launcher, --gpus must equal WORLD_SIZE (no silent one-GPU run)."""
+    env = dict(os.environ, PYTHONPATH=ROOT, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "8", *SMALL], cwd=ROOT, env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode != 0 and "WORLD_SIZE=2" in r.stderr
+
+
+def test_bench_emulated_rank_cpu():
+    """--emulate-rank R --emulate-world N: one process runs rank R's share; collectives are
+    counted no-ops (the bytes of the real N-rank run are still reported)."""
+    out = _run([sys.executable, "bench.py", "--emulate-rank", "1", "--emulate-world", "4", *SMALL])
+    assert out["emulated"] is True and out["world"] == 4 and out["n_gpus"] == 1
+    assert out["dist_backend"] == "emulated"
+    assert out["config"]["parallelism"] == "emulated rank 1 of client-dp4"
+    assert out["comm_bytes_per_round"].get("all_reduce", 0) > 0

@@ -98,8 +98,10 @@ def test_fedavg_bitwise_and_bytes(tmp_path, world):
     # round 12: the attacker (41) is the round's only long client; only its two snapshots
     # (pre-scaling, final) are gathered for its image-sharded tests.  (Round 11's clients are
     # all equally long, so all their tests are sharded and their snapshots gathered.)
+    # (each gathered row is padded to the §5.8 unit like every other collective)
+    u4 = DistCtx(world=world).pad_unit(4)
     ag12 = many[0]["comm"][1][1]
-    assert ag12 == world * 2 * S * 4, (ag12, S)
+    assert ag12 == world * 2 * ((S + u4 - 1) // u4 * u4) * 4, (ag12, S)
     assert one[0]["comm"] == [[0, 0, 0]] * len(rounds)
 
 
