@@ -87,6 +87,9 @@ _DEFAULTS: Dict[str, Any] = {
     "synthetic_data": "auto",     # auto: real files if present under data_dir, else synthetic
     "synthetic_train_size": None,  # override synthetic dataset sizes (tests / smoke runs)
     "synthetic_test_size": None,
+    # synthetic LOAN rows over all 51 states (default: the LendingClub dump's 2,260,668 loans,
+    # split by approximate LendingClub state shares; tests pass a small value)
+    "synthetic_loan_rows": None,
     "synthetic_noise": None,       # synthetic image pixel-noise sigma (None: per-dataset default)
     "synthetic_shared": None,      # fraction of the class template shared by all classes
     "synthetic_clutter": None,     # weight of the per-image random background field

@@ -199,6 +199,15 @@ LOAN_NAMED_FEATURES = ["num_tl_120dpd_2m", "num_tl_90g_dpd_24m", "pub_rec_bankru
                        "last_pymnt_amnt", "all_util"]
 LOAN_COUNT_FEATURES = ["num_tl_120dpd_2m", "num_tl_90g_dpd_24m", "pub_rec_bankruptcies", "pub_rec",
                        "acc_now_delinq", "tax_liens"]
+# approximate share of each state's loans in the LendingClub dump (population-like: CA, NY,
+# TX, FL lead; the DBA attackers CT / MO / TN hold ~1.5 % each), in US_STATES order
+LOAN_STATE_SHARE = [0.0023, 0.0123, 0.0074, 0.0240, 0.1390, 0.0217, 0.0152, 0.0024, 0.0029, 0.0718,
+                    0.0325, 0.0050, 0.0001, 0.0012, 0.0399, 0.0163, 0.0083, 0.0097, 0.0113, 0.0229,
+                    0.0236, 0.0018, 0.0262, 0.0180, 0.0161, 0.0054, 0.0029, 0.0280, 0.0016, 0.0033,
+                    0.0049, 0.0362, 0.0054, 0.0149, 0.0829, 0.0330, 0.0090, 0.0122, 0.0340, 0.0044,
+                    0.0120, 0.0021, 0.0156, 0.0822, 0.0071, 0.0280, 0.0021, 0.0212, 0.0131, 0.0037,
+                    0.0022]
+LENDINGCLUB_ROWS = 2_260_668
 LOAN_NUM_FEATURES = 91   # reference loan_model.py:11 in_dim
 LOAN_NUM_CLASSES = 9     # loan_helper.py:149-152
 
@@ -212,14 +221,24 @@ def loan_columns() -> List[str]:
     return cols
 
 
-def synthetic_loan(seed: int = 1, total_rows: int = 120000) -> List[TabularDataset]:
+def synthetic_loan(seed: int = 1, total_rows: int = LENDINGCLUB_ROWS) -> List[TabularDataset]:
     """51 per-state tabular datasets (91 features, 9 classes), 80/20 split.
 
     Feature scales mimic the reference preprocessing (``loan_preprocess.py``: values
     divided down to roughly O(1-10)).  Labels come from a fixed random linear teacher so
     the task is learnable; class priors are skewed like LendingClub's.
+
+    Size: by default the LendingClub dump's row count, split by approximate state shares
+    (``LOAN_STATE_SHARE``).  The size matters to the attack: the reference recipe's
+    MultiStepLR (``loan_train.py:83-92``, milestones 0.2E / 0.8E stepped at the start of each
+    internal epoch) runs ONE of the 10 poison epochs at ``poison_lr`` and the rest at 1/10 and
+    1/100 of it, so the attacker's trigger is learned from about 1.7 epochs' worth of
+    full-rate SGD steps over its state's rows.  A 20x smaller dataset leaves it 20x fewer
+    steps and the trigger unlearned (LOAN ASR 0 in every round:
+    profiles/asr_r1_synthetic_calibration.md, profiles/loan_attack_r3.md).
     """
     rng = np.random.RandomState(seed * 31 + 5)
+    gen = np.random.default_rng(seed * 31 + 7)      # bulk float32 draws (2.3 M x 91)
     cols = loan_columns()
     f = len(cols)
     teacher = rng.randn(f, LOAN_NUM_CLASSES).astype(np.float32)
@@ -229,14 +248,16 @@ def synthetic_loan(seed: int = 1, total_rows: int = 120000) -> List[TabularDatas
     counts = [cols.index(c) for c in LOAN_COUNT_FEATURES]
     teacher[counts] = 0.0
     prior = np.log(np.array([40, 35, 3, 2, 12, 1.5, 0.5, 3, 3], dtype=np.float32))
-    weights = rng.gamma(1.2, 1.0, size=len(US_STATES))
+    weights = np.array(LOAN_STATE_SHARE, dtype=np.float64)
     weights = weights / weights.sum()
+    scale = rng.uniform(0.2, 3.0, size=(1, f)).astype(np.float32)
     out: List[TabularDataset] = []
     for si, st in enumerate(US_STATES):
         n = max(60, int(total_rows * weights[si]))
-        x = np.abs(rng.randn(n, f).astype(np.float32)) * rng.uniform(0.2, 3.0, size=(1, f)).astype(np.float32)
-        x[:, counts] = rng.poisson(0.05, size=(n, len(counts))).astype(np.float32)
-        logits = x @ teacher * 0.6 + prior + rng.randn(n, LOAN_NUM_CLASSES).astype(np.float32) * 0.5
+        x = np.abs(gen.standard_normal((n, f), dtype=np.float32))
+        x *= scale
+        x[:, counts] = gen.poisson(0.05, size=(n, len(counts))).astype(np.float32)
+        logits = x @ teacher * 0.6 + prior + gen.standard_normal((n, LOAN_NUM_CLASSES), dtype=np.float32) * 0.5
         y = logits.argmax(1).astype(np.int64)
         perm = np.random.RandomState(42 + si).permutation(n)  # stands in for random_state=42
         n_te = int(np.ceil(n * 0.2))

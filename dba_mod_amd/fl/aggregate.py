@@ -11,8 +11,8 @@ broadcast is needed and every rank ends the round with a bit-identical global mo
   bucket (D1: the reference's float→int64 add crashes on modern torch).
 * :func:`geometric_median` / :func:`geometric_median_distributed` — RFA / Weiszfeld,
   ``helper.py:295-373`` (the latter with the points resident on their owner ranks): one batched distance
-  kernel (all n clients in one pass) and one weighted-sum kernel per iteration; the n
-  weights and the stopping test are the only host traffic.  Quirk D5 (``wv`` undefined if
+  kernel (all n clients in one pass) and one weighted-sum kernel per iteration; weights and
+  the stopping test stay on the device (one host read per aggregation).  Quirk D5 (``wv`` undefined if
   converged at iteration 0) resolves to the current weights.
 * :class:`FoolsGold` — ``helper.py:527-607``: cosine similarity of the clients' final-FC
   gradient features (history-summed with ``fg_use_memory``), pardoning, logit weights,
@@ -45,43 +45,70 @@ def fedavg_apply(global_state: torch.Tensor, delta_sum: torch.Tensor, eta: float
     ops.add_noise_scaled(global_state[:n_update], delta_sum, eta / no_models, sigma, seed, dp)
 
 
+def _weiszfeld(avg, dists, alphas: torch.Tensor, maxiter: int, eps: float, ftol: float):
+    """Weiszfeld iteration control on the DEVICE (reference ``helper.py:320-352``, SURVEY
+    §7.4.4): ``maxiter`` iterations are always enqueued; the stopping test
+    ``|f_prev - f| < ftol * f`` clears a device flag that freezes the median, distances and
+    weights from the converging iteration on (exactly the values the reference's ``break``
+    leaves).  No host sync inside the loop: one read of the per-iteration objectives at the
+    end (for the reference's log lines).  ``avg(w)``: weighted sum of the points for the
+    normalised fp64 weights ``w`` (device); ``dists(m)``: fp64 distances of the points to m."""
+    dev = alphas.device
+    median = avg(alphas)
+    d = dists(median)
+    obj = (alphas * d).sum()
+    active = torch.ones((), dtype=torch.bool, device=dev)
+    weights = alphas.clone()
+    wv = None
+    hist = torch.zeros(maxiter, 3, dtype=torch.float64, device=dev)   # prev_obj, obj, logged
+    for i in range(maxiter):
+        w = alphas / torch.clamp(d, min=eps)
+        w = w / w.sum()
+        m_new = avg(w)
+        d_new = dists(m_new)
+        o_new = (alphas * d_new).sum()
+        conv = (obj - o_new).abs() < ftol * o_new
+        hist[i, 0], hist[i, 1] = obj, o_new
+        hist[i, 2] = (active & ~conv).double()
+        weights = torch.where(active, w, weights)
+        median = torch.where(active, m_new, median)
+        d = torch.where(active, d_new, d)
+        obj = torch.where(active, o_new, obj)
+        # wv = the weights of the last iteration that did NOT converge (D5: the current ones)
+        upd = active & ~conv
+        wv = torch.where(upd, w, wv) if wv is not None else torch.where(upd, w, torch.full_like(w, float("nan")))
+        active = active & ~conv
+    h = hist.cpu().numpy()                       # the one host read of the aggregation
+    for i in range(maxiter):
+        if h[i, 2] > 0:
+            log.info(f"[rfa agg] iter:  {i}, prev_obj_val: {h[i, 0]}, obj_val: {h[i, 1]}, "
+                     f"abs dis: {abs(h[i, 0] - h[i, 1])}")
+    wv_h = wv.cpu().numpy() if wv is not None else None
+    if wv_h is None or np.isnan(wv_h).any():      # D5: converged at iteration 0
+        wv_h = weights.cpu().numpy()
+    return median, d, wv_h
+
+
 def geometric_median(global_state: torch.Tensor, finals: torch.Tensor, num_samples: Sequence[int],
                      eta: float, maxiter: int, dp: bool, sigma: float, seed: int, n_update: int,
                      eps: float = 1e-5, ftol: float = 1e-6,
                      max_update_norm: Optional[float] = None) -> Tuple[bool, List[float], List[float], int]:
     """Weiszfeld geometric median of the client deltas; returns (updated, wv, alphas, oracle calls)."""
     points = finals[:, :n_update] - global_state[None, :n_update]
-    a = np.asarray(num_samples, dtype=np.float64)
+    a = torch.tensor(num_samples, dtype=torch.float64, device=points.device)
     alphas = a / a.sum()
 
-    def avg(w: np.ndarray) -> torch.Tensor:
-        wn = torch.tensor(w / w.sum(), dtype=torch.float32, device=points.device)
-        return ops.weighted_sum(points, wn)
+    def avg(w: torch.Tensor) -> torch.Tensor:
+        return ops.weighted_sum(points, (w / w.sum()).float())
 
-    def dists(m: torch.Tensor) -> np.ndarray:
-        return np.sqrt(np.maximum(ops.sq_dists(points, m).double().cpu().numpy(), 0.0))
+    def dists(m: torch.Tensor) -> torch.Tensor:
+        return ops.sq_dists(points, m).double().clamp(min=0.0).sqrt()
 
-    median = avg(alphas)
-    calls = 1
-    d = dists(median)
-    obj = float((alphas * d).sum())
-    wv: Optional[np.ndarray] = None
-    weights = alphas.copy()
-    for i in range(maxiter):
-        prev_obj = obj
-        weights = alphas / np.maximum(eps, d)
-        weights = weights / weights.sum()
-        median = avg(weights)
-        calls += 1
-        d = dists(median)
-        obj = float((alphas * d).sum())
-        if abs(prev_obj - obj) < ftol * obj:
-            break
-        log.info(f"[rfa agg] iter:  {i}, prev_obj_val: {prev_obj}, obj_val: {obj}, abs dis: {abs(prev_obj - obj)}")
-        wv = weights.copy()
-    if wv is None:  # D5
-        wv = weights.copy()
-    final_alphas = d.tolist()
+    median, d, wv = _weiszfeld(avg, dists, alphas, maxiter, eps, ftol)
+    return _rfa_apply(global_state, median, d, wv, eta, dp, sigma, seed, n_update, max_update_norm, maxiter)
+
+
+def _rfa_apply(global_state, median, d, wv, eta, dp, sigma, seed, n_update, max_update_norm, maxiter):
     upd_norm = float(torch.linalg.vector_norm(median.double()).item())
     if max_update_norm is None or upd_norm < max_update_norm:
         ops.add_noise_scaled(global_state[:n_update], median, eta, sigma, seed, dp)
@@ -89,7 +116,7 @@ def geometric_median(global_state: torch.Tensor, finals: torch.Tensor, num_sampl
     else:
         log.info(f"\t\t\tUpdate norm = {upd_norm} is too large. Update rejected")
         updated = False
-    return updated, [float(x) for x in wv], final_alphas, calls
+    return updated, [float(x) for x in wv], [float(x) for x in d.cpu().tolist()], maxiter + 1
 
 
 def geometric_median_distributed(global_state: torch.Tensor, local_finals: torch.Tensor, local_idx: Sequence[int],
@@ -100,58 +127,32 @@ def geometric_median_distributed(global_state: torch.Tensor, local_finals: torch
     """Weiszfeld with the client deltas resident on their owner ranks (reference
     ``helper.py:320-352``): per iteration each rank forms its partial weighted sum of its own
     points (``reduce`` = all-reduce of the S-vector) and its points' distances to the median
-    (all-reduce of an n-vector with zeros for other ranks' clients).  Same iteration and
-    stopping rule as :func:`geometric_median`."""
+    (all-reduce of an n-vector with zeros for other ranks' clients).  Same device-side
+    iteration control and stopping rule as :func:`geometric_median`."""
     n = len(num_samples)
     dev = global_state.device
     idx = list(local_idx)
     points = local_finals[:, :n_update] - global_state[None, :n_update] if idx else None
-    a = np.asarray(num_samples, dtype=np.float64)
+    a = torch.tensor(num_samples, dtype=torch.float64, device=dev)
     alphas = a / a.sum()
+    idx_t = torch.tensor(idx, dtype=torch.int64, device=dev) if idx else None
 
-    def avg(w: np.ndarray) -> torch.Tensor:
+    def avg(w: torch.Tensor) -> torch.Tensor:
         wn = w / w.sum()
         if idx:
-            part = ops.weighted_sum(points, torch.tensor(wn[idx], dtype=torch.float32, device=dev),
-                                    out_dtype=torch.float64)
+            part = ops.weighted_sum(points, wn[idx_t].float(), out_dtype=torch.float64)
         else:
             part = torch.zeros(n_update, dtype=torch.float64, device=dev)
         return reduce(part).float()
 
-    def dists(m: torch.Tensor) -> np.ndarray:
+    def dists(m: torch.Tensor) -> torch.Tensor:
         full = torch.zeros(n, dtype=torch.float64, device=dev)
         if idx:
-            full[torch.tensor(idx, device=dev)] = ops.sq_dists(points, m).double()
-        return np.sqrt(np.maximum(reduce(full).cpu().numpy(), 0.0))
+            full[idx_t] = ops.sq_dists(points, m).double()
+        return reduce(full).clamp(min=0.0).sqrt()
 
-    median = avg(alphas)
-    calls = 1
-    d = dists(median)
-    obj = float((alphas * d).sum())
-    wv: Optional[np.ndarray] = None
-    weights = alphas.copy()
-    for i in range(maxiter):
-        prev_obj = obj
-        weights = alphas / np.maximum(eps, d)
-        weights = weights / weights.sum()
-        median = avg(weights)
-        calls += 1
-        d = dists(median)
-        obj = float((alphas * d).sum())
-        if abs(prev_obj - obj) < ftol * obj:
-            break
-        log.info(f"[rfa agg] iter:  {i}, prev_obj_val: {prev_obj}, obj_val: {obj}, abs dis: {abs(prev_obj - obj)}")
-        wv = weights.copy()
-    if wv is None:  # D5
-        wv = weights.copy()
-    upd_norm = float(torch.linalg.vector_norm(median.double()).item())
-    if max_update_norm is None or upd_norm < max_update_norm:
-        ops.add_noise_scaled(global_state[:n_update], median, eta, sigma, seed, dp)
-        updated = True
-    else:
-        log.info(f"\t\t\tUpdate norm = {upd_norm} is too large. Update rejected")
-        updated = False
-    return updated, [float(x) for x in wv], d.tolist(), calls
+    median, d, wv = _weiszfeld(avg, dists, alphas, maxiter, eps, ftol)
+    return _rfa_apply(global_state, median, d, wv, eta, dp, sigma, seed, n_update, max_update_norm, maxiter)
 
 
 class FoolsGold:

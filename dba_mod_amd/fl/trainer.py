@@ -234,6 +234,10 @@ class GroupTrainer:
         gstate = global_state[None, :self.spec.P]
         solo = self._solo_tail(clients, T)
         cur, row_of, cur_sched = b, list(range(G)), sched
+        # the round's global model norm (helper.model_global_norm(target_model),
+        # image_train.py:144, loan_train.py:148), once per wave, for the poison-phase log lines
+        gn2 = (ops.sq_dists(global_state[None, :self.spec.P], self._zeros_p())[0]
+               if any(ph.pre_scale_snap is not None for c in clients for ph in c.phases) else None)
         for t in range(T):
             if solo is not None and t == solo[0]:
                 # only client solo[1] is left: its remaining steps run in the G=1 graph
@@ -247,7 +251,7 @@ class GroupTrainer:
                 dist = (b.state[:, :self.spec.P] - gstate).float().pow(2).sum(1).sqrt()
                 trace.append(torch.stack([self._last_loss.float(), dist], 1))
             for (g, ph) in events.get(t + 1, []):
-                self._phase_end(cur, row_of[g], ph, snaps[g], pend_dist, g)
+                self._phase_end(cur, row_of[g], ph, snaps[g], pend_dist, g, gn2)
                 if on_client_done is not None and ph is clients[g].phases[-1]:
                     on_client_done(clients[g], snaps[g])
         if cur is not b:
@@ -345,10 +349,12 @@ class GroupTrainer:
                 ev.setdefault(ph.end_step, []).append((g, ph))
         return ev
 
-    def _phase_end(self, b: _GroupBuffers, g: int, ph, snaps, pend_dist, client: int) -> None:
+    def _phase_end(self, b: _GroupBuffers, g: int, ph, snaps, pend_dist, client: int,
+                   gn2: Optional[torch.Tensor] = None) -> None:
         """End of a local round: optional model-replacement scaling + snapshots.  ``g``: the
         client's row in ``b``; ``snaps``: the client's snapshot dict; ``client``: its index in
-        the wave (the key of its pending distances)."""
+        the wave (the key of its pending distances); ``gn2``: the round's squared global
+        model norm."""
         P = self.spec.P
         if ph.pre_scale_snap is not None:
             pre = b.state[g].clone()
@@ -359,12 +365,14 @@ class GroupTrainer:
             if b.wcomp is not b.state:
                 b.wcomp[g].copy_(b.state[g, :P])
             # norms / distances over parameters only (helper.model_global_norm /
-            # model_dist_norm, helper.py:59-71): scaled distance, global norm, norm and distance
-            # before scaling, scaled norm — squared, on device, read once at collect
+            # model_dist_norm, helper.py:59-71): scaled distance, the round's global model norm,
+            # norm and distance before scaling, scaled norm — squared, on device, read once at
+            # collect
             zero = self._zeros_p()
-            base = b.base[g:g + 1, :P]
+            if gn2 is None:
+                gn2 = ops.sq_dists(b.base[g:g + 1, :P], zero)[0]
             pend_dist.append((client, ph.epoch, [
-                ops.sq_dists(b.state[g:g + 1, :P], b.base[g, :P])[0], ops.sq_dists(base, zero)[0],
+                ops.sq_dists(b.state[g:g + 1, :P], b.base[g, :P])[0], gn2,
                 ops.sq_dists(pre[None, :P], zero)[0], ops.sq_dists(pre[None, :P], b.base[g, :P])[0],
                 ops.sq_dists(b.state[g:g + 1, :P], zero)[0]]))
         snaps[ph.post_snap] = b.state[g].clone()

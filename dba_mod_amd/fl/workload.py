@@ -127,7 +127,12 @@ def build_workload(params: C.Params, device: torch.device) -> Workload:
 def _build_loan(params: C.Params, spec: ModelSpec, device: torch.device, py_rng: random.Random,
                 np_rng: np.random.RandomState, data_dir: str) -> Workload:
     synth = _use_synthetic(params, readers.loan_available(data_dir))
-    states = synthetic.synthetic_loan(seed=int(params["seed"])) if synth else readers.read_loan(data_dir)
+    rows = params["synthetic_loan_rows"]
+    if rows is None and params["synthetic_train_size"] is not None:   # small test / smoke runs
+        rows = int(params["synthetic_train_size"]) * 5 // 4
+    states = (synthetic.synthetic_loan(seed=int(params["seed"]),
+                                       **({"total_rows": int(rows)} if rows is not None else {}))
+              if synth else readers.read_loan(data_dir))
     feature_index = {name: k for k, name in enumerate(states[0].columns)}
     tr_x, tr_y, te_x, te_y = [], [], [], []
     client_indices: Dict[Any, np.ndarray] = {}

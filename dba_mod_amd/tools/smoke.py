@@ -4,9 +4,10 @@ Runs the step in the framework's default (reference) precision, fp32, through th
 kernels (the HIP split-bf16 family on GPU) and checks it against the plain-PyTorch reference
 ops evaluated in fp64 on the CPU from the same inputs: loss, gradient and folded-BN eval
 logits must agree at fp32 level (not merely be finite).  The fp64 run replays the device
-run's ReLU / max-pool branches (ops/branches.py), so a near-tie that fp32 rounding decides
-differently from fp64 does not masquerade as arithmetic error; the unmatched errors are
-reported too."""
+run's ReLU / max-pool branches at near-ties only (ops/branches.py), so a near-tie that fp32
+rounding decides differently from fp64 does not masquerade as arithmetic error, while a
+clearly wrong branch still fails.  Plain torch-fp32 on the same device, under the same
+replay, is the like-for-like yardstick; the unmatched errors are reported too."""
 from __future__ import annotations
 
 import time
@@ -81,24 +82,33 @@ def run_smoke(device: torch.device, G: int = 2, N: int = 8) -> dict:
     old = ref.COMPUTE_DTYPE
     ref.COMPUTE_DTYPE = torch.float64
     try:
-        br.replay = True
+        br.start_replay()
         loss_r, g_r, el_r = _step(torch.device("cpu"), torch.float64, ref, G, N, over=br.wrap(ref))
+        ties = {"replayed": br.flips, "outside_tie_band": br.hard, "decisions": br.elements}
         _, g_u, el_u = _step(torch.device("cpu"), torch.float64, ref, G, N)   # fp64's own branches
     finally:
         ref.COMPUTE_DTYPE = old
-    # plain PyTorch fp32 on the same device: the precision the reference runs at
+    # plain PyTorch fp32 on the same device: the precision the reference runs at, both with
+    # its own branches and with the HIP run's near-tie branches replayed (like for like)
     _, g_t, el_t = _step(device, torch.float32, ref, G, N)
+    br.start_replay()
+    _, g_tm, el_tm = _step(device, torch.float32, ref, G, N, over=br.wrap(ref))
     out = {"device": str(device), "backend": ops.backend_name(device), "dtype": "fp32",
            "loss": [float(v) for v in loss], "loss_ref_fp64": [float(v) for v in loss_r],
            "grad_norm": float(g.double().norm()), "grad_norm_ref": float(g_r.norm()),
            "grad_rel_err": _rel(g, g_r), "eval_logits_rel_err": _rel(el, el_r),
+           "torch_fp32_grad_rel_err": _rel(g_tm, g_r), "torch_fp32_eval_logits_rel_err": _rel(el_tm, el_r),
            "grad_rel_err_unmatched_branches": _rel(g, g_u), "eval_logits_rel_err_unmatched_branches": _rel(el, el_u),
-           "torch_fp32_grad_rel_err": _rel(g_t, g_u), "torch_fp32_eval_logits_rel_err": _rel(el_t, el_u),
-           "seconds": round(secs, 3)}
+           "torch_fp32_grad_rel_err_unmatched": _rel(g_t, g_u),
+           "torch_fp32_eval_logits_rel_err_unmatched": _rel(el_t, el_u),
+           "near_tie_branches": ties, "seconds": round(secs, 3)}
     assert all(abs(a - b) <= 1e-5 * max(1.0, abs(b)) for a, b in zip(out["loss"], out["loss_ref_fp64"])), out
-    # with the branches matched, only arithmetic error is left: fp32 level (a bf16 path lands
-    # at ~2e-1); unmatched, a random-init ResNet with 8-image BatchNorm turns near-tie flips
-    # into ~1e-3 (plain torch-fp32 on these inputs: ~1e-3 too)
-    assert out["grad_rel_err"] < 1e-4, out
+    # branches matched only at near-ties (|pre| <= 1e-4 rms, ops/branches.py) and only a tiny
+    # fraction of them: what is left is arithmetic error, at fp32 level — compared like for
+    # like with torch-fp32 under the same replay; unmatched, a random-init ResNet with
+    # 8-image BatchNorm turns near-tie flips into ~1e-3 for torch-fp32 and HIP alike
+    assert ties["replayed"] <= 1e-4 * ties["decisions"] and ties["outside_tie_band"] == 0, out
+    assert out["grad_rel_err"] < max(1e-5, 3 * out["torch_fp32_grad_rel_err"]), out
     assert out["eval_logits_rel_err"] < max(1e-6, 4 * out["torch_fp32_eval_logits_rel_err"]), out
+    assert out["grad_rel_err_unmatched_branches"] < max(1e-4, 10 * out["torch_fp32_grad_rel_err_unmatched"]), out
     return out

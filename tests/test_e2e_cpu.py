@@ -116,7 +116,7 @@ def test_loan_workload_round(tmp_path):
                   "1_poison_trigger_values": [20, 100], "0_poison_epochs": [2], "1_poison_epochs": [3],
                   "lr": 0.001, "poison_lr": 0.0005, "internal_poison_epochs": 3, "poisoning_per_batch": 10,
                   "scale_weights_poison": 30, "save_dir": str(tmp_path), "start_epoch": 1, "epochs": 3,
-                  "sampling_dirichlet": False})
+                  "sampling_dirichlet": False, "synthetic_loan_rows": 60000})
     s = Server(p, DistCtx(), write_outputs=True)
     r1 = s.run_round(1)
     r2 = s.run_round(2)        # CT poisons (needs the pre-eval ASR for the adaptive poison lr)

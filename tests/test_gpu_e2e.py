@@ -123,17 +123,87 @@ def _small_params(**kw):
     return C.load_params(os.path.join(root, "configs", "mnist_params.yaml"), base)
 
 
-def test_graph_replay_matches_eager(dev, tmp_path):
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_graph_replay_matches_eager(dev, tmp_path, dtype):
+    """A captured HIP graph replays the same launches as the eager step: bit-identical in the
+    deterministic fp32 family; the bf16 family within its rounding band."""
     from dba_mod_amd.fl.server import Server
     from dba_mod_amd.parallel.dist import DistCtx
     outs = []
     for cap in (False, True):
-        p = _small_params(graph_capture=cap, save_dir=str(tmp_path))
+        p = _small_params(graph_capture=cap, save_dir=str(tmp_path), compute_dtype=dtype)
         s = Server(p, DistCtx(device=dev), write_outputs=False)
         s.run_round(11)
         s.run_round(12)          # attacker 41 poisons in round 12
         outs.append(s.global_state.clone())
-    assert _rel(outs[1], outs[0]) < 2e-2
+    if dtype == "fp32":
+        assert torch.equal(outs[1], outs[0])
+    else:
+        assert _rel(outs[1], outs[0]) < 2e-2
+
+
+@pytest.mark.parametrize("dtype,agg", [("fp32", "mean"), ("bf16", "mean"), ("fp32", "foolsgold")])
+def test_solo_tail_bitwise(dev, tmp_path, dtype, agg):
+    """The solo tail (the long attacker's last steps move from the G-replica graph to the
+    one-replica graph mid-wave, fl/trainer.py _solo_enter/_solo_leave) changes no bit: every
+    snapshot, the per-epoch stats and the FoolsGold gradient sums equal a run without it."""
+    from dba_mod_amd.fl.server import Server
+    from dba_mod_amd.parallel.dist import DistCtx
+    got = []
+    for solo in (0, 4):
+        p = _small_params(save_dir=str(tmp_path / f"s{solo}"), compute_dtype=dtype, aggregation_methods=agg)
+        s = Server(p, DistCtx(device=dev), write_outputs=False)
+        s.trainer.SOLO_MIN_STEPS = solo
+        st = s._train_begin(12)                     # attacker 41: 10 poison epochs vs 1 benign
+        if solo:
+            assert s.trainer._solo_tail(st["plan"].clients, max(len(c.steps) for c in st["plan"].clients))
+        got.append({r.name: r for r in st["handle"].collect()})
+    a, b = got
+    assert a.keys() == b.keys()
+    for name in a:
+        ra, rb = a[name], b[name]
+        assert ra.snapshots.keys() == rb.snapshots.keys()
+        for k in ra.snapshots:
+            assert torch.equal(ra.snapshots[k], rb.snapshots[k]), (name, k)
+        assert np.array_equal(ra.stats, rb.stats), name
+        if agg == "foolsgold":
+            assert torch.equal(ra.fg_grad, rb.fg_grad), name
+
+
+def test_fp32_eval_argmax_warm_model(dev, tmp_path):
+    """The fp32 eval forward (folded BN, fp16-pair split) on a WARM CIFAR model agrees with
+    plain torch-fp32 on the predicted class of >= 99.9 % of 1000 test images."""
+    from dba_mod_amd import ops
+    from dba_mod_amd.fl.server import Server
+    from dba_mod_amd.models import program as P
+    from dba_mod_amd.ops import hip, reference
+    from dba_mod_amd.parallel.dist import DistCtx
+    p = _cifar_small(tmp_path, pretrain_rounds=12, start_epoch=1, is_poison=False)
+    s = Server(p, DistCtx(device=dev), write_outputs=False)
+    spec = s.spec
+    bank = s.global_state[None].clone()
+    store = s.wl.test_store
+    n = min(1000, int(store.labels.numel()))
+    x = store.images[:n].to(dev).float().div(255.0)[None].contiguous()
+
+    def run(mod):
+        saved = {k: getattr(ops, k) for k in ops._OPS}
+        for k in ops._OPS:
+            setattr(ops, k, getattr(mod, k))
+        try:
+            ctx = P.Ctx(spec, None, None, torch.zeros(1, dtype=torch.int32, device=dev), train=False,
+                        folded=P.fold_bank(spec, bank, torch.float32), act_dtype=torch.float32)
+            return P.forward(ctx, x).float()
+        finally:
+            for k, v in saved.items():
+                setattr(ops, k, v)
+
+    oh, orf = run(hip), run(reference)
+    agree = (oh.argmax(-1) == orf.argmax(-1)).float().mean().item()
+    acc = (orf.argmax(-1)[0].cpu() == store.labels[:n].long().cpu()).float().mean().item()
+    assert acc > 0.3, acc                        # the model is warm (chance: 0.1)
+    assert agree >= 0.999, (agree, _rel(oh, orf))
+    assert _rel(oh, orf) < 1e-5
 
 
 @pytest.mark.parametrize("agg", ["mean", "geom_median", "foolsgold"])

@@ -490,18 +490,28 @@ def test_fp32_train_step_vs_fp64(H, R64, arch, shp):
     lh, gh, sh = run(H, dev, torch.float32, br.wrap(H))
     lh2, gh2, sh2 = run(H, dev, torch.float32)
     assert torch.equal(gh, gh2) and torch.equal(sh, sh2) and torch.equal(lh, lh2), "not bitwise reproducible"
-    br.replay = True
+    br.start_replay()
     lr_, gr, sr = run(R64, torch.device("cpu"), torch.float64, br.wrap(R64))
     assert br.i == len(br.rec)
-    # the same step in plain fp32 torch (CPU): deep nets at random init (ResNet-50) amplify
-    # fp32 rounding itself to ~1 %, so the bound is the larger of 1e-4 and 3x that band
+    # near-ties only, and only a tiny fraction of the decisions; nothing outside the tie band
+    # (a clearly wrong ReLU / max-pool decision of the kernels is NOT replayed, ops/branches.py)
+    assert br.flips <= 1e-4 * br.elements and br.hard == 0, (arch, br.flips, br.hard, br.elements)
+    # the same step in plain fp32 torch (CPU) under the same near-tie replay: like for like.
+    # Deep nets at random init (ResNet-50) amplify fp32 rounding itself to ~1 %, so the bound
+    # is the larger of 1e-4 and 3x that band
     R64.COMPUTE_DTYPE = torch.float32
-    _, g32, _ = run(R64, torch.device("cpu"), torch.float32)
+    br.start_replay()
+    _, g32, _ = run(R64, torch.device("cpu"), torch.float32, br.wrap(R64))
+    _, g32u, _ = run(R64, torch.device("cpu"), torch.float32)
     R64.COMPUTE_DTYPE = torch.float64
+    _, gu, _ = run(R64, torch.device("cpu"), torch.float64)   # fp64's own branches
     for g in range(2):
         assert abs(lh[g].item() - lr_[g].item()) < 1e-5 * max(1.0, abs(lr_[g].item())), (lh[g], lr_[g])
         e, band = _rel(gh[g], gr[g]), _rel(g32[g], gr[g])
         assert e < max(1e-4, 3 * band), (arch, g, e, band)
+        # unmatched (each run its own branches): a loose bound against torch-fp32's own
+        eu, bandu = _rel(gh[g], gu[g]), _rel(g32u[g], gu[g])
+        assert eu < max(1e-4, 10 * bandu), (arch, g, eu, bandu)
         if spec.B:
             assert _rel(sh[g, spec.P:], sr[g, spec.P:]) < 1e-5
     assert gh[2].abs().max().item() == 0.0          # inactive replica untouched
