@@ -267,6 +267,12 @@ class GroupTrainer:
         2-epoch clients finished) for at least SOLO_MIN_STEPS steps; graph mode, G > 1 only."""
         if not self.use_graph or len(clients) < 2 or self.SOLO_MIN_STEPS <= 0:
             return None
+        # only where it is bit-identical: the fp32 family decides every kernel parameter from
+        # the per-replica geometry; the bf16 family's split-K / tile choices depend on the
+        # launch's replica count, so moving a client to the one-replica graph would change its
+        # rounding (tests/test_gpu_e2e.py test_solo_tail_bitwise)
+        if self.dtype != torch.float32:
+            return None
         lens = sorted(((len(c.steps), g) for g, c in enumerate(clients)), reverse=True)
         (n0, g0), (n1, _) = lens[0], lens[1]
         if n0 != T or n0 - n1 < self.SOLO_MIN_STEPS:

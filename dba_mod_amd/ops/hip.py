@@ -87,6 +87,8 @@ _SIGS = {
     "dba_xwgrad_ws_floats": [_I] * 8 + [_P],
     "dba_xwgrad": [_P, _LL, _P, _LL, _P, _LL, _P] + [_I] * 12 + [_P, _I] * 2 + [_P, _LL, _I, _P],
     "dba_xwgrad_reduce_batch": [_P, _I, _I, _LL, _P],
+    # image stems in exact fp32 (csrc/kernels/stem.hip)
+    "dba_xstem_fwd": [_P, _LL, _P, _LL, _P, _P, _LL, _P, _P, _LL, _P] + [_I] * 13 + [_P, _I, _P, _P],
 }
 for _name, _args in _SIGS.items():
     _fn = getattr(_L, _name)
@@ -467,8 +469,22 @@ def _xconv_fwd(x, w, wsel, stride, pad, bias, residual, relu, nvalid, out_dtype,
         ax, aw = _amax_act(x, nvalid), _amax_w(w, ws, Cout * KH * KW * Cin)
         ay = _amax_out(y)   # the output's max, for its consumers
     part = None
-    if (bn_stats and _BN_FUSED_STATS and n == 0 and bias is None and res is None and not relu
-            and N * Ho * Wo > _BN_SMALL_ROWS):
+    want_part = (bn_stats and _BN_FUSED_STATS and bias is None and res is None and not relu
+                 and N * Ho * Wo > _BN_SMALL_ROWS)
+    if Cin <= 4 and out_dtype in (None, _F32):
+        # few-channel image stems: exact-fp32 direct conv (stem.hip), -100 = not a stem shape
+        if want_part:
+            nblk = (N * Ho * Wo + 31) // 32
+            part = torch.empty(G * Cout * 2 * nblk, dtype=torch.float64, device=x.device)
+        rc = _call("dba_xstem_fwd", x.data_ptr(), N * H * W * Cin, w.data_ptr(), ws, _ptr(_i32(wsel)), _ptr(bias), bs,
+                   _ptr(res), y.data_ptr(), N * Ho * Wo * Cout, _ptr(_i32(nvalid)), G, N, H, W, Cin, Ho, Wo, Cout,
+                   KH, KW, stride, pad, int(relu), *_aptr(ay), _ptr(part), _stream())
+        if rc != NOT_HANDLED:
+            if part is not None:
+                y._dba_bnpart = (part, nblk)
+            return y
+        part = None
+    if want_part and n == 0:
         nblk = (N * Ho * Wo + 31) // 32
         part = torch.empty(G * Cout * 2 * nblk, dtype=torch.float64, device=x.device)
         if os.environ.get("DBA_BN_FUSED_POISON") == "1":   # diagnostics: unwritten slots -> NaN

@@ -1,4 +1,5 @@
-"""Runs a few kernels on fixed shapes for rocprofv3 PMC counter collection: conv shapes and the
+"""Runs a few kernels on fixed shapes for rocprofv3 PMC counter collection: conv shapes (``f32:<shape>``:
+the fp32 family on a ``tools.bench_kernels`` shape) and the
 training BN forward / backward ``bn1``-``bn3`` (10 replicas x 64 images; ResNet stages 1-3:
 32x32 x 32, 16x16 x 64, 8x8 x 128 channels), as ``scripts/gpu/pmc_bn.sh`` profiles them."""
 from __future__ import annotations
@@ -31,6 +32,17 @@ def main() -> int:
             for _ in range(3):
                 out, mean, invstd = H.bn_train(y, gamma, beta, rm, rv, nv, 0.1, 1e-5, True, None)
                 H.bn_train_bwd(dout, y, out, mean, invstd, gamma, nv, True, dg, db)
+        elif name.startswith("f32:"):
+            # fp32-family forward of a bench_kernels shape (e.g. f32:eval.layer1), 3 calls
+            from dba_mod_amd.tools.bench_kernels import SHAPES
+            _, G, N, Hh, Cin, Cout, k, s, p = next(r for r in SHAPES if r[0] == name[4:])
+            H.set_fp32_planes(H.F16_PAIR)
+            x = torch.randn(G, N, Hh, Hh, Cin, device=dev)
+            w = torch.randn(G, Cout, k, k, Cin, device=dev) * 0.05
+            per = Cout * k * k * Cin
+            H.split_weights(w, per, per, H._amax_w(w, per, per))
+            for _ in range(3):
+                H.conv2d(x, w, None, s, p, relu=True)
         elif name.startswith("pconv"):
             G, N, Hh, C = (17, 1024, 32, 32) if name == "pconv1" else (17, 1024, 16, 64)
             x = torch.randn(G, N, Hh, Hh, C, device=dev).bfloat16()

@@ -146,7 +146,9 @@ def test_graph_replay_matches_eager(dev, tmp_path, dtype):
 def test_solo_tail_bitwise(dev, tmp_path, dtype, agg):
     """The solo tail (the long attacker's last steps move from the G-replica graph to the
     one-replica graph mid-wave, fl/trainer.py _solo_enter/_solo_leave) changes no bit: every
-    snapshot, the per-epoch stats and the FoolsGold gradient sums equal a run without it."""
+    snapshot, the per-epoch stats and the FoolsGold gradient sums equal a run without it.
+    The bf16 family picks split-K / tiles from the replica count, so it never takes the solo
+    tail (it would change the rounding): there both runs are the plain group graph."""
     from dba_mod_amd.fl.server import Server
     from dba_mod_amd.parallel.dist import DistCtx
     got = []
@@ -156,7 +158,8 @@ def test_solo_tail_bitwise(dev, tmp_path, dtype, agg):
         s.trainer.SOLO_MIN_STEPS = solo
         st = s._train_begin(12)                     # attacker 41: 10 poison epochs vs 1 benign
         if solo:
-            assert s.trainer._solo_tail(st["plan"].clients, max(len(c.steps) for c in st["plan"].clients))
+            engaged = s.trainer._solo_tail(st["plan"].clients, max(len(c.steps) for c in st["plan"].clients))
+            assert bool(engaged) == (dtype == "fp32")
         got.append({r.name: r for r in st["handle"].collect()})
     a, b = got
     assert a.keys() == b.keys()
