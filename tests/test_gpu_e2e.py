@@ -148,7 +148,8 @@ def test_solo_tail_bitwise(dev, tmp_path, dtype, agg):
     one-replica graph mid-wave, fl/trainer.py _solo_enter/_solo_leave) changes no bit: every
     snapshot, the per-epoch stats and the FoolsGold gradient sums equal a run without it.
     The bf16 family picks split-K / tiles from the replica count, so it never takes the solo
-    tail (it would change the rounding): there both runs are the plain group graph."""
+    tail (it would change the rounding), and its kernels use float atomics (not bitwise
+    run to run): there the test checks that the solo tail stays off."""
     from dba_mod_amd.fl.server import Server
     from dba_mod_amd.parallel.dist import DistCtx
     got = []
@@ -161,6 +162,8 @@ def test_solo_tail_bitwise(dev, tmp_path, dtype, agg):
             engaged = s.trainer._solo_tail(st["plan"].clients, max(len(c.steps) for c in st["plan"].clients))
             assert bool(engaged) == (dtype == "fp32")
         got.append({r.name: r for r in st["handle"].collect()})
+    if dtype != "fp32":
+        return
     a, b = got
     assert a.keys() == b.keys()
     for name in a:
