@@ -807,6 +807,209 @@ __global__ __launch_bounds__(256) void xhalo_kernel(const XArgs a) {
   if (a.amax_out) amax_fold(a.amax_out, a.amax_out_ld, g, vmax);
 }
 
+// ============================================================ persistent halo conv
+// Weight-stationary, persistent form of xhalo_kernel for the stage-1 shape (W 32, Cs 32,
+// Ncol 32, fp16 pair): the same per-element MFMA sequence (tap-major k-steps, plane products in
+// prod_pa/pb order) — identical bits — but
+//   * a block owns a contiguous run of (replica, image, row-tile) items and keeps its replica's
+//     split weights for ALL nine taps resident in LDS (36 KB, reloaded only when the run
+//     crosses into the next replica), instead of streaming them through a two-stage ring with a
+//     barrier per 32-deep k-step (xhalo_kernel: 9 barriers and 37 KB of weight traffic per
+//     128-pixel tile);
+//   * the next item's input patch is loaded into registers while the current item's 54 MFMAs
+//     per wave run (the patch load is the latency the per-tile kernel exposes every block);
+//   * consecutive row tiles of one image go to the same block, so the two halo rows a tile
+//     shares with its neighbour are L2 / L1 hits.
+// Weight LDS image: per plane, row n (output channel) holds its K = 288 fp16 in 36 16-B chunks,
+// chunk c at c ^ ((n >> 2) & 3): the B-fragment reads of a wave (32 rows, one k-chunk) hit 16
+// distinct bank slots per ds_read_b128 lane group (as lds_put's swizzle).  63 KB of LDS: two
+// blocks per CU.
+template <int TR, bool PRE>
+__global__ __launch_bounds__(256, 2) void xhalo_ws_kernel(const XArgs a, int G, int per_block) {
+  constexpr int W = 32, CS = 32, NC = 32, P = 2;
+  constexpr int BM = TR * W, PW = W + 2, PR = TR + 2, PP = PR * PW;
+  constexpr int CH = CS / 8, PATCH = PP * CH;              // uint4 per patch plane
+  constexpr int K = 9 * CS, KC = K / 8, WPL = NC * KC;     // weight chunks per row / plane
+  constexpr int TM = BM / 4, MI = TM / 32;                 // 4 waves stacked along M
+  constexpr int Q4 = CS / 4, NE = (PP * Q4 + 255) / 256;
+  static_assert(BM * NC <= P * PATCH * 4, "epilogue tile fits the patch");
+  __shared__ __attribute__((aligned(16))) uint4 wlds[P * WPL];
+  __shared__ __attribute__((aligned(16))) uint4 patch[P * PATCH];
+
+  const int tid = threadIdx.x, lane = tid & 63, wm = tid >> 6;
+  const int fr = lane & 31, hf = lane >> 5;
+  const int HT = a.Ho / TR;
+  const bool flip = a.dsg < 0;
+  int total = 0;
+  for (int gg = 0; gg < G; ++gg) total += valid_rows(a.nvalid, gg, a.N) * HT;
+  if (a.bnpart) {   // BN partials of the invalid images' 32-row groups are zeros (the finalize sums all)
+    const int HoWo = a.Ho * a.Wo;
+    for (int gg = 0; gg < G; ++gg) {
+      const int b0 = valid_rows(a.nvalid, gg, a.N) * HoWo / 32;
+      for (long long e = b0 * (long long)NC + blockIdx.x * 256LL + tid; e < (long long)a.bnpart_nblk * NC;
+           e += (long long)gridDim.x * 256) {
+        const int c = (int)(e % NC), b = (int)(e / NC);
+        double* p = a.bnpart + ((long long)gg * NC + c) * 2 * a.bnpart_nblk + b;
+        p[0] = 0.0;
+        p[a.bnpart_nblk] = 0.0;
+      }
+    }
+  }
+  int item = blockIdx.x * per_block;
+  const int end = min(total, item + per_block);
+  if (item >= end) return;
+
+  // item -> (g, img, h0): items are counted over the valid images of every replica in order
+  auto decode = [&](int it, int& g, int& img, int& h0) __attribute__((always_inline)) {
+    g = 0;
+    int base = 0;
+    for (;; ++g) {
+      const int n = valid_rows(a.nvalid, g, a.N) * HT;
+      if (it < base + n) break;
+      base += n;
+    }
+    const int r = it - base;
+    img = r / HT;
+    h0 = (r - img * HT) * TR;
+  };
+  float4 pv[NE];
+  auto patch_load = [&](int g, int img, int h0) __attribute__((always_inline)) {
+    const float* __restrict__ src = a.src + (long long)g * a.src_gstride;
+    const __amdgpu_buffer_rsrc_t rA = rsrc(src, (long long)a.N * a.Hs * a.Ws * CS * 4);
+#pragma unroll
+    for (int u = 0; u < NE; ++u) {
+      const int e = tid + 256 * u;
+      const int pp = e / Q4, q = e - pp * Q4;
+      const int pr = pp / PW, pc = pp - pr * PW;
+      const int h = h0 - 1 + pr, w = pc - 1;
+      const bool ok = e < PP * Q4 && (unsigned)h < (unsigned)a.Hs && (unsigned)w < (unsigned)a.Ws;
+      pv[u] = bload4(rA, ok ? (((img * a.Hs + h) * a.Ws + w) * CS + q * 4) * 4 : kOOB);
+    }
+  };
+  auto patch_put = [&](float ma) __attribute__((always_inline)) {
+#pragma unroll
+    for (int u = 0; u < NE; ++u) {
+      const int e = tid + 256 * u;
+      if (e >= PP * Q4) break;
+      const int pp = e / Q4, q = e - pp * Q4;
+      uint2 sp[P];
+      split4h(pv[u].x, pv[u].y, pv[u].z, pv[u].w, ma, sp);
+      const int o = pp * CH + ((q >> 1) ^ hswz<W, CS>(pp));
+#pragma unroll
+      for (int p = 0; p < P; ++p) ((uint2*)&patch[p * PATCH + o])[q & 1] = sp[p];
+    }
+  };
+  auto weights_put = [&](int slot, float mb) __attribute__((always_inline)) {
+    for (int e = tid; e < WPL; e += 256) {       // chunk e = row n, chunk c (8 k-elements)
+      const int n = e / KC, c = e - n * KC;
+      const int o = n * KC + (c ^ ((n >> 2) & 3));
+      if constexpr (PRE) {
+        const uint16_t* Bh = a.wp + (long long)slot * a.wp_sstride;
+        const uint4* ph = (const uint4*)(Bh + (long long)n * K + c * 8);
+        const uint4* pl = (const uint4*)(Bh + (a.wp_sstride >> 1) + (long long)n * K + c * 8);
+        wlds[o] = *ph;
+        wlds[WPL + o] = *pl;
+      } else {
+        const float* Bp = a.w + (long long)slot * a.w_sstride + (long long)n * K + c * 8;
+        const float4 x0 = ((const float4*)Bp)[0], x1 = ((const float4*)Bp)[1];
+        uint2 s0[2], s1[2];
+        split4h(x0.x, x0.y, x0.z, x0.w, mb, s0);
+        split4h(x1.x, x1.y, x1.z, x1.w, mb, s1);
+        wlds[o] = make_uint4(s0[0].x, s0[0].y, s1[0].x, s1[0].y);
+        wlds[WPL + o] = make_uint4(s0[1].x, s0[1].y, s1[1].x, s1[1].y);
+      }
+    }
+  };
+
+  int g, img, h0;
+  decode(item, g, img, h0);
+  patch_load(g, img, h0);
+  int cur_g = -1, slot = 0;
+  HScale hs;
+  float vmax = 0.f;
+  int apix[MI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i) {
+    const int m = wm * TM + i * 32 + fr;
+    apix[i] = (m / W) * PW + (m % W);
+  }
+  for (; item < end; ++item) {
+    if (g != cur_g) {
+      if (cur_g >= 0 && a.amax_out) {             // the previous replica's output max
+        amax_fold(a.amax_out, a.amax_out_ld, cur_g, vmax);
+        vmax = 0.f;
+      }
+      slot = a.wsel ? a.wsel[g] : g;
+      hs.init(amax_read(a.amax_src, a.amax_src_ld, g), amax_read(a.amax_w, a.amax_w_ld, slot));
+      __syncthreads();                            // previous weights no longer read
+      weights_put(slot, hs.mb);
+      cur_g = g;
+    }
+    patch_put(hs.ma);
+    __syncthreads();
+    const int ig = g, iimg = img, ih0 = h0;
+    if (item + 1 < end) {                         // next item's patch: in flight during the MFMAs
+      decode(item + 1, g, img, h0);
+      patch_load(g, img, h0);
+    }
+    f32x16_t acc[MI][1];
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][0][r] = 0.f;
+#pragma unroll 1
+    for (int tap = 0; tap < 9; ++tap) {
+      int ti = tap / 3, tj = tap - ti * 3;
+      if (flip) { ti = 2 - ti; tj = 2 - tj; }
+      const int toff = ti * PW + tj;
+      sfor<2>([&](auto KK) __attribute__((always_inline)) {
+        const int ch = decltype(KK)::value * 2 + hf;
+        uint4 af[P][MI], bfr[P][1];
+#pragma unroll
+        for (int i = 0; i < MI; ++i) {
+          const int pp = apix[i] + toff;
+          const int o = pp * CH + (ch ^ hswz<W, CS>(pp));
+#pragma unroll
+          for (int p = 0; p < P; ++p) af[p][i] = patch[p * PATCH + o];
+        }
+        const int ob = fr * KC + ((tap * 4 + ch) ^ ((fr >> 2) & 3));
+#pragma unroll
+        for (int p = 0; p < P; ++p) bfr[p][0] = wlds[p * WPL + ob];
+        mma_half<MI, 1, P, true, 0, decltype(KK)::value>(af, bfr, acc, [&](int) {});
+      });
+    }
+    hs.finish(acc);
+    __syncthreads();                              // patch reads done: reuse it as the tile
+    float* Ct = reinterpret_cast<float*>(patch);
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) Ct[(wm * TM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * hf) * NC + fr] = acc[i][0][r];
+    __syncthreads();
+    const int tm = iimg * HT + ih0 / TR;
+    if (a.bnpart) bn_tile_stats<BM, NC>(Ct, a.bnpart, a.bnpart_nblk, ig, NC, tm * BM, 0, false);
+    float* out = a.out + (long long)ig * a.out_gstride;
+    const float* bias = a.bias ? a.bias + (long long)slot * a.b_sstride : nullptr;
+    const float* res = a.res ? a.res + (long long)ig * a.out_gstride : nullptr;
+    constexpr int C4 = NC / 4;
+    for (int e = tid; e < BM * C4; e += 256) {
+      const int row = e / C4, cc = (e - row * C4) * 4;
+      const long long o = (((long long)iimg * a.Ho + ih0 + row / W) * a.Wo + row % W) * NC + cc;
+      float4 v = *(const float4*)&Ct[row * NC + cc];
+      if (bias) { v.x += bias[cc]; v.y += bias[cc + 1]; v.z += bias[cc + 2]; v.w += bias[cc + 3]; }
+      if (res) {
+        const float4 rv = *(const float4*)(res + o);
+        v.x += rv.x; v.y += rv.y; v.z += rv.z; v.w += rv.w;
+      }
+      if (a.relu) { v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f); }
+      vmax = fmaxf(vmax, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+      *(float4*)(out + o) = v;
+    }
+    __syncthreads();                              // tile consumed before the next patch_put
+  }
+  if (a.amax_out) amax_fold(a.amax_out, a.amax_out_ld, cur_g, vmax);
+}
+
 // sum of split-K slabs ws[z][g][m][n] (fixed z order) + bias (+ residual) (ReLU), valid rows
 __global__ __launch_bounds__(256) void xsplitk_reduce_kernel(const float* __restrict__ ws, int S, long long zstride,
                                                              long long gstride, const int* __restrict__ nvalid, int N,
@@ -1324,6 +1527,29 @@ int xhalo_go(const XArgs& a, int G, hipStream_t st) {
   DBA_LAUNCH_CHECK();
 }
 
+// persistent weight-stationary stage-1 halo conv: ~2 blocks per CU (DBA_F32_HALO_WS=0: off).
+// Items are (replica, image, 4-row tile); the grid never depends on G beyond the item count,
+// and every item computes the same bits as xhalo_kernel.
+int& halo_ws_on() {
+  static int on = env_int("DBA_F32_HALO_WS", 1);
+  return on;
+}
+int xhalo_ws_try(const XArgs& a, int G, hipStream_t st) {
+  static const int blocks = env_int("DBA_F32_HALO_WS_BLOCKS", 512);
+  if (!halo_ws_on() || a.Ho % 4 != 0) return -100;
+  if (a.wp && (((uintptr_t)a.wp & 15) || (a.wp_sstride % 8))) return -100;
+  // the item count: valid images of every replica (host view: nvalid lives on the device, so
+  // size the grid for all N images; blocks past the valid items return at once)
+  const long long total = (long long)G * a.N * (a.Ho / 4);
+  if (total >= (1LL << 31)) return -100;
+  const int nb = (int)std::max(1LL, std::min<long long>(blocks, total));
+  const int per = (int)((total + nb - 1) / nb);
+  const dim3 grid((unsigned)nb);
+  if (a.wp) hipLaunchKernelGGL((xhalo_ws_kernel<4, true>), grid, dim3(256), 0, st, a, G, per);
+  else hipLaunchKernelGGL((xhalo_ws_kernel<4, false>), grid, dim3(256), 0, st, a, G, per);
+  DBA_LAUNCH_CHECK();
+}
+
 // the halo kernel's shapes: 3x3 stride-1 pad-1 (fwd) or its stride-1 data gradient, one class,
 // square W 32, Cs 32, Ncol <= 32, aligned fp32 operands (DBA_F32_HALO=0 off)
 int xhalo_try(const XArgs& a, int G, int KH, int KW, hipStream_t st) {
@@ -1338,6 +1564,10 @@ int xhalo_try(const XArgs& a, int G, int KH, int KW, hipStream_t st) {
   static const bool big_ok = env_int("DBA_F32_HALO_BIG", 0) != 0;   // measured slower in the bench (profiles/r2_halo_tiles_ab.md)
   const bool big = big_ok && a.Ho % 8 == 0 && (long long)a.N * (a.Ho / 8) * G >= 1024;
   if (a.Wo == 32 && a.Cs == 32 && a.Ncol <= 32 && a.Ho % 4 == 0) {
+    if (a.amax_src && a.Ncol == 32) {
+      const int rc = xhalo_ws_try(a, G, st);
+      if (rc != -100) return rc;
+    }
     if (a.amax_src && big && !a.wp) return xhalo_go<32, 32, 256, 32, 4, 1, 2, true>(a, G, st);
     if (a.amax_src && a.wp) return xhalo_go<32, 32, 128, 32, 4, 1, 2, true, true>(a, G, st);
     if (a.amax_src) return xhalo_go<32, 32, 128, 32, 4, 1, 2, true>(a, G, st);
@@ -1434,6 +1664,13 @@ ClassGeom dgrad_classes(int H, int W, int Cin, int Cout, int KH, int KW, int s, 
 }
 
 }  // namespace
+
+// persistent weight-stationary stage-1 halo conv on / off (tests: bitwise A/B); returns the previous
+DBA_EXPORT int dba_xhalo_ws_set(int on) {
+  const int prev = halo_ws_on();
+  if (on >= 0) halo_ws_on() = on;
+  return prev;
+}
 
 DBA_EXPORT int dba_xgemm_set_planes(int p) {
   const int prev = planes();

@@ -77,6 +77,7 @@ _SIGS = {
     "dba_dist_loss_grad": [_P, _LL, _P, _LL, _P, _LL, _I, _P, _P, _F, _P, _P, _P],
     # reference-precision (fp32) family: csrc/kernels/xgemm.hip
     "dba_xgemm_set_planes": [_I],
+    "dba_xhalo_ws_set": [_I],
     "dba_xconv_ws_floats": [_I] * 8,
     "dba_xconv_fwd": [_P, _LL, _P, _LL, _P, _P, _LL, _P, _P, _LL, _P] + [_I] * 13 + [_P, _I] * 3 + [_P, _LL] * 2 + [_P, _P],
     "dba_bn_finalize_part": [_P, _I, _P, _I, _I, _I, _I, _P, _P, _LL, _F, _F, _P, _P, _P],
@@ -248,13 +249,14 @@ def set_gemm3_tiles(small: int = -1, big: int = -1) -> Tuple[int, int]:
 
 
 F16_PAIR = 16
-# which conv passes take the fp16 pair in F16_PAIR mode (DBA_F32_H_OPS; the others take 3 bf16
-# planes).  Training steps default to TRAIN_H_OPS: the forward convs stay on 3 bf16 planes (a
-# training step's error against fp64 is set by its forward — BN over a small batch amplifies
-# forward rounding ~1e4-fold — while the fp16 pair in the data / weight gradients leaves it at
-# the 3-plane level: tools/smoke.py), evaluation forwards use the pair (argmax counts).
+# which conv passes take the fp16 pair in F16_PAIR mode (DBA_F32_H_OPS / DBA_F32_TRAIN_H_OPS; the
+# others take 3 bf16 planes).  Every pass takes the pair by default: against the fp64 oracle
+# with the device's near-tie branches replayed (ops/branches.py), the smoke step's gradient error
+# is 1.63e-6 with the pair in the training forward vs 1.83e-6 with 3 bf16 planes there
+# (torch-fp32 under the same replay: 1.62e-6; profiles/split_policy_r3.md) — the 6-MFMA forward
+# of round 2 was chosen on an oracle without branch matching and buys nothing.
 _H_OPS = set(os.environ.get("DBA_F32_H_OPS", "fwd,dgrad,wgrad").split(","))
-TRAIN_H_OPS = tuple(os.environ.get("DBA_F32_TRAIN_H_OPS", "dgrad,wgrad").split(","))
+TRAIN_H_OPS = tuple(os.environ.get("DBA_F32_TRAIN_H_OPS", "fwd,dgrad,wgrad").split(","))
 
 
 def set_fp32_planes(planes: int) -> int:
@@ -268,6 +270,12 @@ def set_fp32_planes(planes: int) -> int:
     prev = int(_L.dba_xgemm_set_planes(int(planes)))
     _MODE = int(planes)
     return prev
+
+
+def set_halo_ws(on: int) -> int:
+    """Persistent weight-stationary stage-1 halo conv (xgemm.hip xhalo_ws_kernel) on / off;
+    -1 queries.  Returns the previous setting."""
+    return int(_L.dba_xhalo_ws_set(int(on)))
 
 
 def fp32_mode() -> int:

@@ -184,7 +184,10 @@ def test_fp32_eval_argmax_warm_model(dev, tmp_path):
     from dba_mod_amd.models import program as P
     from dba_mod_amd.ops import hip, reference
     from dba_mod_amd.parallel.dist import DistCtx
-    p = _cifar_small(tmp_path, pretrain_rounds=12, start_epoch=1, is_poison=False)
+    from dba_mod_amd import config as C
+    p = C.load_params(os.path.join(os.path.dirname(__file__), "..", "configs", "cifar_params.yaml"),
+                      {"resumed_model": False, "synthetic_data": True, "pretrain_rounds": 40, "start_epoch": 201,
+                       "save_dir": str(tmp_path), "is_poison": False})
     s = Server(p, DistCtx(device=dev), write_outputs=False)
     spec = s.spec
     bank = s.global_state[None].clone()
@@ -207,7 +210,7 @@ def test_fp32_eval_argmax_warm_model(dev, tmp_path):
     oh, orf = run(hip), run(reference)
     agree = (oh.argmax(-1) == orf.argmax(-1)).float().mean().item()
     acc = (orf.argmax(-1)[0].cpu() == store.labels[:n].long().cpu()).float().mean().item()
-    assert acc > 0.3, acc                        # the model is warm (chance: 0.1)
+    assert acc > 0.5, acc                        # the model is warm (chance: 0.1)
     assert agree >= 0.999, (agree, _rel(oh, orf))
     assert _rel(oh, orf) < 1e-5
 

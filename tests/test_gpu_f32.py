@@ -518,3 +518,69 @@ def test_fp32_train_step_vs_fp64(H, R64, arch, shp):
         if spec.B:
             assert _rel(sh[g, spec.P:], sr[g, spec.P:]) < 1e-5
     assert gh[2].abs().max().item() == 0.0          # inactive replica untouched
+
+
+@pytest.mark.parametrize("case", [CASES[1], CASES[15], (3, 9, 32, 32, 32, 32, 3, 1, 1)])
+@pytest.mark.parametrize("presplit", [False, True])
+def test_halo_ws_bitwise_vs_tiled(H, R64, case, presplit):
+    """The persistent weight-stationary stage-1 halo conv (xhalo_ws_kernel: weights resident in
+    LDS, next patch prefetched under the MFMAs) computes the same bits as the per-tile halo
+    kernel — forward (bias / residual / ReLU, partly valid replicas, a slot map), the stride-1
+    data gradient, and the fused BN statistics — and matches fp64 at fp32 level."""
+    prev = H.set_fp32_planes(16)
+    prev_ws = H.set_halo_ws(-1)
+    try:
+        dev = torch.device("cuda")
+        G, N, Hh, Ww, Cin, Cout, k, s, p = case
+        x, w, wsel, bias, nvalid, res, dy, acc = _inputs(case, dev)
+        if presplit:
+            per = Cout * k * k * Cin
+            H.split_weights(w, per, per, H._amax_w(w, per, per))
+        outs = []
+        for on in (1, 0):
+            H.set_halo_ws(on)
+            x2 = x.clone()   # fresh amax slots
+            y = H.conv2d(x2, w, wsel, s, p, bias=bias, residual=res, relu=True, nvalid=nvalid)
+            dx = H.conv2d_dgrad(dy, w, wsel, s, p, (Hh, Ww), nvalid=nvalid, accum=acc) if not presplit else None
+            outs.append((y, None, dx))
+        for g in range(G):
+            n = int(nvalid[g])
+            assert torch.equal(outs[0][0][g, :n], outs[1][0][g, :n]), (case, g, "fwd")
+            if outs[0][2] is not None:
+                assert torch.equal(outs[0][2][g, :n], outs[1][2][g, :n]), (case, g, "dgrad")
+        yr = R64.conv2d(_c(x), _c(w), wsel.cpu(), s, p, bias=_c(bias), residual=_c(res), relu=True)
+        for g in range(G):
+            n = int(nvalid[g])
+            assert _rel(outs[0][0][g, :n], yr[g, :n]) < 2e-6, (case, g)
+    finally:
+        H.set_halo_ws(prev_ws)
+        H.set_fp32_planes(prev)
+
+
+def test_halo_ws_bn_partials_bitwise(H):
+    """Training forward with fused BN statistics through the persistent halo conv: the fp64
+    partials (incl. the zeroed groups of invalid images) equal the per-tile kernel's."""
+    prev = H.set_fp32_planes(16)
+    prev_ws = H.set_halo_ws(-1)
+    try:
+        dev = torch.device("cuda")
+        g0 = torch.Generator().manual_seed(5)
+        G, N = 3, 12
+        x = torch.randn(G, N, 32, 32, 32, generator=g0).to(dev)
+        w = (torch.randn(G, 32, 3, 3, 32, generator=g0) * 0.06).to(dev)
+        nvalid = torch.tensor([N, 7, 0], dtype=torch.int32, device=dev)
+        parts = []
+        for on in (1, 0):
+            H.set_halo_ws(on)
+            y = H.conv2d(x.clone(), w, None, 1, 1, nvalid=nvalid, bn_stats=True)
+            part, nblk = y._dba_bnpart
+            parts.append((y, part.view(G, 32, 2, nblk).clone()))
+        (ya, pa), (yb, pb) = parts
+        for g in range(G):
+            n = int(nvalid[g])
+            assert torch.equal(ya[g, :n], yb[g, :n])
+        assert torch.equal(pa, pb)
+        assert pa[2].abs().max().item() == 0.0 and pa[1, :, :, 7 * 32:].abs().max().item() == 0.0
+    finally:
+        H.set_halo_ws(prev_ws)
+        H.set_fp32_planes(prev)
