@@ -81,3 +81,5 @@ def amax_arena(G: int, device: torch.device):
 
 
 __all__ = list(_OPS) + ["backend_for", "backend_name", "hip_module", "fp32_split", "train_h_ops", "amax_arena"]
+
+from . import library  # noqa: E402,F401  (torch.library registration of the dba:: ops)

@@ -436,3 +436,20 @@ def test_flat_aggregation_ops(H, R):
     for nn_, d in ((10, 2560), (37, 5000), (4, 207)):
         f = torch.randn(nn_, d, device=dev)
         _close(H.gram(f), R.gram(f), 1e-4, 1e-2, "gram")
+
+
+def test_torch_library_ops_run_hip():
+    """torch.ops.dba.* on GPU tensors dispatch to the HIP kernels (same bits as the direct
+    launcher call) — ops/library.py."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from dba_mod_amd.ops import hip as H
+    dev = torch.device("cuda")
+    g = torch.Generator().manual_seed(0)
+    x = torch.randn(2, 4, 16, 16, 32, generator=g).to(dev)
+    w = (torch.randn(2, 32, 3, 3, 32, generator=g) * 0.05).to(dev)
+    y = torch.ops.dba.conv2d(x, w, None, 1, 1, None, None, True, None)
+    assert torch.equal(y, H.conv2d(x, w, None, 1, 1, relu=True))
+    pts = torch.randn(5, 10000, generator=g).to(dev)
+    assert torch.equal(torch.ops.dba.gram(pts), H.gram(pts))
+    assert torch.equal(torch.ops.dba.sq_dists(pts, pts[0]), H.sq_dists(pts, pts[0]))
