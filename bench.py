@@ -231,6 +231,7 @@ def _run(args) -> int:
             "devices": devices,
             "rccl_ok": dctx.selfcheck_ok if dctx.backend == "nccl" else None,
             "collective_selfcheck_ok": dctx.selfcheck_ok,
+            "backend_repinned_cpu_affinity": dctx.affinity_changed,
             "comm_bytes_per_round": comm_mean,
             "ops_backend": ops.backend_name(dctx.device),
             "fp32_split": _split_label(server),

@@ -825,7 +825,7 @@ __global__ __launch_bounds__(256) void xhalo_kernel(const XArgs a) {
 // distinct bank slots per ds_read_b128 lane group (as lds_put's swizzle).  63 KB of LDS: two
 // blocks per CU.
 template <int TR, bool PRE>
-__global__ __launch_bounds__(256, 2) void xhalo_ws_kernel(const XArgs a, int G, int per_block) {
+__global__ __launch_bounds__(256, 2) void xhalo_ws_kernel(const XArgs a, int G) {
   constexpr int W = 32, CS = 32, NC = 32, P = 2;
   constexpr int BM = TR * W, PW = W + 2, PR = TR + 2, PP = PR * PW;
   constexpr int CH = CS / 8, PATCH = PP * CH;              // uint4 per patch plane
@@ -855,8 +855,10 @@ __global__ __launch_bounds__(256, 2) void xhalo_ws_kernel(const XArgs a, int G, 
       }
     }
   }
-  int item = blockIdx.x * per_block;
-  const int end = min(total, item + per_block);
+  // the valid items, split evenly over the grid (inactive replicas leave no idle blocks)
+  const int per = (total + gridDim.x - 1) / gridDim.x;
+  int item = blockIdx.x * per;
+  const int end = min(total, item + per);
   if (item >= end) return;
 
   // item -> (g, img, h0): items are counted over the valid images of every replica in order
@@ -1543,10 +1545,9 @@ int xhalo_ws_try(const XArgs& a, int G, hipStream_t st) {
   const long long total = (long long)G * a.N * (a.Ho / 4);
   if (total >= (1LL << 31)) return -100;
   const int nb = (int)std::max(1LL, std::min<long long>(blocks, total));
-  const int per = (int)((total + nb - 1) / nb);
   const dim3 grid((unsigned)nb);
-  if (a.wp) hipLaunchKernelGGL((xhalo_ws_kernel<4, true>), grid, dim3(256), 0, st, a, G, per);
-  else hipLaunchKernelGGL((xhalo_ws_kernel<4, false>), grid, dim3(256), 0, st, a, G, per);
+  if (a.wp) hipLaunchKernelGGL((xhalo_ws_kernel<4, true>), grid, dim3(256), 0, st, a, G);
+  else hipLaunchKernelGGL((xhalo_ws_kernel<4, false>), grid, dim3(256), 0, st, a, G);
   DBA_LAUNCH_CHECK();
 }
 

@@ -67,6 +67,7 @@ class DistCtx:
     emulated: bool = False          # rank R of an N-rank round, alone: collectives are no-ops
     selfcheck_ok: Optional[bool] = None   # init-time all-reduce self-check (None: no group)
     pg: bool = False                # a torch.distributed process group exists
+    affinity_changed: Optional[bool] = None   # the backend's init re-pinned the host thread
 
     @property
     def is_main(self) -> bool:
@@ -191,10 +192,19 @@ def init_distributed(prefer_gpu: bool = True, timeout_s: int = 1800) -> DistCtx:
               timeout=datetime.timedelta(seconds=timeout_s))
     if backend == "nccl":
         kw["device_id"] = device
+    # RCCL binds the initialising thread to the GPU's NUMA-local cores; inside a container
+    # whose cgroup CPU set does not match, that pins the one host thread that enqueues every
+    # kernel onto a few (shared) cores — measured: the 1-GPU bench with a world-1 RCCL group
+    # ran at 2.18 rounds/s vs 2.94 without (profiles/bench_r3_rccl_affinity.md).  Keep the
+    # affinity the process started with (DBA_KEEP_RCCL_AFFINITY=1 keeps RCCL's choice).
+    aff = os.sched_getaffinity(0) if hasattr(os, "sched_getaffinity") else None
     if not dist.is_initialized():
         dist.init_process_group(**kw)
     ctx = DistCtx(rank, world, dev_index, device, backend, pg=True)
     ctx.selfcheck_ok = selfcheck(ctx)
+    if aff is not None and os.environ.get("DBA_KEEP_RCCL_AFFINITY") != "1":
+        ctx.affinity_changed = os.sched_getaffinity(0) != aff
+        os.sched_setaffinity(0, aff)
     if not ctx.selfcheck_ok:
         raise RuntimeError(f"rank {rank}: {backend} all-reduce self-check failed (world {world})")
     return ctx
