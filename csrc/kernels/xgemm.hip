@@ -1529,11 +1529,14 @@ int xhalo_go(const XArgs& a, int G, hipStream_t st) {
   DBA_LAUNCH_CHECK();
 }
 
-// persistent weight-stationary stage-1 halo conv: ~2 blocks per CU (DBA_F32_HALO_WS=0: off).
+// persistent weight-stationary stage-1 halo conv: ~2 blocks per CU.  OFF by default
+// (DBA_F32_HALO_WS=1: on): alone it matches the per-tile kernel (eval.layer1 1504 vs 1509 us:
+// the layer is HBM-bound), but its long-lived blocks hold CUs the high-priority training stream
+// needs, so the overlapped round is slower (3.06 vs 3.20 rounds/s, profiles/halo_ws_r3.md).
 // Items are (replica, image, 4-row tile); the grid never depends on G beyond the item count,
 // and every item computes the same bits as xhalo_kernel.
 int& halo_ws_on() {
-  static int on = env_int("DBA_F32_HALO_WS", 1);
+  static int on = env_int("DBA_F32_HALO_WS", 0);
   return on;
 }
 int xhalo_ws_try(const XArgs& a, int G, hipStream_t st) {
