@@ -37,7 +37,7 @@ struct StemArgs {
   double* bnpart; int bnpart_nblk;          // [G][COUT][2][nblk] (optional)
 };
 
-template <int KH, int KW, int CIN, int COUT, int CPT>
+template <int KH, int KW, int CIN, int COUT, int CPT, int ITER>
 __global__ __launch_bounds__(256) void xstem_kernel(const StemArgs a) {
   constexpr int K = KH * KW * CIN;
   constexpr int TPP = COUT / CPT;            // threads per pixel
@@ -50,12 +50,12 @@ __global__ __launch_bounds__(256) void xstem_kernel(const StemArgs a) {
   const int tid = threadIdx.x;
   const int HoWo = a.Ho * a.Wo;
   const int Mv = valid_rows(a.nvalid, g, a.N) * HoWo;
-  const int m0 = blockIdx.x * PIX;
   const bool want_stats = a.bnpart != nullptr;
-  if (m0 >= Mv) {
+  const int mb = blockIdx.x * (ITER * PIX);
+  if (mb >= Mv) {   // no valid pixel in the block's tiles: zero BN partials only
     if (want_stats) {
-      for (int e = tid; e < (PIX / 32) * COUT; e += 256) {
-        const int grp = e / COUT, c = e - grp * COUT, b = m0 / 32 + grp;
+      for (int e = tid; e < ITER * (PIX / 32) * COUT; e += 256) {
+        const int grp = e / COUT, c = e - grp * COUT, b = mb / 32 + grp;
         if (b >= a.bnpart_nblk) continue;
         double* p = a.bnpart + ((long long)g * COUT + c) * 2 * a.bnpart_nblk + b;
         p[0] = 0.0;
@@ -66,86 +66,88 @@ __global__ __launch_bounds__(256) void xstem_kernel(const StemArgs a) {
   }
   const int slot = a.wsel ? a.wsel[g] : g;
   const float* __restrict__ wg = a.w + (long long)slot * a.w_sstride;
-  for (int e = tid; e < K * COUT; e += 256) {   // coalesced read, transposed LDS write
-    const int c = e / K, k = e - c * K;
-    wt[k * COUT + c] = wg[e];
+  for (int e = tid; e < K * COUT; e += 256) {   // conflict-free LDS writes (the reads hit L1)
+    const int k = e / COUT, c = e - k * COUT;
+    wt[e] = wg[c * K + k];
   }
   __syncthreads();
 
   const int pl = tid / TPP, cg = tid - pl * TPP;
-  const int m = m0 + pl;
-  const bool live = pl < PIX && m < Mv;
   const int c0 = cg * CPT;
-  float acc[CPT];
+  float vmax = 0.f;
+  const float* bp = a.bias ? a.bias + (long long)slot * a.b_sstride + c0 : nullptr;
+  for (int it = 0; it < ITER; ++it) {   // the weights in LDS serve ITER pixel tiles
+    const int m0 = mb + it * PIX;
+    const int m = m0 + pl;
+    const bool live = pl < PIX && m < Mv;
+    float acc[CPT];
 #pragma unroll
-  for (int c = 0; c < CPT; ++c) acc[c] = 0.f;
-  if (live) {
-    const int img = m / HoWo, rem = m - img * HoWo, p = rem / a.Wo, q = rem - p * a.Wo;
-    const float* __restrict__ xg = a.x + (long long)g * a.x_gstride + (long long)img * a.H * a.W * CIN;
-    const int h0 = p * a.stride - a.pad, w0 = q * a.stride - a.pad;
+    for (int c = 0; c < CPT; ++c) acc[c] = 0.f;
+    if (live) {
+      const int img = m / HoWo, rem = m - img * HoWo, p = rem / a.Wo, q = rem - p * a.Wo;
+      const float* __restrict__ xg = a.x + (long long)g * a.x_gstride + (long long)img * a.H * a.W * CIN;
+      const int h0 = p * a.stride - a.pad, w0 = q * a.stride - a.pad;
 #pragma unroll 1
-    for (int kh = 0; kh < KH; ++kh) {
-      const int h = h0 + kh;
-      const bool hok = (unsigned)h < (unsigned)a.H;
-      float xr[KW * CIN];
+      for (int kh = 0; kh < KH; ++kh) {
+        const int h = h0 + kh;
+        const bool hok = (unsigned)h < (unsigned)a.H;
+        float xr[KW * CIN];
 #pragma unroll
-      for (int kw = 0; kw < KW; ++kw) {
-        const int w = w0 + kw;
-        const bool ok = hok && (unsigned)w < (unsigned)a.W;
+        for (int kw = 0; kw < KW; ++kw) {
+          const int w = w0 + kw;
+          const bool ok = hok && (unsigned)w < (unsigned)a.W;
 #pragma unroll
-        for (int ci = 0; ci < CIN; ++ci) xr[kw * CIN + ci] = ok ? xg[((long long)h * a.W + w) * CIN + ci] : 0.f;
-      }
+          for (int ci = 0; ci < CIN; ++ci) xr[kw * CIN + ci] = ok ? xg[((long long)h * a.W + w) * CIN + ci] : 0.f;
+        }
 #pragma unroll
-      for (int j = 0; j < KW * CIN; ++j) {
-        const float4* wr = (const float4*)&wt[(kh * KW * CIN + j) * COUT + c0];
+        for (int j = 0; j < KW * CIN; ++j) {
+          const float4* wr = (const float4*)&wt[(kh * KW * CIN + j) * COUT + c0];
 #pragma unroll
-        for (int c4 = 0; c4 < CPT / 4; ++c4) {
-          const float4 wv = wr[c4];
-          acc[c4 * 4 + 0] = fmaf(wv.x, xr[j], acc[c4 * 4 + 0]);
-          acc[c4 * 4 + 1] = fmaf(wv.y, xr[j], acc[c4 * 4 + 1]);
-          acc[c4 * 4 + 2] = fmaf(wv.z, xr[j], acc[c4 * 4 + 2]);
-          acc[c4 * 4 + 3] = fmaf(wv.w, xr[j], acc[c4 * 4 + 3]);
+          for (int c4 = 0; c4 < CPT / 4; ++c4) {
+            const float4 wv = wr[c4];
+            acc[c4 * 4 + 0] = fmaf(wv.x, xr[j], acc[c4 * 4 + 0]);
+            acc[c4 * 4 + 1] = fmaf(wv.y, xr[j], acc[c4 * 4 + 1]);
+            acc[c4 * 4 + 2] = fmaf(wv.z, xr[j], acc[c4 * 4 + 2]);
+            acc[c4 * 4 + 3] = fmaf(wv.w, xr[j], acc[c4 * 4 + 3]);
+          }
         }
       }
-    }
-  }
-  float vmax = 0.f;
-  if (live) {
-    const long long o = (long long)g * a.out_gstride + (long long)m * COUT + c0;
-    const float* bp = a.bias ? a.bias + (long long)slot * a.b_sstride + c0 : nullptr;
+      const long long o = (long long)g * a.out_gstride + (long long)m * COUT + c0;
 #pragma unroll
-    for (int c4 = 0; c4 < CPT / 4; ++c4) {
-      float4 v = make_float4(acc[c4 * 4], acc[c4 * 4 + 1], acc[c4 * 4 + 2], acc[c4 * 4 + 3]);
-      if (bp) { v.x += bp[c4 * 4]; v.y += bp[c4 * 4 + 1]; v.z += bp[c4 * 4 + 2]; v.w += bp[c4 * 4 + 3]; }
-      if (a.res) {
-        const float4 r = *(const float4*)(a.res + o + c4 * 4);
-        v.x += r.x; v.y += r.y; v.z += r.z; v.w += r.w;
+      for (int c4 = 0; c4 < CPT / 4; ++c4) {
+        float4 v = make_float4(acc[c4 * 4], acc[c4 * 4 + 1], acc[c4 * 4 + 2], acc[c4 * 4 + 3]);
+        if (bp) { v.x += bp[c4 * 4]; v.y += bp[c4 * 4 + 1]; v.z += bp[c4 * 4 + 2]; v.w += bp[c4 * 4 + 3]; }
+        if (a.res) {
+          const float4 r = *(const float4*)(a.res + o + c4 * 4);
+          v.x += r.x; v.y += r.y; v.z += r.z; v.w += r.w;
+        }
+        if (a.relu) { v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f); }
+        vmax = fmaxf(vmax, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+        *(float4*)(a.out + o + c4 * 4) = v;
+        acc[c4 * 4] = v.x; acc[c4 * 4 + 1] = v.y; acc[c4 * 4 + 2] = v.z; acc[c4 * 4 + 3] = v.w;
       }
-      if (a.relu) { v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f); }
-      vmax = fmaxf(vmax, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
-      *(float4*)(a.out + o + c4 * 4) = v;
-      acc[c4 * 4] = v.x; acc[c4 * 4 + 1] = v.y; acc[c4 * 4 + 2] = v.z; acc[c4 * 4 + 3] = v.w;
     }
-  }
-  if (want_stats) {   // statistics of the raw output (bnpart implies no bias / residual / ReLU)
-    if (pl < PIX) {
+    if (want_stats) {   // statistics of the raw output (bnpart implies no bias / residual / ReLU)
+      if (pl < PIX) {
 #pragma unroll
-      for (int c = 0; c < CPT; ++c) tile[pl * COUT + c0 + c] = live ? acc[c] : 0.f;
-    }
-    __syncthreads();
-    for (int e = tid; e < (PIX / 32) * COUT; e += 256) {
-      const int grp = e / COUT, c = e - grp * COUT, b = m0 / 32 + grp;
-      if (b >= a.bnpart_nblk) continue;
-      double s0 = 0.0, s1 = 0.0;
+        for (int c = 0; c < CPT; ++c) tile[pl * COUT + c0 + c] = live ? acc[c] : 0.f;
+      }
+      __syncthreads();
+      for (int e = tid; e < (PIX / 32) * COUT; e += 256) {
+        const int grp = e / COUT, c = e - grp * COUT, b = m0 / 32 + grp;
+        if (b >= a.bnpart_nblk) continue;
+        double s0 = 0.0, s1 = 0.0;
 #pragma unroll 8
-      for (int r = 0; r < 32; ++r) {
-        const double v = (double)tile[(grp * 32 + r) * COUT + c];
-        s0 += v;
-        s1 = fma(v, v, s1);
+        for (int r = 0; r < 32; ++r) {
+          const double v = (double)tile[(grp * 32 + r) * COUT + c];
+          s0 += v;
+          s1 = fma(v, v, s1);
+        }
+        double* pp = a.bnpart + ((long long)g * COUT + c) * 2 * a.bnpart_nblk + b;
+        pp[0] = s0;
+        pp[a.bnpart_nblk] = s1;
       }
-      double* pp = a.bnpart + ((long long)g * COUT + c) * 2 * a.bnpart_nblk + b;
-      pp[0] = s0;
-      pp[a.bnpart_nblk] = s1;
+      __syncthreads();
     }
   }
   if (a.amax_out) amax_fold(a.amax_out, a.amax_ld, g, vmax);
@@ -154,10 +156,11 @@ __global__ __launch_bounds__(256) void xstem_kernel(const StemArgs a) {
 template <int KH, int KW, int CIN, int COUT, int CPT>
 int stem_go(const StemArgs& a, int G, hipStream_t st) {
   constexpr int PIX = 256 / (COUT / CPT);
+  constexpr int ITER = 4;   // pixel tiles per block: one weight load (LDS transpose) per 4 tiles
   if (a.bnpart && PIX % 32 != 0) return -100;
   const long long M = (long long)a.N * a.Ho * a.Wo;
-  const dim3 grid((unsigned)ceil_div(M, PIX), G);
-  hipLaunchKernelGGL((xstem_kernel<KH, KW, CIN, COUT, CPT>), grid, dim3(256), 0, st, a);
+  const dim3 grid((unsigned)ceil_div(M, PIX * ITER), G);
+  hipLaunchKernelGGL((xstem_kernel<KH, KW, CIN, COUT, CPT, ITER>), grid, dim3(256), 0, st, a);
   DBA_LAUNCH_CHECK();
 }
 

@@ -585,10 +585,18 @@ __global__ __launch_bounds__(256) void xconv_kernel(const XArgs a) {
 // weights stream through the same two-stage register/LDS pipeline as in xconv_kernel; the
 // k-step order (tap-major, 32 channels per step) and the MFMA sequence per output element are
 // the same, so both kernels compute identical bits.
+// Patch image: pixel pp (patch column c = pp % (W + 2)) holds CH 16-B chunks, chunk q at
+// q ^ hswz.  CH 4 (Cs 32): swizzle by pixel, (pp >> 2) & 3 — conflict-free.  CH 8 (Cs 64,
+// 128 B per pixel, two pixels per 256-B bank row): a ds_read_b128 lane group of a wave reads
+// 8 pixels of one patch row (columns c0+{0..3, 12..15}) and 8 of the next (c0+{4..11}), or the
+// mirror image; the bank slot is 8 * (c & 1) + (q ^ swz) & 7, and swz = (c >> 1) & 7 maps those
+// 16 pixels to 16 distinct slots for every tap column c0 (the former (pp >> 1) & 7 put pixels
+// 16 apart on one slot: 2-way conflicts on ~29 % of the LDS cycles, profiles/pmc_eval_r3.md).
 template <int W, int CS>
-__device__ __forceinline__ int hswz(int pp) {
+__device__ __forceinline__ int hswz(int pp, int col) {
   constexpr int CH = CS / 8;                    // 16-B chunks per pixel (4 or 8)
-  return (pp >> (CH == 4 ? 2 : 1)) & (CH - 1);
+  if constexpr (CH == 4) return (pp >> 2) & 3;
+  else return (col >> 1) & 7;
 }
 
 template <int W, int CS, int BM, int BN, int WM, int WN, int P, bool H, bool PRE = false>
@@ -657,7 +665,7 @@ __global__ __launch_bounds__(256) void xhalo_kernel(const XArgs a) {
       uint2 sp[P];
       if constexpr (H) split4h(pv[u].x, pv[u].y, pv[u].z, pv[u].w, hs.ma, sp);
       else split4<P>(pv[u].x, pv[u].y, pv[u].z, pv[u].w, sp);
-      const int o = pp * CH + ((q >> 1) ^ hswz<W, CS>(pp));
+      const int o = pp * CH + ((q >> 1) ^ hswz<W, CS>(pp, pp % PW));
 #pragma unroll
       for (int p = 0; p < P; ++p) ((uint2*)&patch[p * PATCH + o])[q & 1] = sp[p];
     }
@@ -714,11 +722,12 @@ __global__ __launch_bounds__(256) void xhalo_kernel(const XArgs a) {
 
   const int fr = lane & 31, hf = lane >> 5;
   // patch pixel of each A fragment row at tap offset (0, 0)
-  int apix[MI];
+  int apix[MI], acol[MI];
 #pragma unroll
   for (int i = 0; i < MI; ++i) {
     const int m = wm * TM + i * 32 + fr;
     apix[i] = (m / W) * PW + (m % W);
+    acol[i] = m % W;
   }
   auto mma = [&](int t, int buf, int stn) __attribute__((always_inline)) {
     const int tap = t / CB, cb = t - tap * CB;
@@ -732,7 +741,7 @@ __global__ __launch_bounds__(256) void xhalo_kernel(const XArgs a) {
 #pragma unroll
       for (int i = 0; i < MI; ++i) {
         const int pp = apix[i] + toff;
-        const int o = pp * CH + ((cb * 4 + ch) ^ hswz<W, CS>(pp));
+        const int o = pp * CH + ((cb * 4 + ch) ^ hswz<W, CS>(pp, acol[i] + tj));
 #pragma unroll
         for (int p = 0; p < P; ++p) af[p][i] = patch[p * PATCH + o];
       }
@@ -896,7 +905,7 @@ __global__ __launch_bounds__(256, 2) void xhalo_ws_kernel(const XArgs a, int G) 
       const int pp = e / Q4, q = e - pp * Q4;
       uint2 sp[P];
       split4h(pv[u].x, pv[u].y, pv[u].z, pv[u].w, ma, sp);
-      const int o = pp * CH + ((q >> 1) ^ hswz<W, CS>(pp));
+      const int o = pp * CH + ((q >> 1) ^ hswz<W, CS>(pp, pp % PW));
 #pragma unroll
       for (int p = 0; p < P; ++p) ((uint2*)&patch[p * PATCH + o])[q & 1] = sp[p];
     }
@@ -970,7 +979,7 @@ __global__ __launch_bounds__(256, 2) void xhalo_ws_kernel(const XArgs a, int G) 
 #pragma unroll
         for (int i = 0; i < MI; ++i) {
           const int pp = apix[i] + toff;
-          const int o = pp * CH + (ch ^ hswz<W, CS>(pp));
+          const int o = pp * CH + (ch ^ hswz<W, CS>(pp, 0));
 #pragma unroll
           for (int p = 0; p < P; ++p) af[p][i] = patch[p * PATCH + o];
         }

@@ -16,8 +16,8 @@ from collections import defaultdict
 
 
 def _short(name: str) -> str:
-    name = name.split("(")[0]
-    return name.replace("(anonymous namespace)::", "")[:90]
+    name = name.replace("(anonymous namespace)::", "").replace("void ", "")
+    return name.split("(")[0][:90]
 
 
 def main(argv=None) -> int:
@@ -34,7 +34,7 @@ def main(argv=None) -> int:
     for f in glob.glob(os.path.join(a.dir, "**", "*kernel_trace.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
             k = _short(r.get("Kernel_Name", ""))
-            if a.match in k:
+            if a.match in k and "Kernel_Name" in r:
                 vals[k]["dur_us"].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
     cols = sorted({c for v in vals.values() for c in v})
     print("| kernel | " + " | ".join(cols) + " |")
