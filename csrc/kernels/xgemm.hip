@@ -102,8 +102,8 @@ __device__ __forceinline__ int hexp(int maxbits) { return min(kSMax, 141 - (maxb
 struct HScale {
   float ma = 1.f, mb = 1.f;   // fill multipliers 2^sa, 2^sb
   int s = 0;                  // the accumulators hold sum * 2^s
-  __device__ __forceinline__ void init(int maxa, int maxb) {
-    const int sa = hexp(maxa), sb = hexp(maxb);
+  __device__ __forceinline__ void init(int maxa, int maxb, const int* sexp_a = nullptr, int g = 0) {
+    const int sa = sexp_a ? sexp_a[g] : hexp(maxa), sb = hexp(maxb);
     ma = __uint_as_float((uint32_t)(sa + 127) << 23);
     mb = __uint_as_float((uint32_t)(sb + 127) << 23);
     s = sa + sb;
@@ -117,6 +117,30 @@ struct HScale {
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[i][j][r] = ldexpf(acc[i][j][r], -s);
   }
+};
+
+// ---- fp16-pair activations (evaluation forwards).  A conv output that only feeds other convs
+// is stored in the split form its consumer needs: every 4 consecutive channels as 16 B =
+// 4 fp16 hi + 4 fp16 lo of x * 2^s (split4h), the same 4 bytes per element as fp32.  The
+// consumer's A staging then only moves bits (no per-tap re-split: the VALU that co-bounds the
+// MFMA in the implicit GEMM, profiles/pmc_eval_r3.md) and a residual read decodes hi + lo.
+// The scale is fixed before the producer runs, from a BOUND of its output: |y| <= L1max(w) *
+// max|x| + max|b| + max|res| (weights' max row L1 per slot from the eval fold, the input's and
+// the residual's max from their producers' amax slots); 2 * bound * 2^s in [2^14, 2^15), so
+// nothing overflows, and an element's absolute error stays below bound * 2^-38 (fp16 subnormal
+// lo planes) or 2^-22 relative — under one fp32 ulp of the tensor's max while the bound is
+// within 2^14 of it.  Every block computes the same s; each writes it to out_sexp[g].
+struct PairAct {
+  __device__ __forceinline__ static float4 decode(uint4 u, float inv) {
+    const f32x2v h0 = unpkh(u.x), h1 = unpkh(u.y), l0 = unpkh(u.z), l1 = unpkh(u.w);
+    return make_float4((h0.x + l0.x) * inv, (h0.y + l0.y) * inv, (h1.x + l1.x) * inv, (h1.y + l1.y) * inv);
+  }
+  __device__ __forceinline__ static uint4 encode(float4 v, float m) {
+    uint2 sp[2];
+    split4h(v.x, v.y, v.z, v.w, m, sp);
+    return make_uint4(sp[0].x, sp[0].y, sp[1].x, sp[1].y);
+  }
+  __device__ __forceinline__ static float mul(int s) { return __uint_as_float((uint32_t)(s + 127) << 23); }
 };
 
 // LDS images: per plane, rows of 32 reduction elements (64 B = 4 x 16-B chunks).  A row's
@@ -259,8 +283,26 @@ struct XArgs {
   long long wp_sstride;                      //    2 planes of wp_sstride/2 fp16, scaled like amax_w
   double* bnpart;                            // optional: BN statistics of the output (bn_tile_stats)
   int bnpart_nblk;                           //    32-row groups per replica
+  // fp16-pair activations (PairAct below): the A operand arrives pre-split (in_sexp: its
+  // per-replica scale exponent), the output leaves pre-split (out_sexp: written per replica;
+  // bound: per weight slot {max row L1 of w, max |bias|}; amax_res: the residual's max), the
+  // residual arrives pre-split (res_sexp)
+  const int* in_sexp;
+  int* out_sexp;
+  const float* bound;
+  const int* amax_res; int amax_res_ld;
+  const int* res_sexp;
   XClass cls[4];
 };
+
+// fp16-pair output exponent of replica g (slot: its weight slot; PairAct); every lane of the
+// wave calls it (amax_read)
+__device__ __forceinline__ int pair_out_exp(const XArgs& a, int g, int slot) {
+  const float ax = __int_as_float(amax_read(a.amax_src, a.amax_src_ld, g));
+  const float ar = a.amax_res ? __int_as_float(amax_read(a.amax_res, a.amax_res_ld, g)) : 0.f;
+  const float b = a.bound[2 * slot] * ax + a.bound[2 * slot + 1] + ar;
+  return hexp(__float_as_int(2.f * b));
+}
 
 // Training-BN statistics of a conv's output, folded into its epilogue (the separate BN
 // reduce pass over y is gone): for every 32-row group of GEMM rows (pixels) of the tile
@@ -295,10 +337,11 @@ __device__ __forceinline__ void bn_tile_stats(const float* Ct, double* __restric
   }
 }
 
-template <int BM, int BN, int WM, int WN, int P, int VEC, bool H, bool PW = false>
+template <int BM, int BN, int WM, int WN, int P, int VEC, bool H, bool PW = false, bool PA = false>
 __global__ __launch_bounds__(256) void xconv_kernel(const XArgs a) {
   static_assert(!H || P == 2, "fp16 split: 2 planes");
   static_assert(!PW || (H && VEC >= 4), "pre-split weights: fp16 pair, vector loads");
+  static_assert(!PA || (PW && VEC >= 4), "pre-split activations (PairAct): with pre-split weights");
   constexpr int TM = BM / WM, TN = BN / WN, MI = TM / 32, NJ = TN / 32;
   static_assert(WM * WN == 4 && MI >= 1 && NJ >= 1, "wave tiling");
   constexpr int ROWS = BM + BN, PL = ROWS * 4;   // uint4 per plane image
@@ -460,13 +503,21 @@ __global__ __launch_bounds__(256) void xconv_kernel(const XArgs a) {
   };
   // quarter q of stage st -> LDS buffer buf
   HScale hs;
-  if constexpr (H) hs.init(amax_read(a.amax_src, a.amax_src_ld, g), amax_read(a.amax_w, a.amax_w_ld, slot));
+  if constexpr (H)
+    hs.init(amax_read(a.amax_src, a.amax_src_ld, g), amax_read(a.amax_w, a.amax_w_ld, slot), PA ? a.in_sexp : nullptr, g);
   auto lput_q = [&](int buf, int st, int q) __attribute__((always_inline)) {
     uint4* L = lds + buf * P * PL;
     uint2 sp[P];
     if (q < RA) {
-      if constexpr (H) split4h(ra[st][q].x, ra[st][q].y, ra[st][q].z, ra[st][q].w, hs.ma, sp);
-      else split4<P>(ra[st][q].x, ra[st][q].y, ra[st][q].z, ra[st][q].w, sp);
+      if constexpr (PA) {   // pre-split activations: the loaded bits are {4 hi, 4 lo}
+        const uint4 u = __builtin_bit_cast(uint4, ra[st][q]);
+        sp[0] = make_uint2(u.x, u.y);
+        sp[1] = make_uint2(u.z, u.w);
+      } else if constexpr (H) {
+        split4h(ra[st][q].x, ra[st][q].y, ra[st][q].z, ra[st][q].w, hs.ma, sp);
+      } else {
+        split4<P>(ra[st][q].x, ra[st][q].y, ra[st][q].z, ra[st][q].w, sp);
+      }
       lds_put<P, false, BM>(L, PL, 0, r0 + 32 * q, kq, sp);
     } else {
       const int j = q - RA;
@@ -544,6 +595,14 @@ __global__ __launch_bounds__(256) void xconv_kernel(const XArgs a) {
   float vmax = 0.f;
   if ((a.Ncol & 3) == 0) {
     constexpr int C4 = BN / 4;
+    // fp16-pair residual / output (PairAct): block-uniform scales
+    const float rinv = (res && a.res_sexp) ? PairAct::mul(-a.res_sexp[g]) : 0.f;
+    int so = 0;
+    if (fin && a.out_sexp) {
+      so = pair_out_exp(a, g, slot);
+      if (tid == 0) a.out_sexp[g] = so;
+    }
+    const float omul = PairAct::mul(so);
     for (int e = tid; e < BM * C4; e += 256) {
       const int row = e / C4, cc = (e - row * C4) * 4;
       const int n = n0 + cc;
@@ -552,12 +611,14 @@ __global__ __launch_bounds__(256) void xconv_kernel(const XArgs a) {
       float4 v = *(const float4*)&Ct[row * BN + cc];
       if (bias) { v.x += bias[n]; v.y += bias[n + 1]; v.z += bias[n + 2]; v.w += bias[n + 3]; }
       if (res) {
-        const float4 rv = *(const float4*)(res + o + n);
+        const float4 rv = a.res_sexp ? PairAct::decode(*(const uint4*)(res + o + n), rinv)
+                                     : *(const float4*)(res + o + n);
         v.x += rv.x; v.y += rv.y; v.z += rv.z; v.w += rv.w;
       }
       if (relu) { v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f); }
       vmax = fmaxf(vmax, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
-      *(float4*)(out + o + n) = v;
+      if (fin && a.out_sexp) *(uint4*)(out + o + n) = PairAct::encode(v, omul);
+      else *(float4*)(out + o + n) = v;
     }
   } else {
     for (int e = tid; e < BM * BN; e += 256) {
@@ -599,10 +660,11 @@ __device__ __forceinline__ int hswz(int pp, int col) {
   else return (col >> 1) & 7;
 }
 
-template <int W, int CS, int BM, int BN, int WM, int WN, int P, bool H, bool PRE = false>
+template <int W, int CS, int BM, int BN, int WM, int WN, int P, bool H, bool PRE = false, bool PA = false>
 __global__ __launch_bounds__(256) void xhalo_kernel(const XArgs a) {
   static_assert(!H || P == 2, "fp16 split: 2 planes");
   static_assert(!PRE || H, "pre-split weights: fp16 pair");
+  static_assert(!PA || PRE, "pre-split activations (PairAct): with pre-split weights");
   constexpr int TR = BM / W, PW = W + 2, PR = TR + 2, PP = PR * PW;
   constexpr int CH = CS / 8, PATCH = PP * CH;             // uint4 per plane
   constexpr int TM = BM / WM, TN = BN / WN, MI = TM / 32, NJ = TN / 32;
@@ -655,7 +717,8 @@ __global__ __launch_bounds__(256) void xhalo_kernel(const XArgs a) {
     }
   }
   HScale hs;
-  if constexpr (H) hs.init(amax_read(a.amax_src, a.amax_src_ld, g), amax_read(a.amax_w, a.amax_w_ld, slot));
+  if constexpr (H)
+    hs.init(amax_read(a.amax_src, a.amax_src_ld, g), amax_read(a.amax_w, a.amax_w_ld, slot), PA ? a.in_sexp : nullptr, g);
   auto patch_put = [&]() __attribute__((always_inline)) {
 #pragma unroll
     for (int u = 0; u < NE; ++u) {
@@ -663,8 +726,15 @@ __global__ __launch_bounds__(256) void xhalo_kernel(const XArgs a) {
       if (e >= PP * Q4) break;
       const int pp = e / Q4, q = e - pp * Q4;
       uint2 sp[P];
-      if constexpr (H) split4h(pv[u].x, pv[u].y, pv[u].z, pv[u].w, hs.ma, sp);
-      else split4<P>(pv[u].x, pv[u].y, pv[u].z, pv[u].w, sp);
+      if constexpr (PA) {   // pre-split activations: the loaded bits are {4 hi, 4 lo}
+        const uint4 uu = __builtin_bit_cast(uint4, pv[u]);
+        sp[0] = make_uint2(uu.x, uu.y);
+        sp[1] = make_uint2(uu.z, uu.w);
+      } else if constexpr (H) {
+        split4h(pv[u].x, pv[u].y, pv[u].z, pv[u].w, hs.ma, sp);
+      } else {
+        split4<P>(pv[u].x, pv[u].y, pv[u].z, pv[u].w, sp);
+      }
       const int o = pp * CH + ((q >> 1) ^ hswz<W, CS>(pp, pp % PW));
 #pragma unroll
       for (int p = 0; p < P; ++p) ((uint2*)&patch[p * PATCH + o])[q & 1] = sp[p];
@@ -798,6 +868,13 @@ __global__ __launch_bounds__(256) void xhalo_kernel(const XArgs a) {
   const float* res = a.res ? a.res + (long long)g * a.out_gstride : nullptr;
   constexpr int C4 = BN / 4;
   float vmax = 0.f;
+  const float rinv = (res && a.res_sexp) ? PairAct::mul(-a.res_sexp[g]) : 0.f;
+  int so = 0;
+  if (a.out_sexp) {
+    so = pair_out_exp(a, g, slot);
+    if (tid == 0) a.out_sexp[g] = so;
+  }
+  const float omul = PairAct::mul(so);
   for (int e = tid; e < BM * C4; e += 256) {
     const int row = e / C4, cc = (e - row * C4) * 4;
     const int n = n0 + cc;
@@ -806,12 +883,14 @@ __global__ __launch_bounds__(256) void xhalo_kernel(const XArgs a) {
     float4 v = *(const float4*)&Ct[row * BN + cc];
     if (bias) { v.x += bias[n]; v.y += bias[n + 1]; v.z += bias[n + 2]; v.w += bias[n + 3]; }
     if (res) {
-      const float4 rv = *(const float4*)(res + o + n);
+      const float4 rv = a.res_sexp ? PairAct::decode(*(const uint4*)(res + o + n), rinv)
+                                   : *(const float4*)(res + o + n);
       v.x += rv.x; v.y += rv.y; v.z += rv.z; v.w += rv.w;
     }
     if (a.relu) { v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f); }
     vmax = fmaxf(vmax, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
-    *(float4*)(out + o + n) = v;
+    if (a.out_sexp) *(uint4*)(out + o + n) = PairAct::encode(v, omul);
+    else *(float4*)(out + o + n) = v;
   }
   if (a.amax_out) amax_fold(a.amax_out, a.amax_out_ld, g, vmax);
 }
@@ -1429,6 +1508,38 @@ __global__ __launch_bounds__(256) void xsplit_w_kernel(const float* __restrict__
   }
 }
 
+// output bound of an evaluation conv per weight slot (PairAct): out[slot] = {max over rows of
+// sum |w[row][k]|, max |bias|}.  One block per slot; each row's L1 is one thread's sequential
+// fp32 sum (relative rounding <= K * 2^-24; the 2x in the exponent choice covers it), x (1 + 2^-10).
+__global__ __launch_bounds__(256) void row_bound_kernel(const float* __restrict__ w, long long w_sstride, int rows,
+                                                        int rowlen, const float* __restrict__ bias,
+                                                        long long b_sstride, float* __restrict__ out) {
+  __shared__ float red[2][256];
+  const int sl = blockIdx.x, tid = threadIdx.x;
+  const float* __restrict__ ws = w + (long long)sl * w_sstride;
+  float l1 = 0.f, bm = 0.f;
+  for (int r = tid; r < rows; r += 256) {
+    float acc = 0.f;
+    for (int k = 0; k < rowlen; ++k) acc += fabsf(ws[(long long)r * rowlen + k]);
+    l1 = fmaxf(l1, acc * (1.f + 0x1p-10f));
+    if (bias) bm = fmaxf(bm, fabsf(bias[(long long)sl * b_sstride + r]));
+  }
+  red[0][tid] = l1;
+  red[1][tid] = bm;
+  __syncthreads();
+  for (int st = 128; st > 0; st >>= 1) {
+    if (tid < st) {
+      red[0][tid] = fmaxf(red[0][tid], red[0][tid + st]);
+      red[1][tid] = fmaxf(red[1][tid], red[1][tid + st]);
+    }
+    __syncthreads();
+  }
+  if (tid == 0) {
+    out[2 * sl] = red[0][0];
+    out[2 * sl + 1] = red[1][0];
+  }
+}
+
 // max |x| of n segments (offset, length) of every replica's flat row (the conv weights of a
 // model replica: one launch per training step instead of one per conv); out[s][g]
 constexpr int kAmaxSegs = 64;
@@ -1506,35 +1617,35 @@ int& planes() {
   return p;
 }
 
-template <int BM, int BN, int WM, int WN, int P, int VEC, bool H, bool PW>
+template <int BM, int BN, int WM, int WN, int P, int VEC, bool H, bool PW, bool PA = false>
 int xconv_go(const XArgs& a, long long Mmax, int G, int nclass, hipStream_t st) {
   XArgs b = a;
   b.tiles_n = ceil_div(a.Ncol, BN);
   const dim3 grid((unsigned)(ceil_div(Mmax, BM) * b.tiles_n), G, nclass * a.splitk);
-  hipLaunchKernelGGL((xconv_kernel<BM, BN, WM, WN, P, VEC, H, PW>), grid, dim3(256), 0, st, b);
+  hipLaunchKernelGGL((xconv_kernel<BM, BN, WM, WN, P, VEC, H, PW, PA>), grid, dim3(256), 0, st, b);
   DBA_LAUNCH_CHECK();
 }
 
-template <int P, int VEC, bool H, bool PW = false>
+template <int P, int VEC, bool H, bool PW = false, bool PA = false>
 int xconv_tile(const XArgs& a, long long Mmax, int G, int nclass, int bm, hipStream_t st) {
-  if (a.Ncol <= 32) return xconv_go<128, 32, 4, 1, P, VEC, H, PW>(a, Mmax, G, nclass, st);
+  if (a.Ncol <= 32) return xconv_go<128, 32, 4, 1, P, VEC, H, PW, PA>(a, Mmax, G, nclass, st);
   if (a.Ncol <= 64) {
-    if (bm == 64) return xconv_go<64, 64, 2, 2, P, VEC, H, PW>(a, Mmax, G, nclass, st);
-    return xconv_go<128, 64, 2, 2, P, VEC, H, PW>(a, Mmax, G, nclass, st);
+    if (bm == 64) return xconv_go<64, 64, 2, 2, P, VEC, H, PW, PA>(a, Mmax, G, nclass, st);
+    return xconv_go<128, 64, 2, 2, P, VEC, H, PW, PA>(a, Mmax, G, nclass, st);
   }
-  if (bm == 32) return xconv_go<32, 128, 1, 4, P, VEC, H, PW>(a, Mmax, G, nclass, st);
-  if (bm == 64) return xconv_go<64, 128, 2, 2, P, VEC, H, PW>(a, Mmax, G, nclass, st);
-  return xconv_go<128, 128, 2, 2, P, VEC, H, PW>(a, Mmax, G, nclass, st);
+  if (bm == 32) return xconv_go<32, 128, 1, 4, P, VEC, H, PW, PA>(a, Mmax, G, nclass, st);
+  if (bm == 64) return xconv_go<64, 128, 2, 2, P, VEC, H, PW, PA>(a, Mmax, G, nclass, st);
+  return xconv_go<128, 128, 2, 2, P, VEC, H, PW, PA>(a, Mmax, G, nclass, st);
 }
 
 bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
-template <int W, int CS, int BM, int BN, int WM, int WN, int P, bool H, bool PRE = false>
+template <int W, int CS, int BM, int BN, int WM, int WN, int P, bool H, bool PRE = false, bool PA = false>
 int xhalo_go(const XArgs& a, int G, hipStream_t st) {
   XArgs b = a;
   b.tiles_n = ceil_div(a.Ncol, BN);
   const dim3 grid((unsigned)(a.N * (a.Ho / (BM / W)) * b.tiles_n), G, 1);
-  hipLaunchKernelGGL((xhalo_kernel<W, CS, BM, BN, WM, WN, P, H, PRE>), grid, dim3(256), 0, st, b);
+  hipLaunchKernelGGL((xhalo_kernel<W, CS, BM, BN, WM, WN, P, H, PRE, PA>), grid, dim3(256), 0, st, b);
   DBA_LAUNCH_CHECK();
 }
 
@@ -1576,8 +1687,11 @@ int xhalo_try(const XArgs& a, int G, int KH, int KW, hipStream_t st) {
   // launch >= 1024 blocks; 4-row tiles otherwise
   static const bool big_ok = env_int("DBA_F32_HALO_BIG", 0) != 0;   // measured slower in the bench (profiles/r2_halo_tiles_ab.md)
   const bool big = big_ok && a.Ho % 8 == 0 && (long long)a.N * (a.Ho / 8) * G >= 1024;
+  const bool pairs = a.in_sexp || a.out_sexp || a.res_sexp;
+  if (pairs && !(a.amax_src && a.wp)) return -107;   // fp16-pair activations: evaluation forwards only
   if (a.Wo == 32 && a.Cs == 32 && a.Ncol <= 32 && a.Ho % 4 == 0) {
-    if (a.amax_src && a.Ncol == 32) {
+    if (a.in_sexp) return xhalo_go<32, 32, 128, 32, 4, 1, 2, true, true, true>(a, G, st);
+    if (a.amax_src && a.Ncol == 32 && !pairs) {
       const int rc = xhalo_ws_try(a, G, st);
       if (rc != -100) return rc;
     }
@@ -1592,6 +1706,7 @@ int xhalo_try(const XArgs& a, int G, int KH, int KW, hipStream_t st) {
   // work dominates and the implicit GEMM was faster: 154 vs 147 TF, kbench_r2_fp32_p3.json)
   static const bool h16 = env_int("DBA_F32_HALO16", 1) != 0;
   if (h16 && a.amax_src && a.Wo == 16 && a.Cs == 64 && a.Ncol <= 64 && a.Ho % 8 == 0) {
+    if (a.in_sexp) return xhalo_go<16, 64, 128, 64, 2, 2, 2, true, true, true>(a, G, st);
     if (a.wp) return xhalo_go<16, 64, 128, 64, 2, 2, 2, true, true>(a, G, st);
     return xhalo_go<16, 64, 128, 64, 2, 2, 2, true>(a, G, st);
   }
@@ -1609,6 +1724,10 @@ int xconv_dispatch(const XArgs& a, long long Mmax, int G, int nclass, int vec, h
   int bm = (bn > 32 && blocks < 512) ? 64 : 128;
   if (bn == 128 && 2 * blocks < bm32_below) bm = 32;
   if (vec == 4 && a.Cs % 32 == 0) vec = 32;
+  if (a.in_sexp) {   // fp16-pair activations (evaluation; the launcher checked wp and vec)
+    if (vec == 32) return xconv_tile<2, 32, true, true, true>(a, Mmax, G, nclass, bm, st);
+    return xconv_tile<2, 4, true, true, true>(a, Mmax, G, nclass, bm, st);
+  }
   if (a.amax_src && a.wp && vec >= 4) {
     if (vec == 32) return xconv_tile<2, 32, true, true>(a, Mmax, G, nclass, bm, st);
     return xconv_tile<2, 4, true, true>(a, Mmax, G, nclass, bm, st);
@@ -1705,7 +1824,8 @@ DBA_EXPORT int dba_xconv_fwd(const float* x, long long x_gstride, const float* w
                              int Wo, int Cout, int KH, int KW, int stride, int pad, int relu, const int* amax_x,
                              int amax_x_ld, const int* amax_w, int amax_w_ld, int* amax_out, int amax_out_ld,
                              const uint16_t* wp, long long wp_sstride, float* ws, long long ws_floats,
-                             double* bnpart, void* stream) {
+                             double* bnpart, const int* in_sexp, int* out_sexp, const float* bound,
+                             const int* amax_res, int amax_res_ld, const int* res_sexp, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   if ((long long)N * H * W * Cin >= (1LL << 29)) return -103;   // 32-bit in-replica byte offsets
   const long long M = (long long)N * Ho * Wo;
@@ -1720,13 +1840,17 @@ DBA_EXPORT int dba_xconv_fwd(const float* x, long long x_gstride, const float* w
   a.amax_src_ld = amax_x_ld; a.amax_w_ld = amax_w_ld; a.amax_out_ld = amax_out_ld;
   a.wp = wp; a.wp_sstride = wp_sstride;
   a.bnpart = bnpart; a.bnpart_nblk = (int)ceil_div(M, 32);
+  a.in_sexp = in_sexp; a.out_sexp = out_sexp; a.bound = bound;
+  a.amax_res = amax_res; a.amax_res_ld = amax_res_ld; a.res_sexp = res_sexp;
   a.cls[0] = XClass{KH, KW, -pad, -pad, 0, 0, Ho, Wo, 0};
   if (bnpart && (bias || res || relu)) return -106;   // statistics of the raw conv output only
+  const bool pairs = in_sexp || out_sexp || res_sexp;
+  if (pairs && (!amax_x || !wp || vec < 4 || (Cout & 3) || bnpart || (out_sexp && !bound))) return -107;
   if (stride == 1) {
     const int rc = xhalo_try(a, G, KH, KW, st);
     if (rc != -100) return rc;
   }
-  const int s = xsplitk(M, G, Cout, K);
+  const int s = pairs ? 1 : xsplitk(M, G, Cout, K);
   if (bnpart && s > 1) return -106;   // split-K outputs: BN statistics by the BN kernels
   if (s > 1 && ws != nullptr && ws_floats >= (long long)s * G * M * Cout) {
     XArgs b = a;
@@ -1924,6 +2048,14 @@ DBA_EXPORT int dba_amax(const float* x, long long gstride, long long n_per_g, co
   const long long per = nvalid ? per_item * (n_per_g / std::max(1LL, per_item)) : n_per_g;
   const dim3 grid((unsigned)std::max(1LL, std::min(256LL, (per + 4095) / 4096)), G);
   hipLaunchKernelGGL(amax_kernel, grid, dim3(256), 0, st, x, gstride, n_per_g, nvalid, per_item, vec, out, ld);
+  DBA_LAUNCH_CHECK();
+}
+
+// out [slots][2]: {max row L1 of w [slots][rows][rowlen], max |bias|} (bias optional)
+DBA_EXPORT int dba_row_bound(const float* w, long long w_sstride, int rows, int rowlen, const float* bias,
+                             long long b_sstride, int slots, float* out, void* stream) {
+  hipLaunchKernelGGL(row_bound_kernel, dim3(slots), dim3(256), 0, (hipStream_t)stream, w, w_sstride, rows, rowlen,
+                     bias, b_sstride, out);
   DBA_LAUNCH_CHECK();
 }
 

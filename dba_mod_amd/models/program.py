@@ -15,6 +15,7 @@ selecting its weights through ``wsel``.  Reference forward definitions: see
 """
 from __future__ import annotations
 
+import os
 from typing import Callable, Dict, List, Optional, Tuple
 
 import torch
@@ -106,6 +107,12 @@ class Ctx:
         self._drop_ctr = 0
         self.act_dtype = act_dtype
         self._wamax = self._weight_scales() if train else None
+        # evaluation forwards of the fp32 family on the HIP backend keep conv-to-conv
+        # activations as fp16 pairs (ops.hip PairAct); DBA_EVAL_PAIRS=0 keeps fp32
+        self.eval_pairs = (not train and folded is not None and act_dtype == torch.float32
+                           and any(t.is_cuda for t, _ in folded.values())
+                           and ops.backend_name(next(iter(folded.values()))[0].device) == "hip"
+                           and os.environ.get("DBA_EVAL_PAIRS", "1") != "0")
 
     def _weight_scales(self) -> Optional[Dict[str, Tensor]]:
         """fp32 kernels on the fp16 pair (ops.hip F16_PAIR): every conv / linear weight's
@@ -144,11 +151,15 @@ class Ctx:
 
     # ------------------------------------------------------------------ layers
     def conv_bn(self, x: Tensor, conv: str, bn: str, stride: int, pad: int, relu: bool,
-                residual: Optional[Tensor] = None) -> Tensor:
+                residual: Optional[Tensor] = None, to_conv: bool = True) -> Tensor:
+        """``to_conv``: the output only feeds convs (A operand or residual), so an evaluation
+        forward may keep it as fp16-pair activations (ops.hip PairAct); False where a pooling
+        or a linear layer reads it."""
         if not self.train:
             wf, bf = self.folded[conv]
+            kw = {"out_pairs": True} if (to_conv and self.eval_pairs) else {}
             return ops.conv2d(x, wf, self.wsel, stride, pad, bias=bf, residual=residual, relu=relu,
-                              nvalid=self.nvalid)
+                              nvalid=self.nvalid, **kw)
         w = self.w(conv)
         y = ops.conv2d(x, w, self.wsel, stride, pad, nvalid=self.nvalid, bn_stats=True)
         gamma, beta = self.m(bn + ".weight"), self.m(bn + ".bias")
@@ -289,7 +300,9 @@ def _resnet_cifar(ctx: Ctx, x: Tensor) -> Tensor:
                 sc = ctx.conv_bn(out, pre + "shortcut.0.weight", pre + "shortcut.1", stride, 0, relu=False)
             else:
                 sc = out
-            out = ctx.conv_bn(a, pre + f"conv{last}.weight", pre + f"bn{last}", 1, p, relu=True, residual=sc)
+            final = li == 3 and bi == blocks[li] - 1
+            out = ctx.conv_bn(a, pre + f"conv{last}.weight", pre + f"bn{last}", 1, p, relu=True, residual=sc,
+                              to_conv=not final)
             cin = w * exp
     out = ctx.gap(out)
     G, N = out.shape[:2]
@@ -297,7 +310,7 @@ def _resnet_cifar(ctx: Ctx, x: Tensor) -> Tensor:
 
 
 def _resnet_tiny(ctx: Ctx, x: Tensor) -> Tensor:
-    out = ctx.conv_bn(x, "conv1.weight", "bn1", 2, 3, relu=True)
+    out = ctx.conv_bn(x, "conv1.weight", "bn1", 2, 3, relu=True, to_conv=False)   # -> max-pool
     out = ctx.maxpool(out, 3, 2, 1)
     cin = 64
     for li, w in enumerate((64, 128, 256, 512)):
@@ -309,7 +322,8 @@ def _resnet_tiny(ctx: Ctx, x: Tensor) -> Tensor:
             else:
                 sc = out
             a = ctx.conv_bn(out, pre + "conv1.weight", pre + "bn1", stride, 1, relu=True)
-            out = ctx.conv_bn(a, pre + "conv2.weight", pre + "bn2", 1, 1, relu=True, residual=sc)
+            out = ctx.conv_bn(a, pre + "conv2.weight", pre + "bn2", 1, 1, relu=True, residual=sc,
+                              to_conv=not (li == 3 and bi == 1))
             cin = w
     out = ctx.gap(out)
     G, N = out.shape[:2]

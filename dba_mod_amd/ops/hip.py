@@ -79,7 +79,9 @@ _SIGS = {
     "dba_xgemm_set_planes": [_I],
     "dba_xhalo_ws_set": [_I],
     "dba_xconv_ws_floats": [_I] * 8,
-    "dba_xconv_fwd": [_P, _LL, _P, _LL, _P, _P, _LL, _P, _P, _LL, _P] + [_I] * 13 + [_P, _I] * 3 + [_P, _LL] * 2 + [_P, _P],
+    "dba_xconv_fwd": [_P, _LL, _P, _LL, _P, _P, _LL, _P, _P, _LL, _P] + [_I] * 13 + [_P, _I] * 3 + [_P, _LL] * 2
+    + [_P, _P, _P, _P, _P, _I, _P, _P],
+    "dba_row_bound": [_P, _LL, _I, _I, _P, _LL, _I, _P, _P],
     "dba_bn_finalize_part": [_P, _I, _P, _I, _I, _I, _I, _P, _P, _LL, _F, _F, _P, _P, _P],
     "dba_xconv_dgrad": [_P, _LL, _P, _LL, _P, _P, _P, _LL, _P] + [_I] * 12 + [_P, _I] * 2 + [_P, _LL] * 2 + [_P],
     "dba_xsplit_w": [_P, _LL, _LL, _I, _P, _I, _P, _P],
@@ -89,7 +91,7 @@ _SIGS = {
     "dba_xwgrad": [_P, _LL, _P, _LL, _P, _LL, _P] + [_I] * 12 + [_P, _I] * 2 + [_P, _LL, _I, _P],
     "dba_xwgrad_reduce_batch": [_P, _I, _I, _LL, _P],
     # image stems in exact fp32 (csrc/kernels/stem.hip)
-    "dba_xstem_fwd": [_P, _LL, _P, _LL, _P, _P, _LL, _P, _P, _LL, _P] + [_I] * 13 + [_P, _I, _P, _P],
+    "dba_xstem_fwd": [_P, _LL, _P, _LL, _P, _P, _LL, _P, _P, _LL, _P] + [_I] * 13 + [_P, _I, _P, _P, _I, _P, _P, _P],
 }
 for _name, _args in _SIGS.items():
     _fn = getattr(_L, _name)
@@ -150,6 +152,8 @@ def _act(t: Tensor, dt: Optional[torch.dtype] = None, what: str = "activation") 
     if dt is not None and t.dtype != dt:
         raise TypeError(f"{what}: dtype {t.dtype} does not match the op's {dt} operands "
                         f"(no silent precision conversion)")
+    if getattr(t, "_dba_pair", None) is not None and what not in ("conv input", "residual"):
+        raise TypeError(f"{what}: an fp16-pair activation (PairAct) can only feed a conv")
     return t.contiguous()
 
 
@@ -435,6 +439,8 @@ def _amax_act(t, nvalid):
     a = getattr(t, "_dba_amax", None)
     if a is not None:
         return a
+    if getattr(t, "_dba_pair", None) is not None:
+        raise RuntimeError("fp16-pair activation without its producer's max slot")
     per_item = t[0, 0].numel()
     a = _amax(t, t.stride(0), t.shape[1] * per_item, nvalid, per_item)
     t._dba_amax = a   # activations are never written in place: the fwd / wgrad pair shares it
@@ -447,7 +453,12 @@ def _pconv_ok(Cin, Cout, H, W, KH, KW, stride, pad) -> bool:
             and (Cin, Cout, W, stride) in _PCONV_SHAPES)
 
 
-def _xconv_fwd(x, w, wsel, stride, pad, bias, residual, relu, nvalid, out_dtype, bn_stats=False):
+def _pair_sexp(t):
+    """The per-replica scale exponents of an fp16-pair activation (PairAct), else None."""
+    return getattr(t, "_dba_pair", None)
+
+
+def _xconv_fwd(x, w, wsel, stride, pad, bias, residual, relu, nvalid, out_dtype, bn_stats=False, out_pairs=False):
     """Reference-precision conv (fp32 in / fp32 out, split MFMA: xgemm.hip).  ``bn_stats``:
     the output feeds a training BN — the epilogue also folds its per-32-pixel column sums /
     sums of squares (``y._dba_bnpart``), which :func:`bn_train` finalises instead of
@@ -476,6 +487,18 @@ def _xconv_fwd(x, w, wsel, stride, pad, bias, residual, relu, nvalid, out_dtype,
     if _MODE == F16_PAIR and "fwd" in _H_OPS:
         ax, aw = _amax_act(x, nvalid), _amax_w(w, ws, Cout * KH * KW * Cin)
         ay = _amax_out(y)   # the output's max, for its consumers
+    # fp16-pair activations (xgemm.hip PairAct; evaluation forwards with pre-split weights):
+    # the input may arrive split, the output may leave split; every user of such a tensor is a
+    # conv of this family (A operand or residual)
+    in_sexp, res_sexp = _pair_sexp(x), (_pair_sexp(residual) if residual is not None else None)
+    pairs_ok = (ax is not None and getattr(w, "_dba_planes", None) is not None and Cin % 4 == 0 and not bn_stats)
+    if (in_sexp is not None or res_sexp is not None) and not pairs_ok:
+        raise RuntimeError("fp16-pair activation fed to a conv outside the evaluation pair path")
+    out_sexp = None
+    if out_pairs and pairs_ok and Cout % 4 == 0 and getattr(w, "_dba_bound", None) is not None:
+        out_sexp = torch.zeros(G, dtype=torch.int32, device=x.device)
+    bound = getattr(w, "_dba_bound", None)
+    ares = _amax_act(residual, nvalid) if (residual is not None and out_sexp is not None) else None
     part = None
     want_part = (bn_stats and _BN_FUSED_STATS and bias is None and res is None and not relu
                  and N * Ho * Wo > _BN_SMALL_ROWS)
@@ -486,10 +509,13 @@ def _xconv_fwd(x, w, wsel, stride, pad, bias, residual, relu, nvalid, out_dtype,
             part = torch.empty(G * Cout * 2 * nblk, dtype=torch.float64, device=x.device)
         rc = _call("dba_xstem_fwd", x.data_ptr(), N * H * W * Cin, w.data_ptr(), ws, _ptr(_i32(wsel)), _ptr(bias), bs,
                    _ptr(res), y.data_ptr(), N * Ho * Wo * Cout, _ptr(_i32(nvalid)), G, N, H, W, Cin, Ho, Wo, Cout,
-                   KH, KW, stride, pad, int(relu), *_aptr(ay), _ptr(part), _stream())
+                   KH, KW, stride, pad, int(relu), *_aptr(ay), _ptr(part), *_aptr(ax if out_sexp is not None else None),
+                   _ptr(out_sexp), _ptr(bound if out_sexp is not None else None), _stream())
         if rc != NOT_HANDLED:
             if part is not None:
                 y._dba_bnpart = (part, nblk)
+            if out_sexp is not None:
+                y._dba_pair = out_sexp
             return y
         part = None
     if want_part and n == 0:
@@ -501,15 +527,23 @@ def _xconv_fwd(x, w, wsel, stride, pad, bias, residual, relu, nvalid, out_dtype,
     _call("dba_xconv_fwd", x.data_ptr(), N * H * W * Cin, w.data_ptr(), ws, _ptr(_i32(wsel)), _ptr(bias), bs,
           _ptr(res), y.data_ptr(), N * Ho * Wo * Cout, _ptr(_i32(nvalid)), G, N, H, W, Cin, Ho, Wo, Cout, KH, KW,
           stride, pad, int(relu), *_aptr(ax), *_aptr(aw), *_aptr(ay), *_wplanes(w), _ptr(wsb), n, _ptr(part),
+          _ptr(in_sexp), _ptr(out_sexp), _ptr(bound if out_sexp is not None else None), *_aptr(ares), _ptr(res_sexp),
           _stream())
+    if out_sexp is not None:
+        y._dba_pair = out_sexp
     return y
 
 
 def conv2d(x, w, wsel, stride, pad, bias=None, residual=None, relu=False, nvalid=None, out_dtype=None,
-           bn_stats=False):
+           bn_stats=False, out_pairs=False):
+    """``out_pairs``: the output may be emitted as fp16-pair activations (fp32 family,
+    evaluation with pre-split weights; y._dba_pair set) — only for outputs consumed by convs."""
+    sx = _pair_sexp(x)
     x = _act(x, None, "conv input")
+    if sx is not None:
+        x._dba_pair = sx
     if x.dtype == _F32:
-        return _xconv_fwd(x, w, wsel, stride, pad, bias, residual, relu, nvalid, out_dtype, bn_stats)
+        return _xconv_fwd(x, w, wsel, stride, pad, bias, residual, relu, nvalid, out_dtype, bn_stats, out_pairs)
     G, N, H, W, Cin = x.shape
     w, ws = _check_w(w)
     Cout, KH, KW = w.shape[1], w.shape[2], w.shape[3]
@@ -895,7 +929,20 @@ def bn_fold(w, conv_bias, gamma, beta, rmean, rvar, eps, out_dtype):
         wf._dba_amax = _amax(wf, Cout * K, Cout * K)   # the folded weights' scale, once per fold
         if _MODE == F16_PAIR:
             split_weights(wf, Cout * K, Cout * K, wf._dba_amax)   # and their fp16 planes
+            wf._dba_bound = row_bound(wf, bf)   # output bound: fp16-pair activations (PairAct)
     return wf, bf
+
+
+def row_bound(w, bias):
+    """[slots, 2] fp32 {max row L1 of w, max |bias|} per weight slot (xgemm.hip row_bound_kernel):
+    the output bound that fixes an evaluation conv's fp16-pair output scale before it runs."""
+    slots, Cout = w.shape[0], w.shape[1]
+    per = w[0].numel()
+    wv, ws = _rowview(w)
+    out = torch.empty(slots, 2, dtype=torch.float32, device=w.device)
+    bv, bs = _rowview(bias) if bias is not None else (None, 0)
+    _call("dba_row_bound", wv.data_ptr(), ws, Cout, per // Cout, _ptr(bv), bs, slots, out.data_ptr(), _stream())
+    return out
 
 
 # --------------------------------------------------------------------------- pooling

@@ -113,9 +113,10 @@ def gather_rows(src: Tensor, labels: Tensor, idx: Tensor, trig_cols: Tensor, tri
 def conv2d(x: Tensor, w: Tensor, wsel: Optional[Tensor], stride: int, pad: int,
            bias: Optional[Tensor] = None, residual: Optional[Tensor] = None,
            relu: bool = False, nvalid: Optional[Tensor] = None,
-           out_dtype: Optional[torch.dtype] = None, bn_stats: bool = False) -> Tensor:
+           out_dtype: Optional[torch.dtype] = None, bn_stats: bool = False, out_pairs: bool = False) -> Tensor:
     """y = act(conv(x, w) + bias + residual); NHWC in/out (K1, K3, K4, K8).  ``bn_stats`` (a
-    hint that y feeds a training BN) only matters to the HIP backend."""
+    hint that y feeds a training BN) and ``out_pairs`` (y may be stored as fp16-pair
+    activations) only matter to the HIP backend."""
     G = x.shape[0]
     outs = []
     for g in range(G):

@@ -190,8 +190,8 @@ def init_distributed(prefer_gpu: bool = True, timeout_s: int = 1800) -> DistCtx:
     backend = os.environ.get("DBA_DIST_BACKEND") or ("nccl" if use_gpu else "gloo")   # "nccl" is RCCL
     kw = dict(backend=backend, rank=rank, world_size=world,
               timeout=datetime.timedelta(seconds=timeout_s))
-    if backend == "nccl":
-        kw["device_id"] = device
+    if backend == "nccl" and os.environ.get("DBA_PG_LAZY") != "1":
+        kw["device_id"] = device   # eager communicator (DBA_PG_LAZY=1: created at the first collective)
     # RCCL binds the initialising thread to the GPU's NUMA-local cores; inside a container
     # whose cgroup CPU set does not match, that pins the one host thread that enqueues every
     # kernel onto a few (shared) cores — measured: the 1-GPU bench with a world-1 RCCL group
@@ -201,11 +201,11 @@ def init_distributed(prefer_gpu: bool = True, timeout_s: int = 1800) -> DistCtx:
     if not dist.is_initialized():
         dist.init_process_group(**kw)
     ctx = DistCtx(rank, world, dev_index, device, backend, pg=True)
-    ctx.selfcheck_ok = selfcheck(ctx)
+    ctx.selfcheck_ok = selfcheck(ctx) if os.environ.get("DBA_PG_SKIP_SELFCHECK") != "1" else None
     if aff is not None and os.environ.get("DBA_KEEP_RCCL_AFFINITY") != "1":
         ctx.affinity_changed = os.sched_getaffinity(0) != aff
         os.sched_setaffinity(0, aff)
-    if not ctx.selfcheck_ok:
+    if ctx.selfcheck_ok is False:
         raise RuntimeError(f"rank {rank}: {backend} all-reduce self-check failed (world {world})")
     return ctx
 

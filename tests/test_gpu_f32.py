@@ -584,3 +584,63 @@ def test_halo_ws_bn_partials_bitwise(H):
     finally:
         H.set_halo_ws(prev_ws)
         H.set_fp32_planes(prev)
+
+
+@pytest.mark.parametrize("arch,shp", [("resnet18_cifar", (32, 32, 3)), ("resnet18_tiny", (64, 64, 3)),
+                                      ("resnet50_cifar", (32, 32, 3))])
+def test_eval_pair_activations(H, R64, arch, shp):
+    """Evaluation forwards keep conv-to-conv activations as fp16 pairs (ops.hip PairAct: the
+    producer's epilogue splits with a bound-derived scale, the consumer stages bits, residuals
+    decode): logits at fp32 level against fp64 and against the fp32-activation forward, for a
+    model bank with a slot map and a partly valid job."""
+    import os
+    from dba_mod_amd import ops
+    from dba_mod_amd.models import program as P
+    from dba_mod_amd.models.spec import get_spec
+    prev = H.set_fp32_planes(16)
+    try:
+        spec = get_spec(arch)
+        dev = torch.device("cuda")
+        torch.manual_seed(0)
+        bank = torch.stack([spec.init_flat(1), spec.init_flat(2)])
+        # non-trivial BN running statistics and affine parameters (as after training)
+        g0 = torch.Generator().manual_seed(3)
+        for e in spec.params:
+            if e.kind not in ("conv_w", "lin_w"):
+                v = spec.view(bank, e.name)
+                v += 0.1 * torch.randn(v.shape, generator=g0)
+        bank[:, spec.P:] = bank[:, spec.P:] + 0.05 * torch.rand(bank[:, spec.P:].shape, generator=g0)
+        bank = bank.to(dev)
+        x = torch.rand(3, 12, *shp, device=dev)
+        sel = torch.tensor([0, 1, 0], dtype=torch.int32, device=dev)
+        nval = torch.tensor([12, 12, 7], dtype=torch.int32, device=dev)
+
+        def run(mod, dt, d, pairs):
+            saved = {k: getattr(ops, k) for k in ops._OPS}
+            for k in ops._OPS:
+                setattr(ops, k, getattr(mod, k))
+            old = os.environ.get("DBA_EVAL_PAIRS")
+            os.environ["DBA_EVAL_PAIRS"] = "1" if pairs else "0"
+            try:
+                ctx = P.Ctx(spec, None, None, sel.to(d), train=False, folded=P.fold_bank(spec, bank.to(d, dt), dt),
+                            nvalid=nval.to(d), act_dtype=dt)
+                assert ctx.eval_pairs == (pairs and d.type == "cuda")
+                return P.forward(ctx, x.to(d, dt)).double().cpu()
+            finally:
+                for k, v in saved.items():
+                    setattr(ops, k, v)
+                if old is None:
+                    del os.environ["DBA_EVAL_PAIRS"]
+                else:
+                    os.environ["DBA_EVAL_PAIRS"] = old
+
+        lp = run(H, torch.float32, dev, True)
+        lf = run(H, torch.float32, dev, False)
+        lr = run(R64, torch.float64, torch.device("cpu"), False)
+        for g in range(3):
+            n = int(nval[g])
+            assert torch.isfinite(lp[g, :n]).all()
+            assert _rel(lp[g, :n], lr[g, :n]) < 2e-6, (arch, g, _rel(lp[g, :n], lr[g, :n]), _rel(lf[g, :n], lr[g, :n]))
+            assert _rel(lp[g, :n], lf[g, :n]) < 2e-6, (arch, g)
+    finally:
+        H.set_fp32_planes(prev)
