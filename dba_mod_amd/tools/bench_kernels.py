@@ -76,6 +76,14 @@ def _bench_fp32(name, G, N, Hh, Cin, Cout, k, s, p, reps, dev):
         per = Cout * k * k * Cin
         H.split_weights(w, per, per, H._amax_w(w, per, per))
     ops = [("fwd", lambda: H.conv2d(x, w, None, s, p, relu=True))]
+    if name.startswith("eval") and H.fp32_mode() == H.F16_PAIR and Cin == Cout and Cin % 4 == 0 and s == 1:
+        # fp16-pair activations in and out (ops.hip PairAct): the input is a pair tensor made by a
+        # producer conv of the same shape
+        w._dba_bound = H.row_bound(w, None)
+        x._dba_amax = H._amax_act(x, None)
+        xp = H.conv2d(x, w, None, s, p, relu=True, out_pairs=True)
+        assert getattr(xp, "_dba_pair", None) is not None
+        ops.append(("fwd_pairs", lambda: H.conv2d(xp, w, None, s, p, relu=True, out_pairs=True)))
     if name.startswith("train"):
         wt = H.prepare_dgrad_weights(w, [(w, None, s, p, (Hh, Hh), None, G)])[0]
         dw = torch.zeros(G, Cout, k, k, Cin, device=dev)

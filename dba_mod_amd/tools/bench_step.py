@@ -32,8 +32,14 @@ def main(argv=None) -> int:
     ap.add_argument("--clients", type=int, default=0,
                     help="keep only the k longest clients (k=1: the lone-attacker latency regime)")
     ap.add_argument("--dtype", choices=("fp32", "bf16"), default="fp32")
+    ap.add_argument("--rccl", action="store_true",
+                    help="create a world-1 RCCL communicator first (one all-reduce): its effect on step time")
     args = ap.parse_args(argv)
     dev = torch.device("cuda")
+    if args.rccl:
+        from ..parallel.dist import init_distributed
+        os.environ.update(DBA_FORCE_PG="1", MASTER_ADDR="127.0.0.1", MASTER_PORT=os.environ.get("MASTER_PORT", "29561"))
+        assert init_distributed().selfcheck_ok
     p = C.load_params(args.config, {"resumed_model": False, "synthetic_data": True, "overlap_eval": False,
                                     "start_epoch": args.epoch, "compute_dtype": args.dtype})
     s = Server(p, DistCtx(device=dev), write_outputs=False)
