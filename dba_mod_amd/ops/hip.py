@@ -453,6 +453,19 @@ def _pconv_ok(Cin, Cout, H, W, KH, KW, stride, pad) -> bool:
             and (Cin, Cout, W, stride) in _PCONV_SHAPES)
 
 
+def decode_pairs(t: Tensor) -> Tensor:
+    """fp32 values of an fp16-pair activation (PairAct layout: every 4 channels = 4 fp16 hi +
+    4 fp16 lo of x * 2^s[g]) — for oracles and diagnostics; the kernels decode in-register."""
+    sexp = _pair_sexp(t)
+    if sexp is None:
+        return t
+    G, C = t.shape[0], t.shape[-1]
+    h = t.contiguous().view(torch.float16).reshape(*t.shape[:-1], C // 4, 2, 4).float()
+    v = (h[..., 0, :] + h[..., 1, :]).reshape(t.shape)
+    scale = torch.exp2(-sexp.to(torch.float32)).view(G, *([1] * (t.dim() - 1)))
+    return v * scale
+
+
 def _pair_sexp(t):
     """The per-replica scale exponents of an fp16-pair activation (PairAct), else None."""
     return getattr(t, "_dba_pair", None)

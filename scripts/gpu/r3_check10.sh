@@ -4,8 +4,6 @@ set -o pipefail
 mkdir -p gpurun_out/r3
 timeout -k 10 300 python -u -m pytest tests/test_gpu_f32.py -x -v --timeout 120 --timeout-method thread -k "eval_pair" > gpurun_out/r3/tests_pairs.log 2>&1 || { grep -E "PASSED|FAILED" gpurun_out/r3/tests_pairs.log; grep -E "^E " gpurun_out/r3/tests_pairs.log | head -20; exit 1; }
 grep -E "PASSED|FAILED" gpurun_out/r3/tests_pairs.log
-timeout -k 10 900 python -u -m pytest tests/test_gpu_f32.py tests/test_gpu_e2e.py tests/test_gpu_kernels.py -x -q --timeout 300 --timeout-method thread -k "not dba_attack_lands" > gpurun_out/r3/tests10.log 2>&1 || { grep -E "FAILED|^E " gpurun_out/r3/tests10.log | head -20; exit 1; }
-tail -1 gpurun_out/r3/tests10.log
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r3/smoke10.log 2>&1 || { tail -20 gpurun_out/r3/smoke10.log; exit 1; }
 echo "smoke: $(tail -1 gpurun_out/r3/smoke10.log | cut -c1-500)"
 timeout -k 10 300 python -m dba_mod_amd.tools.bench_kernels --dtype fp32 --planes 16 --reps 10 --only eval > gpurun_out/r3/kbench_eval10.log 2>&1 || exit $?
