@@ -509,7 +509,7 @@ def _xconv_fwd(x, w, wsel, stride, pad, bias, residual, relu, nvalid, out_dtype,
         raise RuntimeError("fp16-pair activation fed to a conv outside the evaluation pair path")
     out_sexp = None
     if out_pairs and pairs_ok and Cout % 4 == 0 and getattr(w, "_dba_bound", None) is not None:
-        out_sexp = torch.zeros(G, dtype=torch.int32, device=x.device)
+        out_sexp = torch.empty(G, dtype=torch.int32, device=x.device)   # every block with rows writes it
     bound = getattr(w, "_dba_bound", None)
     ares = _amax_act(residual, nvalid) if (residual is not None and out_sexp is not None) else None
     part = None
