@@ -1,0 +1,66 @@
+"""Eager launch cost with / without a live RCCL communicator (round-3 diagnosis of the
+world-1 RCCL slowdown): times a chunk-like sequence of eager fp32 conv launches (host wall,
+synchronised) and the same sequence replayed from a captured HIP graph.
+
+    python -m dba_mod_amd.tools.launch_probe [--rccl]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import time
+
+import torch
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rccl", action="store_true")
+    ap.add_argument("--reps", type=int, default=30)
+    args = ap.parse_args(argv)
+    if args.rccl:
+        from ..parallel.dist import init_distributed
+        os.environ.update(DBA_FORCE_PG="1", MASTER_ADDR="127.0.0.1", MASTER_PORT=os.environ.get("MASTER_PORT", "29591"))
+        assert init_distributed().selfcheck_ok
+    from ..ops import hip as H
+    dev = torch.device("cuda")
+    out = {"rccl": args.rccl}
+    for name, (G, N, Hh, C) in {"small": (2, 64, 8, 128), "large": (4, 512, 16, 64)}.items():
+        x = torch.randn(G, N, Hh, Hh, C, device=dev)
+        w = torch.randn(G, C, 3, 3, C, device=dev) * 0.05
+
+        def seq():
+            y = x
+            for _ in range(20):
+                y = H.conv2d(y, w, None, 1, 1, relu=True)
+            return y
+        for _ in range(3):
+            seq()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.reps):
+            seq()
+        torch.cuda.synchronize()
+        eager = (time.perf_counter() - t0) / args.reps
+        g = torch.cuda.CUDAGraph()
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            seq()
+        torch.cuda.current_stream().wait_stream(s)
+        with torch.cuda.graph(g):
+            seq()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.reps):
+            g.replay()
+        torch.cuda.synchronize()
+        graph = (time.perf_counter() - t0) / args.reps
+        out[name] = {"eager_ms": round(eager * 1e3, 3), "graph_ms": round(graph * 1e3, 3)}
+    print(json.dumps(out), flush=True)
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())
