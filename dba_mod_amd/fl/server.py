@@ -21,7 +21,7 @@ import yaml
 
 from .. import config as C
 from .. import ops
-from ..parallel.dist import DistCtx
+from ..parallel.dist import DistCtx, framework_streams
 from ..utils import checkpoint as ckpt
 from ..utils import native
 from ..utils.csv_record import CsvRecorder
@@ -149,14 +149,12 @@ class Server:
         if self.device.type == "cuda" and bool(params.get("overlap_eval", True)):
             # training runs on a HIGH-priority stream (its kernels are small and latency-bound,
             # they win every CU that frees up); evaluation fills the rest at default priority
-            torch.cuda.synchronize(self.device)
-            self._main_stream = torch.cuda.Stream(self.device, priority=-1)
-            torch.cuda.set_stream(self._main_stream)
-            self._eval_stream = torch.cuda.Stream(self.device, priority=0)
             # local tests of clients that finished training get their own low-priority stream,
             # so the global tests of round r (ready at once) never queue behind the local tests
             # of round r+1 (each waiting for its client to finish)
-            self._early_stream = torch.cuda.Stream(self.device, priority=0)
+            torch.cuda.synchronize(self.device)
+            self._main_stream, self._eval_stream, self._early_stream = framework_streams(self.device)
+            torch.cuda.set_stream(self._main_stream)
         if self.write:
             with open(os.path.join(self.folder, "params.yaml"), "w") as f:
                 yaml.safe_dump(params.to_plain(), f)

@@ -169,6 +169,25 @@ class DistCtx:
         return out
 
 
+_STREAMS: Dict[int, tuple] = {}
+
+
+def framework_streams(device: torch.device):
+    """The process's (train, eval, early-eval) streams, created once per device: training on a
+    HIGH-priority stream, the two evaluation streams at default priority (``fl/server.py``).
+
+    ``torch.cuda.Stream`` hands out streams round-robin from PyTorch's per-priority pools, and
+    HIP maps those streams onto the process's few hardware queues (``GPU_MAX_HW_QUEUES``, 4 on
+    the box).  :func:`init_distributed` takes these three before the process group exists
+    (``DBA_STREAMS_FIRST=0``: after), so RCCL's own pool streams cannot shift the training and
+    evaluation streams onto a shared hardware queue."""
+    key = device.index if device.index is not None else torch.cuda.current_device()
+    if key not in _STREAMS:
+        _STREAMS[key] = (torch.cuda.Stream(device, priority=-1), torch.cuda.Stream(device, priority=0),
+                         torch.cuda.Stream(device, priority=0))
+    return _STREAMS[key]
+
+
 def init_distributed(prefer_gpu: bool = True, timeout_s: int = 1800) -> DistCtx:
     """Initialise from torchrun's env (RANK/WORLD_SIZE/LOCAL_RANK/MASTER_*); world 1 otherwise."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -198,6 +217,8 @@ def init_distributed(prefer_gpu: bool = True, timeout_s: int = 1800) -> DistCtx:
     # ran at 2.18 rounds/s vs 2.94 without (profiles/bench_r3_rccl_affinity.md).  Keep the
     # affinity the process started with (DBA_KEEP_RCCL_AFFINITY=1 keeps RCCL's choice).
     aff = os.sched_getaffinity(0) if hasattr(os, "sched_getaffinity") else None
+    if use_gpu and os.environ.get("DBA_STREAMS_FIRST", "1") != "0":
+        framework_streams(device)
     if not dist.is_initialized():
         dist.init_process_group(**kw)
     ctx = DistCtx(rank, world, dev_index, device, backend, pg=True)
