@@ -11,6 +11,8 @@
 //   * dba_lpt_assign   — longest-processing-time placement of clients onto ranks
 //                        (client-parallel data parallelism).
 //   * dba_shard_index  — strided sharding of evaluation index lists across ranks.
+//   * dba_balance_shares — water-filling shares of a round's image-sharded evaluation over
+//                        ranks, given each rank's training + local-test load in the window.
 //
 // Row layout (D = G*B + 8*G int32 words):
 //   idx[G*B] | poison_n[G] | trig[G] | first[G] | active[G] | nvalid[G] | slot[G] | seed[G] | lr[G] (f32 bits)
@@ -35,7 +37,7 @@ inline uint32_t lowbias32(uint32_t x) {
 
 extern "C" {
 
-int dba_runtime_version() { return 3; }
+int dba_runtime_version() { return 4; }
 
 uint32_t dba_hash2(uint32_t seed, uint32_t counter) { return lowbias32(counter ^ lowbias32(seed)); }
 
@@ -112,6 +114,35 @@ int64_t dba_shard_index(const int64_t* idx, int64_t n, int rank, int world, int6
   int64_t k = 0;
   for (int64_t i = rank; i < n; i += world) out[k++] = idx[i];
   return k;
+}
+
+// Water-filling split of `work` units over ranks already carrying base[r] units in the same
+// window: rank r gets share[r] = max(0, L - base[r]) / work with the level L chosen so the
+// shares sum to 1 (the least-loaded ranks fill up first; a rank whose base alone exceeds the
+// level gets nothing).  work <= 0: shares 1/world.  Deterministic (pure function of inputs):
+// every rank computes the same shares.
+void dba_balance_shares(int world, const double* base, double work, double* share) {
+  if (world <= 0) return;
+  if (!(work > 0.0)) {
+    for (int r = 0; r < world; ++r) share[r] = 1.0 / world;
+    return;
+  }
+  std::vector<double> b(base, base + world);
+  std::sort(b.begin(), b.end());
+  // the level lies between b[k-1] and b[k] for the first k with k*b[k] - sum(b[0..k)) >= work
+  double level = 0.0, pref = 0.0;
+  int k = 0;
+  for (; k < world; ++k) {
+    if (k > 0 && (double)k * b[k] - pref >= work) break;
+    pref += b[k];
+  }
+  level = (work + pref) / k;
+  double tot = 0.0;
+  for (int r = 0; r < world; ++r) {
+    share[r] = base[r] < level ? (level - base[r]) / work : 0.0;
+    tot += share[r];
+  }
+  for (int r = 0; r < world; ++r) share[r] /= tot;   // exact sum 1 up to rounding
 }
 
 }  // extern "C"

@@ -104,6 +104,12 @@ _DEFAULTS: Dict[str, Any] = {
     "graph_capture": True,         # HIP-graph the grouped training step on GPU
     "overlap_eval": True,          # evaluate round r on a side stream under round r+1's training
     "early_local_eval": True,      # enqueue a client's local tests as soon as it finishes training
+    # N > 1 ranks: image-sharded tests split by water-filling over each rank's load in the
+    # window (training of the next round + its local tests), in eval image-forward units:
+    # one grouped training step costs balance_step_latency + balance_step_per_client * active
+    "eval_balance": True,
+    "balance_step_latency": 1200.0,
+    "balance_step_per_client": 420.0,
     "rfa_mode": "auto",            # RFA across ranks: gather | distributed | auto (fewer bytes)
     "pretrain_rounds": 0,          # benign FedAvg warm start when not resuming (Server.pretrain)
     "pretrain_central_epochs": 0,  # centralised warm start epochs, before any FedAvg warm start

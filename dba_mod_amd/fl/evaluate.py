@@ -18,7 +18,7 @@ full test set; poison = every sample of the non-target subset triggered and rela
 from __future__ import annotations
 
 import logging
-from typing import List, Sequence
+from typing import List, Optional, Sequence
 
 import numpy as np
 import torch
@@ -42,9 +42,12 @@ class Evaluator:
         self.max_groups = int(max_groups)
         self.target = int(wl.params["poison_label_swap"])
 
-    def run(self, bank: torch.Tensor, jobs: Sequence[EvalJob], rank: int = 0, world: int = 1) -> torch.Tensor:
+    def run(self, bank: torch.Tensor, jobs: Sequence[EvalJob], rank: int = 0, world: int = 1,
+            shares: Optional[Sequence[float]] = None) -> torch.Tensor:
         """bank [M, S] model states -> device tensor [J, 3] (loss_sum, correct, count), this
-        rank's shard only (caller all-reduces)."""
+        rank's shard only (caller all-reduces).  ``shares`` (one per rank, summing to 1): rank
+        r takes a contiguous ``shares[r]`` fraction of every test list (load-balanced sharding,
+        :meth:`Server._eval_shares`) instead of the strided ``[rank::world]`` shard."""
         wl = self.wl
         dev = wl.device
         J = len(jobs)
@@ -58,7 +61,13 @@ class Evaluator:
         folded = prog.fold_bank(wl.spec, sub, self.dtype)
         lists = {}
         for kind, idx in (("clean", wl.test_clean_idx), ("poison", wl.test_poison_idx)):
-            lists[kind] = native.shard_index(idx, rank, world) if world > 1 else idx
+            if world <= 1:
+                lists[kind] = idx
+            elif shares is not None:
+                lo, hi = native.share_range(len(idx), shares, rank)
+                lists[kind] = idx[lo:hi]
+            else:
+                lists[kind] = native.shard_index(idx, rank, world)
         for j0 in range(0, J, self.max_groups):
             grp = list(range(j0, min(J, j0 + self.max_groups)))
             self._run_group(folded, [jobs[j] for j in grp], [remap[jobs[j].model] for j in grp],

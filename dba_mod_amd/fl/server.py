@@ -285,10 +285,53 @@ class Server:
             owners, _ = native.lpt_assign(costs, self.d.world)
             mine = [c for c, o in zip(plan.clients, owners) if o == self.d.rank]
         early = _EarlyEval(self, plan) if (evaluate and p["early_local_eval"]) else None
+        load = self._window_loads(plan, owners, early) if self.d.world > 1 else None
         with self.timer.phase("train_enqueue", sync=False):
             handle = self.trainer.train_async(mine, self.global_state, on_client_done=early)
         return {"epoch": epoch, "plan": plan, "owners": owners, "adversarial": adversarial, "t0": t0,
-                "handle": handle, "early": early, "clients_on_rank": len(mine), "evaluate": evaluate}
+                "handle": handle, "early": early, "clients_on_rank": len(mine), "evaluate": evaluate,
+                "load": load}
+
+    def _job_images(self, job) -> int:
+        return len(self.wl.test_clean_idx if job.kind == "clean" else self.wl.test_poison_idx)
+
+    def _window_loads(self, plan: RoundPlan, owners: List[int], early: Optional["_EarlyEval"]) -> List[float]:
+        """Each rank's GPU work while round r's image-sharded tests run (round r+1's training
+        and its clients' early local tests), in eval image-forward units — the base of the
+        water-filling split of those tests (:meth:`_eval_shares`).  Identical on every rank
+        (a pure function of the plan).  A grouped step costs ``balance_step_latency +
+        balance_step_per_client * active``: the latency floor of a lone client's step
+        (1.9 ms at fp32 on MI355X) is worth ~1.2k image forwards of evaluation."""
+        p = self.params
+        lat, per = float(p["balance_step_latency"]), float(p["balance_step_per_client"])
+        world = self.d.world
+        load = [0.0] * world
+        lens: List[List[int]] = [[] for _ in range(world)]
+        for c, o in zip(plan.clients, owners):
+            lens[o].append(len(c.steps))
+        for r in range(world):
+            ls = sorted(lens[r], reverse=True)
+            prev = 0
+            for k in range(len(ls), 0, -1):      # steps with k active clients
+                n = ls[k - 1] - prev
+                if n > 0:
+                    load[r] += n * (lat + per * k)
+                    prev = ls[k - 1]
+        if early is not None:
+            owner_of = {c.name: o for c, o in zip(plan.clients, owners)}
+            for name, js in early.by_client.items():
+                if name in early.late:
+                    continue
+                load[owner_of[name]] += sum(self._job_images(plan.jobs[j]) for j in js)
+        return load
+
+    def _eval_shares(self, jobs, base: Optional[List[float]]) -> Optional[List[float]]:
+        """Per-rank shares of the image-sharded tests ``jobs``: water-filling over ``base``
+        (None: the strided even split)."""
+        if self.d.world <= 1 or base is None or not self.params["eval_balance"]:
+            return None
+        work = float(sum(self._job_images(j) for j in jobs))
+        return native.balance_shares(base, work)
 
     def _train_end(self, st: Dict[str, Any]) -> Dict[str, Any]:
         """Wait for the round's training, gather the snapshots, aggregate."""
@@ -317,16 +360,17 @@ class Server:
     def _train_half(self, epoch: int, evaluate: bool = True) -> Dict[str, Any]:
         return self._train_end(self._train_begin(epoch, evaluate))
 
-    def _launch_eval(self, pend: Dict[str, Any]) -> None:
-        """Enqueue the round's evaluation on the eval stream (returns immediately)."""
+    def _launch_eval(self, pend: Dict[str, Any], base: Optional[List[float]] = None) -> None:
+        """Enqueue the round's evaluation on the eval stream (returns immediately).  ``base``:
+        every rank's load in the window the tests run in (:meth:`_window_loads`)."""
         t0 = time.perf_counter()
         try:
-            self._launch_eval_impl(pend)
+            self._launch_eval_impl(pend, base)
         finally:
             pend["phases"]["launch_eval"] = time.perf_counter() - t0
 
     def _enqueue_eval(self, bank: torch.Tensor, jobs: List[Any], rows: List[int], acc: torch.Tensor,
-                      sharded: bool, stream=None) -> None:
+                      sharded: bool, stream=None, shares: Optional[List[float]] = None) -> None:
         """Evaluate ``jobs`` (models = rows of ``bank``) into ``acc[rows]`` on the eval stream,
         ordered after everything already enqueued on the current (training) stream.
         ``sharded``: this rank takes its ``[rank::world]`` image shard (the all-reduce in
@@ -334,7 +378,8 @@ class Server:
         rank, world = (self.d.rank, self.d.world) if sharded else (0, 1)
         stream = stream if stream is not None else self._eval_stream
         if stream is None:
-            acc.index_add_(0, to_device(rows, self.device, torch.int64), self.evaluator.run(bank, jobs, rank, world))
+            acc.index_add_(0, to_device(rows, self.device, torch.int64),
+                           self.evaluator.run(bank, jobs, rank, world, shares))
             return
         ready = torch.cuda.Event()
         ready.record(torch.cuda.current_stream(self.device))
@@ -344,9 +389,9 @@ class Server:
             # (a freed training-stream block is reused at once by the training stream)
             stream.wait_event(ready)
             idx = to_device(rows, self.device, torch.int64)
-            acc.index_add_(0, idx, self.evaluator.run(bank, jobs, rank, world))
+            acc.index_add_(0, idx, self.evaluator.run(bank, jobs, rank, world, shares))
 
-    def _launch_eval_impl(self, pend: Dict[str, Any]) -> None:
+    def _launch_eval_impl(self, pend: Dict[str, Any], base: Optional[List[float]] = None) -> None:
         plan = pend["plan"]
         early = pend.get("early")
         if early is not None:
@@ -356,7 +401,8 @@ class Server:
         pend["acc"] = acc
         rest = [j for j in range(len(plan.jobs)) if j not in done]
         if rest:
-            self._enqueue_eval(pend["bank"], [plan.jobs[j] for j in rest], rest, acc, sharded=True)
+            rjobs = [plan.jobs[j] for j in rest]
+            self._enqueue_eval(pend["bank"], rjobs, rest, acc, sharded=True, shares=self._eval_shares(rjobs, base))
         if self._eval_stream is not None:
             pend["done"] = torch.cuda.Event()
             pend["done"].record(self._eval_stream)
@@ -411,7 +457,8 @@ class Server:
             out.extend(self._completed)
             self._completed = []
             if self._unlaunched is not None:
-                self._launch_eval(self._unlaunched)
+                # round r-1's tests share the GPUs with round r's training and local tests
+                self._launch_eval(self._unlaunched, base=st.get("load"))
                 self._launched.append(self._unlaunched)
                 self._unlaunched = None
             while len(self._launched) > 1:
@@ -471,7 +518,7 @@ class Server:
         """Snapshot bank + this rank's aggregation inputs + per-client scalars on every rank.
 
         Client snapshots stay on their owner rank.  Only the rows some other rank reads are
-        all-gathered: the snapshots of clients whose tests are image-sharded across ranks
+        broadcast from their owners: the snapshots of clients whose tests are image-sharded across ranks
         (the round's longest clients, or every client without early local tests) and, for
         RFA in gather mode, the final states.  Aggregation itself reduces (``_aggregate``)."""
         S, P = self.spec.S, self.spec.P
@@ -498,19 +545,13 @@ class Server:
                               if j not in done_early and plan.jobs[j].model != 0)
             if (self.params["aggregation_methods"] == C.AGGR_GEO_MED and self._rfa_gather(len(plan.clients))):
                 shared.update(c.final_snap for c in plan.clients)
-            per_rank = [[s for s in sorted(shared) if slot_owner[s] == r] for r in range(world)]
-            k_max = max(len(x) for x in per_rank)
             for s, t in local_snaps.items():
                 bank[s] = t
-            if k_max > 0:
-                local = (torch.stack([local_snaps[s] for s in per_rank[rank]]) if per_rank[rank]
-                         else torch.zeros(0, S, device=self.device))
-                allrows = self.d.all_gather_rows(local, k_max)
-                for r in range(world):
-                    if r == rank:
-                        continue
-                    for i, s in enumerate(per_rank[r]):
-                        bank[s] = allrows[r * k_max + i]
+            # each shared row is broadcast from its owner straight into the bank (every rank
+            # receives each row once; a zero-padded all-gather of [world, k_max] rows would
+            # move world x the bytes when one rank owns the round's long clients)
+            for s in sorted(shared):
+                self.d.broadcast_(bank[s], slot_owner[s])
         mine = [i for i, c in enumerate(plan.clients) if c.name in by_name]
         local_in: Dict[str, Any] = {
             "idx": mine,

@@ -40,6 +40,8 @@ def lib():
                 L.dba_lpt_assign.argtypes = [ctypes.c_int, _F64P, ctypes.c_int, _I32P, _F64P]
                 L.dba_shard_index.restype = ctypes.c_int64
                 L.dba_shard_index.argtypes = [_I64P, ctypes.c_int64, ctypes.c_int, ctypes.c_int, _I64P]
+                L.dba_balance_shares.restype = None
+                L.dba_balance_shares.argtypes = [ctypes.c_int, _F64P, ctypes.c_double, _F64P]
                 L.dba_hash2.restype = ctypes.c_uint32
                 L.dba_hash2.argtypes = [ctypes.c_uint32, ctypes.c_uint32]
                 _LIB = L
@@ -90,6 +92,25 @@ def shard_index(idx: np.ndarray, rank: int, world: int) -> np.ndarray:
     out = np.empty(max(1, (a.shape[0] + world - 1) // world), dtype=np.int64)
     k = lib().dba_shard_index(_p(a, _I64P), a.shape[0], rank, world, _p(out, _I64P))
     return out[:k]
+
+
+def balance_shares(base: Sequence[float], work: float) -> List[float]:
+    """Water-filling shares of ``work`` over ranks already loaded with ``base`` (same units):
+    the least-loaded ranks take the work first, shares sum to 1 (runtime.cpp)."""
+    b = np.ascontiguousarray(base, dtype=np.float64)
+    out = np.zeros(b.shape[0], dtype=np.float64)
+    lib().dba_balance_shares(int(b.shape[0]), _p(b, _F64P), float(work), _p(out, _F64P))
+    return out.tolist()
+
+
+def share_range(n: int, shares: Sequence[float], rank: int) -> Tuple[int, int]:
+    """[lo, hi) of an n-element list owned by ``rank`` under ``shares`` (contiguous blocks,
+    boundaries floor(n * cumulative share), the last one n): every rank computes the same
+    boundaries, so the blocks tile the list exactly."""
+    cum = np.concatenate([[0.0], np.cumsum(np.asarray(shares, dtype=np.float64))])
+    edges = np.minimum(np.floor(cum * n).astype(np.int64), n)
+    edges[-1] = n
+    return int(edges[rank]), int(edges[rank + 1])
 
 
 def hash2(seed: int, counter: int) -> int:

@@ -80,7 +80,8 @@ def _same_rows(a, b):
 def test_fedavg_bitwise_and_bytes(tmp_path, world):
     """FedAvg at world W: bit-identical global model and equal CSV rows vs world 1; the round's
     aggregation moves ONE §5.8-padded fp64 S-vector all-reduce (no snapshot all-gather of the
-    aggregated clients), the only all-gather carries the image-sharded clients' snapshots."""
+    aggregated clients); only the image-sharded clients' snapshots are broadcast, each once,
+    from their owner rank."""
     from dba_mod_amd.parallel.dist import DistCtx
     over = _over(tmp_path)
     rounds = [11, 12]
@@ -94,14 +95,12 @@ def test_fedavg_bitwise_and_bytes(tmp_path, world):
     fedavg = (S + unit - 1) // unit * unit * 8
     for ar, ag, bc in many[0]["comm"]:
         assert ar >= fedavg and ar < fedavg + 64 * 1024, (ar, fedavg)   # + small stats / eval counters
-        assert bc == 0
+        assert ag == 0
     # round 12: the attacker (41) is the round's only long client; only its two snapshots
-    # (pre-scaling, final) are gathered for its image-sharded tests.  (Round 11's clients are
-    # all equally long, so all their tests are sharded and their snapshots gathered.)
-    # (each gathered row is padded to the §5.8 unit like every other collective)
-    u4 = DistCtx(world=world).pad_unit(4)
-    ag12 = many[0]["comm"][1][1]
-    assert ag12 == world * 2 * ((S + u4 - 1) // u4 * u4) * 4, (ag12, S)
+    # (pre-scaling, final) are broadcast for its image-sharded tests.  (Round 11's clients are
+    # all equally long, so all their tests are sharded and their snapshots broadcast.)
+    bc12 = many[0]["comm"][1][2]
+    assert bc12 == 2 * S * 4, (bc12, S)
     assert one[0]["comm"] == [[0, 0, 0]] * len(rounds)
 
 
