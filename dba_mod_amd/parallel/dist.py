@@ -19,12 +19,14 @@ logical reduction points are ``helper.py:218-257`` FedAvg, ``:320-352`` Weiszfel
    broadcast);
 5. a client's local tests run on its owner rank as soon as it finishes training; only the
    snapshots of the clients whose tests are image-sharded across ranks (the round's longest
-   clients) are all-gathered; ONE all-reduce of the ``[jobs, 3]`` counters combines the
-   tests.
+   clients) are broadcast from their owners; the image-sharded tests are split by
+   water-filling over every rank's load in the window (``Server._eval_shares``); ONE
+   all-reduce of the ``[jobs, 3]`` counters combines the tests.
 
 Bucket policy: every collective moves one contiguous flat buffer (never
-per-layer calls), padded to a multiple of world x 7 xGMI links x 4 KiB so each ring chunk
-is equal and 4 KiB aligned, and issued in pieces of at most 64 MB.  ``bytes`` counts the
+per-layer calls); the all-reduce buckets are padded to a multiple of world x 7 xGMI links x
+4 KiB so each ring chunk is equal and 4 KiB aligned, and issued in pieces of at most 64 MB
+(a snapshot broadcast is one unpadded model row, <= 45 MB for the largest model).  ``bytes`` counts the
 payload of every collective (per kind) for tests and the round metrics.  The int64 BN
 counters never enter a float bucket.
 
@@ -183,7 +185,8 @@ def framework_streams(device: torch.device):
     evaluation streams onto a shared hardware queue."""
     key = device.index if device.index is not None else torch.cuda.current_device()
     if key not in _STREAMS:
-        _STREAMS[key] = (torch.cuda.Stream(device, priority=-1), torch.cuda.Stream(device, priority=0),
+        pri = int(os.environ.get("DBA_TRAIN_STREAM_PRIORITY", "-1"))
+        _STREAMS[key] = (torch.cuda.Stream(device, priority=pri), torch.cuda.Stream(device, priority=0),
                          torch.cuda.Stream(device, priority=0))
     return _STREAMS[key]
 
