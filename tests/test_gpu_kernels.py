@@ -229,7 +229,8 @@ def test_bn_train_large_multiblock(H, R, C, Hh):
     dev = torch.device("cuda")
     torch.manual_seed(2)
     G, N = 3, 10
-    assert N * Hh * Hh > hip_ops._BN_SMALL_ROWS
+    if N * Hh * Hh <= hip_ops._BN_SMALL_ROWS:
+        pytest.skip("rows within the single-launch limit (DBA_BN_SMALL_ROWS raised)")
     y = (torch.randn(G, N, Hh, Hh, C, device=dev) * 1.5 - 0.3).bfloat16()
     nvalid = torch.tensor([10, 4, 0], dtype=torch.int32, device=dev)
     gamma = torch.rand(G, C, device=dev) + 0.5
