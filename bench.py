@@ -232,6 +232,7 @@ def _run(args) -> int:
             "rccl_ok": dctx.selfcheck_ok if dctx.backend == "nccl" else None,
             "collective_selfcheck_ok": dctx.selfcheck_ok,
             "backend_repinned_cpu_affinity": dctx.affinity_changed,
+            "hw_queues": dctx.hw_queues, "train_stream_priority": os.environ.get("DBA_TRAIN_STREAM_PRIORITY", "-1"),
             "comm_bytes_per_round": comm_mean,
             "ops_backend": ops.backend_name(dctx.device),
             "fp32_split": _split_label(server),

@@ -70,6 +70,8 @@ class DistCtx:
     selfcheck_ok: Optional[bool] = None   # init-time all-reduce self-check (None: no group)
     pg: bool = False                # a torch.distributed process group exists
     affinity_changed: Optional[bool] = None   # the backend's init re-pinned the host thread
+    hw_queues: Optional[str] = None           # GPU_MAX_HW_QUEUES of this process (GPU groups)
+    queue_policy: bool = False                # configure_hip_queues applied
 
     @property
     def is_main(self) -> bool:
@@ -191,11 +193,40 @@ def framework_streams(device: torch.device):
     return _STREAMS[key]
 
 
+# Hardware queues and stream priorities of a process that holds an RCCL communicator.  A live
+# communicator stops a high-priority stream from running concurrently with a default-priority
+# one (tools/launch_probe two-stream check: overlap 1.23x without a communicator, 0.82x with
+# one — slower than serial), which costs the overlapped round (evaluation under latency-bound
+# training) 26 %: world-1 group 2.04 vs 2.75 rounds/s.  Measured on one box
+# (profiles/prio_r3/, 12 rounds each): with the communicator, default-priority streams on 6 or
+# 8 hardware queues run at 2.83 (= no communicator, 2.75-2.82); 4 queues 2.44, 16 queues 2.09,
+# high priority on 8 queues 1.99.  Without a communicator the HIP defaults (4 queues, high-
+# priority training) are the best (8 queues: 2.04-2.07).  So ranks that create a communicator
+# take 8 queues and default priority; the variable must be set before HIP initialises.
+PG_HW_QUEUES = "8"
+
+
+def configure_hip_queues(world: int, force_pg: bool) -> bool:
+    """Apply the communicator-process queue / priority policy (before any HIP call).  Returns
+    whether it was applied.  ``DBA_HW_QUEUES=keep`` leaves the environment alone."""
+    if not (world > 1 or force_pg) or os.environ.get("DBA_HW_QUEUES") == "keep":
+        return False
+    if torch.cuda.is_initialized():
+        return False                      # too late: HIP read its queue count at init
+    os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("DBA_HW_QUEUES", PG_HW_QUEUES)
+    os.environ.setdefault("DBA_TRAIN_STREAM_PRIORITY", "0")
+    return True
+
+
 def init_distributed(prefer_gpu: bool = True, timeout_s: int = 1800) -> DistCtx:
     """Initialise from torchrun's env (RANK/WORLD_SIZE/LOCAL_RANK/MASTER_*); world 1 otherwise."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    force_pg = os.environ.get("DBA_FORCE_PG") == "1" and "MASTER_PORT" in os.environ
+    backend_env = os.environ.get("DBA_DIST_BACKEND")
+    queues = (configure_hip_queues(world, force_pg) if prefer_gpu and backend_env in (None, "nccl")
+              else False)
     use_gpu = prefer_gpu and torch.cuda.is_available()
     # rehearsal knobs for a one-GPU box: DBA_SHARE_GPU=1 puts every rank on device 0 and
     # DBA_DIST_BACKEND=gloo replaces RCCL (which refuses two ranks on one GPU)
@@ -205,7 +236,6 @@ def init_distributed(prefer_gpu: bool = True, timeout_s: int = 1800) -> DistCtx:
         device = torch.device("cuda", dev_index)
     else:
         device = torch.device("cpu")
-    force_pg = os.environ.get("DBA_FORCE_PG") == "1" and "MASTER_PORT" in os.environ
     if world <= 1 and not force_pg:
         return DistCtx(0, 1, 0, device, "none")
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -225,6 +255,8 @@ def init_distributed(prefer_gpu: bool = True, timeout_s: int = 1800) -> DistCtx:
     if not dist.is_initialized():
         dist.init_process_group(**kw)
     ctx = DistCtx(rank, world, dev_index, device, backend, pg=True)
+    ctx.hw_queues = os.environ.get("GPU_MAX_HW_QUEUES") if use_gpu else None
+    ctx.queue_policy = queues
     ctx.selfcheck_ok = selfcheck(ctx) if os.environ.get("DBA_PG_SKIP_SELFCHECK") != "1" else None
     if aff is not None and os.environ.get("DBA_KEEP_RCCL_AFFINITY") != "1":
         ctx.affinity_changed = os.sched_getaffinity(0) != aff
