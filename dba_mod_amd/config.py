@@ -108,7 +108,7 @@ _DEFAULTS: Dict[str, Any] = {
     # window (training of the next round + its local tests), in eval image-forward units:
     # one grouped training step costs balance_step_latency + balance_step_per_client * active
     "eval_balance": True,
-    "balance_step_latency": 1200.0,
+    "balance_step_latency": 2400.0,
     "balance_step_per_client": 420.0,
     "rfa_mode": "auto",            # RFA across ranks: gather | distributed | auto (fewer bytes)
     "pretrain_rounds": 0,          # benign FedAvg warm start when not resuming (Server.pretrain)

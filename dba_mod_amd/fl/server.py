@@ -301,7 +301,9 @@ class Server:
         water-filling split of those tests (:meth:`_eval_shares`).  Identical on every rank
         (a pure function of the plan).  A grouped step costs ``balance_step_latency +
         balance_step_per_client * active``: the latency floor of a lone client's step
-        (1.9 ms at fp32 on MI355X) is worth ~1.2k image forwards of evaluation."""
+        (1.75 ms at fp32 on MI355X, ~1.2k image forwards of evaluation) is weighted double: evaluation
+        kernels running beside it stretch the latency-bound chain (emulated same-box sweep:
+        profiles/balance_sweep_r3/)."""
         p = self.params
         lat, per = float(p["balance_step_latency"]), float(p["balance_step_per_client"])
         world = self.d.world
