@@ -11,6 +11,7 @@
 //             forward output) + one fused apply that also emits the residual-branch grad.
 #include "common.hpp"
 #include <algorithm>
+#include <cstdlib>
 
 namespace {
 
@@ -375,6 +376,78 @@ __global__ void bn_bwd_finalize_kernel(const float* __restrict__ part, int nblk,
 }
 
 
+// Backward apply with the finalize folded in, for small launches (a lone client's grouped
+// step, where the separate finalize launch is ~5 us of latency for a few KB of work): every
+// block first sums its replica's reduce partials for ALL channels itself — sum_partials, the
+// finalize's exact fixed order, rounded to fp32 like the finalize's stored sums — so the
+// coefficients, and every output bit, equal the reduce / finalize / apply path; block 0 alone
+// accumulates dgamma / dbeta.  The partials are 2 * C * nblk = 8192 fp32 per replica for every
+// ResNet stage (rows_per_block), L2-resident after the first block of an XCD reads them; the
+// grid is capped (grid-stride rows) so few blocks repeat the sum.
+template <typename T>
+__global__ __launch_bounds__(256) void bn_bwd_apply_fin_kernel(
+    const T* __restrict__ dout, const T* __restrict__ out, const T* __restrict__ y, const float* __restrict__ mean,
+    const float* __restrict__ invstd, const float* __restrict__ gamma, long long p_gstride,
+    const float* __restrict__ part, int nblk, float* __restrict__ dgamma, float* __restrict__ dbeta,
+    long long g_gstride, int relu, T* __restrict__ dy, T* __restrict__ dres, const int* __restrict__ nvalid, int N,
+    int HW, int C, int* __restrict__ amax, int amax_ld) {
+  __shared__ float sums[2][2048];              // C <= 2048 (bn_layout_ok)
+  const int g = blockIdx.y;
+  const int c8 = C / 8;
+  const int nv = valid_rows(nvalid, g, N) * HW;
+  const int total = nv * c8;
+  if (blockIdx.x != 0 && (int)(blockIdx.x * blockDim.x) >= total) return;   // block-uniform
+  const int cpb = bn_cpb(C);
+  for (int cb = 0; cb < C; cb += cpb) {
+    const int c = cb + (int)(threadIdx.x % cpb);
+    double s0, s1;
+    sum_partials(part, nblk, C, g, c, c < C, s0, s1);
+    if ((int)threadIdx.x < cpb && c < C) {
+      sums[0][c] = (float)s0;
+      sums[1][c] = (float)s1;
+      if (blockIdx.x == 0) {
+        dbeta[(long long)g * g_gstride + c] += (float)s0;
+        dgamma[(long long)g * g_gstride + c] += (float)s1;
+      }
+    }
+    __syncthreads();   // sum_partials' LDS is reused by the next channel group
+  }
+  const int tid0 = blockIdx.x * blockDim.x + threadIdx.x;
+  if ((int)(blockIdx.x * blockDim.x) >= total) return;
+  const int c0 = (tid0 % c8) * 8;
+  const float n = (float)nv;
+  float A[8], B[8], K[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const int c = c0 + e;
+    const float is = invstd[g * C + c];
+    const float ga = gamma[(long long)g * p_gstride + c] * is;
+    const float sd = sums[0][c];
+    const float sdx = sums[1][c];
+    A[e] = ga;
+    B[e] = -ga * is * sdx / n;
+    K[e] = -ga * sd / n - B[e] * mean[g * C + c];
+  }
+  const long long base = (long long)g * N * HW * c8;
+  float vmax = 0.f;
+  for (int t = tid0; t < total; t += gridDim.x * blockDim.x) {
+    const long long o = (base + t) * 8;
+    float dp[8], yp[8], op[8], p1[8];
+    ld8(dout + o, dp);
+    ld8(y + o, yp);
+    if (relu) ld8(out + o, op);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      if (relu && !(op[e] > 0.f)) dp[e] = 0.f;
+      p1[e] = fmaf(A[e], dp[e], fmaf(B[e], yp[e], K[e]));
+      vmax = fmaxf(vmax, fabsf(p1[e]));
+    }
+    st8(dy + o, p1);
+    if (dres) st8(dres + o, dp);
+  }
+  if (amax) amax_fold(amax, amax_ld, g, vmax);
+}
+
 // ---------------------------------------------------------------- narrow-spatial layers
 // One block owns 8 channels of one replica for ALL of its valid rows (<= 16K rows: ResNet
 // stages 2-4 at batch 64), so statistics, finalize (running stats), and apply — or the
@@ -626,6 +699,18 @@ __global__ void bn_fold_kernel(const float* __restrict__ w, long long w_sstride,
 
 int egrid(long long n) { return (int)std::max(1LL, std::min(16384LL, (n + 255) / 256)); }
 
+int env_int(const char* name, int dflt) {
+  const char* e = getenv(name);
+  return e ? atoi(e) : dflt;
+}
+
+// launches of at most this many replicas fold the backward finalize into the apply
+// (DBA_BN_BWD_FUSE_G, default 4; 0 = off; dba_bn_bwd_fuse_set for tests)
+int& bwd_fuse_g() {
+  static int g = env_int("DBA_BN_BWD_FUSE_G", 4);
+  return g;
+}
+
 // per-replica grid for the row-gated elementwise passes: ~16K blocks over the launch
 dim3 ggrid(int G, int N, int HW, int C) {
   const long long per = (long long)N * HW * (C / 8);
@@ -636,6 +721,13 @@ dim3 ggrid(int G, int N, int HW, int C) {
 }  // namespace
 
 DBA_EXPORT int dba_bn_partial_blocks(int N, int HW, int C) { return ceil_div((long long)N * HW, rows_per_block(C)); }
+
+// folded backward finalize for launches of <= g replicas (0: off); returns the previous value
+DBA_EXPORT int dba_bn_bwd_fuse_set(int g) {
+  const int prev = bwd_fuse_g();
+  if (g >= 0) bwd_fuse_g() = g;
+  return prev;
+}
 
 // Channel-layout contract of every BN launcher (returns -102 otherwise): C % 8 == 0 and
 // 256 % (C / 8) == 0, so a thread of the grid-stride elementwise passes always owns the same
@@ -703,6 +795,16 @@ DBA_EXPORT int dba_bn_bwd(const void* dout, const void* out, const void* y, cons
   }
   BN_T(f32, hipLaunchKernelGGL((bn_reduce_kernel<true, T>), dim3(nblk, G), dim3(256), 0, st, (const T*)y,
                                (const T*)dout, (const T*)out, mean, invstd, relu, nvalid, N, HW, C, part, fin));
+  // launches of few replicas (a lone client's step): the finalize folds into the apply
+  // (bn_bwd_apply_fin_kernel, same bits); DBA_BN_BWD_FUSE_G=0 keeps three launches
+  if (!counter && G <= bwd_fuse_g()) {
+    dim3 ga = ggrid(G, N, HW, C);
+    ga.x = std::min(ga.x, 128u);
+    BN_T(f32, hipLaunchKernelGGL((bn_bwd_apply_fin_kernel<T>), ga, dim3(256), 0, st, (const T*)dout, (const T*)out,
+                                 (const T*)y, mean, invstd, gamma, p_gstride, part, nblk, dgamma, dbeta, g_gstride,
+                                 relu, (T*)dy, (T*)dres, nvalid, N, HW, C, amax, amax_ld));
+    DBA_LAUNCH_CHECK();
+  }
   if (!counter)
     hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(ceil_div(C, C < 64 ? C : 64), G), dim3(256), 0, st, part, nblk,
                        sums, dgamma, dbeta, g_gstride, G, C);

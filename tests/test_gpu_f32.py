@@ -557,6 +557,45 @@ def test_halo_ws_bitwise_vs_tiled(H, R64, case, presplit):
         H.set_fp32_planes(prev)
 
 
+@pytest.mark.parametrize("G,C,Hh,N", [(1, 32, 32, 64), (3, 64, 16, 20), (2, 128, 8, 64), (4, 256, 8, 9)])
+@pytest.mark.parametrize("relu,with_res", [(True, False), (True, True), (False, False)])
+def test_bn_bwd_folded_finalize_bitwise(H, G, C, Hh, N, relu, with_res):
+    """Backward BN with the finalize folded into the apply (bn_bwd_apply_fin_kernel, small
+    launches) is bit-identical to reduce / finalize / apply: dy, the residual gradient, the
+    accumulated dgamma / dbeta and the fp16-pair max slot."""
+    dev = torch.device("cuda")
+    torch.manual_seed(3)
+    y = torch.randn(G, N, Hh, Hh, C, device=dev) * 1.7 - 0.2
+    nvalid = torch.tensor([N, max(1, N - 5), 0, N][:G], dtype=torch.int32, device=dev)
+    gamma = torch.rand(G, C, device=dev) + 0.5
+    beta = torch.randn(G, C, device=dev)
+    rm, rv = torch.zeros(G, C, device=dev), torch.ones(G, C, device=dev)
+    res = torch.randn_like(y) if with_res else None
+    out, mean, invstd = H.bn_train(y, gamma, beta, rm, rv, nvalid, 0.1, 1e-5, relu, res)
+    dout = torch.randn_like(y)
+    seed_g, seed_b = torch.randn(G, C, device=dev), torch.randn(G, C, device=dev)
+    res_by = []
+    prev = H.set_bn_bwd_fuse(-1)
+    try:
+        for fuse in (8, 0):
+            H.set_bn_bwd_fuse(fuse)
+            dg, db = seed_g.clone(), seed_b.clone()
+            r = H.bn_train_bwd(dout, y, out, mean, invstd, gamma, nvalid, relu, dg, db, want_dres=with_res)
+            dyh, dres = r if with_res else (r, None)
+            res_by.append((dyh, dres, dg, db, getattr(dyh, "_dba_amax", None)))
+    finally:
+        H.set_bn_bwd_fuse(prev)
+    (a, ra, ga, ba, ma), (b, rb, gb, bb, mb) = res_by
+    for g in range(G):
+        n = int(nvalid[g])
+        assert torch.equal(a[g, :n], b[g, :n])
+        if with_res:
+            assert torch.equal(ra[g, :n], rb[g, :n])
+    assert torch.equal(ga, gb) and torch.equal(ba, bb)
+    if ma is not None:
+        assert torch.equal(ma, mb)
+
+
 def test_halo_ws_bn_partials_bitwise(H):
     """Training forward with fused BN statistics through the persistent halo conv: the fp64
     partials (incl. the zeroed groups of invalid images) equal the per-tile kernel's."""
