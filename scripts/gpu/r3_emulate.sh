@@ -9,7 +9,7 @@ TAG=${TAG:-emu}
 mkdir -p gpurun_out/r3/$TAG
 for N in ${WORLDS:-2 4 8}; do
   for R in $(seq 0 $((N - 1))); do
-    timeout -k 10 300 python bench.py --emulate-rank $R --emulate-world $N --steps $ROUNDS --warmup 2 \
+    timeout -k 10 300 python bench.py --emulate-rank $R --emulate-world $N --steps $ROUNDS --warmup ${WARMUP:-2} \
       ${DBA_EMU_SET:+--set $DBA_EMU_SET} > gpurun_out/r3/$TAG/emu_${N}_${R}.log 2>&1 || { tail -20 gpurun_out/r3/$TAG/emu_${N}_${R}.log; exit 1; }
     echo "N=$N R=$R $(grep -o '"ms_per_step": [0-9.]*' gpurun_out/r3/$TAG/emu_${N}_${R}.log) $(grep -o '"train_enqueue": [0-9.]*' gpurun_out/r3/$TAG/emu_${N}_${R}.log) $(grep -o '"eval_wait": [0-9.]*' gpurun_out/r3/$TAG/emu_${N}_${R}.log)"
   done
