@@ -1762,8 +1762,11 @@ int xsplitk(long long M, int /*G*/, int Ncol, int K) {
   const long long tiles = (long long)ceil_div(M, 64) * ceil_div(Ncol, bn);
   if (tiles >= target) return 1;
   const int nkt = (K + 31) / 32;
-  int s = (int)std::min<long long>(8, (target + tiles - 1) / tiles);
-  while (s > 1 && nkt / s < 8) --s;
+  // a slab keeps >= DBA_F32_SPLITK_MINK k-steps (default 8), at most DBA_F32_SPLITK_MAX slabs
+  static const int mink = std::max(1, env_int("DBA_F32_SPLITK_MINK", 8));
+  static const int smax = std::max(1, env_int("DBA_F32_SPLITK_MAX", 8));
+  int s = (int)std::min<long long>(smax, (target + tiles - 1) / tiles);
+  while (s > 1 && nkt / s < mink) --s;
   return s;
 }
 
@@ -1944,7 +1947,8 @@ DBA_EXPORT long long dba_xwgrad_ws_floats(int G, int N, int Ho, int Wo, int Cin,
   const long long tiles = (long long)ceil_div(Cout, bno) * ceil_div(K, 128);
   const long long M = (long long)N * Ho * Wo;
   const int target = env_int("DBA_F32_WGRAD_BLOCKS", 256);
-  long long Z = std::max(1LL, std::min((target + tiles - 1) / tiles, M / 256));
+  static const int minrows = std::max(32, env_int("DBA_F32_WGRAD_MINROWS", 256));   // rows per slab
+  long long Z = std::max(1LL, std::min((target + tiles - 1) / tiles, M / minrows));
   int mchunk = (int)((M + Z - 1) / Z);
   mchunk = (mchunk + 31) / 32 * 32;
   Z = (M + mchunk - 1) / mchunk;
