@@ -75,6 +75,21 @@ class Tape:
             self.on_end()
 
 
+_WGRAD_STREAMS: Dict[int, "torch.cuda.Stream"] = {}
+
+
+def _wgrad_stream(device: torch.device) -> Optional["torch.cuda.Stream"]:
+    """The per-device side stream weight gradients run on (``DBA_WGRAD_STREAM=1``; default off:
+    launch on the caller's stream).  Same priority as the training stream."""
+    if os.environ.get("DBA_WGRAD_STREAM", "0") == "0":
+        return None
+    key = device.index if device.index is not None else torch.cuda.current_device()
+    if key not in _WGRAD_STREAMS:
+        pri = int(os.environ.get("DBA_TRAIN_STREAM_PRIORITY", "-1"))
+        _WGRAD_STREAMS[key] = torch.cuda.Stream(device, priority=pri)
+    return _WGRAD_STREAMS[key]
+
+
 class Ctx:
     """Per-forward context: where the weights live, which mode, the tape.
 
@@ -99,10 +114,15 @@ class Ctx:
         # weight-gradient slab reductions of the whole backward pass, run as one launch when
         # it ends (ops.wgrad_flush)
         self._wdefer: List[tuple] = []
+        # weight gradients on a side stream (GPU training): they feed only the end-of-pass slab
+        # reduction and the SGD, so they run beside the data-gradient / BN chain that bounds a
+        # latency-bound step; joined before the reduction (_end_backward)
+        self._side = _wgrad_stream(state.device) if (train and state is not None and state.is_cuda) else None
+        self._side_used = False
+        self._side_keep: List[Tensor] = []
         if self.tape is not None:
             self.tape.on_begin = self._prepare_dgrad
-            self.tape.on_end = lambda: (ops.backend_for(self.state).wgrad_flush(self._wdefer)
-                                        if self._wdefer else None)
+            self.tape.on_end = self._end_backward
         self.dropout_seed = dropout_seed
         self._drop_ctr = 0
         self.act_dtype = act_dtype
@@ -129,6 +149,26 @@ class Ctx:
     def _want_dgrad(self, w: Tensor, stride: int, pad: int, in_hw: Tuple[int, int], G: int) -> int:
         self._dgrad_items.append((w, self.wsel, stride, pad, in_hw, self.nvalid, G))
         return len(self._dgrad_items) - 1
+
+    def _end_backward(self) -> None:
+        if self._side_used:
+            torch.cuda.current_stream(self._side.device).wait_stream(self._side)
+            self._side_used = False
+        if self._wdefer:
+            ops.backend_for(self.state).wgrad_flush(self._wdefer)
+        self._side_keep.clear()     # the operands the side stream read (alive until the join)
+
+    def _wgrad(self, dy: Tensor, x: Tensor, fn: Callable[[], None]) -> None:
+        """Run the weight-gradient launch ``fn`` (reading ``dy`` and ``x``) on the side stream."""
+        if self._side is None:
+            fn()
+            return
+        ops.wgrad_prepare(dy, x, self.nvalid)      # operand maxima on the main stream
+        self._side.wait_stream(torch.cuda.current_stream(self._side.device))
+        with torch.cuda.stream(self._side):
+            fn()
+        self._side_used = True
+        self._side_keep.extend((dy, x))
 
     def _prepare_dgrad(self) -> None:
         if self._dgrad_items:
@@ -176,7 +216,8 @@ class Ctx:
                                  self.g(bn + ".weight"), self.g(bn + ".bias"),
                                  want_dres=residual is not None)
             dy, dres = r if residual is not None else (r, None)
-            ops.conv2d_wgrad(dy, x, stride, pad, kh, kw, self.g(conv), nvalid=self.nvalid, defer=self._wdefer)
+            self._wgrad(dy, x, lambda: ops.conv2d_wgrad(dy, x, stride, pad, kh, kw, self.g(conv), nvalid=self.nvalid,
+                                                        defer=self._wdefer))
             dx = None
             if need_dx:
                 # the other consumer of x (shortcut branch) already delivered its gradient
@@ -204,8 +245,9 @@ class Ctx:
 
         def bwd(dout: Tensor):
             d = ops.relu_mask_bwd(dout, y) if relu else dout
-            ops.conv2d_wgrad(d, x, stride, pad, kh, kw, self.g(name),
-                             self.g(bias) if bias is not None else None, nvalid=self.nvalid, defer=self._wdefer)
+            self._wgrad(d, x, lambda: ops.conv2d_wgrad(d, x, stride, pad, kh, kw, self.g(name),
+                                                       self.g(bias) if bias is not None else None, nvalid=self.nvalid,
+                                                       defer=self._wdefer))
             return (ops.conv2d_dgrad(d, w, self.wsel, stride, pad, in_hw, nvalid=self.nvalid, wt=self._wt.get(k))
                     if need_dx else None,)
 
@@ -239,8 +281,9 @@ class Ctx:
 
         def bwd(dout: Tensor):
             d = ops.relu_mask_bwd(dout, y) if relu else dout
-            ops.conv2d_wgrad(d, x4, 1, 0, 1, 1, gv.reshape(gv.shape[0], gv.shape[1], 1, 1, gv.shape[2]),
-                             self.g(bias), nvalid=self.nvalid, defer=self._wdefer)
+            self._wgrad(d, x4, lambda: ops.conv2d_wgrad(d, x4, 1, 0, 1, 1,
+                                                        gv.reshape(gv.shape[0], gv.shape[1], 1, 1, gv.shape[2]),
+                                                        self.g(bias), nvalid=self.nvalid, defer=self._wdefer))
             return (ops.conv2d_dgrad(d, w, self.wsel, 1, 0, (1, 1), nvalid=self.nvalid, wt=self._wt.get(k))
                     if need_dx else None,)
 

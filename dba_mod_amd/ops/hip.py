@@ -823,6 +823,16 @@ def conv2d_wgrad(dy, x, stride, pad, kh, kw, dw, dbias=None, nvalid=None, defer=
               dbias.data_ptr(), dbias.stride(0), _stream())
 
 
+def wgrad_prepare(dy, x, nvalid=None):
+    """Attach the fp16-pair operand maxima of a weight gradient's ``dy`` and ``x`` on the
+    CURRENT stream.  Called before the weight gradient moves to the side stream
+    (models/program.py): a max computed there would be read unordered by the data gradient,
+    which runs on the main stream and shares ``dy``'s max slot."""
+    if _MODE == F16_PAIR and "wgrad" in _H_OPS and dy.dtype == _F32:
+        _amax_act(_act(dy, None, "wgrad dy"), nvalid)
+        _amax_act(_act(x, _F32, "wgrad x"), nvalid)
+
+
 def wgrad_flush(defer):
     """Run the weight-gradient slab reductions queued by ``conv2d_wgrad(..., defer=)``."""
     if not defer:

@@ -134,6 +134,12 @@ def conv2d(x: Tensor, w: Tensor, wsel: Optional[Tensor], stride: int, pad: int,
     return torch.stack(outs).to(out_dtype or x.dtype)
 
 
+def wgrad_prepare(dy, x, nvalid=None):
+    """HIP backend: attaches the operands' fp16-pair maxima before the weight gradient moves to
+    a side stream.  Nothing to prepare here."""
+    return None
+
+
 def wgrad_flush(defer: list) -> None:
     """Backend hook for deferred weight-gradient reductions; the reference has none."""
     if defer:
