@@ -4,11 +4,13 @@ client outlasts every other by at least SOLO_MIN_STEPS steps (the 6-epoch attack
 the two paths is covered by the bitwise world-1 / world-2 and reproducibility GPU tests."""
 from types import SimpleNamespace
 
+import torch
+
 from dba_mod_amd.fl.trainer import GroupTrainer
 
 
-def _tail(lens, use_graph=True, min_steps=4):
-    self = SimpleNamespace(use_graph=use_graph, SOLO_MIN_STEPS=min_steps)
+def _tail(lens, use_graph=True, min_steps=4, dtype=torch.float32):
+    self = SimpleNamespace(use_graph=use_graph, SOLO_MIN_STEPS=min_steps, dtype=dtype)
     clients = [SimpleNamespace(steps=[None] * n) for n in lens]
     return GroupTrainer._solo_tail(self, clients, max(lens))
 
@@ -28,3 +30,9 @@ def test_solo_tail_off_without_graphs_or_group():
     assert _tail([18, 54], use_graph=False) is None
     assert _tail([54]) is None
     assert _tail([18, 54], min_steps=0) is None
+
+
+def test_solo_tail_fp32_family_only():
+    # the bf16 family's tile / split-K choices follow the launch's replica count, so moving a
+    # client to the one-replica graph would change its rounding: no solo tail there
+    assert _tail([18, 54], dtype=torch.bfloat16) is None
