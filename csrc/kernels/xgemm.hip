@@ -1509,34 +1509,34 @@ __global__ __launch_bounds__(256) void xsplit_w_kernel(const float* __restrict__
 }
 
 // output bound of an evaluation conv per weight slot (PairAct): out[slot] = {max over rows of
-// sum |w[row][k]|, max |bias|}.  One block per slot; each row's L1 is one thread's sequential
-// fp32 sum (relative rounding <= K * 2^-24; the 2x in the exponent choice covers it), x (1 + 2^-10).
+// sum |w[row][k]|, max |bias|}; each row's L1 is an fp32 sum (relative rounding <= K * 2^-24;
+// the 2x in the exponent choice covers it), x (1 + 2^-9).
+// Grid (slots, row groups of 16): each wave
+// sums whole rows with coalesced loads (lanes stride the row, a fixed shuffle tree), the
+// block's max row goes to out[2 * slot] by an integer atomicMax on the non-negative float bits
+// (exact and order-independent, so the bound is deterministic); out must be zeroed.  The
+// former one-block-per-slot form walked each row with one thread (uncoalesced, ~95 us per
+// eval fold launch, 3.8 % of the bench's kernel time: profiles/r3_bench_kernel_stats.csv).
 __global__ __launch_bounds__(256) void row_bound_kernel(const float* __restrict__ w, long long w_sstride, int rows,
                                                         int rowlen, const float* __restrict__ bias,
                                                         long long b_sstride, float* __restrict__ out) {
-  __shared__ float red[2][256];
-  const int sl = blockIdx.x, tid = threadIdx.x;
+  const int sl = blockIdx.x, lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const float* __restrict__ ws = w + (long long)sl * w_sstride;
-  float l1 = 0.f, bm = 0.f;
-  for (int r = tid; r < rows; r += 256) {
+  float l1 = 0.f;
+  const int r0 = blockIdx.y * 16;
+  for (int r = r0 + wv; r < min(rows, r0 + 16); r += 4) {
+    const float* __restrict__ row = ws + (long long)r * rowlen;
     float acc = 0.f;
-    for (int k = 0; k < rowlen; ++k) acc += fabsf(ws[(long long)r * rowlen + k]);
-    l1 = fmaxf(l1, acc * (1.f + 0x1p-10f));
-    if (bias) bm = fmaxf(bm, fabsf(bias[(long long)sl * b_sstride + r]));
+    for (int k = lane; k < rowlen; k += 64) acc += fabsf(row[k]);
+    acc = wave_sum(acc);
+    l1 = fmaxf(l1, acc * (1.f + 0x1p-9f));   // covers the fp32 rounding of any summation order
   }
-  red[0][tid] = l1;
-  red[1][tid] = bm;
-  __syncthreads();
-  for (int st = 128; st > 0; st >>= 1) {
-    if (tid < st) {
-      red[0][tid] = fmaxf(red[0][tid], red[0][tid + st]);
-      red[1][tid] = fmaxf(red[1][tid], red[1][tid + st]);
-    }
-    __syncthreads();
-  }
-  if (tid == 0) {
-    out[2 * sl] = red[0][0];
-    out[2 * sl + 1] = red[1][0];
+  if (lane == 0) atomicMax(reinterpret_cast<int*>(out) + 2 * sl, __float_as_int(l1));
+  if (bias && blockIdx.y == 0) {
+    float bm = 0.f;
+    for (int r = threadIdx.x; r < rows; r += 256) bm = fmaxf(bm, fabsf(bias[(long long)sl * b_sstride + r]));
+    bm = wave_max(bm);
+    if (lane == 0) atomicMax(reinterpret_cast<int*>(out) + 2 * sl + 1, __float_as_int(bm));
   }
 }
 
@@ -2058,8 +2058,8 @@ DBA_EXPORT int dba_amax(const float* x, long long gstride, long long n_per_g, co
 // out [slots][2]: {max row L1 of w [slots][rows][rowlen], max |bias|} (bias optional)
 DBA_EXPORT int dba_row_bound(const float* w, long long w_sstride, int rows, int rowlen, const float* bias,
                              long long b_sstride, int slots, float* out, void* stream) {
-  hipLaunchKernelGGL(row_bound_kernel, dim3(slots), dim3(256), 0, (hipStream_t)stream, w, w_sstride, rows, rowlen,
-                     bias, b_sstride, out);
+  hipLaunchKernelGGL(row_bound_kernel, dim3(slots, ceil_div(rows, 16)), dim3(256), 0, (hipStream_t)stream, w,
+                     w_sstride, rows, rowlen, bias, b_sstride, out);
   DBA_LAUNCH_CHECK();
 }
 

@@ -969,7 +969,7 @@ def row_bound(w, bias):
     slots, Cout = w.shape[0], w.shape[1]
     per = w[0].numel()
     wv, ws = _rowview(w)
-    out = torch.empty(slots, 2, dtype=torch.float32, device=w.device)
+    out = torch.zeros(slots, 2, dtype=torch.float32, device=w.device)   # atomic-max target
     bv, bs = _rowview(bias) if bias is not None else (None, 0)
     _call("dba_row_bound", wv.data_ptr(), ws, Cout, per // Cout, _ptr(bv), bs, slots, out.data_ptr(), _stream())
     return out

@@ -596,6 +596,22 @@ def test_bn_bwd_folded_finalize_bitwise(H, G, C, Hh, N, relu, with_res):
         assert torch.equal(ma, mb)
 
 
+@pytest.mark.parametrize("slots,Cout,K", [(1, 32, 27), (17, 32, 288), (5, 256, 2304), (3, 10, 256), (2, 70, 33)])
+def test_row_bound(H, slots, Cout, K):
+    """PairAct output bound per weight slot: {max row L1 of w, max |bias|} — an upper bound
+    within 2^-8 of the fp64 value, identical run to run."""
+    dev = torch.device("cuda")
+    g0 = torch.Generator().manual_seed(slots * 7 + K)
+    w = (torch.randn(slots, Cout, 1, 1, K, generator=g0) * torch.rand(slots, Cout, 1, 1, 1, generator=g0)).to(dev)
+    b = torch.randn(slots, Cout, generator=g0).to(dev)
+    out = H.row_bound(w, b)
+    l1 = w.double().abs().sum(-1).reshape(slots, Cout).amax(1)
+    assert torch.all(out[:, 0].double() >= l1) and torch.all(out[:, 0].double() <= l1 * (1 + 2 ** -8))
+    assert torch.equal(out[:, 1], b.abs().amax(1))
+    assert torch.equal(H.row_bound(w, b), out)
+    assert torch.equal(H.row_bound(w, None)[:, 1], torch.zeros(slots, device=dev))
+
+
 def test_halo_ws_bn_partials_bitwise(H):
     """Training forward with fused BN statistics through the persistent halo conv: the fp64
     partials (incl. the zeroed groups of invalid images) equal the per-tile kernel's."""
