@@ -15,14 +15,16 @@
 // f32 MFMA (157 TF).  The split costs 2.5 VALU ops per element (v_cvt_pk_bf16_f32,
 // shift/mask, v_pk_add_f32, v_cvt_pk_bf16_f32), done once per staged element.
 //
-// Kernels (all deterministic: no atomics, fixed reduction orders):
+// Kernels (all deterministic: fixed reduction orders, no float atomics; the in-launch split-K
+// combine draws integer arrival tickets that only pick WHICH block sums the slabs):
 //   xconv_kernel    implicit-GEMM conv forward (bias / residual / ReLU epilogue) and data
 //                   gradient; a stride-s data gradient runs as s*s parity classes, each an
 //                   implicit GEMM over its own taps (no zero-tap MFMA work), in one launch;
 //   xwgrad_kernel   weight gradient: C[cout][k] = sum_m dy[m][cout] * im2col(x)[m][k], both
 //                   operands transposed to reduction-major while staging; split over m into
 //                   fp32 slabs summed in a fixed order by xwgrad_reduce_kernel;
-//   xsplitk_reduce  split-K slabs of small forward launches + epilogue;
+//   xsplitk_reduce  split-K slabs of small forward launches + epilogue (when the caller has
+//                   no arrival counters: otherwise sk_combine sums them in the launch);
 //   xtranspose      forward weights -> parity-class packed data-gradient weights;
 //   xcolsum         bias gradient (column sums, fixed order).
 #include "common.hpp"
@@ -292,8 +294,72 @@ struct XArgs {
   const float* bound;
   const int* amax_res; int amax_res_ld;
   const int* res_sexp;
+  // in-launch split-K combine (xconv_kernel sk_combine): slab z of replica g at
+  // sk_ws + z * zstride + g * sk_gstride; sk_cnt: zeroed arrival counters, one per
+  // (replica, tile, class); out / out_gstride stay the real output
+  float* sk_ws; long long sk_gstride;
+  int* sk_cnt;
   XClass cls[4];
 };
+
+typedef __attribute__((ext_vector_type(4))) unsigned int u32x4v;
+
+// In-launch split-K combine (the CDNA4 guide's counter hand-off, write-through form): every
+// K-slice block stores its fp32 tile slab write-through (sc1: no release fence needed), drains
+// it (every wave s_waitcnt vmcnt(0), then the barrier), and one lane draws a ticket on the
+// tile's agent-scope counter; the block drawing S-1 acquires (agent) and sums the S slabs into
+// Ct in z order 0..S-1 — xsplitk_reduce_kernel's order, so every output bit is unchanged — then
+// runs the normal epilogue (bias / residual / ReLU / BN statistics / max).  No block waits on
+// another (the last arriver does the work), so the grid always drains.  Replaces the separate
+// reduce launch (~5 us of launch latency at a lone client's stage-3/4 convs) and lets the
+// epilogue fold BN statistics of split launches.  Returns false for the blocks that are done.
+template <int BM, int BN>
+__device__ __forceinline__ bool sk_combine(const XArgs& a, float* Ct, const long long* orow, int g, int zc, int kz,
+                                           int n0, int* flag) {
+  constexpr int C4 = BN / 4;
+  const int tid = threadIdx.x, S = a.splitk;
+  const float* base = a.sk_ws + (long long)g * a.sk_gstride;
+  const __amdgpu_buffer_rsrc_t rs = rsrc(base + (long long)kz * a.zstride, a.sk_gstride * 4);
+  for (int e = tid; e < BM * C4; e += 256) {
+    const int row = e / C4, cc = (e - row * C4) * 4;
+    const int n = n0 + cc;
+    const long long o = orow[row];
+    if (o < 0 || n >= a.Ncol) continue;
+    const float4 v = *(const float4*)&Ct[row * BN + cc];
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, v), rs, (int)((o + n) * 4), 0, 16);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave drains its slab
+  __syncthreads();
+  if (tid == 0) {
+    int* cnt = a.sk_cnt + ((long long)g * gridDim.x + blockIdx.x) * (gridDim.z / S) + zc;
+    const int t = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = t == S - 1;
+    if (last) {
+      __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // reusable
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    *flag = last;
+  }
+  __syncthreads();
+  if (!*flag) return false;
+  for (int e = tid; e < BM * C4; e += 256) {
+    const int row = e / C4, cc = (e - row * C4) * 4;
+    const int n = n0 + cc;
+    const long long o = orow[row];
+    if (o < 0 || n >= a.Ncol) continue;
+    float4* cp = (float4*)&Ct[row * BN + cc];
+    const float4 own = *cp;
+    float4 v = kz == 0 ? own : *(const float4*)(base + o + n);
+    for (int z = 1; z < S; ++z) {
+      const float4 w = z == kz ? own : *(const float4*)(base + (long long)z * a.zstride + o + n);
+      v.x += w.x; v.y += w.y; v.z += w.z; v.w += w.w;
+    }
+    *cp = v;
+  }
+  __syncthreads();
+  return true;
+}
 
 // fp16-pair output exponent of replica g (slot: its weight slot; PairAct); every lane of the
 // wave calls it (amax_read)
@@ -358,7 +424,8 @@ __global__ __launch_bounds__(256) void xconv_kernel(const XArgs a) {
   const int tn = blockIdx.x % a.tiles_n, tm = blockIdx.x / a.tiles_n;
   const int m0 = tm * BM, n0 = tn * BN;
   if (m0 >= Mv) {
-    if (a.bnpart && a.splitk == 1) bn_tile_stats<BM, BN>(nullptr, a.bnpart, a.bnpart_nblk, g, a.Ncol, m0, n0, true);
+    if (a.bnpart && (a.splitk == 1 || (a.sk_cnt && kz == 0)))
+      bn_tile_stats<BM, BN>(nullptr, a.bnpart, a.bnpart_nblk, g, a.Ncol, m0, n0, true);
     return;
   }
   const int slot = a.wsel ? a.wsel[g] : g;
@@ -586,7 +653,12 @@ __global__ __launch_bounds__(256) void xconv_kernel(const XArgs a) {
       for (int r = 0; r < 16; ++r)
         Ct[(wm * TM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * hf) * BN + wn * TN + j * 32 + fr] = acc[i][j][r];
   __syncthreads();
-  const bool fin = a.splitk == 1;
+  bool fin = a.splitk == 1;
+  if (!fin && a.sk_cnt) {
+    __shared__ int sk_last;
+    if (!sk_combine<BM, BN>(a, Ct, orow, g, zc, kz, n0, &sk_last)) return;
+    fin = true;
+  }
   if (fin && a.bnpart) bn_tile_stats<BM, BN>(Ct, a.bnpart, a.bnpart_nblk, g, a.Ncol, m0, n0, false);
   float* out = a.out + (long long)g * a.out_gstride + (fin ? 0 : (long long)kz * a.zstride);
   const float* bias = (fin && a.bias) ? a.bias + (long long)slot * a.b_sstride : nullptr;
@@ -1713,16 +1785,42 @@ int xhalo_try(const XArgs& a, int G, int KH, int KW, hipStream_t st) {
   return -100;
 }
 
-int xconv_dispatch(const XArgs& a, long long Mmax, int G, int nclass, int vec, hipStream_t st) {
-  // small launches (a lone client's grouped step) take 64-row tiles, the smallest (a lone
-  // client's stage-3/4 convs: 32-64 tiles of 64 rows) 32-row tiles with one 32x32 MFMA tile
-  // per wave.  The tile shape never changes a result bit: every output element sees the same
-  // k-step order and the same plane-product order within a step.
+// the implicit GEMM's tile rows for a launch (xconv_tile maps it to the kernel's BM).  Small
+// launches (a lone client's grouped step) take 64-row tiles, the smallest (a lone client's
+// stage-3/4 convs: 32-64 tiles of 64 rows) 32-row tiles with one 32x32 MFMA tile per wave.
+int xconv_bm(long long Mmax, int Ncol, int G, int nclass, int splitk) {
   static const int bm32_below = env_int("DBA_F32_BM32_BLOCKS", 256);
-  const int bn = a.Ncol <= 32 ? 32 : a.Ncol <= 64 ? 64 : 128;
-  const long long blocks = (long long)ceil_div(Mmax, 128) * ceil_div(a.Ncol, bn) * G * nclass * a.splitk;
+  const int bn = Ncol <= 32 ? 32 : Ncol <= 64 ? 64 : 128;
+  const long long blocks = (long long)ceil_div(Mmax, 128) * ceil_div(Ncol, bn) * G * nclass * splitk;
   int bm = (bn > 32 && blocks < 512) ? 64 : 128;
   if (bn == 128 && 2 * blocks < bm32_below) bm = 32;
+  return bm;
+}
+
+// arrival counters an in-launch split-K combine needs: one per (replica, tile, class)
+long long xconv_sk_count(long long Mmax, int Ncol, int G, int nclass, int splitk) {
+  const int bn = Ncol <= 32 ? 32 : Ncol <= 64 ? 64 : 128;
+  const int bm = Ncol <= 32 ? 128 : xconv_bm(Mmax, Ncol, G, nclass, splitk);
+  return (long long)ceil_div(Mmax, bm) * ceil_div(Ncol, bn) * G * nclass;
+}
+
+// in-launch split-K combine on (DBA_F32_SK_INLAUNCH=0: the separate xsplitk_reduce launch)
+bool sk_inlaunch_on() {
+  static const bool on = env_int("DBA_F32_SK_INLAUNCH", 1) != 0;
+  return on;
+}
+
+// the in-launch combine applies: counters given and enough of them, 4-column output vectors,
+// a replica's slab addressable by a 32-bit buffer offset
+bool sk_ok(const int* cnt, long long cnt_n, long long M, int Ncol, int G, int nclass, int s) {
+  return cnt && sk_inlaunch_on() && (Ncol & 3) == 0 && M * Ncol < (1LL << 29) &&
+         cnt_n >= xconv_sk_count(M, Ncol, G, nclass, s);
+}
+
+int xconv_dispatch(const XArgs& a, long long Mmax, int G, int nclass, int vec, hipStream_t st) {
+  // The tile shape never changes a result bit: every output element sees the same k-step
+  // order and the same plane-product order within a step.
+  const int bm = xconv_bm(Mmax, a.Ncol, G, nclass, a.splitk);
   if (vec == 4 && a.Cs % 32 == 0) vec = 32;
   if (a.in_sexp) {   // fp16-pair activations (evaluation; the launcher checked wp and vec)
     if (vec == 32) return xconv_tile<2, 32, true, true, true>(a, Mmax, G, nclass, bm, st);
@@ -1820,6 +1918,15 @@ DBA_EXPORT long long dba_xconv_ws_floats(int G, int N, int Ho, int Wo, int Cin, 
   return s > 1 ? (long long)s * G * M * Cout : 0;
 }
 
+// arrival counters (int32, zeroed) the in-launch split-K combine of this shape needs (0: it
+// does not split, or the combine is off / not applicable: the separate reduce launch runs)
+DBA_EXPORT long long dba_xconv_sk_ints(int G, int N, int Ho, int Wo, int Cin, int Cout, int KH, int KW) {
+  const long long M = (long long)N * Ho * Wo;
+  const int s = xsplitk(M, G, Cout, KH * KW * Cin);
+  if (s <= 1 || !sk_inlaunch_on() || (Cout & 3) || M * Cout >= (1LL << 29)) return 0;
+  return xconv_sk_count(M, Cout, G, 1, s);
+}
+
 // y = act(conv(x, w) + bias + res), fp32 NHWC; w [slots][Cout][KH][KW][Cin]
 DBA_EXPORT int dba_xconv_fwd(const float* x, long long x_gstride, const float* w, long long w_sstride,
                              const int* wsel, const float* bias, long long b_sstride, const float* res, float* out,
@@ -1828,7 +1935,8 @@ DBA_EXPORT int dba_xconv_fwd(const float* x, long long x_gstride, const float* w
                              int amax_x_ld, const int* amax_w, int amax_w_ld, int* amax_out, int amax_out_ld,
                              const uint16_t* wp, long long wp_sstride, float* ws, long long ws_floats,
                              double* bnpart, const int* in_sexp, int* out_sexp, const float* bound,
-                             const int* amax_res, int amax_res_ld, const int* res_sexp, void* stream) {
+                             const int* amax_res, int amax_res_ld, const int* res_sexp, int* sk_cnt,
+                             long long sk_cnt_n, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   if ((long long)N * H * W * Cin >= (1LL << 29)) return -103;   // 32-bit in-replica byte offsets
   const long long M = (long long)N * Ho * Wo;
@@ -1854,8 +1962,17 @@ DBA_EXPORT int dba_xconv_fwd(const float* x, long long x_gstride, const float* w
     if (rc != -100) return rc;
   }
   const int s = pairs ? 1 : xsplitk(M, G, Cout, K);
-  if (bnpart && s > 1) return -106;   // split-K outputs: BN statistics by the BN kernels
-  if (s > 1 && ws != nullptr && ws_floats >= (long long)s * G * M * Cout) {
+  const bool ws_ok = s > 1 && ws != nullptr && ws_floats >= (long long)s * G * M * Cout;
+  if (ws_ok && sk_ok(sk_cnt, sk_cnt_n, M, Cout, G, 1, s)) {
+    // in-launch combine (sk_combine): one launch, BN statistics folded by the reducing block
+    XArgs b = a;
+    b.splitk = s;
+    b.zstride = (long long)G * M * Cout;
+    b.sk_ws = ws; b.sk_gstride = M * Cout; b.sk_cnt = sk_cnt;
+    return xconv_dispatch(b, M, G, 1, vec, st);
+  }
+  if (bnpart && s > 1) return -106;   // separate reduce launch: BN statistics by the BN kernels
+  if (ws_ok) {
     XArgs b = a;
     b.splitk = s;
     b.out = ws;
@@ -1879,7 +1996,7 @@ DBA_EXPORT int dba_xconv_dgrad(const float* dy, long long dy_gstride, const floa
                                const int* nvalid, int G, int N, int H, int W, int Cin, int Ho, int Wo, int Cout,
                                int KH, int KW, int stride, int pad, const int* amax_dy, int amax_dy_ld,
                                const int* amax_w, int amax_w_ld, const uint16_t* wp, long long wp_sstride, float* ws,
-                               long long ws_floats, void* stream) {
+                               long long ws_floats, int* sk_cnt, long long sk_cnt_n, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   if ((long long)N * Ho * Wo * Cout >= (1LL << 29)) return -103;   // 32-bit in-replica byte offsets
   const ClassGeom cg = dgrad_classes(H, W, Cin, Cout, KH, KW, stride, pad);
@@ -1902,7 +2019,15 @@ DBA_EXPORT int dba_xconv_dgrad(const float* dy, long long dy_gstride, const floa
     if (rc != -100) return rc;
     const long long M = (long long)N * H * W;
     const int s = xsplitk(M, G, Cin, KH * KW * Cout);
-    if (s > 1 && ws != nullptr && ws_floats >= (long long)s * G * M * Cin) {
+    const bool ws_ok = s > 1 && ws != nullptr && ws_floats >= (long long)s * G * M * Cin;
+    if (ws_ok && sk_ok(sk_cnt, sk_cnt_n, M, Cin, G, 1, s)) {
+      XArgs b = a;
+      b.splitk = s;
+      b.zstride = (long long)G * M * Cin;
+      b.sk_ws = ws; b.sk_gstride = M * Cin; b.sk_cnt = sk_cnt;
+      return xconv_dispatch(b, M, G, 1, vec, st);
+    }
+    if (ws_ok) {
       XArgs b = a;
       b.splitk = s;
       b.out = ws;

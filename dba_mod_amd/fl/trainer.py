@@ -35,6 +35,11 @@ from .workload import Workload
 
 log = logging.getLogger("logger")
 
+# arrival counters per training step for the in-launch split-K combines of the fp32 convs
+# (xgemm.hip sk_combine): a ResNet-18 step needs ~14 launches x <= 512 per replica group;
+# zeroed with the step's operand-max arena (no extra launch).  0: separate reduce launches
+SK_COUNTERS = int(os.environ.get("DBA_SK_COUNTERS", "0"))
+
 
 @dataclass
 class ClientResult:
@@ -127,7 +132,7 @@ class GroupTrainer:
         # the training step's fp32 split (kernel choice is made at launch, so a captured graph
         # keeps it): DBA_F32_TRAIN_PLANES, default = the library-wide setting
         with ops.fp32_split(self.device, self.split_mode, ops.train_h_ops(self.device)), \
-                ops.amax_arena(b.state.shape[0], self.device):
+                ops.amax_arena(b.state.shape[0], self.device, counters=SK_COUNTERS):
             self._step_ops(b)
 
     def _step_ops(self, b: _GroupBuffers) -> None:

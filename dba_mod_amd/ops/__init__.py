@@ -73,11 +73,12 @@ def train_h_ops(device: torch.device):
     return hip_module().TRAIN_H_OPS if backend_name(device) == "hip" else None
 
 
-def amax_arena(G: int, device: torch.device):
+def amax_arena(G: int, device: torch.device, counters: int = 0):
     """Context: one zeroed allocation for the fp16-pair operand-max slots of the enclosed
-    launches (``ops.hip.amax_arena``); a no-op off the HIP backend."""
+    launches (``ops.hip.amax_arena``), plus ``counters`` arrival counters for their in-launch
+    split-K combines; a no-op off the HIP backend."""
     if backend_name(device) == "hip":
-        return hip_module().amax_arena(G, device)
+        return hip_module().amax_arena(G, device, counters=counters)
     return contextlib.nullcontext()
 
 

@@ -81,10 +81,11 @@ _SIGS = {
     "dba_bn_bwd_fuse_set": [_I],
     "dba_xconv_ws_floats": [_I] * 8,
     "dba_xconv_fwd": [_P, _LL, _P, _LL, _P, _P, _LL, _P, _P, _LL, _P] + [_I] * 13 + [_P, _I] * 3 + [_P, _LL] * 2
-    + [_P, _P, _P, _P, _P, _I, _P, _P],
+    + [_P, _P, _P, _P, _P, _I, _P, _P, _LL, _P],
+    "dba_xconv_sk_ints": [_I] * 8,
     "dba_row_bound": [_P, _LL, _I, _I, _P, _LL, _I, _P, _P],
     "dba_bn_finalize_part": [_P, _I, _P, _I, _I, _I, _I, _P, _P, _LL, _F, _F, _P, _P, _P],
-    "dba_xconv_dgrad": [_P, _LL, _P, _LL, _P, _P, _P, _LL, _P] + [_I] * 12 + [_P, _I] * 2 + [_P, _LL] * 2 + [_P],
+    "dba_xconv_dgrad": [_P, _LL, _P, _LL, _P, _P, _P, _LL, _P] + [_I] * 12 + [_P, _I] * 2 + [_P, _LL] * 3 + [_P],
     "dba_xsplit_w": [_P, _LL, _LL, _I, _P, _I, _P, _P],
     "dba_amax": [_P, _LL, _LL, _P, _LL, _I, _P, _I, _P],
     "dba_xtranspose": [_P, _I, _I, _LL, _P, _P],
@@ -100,6 +101,7 @@ for _name, _args in _SIGS.items():
     _fn.restype = ctypes.c_int
 _L.dba_conv3_splitk_floats.restype = ctypes.c_longlong
 _L.dba_xconv_ws_floats.restype = ctypes.c_longlong
+_L.dba_xconv_sk_ints.restype = ctypes.c_longlong
 _L.dba_xwgrad_ws_floats.restype = ctypes.c_longlong
 _MODE = int(_L.dba_xgemm_set_planes(0))   # fp32 split mode (0: query only; DBA_F32_PLANES)
 
@@ -325,9 +327,20 @@ class _AmaxArena:
     (captured into the training step's graph: re-zeroed at every replay) instead of one per
     producer."""
 
-    def __init__(self, G: int, device, n: int) -> None:
+    def __init__(self, G: int, device, n: int, counters: int = 0) -> None:
         self.G, self.ld, self.next = G, _amax_ld(G), 0
-        self.buf = torch.zeros(n, AMAX_SUB, self.ld, dtype=torch.int32, device=device)
+        slots = n * AMAX_SUB * self.ld
+        flat = torch.zeros(slots + counters, dtype=torch.int32, device=device)
+        self.buf = flat[:slots].view(n, AMAX_SUB, self.ld)
+        # arrival counters of the in-launch split-K combines (xgemm.hip sk_combine), zeroed by
+        # the same fill
+        self.cnt, self.cnt_next = flat[slots:], 0
+
+    def counters(self, n: int, device):
+        if n <= 0 or device != self.cnt.device or self.cnt_next + n > self.cnt.numel():
+            return None
+        self.cnt_next += n
+        return self.cnt[self.cnt_next - n:self.cnt_next]
 
     def take(self, G: int, device):
         if G != self.G or self.next >= self.buf.shape[0] or device != self.buf.device:
@@ -340,12 +353,13 @@ _ARENA: list = []
 
 
 @contextlib.contextmanager
-def amax_arena(G: int, device, n: int = 128):
-    """Slots for the enclosed launches' fp16-pair operand maxima (fp16-pair mode only)."""
+def amax_arena(G: int, device, n: int = 128, counters: int = 0):
+    """Slots for the enclosed launches' fp16-pair operand maxima (fp16-pair mode only), and
+    ``counters`` zeroed ints for their in-launch split-K combines (:func:`_sk_counters`)."""
     if _MODE != F16_PAIR:
         yield
         return
-    _ARENA.append(_AmaxArena(G, device, n))
+    _ARENA.append(_AmaxArena(G, device, n, counters))
     try:
         yield
     finally:
@@ -355,6 +369,15 @@ def amax_arena(G: int, device, n: int = 128):
 def _amax_new(G: int, device):
     a = _ARENA[-1].take(G, device) if _ARENA else None
     return a if a is not None else torch.zeros(AMAX_SUB, _amax_ld(G), dtype=torch.int32, device=device)
+
+
+def _sk_counters(n: int, device):
+    """``n`` zeroed arrival counters for an in-launch split-K combine (xgemm.hip sk_combine)
+    from the enclosing arena (None: no arena / exhausted — the launch then runs the separate
+    reduce kernel, same bits)."""
+    if n <= 0 or not _ARENA:
+        return None
+    return _ARENA[-1].counters(n, device)
 
 
 def _bn_counter(G: int, device):
@@ -503,6 +526,9 @@ def _xconv_fwd(x, w, wsel, stride, pad, bias, residual, relu, nvalid, out_dtype,
     res = _act(residual, _F32, "residual") if residual is not None else None
     n = int(_L.dba_xconv_ws_floats(G, N, Ho, Wo, Cin, Cout, KH, KW))
     wsb = torch.empty(n, dtype=_F32, device=x.device) if n > 0 else None
+    # split-K launch: slabs combined in the launch when the arena has counters for it
+    ncnt = int(_L.dba_xconv_sk_ints(G, N, Ho, Wo, Cin, Cout, KH, KW)) if n > 0 else 0
+    cnt = _sk_counters(ncnt, x.device)
     ax = aw = ay = None
     if _MODE == F16_PAIR and "fwd" in _H_OPS:
         ax, aw = _amax_act(x, nvalid), _amax_w(w, ws, Cout * KH * KW * Cin)
@@ -538,7 +564,7 @@ def _xconv_fwd(x, w, wsel, stride, pad, bias, residual, relu, nvalid, out_dtype,
                 y._dba_pair = out_sexp
             return y
         part = None
-    if want_part and n == 0:
+    if want_part and (n == 0 or cnt is not None):
         nblk = (N * Ho * Wo + 31) // 32
         part = torch.empty(G * Cout * 2 * nblk, dtype=torch.float64, device=x.device)
         if os.environ.get("DBA_BN_FUSED_POISON") == "1":   # diagnostics: unwritten slots -> NaN
@@ -548,7 +574,7 @@ def _xconv_fwd(x, w, wsel, stride, pad, bias, residual, relu, nvalid, out_dtype,
           _ptr(res), y.data_ptr(), N * Ho * Wo * Cout, _ptr(_i32(nvalid)), G, N, H, W, Cin, Ho, Wo, Cout, KH, KW,
           stride, pad, int(relu), *_aptr(ax), *_aptr(aw), *_aptr(ay), *_wplanes(w), _ptr(wsb), n, _ptr(part),
           _ptr(in_sexp), _ptr(out_sexp), _ptr(bound if out_sexp is not None else None), *_aptr(ares), _ptr(res_sexp),
-          _stream())
+          _ptr(cnt), 0 if cnt is None else cnt.numel(), _stream())
     if out_sexp is not None:
         y._dba_pair = out_sexp
     return y
@@ -701,13 +727,15 @@ def _xconv_dgrad(dy, w, wsel, stride, pad, in_hw, nvalid, out_dtype, accum, wt):
         assert acc.shape == dx.shape
     n = int(_L.dba_xconv_ws_floats(G, N, H, W, Cout, Cin, KH, KW)) if stride == 1 else 0
     wsb = torch.empty(n, dtype=_F32, device=dy.device) if n > 0 else None
+    cnt = _sk_counters(int(_L.dba_xconv_sk_ints(G, N, H, W, Cout, Cin, KH, KW)) if n > 0 else 0, dy.device)
     ad = aw = None
     if _MODE == F16_PAIR and "dgrad" in _H_OPS:
         a0 = getattr(w, "_dba_amax", None)   # the forward weights' max is the transpose's
         ad, aw = _amax_act(dy, nvalid), (a0 if a0 is not None else _amax(wt, per, per))
     _call("dba_xconv_dgrad", dy.data_ptr(), N * Ho * Wo * Cout, wt.data_ptr(), per, _ptr(_i32(wsel)), _ptr(acc),
           dx.data_ptr(), N * H * W * Cin, _ptr(_i32(nvalid)), G, N, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad,
-          *_aptr(ad), *_aptr(aw), *_wplanes(wt), _ptr(wsb), n, _stream())
+          *_aptr(ad), *_aptr(aw), *_wplanes(wt), _ptr(wsb), n, _ptr(cnt), 0 if cnt is None else cnt.numel(),
+          _stream())
     return dx
 
 

@@ -1,0 +1,140 @@
+"""In-launch split-K combine of the fp32 convs (``csrc/kernels/xgemm.hip`` ``sk_combine``) vs
+the separate ``xsplitk_reduce`` launch it replaces (GPU only).
+
+The K-slice blocks of a split launch (a lone client's stage-3/4 convs and data gradients,
+``xsplitk``) store write-through slabs and draw arrival tickets; the last arriver sums the
+slabs in z order — the reduce kernel's order — so every output bit must equal the two-launch
+path: forward with bias / residual / ReLU, the data gradient with its accumulated input, for
+a lone client and for groups with a partly valid and an inactive replica.  The combine also
+lets the epilogue fold training-BN statistics of a split conv (previously a separate BN
+reduce + finalize): those match fp64 statistics of the output to fp32 rounding.
+"""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def H():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from dba_mod_amd.ops import hip
+    prev = hip.set_fp32_planes(16)   # the step's mode: the arena (and its counters) exists
+    yield hip
+    hip.set_fp32_planes(prev)
+
+
+SHAPES = [
+    # G, N, Hh, Cin, Cout
+    (1, 64, 4, 256, 256),    # lone client, stage 4
+    (1, 64, 8, 128, 128),    # lone client, stage 3
+    (3, 64, 8, 128, 128),    # group: full, partly valid, inactive replica
+    (4, 64, 4, 256, 256),
+]
+
+
+def _data(G, N, Hh, Cin, Cout, dev, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    x = torch.randn(G, N, Hh, Hh, Cin, generator=g).to(dev)
+    w = (torch.randn(G, Cout, 3, 3, Cin, generator=g) / (9 * Cin) ** 0.5).to(dev)
+    bias = torch.randn(G, Cout, generator=g).to(dev)
+    res = torch.randn(G, N, Hh, Hh, Cout, generator=g).to(dev)
+    dy = torch.randn(G, N, Hh, Hh, Cout, generator=g).to(dev)
+    acc = torch.randn(G, N, Hh, Hh, Cin, generator=g).to(dev)
+    nvalid = torch.tensor([N, N // 2 + 1, 0, N - 3][:G], dtype=torch.int32, device=dev)
+    for i in range(G):
+        dy[i, int(nvalid[i]):] = 0
+    return x, w, bias, res, dy, acc, nvalid
+
+
+def _valid_equal(a, b, nvalid):
+    for g in range(a.shape[0]):
+        n = int(nvalid[g])
+        assert torch.equal(a[g, :n], b[g, :n]), g
+
+
+@pytest.mark.parametrize("shape", SHAPES)
+def test_inlaunch_combine_bitwise(H, shape):
+    G, N, Hh, Cin, Cout = shape
+    dev = torch.device("cuda")
+    x, w, bias, res, dy, acc, nvalid = _data(G, N, Hh, Cin, Cout, dev)
+    assert int(H._L.dba_xconv_sk_ints(G, N, Hh, Hh, Cin, Cout, 3, 3)) > 0, "shape does not split"
+    assert int(H._L.dba_xconv_sk_ints(G, N, Hh, Hh, Cout, Cin, 3, 3)) > 0, "dgrad does not split"
+
+    def run(counters):
+        with H.amax_arena(G, dev, counters=counters):
+            y = H.conv2d(x, w, None, 1, 1, bias=bias, residual=res, relu=True, nvalid=nvalid)
+            dx = H.conv2d_dgrad(dy, w, None, 1, 1, (Hh, Hh), nvalid=nvalid, accum=acc)
+        torch.cuda.synchronize()
+        return y, dx
+
+    y0, dx0 = run(0)                  # separate reduce launches
+    for _ in range(3):                # in-launch combine, repeated (ticket order varies)
+        y1, dx1 = run(1 << 15)
+        _valid_equal(y0, y1, nvalid)
+        _valid_equal(dx0, dx1, nvalid)
+    # fp32-level agreement with an fp64 conv (the bits above are the reduce path's)
+    xd = x.double().permute(0, 1, 4, 2, 3)
+    for g in range(G):
+        n = int(nvalid[g])
+        if n == 0:
+            continue
+        ref = torch.nn.functional.conv2d(xd[g, :n].cpu(), w[g].double().permute(0, 3, 1, 2).cpu(),
+                                         bias[g].double().cpu(), padding=1).permute(0, 2, 3, 1)
+        ref = (ref + res[g, :n].double().cpu()).clamp(min=0)
+        err = ((y1[g, :n].double().cpu() - ref).norm() / ref.norm()).item()
+        assert err < 1e-5, (g, err)
+
+
+def test_inlaunch_combine_graph_replay(H):
+    """Inside a captured graph the arena's fill re-zeroes the counters every replay."""
+    G, N, Hh, Cin, Cout = 1, 64, 4, 256, 256
+    dev = torch.device("cuda")
+    x, w, bias, res, dy, acc, nvalid = _data(G, N, Hh, Cin, Cout, dev, seed=1)
+    with H.amax_arena(G, dev, counters=0):
+        ref = H.conv2d(x, w, None, 1, 1, bias=bias, relu=True, nvalid=nvalid)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for _ in range(2):   # warm up the allocator outside the capture
+            with H.amax_arena(G, dev, counters=1 << 12):
+                H.conv2d(x, w, None, 1, 1, bias=bias, relu=True, nvalid=nvalid)
+    torch.cuda.current_stream().wait_stream(s)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        with H.amax_arena(G, dev, counters=1 << 12):
+            out = H.conv2d(x, w, None, 1, 1, bias=bias, relu=True, nvalid=nvalid)
+    for _ in range(4):
+        out.fill_(float("nan"))
+        graph.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(out, ref)
+
+
+@pytest.mark.parametrize("shape", [(1, 64, 8, 128, 128), (3, 64, 8, 128, 128)])
+def test_inlaunch_combine_bn_stats(H, shape):
+    """A split conv feeding a training BN folds the statistics in the reducing block:
+    bn_train finalises them (no pass over y) to fp64 accuracy."""
+    G, N, Hh, Cin, Cout = shape
+    dev = torch.device("cuda")
+    x, w, _, _, _, _, nvalid = _data(G, N, Hh, Cin, Cout, dev, seed=2)
+    gamma = torch.ones(G, Cout, device=dev)
+    beta = torch.zeros(G, Cout, device=dev)
+    with H.amax_arena(G, dev, counters=1 << 15):
+        y = H.conv2d(x, w, None, 1, 1, nvalid=nvalid, bn_stats=True)
+        assert hasattr(y, "_dba_bnpart"), "split conv did not fold BN statistics"
+        rm, rv = torch.zeros(G, Cout, device=dev), torch.ones(G, Cout, device=dev)
+        out, mean, invstd = H.bn_train(y, gamma, beta, rm, rv, nvalid, 0.1, 1e-5, False, None)
+    torch.cuda.synchronize()
+    for g in range(G):
+        n = int(nvalid[g])
+        if n == 0:
+            assert torch.all(mean[g] == 0) and torch.all(invstd[g] == 0)
+            continue
+        yv = y[g, :n].double().cpu().reshape(-1, Cout)
+        m, var = yv.mean(0), yv.var(0, unbiased=False)
+        assert ((mean[g].double().cpu() - m).norm() / m.norm()).item() < 1e-6
+        ist = 1 / (var + 1e-5).sqrt()
+        assert ((invstd[g].double().cpu() - ist).norm() / ist.norm()).item() < 1e-6
+        assert ((rv[g].double().cpu() - (0.9 + 0.1 * yv.var(0, unbiased=True))).norm()).item() < 1e-5
