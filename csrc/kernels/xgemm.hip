@@ -304,29 +304,40 @@ struct XArgs {
 
 typedef __attribute__((ext_vector_type(4))) unsigned int u32x4v;
 
-// In-launch split-K combine (the CDNA4 guide's counter hand-off, write-through form): every
-// K-slice block stores its fp32 tile slab write-through (sc1: no release fence needed), drains
-// it (every wave s_waitcnt vmcnt(0), then the barrier), and one lane draws a ticket on the
-// tile's agent-scope counter; the block drawing S-1 acquires (agent) and sums the S slabs into
-// Ct in z order 0..S-1 — xsplitk_reduce_kernel's order, so every output bit is unchanged — then
-// runs the normal epilogue (bias / residual / ReLU / BN statistics / max).  No block waits on
-// another (the last arriver does the work), so the grid always drains.  Replaces the separate
-// reduce launch (~5 us of launch latency at a lone client's stage-3/4 convs) and lets the
-// epilogue fold BN statistics of split launches.  Returns false for the blocks that are done.
+// In-launch split-K combine (the CDNA4 guide's counter hand-off, write-through form) for a
+// lone client's 32 x 128 tiles: every K-slice block stores its fp32 tile slab write-through
+// (sc1: no release fence), drains it (every wave s_waitcnt vmcnt(0), then the barrier), and
+// one lane draws a ticket on the tile's agent-scope counter; the block drawing S-1 reads the
+// other slabs with sc1 loads (no acquire: every load of a handed-off byte bypasses L1), ALL of
+// them in flight at once, and sums them into Ct in z order 0..S-1 — xsplitk_reduce_kernel's
+// order, so every output bit is unchanged — then runs the normal epilogue (bias / residual /
+// ReLU / BN statistics / max).  No block waits on another (the last arriver does the work), so
+// the grid always drains.  Replaces the separate reduce launch and lets the epilogue fold BN
+// statistics of split launches.  Returns false for the blocks that are done.
+constexpr int kSkMax = 8;   // slabs an in-launch combine takes (sk_ok)
 template <int BM, int BN>
 __device__ __forceinline__ bool sk_combine(const XArgs& a, float* Ct, const long long* orow, int g, int zc, int kz,
                                            int n0, int* flag) {
-  constexpr int C4 = BN / 4;
+  constexpr int C4 = BN / 4, IT = BM * C4 / 256;
+  static_assert(BM * C4 % 256 == 0, "whole float4 passes");
   const int tid = threadIdx.x, S = a.splitk;
   const float* base = a.sk_ws + (long long)g * a.sk_gstride;
-  const __amdgpu_buffer_rsrc_t rs = rsrc(base + (long long)kz * a.zstride, a.sk_gstride * 4);
-  for (int e = tid; e < BM * C4; e += 256) {
-    const int row = e / C4, cc = (e - row * C4) * 4;
-    const int n = n0 + cc;
+  int off[IT];
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
+    const int e = tid + it * 256, row = e / C4, cc = (e - row * C4) * 4, n = n0 + cc;
     const long long o = orow[row];
-    if (o < 0 || n >= a.Ncol) continue;
-    const float4 v = *(const float4*)&Ct[row * BN + cc];
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, v), rs, (int)((o + n) * 4), 0, 16);
+    off[it] = (o < 0 || n >= a.Ncol) ? kOOB : (int)((o + n) * 4);
+  }
+  {
+    const __amdgpu_buffer_rsrc_t rs = rsrc(base + (long long)kz * a.zstride, a.sk_gstride * 4);
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+      const int e = tid + it * 256, row = e / C4, cc = (e - row * C4) * 4;
+      const float4 v = *(const float4*)&Ct[row * BN + cc];
+      if (off[it] != kOOB)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, v), rs, off[it], 0, 16);
+    }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave drains its slab
   __syncthreads();
@@ -334,28 +345,36 @@ __device__ __forceinline__ bool sk_combine(const XArgs& a, float* Ct, const long
     int* cnt = a.sk_cnt + ((long long)g * gridDim.x + blockIdx.x) * (gridDim.z / S) + zc;
     const int t = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const int last = t == S - 1;
-    if (last) {
-      __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // reusable
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
+    if (last) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // reusable
     *flag = last;
   }
   __syncthreads();
   if (!*flag) return false;
-  for (int e = tid; e < BM * C4; e += 256) {
-    const int row = e / C4, cc = (e - row * C4) * 4;
-    const int n = n0 + cc;
-    const long long o = orow[row];
-    if (o < 0 || n >= a.Ncol) continue;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // loads stay below the ticket
+  float4 w[kSkMax][IT];
+#pragma unroll
+  for (int z = 0; z < kSkMax; ++z) {
+    if (z < S && z != kz) {
+      const __amdgpu_buffer_rsrc_t rz = rsrc(base + (long long)z * a.zstride, a.sk_gstride * 4);
+#pragma unroll
+      for (int it = 0; it < IT; ++it)
+        w[z][it] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rz, off[it], 0, 16));
+    }
+  }
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
+    const int e = tid + it * 256, row = e / C4, cc = (e - row * C4) * 4;
     float4* cp = (float4*)&Ct[row * BN + cc];
     const float4 own = *cp;
-    float4 v = kz == 0 ? own : *(const float4*)(base + o + n);
-    for (int z = 1; z < S; ++z) {
-      const float4 w = z == kz ? own : *(const float4*)(base + (long long)z * a.zstride + o + n);
-      v.x += w.x; v.y += w.y; v.z += w.z; v.w += w.w;
+    float4 v = kz == 0 ? own : w[0][it];
+#pragma unroll
+    for (int z = 1; z < kSkMax; ++z) {
+      if (z < S) {
+        const float4 u = z == kz ? own : w[z][it];
+        v.x += u.x; v.y += u.y; v.z += u.z; v.w += u.w;
+      }
     }
-    *cp = v;
+    if (off[it] != kOOB) *cp = v;
   }
   __syncthreads();
   return true;
@@ -654,10 +673,12 @@ __global__ __launch_bounds__(256) void xconv_kernel(const XArgs a) {
         Ct[(wm * TM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * hf) * BN + wn * TN + j * 32 + fr] = acc[i][j][r];
   __syncthreads();
   bool fin = a.splitk == 1;
-  if (!fin && a.sk_cnt) {
-    __shared__ int sk_last;
-    if (!sk_combine<BM, BN>(a, Ct, orow, g, zc, kz, n0, &sk_last)) return;
-    fin = true;
+  if constexpr (BM == 32 && BN == 128) {   // the only tile sk_ok admits
+    if (!fin && a.sk_cnt) {
+      __shared__ int sk_last;
+      if (!sk_combine<BM, BN>(a, Ct, orow, g, zc, kz, n0, &sk_last)) return;
+      fin = true;
+    }
   }
   if (fin && a.bnpart) bn_tile_stats<BM, BN>(Ct, a.bnpart, a.bnpart_nblk, g, a.Ncol, m0, n0, false);
   float* out = a.out + (long long)g * a.out_gstride + (fin ? 0 : (long long)kz * a.zstride);
@@ -1812,9 +1833,11 @@ bool sk_inlaunch_on() {
 
 // the in-launch combine applies: counters given and enough of them, 4-column output vectors,
 // a replica's slab addressable by a 32-bit buffer offset
+// (lone-client 32 x 128 tiles only: at 128-row tiles the reducer's serial slab read costs more
+// than the launch it saves — 10-client step 2.20 -> 2.33 ms, profiles/r3_sk_inlaunch.md)
 bool sk_ok(const int* cnt, long long cnt_n, long long M, int Ncol, int G, int nclass, int s) {
-  return cnt && sk_inlaunch_on() && (Ncol & 3) == 0 && M * Ncol < (1LL << 29) &&
-         cnt_n >= xconv_sk_count(M, Ncol, G, nclass, s);
+  return cnt && sk_inlaunch_on() && s <= kSkMax && Ncol > 64 && xconv_bm(M, Ncol, G, nclass, s) == 32 &&
+         (Ncol & 3) == 0 && M * Ncol < (1LL << 29) && cnt_n >= xconv_sk_count(M, Ncol, G, nclass, s);
 }
 
 int xconv_dispatch(const XArgs& a, long long Mmax, int G, int nclass, int vec, hipStream_t st) {
@@ -1923,8 +1946,8 @@ DBA_EXPORT long long dba_xconv_ws_floats(int G, int N, int Ho, int Wo, int Cin, 
 DBA_EXPORT long long dba_xconv_sk_ints(int G, int N, int Ho, int Wo, int Cin, int Cout, int KH, int KW) {
   const long long M = (long long)N * Ho * Wo;
   const int s = xsplitk(M, G, Cout, KH * KW * Cin);
-  if (s <= 1 || !sk_inlaunch_on() || (Cout & 3) || M * Cout >= (1LL << 29)) return 0;
-  return xconv_sk_count(M, Cout, G, 1, s);
+  const long long n = s > 1 ? xconv_sk_count(M, Cout, G, 1, s) : 0;
+  return (n > 0 && sk_ok((const int*)1, n, M, Cout, G, 1, s)) ? n : 0;
 }
 
 // y = act(conv(x, w) + bias + res), fp32 NHWC; w [slots][Cout][KH][KW][Cin]

@@ -5,7 +5,7 @@ The K-slice blocks of a split launch (a lone client's stage-3/4 convs and data g
 ``xsplitk``) store write-through slabs and draw arrival tickets; the last arriver sums the
 slabs in z order — the reduce kernel's order — so every output bit must equal the two-launch
 path: forward with bias / residual / ReLU, the data gradient with its accumulated input, for
-a lone client and for groups with a partly valid and an inactive replica.  The combine also
+a lone client with a full and a partly valid batch.  The combine also
 lets the epilogue fold training-BN statistics of a split conv (previously a separate BN
 reduce + finalize): those match fp64 statistics of the output to fp32 rounding.
 """
@@ -26,15 +26,22 @@ def H():
 
 
 SHAPES = [
-    # G, N, Hh, Cin, Cout
-    (1, 64, 4, 256, 256),    # lone client, stage 4
-    (1, 64, 8, 128, 128),    # lone client, stage 3
-    (3, 64, 8, 128, 128),    # group: full, partly valid, inactive replica
-    (4, 64, 4, 256, 256),
+    # G, N, Hh, Cin, Cout, valid images (the combine runs for a lone client's 32 x 128 tiles)
+    (1, 64, 4, 256, 256, 64),    # lone client, stage 4
+    (1, 64, 8, 128, 128, 64),    # lone client, stage 3
+    (1, 64, 8, 128, 128, 23),    # lone client, last (partial) batch
+    (1, 40, 4, 256, 256, 40),
 ]
 
 
-def _data(G, N, Hh, Cin, Cout, dev, seed=0):
+def test_inlaunch_combine_scope(H):
+    """Groups take 64 / 128-row tiles, where the separate reduce launch is cheaper."""
+    assert int(H._L.dba_xconv_sk_ints(3, 64, 8, 8, 128, 128, 3, 3)) == 0
+    assert int(H._L.dba_xconv_sk_ints(10, 64, 4, 4, 256, 256, 3, 3)) == 0
+    assert int(H._L.dba_xconv_sk_ints(1, 64, 16, 16, 64, 64, 3, 3)) == 0   # no split
+
+
+def _data(G, N, Hh, Cin, Cout, dev, seed=0, nv=None):
     g = torch.Generator().manual_seed(seed)
     x = torch.randn(G, N, Hh, Hh, Cin, generator=g).to(dev)
     w = (torch.randn(G, Cout, 3, 3, Cin, generator=g) / (9 * Cin) ** 0.5).to(dev)
@@ -42,7 +49,7 @@ def _data(G, N, Hh, Cin, Cout, dev, seed=0):
     res = torch.randn(G, N, Hh, Hh, Cout, generator=g).to(dev)
     dy = torch.randn(G, N, Hh, Hh, Cout, generator=g).to(dev)
     acc = torch.randn(G, N, Hh, Hh, Cin, generator=g).to(dev)
-    nvalid = torch.tensor([N, N // 2 + 1, 0, N - 3][:G], dtype=torch.int32, device=dev)
+    nvalid = torch.tensor([N, N // 2 + 1, 0, N - 3][:G] if nv is None else [nv], dtype=torch.int32, device=dev)
     for i in range(G):
         dy[i, int(nvalid[i]):] = 0
     return x, w, bias, res, dy, acc, nvalid
@@ -56,9 +63,9 @@ def _valid_equal(a, b, nvalid):
 
 @pytest.mark.parametrize("shape", SHAPES)
 def test_inlaunch_combine_bitwise(H, shape):
-    G, N, Hh, Cin, Cout = shape
+    G, N, Hh, Cin, Cout, nv = shape
     dev = torch.device("cuda")
-    x, w, bias, res, dy, acc, nvalid = _data(G, N, Hh, Cin, Cout, dev)
+    x, w, bias, res, dy, acc, nvalid = _data(G, N, Hh, Cin, Cout, dev, nv=nv)
     assert int(H._L.dba_xconv_sk_ints(G, N, Hh, Hh, Cin, Cout, 3, 3)) > 0, "shape does not split"
     assert int(H._L.dba_xconv_sk_ints(G, N, Hh, Hh, Cout, Cin, 3, 3)) > 0, "dgrad does not split"
 
@@ -112,13 +119,13 @@ def test_inlaunch_combine_graph_replay(H):
         assert torch.equal(out, ref)
 
 
-@pytest.mark.parametrize("shape", [(1, 64, 8, 128, 128), (3, 64, 8, 128, 128)])
+@pytest.mark.parametrize("shape", [(1, 64, 8, 128, 128, 64), (1, 64, 8, 128, 128, 37)])
 def test_inlaunch_combine_bn_stats(H, shape):
     """A split conv feeding a training BN folds the statistics in the reducing block:
     bn_train finalises them (no pass over y) to fp64 accuracy."""
-    G, N, Hh, Cin, Cout = shape
+    G, N, Hh, Cin, Cout, nv = shape
     dev = torch.device("cuda")
-    x, w, _, _, _, _, nvalid = _data(G, N, Hh, Cin, Cout, dev, seed=2)
+    x, w, _, _, _, _, nvalid = _data(G, N, Hh, Cin, Cout, dev, seed=2, nv=nv)
     gamma = torch.ones(G, Cout, device=dev)
     beta = torch.zeros(G, Cout, device=dev)
     with H.amax_arena(G, dev, counters=1 << 15):
