@@ -36,9 +36,9 @@ from .workload import Workload
 log = logging.getLogger("logger")
 
 # arrival counters per training step for the in-launch split-K combines of the fp32 convs
-# (xgemm.hip sk_combine): a ResNet-18 step needs ~14 launches x <= 512 per replica group;
+# (xgemm.hip sk_combine, lone-client launches): a ResNet-18 step needs 14 launches x <= 128;
 # zeroed with the step's operand-max arena (no extra launch).  0: separate reduce launches
-SK_COUNTERS = int(os.environ.get("DBA_SK_COUNTERS", "0"))
+SK_COUNTERS = int(os.environ.get("DBA_SK_COUNTERS", str(1 << 15)))
 
 
 @dataclass
