@@ -15,18 +15,12 @@
 
 namespace {
 
-int env_int_early(const char* name, int dflt) {
-  const char* e = getenv(name);
-  return e ? atoi(e) : dflt;
-}
-
 // Rows per reduction block: ~16K elements per block (8 passes of 256 threads x 8 channels),
 // so narrow-spatial / wide-channel layers (ResNet stage 4: 16 px x 256 ch) still launch
 // enough blocks to cover the chip instead of 2 per replica.
-int block_elems();
-inline int rows_per_block(int C) {
+__host__ __device__ inline int rows_per_block(int C) {
   const int rpp = 256 / (C / 8);
-  const int r = block_elems() / C;
+  const int r = 16384 / C;
   return r > rpp ? r : rpp;
 }
 
@@ -95,12 +89,13 @@ __global__ __launch_bounds__(256) void bn_reduce_kernel(const T* __restrict__ y,
                                                         const T* __restrict__ out, const float* __restrict__ mean,
                                                         const float* __restrict__ invstd, int relu,
                                                         const int* __restrict__ nvalid, int N, int HW, int C,
-                                                        int rpb, float* __restrict__ part, const BnFin fin) {
+                                                        float* __restrict__ part, const BnFin fin) {
   __shared__ float red[2][256][8];
   __shared__ int last;
   const int g = blockIdx.y;
   const int R = N * HW;
   const int Rv = valid_rows(nvalid, g, N) * HW;
+  const int rpb = rows_per_block(C);
   const int r0 = blockIdx.x * rpb;
   const int tid = threadIdx.x;
   float* pg = part + ((long long)g * gridDim.x + blockIdx.x) * 2 * C;
@@ -702,13 +697,6 @@ __global__ void bn_fold_kernel(const float* __restrict__ w, long long w_sstride,
   }
 }
 
-// elements per BN reduce block (DBA_BN_BLOCK_ELEMS, default 16384): sets rows_per_block, so
-// the partials' summation order — a per-replica geometry, never the group count
-int block_elems() {
-  static const int e = std::max(256, env_int_early("DBA_BN_BLOCK_ELEMS", 16384));
-  return e;
-}
-
 int egrid(long long n) { return (int)std::max(1LL, std::min(16384LL, (n + 255) / 256)); }
 
 int env_int(const char* name, int dflt) {
@@ -763,7 +751,7 @@ DBA_EXPORT int dba_bn_stats(const void* y, const int* nvalid, int G, int N, int 
     fin.eps = eps; fin.mean_out = mean; fin.invstd_out = invstd;
   }
   BN_T(f32, hipLaunchKernelGGL((bn_reduce_kernel<false, T>), dim3(nblk, G), dim3(256), 0, st, (const T*)y, nullptr,
-                               nullptr, nullptr, nullptr, 0, nvalid, N, HW, C, rows_per_block(C), part, fin));
+                               nullptr, nullptr, nullptr, 0, nvalid, N, HW, C, part, fin));
   if (!counter)
     hipLaunchKernelGGL(bn_finalize_kernel, dim3(ceil_div(C, C < 64 ? C : 64), G), dim3(256), 0, st, part, nblk, nvalid,
                        N, HW, C, rm, rv, s_gstride, momentum, eps, mean, invstd, G);
@@ -806,8 +794,7 @@ DBA_EXPORT int dba_bn_bwd(const void* dout, const void* out, const void* y, cons
     fin.counter = counter; fin.sums = sums; fin.dgamma = dgamma; fin.dbeta = dbeta; fin.g_gstride = g_gstride;
   }
   BN_T(f32, hipLaunchKernelGGL((bn_reduce_kernel<true, T>), dim3(nblk, G), dim3(256), 0, st, (const T*)y,
-                               (const T*)dout, (const T*)out, mean, invstd, relu, nvalid, N, HW, C, rows_per_block(C),
-                               part, fin));
+                               (const T*)dout, (const T*)out, mean, invstd, relu, nvalid, N, HW, C, part, fin));
   // launches of few replicas (a lone client's step): the finalize folds into the apply
   // (bn_bwd_apply_fin_kernel, same bits); DBA_BN_BWD_FUSE_G=0 keeps three launches
   if (!counter && G <= bwd_fuse_g()) {
