@@ -127,12 +127,15 @@ class Ctx:
         self._drop_ctr = 0
         self.act_dtype = act_dtype
         self._wamax = self._weight_scales() if train else None
-        # evaluation forwards of the fp32 family on the HIP backend keep conv-to-conv
-        # activations as fp16 pairs (ops.hip PairAct); DBA_EVAL_PAIRS=0 keeps fp32
+        # evaluation forwards of the fp32 family on the HIP backend may keep conv-to-conv
+        # activations as fp16 pairs (ops.hip PairAct, DBA_EVAL_PAIRS=1).  OFF by default: same-box
+        # A/B of the round-4 tree, 20 timed rounds after 5 warm-up rounds, twice each: 2.924 /
+        # 2.976 rounds/s with pairs vs 3.022 / 3.024 without (profiles/r4/bench_pairs*.json) —
+        # faster per conv in isolation (profiles/kbench_r3_eval_pairs.log), slower in the round
         self.eval_pairs = (not train and folded is not None and act_dtype == torch.float32
                            and any(t.is_cuda for t, _ in folded.values())
                            and ops.backend_name(next(iter(folded.values()))[0].device) == "hip"
-                           and os.environ.get("DBA_EVAL_PAIRS", "1") != "0")
+                           and os.environ.get("DBA_EVAL_PAIRS", "0") == "1")
 
     def _weight_scales(self) -> Optional[Dict[str, Tensor]]:
         """fp32 kernels on the fp16 pair (ops.hip F16_PAIR): every conv / linear weight's
