@@ -15,6 +15,7 @@
 // (common.hpp amax_fold) and, for a training BN, the fixed 32-row fp64 column sums / sums of
 // squares (same layout and definition as xgemm.hip bn_tile_stats).
 #include "common.hpp"
+#include "bnfuse.hpp"
 #include <cstdlib>
 
 namespace {
@@ -38,6 +39,7 @@ struct StemArgs {
   // fp16-pair output (xgemm.hip PairAct): per-replica exponent from the bound
   // L1max(w) * max|x| + max|b|; x's max slot, the slot's {L1max, bmax}
   int* out_sexp; const float* bound; const int* amax_x; int amax_x_ld;
+  BnFuse bf;                                // fused training BN statistics (bnfuse.hpp), mode 1
 };
 
 typedef __attribute__((ext_vector_type(2))) float f32x2s;
@@ -67,10 +69,10 @@ __global__ __launch_bounds__(256) void xstem_kernel(const StemArgs a) {
   const int tid = threadIdx.x;
   const int HoWo = a.Ho * a.Wo;
   const int Mv = valid_rows(a.nvalid, g, a.N) * HoWo;
-  const bool want_stats = a.bnpart != nullptr;
+  const bool want_stats = a.bnpart != nullptr || a.bf.mode == 1;
   const int mb = blockIdx.x * (ITER * PIX);
   if (mb >= Mv) {   // no valid pixel in the block's tiles: zero BN partials only
-    if (want_stats) {
+    if (a.bnpart) {
       for (int e = tid; e < ITER * (PIX / 32) * COUT; e += 256) {
         const int grp = e / COUT, c = e - grp * COUT, b = mb / 32 + grp;
         if (b >= a.bnpart_nblk) continue;
@@ -159,7 +161,25 @@ __global__ __launch_bounds__(256) void xstem_kernel(const StemArgs a) {
         for (int c = 0; c < CPT; ++c) tile[pl * COUT + c0 + c] = live ? acc[c] : 0.f;
       }
       __syncthreads();
-      for (int e = tid; e < (PIX / 32) * COUT; e += 256) {
+      if (a.bf.mode == 1) {   // level-0 records (bnfuse.hpp bnf_tile_records' order)
+        const int gv = ceil_div_d(Mv, kBnGrp);
+        for (int e = tid; e < (PIX / 32) * COUT; e += 256) {
+          const int grp = e / COUT, c = e - grp * COUT, b = m0 / 32 + grp;
+          if (b >= gv) continue;
+          double r4[4];
+          bnf_init(r4, 1);
+          for (int r = 0; r < 32; ++r) {
+            if (m0 + grp * 32 + r >= Mv) break;
+            const double v = (double)tile[(grp * 32 + r) * COUT + c];
+            r4[0] += v;
+            r4[1] = fma(v, v, r4[1]);
+            r4[2] = fmax(r4[2], v);
+            r4[3] = fmin(r4[3], v);
+          }
+          bnf_store_rec(a.bf.rec0, ((long long)g * a.bf.ngrp + b) * COUT + c, 0, r4[0], r4[1], r4[2], r4[3]);
+        }
+      }
+      for (int e = tid; e < (PIX / 32) * COUT && a.bnpart; e += 256) {
         const int grp = e / COUT, c = e - grp * COUT, b = m0 / 32 + grp;
         if (b >= a.bnpart_nblk) continue;
         double s0 = 0.0, s1 = 0.0;
@@ -177,13 +197,15 @@ __global__ __launch_bounds__(256) void xstem_kernel(const StemArgs a) {
     }
   }
   if (a.amax_out) amax_fold(a.amax_out, a.amax_ld, g, vmax);
+  if (a.bf.mode == 1) bnf_tile_done(a.bf, g, mb, ITER * PIX, 1, Mv);
 }
 
 template <int KH, int KW, int CIN, int COUT, int CPT>
 int stem_go(const StemArgs& a, int G, hipStream_t st) {
   constexpr int PIX = 256 / (COUT / CPT);
   constexpr int ITER = 4;   // pixel tiles per block: one weight load (LDS transpose) per 4 tiles
-  if (a.bnpart && PIX % 32 != 0) return -100;
+  if ((a.bnpart || a.bf.mode) && PIX % 32 != 0) return -100;
+  static_assert(kBnSg % (PIX * ITER) == 0 || PIX % 32 != 0, "a block covers whole groups of one super group");
   const long long M = (long long)a.N * a.Ho * a.Wo;
   const dim3 grid((unsigned)ceil_div(M, PIX * ITER), G);
   hipLaunchKernelGGL((xstem_kernel<KH, KW, CIN, COUT, CPT, ITER>), grid, dim3(256), 0, st, a);
@@ -199,7 +221,7 @@ DBA_EXPORT int dba_xstem_fwd(const float* x, long long x_gstride, const float* w
                              long long out_gstride, const int* nvalid, int G, int N, int H, int W, int Cin, int Ho,
                              int Wo, int Cout, int KH, int KW, int stride, int pad, int relu, int* amax_out,
                              int amax_ld, double* bnpart, const int* amax_x, int amax_x_ld, int* out_sexp,
-                             const float* bound, void* stream) {
+                             const float* bound, const void* bnf, void* stream) {
   if (env_off()) return -100;
   if (out_sexp && (!bound || !amax_x || bnpart || res)) return -107;
   if (((uintptr_t)out & 15) || (out_gstride & 3) || (res && ((uintptr_t)res & 15))) return -100;
@@ -211,6 +233,10 @@ DBA_EXPORT int dba_xstem_fwd(const float* x, long long x_gstride, const float* w
   a.relu = relu; a.amax_out = amax_out; a.amax_ld = amax_ld;
   a.bnpart = bnpart; a.bnpart_nblk = (int)ceil_div((long long)N * Ho * Wo, 32);
   a.out_sexp = out_sexp; a.bound = bound; a.amax_x = amax_x; a.amax_x_ld = amax_x_ld;
+  if (bnf) {
+    a.bf = *(const BnFuse*)bnf;
+    if (a.bf.mode != 1 || bias || res || relu || out_sexp || a.bf.C != Cout) return -108;
+  }
   hipStream_t st = (hipStream_t)stream;
   if (KH == 3 && KW == 3 && Cin == 3 && Cout == 32) return stem_go<3, 3, 3, 32, 8>(a, G, st);
   if (KH == 7 && KW == 7 && Cin == 3 && Cout == 64) return stem_go<7, 7, 3, 64, 8>(a, G, st);

@@ -28,6 +28,7 @@
 //   xtranspose      forward weights -> parity-class packed data-gradient weights;
 //   xcolsum         bias gradient (column sums, fixed order).
 #include "common.hpp"
+#include "bnfuse.hpp"
 #include <algorithm>
 #include <type_traits>
 #include <utility>
@@ -299,6 +300,13 @@ struct XArgs {
   // (replica, tile, class); out / out_gstride stay the real output
   float* sk_ws; long long sk_gstride;
   int* sk_cnt;
+  // training BN fused into the conv (bnfuse.hpp): forward statistics / backward mask + reduce of
+  // the OUTPUT (bf.mode), and the lazy BN(+ReLU) A operand: the source holds the pre-BN values y
+  // and every staged element is relu?(fma(y, scale, shift)) (lz_coef: the source BN's
+  // coefficient rows [G][kBnRows][Cs]; zero outside the image)
+  BnFuse bf;
+  const float* lz_coef;
+  int lz_relu;
   XClass cls[4];
 };
 
@@ -422,9 +430,10 @@ __device__ __forceinline__ void bn_tile_stats(const float* Ct, double* __restric
   }
 }
 
-template <int BM, int BN, int WM, int WN, int P, int VEC, bool H, bool PW = false, bool PA = false>
+template <int BM, int BN, int WM, int WN, int P, int VEC, bool H, bool PW = false, bool PA = false, bool LZ = false>
 __global__ __launch_bounds__(256) void xconv_kernel(const XArgs a) {
   static_assert(!H || P == 2, "fp16 split: 2 planes");
+  static_assert(!LZ || (H && !PA && VEC >= 4), "lazy BN operand: fp16 pair, fp32 source, 4-channel vectors");
   static_assert(!PW || (H && VEC >= 4), "pre-split weights: fp16 pair, vector loads");
   static_assert(!PA || (PW && VEC >= 4), "pre-split activations (PairAct): with pre-split weights");
   constexpr int TM = BM / WM, TN = BN / WN, MI = TM / 32, NJ = TN / 32;
@@ -434,6 +443,7 @@ __global__ __launch_bounds__(256) void xconv_kernel(const XArgs a) {
   static_assert(BM * BN <= 2 * P * PL * 4, "epilogue tile fits the LDS images");
   __shared__ __attribute__((aligned(16))) uint4 lds[2 * P * PL];
   __shared__ long long orow[BM];
+  __shared__ __attribute__((aligned(16))) float lzc[LZ ? 1024 : 4];   // lazy operand: scale | shift
 
   const int zc = blockIdx.z / a.splitk, kz = blockIdx.z - zc * a.splitk;
   const XClass c = a.cls[zc];
@@ -449,6 +459,13 @@ __global__ __launch_bounds__(256) void xconv_kernel(const XArgs a) {
   }
   const int slot = a.wsel ? a.wsel[g] : g;
   const int Cs = a.Cs;
+  if constexpr (LZ) {   // the source BN's scale / shift (Cs <= 512: checked on the host)
+    const float* cf = a.lz_coef + (long long)g * kBnRows * Cs;
+    for (int c = threadIdx.x; c < Cs; c += 256) {
+      lzc[c] = cf[kCScale * Cs + c];
+      lzc[512 + c] = cf[kCShift * Cs + c];
+    }
+  }
   const int K = c.nI * c.nJ * Cs;
   const int nkt = (K + 31) >> 5;
   const int kt0 = (int)((long long)nkt * kz / a.splitk), kt1 = (int)((long long)nkt * (kz + 1) / a.splitk);
@@ -514,10 +531,13 @@ __global__ __launch_bounds__(256) void xconv_kernel(const XArgs a) {
   float4 ra[2][RA], rb[2][RB];
   int g_kb = 0, g_toff = 0, g_dh = 0, g_dw = 0;   // VEC >= 4: the prepared step's geometry
   bool g_kv = false;
+  int g_kc = 0;                                   // LZ: the prepared step's first channel
+  int s_kq[2][RA];                                // LZ: per stage / A quarter: channel | in-image << 16
   int e_off[4], e_dh[4], e_dw[4];                 // VEC 1: per element
   bool e_kv[4];
   auto gprep = [&]() __attribute__((always_inline)) {   // the step at the current reduction state, then advance it
     g_kb = (ki * c.nJ + kj) * Cs + kc;   // == kt*32 + kq*4
+    g_kc = kc;
     if constexpr (VEC >= 4) {
       g_kv = ki < c.nI;
       g_dh = a.dsg * ki;
@@ -556,6 +576,7 @@ __global__ __launch_bounds__(256) void xconv_kernel(const XArgs a) {
       if constexpr (VEC >= 4) {
         const bool ok = g_kv && (unsigned)(ah[q] + g_dh) < (unsigned)a.Hs && (unsigned)(aw[q] + g_dw) < (unsigned)a.Ws;
         ra[st][q] = bload4(rA, ok ? (abase[q] + g_toff) * 4 : kOOB);
+        if constexpr (LZ) s_kq[st][q] = g_kc | ((int)ok << 16);
       } else {
         float v[4];
 #pragma unroll
@@ -599,6 +620,15 @@ __global__ __launch_bounds__(256) void xconv_kernel(const XArgs a) {
         const uint4 u = __builtin_bit_cast(uint4, ra[st][q]);
         sp[0] = make_uint2(u.x, u.y);
         sp[1] = make_uint2(u.z, u.w);
+      } else if constexpr (LZ) {   // relu?(fma(y, scale, shift)) in the image, 0 in the padding
+        const int kq4 = s_kq[st][q] & 0xffff;
+        const bool ok = (s_kq[st][q] >> 16) != 0;
+        const float4 sc = *(const float4*)&lzc[kq4], sh = *(const float4*)&lzc[512 + kq4];
+        float4 v = ra[st][q];
+        v.x = fmaf(v.x, sc.x, sh.x); v.y = fmaf(v.y, sc.y, sh.y); v.z = fmaf(v.z, sc.z, sh.z); v.w = fmaf(v.w, sc.w, sh.w);
+        if (a.lz_relu) { v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f); }
+        if (!ok) v = make_float4(0.f, 0.f, 0.f, 0.f);
+        split4h(v.x, v.y, v.z, v.w, hs.ma, sp);
       } else if constexpr (H) {
         split4h(ra[st][q].x, ra[st][q].y, ra[st][q].z, ra[st][q].w, hs.ma, sp);
       } else {
@@ -628,6 +658,7 @@ __global__ __launch_bounds__(256) void xconv_kernel(const XArgs a) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
+  if constexpr (LZ) __syncthreads();   // lzc
   if (kt0 < kt1) {
     // loads past the slice's last step are harmless (past K they zero-fill), so the loop body
     // has no branches and the accumulators stay in place across iterations
@@ -681,6 +712,7 @@ __global__ __launch_bounds__(256) void xconv_kernel(const XArgs a) {
     }
   }
   if (fin && a.bnpart) bn_tile_stats<BM, BN>(Ct, a.bnpart, a.bnpart_nblk, g, a.Ncol, m0, n0, false);
+  const int bfm = fin ? a.bf.mode : 0;   // fused training BN of the output (bnfuse.hpp)
   float* out = a.out + (long long)g * a.out_gstride + (fin ? 0 : (long long)kz * a.zstride);
   const float* bias = (fin && a.bias) ? a.bias + (long long)slot * a.b_sstride : nullptr;
   const float* res = (fin && a.res) ? a.res + (long long)g * a.out_gstride : nullptr;
@@ -709,6 +741,10 @@ __global__ __launch_bounds__(256) void xconv_kernel(const XArgs a) {
         v.x += rv.x; v.y += rv.y; v.z += rv.z; v.w += rv.w;
       }
       if (relu) { v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f); }
+      if (bfm == 2) {   // backward: d = the gradient where the BN(+ReLU) output is > 0
+        v = bnf_mask4(a.bf, g, o, n, v);
+        *(float4*)&Ct[row * BN + cc] = v;
+      }
       vmax = fmaxf(vmax, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
       if (fin && a.out_sexp) *(uint4*)(out + o + n) = PairAct::encode(v, omul);
       else *(float4*)(out + o + n) = v;
@@ -728,6 +764,11 @@ __global__ __launch_bounds__(256) void xconv_kernel(const XArgs a) {
     }
   }
   if (fin && a.amax_out) amax_fold(a.amax_out, a.amax_out_ld, g, vmax);
+  if (bfm) {
+    __syncthreads();   // d in Ct (backward)
+    bnf_tile_records<BM, BN>(a.bf, Ct, orow, g, m0, n0, Mv);
+    bnf_tile_done(a.bf, g, m0, BM, a.tiles_n, Mv);
+  }
 }
 
 // ======================================================================= halo conv
@@ -753,9 +794,11 @@ __device__ __forceinline__ int hswz(int pp, int col) {
   else return (col >> 1) & 7;
 }
 
-template <int W, int CS, int BM, int BN, int WM, int WN, int P, bool H, bool PRE = false, bool PA = false>
+template <int W, int CS, int BM, int BN, int WM, int WN, int P, bool H, bool PRE = false, bool PA = false,
+          bool LZ = false>
 __global__ __launch_bounds__(256) void xhalo_kernel(const XArgs a) {
   static_assert(!H || P == 2, "fp16 split: 2 planes");
+  static_assert(!LZ || (H && !PA), "lazy BN operand: fp16 pair, fp32 source");
   static_assert(!PRE || H, "pre-split weights: fp16 pair");
   static_assert(!PA || PRE, "pre-split activations (PairAct): with pre-split weights");
   constexpr int TR = BM / W, PW = W + 2, PR = TR + 2, PP = PR * PW;
@@ -776,7 +819,8 @@ __global__ __launch_bounds__(256) void xhalo_kernel(const XArgs a) {
   const int tn = blockIdx.x % a.tiles_n, tm = blockIdx.x / a.tiles_n;
   const int img = tm / HT, h0 = (tm - img * HT) * TR;
   const int n0 = tn * BN;
-  if (img >= valid_rows(a.nvalid, g, a.N)) {
+  const int nv_img = valid_rows(a.nvalid, g, a.N);
+  if (img >= nv_img) {
     if (a.bnpart) bn_tile_stats<BM, BN>(nullptr, a.bnpart, a.bnpart_nblk, g, a.Ncol, tm * BM, n0, true);
     return;
   }
@@ -812,6 +856,7 @@ __global__ __launch_bounds__(256) void xhalo_kernel(const XArgs a) {
   HScale hs;
   if constexpr (H)
     hs.init(amax_read(a.amax_src, a.amax_src_ld, g), amax_read(a.amax_w, a.amax_w_ld, slot), PA ? a.in_sexp : nullptr, g);
+  const float* lzc = LZ ? a.lz_coef + (long long)g * kBnRows * CS : nullptr;
   auto patch_put = [&]() __attribute__((always_inline)) {
 #pragma unroll
     for (int u = 0; u < NE; ++u) {
@@ -823,6 +868,16 @@ __global__ __launch_bounds__(256) void xhalo_kernel(const XArgs a) {
         const uint4 uu = __builtin_bit_cast(uint4, pv[u]);
         sp[0] = make_uint2(uu.x, uu.y);
         sp[1] = make_uint2(uu.z, uu.w);
+      } else if constexpr (LZ) {   // relu?(fma(y, scale, shift)) in the image, 0 in the padding
+        const int pr = pp / PW, pc = pp - pr * PW;
+        const int h = h0 - 1 + pr, w = pc - 1;
+        const bool ok = (unsigned)h < (unsigned)a.Hs && (unsigned)w < (unsigned)a.Ws;
+        const float4 sc = *(const float4*)(lzc + kCScale * CS + q * 4), sh = *(const float4*)(lzc + kCShift * CS + q * 4);
+        float4 v = pv[u];
+        v.x = fmaf(v.x, sc.x, sh.x); v.y = fmaf(v.y, sc.y, sh.y); v.z = fmaf(v.z, sc.z, sh.z); v.w = fmaf(v.w, sc.w, sh.w);
+        if (a.lz_relu) { v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f); }
+        if (!ok) v = make_float4(0.f, 0.f, 0.f, 0.f);
+        split4h(v.x, v.y, v.z, v.w, hs.ma, sp);
       } else if constexpr (H) {
         split4h(pv[u].x, pv[u].y, pv[u].z, pv[u].w, hs.ma, sp);
       } else {
@@ -981,11 +1036,21 @@ __global__ __launch_bounds__(256) void xhalo_kernel(const XArgs a) {
       v.x += rv.x; v.y += rv.y; v.z += rv.z; v.w += rv.w;
     }
     if (a.relu) { v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f); }
+    if (a.bf.mode == 2) {   // backward: d = the gradient where the BN(+ReLU) output is > 0
+      v = bnf_mask4(a.bf, g, o, n, v);
+      *(float4*)&Ct[row * BN + cc] = v;
+    }
     vmax = fmaxf(vmax, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
     if (a.out_sexp) *(uint4*)(out + o + n) = PairAct::encode(v, omul);
     else *(float4*)(out + o + n) = v;
   }
   if (a.amax_out) amax_fold(a.amax_out, a.amax_out_ld, g, vmax);
+  if (a.bf.mode) {
+    __syncthreads();   // d in Ct (backward)
+    const int Mv = nv_img * a.Ho * a.Wo;
+    bnf_tile_records<BM, BN>(a.bf, Ct, orow, g, tm * BM, n0, Mv);
+    bnf_tile_done(a.bf, g, tm * BM, BM, a.tiles_n, Mv);
+  }
 }
 
 // ============================================================ persistent halo conv
@@ -1242,11 +1307,18 @@ struct XWArgs {
   const int* amax_x;
   int amax_dy_ld, amax_x_ld;
   FDiv dHoWo, dWo;
+  // lazy operands (bnfuse.hpp).  DLZ: dy = fma(A, d, fma(B, y, K)) of the BN below the conv
+  // (dy points at d; dy_y: that BN's input y; dy_coef: its rows [G][kBnRows][Cout]); the k-tile-0
+  // blocks store dy once to dy_out (the data gradient's operand).  XLZ: x = relu?(fma(y, scale,
+  // shift)) of the BN that produced the conv's input (x points at y; zero in the padding).
+  const float* dy_y; const float* dy_coef; float* dy_out;
+  const float* x_coef; int x_relu;
 };
 
-template <int BNO, int BK, int WN_, int WK_, int P, int VEC, bool H>
+template <int BNO, int BK, int WN_, int WK_, int P, int VEC, bool H, bool DLZ = false, bool XLZ = false>
 __global__ __launch_bounds__(256) void xwgrad_kernel(const XWArgs a) {
   static_assert(!H || P == 2, "fp16 split: 2 planes");
+  static_assert(!(DLZ || XLZ) || H, "lazy BN operands: fp16 pair");
   constexpr int TNo = BNO / WN_, TK = BK / WK_, MI = TNo / 32, NJ = TK / 32;
   static_assert(WN_ * WK_ == 4 && MI >= 1 && NJ >= 1, "wave tiling");
   static_assert(BK == 128, "x micro-tiles: one per thread");
@@ -1285,6 +1357,30 @@ __global__ __launch_bounds__(256) void xwgrad_kernel(const XWArgs a) {
   }
 
   float dv[2][4][4], xv[2][4][4];   // [stage][m][n or k]
+  float yv[DLZ ? 2 : 1][4][4];      // DLZ: the BN input y at dy's positions
+  int s_mt[2] = {0, 0};             // the m-step each stage holds (DLZ: row validity)
+  unsigned s_xok[2] = {0u, 0u};     // XLZ: in-image bit (r * 4 + e) per stage
+  float cA[4], cB[4], cK[4], xsc[4], xsh[4];
+  if constexpr (DLZ) {
+    const float* cf = a.dy_coef + (long long)g * kBnRows * a.Cout;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const bool ok = dact && dn + e < a.Cout;
+      cA[e] = ok ? cf[kCA * a.Cout + dn + e] : 0.f;
+      cB[e] = ok ? cf[kCB * a.Cout + dn + e] : 0.f;
+      cK[e] = ok ? cf[kCK * a.Cout + dn + e] : 0.f;
+    }
+  }
+  if constexpr (XLZ) {
+    const float* cf = a.x_coef + (long long)g * kBnRows * a.Cin;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      xsc[e] = xkv[e] ? cf[kCScale * a.Cin + xc[e]] : 0.f;
+      xsh[e] = xkv[e] ? cf[kCShift * a.Cin + xc[e]] : 0.f;
+    }
+  }
+  const __amdgpu_buffer_rsrc_t rY = rsrc(DLZ ? a.dy_y + (long long)g * a.dy_gstride : nullptr,
+                                         (long long)a.N * HoWo * a.Cout * 4);
   // bounds-checked buffer loads (32-bit in-replica offsets: checked on the host)
   const __amdgpu_buffer_rsrc_t rD = rsrc(dy, (long long)a.N * HoWo * a.Cout * 4);
   const __amdgpu_buffer_rsrc_t rX = rsrc(x, (long long)a.N * a.H * a.W * a.Cin * 4);
@@ -1293,11 +1389,17 @@ __global__ __launch_bounds__(256) void xwgrad_kernel(const XWArgs a) {
     const int m0 = mt + m4 * 4;
     if constexpr (VEC == 4) {
       if (part == 0) {
+        s_mt[st] = mt;
         if (dact) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const float4 v = bload4(rD, (m0 + r < me && dn < a.Cout) ? ((m0 + r) * a.Cout + dn) * 4 : kOOB);
+            const int off = (m0 + r < me && dn < a.Cout) ? ((m0 + r) * a.Cout + dn) * 4 : kOOB;
+            const float4 v = bload4(rD, off);
             dv[st][r][0] = v.x; dv[st][r][1] = v.y; dv[st][r][2] = v.z; dv[st][r][3] = v.w;
+            if constexpr (DLZ) {
+              const float4 u = bload4(rY, off);
+              yv[st][r][0] = u.x; yv[st][r][1] = u.y; yv[st][r][2] = u.z; yv[st][r][3] = u.w;
+            }
           }
         }
         return;
@@ -1313,23 +1415,30 @@ __global__ __launch_bounds__(256) void xwgrad_kernel(const XWArgs a) {
       const int h = p * a.stride - a.pad + xkh[0];
       const bool hok = xkv[0] && (unsigned)h < (unsigned)a.H;
       const int xrow = (img * a.H + h) * a.W;
+      unsigned okm = 0u;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int w = (q + r) * a.stride - a.pad + xkw[0];
         const bool ok = m0 + r < me && hok && (unsigned)w < (unsigned)a.W;
         const float4 v = bload4(rX, ok ? ((xrow + w) * a.Cin + xc[0]) * 4 : kOOB);
         xv[st][r][0] = v.x; xv[st][r][1] = v.y; xv[st][r][2] = v.z; xv[st][r][3] = v.w;
+        okm |= ok ? (0xfu << (r * 4)) : 0u;
       }
+      if constexpr (XLZ) s_xok[st] = okm;
     } else {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int m = m0 + r;
         const bool mv = m < me;
         if (part == 0) {
+          s_mt[st] = mt;
           if (dact) {
 #pragma unroll
-            for (int e = 0; e < 4; ++e)
-              dv[st][r][e] = bload1(rD, (mv && dn + e < a.Cout) ? (m * a.Cout + dn + e) * 4 : kOOB);
+            for (int e = 0; e < 4; ++e) {
+              const int off = (mv && dn + e < a.Cout) ? (m * a.Cout + dn + e) * 4 : kOOB;
+              dv[st][r][e] = bload1(rD, off);
+              if constexpr (DLZ) yv[st][r][e] = bload1(rY, off);
+            }
           }
           continue;
         }
@@ -1346,6 +1455,10 @@ __global__ __launch_bounds__(256) void xwgrad_kernel(const XWArgs a) {
           const int h = hb + xkh[e], w = wb + xkw[e];
           const bool ok = mv && xkv[e] && (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W;
           xv[st][r][e] = bload1(rX, ok ? (((img * a.H + h) * a.W + w) * a.Cin + xc[e]) * 4 : kOOB);
+          if constexpr (XLZ) {
+            if (r == 0 && e == 0) s_xok[st] = 0u;
+            s_xok[st] |= ok ? (1u << (r * 4 + e)) : 0u;
+          }
         }
       }
     }
@@ -1357,9 +1470,37 @@ __global__ __launch_bounds__(256) void xwgrad_kernel(const XWArgs a) {
   // piece q of stage st -> LDS buffer buf: q < 4 transposes dy column e = q, q >= 4 x column q-4
   HScale hs;
   if constexpr (H) hs.init(amax_read(a.amax_dy, a.amax_dy_ld, g), amax_read(a.amax_x, a.amax_x_ld, g));
+  const bool dy_store = DLZ && a.dy_out != nullptr && tk == 0;
+  float* __restrict__ dyo = DLZ && a.dy_out ? a.dy_out + (long long)g * a.dy_gstride : nullptr;
   auto lput_q = [&](int buf, int st, int q) __attribute__((always_inline)) {
     uint4* L = lds + buf * P * PL;
     uint2 sp[P];
+    if constexpr (DLZ) {
+      if (q == 0 && dact) {   // dy of the stage's 4 x 4 micro tile (0 past the rows / channels)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = s_mt[st] + m4 * 4 + r;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const bool ok = m < me && dn + e < a.Cout;
+            const float v = fmaf(cA[e], dv[st][r][e], fmaf(cB[e], yv[st][r][e], cK[e]));
+            dv[st][r][e] = ok ? v : 0.f;
+            if (dy_store && ok) dyo[(long long)m * a.Cout + dn + e] = v;
+          }
+        }
+      }
+    }
+    if constexpr (XLZ) {
+      if (q >= 4) {
+        const int e = q - 4;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float v = fmaf(xv[st][r][e], xsc[e], xsh[e]);
+          if (a.x_relu) v = fmaxf(v, 0.f);
+          xv[st][r][e] = ((s_xok[st] >> (r * 4 + e)) & 1u) ? v : 0.f;
+        }
+      }
+    }
     if (q < 4) {
       if (dact) {
         if constexpr (H) split4h(dv[st][0][q], dv[st][1][q], dv[st][2][q], dv[st][3][q], hs.ma, sp);
@@ -1695,7 +1836,134 @@ __global__ __launch_bounds__(256) void xcolsum_kernel(const float* __restrict__ 
   }
 }
 
+// ===================================================== fused training BN: standalone pass
+// One block per (super group, replica) over a MATERIALISED tensor, for the producers whose
+// epilogue cannot reduce (the separate split-K reduce of multi-replica launches, stride-s data
+// gradients, the global average pool's gradient, max-pool gradients): the same level-0 records
+// in the same order as bnf_tile_records, summed into the SG record in group order, then the
+// replica ticket (bnfuse.hpp).  mode 1: statistics of src; mode 2: d = mask(g) -> dst (may alias
+// src), g = src or, with pool, pool[g][img][c] * pool_scale (the global average pool's gradient,
+// elementwise.hip avgpool_bwd's value).
+__global__ __launch_bounds__(256) void bnx_rows_kernel(const BnFuse f, const float* __restrict__ src, float* dst,
+                                                       long long gstride, const int* __restrict__ nvalid, int N, int HW,
+                                                       const float* __restrict__ pool, float pool_scale) {
+  __shared__ double rec[kBnGpS][64][4];   // one 64-channel chunk of the SG's group records
+  const int s = blockIdx.x, g = blockIdx.y, tid = threadIdx.x;
+  const int Mv = valid_rows(nvalid, g, N) * HW;
+  const int r0 = s * kBnSg;
+  if (r0 >= Mv) return;
+  const int r1 = min(Mv, r0 + kBnSg);
+  const int C = f.C;
+  const float* sgp = pool ? nullptr : src + (long long)g * gstride;
+  float* dg = dst ? dst + (long long)g * gstride : nullptr;
+  const float* ya = f.mode == 2 && f.ya ? f.ya + (long long)g * gstride : nullptr;
+  const float* yb = f.mode == 2 && f.yb ? f.yb + (long long)g * gstride : nullptr;
+  const float* mo = f.mask_out ? f.mask_out + (long long)g * gstride : nullptr;
+  const float* ca = f.coef_a + (long long)g * kBnRows * C;
+  const float* cb = f.coef_b ? f.coef_b + (long long)g * kBnRows * C : nullptr;
+  const int ngv = ceil_div_d(r1 - r0, kBnGrp);
+  for (int c0 = 0; c0 < C; c0 += 64) {
+    const int cw = min(64, C - c0);
+    for (int e = tid; e < kBnGpS * 64; e += 256) {
+      const int j = e / 64, cc = e - j * 64, c = c0 + cc;
+      const int b0 = r0 + j * kBnGrp;
+      double a[4];
+      bnf_init(a, f.mode);
+      if (cc < cw && b0 < r1) {
+        if (f.mode == 1) {
+          for (int m = b0; m < min(r1, b0 + kBnGrp); ++m) {
+            const double v = (double)sgp[(long long)m * C + c];
+            a[0] += v;
+            a[1] = fma(v, v, a[1]);
+            a[2] = fmax(a[2], v);
+            a[3] = fmin(a[3], v);
+          }
+        } else {
+          const float ma = ca[kCMean * C + c], ia = ca[kCInv * C + c];
+          const float sc = ca[kCScale * C + c], sh = ca[kCShift * C + c];
+          const float mb = cb ? cb[kCMean * C + c] : 0.f, ib = cb ? cb[kCInv * C + c] : 0.f;
+          for (int m = b0; m < min(r1, b0 + kBnGrp); ++m) {
+            const long long o = (long long)m * C + c;
+            const float gv = pool ? pool[((long long)g * N + m / HW) * C + c] * pool_scale : sgp[o];
+            const float y = ya[o];
+            const bool keep = mo ? mo[o] > 0.f : (f.mask_lazy ? fmaf(y, sc, sh) > 0.f : true);
+            const float d = keep ? gv : 0.f;
+            dg[o] = d;
+            a[0] += (double)d;
+            a[1] = fma((double)d, (double)((y - ma) * ia), a[1]);
+            if (yb) a[2] = fma((double)d, (double)((yb[o] - mb) * ib), a[2]);
+            a[3] = fmax(a[3], (double)fabsf(d));
+          }
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) rec[j][cc][k] = a[k];
+    }
+    __syncthreads();
+    if (tid < cw) {
+      double a[4];
+      bnf_init(a, f.mode);
+      for (int j = 0; j < ngv; ++j) {
+        const double v[4] = {rec[j][tid][0], rec[j][tid][1], rec[j][tid][2], rec[j][tid][3]};
+        bnf_acc(a, v, f.mode);
+      }
+      bnf_store_rec(f.rec1, ((long long)g * f.nsg + s) * C + c0 + tid, 0, a[0], a[1], a[2], a[3]);
+    }
+    __syncthreads();
+  }
+  const int nsg_v = ceil_div_d(Mv, kBnSg);
+  if (bnf_arrive(f.cnt2 + g, nsg_v)) bnf_finalize_replica(f, g, nsg_v, (double)Mv);
+}
+
+// The materialised output of a training BN (+ residual) (+ ReLU) (bnfuse.hpp): out =
+// relu?(fma(ya, scale_a, shift_a) + r), r = res (identity shortcut) or fma(yb, scale_b, shift_b)
+// (a shortcut conv's BN; relu_b: a lazy BN+ReLU output, e.g. the stem's) or 0 — bn.hip
+// bn_apply's arithmetic; folds max |out| for the fp16-pair operand scale of its consumers.
+// Valid rows only.
+__global__ __launch_bounds__(256) void bnx_apply_kernel(const float* __restrict__ ya, const float* __restrict__ ca,
+                                                        const float* __restrict__ res, const float* __restrict__ yb,
+                                                        const float* __restrict__ cb, int relu_b, int relu,
+                                                        float* __restrict__ out,
+                                                        long long gstride, const int* __restrict__ nvalid, int N,
+                                                        int HW, int C, int* __restrict__ amax, int amax_ld) {
+  const int g = blockIdx.y;
+  const int C4 = C >> 2;
+  const long long total = (long long)valid_rows(nvalid, g, N) * HW * C4;
+  const long long base = (long long)g * gstride;
+  const float* cag = ca + (long long)g * kBnRows * C;
+  const float* cbg = cb ? cb + (long long)g * kBnRows * C : nullptr;
+  float vmax = 0.f;
+  for (long long t = blockIdx.x * 256LL + threadIdx.x; t < total; t += (long long)gridDim.x * 256) {
+    const int c = (int)(t % C4) * 4;
+    const long long o = base + t * 4;
+    const float4 y = *(const float4*)(ya + o);
+    const float4 sc = *(const float4*)(cag + kCScale * C + c), sh = *(const float4*)(cag + kCShift * C + c);
+    float4 v = make_float4(fmaf(y.x, sc.x, sh.x), fmaf(y.y, sc.y, sh.y), fmaf(y.z, sc.z, sh.z), fmaf(y.w, sc.w, sh.w));
+    if (res) {
+      const float4 r = *(const float4*)(res + o);
+      v.x += r.x; v.y += r.y; v.z += r.z; v.w += r.w;
+    } else if (yb) {
+      const float4 u = *(const float4*)(yb + o);
+      const float4 sb = *(const float4*)(cbg + kCScale * C + c), hb = *(const float4*)(cbg + kCShift * C + c);
+      float4 b = make_float4(fmaf(u.x, sb.x, hb.x), fmaf(u.y, sb.y, hb.y), fmaf(u.z, sb.z, hb.z), fmaf(u.w, sb.w, hb.w));
+      if (relu_b) { b.x = fmaxf(b.x, 0.f); b.y = fmaxf(b.y, 0.f); b.z = fmaxf(b.z, 0.f); b.w = fmaxf(b.w, 0.f); }
+      v.x += b.x; v.y += b.y; v.z += b.z; v.w += b.w;
+    }
+    if (relu) { v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f); }
+    vmax = fmaxf(vmax, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+    *(float4*)(out + o) = v;
+  }
+  if (amax) amax_fold(amax, amax_ld, g, vmax);
+}
+
 // ============================================================================ host
+int bnx_rows_go(const BnFuse& f, const float* src, float* dst, long long gstride, const int* nvalid, int G, int N,
+                int HW, const float* pool, float pool_scale, hipStream_t st) {
+  const dim3 grid((unsigned)ceil_div((long long)N * HW, kBnSg), G);
+  hipLaunchKernelGGL(bnx_rows_kernel, grid, dim3(256), 0, st, f, src, dst, gstride, nvalid, N, HW, pool, pool_scale);
+  DBA_LAUNCH_CHECK();
+}
+
 int env_int(const char* name, int dflt) {
   const char* e = getenv(name);
   return e ? atoi(e) : dflt;
@@ -1710,35 +1978,36 @@ int& planes() {
   return p;
 }
 
-template <int BM, int BN, int WM, int WN, int P, int VEC, bool H, bool PW, bool PA = false>
+template <int BM, int BN, int WM, int WN, int P, int VEC, bool H, bool PW, bool PA = false, bool LZ = false>
 int xconv_go(const XArgs& a, long long Mmax, int G, int nclass, hipStream_t st) {
   XArgs b = a;
   b.tiles_n = ceil_div(a.Ncol, BN);
   const dim3 grid((unsigned)(ceil_div(Mmax, BM) * b.tiles_n), G, nclass * a.splitk);
-  hipLaunchKernelGGL((xconv_kernel<BM, BN, WM, WN, P, VEC, H, PW, PA>), grid, dim3(256), 0, st, b);
+  hipLaunchKernelGGL((xconv_kernel<BM, BN, WM, WN, P, VEC, H, PW, PA, LZ>), grid, dim3(256), 0, st, b);
   DBA_LAUNCH_CHECK();
 }
 
-template <int P, int VEC, bool H, bool PW = false, bool PA = false>
+template <int P, int VEC, bool H, bool PW = false, bool PA = false, bool LZ = false>
 int xconv_tile(const XArgs& a, long long Mmax, int G, int nclass, int bm, hipStream_t st) {
-  if (a.Ncol <= 32) return xconv_go<128, 32, 4, 1, P, VEC, H, PW, PA>(a, Mmax, G, nclass, st);
+  if (a.Ncol <= 32) return xconv_go<128, 32, 4, 1, P, VEC, H, PW, PA, LZ>(a, Mmax, G, nclass, st);
   if (a.Ncol <= 64) {
-    if (bm == 64) return xconv_go<64, 64, 2, 2, P, VEC, H, PW, PA>(a, Mmax, G, nclass, st);
-    return xconv_go<128, 64, 2, 2, P, VEC, H, PW, PA>(a, Mmax, G, nclass, st);
+    if (bm == 64) return xconv_go<64, 64, 2, 2, P, VEC, H, PW, PA, LZ>(a, Mmax, G, nclass, st);
+    return xconv_go<128, 64, 2, 2, P, VEC, H, PW, PA, LZ>(a, Mmax, G, nclass, st);
   }
-  if (bm == 32) return xconv_go<32, 128, 1, 4, P, VEC, H, PW, PA>(a, Mmax, G, nclass, st);
-  if (bm == 64) return xconv_go<64, 128, 2, 2, P, VEC, H, PW, PA>(a, Mmax, G, nclass, st);
-  return xconv_go<128, 128, 2, 2, P, VEC, H, PW, PA>(a, Mmax, G, nclass, st);
+  if (bm == 32) return xconv_go<32, 128, 1, 4, P, VEC, H, PW, PA, LZ>(a, Mmax, G, nclass, st);
+  if (bm == 64) return xconv_go<64, 128, 2, 2, P, VEC, H, PW, PA, LZ>(a, Mmax, G, nclass, st);
+  return xconv_go<128, 128, 2, 2, P, VEC, H, PW, PA, LZ>(a, Mmax, G, nclass, st);
 }
 
 bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
-template <int W, int CS, int BM, int BN, int WM, int WN, int P, bool H, bool PRE = false, bool PA = false>
+template <int W, int CS, int BM, int BN, int WM, int WN, int P, bool H, bool PRE = false, bool PA = false,
+          bool LZ = false>
 int xhalo_go(const XArgs& a, int G, hipStream_t st) {
   XArgs b = a;
   b.tiles_n = ceil_div(a.Ncol, BN);
   const dim3 grid((unsigned)(a.N * (a.Ho / (BM / W)) * b.tiles_n), G, 1);
-  hipLaunchKernelGGL((xhalo_kernel<W, CS, BM, BN, WM, WN, P, H, PRE, PA>), grid, dim3(256), 0, st, b);
+  hipLaunchKernelGGL((xhalo_kernel<W, CS, BM, BN, WM, WN, P, H, PRE, PA, LZ>), grid, dim3(256), 0, st, b);
   DBA_LAUNCH_CHECK();
 }
 
@@ -1754,7 +2023,7 @@ int& halo_ws_on() {
 }
 int xhalo_ws_try(const XArgs& a, int G, hipStream_t st) {
   static const int blocks = env_int("DBA_F32_HALO_WS_BLOCKS", 512);
-  if (!halo_ws_on() || a.Ho % 4 != 0) return -100;
+  if (!halo_ws_on() || a.Ho % 4 != 0 || a.bf.mode || a.lz_coef) return -100;
   if (a.wp && (((uintptr_t)a.wp & 15) || (a.wp_sstride % 8))) return -100;
   // the item count: valid images of every replica (host view: nvalid lives on the device, so
   // size the grid for all N images; blocks past the valid items return at once)
@@ -1766,6 +2035,8 @@ int xhalo_ws_try(const XArgs& a, int G, hipStream_t st) {
   else hipLaunchKernelGGL((xhalo_ws_kernel<4, false>), grid, dim3(256), 0, st, a, G);
   DBA_LAUNCH_CHECK();
 }
+
+bool flip_dgrad(const XArgs& a) { return a.dsg < 0; }
 
 // the halo kernel's shapes: 3x3 stride-1 pad-1 (fwd) or its stride-1 data gradient, one class,
 // square W 32, Cs 32, Ncol <= 32, aligned fp32 operands (DBA_F32_HALO=0 off)
@@ -1782,7 +2053,9 @@ int xhalo_try(const XArgs& a, int G, int KH, int KW, hipStream_t st) {
   const bool big = big_ok && a.Ho % 8 == 0 && (long long)a.N * (a.Ho / 8) * G >= 1024;
   const bool pairs = a.in_sexp || a.out_sexp || a.res_sexp;
   if (pairs && !(a.amax_src && a.wp)) return -107;   // fp16-pair activations: evaluation forwards only
+  if (a.lz_coef && (!a.amax_src || pairs || a.wp || flip_dgrad(a))) return -108;   // lazy BN operand: training fwd
   if (a.Wo == 32 && a.Cs == 32 && a.Ncol <= 32 && a.Ho % 4 == 0) {
+    if (a.lz_coef) return xhalo_go<32, 32, 128, 32, 4, 1, 2, true, false, false, true>(a, G, st);
     if (a.in_sexp) return xhalo_go<32, 32, 128, 32, 4, 1, 2, true, true, true>(a, G, st);
     if (a.amax_src && a.Ncol == 32 && !pairs) {
       const int rc = xhalo_ws_try(a, G, st);
@@ -1799,6 +2072,7 @@ int xhalo_try(const XArgs& a, int G, int KH, int KW, hipStream_t st) {
   // work dominates and the implicit GEMM was faster: 154 vs 147 TF, kbench_r2_fp32_p3.json)
   static const bool h16 = env_int("DBA_F32_HALO16", 1) != 0;
   if (h16 && a.amax_src && a.Wo == 16 && a.Cs == 64 && a.Ncol <= 64 && a.Ho % 8 == 0) {
+    if (a.lz_coef) return xhalo_go<16, 64, 128, 64, 2, 2, 2, true, false, false, true>(a, G, st);
     if (a.in_sexp) return xhalo_go<16, 64, 128, 64, 2, 2, 2, true, true, true>(a, G, st);
     if (a.wp) return xhalo_go<16, 64, 128, 64, 2, 2, 2, true, true>(a, G, st);
     return xhalo_go<16, 64, 128, 64, 2, 2, 2, true>(a, G, st);
@@ -1848,6 +2122,10 @@ int xconv_dispatch(const XArgs& a, long long Mmax, int G, int nclass, int vec, h
   if (a.in_sexp) {   // fp16-pair activations (evaluation; the launcher checked wp and vec)
     if (vec == 32) return xconv_tile<2, 32, true, true, true>(a, Mmax, G, nclass, bm, st);
     return xconv_tile<2, 4, true, true, true>(a, Mmax, G, nclass, bm, st);
+  }
+  if (a.lz_coef) {   // lazy BN operand (training forward; the launcher checked amax, wp, vec)
+    if (vec == 32) return xconv_tile<2, 32, true, false, false, true>(a, Mmax, G, nclass, bm, st);
+    return xconv_tile<2, 4, true, false, false, true>(a, Mmax, G, nclass, bm, st);
   }
   if (a.amax_src && a.wp && vec >= 4) {
     if (vec == 32) return xconv_tile<2, 32, true, true>(a, Mmax, G, nclass, bm, st);
@@ -1959,7 +2237,7 @@ DBA_EXPORT int dba_xconv_fwd(const float* x, long long x_gstride, const float* w
                              const uint16_t* wp, long long wp_sstride, float* ws, long long ws_floats,
                              double* bnpart, const int* in_sexp, int* out_sexp, const float* bound,
                              const int* amax_res, int amax_res_ld, const int* res_sexp, int* sk_cnt,
-                             long long sk_cnt_n, void* stream) {
+                             long long sk_cnt_n, const void* bnf, const float* lz_coef, int lz_relu, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   if ((long long)N * H * W * Cin >= (1LL << 29)) return -103;   // 32-bit in-replica byte offsets
   const long long M = (long long)N * Ho * Wo;
@@ -1980,6 +2258,14 @@ DBA_EXPORT int dba_xconv_fwd(const float* x, long long x_gstride, const float* w
   if (bnpart && (bias || res || relu)) return -106;   // statistics of the raw conv output only
   const bool pairs = in_sexp || out_sexp || res_sexp;
   if (pairs && (!amax_x || !wp || vec < 4 || (Cout & 3) || bnpart || (out_sexp && !bound))) return -107;
+  if (bnf) {
+    a.bf = *(const BnFuse*)bnf;
+    if (a.bf.mode != 1 || bias || res || relu || pairs || bnpart || (Cout & 3) || a.bf.C != Cout) return -108;
+  }
+  if (lz_coef) {
+    if (!amax_x || wp || pairs || vec < 4 || Cin > 512) return -108;
+    a.lz_coef = lz_coef; a.lz_relu = lz_relu;
+  }
   if (stride == 1) {
     const int rc = xhalo_try(a, G, KH, KW, st);
     if (rc != -100) return rc;
@@ -2007,6 +2293,11 @@ DBA_EXPORT int dba_xconv_fwd(const float* x, long long x_gstride, const float* w
     const dim3 grid((unsigned)std::max(1LL, std::min(1024LL, (per + 255) / 256)), G);
     hipLaunchKernelGGL(xsplitk_reduce_kernel, grid, dim3(256), 0, st, (const float*)ws, s, b.zstride, per, nvalid, N,
                        Ho * Wo, Cout, bias, b_sstride, wsel, res, relu, out, amax_out, amax_out_ld);
+    if (a.bf.mode) {   // the statistics from the reduced output, same records (bnfuse.hpp)
+      const int rc = (int)hipGetLastError();
+      if (rc != 0) return rc;
+      return bnx_rows_go(a.bf, out, nullptr, out_gstride, nvalid, G, N, Ho * Wo, nullptr, 0.f, st);
+    }
     DBA_LAUNCH_CHECK();
   }
   return xconv_dispatch(a, M, G, 1, vec, st);
@@ -2019,7 +2310,7 @@ DBA_EXPORT int dba_xconv_dgrad(const float* dy, long long dy_gstride, const floa
                                const int* nvalid, int G, int N, int H, int W, int Cin, int Ho, int Wo, int Cout,
                                int KH, int KW, int stride, int pad, const int* amax_dy, int amax_dy_ld,
                                const int* amax_w, int amax_w_ld, const uint16_t* wp, long long wp_sstride, float* ws,
-                               long long ws_floats, int* sk_cnt, long long sk_cnt_n, void* stream) {
+                               long long ws_floats, int* sk_cnt, long long sk_cnt_n, const void* bnf, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   if ((long long)N * Ho * Wo * Cout >= (1LL << 29)) return -103;   // 32-bit in-replica byte offsets
   const ClassGeom cg = dgrad_classes(H, W, Cin, Cout, KH, KW, stride, pad);
@@ -2032,6 +2323,10 @@ DBA_EXPORT int dba_xconv_dgrad(const float* dy, long long dy_gstride, const floa
   a.amax_src = amax_dy; a.amax_w = amax_w;
   a.amax_src_ld = amax_dy_ld; a.amax_w_ld = amax_w_ld;
   a.wp = wp; a.wp_sstride = wp_sstride;
+  if (bnf) {   // the backward BN mask + reduce of the gradient (stride-1 data gradients: one class)
+    a.bf = *(const BnFuse*)bnf;
+    if (a.bf.mode != 2 || stride != 1 || (Cin & 3) || a.bf.C != Cin) return -108;
+  }
   long long Mmax = 0;
   for (int i = 0; i < cg.n; ++i) {
     a.cls[i] = cg.c[i];
@@ -2062,6 +2357,11 @@ DBA_EXPORT int dba_xconv_dgrad(const float* dy, long long dy_gstride, const floa
       const dim3 grid((unsigned)std::max(1LL, std::min(1024LL, (per + 255) / 256)), G);
       hipLaunchKernelGGL(xsplitk_reduce_kernel, grid, dim3(256), 0, st, (const float*)ws, s, b.zstride, per, nvalid,
                          N, H * W, Cin, nullptr, 0LL, wsel, accum, 0, dx, (int*)nullptr, 0);
+      if (a.bf.mode) {   // mask + reduce the reduced gradient in place, same records (bnfuse.hpp)
+        const int rc = (int)hipGetLastError();
+        if (rc != 0) return rc;
+        return bnx_rows_go(a.bf, dx, dx, dx_gstride, nvalid, G, N, H * W, nullptr, 0.f, st);
+      }
       DBA_LAUNCH_CHECK();
     }
   }
@@ -2111,8 +2411,11 @@ DBA_EXPORT int dba_xwgrad(const float* dy, long long dy_gstride, const float* x,
                           long long dw_gstride, const int* nvalid, int G, int N, int H, int W, int Cin, int Ho,
                           int Wo, int Cout, int KH, int KW, int stride, int pad, const int* amax_dy,
                           int amax_dy_ld, const int* amax_x, int amax_x_ld, float* ws, long long ws_floats, int defer,
+                          const float* dy_y, const float* dy_coef, float* dy_out, const float* x_coef, int x_relu,
                           void* stream) {
   hipStream_t st = (hipStream_t)stream;
+  if ((dy_y || x_coef) && !amax_dy) return -108;   // lazy BN operands: fp16-pair launches only
+  if (dy_y && !dy_coef) return -108;
   int mchunk = 0;
   const long long need = dba_xwgrad_ws_floats(G, N, Ho, Wo, Cin, Cout, KH, KW, &mchunk);
   if (need > 0 && (ws == nullptr || ws_floats < need)) return -101;
@@ -2125,6 +2428,7 @@ DBA_EXPORT int dba_xwgrad(const float* dy, long long dy_gstride, const float* x,
   a.mchunk = mchunk;
   a.amax_dy = amax_dy; a.amax_x = amax_x;
   a.amax_dy_ld = amax_dy_ld; a.amax_x_ld = amax_x_ld;
+  a.dy_y = dy_y; a.dy_coef = dy_coef; a.dy_out = dy_out; a.x_coef = x_coef; a.x_relu = x_relu;
   a.dHoWo = FDiv{Ho * Wo, 1.0f / (float)(Ho * Wo)};
   a.dWo = FDiv{Wo, 1.0f / (float)Wo};
   a.tiles_k = ceil_div(a.K, 128);
@@ -2140,20 +2444,26 @@ DBA_EXPORT int dba_xwgrad(const float* dy, long long dy_gstride, const float* x,
   int bno = Cout <= 32 ? 32 : Cout <= 64 ? 64 : 128;
   if (bno == 128 && (long long)ceil_div(Cout, 128) * a.tiles_k * G * Z < bno64_below) bno = 64;
   const dim3 grid((unsigned)(ceil_div(Cout, bno) * a.tiles_k), G, Z);
-#define XW_GO(BNO_, WN__, WK__, P_, V_, H_) \
-  hipLaunchKernelGGL((xwgrad_kernel<BNO_, 128, WN__, WK__, P_, V_, H_>), grid, dim3(256), 0, st, a)
-#define XW_P(P_, V_, H_)                                  \
-  do {                                                    \
-    if (bno == 32) XW_GO(32, 1, 4, P_, V_, H_);           \
-    else if (bno == 64) XW_GO(64, 2, 2, P_, V_, H_);      \
-    else XW_GO(128, 2, 2, P_, V_, H_);                    \
+#define XW_GO(BNO_, WN__, WK__, P_, V_, H_, D_, X_) \
+  hipLaunchKernelGGL((xwgrad_kernel<BNO_, 128, WN__, WK__, P_, V_, H_, D_, X_>), grid, dim3(256), 0, st, a)
+#define XW_P(P_, V_, H_, D_, X_)                                  \
+  do {                                                            \
+    if (bno == 32) XW_GO(32, 1, 4, P_, V_, H_, D_, X_);           \
+    else if (bno == 64) XW_GO(64, 2, 2, P_, V_, H_, D_, X_);      \
+    else XW_GO(128, 2, 2, P_, V_, H_, D_, X_);                    \
   } while (0)
-  if (amax_dy) {
-    if (v4) XW_P(2, 4, true); else XW_P(2, 1, true);
+  if (amax_dy && dy_y && x_coef) {
+    if (v4) XW_P(2, 4, true, true, true); else XW_P(2, 1, true, true, true);
+  } else if (amax_dy && dy_y) {
+    if (v4) XW_P(2, 4, true, true, false); else XW_P(2, 1, true, true, false);
+  } else if (amax_dy && x_coef) {
+    if (v4) XW_P(2, 4, true, false, true); else XW_P(2, 1, true, false, true);
+  } else if (amax_dy) {
+    if (v4) XW_P(2, 4, true, false, false); else XW_P(2, 1, true, false, false);
   } else if (planes() == 2) {
-    if (v4) XW_P(2, 4, false); else XW_P(2, 1, false);
+    if (v4) XW_P(2, 4, false, false, false); else XW_P(2, 1, false, false, false);
   } else {
-    if (v4) XW_P(3, 4, false); else XW_P(3, 1, false);
+    if (v4) XW_P(3, 4, false, false, false); else XW_P(3, 1, false, false, false);
   }
 #undef XW_P
 #undef XW_GO
@@ -2234,4 +2544,29 @@ DBA_EXPORT int dba_xwgrad_reduce_batch(const void* desc, int n, int Gmax, long l
     if (rc != 0) return rc;
   }
   return 0;
+}
+
+// the fused-BN standalone pass (bnx_rows_kernel) over a materialised tensor; bnf: a BnFuse in
+// host memory (passed by value: graph-capture safe)
+DBA_EXPORT int dba_bnx_rows(const void* bnf, const float* src, float* dst, long long gstride, const int* nvalid, int G,
+                            int N, int HW, const float* pool, float pool_scale, void* stream) {
+  const BnFuse f = *(const BnFuse*)bnf;
+  if (f.mode < 1 || f.mode > 2 || (f.mode == 2 && (!dst || !f.ya))) return -108;
+  return bnx_rows_go(f, src, dst, gstride, nvalid, G, N, HW, pool, pool_scale, (hipStream_t)stream);
+}
+
+// sizeof(BnFuse) (the Python ctypes mirror checks its layout against it)
+DBA_EXPORT int dba_bnfuse_size() { return (int)sizeof(BnFuse); }
+
+DBA_EXPORT int dba_bnx_apply(const float* ya, const float* ca, const float* res, const float* yb, const float* cb,
+                             int relu_b, int relu, float* out, long long gstride, const int* nvalid, int G, int N, int HW, int C,
+                             int* amax, int amax_ld, void* stream) {
+  if (C & 3) return -102;
+  const long long per = (long long)N * HW * (C / 4);
+  const long long cap = std::max(1LL, 8192LL / std::max(1, G));
+  const dim3 grid((unsigned)std::max(1LL, std::min(cap, (per + 255) / 256)), G);
+  hipLaunchKernelGGL(bnx_apply_kernel, grid, dim3(256), 0, (hipStream_t)stream, ya, ca, res, yb, cb, relu_b, relu, out,
+                     gstride,
+                     nvalid, N, HW, C, amax, amax_ld);
+  DBA_LAUNCH_CHECK();
 }

@@ -6,6 +6,12 @@ One forward definition per architecture serves three modes:
   records a backward closure on a :class:`Tape`; ``Tape.backward`` writes parameter
   gradients straight into the flat ``[G, P]`` gradient buffer (no autograd, no per-tensor
   ``.grad``), so the whole step is a fixed launch sequence that a HIP graph can capture.
+  Training BN is fused into the convs (``ops.bnstate``, ``csrc/kernels/bnfuse.hpp``): a conv
+  reduces its output's statistics, a BN output consumed only by convs stays lazy
+  (:class:`~dba_mod_amd.ops.bnstate.LazyBN`), a block output is stored by one apply pass; in
+  the backward pass the kernel producing a BN output's complete gradient finishes it (ReLU mask +
+  BN reductions, a :class:`~dba_mod_amd.ops.bnstate.Fin`) and the weight gradient below applies
+  the BN input gradient on the fly.
 * ``eval`` — BatchNorm folded into the conv weights/bias (:func:`fold_bank`), so every conv
   is one kernel with a fused bias + residual + ReLU epilogue.
 
@@ -21,6 +27,7 @@ from typing import Callable, Dict, List, Optional, Tuple
 import torch
 
 from .. import ops
+from ..ops import bnstate as bs
 from .mirror import CIFAR_RESNETS
 from .spec import ModelSpec
 
@@ -36,6 +43,8 @@ class Tape:
         self.nodes: List[Tuple[Tuple[Tensor, ...], Tuple[Optional[Tensor], ...], Callable]] = []
         self._produced: set = set()
         self._grads: Optional[Dict[int, Tensor]] = None
+        self._uses: Dict[int, int] = {}
+        self.nvalid: Optional[Tensor] = None
         self.on_begin: Optional[Callable[[], None]] = None
         self.on_end: Optional[Callable[[], None]] = None
 
@@ -43,6 +52,20 @@ class Tape:
         self.nodes.append((outputs, inputs, bwd))
         for o in outputs:
             self._produced.add(id(o))
+        for i in inputs:
+            if i is not None:
+                self._uses[id(i)] = self._uses.get(id(i), 0) + 1
+
+    def is_last(self, t) -> bool:
+        """During backward: the node being run is the last one to deliver ``t``'s gradient."""
+        return self._uses.get(id(t), 0) == 1
+
+    @staticmethod
+    def finish_spec(t) -> Optional[bs.Finish]:
+        """How ``t``'s gradient is finished if ``t`` is a training-BN output (else None)."""
+        if isinstance(t, bs.LazyBN):
+            return bs.Finish(ya=t.y, sa=t.stat, lazy=t.relu)
+        return getattr(t, "_dba_finish", None)
 
     def needs_grad(self, t: Optional[Tensor]) -> bool:
         return t is not None and id(t) in self._produced
@@ -61,33 +84,34 @@ class Tape:
         for outputs, inputs, bwd in reversed(self.nodes):
             gouts = [grads.pop(id(o), None) for o in outputs]
             if all(g is None for g in gouts):
+                for i in inputs:
+                    if i is not None:
+                        self._uses[id(i)] -= 1
                 continue
+            # a BN output whose gradient arrived unfinished (its last producer could not fuse the
+            # mask + reduction: a stride-s data gradient, a max-pool, an add): one standalone pass
+            gouts = [ops.bn_finish(g, self.finish_spec(o), self.nvalid)
+                     if isinstance(g, Tensor) and self.finish_spec(o) is not None else g
+                     for o, g in zip(outputs, gouts)]
             gins = bwd(*gouts)
             for inp, gi in zip(inputs, gins):
+                if inp is not None:
+                    self._uses[id(inp)] -= 1
                 if gi is None or inp is None or not self.needs_grad(inp):
                     continue
                 k = id(inp)
-                grads[k] = grads[k] + gi if k in grads else gi
+                if k in grads:
+                    if not (isinstance(grads[k], Tensor) and isinstance(gi, Tensor)):
+                        raise RuntimeError("a finished BN gradient cannot take further contributions")
+                    grads[k] = grads[k] + gi
+                else:
+                    grads[k] = gi
         self.nodes.clear()
         self._produced.clear()
+        self._uses.clear()
         self._grads = None
         if self.on_end is not None:
             self.on_end()
-
-
-_WGRAD_STREAMS: Dict[int, "torch.cuda.Stream"] = {}
-
-
-def _wgrad_stream(device: torch.device) -> Optional["torch.cuda.Stream"]:
-    """The per-device side stream weight gradients run on (``DBA_WGRAD_STREAM=1``; default off:
-    launch on the caller's stream).  Same priority as the training stream."""
-    if os.environ.get("DBA_WGRAD_STREAM", "0") == "0":
-        return None
-    key = device.index if device.index is not None else torch.cuda.current_device()
-    if key not in _WGRAD_STREAMS:
-        pri = int(os.environ.get("DBA_TRAIN_STREAM_PRIORITY", "-1"))
-        _WGRAD_STREAMS[key] = torch.cuda.Stream(device, priority=pri)
-    return _WGRAD_STREAMS[key]
 
 
 class Ctx:
@@ -114,15 +138,10 @@ class Ctx:
         # weight-gradient slab reductions of the whole backward pass, run as one launch when
         # it ends (ops.wgrad_flush)
         self._wdefer: List[tuple] = []
-        # weight gradients on a side stream (GPU training): they feed only the end-of-pass slab
-        # reduction and the SGD, so they run beside the data-gradient / BN chain that bounds a
-        # latency-bound step; joined before the reduction (_end_backward)
-        self._side = _wgrad_stream(state.device) if (train and state is not None and state.is_cuda) else None
-        self._side_used = False
-        self._side_keep: List[Tensor] = []
         if self.tape is not None:
             self.tape.on_begin = self._prepare_dgrad
             self.tape.on_end = self._end_backward
+            self.tape.nvalid = nvalid
         self.dropout_seed = dropout_seed
         self._drop_ctr = 0
         self.act_dtype = act_dtype
@@ -154,24 +173,8 @@ class Ctx:
         return len(self._dgrad_items) - 1
 
     def _end_backward(self) -> None:
-        if self._side_used:
-            torch.cuda.current_stream(self._side.device).wait_stream(self._side)
-            self._side_used = False
         if self._wdefer:
             ops.backend_for(self.state).wgrad_flush(self._wdefer)
-        self._side_keep.clear()     # the operands the side stream read (alive until the join)
-
-    def _wgrad(self, dy: Tensor, x: Tensor, fn: Callable[[], None]) -> None:
-        """Run the weight-gradient launch ``fn`` (reading ``dy`` and ``x``) on the side stream."""
-        if self._side is None:
-            fn()
-            return
-        ops.wgrad_prepare(dy, x, self.nvalid)      # operand maxima on the main stream
-        self._side.wait_stream(torch.cuda.current_stream(self._side.device))
-        with torch.cuda.stream(self._side):
-            fn()
-        self._side_used = True
-        self._side_keep.extend((dy, x))
 
     def _prepare_dgrad(self) -> None:
         if self._dgrad_items:
@@ -219,8 +222,7 @@ class Ctx:
                                  self.g(bn + ".weight"), self.g(bn + ".bias"),
                                  want_dres=residual is not None)
             dy, dres = r if residual is not None else (r, None)
-            self._wgrad(dy, x, lambda: ops.conv2d_wgrad(dy, x, stride, pad, kh, kw, self.g(conv), nvalid=self.nvalid,
-                                                        defer=self._wdefer))
+            ops.conv2d_wgrad(dy, x, stride, pad, kh, kw, self.g(conv), nvalid=self.nvalid, defer=self._wdefer)
             dx = None
             if need_dx:
                 # the other consumer of x (shortcut branch) already delivered its gradient
@@ -230,6 +232,60 @@ class Ctx:
             return dx, dres
 
         self.tape.record((out,), (x, residual), bwd)
+        return out
+
+    # ---------------------------------------------------------- fused training BN
+    def _bnp(self, bn: str) -> bs.BnParams:
+        return bs.BnParams(self.m(bn + ".weight"), self.m(bn + ".bias"), self.m(bn + ".running_mean"),
+                           self.m(bn + ".running_var"), self.g(bn + ".weight"), self.g(bn + ".bias"),
+                           BN_MOMENTUM, BN_EPS)
+
+    def bn_conv(self, x, conv: str, bn: str, stride: int, pad: int, relu: bool):
+        """Training: conv -> BN (-> ReLU) with the BN output left lazy (``LazyBN``: its
+        consumers apply it); ``x`` may itself be lazy.  Evaluation: the BN-folded conv."""
+        if not self.train:
+            return self.conv_bn(x, conv, bn, stride, pad, relu)
+        w = self.w(conv)
+        y, st = ops.conv_bn_stats(x, w, self.wsel, stride, pad, self.nvalid, self._bnp(bn), relu)
+        a = bs.LazyBN(y, st, relu)
+        in_hw = (x.shape[2], x.shape[3])
+        kh, kw = w.shape[2], w.shape[3]
+        need_dx = self.tape.needs_grad(x)
+        k = self._want_dgrad(w, stride, pad, in_hw, x.shape[0]) if need_dx else -1
+
+        def bwd(ga: bs.Fin):
+            # the weight gradient stages dy = A d + B y + K and stores it for the data gradient
+            dy = ops.conv2d_wgrad(bs.LazyGrad(ga.for_stat(st).d, y, st), x, stride, pad, kh, kw, self.g(conv),
+                                  nvalid=self.nvalid, defer=self._wdefer)
+            if not need_dx:
+                return (None,)
+            acc = self.tape.pop_grad(x)
+            fin = self.tape.finish_spec(x) if self.tape.is_last(x) else None
+            return (ops.conv2d_dgrad(dy, w, self.wsel, stride, pad, in_hw, nvalid=self.nvalid, accum=acc,
+                                     wt=self._wt.get(k), finish=fin),)
+
+        self.tape.record((a,), (x,), bwd)
+        return a
+
+    def bn_out(self, a, residual=None, relu: bool = True) -> Tensor:
+        """Training: the stored output relu?(BN(a) + residual) of a block (one pass); ``a`` a
+        lazy BN output without ReLU, ``residual`` a tensor, a lazy BN output or None.  Its
+        gradient is finished (ReLU mask, the sums of a's BN and of a residual BN branch) by
+        whoever produces it last."""
+        out = ops.bn_apply(a, residual, relu, self.nvalid)
+        branch = isinstance(residual, bs.LazyBN) and not residual.relu
+        out._dba_finish = bs.Finish(ya=a.y, sa=a.stat, mask_out=out if relu else None,
+                                    yb=residual.y if branch else None, sb=residual.stat if branch else None)
+
+        def bwd(gout: bs.Fin):
+            gr = None
+            if branch:
+                gr = gout.for_stat(residual.stat)
+            elif residual is not None:
+                gr = gout.d          # a plain contribution to the residual's gradient
+            return gout.for_stat(a.stat), gr
+
+        self.tape.record((out,), (a, residual), bwd)
         return out
 
     def conv(self, x: Tensor, name: str, stride: int, pad: int, bias: Optional[str], relu: bool) -> Tensor:
@@ -248,9 +304,8 @@ class Ctx:
 
         def bwd(dout: Tensor):
             d = ops.relu_mask_bwd(dout, y) if relu else dout
-            self._wgrad(d, x, lambda: ops.conv2d_wgrad(d, x, stride, pad, kh, kw, self.g(name),
-                                                       self.g(bias) if bias is not None else None, nvalid=self.nvalid,
-                                                       defer=self._wdefer))
+            ops.conv2d_wgrad(d, x, stride, pad, kh, kw, self.g(name), self.g(bias) if bias is not None else None,
+                             nvalid=self.nvalid, defer=self._wdefer)
             return (ops.conv2d_dgrad(d, w, self.wsel, stride, pad, in_hw, nvalid=self.nvalid, wt=self._wt.get(k))
                     if need_dx else None,)
 
@@ -284,9 +339,8 @@ class Ctx:
 
         def bwd(dout: Tensor):
             d = ops.relu_mask_bwd(dout, y) if relu else dout
-            self._wgrad(d, x4, lambda: ops.conv2d_wgrad(d, x4, 1, 0, 1, 1,
-                                                        gv.reshape(gv.shape[0], gv.shape[1], 1, 1, gv.shape[2]),
-                                                        self.g(bias), nvalid=self.nvalid, defer=self._wdefer))
+            ops.conv2d_wgrad(d, x4, 1, 0, 1, 1, gv.reshape(gv.shape[0], gv.shape[1], 1, 1, gv.shape[2]),
+                             self.g(bias), nvalid=self.nvalid, defer=self._wdefer)
             return (ops.conv2d_dgrad(d, w, self.wsel, 1, 0, (1, 1), nvalid=self.nvalid, wt=self._wt.get(k))
                     if need_dx else None,)
 
@@ -311,7 +365,14 @@ class Ctx:
         y = ops.avgpool_global(x)
         if self.train:
             hw = (x.shape[2], x.shape[3])
-            self.tape.record((y,), (x,), lambda d: (ops.avgpool_global_bwd(d, hw),))
+
+            def bwd(d):
+                fin = self.tape.finish_spec(x) if self.tape.is_last(x) else None
+                if fin is not None:   # the pool's gradient finished in the same pass
+                    return (ops.bn_finish(None, fin, self.nvalid, pool=d, hw=hw),)
+                return (ops.avgpool_global_bwd(d, hw),)
+
+            self.tape.record((y,), (x,), bwd)
         return y
 
     def dropout(self, x: Tensor, p: float) -> Tensor:
@@ -325,30 +386,39 @@ class Ctx:
 
 
 # ------------------------------------------------------------------- architectures
+def _block_out(ctx: Ctx, a, conv: str, bn: str, pad: int, residual, to_conv: bool):
+    """relu(BN(conv(a)) + residual): evaluation — one BN-folded conv with a fused residual /
+    ReLU epilogue; training — the conv (statistics fused) and one apply pass."""
+    if not ctx.train:
+        return ctx.conv_bn(a, conv, bn, 1, pad, relu=True, residual=residual, to_conv=to_conv)
+    return ctx.bn_out(ctx.bn_conv(a, conv, bn, 1, pad, relu=False), residual, relu=True)
+
+
 def _resnet_cifar(ctx: Ctx, x: Tensor) -> Tensor:
-    """Any member of the half-width CIFAR family (``mirror.CIFAR_RESNETS``)."""
+    """Any member of the half-width CIFAR family (``mirror.CIFAR_RESNETS``).  Training: the
+    stem's output and every block's mid activations stay lazy (consumed by convs and residual
+    adds); block outputs are stored."""
     bottleneck, blocks = CIFAR_RESNETS[ctx.spec.arch]
     exp = 4 if bottleneck else 1
-    out = ctx.conv_bn(x, "conv1.weight", "bn1", 1, 1, relu=True)
+    out = ctx.bn_conv(x, "conv1.weight", "bn1", 1, 1, relu=True)
     cin = 32
     for li, w in enumerate((32, 64, 128, 256)):
         for bi in range(blocks[li]):
             stride = 2 if (li > 0 and bi == 0) else 1
             pre = f"layer{li + 1}.{bi}."
             if bottleneck:
-                a = ctx.conv_bn(out, pre + "conv1.weight", pre + "bn1", 1, 0, relu=True)
-                a = ctx.conv_bn(a, pre + "conv2.weight", pre + "bn2", stride, 1, relu=True)
+                a = ctx.bn_conv(out, pre + "conv1.weight", pre + "bn1", 1, 0, relu=True)
+                a = ctx.bn_conv(a, pre + "conv2.weight", pre + "bn2", stride, 1, relu=True)
                 last, p = "3", 0
             else:
-                a = ctx.conv_bn(out, pre + "conv1.weight", pre + "bn1", stride, 1, relu=True)
+                a = ctx.bn_conv(out, pre + "conv1.weight", pre + "bn1", stride, 1, relu=True)
                 last, p = "2", 1
             if stride != 1 or cin != w * exp:
-                sc = ctx.conv_bn(out, pre + "shortcut.0.weight", pre + "shortcut.1", stride, 0, relu=False)
+                sc = ctx.bn_conv(out, pre + "shortcut.0.weight", pre + "shortcut.1", stride, 0, relu=False)
             else:
                 sc = out
             final = li == 3 and bi == blocks[li] - 1
-            out = ctx.conv_bn(a, pre + f"conv{last}.weight", pre + f"bn{last}", 1, p, relu=True, residual=sc,
-                              to_conv=not final)
+            out = _block_out(ctx, a, pre + f"conv{last}.weight", pre + f"bn{last}", p, sc, to_conv=not final)
             cin = w * exp
     out = ctx.gap(out)
     G, N = out.shape[:2]
@@ -356,7 +426,10 @@ def _resnet_cifar(ctx: Ctx, x: Tensor) -> Tensor:
 
 
 def _resnet_tiny(ctx: Ctx, x: Tensor) -> Tensor:
-    out = ctx.conv_bn(x, "conv1.weight", "bn1", 2, 3, relu=True, to_conv=False)   # -> max-pool
+    if ctx.train:   # the stem's output feeds the max-pool: stored
+        out = ctx.bn_out(ctx.bn_conv(x, "conv1.weight", "bn1", 2, 3, relu=False), None, relu=True)
+    else:
+        out = ctx.conv_bn(x, "conv1.weight", "bn1", 2, 3, relu=True, to_conv=False)   # -> max-pool
     out = ctx.maxpool(out, 3, 2, 1)
     cin = 64
     for li, w in enumerate((64, 128, 256, 512)):
@@ -364,12 +437,11 @@ def _resnet_tiny(ctx: Ctx, x: Tensor) -> Tensor:
             stride = 2 if (li > 0 and bi == 0) else 1
             pre = f"layer{li + 1}.{bi}."
             if stride != 1 or cin != w:
-                sc = ctx.conv_bn(out, pre + "downsample.0.weight", pre + "downsample.1", stride, 0, relu=False)
+                sc = ctx.bn_conv(out, pre + "downsample.0.weight", pre + "downsample.1", stride, 0, relu=False)
             else:
                 sc = out
-            a = ctx.conv_bn(out, pre + "conv1.weight", pre + "bn1", stride, 1, relu=True)
-            out = ctx.conv_bn(a, pre + "conv2.weight", pre + "bn2", 1, 1, relu=True, residual=sc,
-                              to_conv=not (li == 3 and bi == 1))
+            a = ctx.bn_conv(out, pre + "conv1.weight", pre + "bn1", stride, 1, relu=True)
+            out = _block_out(ctx, a, pre + "conv2.weight", pre + "bn2", 1, sc, to_conv=not (li == 3 and bi == 1))
             cin = w
     out = ctx.gap(out)
     G, N = out.shape[:2]

@@ -44,6 +44,27 @@ class BranchReplay:
 
     def wrap(self, mod):
         o_bn, o_conv, o_mp = mod.bn_train, mod.conv2d, mod.maxpool2d
+        o_cbs, o_apply = mod.conv_bn_stats, mod.bn_apply
+
+        def conv_bn_stats(x, w, wsel, stride, pad, nvalid, p, relu):
+            # the fused training BN (ops.bnstate): a lazy BN+ReLU output's decisions are taken
+            # where its value and its backward mask are formed, from stat.relu_mask
+            y, st = o_cbs(x, w, wsel, stride, pad, nvalid, p, relu)
+            if relu:
+                C = y.shape[-1]
+                sh = (y.shape[0],) + (1,) * (y.dim() - 2) + (C,)
+                pre = y * st.coef[:, 2].reshape(sh).to(y.dtype) + st.coef[:, 3].reshape(sh).to(y.dtype)
+                if not self.replay:
+                    self.rec.append((pre > 0).cpu())
+                else:
+                    st.relu_mask = self._decide(pre)
+            return y, st
+
+        def bn_apply(a, residual, relu, nvalid=None):
+            if not (relu and self.replay):
+                out = o_apply(a, residual, relu, nvalid)
+                return self._record(out) if relu else out
+            return self._relu(o_apply(a, residual, False, nvalid))
 
         def bn_train(y, gamma, beta, rmean, rvar, nvalid, momentum, eps, relu, residual):
             if not (relu and self.replay):
@@ -66,7 +87,8 @@ class BranchReplay:
         def maxpool2d(x, kk, st, p):
             y, ind = o_mp(x, kk, st, p)
             return self._pool(x, y, ind)
-        return {"bn_train": bn_train, "conv2d": conv2d, "maxpool2d": maxpool2d}
+        return {"bn_train": bn_train, "conv2d": conv2d, "maxpool2d": maxpool2d, "conv_bn_stats": conv_bn_stats,
+                "bn_apply": bn_apply}
 
     def _valid(self, t):
         v = torch.zeros(t.shape[:2], dtype=torch.bool)
@@ -89,6 +111,20 @@ class BranchReplay:
             vals = hip.decode_pairs(out)
         self.rec.append((vals > 0).cpu())
         return out
+
+    def _decide(self, pre):
+        """The ReLU decisions of ``pre``: its own, with the recorded one taken at near-ties."""
+        m = self.rec[self.i].to(pre.device)
+        self.i += 1
+        keep = self._valid(pre).expand_as(pre)
+        pos = pre > 0
+        tie = pre.abs() <= self.tol * self._rms(pre)
+        differ = keep & (m != pos)
+        take = differ & tie
+        self.flips += int(take.sum())
+        self.hard += int((differ & ~tie).sum())
+        self.elements += int(keep.sum())
+        return torch.where(take, m, pos)
 
     def _relu(self, pre):
         m = self.rec[self.i].to(pre.device)

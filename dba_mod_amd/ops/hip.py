@@ -13,6 +13,7 @@ from typing import Optional, Sequence, Tuple
 
 import torch
 
+from . import bnstate as bs
 from . import build
 
 Tensor = torch.Tensor
@@ -81,19 +82,23 @@ _SIGS = {
     "dba_bn_bwd_fuse_set": [_I],
     "dba_xconv_ws_floats": [_I] * 8,
     "dba_xconv_fwd": [_P, _LL, _P, _LL, _P, _P, _LL, _P, _P, _LL, _P] + [_I] * 13 + [_P, _I] * 3 + [_P, _LL] * 2
-    + [_P, _P, _P, _P, _P, _I, _P, _P, _LL, _P],
+    + [_P, _P, _P, _P, _P, _I, _P, _P, _LL, _P, _P, _I, _P],
     "dba_xconv_sk_ints": [_I] * 8,
     "dba_row_bound": [_P, _LL, _I, _I, _P, _LL, _I, _P, _P],
     "dba_bn_finalize_part": [_P, _I, _P, _I, _I, _I, _I, _P, _P, _LL, _F, _F, _P, _P, _P],
-    "dba_xconv_dgrad": [_P, _LL, _P, _LL, _P, _P, _P, _LL, _P] + [_I] * 12 + [_P, _I] * 2 + [_P, _LL] * 3 + [_P],
+    "dba_xconv_dgrad": [_P, _LL, _P, _LL, _P, _P, _P, _LL, _P] + [_I] * 12 + [_P, _I] * 2 + [_P, _LL] * 3 + [_P, _P],
     "dba_xsplit_w": [_P, _LL, _LL, _I, _P, _I, _P, _P],
     "dba_amax": [_P, _LL, _LL, _P, _LL, _I, _P, _I, _P],
     "dba_xtranspose": [_P, _I, _I, _LL, _P, _P],
     "dba_xwgrad_ws_floats": [_I] * 8 + [_P],
-    "dba_xwgrad": [_P, _LL, _P, _LL, _P, _LL, _P] + [_I] * 12 + [_P, _I] * 2 + [_P, _LL, _I, _P],
+    "dba_xwgrad": [_P, _LL, _P, _LL, _P, _LL, _P] + [_I] * 12 + [_P, _I] * 2 + [_P, _LL, _I] + [_P] * 4 + [_I, _P],
+    # fused training BN (csrc/kernels/bnfuse.hpp)
+    "dba_bnx_rows": [_P, _P, _P, _LL, _P, _I, _I, _I, _P, _F, _P],
+    "dba_bnx_apply": [_P, _P, _P, _P, _P, _I, _I, _P, _LL, _P, _I, _I, _I, _I, _P, _I, _P],
+    "dba_bnfuse_size": [],
     "dba_xwgrad_reduce_batch": [_P, _I, _I, _LL, _P],
     # image stems in exact fp32 (csrc/kernels/stem.hip)
-    "dba_xstem_fwd": [_P, _LL, _P, _LL, _P, _P, _LL, _P, _P, _LL, _P] + [_I] * 13 + [_P, _I, _P, _P, _I, _P, _P, _P],
+    "dba_xstem_fwd": [_P, _LL, _P, _LL, _P, _P, _LL, _P, _P, _LL, _P] + [_I] * 13 + [_P, _I, _P, _P, _I, _P, _P, _P, _P],
 }
 for _name, _args in _SIGS.items():
     _fn = getattr(_L, _name)
@@ -104,6 +109,23 @@ _L.dba_xconv_ws_floats.restype = ctypes.c_longlong
 _L.dba_xconv_sk_ints.restype = ctypes.c_longlong
 _L.dba_xwgrad_ws_floats.restype = ctypes.c_longlong
 _MODE = int(_L.dba_xgemm_set_planes(0))   # fp32 split mode (0: query only; DBA_F32_PLANES)
+
+
+class _BnFuse(ctypes.Structure):
+    """Mirror of csrc/kernels/bnfuse.hpp ``BnFuse`` (passed by host pointer, copied by value
+    into the kernel arguments at launch: graph-capture safe)."""
+    _fields_ = [("mode", _I), ("C", _I), ("ngrp", _I), ("nsg", _I),
+                ("rec0", _P), ("rec1", _P), ("cnt1", _P), ("cnt2", _P),
+                ("coef_a", _P), ("gamma_a", _P), ("beta_a", _P), ("rm_a", _P), ("rv_a", _P),
+                ("p_gstride", _LL), ("momentum", _F), ("eps", _F), ("relu", _I),
+                ("amax_a", _P), ("amax_ld", _I),
+                ("ya", _P), ("yb", _P), ("y_gstride", _LL),
+                ("coef_b", _P), ("gamma_b", _P), ("amax_b", _P),
+                ("dgamma_a", _P), ("dbeta_a", _P), ("dgamma_b", _P), ("dbeta_b", _P), ("gr_gstride", _LL),
+                ("mask_out", _P), ("mask_lazy", _I)]
+
+
+assert ctypes.sizeof(_BnFuse) == int(_L.dba_bnfuse_size()), "BnFuse layout mismatch (rebuild the kernels)"
 
 
 NOT_HANDLED = -100   # a conv2 entry point declining a shape (odd channel counts)
@@ -353,7 +375,7 @@ _ARENA: list = []
 
 
 @contextlib.contextmanager
-def amax_arena(G: int, device, n: int = 128, counters: int = 0):
+def amax_arena(G: int, device, n: int = 256, counters: int = 0):
     """Slots for the enclosed launches' fp16-pair operand maxima (fp16-pair mode only), and
     ``counters`` zeroed ints for their in-launch split-K combines (:func:`_sk_counters`)."""
     if _MODE != F16_PAIR:
@@ -501,7 +523,8 @@ def _pair_sexp(t):
     return getattr(t, "_dba_pair", None)
 
 
-def _xconv_fwd(x, w, wsel, stride, pad, bias, residual, relu, nvalid, out_dtype, bn_stats=False, out_pairs=False):
+def _xconv_fwd(x, w, wsel, stride, pad, bias, residual, relu, nvalid, out_dtype, bn_stats=False, out_pairs=False,
+               bnf=None, lz=None):
     """Reference-precision conv (fp32 in / fp32 out, split MFMA: xgemm.hip).  ``bn_stats``:
     the output feeds a training BN — the epilogue also folds its per-32-pixel column sums /
     sums of squares (``y._dba_bnpart``), which :func:`bn_train` finalises instead of
@@ -531,8 +554,14 @@ def _xconv_fwd(x, w, wsel, stride, pad, bias, residual, relu, nvalid, out_dtype,
     cnt = _sk_counters(ncnt, x.device)
     ax = aw = ay = None
     if _MODE == F16_PAIR and "fwd" in _H_OPS:
-        ax, aw = _amax_act(x, nvalid), _amax_w(w, ws, Cout * KH * KW * Cin)
-        ay = _amax_out(y)   # the output's max, for its consumers
+        ax = lz[2] if lz is not None else _amax_act(x, nvalid)
+        aw = _amax_w(w, ws, Cout * KH * KW * Cin)
+        if bnf is None:
+            ay = _amax_out(y)   # the output's max, for its consumers
+    elif lz is not None or bnf is not None:
+        raise RuntimeError("fused training BN needs the fp16-pair forward (F16_PAIR, 'fwd' in the H ops)")
+    bnf_p = ctypes.byref(bnf) if bnf is not None else None
+    lz_coef, lz_relu = (lz[0].data_ptr(), int(lz[1])) if lz is not None else (None, 0)
     # fp16-pair activations (xgemm.hip PairAct; evaluation forwards with pre-split weights):
     # the input may arrive split, the output may leave split; every user of such a tensor is a
     # conv of this family (A operand or residual)
@@ -556,7 +585,7 @@ def _xconv_fwd(x, w, wsel, stride, pad, bias, residual, relu, nvalid, out_dtype,
         rc = _call("dba_xstem_fwd", x.data_ptr(), N * H * W * Cin, w.data_ptr(), ws, _ptr(_i32(wsel)), _ptr(bias), bs,
                    _ptr(res), y.data_ptr(), N * Ho * Wo * Cout, _ptr(_i32(nvalid)), G, N, H, W, Cin, Ho, Wo, Cout,
                    KH, KW, stride, pad, int(relu), *_aptr(ay), _ptr(part), *_aptr(ax if out_sexp is not None else None),
-                   _ptr(out_sexp), _ptr(bound if out_sexp is not None else None), _stream())
+                   _ptr(out_sexp), _ptr(bound if out_sexp is not None else None), bnf_p, _stream())
         if rc != NOT_HANDLED:
             if part is not None:
                 y._dba_bnpart = (part, nblk)
@@ -574,7 +603,7 @@ def _xconv_fwd(x, w, wsel, stride, pad, bias, residual, relu, nvalid, out_dtype,
           _ptr(res), y.data_ptr(), N * Ho * Wo * Cout, _ptr(_i32(nvalid)), G, N, H, W, Cin, Ho, Wo, Cout, KH, KW,
           stride, pad, int(relu), *_aptr(ax), *_aptr(aw), *_aptr(ay), *_wplanes(w), _ptr(wsb), n, _ptr(part),
           _ptr(in_sexp), _ptr(out_sexp), _ptr(bound if out_sexp is not None else None), *_aptr(ares), _ptr(res_sexp),
-          _ptr(cnt), 0 if cnt is None else cnt.numel(), _stream())
+          _ptr(cnt), 0 if cnt is None else cnt.numel(), bnf_p, lz_coef, lz_relu, _stream())
     if out_sexp is not None:
         y._dba_pair = out_sexp
     return y
@@ -709,7 +738,7 @@ def prepare_dgrad_weights(ref, items):
     return out
 
 
-def _xconv_dgrad(dy, w, wsel, stride, pad, in_hw, nvalid, out_dtype, accum, wt):
+def _xconv_dgrad(dy, w, wsel, stride, pad, in_hw, nvalid, out_dtype, accum, wt, finish=None):
     if out_dtype not in (None, _F32):
         raise TypeError(f"fp32 dgrad cannot emit {out_dtype} (no silent precision conversion)")
     G, N, Ho, Wo, Cout = dy.shape
@@ -732,17 +761,24 @@ def _xconv_dgrad(dy, w, wsel, stride, pad, in_hw, nvalid, out_dtype, accum, wt):
     if _MODE == F16_PAIR and "dgrad" in _H_OPS:
         a0 = getattr(w, "_dba_amax", None)   # the forward weights' max is the transpose's
         ad, aw = _amax_act(dy, nvalid), (a0 if a0 is not None else _amax(wt, per, per))
+    bnf = _bnf_bwd(finish, G, N * H * W, dx.device) if (finish is not None and stride == 1) else None
     _call("dba_xconv_dgrad", dy.data_ptr(), N * Ho * Wo * Cout, wt.data_ptr(), per, _ptr(_i32(wsel)), _ptr(acc),
           dx.data_ptr(), N * H * W * Cin, _ptr(_i32(nvalid)), G, N, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad,
           *_aptr(ad), *_aptr(aw), *_wplanes(wt), _ptr(wsb), n, _ptr(cnt), 0 if cnt is None else cnt.numel(),
-          _stream())
-    return dx
+          ctypes.byref(bnf) if bnf is not None else None, _stream())
+    if finish is None:
+        return dx
+    if bnf is not None:
+        return bs.Fin(dx, finish.stats())
+    return bn_finish(dx, finish, nvalid)   # stride-s data gradient: the standalone pass
 
 
-def conv2d_dgrad(dy, w, wsel, stride, pad, in_hw, nvalid=None, out_dtype=None, accum=None, wt=None):
+def conv2d_dgrad(dy, w, wsel, stride, pad, in_hw, nvalid=None, out_dtype=None, accum=None, wt=None, finish=None):
     dy = _act(dy, None, "dgrad dy")
     if dy.dtype == _F32:
-        return _xconv_dgrad(dy, w, wsel, stride, pad, in_hw, nvalid, out_dtype, accum, wt)
+        return _xconv_dgrad(dy, w, wsel, stride, pad, in_hw, nvalid, out_dtype, accum, wt, finish)
+    if finish is not None:
+        raise RuntimeError("fused training BN: fp32 family only")
     G, N, Ho, Wo, Cout = dy.shape
     w, ws = _check_w(w)
     slots, _, KH, KW, Cin = w.shape
@@ -805,9 +841,23 @@ def conv2d_dgrad(dy, w, wsel, stride, pad, in_hw, nvalid=None, out_dtype=None, a
 
 def conv2d_wgrad(dy, x, stride, pad, kh, kw, dw, dbias=None, nvalid=None, defer=None):
     """``defer`` (a list, fp32 family): the slab reduction is queued there and run for the whole
-    backward pass by :func:`wgrad_flush` (one launch instead of one per conv)."""
-    dy = _act(dy, None, "wgrad dy")
-    x = _act(x, dy.dtype, "wgrad x")
+    backward pass by :func:`wgrad_flush` (one launch instead of one per conv).  ``dy`` may be a
+    ``LazyGrad`` (a training BN's input gradient, staged from (d, y); its value is stored once
+    and returned for the data gradient) and ``x`` a ``LazyBN`` (a training BN's output, staged
+    from y)."""
+    lg = dy if isinstance(dy, bs.LazyGrad) else None
+    lx = x if isinstance(x, bs.LazyBN) else None
+    dy = _act(lg.d if lg is not None else dy, None, "wgrad dy")
+    x = _act(lx.y if lx is not None else x, dy.dtype, "wgrad x")
+    dy_out = None
+    if lg is not None or lx is not None:
+        if dy.dtype != _F32 or _MODE != F16_PAIR or "wgrad" not in _H_OPS or dbias is not None:
+            raise RuntimeError("fused training BN: fp32 family, fp16-pair weight gradient, no bias")
+        if lg is not None:
+            y_ = _act(lg.y, _F32, "wgrad BN input")
+            assert y_.shape == dy.shape and y_.stride(0) == dy.stride(0)
+            dy_out = torch.empty_like(dy)
+            dy_out._dba_amax = lg.stat.dbound
     G, N, Ho, Wo, Cout = dy.shape
     _, _, H, W, Cin = x.shape
     assert dw.dtype == torch.float32 and _inner_contig(dw)
@@ -818,10 +868,13 @@ def conv2d_wgrad(dy, x, stride, pad, kh, kw, dw, dbias=None, nvalid=None, defer=
         nv = _i32(nvalid)
         ad = ax = None
         if _MODE == F16_PAIR and "wgrad" in _H_OPS:
-            ad, ax = _amax_act(dy, nvalid), _amax_act(x, nvalid)
+            ad = lg.stat.dbound if lg is not None else _amax_act(dy, nvalid)
+            ax = lx.stat.bound if lx is not None else _amax_act(x, nvalid)
         _call("dba_xwgrad", dy.data_ptr(), N * Ho * Wo * Cout, x.data_ptr(), N * H * W * Cin, dw.data_ptr(),
               dw.stride(0), _ptr(nv), G, N, H, W, Cin, Ho, Wo, Cout, kh, kw, stride, pad, *_aptr(ad), *_aptr(ax),
-              _ptr(wsb), n, int(defer is not None and n > 0), _stream())
+              _ptr(wsb), n, int(defer is not None and n > 0),
+              _ptr(lg.y) if lg is not None else None, _ptr(lg.stat.coef) if lg is not None else None, _ptr(dy_out),
+              _ptr(lx.stat.coef) if lx is not None else None, int(lx.relu) if lx is not None else 0, _stream())
         if defer is not None and n > 0:
             per = Cout * kh * kw * Cin
             # (keeps the slab workspace and nvalid alive until the flush)
@@ -831,7 +884,7 @@ def conv2d_wgrad(dy, x, stride, pad, kh, kw, dw, dbias=None, nvalid=None, defer=
             assert dbias.dtype == torch.float32 and dbias.stride(1) == 1
             _call("dba_xcolsum", dy.data_ptr(), N * Ho * Wo * Cout, Ho * Wo, _ptr(_i32(nvalid)), G, N, Cout,
                   dbias.data_ptr(), dbias.stride(0), _stream())
-        return
+        return dy_out
     rc = NOT_HANDLED
     if _PCONV and stride == 1 and kh == 3 and kw == 3 and pad == 1 and H == W and Ho == H:
         # halo-tiled transposed-read wgrad (csrc/kernels/pwgrad.hip)
@@ -849,6 +902,138 @@ def conv2d_wgrad(dy, x, stride, pad, kh, kw, dw, dbias=None, nvalid=None, defer=
         assert dbias.dtype == torch.float32 and dbias.stride(1) == 1
         _call("dba_colsum", dy.data_ptr(), N * Ho * Wo * Cout, Ho * Wo, _ptr(_i32(nvalid)), G, N, Cout,
               dbias.data_ptr(), dbias.stride(0), _stream())
+
+
+# ------------------------------------------------------------ fused training BN (bnfuse.hpp)
+def _bn_workspace(G: int, M: int, C: int, device):
+    """Level-0 / level-1 records and the zeroed tickets of one fused BN pass (M rows per
+    replica): the counters come from the step's arena (no fill launch) when it has room."""
+    ngrp, nsg = (M + 31) // 32, (M + 511) // 512
+    rec0 = torch.empty(G * ngrp * C * 4, dtype=torch.float64, device=device)
+    rec1 = torch.empty(G * nsg * C * 4, dtype=torch.float64, device=device)
+    cnt = _sk_counters(G * nsg + G, device)
+    if cnt is None:
+        cnt = torch.zeros(G * nsg + G, dtype=torch.int32, device=device)
+    return ngrp, nsg, rec0, rec1, cnt
+
+
+def _bnf_common(mode: int, G: int, M: int, C: int, device):
+    ngrp, nsg, rec0, rec1, cnt = _bn_workspace(G, M, C, device)
+    f = _BnFuse()
+    f.mode, f.C, f.ngrp, f.nsg = mode, C, ngrp, nsg
+    f.rec0, f.rec1 = rec0.data_ptr(), rec1.data_ptr()
+    f.cnt1, f.cnt2 = cnt.data_ptr(), cnt.data_ptr() + 4 * G * nsg
+    f._keep = (rec0, rec1, cnt)   # alive until the launch has been enqueued
+    return f
+
+
+def _bnf_fwd(p: "bs.BnParams", relu: bool, G: int, M: int, C: int, device):
+    """Forward statistics (mode 1) of a conv output feeding BN ``p``: the BnStat it fills."""
+    coef = torch.empty(G, bs.ROWS, C, dtype=_F32, device=device)
+    bound = _amax_new(G, device)
+    st = bs.BnStat(coef, p, bound)
+    f = _bnf_common(1, G, M, C, device)
+    ps = _same_stride(p.gamma, p.beta, p.rmean, p.rvar)
+    f.coef_a, f.gamma_a, f.beta_a = coef.data_ptr(), p.gamma.data_ptr(), p.beta.data_ptr()
+    f.rm_a, f.rv_a, f.p_gstride = p.rmean.data_ptr(), p.rvar.data_ptr(), ps
+    f.momentum, f.eps, f.relu = float(p.momentum), float(p.eps), int(relu)
+    f.amax_a, f.amax_ld = bound.data_ptr(), bound.shape[1]
+    return f, st
+
+
+def _bnf_bwd(fin: "bs.Finish", G: int, M: int, device):
+    """Backward mask + reduce (mode 2) of a BN output's gradient (``fin``); allocates the dy
+    bound slots of its BNs."""
+    sa, sb = fin.sa, fin.sb
+    C = sa.C
+    f = _bnf_common(2, G, M, C, device)
+    ya = _act(fin.ya, _F32, "BN input")
+    pa = sa.params
+    f.coef_a, f.gamma_a, f.p_gstride = sa.coef.data_ptr(), pa.gamma.data_ptr(), _same_stride(pa.gamma)
+    f.ya, f.y_gstride = ya.data_ptr(), ya.stride(0)
+    f.dgamma_a, f.dbeta_a, f.gr_gstride = pa.dgamma.data_ptr(), pa.dbeta.data_ptr(), _same_stride(pa.dgamma, pa.dbeta)
+    sa.dbound = _amax_new(G, device)
+    f.amax_a, f.amax_ld = sa.dbound.data_ptr(), sa.dbound.shape[1]
+    keep = [ya]
+    if sb is not None:
+        yb = _act(fin.yb, _F32, "BN input")
+        assert yb.stride(0) == ya.stride(0) and sb.C == C
+        pb = sb.params
+        assert _same_stride(pb.gamma) == f.p_gstride and _same_stride(pb.dgamma, pb.dbeta) == f.gr_gstride
+        f.yb, f.coef_b, f.gamma_b = yb.data_ptr(), sb.coef.data_ptr(), pb.gamma.data_ptr()
+        f.dgamma_b, f.dbeta_b = pb.dgamma.data_ptr(), pb.dbeta.data_ptr()
+        sb.dbound = _amax_new(G, device)
+        f.amax_b = sb.dbound.data_ptr()
+        keep.append(yb)
+    if fin.mask_out is not None:
+        mo = _act(fin.mask_out, _F32, "BN output")
+        assert mo.stride(0) == ya.stride(0)
+        f.mask_out = mo.data_ptr()
+        keep.append(mo)
+    f.mask_lazy = int(bool(fin.lazy))
+    f._keep = f._keep + tuple(keep)
+    return f
+
+
+def conv_bn_stats(x, w, wsel, stride, pad, nvalid, p, relu):
+    """y = conv(x, w) with the training-BN statistics of y reduced and finalised in the same
+    launch (running stats updated); x may be a ``LazyBN`` (staged as relu?(y*scale+shift)).
+    Returns (y, BnStat)."""
+    lz = None
+    if isinstance(x, bs.LazyBN):
+        if x.stat.bound is None:
+            raise RuntimeError("lazy BN operand without its bound slot")
+        lz = (x.stat.coef, x.relu, x.stat.bound)
+        x = x.y
+    x = _act(x, _F32, "conv input")
+    G, N, H, W, Cin = x.shape
+    Cout, KH, KW = w.shape[1], w.shape[2], w.shape[3]
+    Ho = (H + 2 * pad - KH) // stride + 1
+    Wo = (W + 2 * pad - KW) // stride + 1
+    f, st = _bnf_fwd(p, relu, G, N * Ho * Wo, Cout, x.device)
+    y = _xconv_fwd(x, w, wsel, stride, pad, None, None, False, nvalid, None, bnf=f, lz=lz)
+    return y, st
+
+
+def bn_apply(a, residual, relu, nvalid=None):
+    """out = relu?(y_a * scale_a + shift_a + r), r = residual (tensor), a lazy BN output's value
+    (its own ReLU off), or 0 — one elementwise pass (xgemm.hip bnx_apply_kernel); folds max |out|."""
+    y = _act(a.y, _F32, "BN input")
+    G, N, H, W, C = y.shape
+    out = torch.empty_like(y)
+    am = _amax_out(out)
+    res = yb = cb = None
+    relu_b = 0
+    if isinstance(residual, bs.LazyBN):
+        yb, cb, relu_b = _act(residual.y, _F32, "BN input"), residual.stat.coef, int(residual.relu)
+        assert yb.shape == y.shape
+    elif residual is not None:
+        res = _act(residual, _F32, "residual")
+        assert res.shape == y.shape
+    _call("dba_bnx_apply", y.data_ptr(), a.stat.coef.data_ptr(), _ptr(res), _ptr(yb), _ptr(cb), relu_b, int(relu),
+          out.data_ptr(), y.stride(0), _ptr(_i32(nvalid)), G, N, H * W, C, *_aptr(am), _stream())
+    return out
+
+
+def bn_finish(g, fin, nvalid=None, pool=None, hw=None):
+    """Finish a BN output's gradient in one standalone pass (xgemm.hip bnx_rows_kernel): d = g
+    where the output is > 0 plus the backward sums / coefficients of its BN(s).  ``pool``
+    ([G, N, 1, 1, C]): g is the global average pool's gradient of it.  Returns a ``Fin``."""
+    ya = _act(fin.ya, _F32, "BN input")
+    G, N, H, W, C = ya.shape
+    f = _bnf_bwd(fin, G, N * H * W, ya.device)
+    d = torch.empty_like(ya)
+    src = None
+    if pool is not None:
+        pool = _act(pool, _F32, "pooled gradient").reshape(G, N, C)
+        assert hw == (H, W)
+    else:
+        src = _act(g, _F32, "BN output gradient")
+        assert src.shape == ya.shape
+    inv_hw = float(torch.tensor(1.0, dtype=torch.float32) / torch.tensor(float(H * W), dtype=torch.float32))
+    _call("dba_bnx_rows", ctypes.byref(f), _ptr(src), d.data_ptr(), ya.stride(0), _ptr(_i32(nvalid)), G, N, H * W,
+          _ptr(pool), inv_hw, _stream())
+    return bs.Fin(d, fin.stats())
 
 
 def wgrad_prepare(dy, x, nvalid=None):

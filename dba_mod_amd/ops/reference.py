@@ -17,6 +17,7 @@ from typing import Optional, Sequence, Tuple
 import torch
 import torch.nn.functional as F
 
+from . import bnstate as bs
 from . import rng
 
 Tensor = torch.Tensor
@@ -134,6 +135,120 @@ def conv2d(x: Tensor, w: Tensor, wsel: Optional[Tensor], stride: int, pad: int,
     return torch.stack(outs).to(out_dtype or x.dtype)
 
 
+def _valid_mask(t: Tensor, nvalid: Optional[Tensor]) -> Tensor:
+    """[G, N, 1, 1, 1] (bool) of the valid images of each replica."""
+    G, N = t.shape[:2]
+    n = torch.full((G,), N, dtype=torch.int64) if nvalid is None else nvalid.long().cpu()
+    v = torch.arange(N)[None, :] < n[:, None]
+    return v.view(G, N, *([1] * (t.dim() - 2))).to(t.device)
+
+
+def _coef(st: "bs.BnStat", row: int, t: Tensor) -> Tensor:
+    """Row ``row`` of a BN's coefficients broadcast over ``t`` [G, N, H, W, C]."""
+    return st.coef[:, row].view(t.shape[0], *([1] * (t.dim() - 2)), t.shape[-1]).to(t.dtype)
+
+
+def lazy_value(a: "bs.LazyBN", nvalid: Optional[Tensor] = None) -> Tensor:
+    """relu?(y * scale + shift) of a lazy training-BN output (zero on invalid images).  A
+    replayed ReLU decision (``ops.branches``) is taken from ``a.stat.relu_mask``."""
+    v = a.y * _coef(a.stat, bs.SCALE, a.y) + _coef(a.stat, bs.SHIFT, a.y)
+    if a.relu:
+        m = getattr(a.stat, "relu_mask", None)   # replayed decisions (ops.branches)
+        tiny = 1e-300 if v.dtype == torch.float64 else 1e-30
+        v = torch.relu(v) if m is None else torch.where(m.to(v.device), v.clamp(min=tiny), torch.zeros_like(v))
+    return torch.where(_valid_mask(v, nvalid), v, torch.zeros_like(v))
+
+
+def lazy_grad_value(lg: "bs.LazyGrad", nvalid: Optional[Tensor] = None) -> Tensor:
+    """dy = A * d + B * y + K of a training BN's input gradient (zero on invalid images)."""
+    st = lg.stat
+    v = _coef(st, bs.A, lg.d) * lg.d + _coef(st, bs.B, lg.y) * lg.y + _coef(st, bs.K, lg.d)
+    return torch.where(_valid_mask(v, nvalid), v, torch.zeros_like(v)).to(lg.d.dtype)
+
+
+def conv_bn_stats(x, w: Tensor, wsel: Optional[Tensor], stride: int, pad: int, nvalid: Optional[Tensor],
+                  p: "bs.BnParams", relu: bool):
+    """y = conv(x, w) and the training-BN statistics of y (running stats updated in place);
+    x may be a lazy BN output.  Returns (y, BnStat) — the fused conv + BN forward
+    (csrc/kernels/bnfuse.hpp); the BN output is :func:`lazy_value` of ``LazyBN(y, stat, relu)``."""
+    xv = lazy_value(x, nvalid) if isinstance(x, bs.LazyBN) else x
+    y = conv2d(xv, w, wsel, stride, pad, nvalid=nvalid)
+    G, N = y.shape[:2]
+    C = y.shape[-1]
+    coef = torch.zeros(G, bs.ROWS, C, dtype=_cdt(), device=y.device)
+    for g in range(G):
+        n = _rows_valid(nvalid, g, N)
+        if n == 0:
+            continue
+        flat = y[g, :n].to(_cdt()).reshape(-1, C)
+        cnt = flat.shape[0]
+        mean = flat.mean(0)
+        var = flat.var(0, unbiased=False)
+        invstd = torch.rsqrt(var + p.eps)
+        unbiased = var * (cnt / max(cnt - 1, 1))
+        p.rmean[g] = (1 - p.momentum) * p.rmean[g] + p.momentum * mean
+        p.rvar[g] = (1 - p.momentum) * p.rvar[g] + p.momentum * unbiased
+        sc = invstd * p.gamma[g].to(_cdt())
+        coef[g, bs.MEAN], coef[g, bs.INV] = mean, invstd
+        coef[g, bs.SCALE], coef[g, bs.SHIFT] = sc, p.beta[g].to(_cdt()) - mean * sc
+        coef[g, bs.YMAX], coef[g, bs.YMIN] = flat.max(0).values, flat.min(0).values
+    return y, bs.BnStat(coef, p)
+
+
+def bn_apply(a: "bs.LazyBN", residual, relu: bool, nvalid: Optional[Tensor] = None) -> Tensor:
+    """out = relu?(lazy BN value of ``a`` (its own ReLU not applied) + residual), residual a
+    tensor, a lazy BN output or None: the stored output of a BasicBlock / the stem."""
+    v = a.y * _coef(a.stat, bs.SCALE, a.y) + _coef(a.stat, bs.SHIFT, a.y)
+    if isinstance(residual, bs.LazyBN):
+        v = v + lazy_value(residual, nvalid)
+    elif residual is not None:
+        v = v + residual.to(v.dtype)
+    if relu:
+        v = torch.relu(v)
+    return torch.where(_valid_mask(v, nvalid), v, torch.zeros_like(v)).to(a.y.dtype)
+
+
+def bn_finish(g: Optional[Tensor], fin: "bs.Finish", nvalid: Optional[Tensor] = None,
+              pool: Optional[Tensor] = None, hw: Optional[Tuple[int, int]] = None) -> "bs.Fin":
+    """Finish the gradient of a BN output: d = g where the output is > 0, then the backward
+    sums of BN a (and BN b) -> dbeta += sum d, dgamma += sum d * xhat and the coefficients A, B,
+    K of dy = A d + B y + K (bn_train_bwd's arithmetic).  ``pool`` ([G, N, 1, 1, C]): g is the
+    global average pool's gradient of it (``avgpool_global_bwd``)."""
+    if pool is not None:
+        g = avgpool_global_bwd(pool, hw)
+    ya = fin.ya
+    d = g.to(_cdt())
+    if fin.mask_out is not None:
+        d = d * (fin.mask_out.to(_cdt()) > 0)
+    elif fin.lazy:
+        m = getattr(fin.sa, "relu_mask", None)
+        pre = ya.to(_cdt()) * _coef(fin.sa, bs.SCALE, ya).to(_cdt()) + _coef(fin.sa, bs.SHIFT, ya).to(_cdt())
+        d = d * ((pre > 0) if m is None else m.to(d.device))
+    d = torch.where(_valid_mask(d, nvalid), d, torch.zeros_like(d))
+    G, N = d.shape[:2]
+    C = d.shape[-1]
+    for y, st in ((ya, fin.sa), (fin.yb, fin.sb)):
+        if st is None:
+            continue
+        p = st.params
+        for gg in range(G):
+            n = _rows_valid(nvalid, gg, N)
+            if n == 0:
+                continue
+            dg = d[gg, :n].reshape(-1, C)
+            mean, inv = st.coef[gg, bs.MEAN].to(_cdt()), st.coef[gg, bs.INV].to(_cdt())
+            xhat = (y[gg, :n].to(_cdt()).reshape(-1, C) - mean) * inv
+            cnt = dg.shape[0]
+            sd, sdx = dg.sum(0), (dg * xhat).sum(0)
+            p.dbeta[gg] += sd.to(p.dbeta.dtype)
+            p.dgamma[gg] += sdx.to(p.dgamma.dtype)
+            A = p.gamma[gg].to(_cdt()) * inv
+            B = -A * inv * sdx / cnt
+            st.coef[gg, bs.A], st.coef[gg, bs.B] = A, B
+            st.coef[gg, bs.K] = -A * sd / cnt - B * mean
+    return bs.Fin(d.to(g.dtype), fin.stats())
+
+
 def wgrad_prepare(dy, x, nvalid=None):
     """HIP backend: attaches the operands' fp16-pair maxima before the weight gradient moves to
     a side stream.  Nothing to prepare here."""
@@ -154,9 +269,13 @@ def prepare_dgrad_weights(ref: Tensor, items: list) -> dict:
 def conv2d_dgrad(dy: Tensor, w: Tensor, wsel: Optional[Tensor], stride: int, pad: int,
                  in_hw: Tuple[int, int], nvalid: Optional[Tensor] = None,
                  out_dtype: Optional[torch.dtype] = None, accum: Optional[Tensor] = None,
-                 wt: Optional[Tensor] = None) -> Tensor:
+                 wt: Optional[Tensor] = None, finish: Optional["bs.Finish"] = None):
     """dX of a conv; ``accum`` (the input's gradient from another branch) is added in.
-    ``wt`` (a backend's pre-transposed weights) is ignored here."""
+    ``wt`` (a backend's pre-transposed weights) is ignored here.  ``finish``: dX is the complete
+    gradient of a training-BN output — return it finished (:func:`bn_finish`, a ``Fin``)."""
+    if finish is not None:
+        dx = conv2d_dgrad(dy, w, wsel, stride, pad, in_hw, nvalid, out_dtype, accum, wt)
+        return bn_finish(dx, finish, nvalid)
     G, N = dy.shape[:2]
     cin = w.shape[-1]
     outs = []
@@ -171,11 +290,18 @@ def conv2d_dgrad(dy: Tensor, w: Tensor, wsel: Optional[Tensor], stride: int, pad
     return dx.to(out_dtype or dy.dtype)
 
 
-def conv2d_wgrad(dy: Tensor, x: Tensor, stride: int, pad: int, kh: int, kw: int,
+def conv2d_wgrad(dy, x, stride: int, pad: int, kh: int, kw: int,
                  dw: Tensor, dbias: Optional[Tensor] = None, nvalid: Optional[Tensor] = None,
-                 defer: Optional[list] = None) -> None:
+                 defer: Optional[list] = None) -> Optional[Tensor]:
     """dw[g] += sum_rows dy (x) x  (fp32 accumulate into the flat grad buffer view).
-    ``defer`` (a backend's batched-reduction queue) is unused here: the sum is immediate."""
+    ``defer`` (a backend's batched-reduction queue) is unused here: the sum is immediate.
+    ``dy`` may be a :class:`LazyGrad` (its value is returned, for the data gradient) and ``x`` a
+    :class:`LazyBN`."""
+    out = None
+    if isinstance(dy, bs.LazyGrad):
+        dy = out = lazy_grad_value(dy, nvalid)
+    if isinstance(x, bs.LazyBN):
+        x = lazy_value(x, nvalid)
     G = dy.shape[0]
     cout = dy.shape[-1]
     cin = x.shape[-1]
@@ -185,6 +311,7 @@ def conv2d_wgrad(dy: Tensor, x: Tensor, stride: int, pad: int, kh: int, kw: int,
         dw[g] += gw.permute(0, 2, 3, 1)
         if dbias is not None:
             dbias[g] += dy[g].to(_cdt()).sum(dim=(0, 1, 2))
+    return out
 
 
 # ------------------------------------------------------------------------ batch norm
