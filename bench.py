@@ -124,6 +124,8 @@ def _args(argv=None):
                     help="run only rank R's share of an --emulate-world N round on one device "
                          "(collectives are counted no-ops; per-rank critical-path timing)")
     ap.add_argument("--emulate-world", type=int, default=None)
+    ap.add_argument("--dump-state", default=None,
+                    help="rank 0 saves the final global model here (torch.save; cross-world tests)")
     return ap.parse_args(argv)
 
 
@@ -195,6 +197,10 @@ def _run(args) -> int:
     sync()
     elapsed = dctx.all_reduce_max(time.perf_counter() - t0)
     rps = args.steps / elapsed if elapsed > 0 else 0.0
+    import hashlib
+    state_sha = hashlib.sha256(server.global_state.detach().cpu().numpy().tobytes()).hexdigest()[:16]
+    if args.dump_state and (dctx.is_main or dctx.emulated):
+        torch.save(server.global_state.detach().cpu(), args.dump_state)
     comm_kinds = sorted({k for r in done for k in r.get("comm_bytes", {})})
     comm_mean = {k: int(round(sum(r.get("comm_bytes", {}).get(k, 0) for r in done) / max(1, len(done))))
                  for k in comm_kinds}
@@ -240,6 +246,8 @@ def _run(args) -> int:
             "global_asr": round(float(last.get("global_asr", 0.0)), 3),
             "rounds": [[int(r["epoch"]), round(float(r.get("global_acc", 0.0)), 2), round(float(r.get("global_asr", 0.0)), 2)]
                        for r in done],
+            # the final global model's bytes (untimed): equal across world sizes (bitwise contract)
+            "state_sha": state_sha,
             "phases_mean_s": {k: round(sum(r.get("phases", {}).get(k, 0.0) for r in done) / max(1, len(done)), 4)
                               for k in (done[0].get("phases", {}) if done else {})},
         }

@@ -26,11 +26,13 @@ def _rel(a, b):
                                       ("resnet18_tiny", (64, 64, 3)), ("loan", (91,)),
                                       ("resnet34_cifar", (32, 32, 3)), ("resnet50_cifar", (32, 32, 3))])
 def test_train_step_hip_vs_reference(dev, arch, shp):
-    """Grouped train step through the HIP kernels vs the fp32 reference.
+    """Grouped train step through the HIP kernels (fp32 family, fused training BN) vs the fp32
+    reference ops.
 
-    At random init these ReLU+BN nets are chaotic: rounding only the *input* to bf16 moves the
-    fp32 gradient by ~20 % (measured on CPU), so the HIP (bf16 storage) gradient is checked
-    against that sensitivity band, and tightly on the well-conditioned final layer."""
+    At random init these ReLU+BN nets are chaotic: a relative 1e-6 perturbation of the input
+    moves the fp32 gradient of the deep ones by up to ~1 %, so the HIP gradient is checked
+    against that sensitivity band, and tightly on the well-conditioned final layer
+    (test_gpu_f32.test_fp32_train_step_vs_fp64 is the branch-matched fp64 check)."""
     from dba_mod_amd import ops
     from dba_mod_amd.models import program as P
     from dba_mod_amd.models.spec import get_spec
@@ -63,27 +65,25 @@ def test_train_step_hip_vs_reference(dev, arch, shp):
                 setattr(ops, k, v)
         return loss, grads, state
 
-    lh, gh, sh = run(hip, torch.bfloat16, x, flat)
+    lh, gh, sh = run(hip, torch.float32, x, flat)
     lr_, gr, sr = run(reference, torch.float32, x, flat)
-    flr = flat.clone()
-    flr[:spec.P] = flr[:spec.P].bfloat16().float()
-    _, gp, _ = run(reference, torch.float32, x.bfloat16().float(), flr)
+    _, gp, _ = run(reference, torch.float32, x * (1 + 1e-6 * torch.randn_like(x)), flat)
     fc = spec.params[-2]
     for g in range(2):
-        assert abs(lh[g].item() - lr_[g].item()) < 0.03 * max(1.0, abs(lr_[g].item()))
+        assert abs(lh[g].item() - lr_[g].item()) < 1e-4 * max(1.0, abs(lr_[g].item()))
         band = _rel(gp[g], gr[g])
-        assert _rel(gh[g], gr[g]) < max(0.08, 1.6 * band), (arch, g, _rel(gh[g], gr[g]), band)
+        assert _rel(gh[g], gr[g]) < max(1e-3, 3 * band), (arch, g, _rel(gh[g], gr[g]), band)
         sl = slice(fc.offset, fc.offset + fc.numel)
         band_fc = _rel(gp[g, sl], gr[g, sl])   # deep nets (ResNet-50+) are chaotic up to the head too
-        assert _rel(gh[g, sl], gr[g, sl]) < max(0.05, 1.6 * band_fc), (arch, "final layer", band_fc)
+        assert _rel(gh[g, sl], gr[g, sl]) < max(1e-4, 3 * band_fc), (arch, "final layer", band_fc)
         if spec.B:
-            assert _rel(sh[g, spec.P:], sr[g, spec.P:]) < 2e-2
+            assert _rel(sh[g, spec.P:], sr[g, spec.P:]) < 1e-5
     assert gh[2].abs().max().item() == 0.0          # inactive replica untouched
 
 
 @pytest.mark.parametrize("arch", ["resnet18_cifar", "resnet50_cifar", "resnet101_cifar"])
 def test_eval_forward_hip_vs_reference(dev, arch):
-    """Folded-BN eval forward of a model bank through the HIP kernels (bf16) vs the fp32
+    """Folded-BN eval forward of a model bank through the HIP kernels (fp32 family) vs the fp32
     reference ops: logits and argmax agreement (the bottleneck family adds 1x1 stride-1
     convs over 32..1024 channels and a 1024-wide linear)."""
     from dba_mod_amd import ops
@@ -107,11 +107,11 @@ def test_eval_forward_hip_vs_reference(dev, arch):
             for k, v in saved.items():
                 setattr(ops, k, v)
 
-    oh, orf = run(hip, torch.bfloat16), run(reference, torch.float32)
+    oh, orf = run(hip, torch.float32), run(reference, torch.float32)
     assert torch.isfinite(oh).all()
     for g in range(3):
-        assert _rel(oh[g], orf[g]) < 0.05, (arch, g, _rel(oh[g], orf[g]))
-    assert (oh.argmax(-1) == orf.argmax(-1)).float().mean().item() > 0.9
+        assert _rel(oh[g], orf[g]) < 1e-4, (arch, g, _rel(oh[g], orf[g]))
+    assert (oh.argmax(-1) == orf.argmax(-1)).float().mean().item() > 0.99
 
 
 def _small_params(**kw):
@@ -123,47 +123,52 @@ def _small_params(**kw):
     return C.load_params(os.path.join(root, "configs", "mnist_params.yaml"), base)
 
 
-@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
-def test_graph_replay_matches_eager(dev, tmp_path, dtype):
-    """A captured HIP graph replays the same launches as the eager step: bit-identical in the
-    deterministic fp32 family; the bf16 family within its rounding band."""
+@pytest.mark.parametrize("which", ["mnist", "cifar"])
+def test_graph_replay_matches_eager(dev, tmp_path, which):
+    """A captured HIP graph replays the same launches as the eager step: bit-identical (the
+    CIFAR case runs the fused training BN: its tickets and counters live in the graph)."""
     from dba_mod_amd.fl.server import Server
     from dba_mod_amd.parallel.dist import DistCtx
     outs = []
     for cap in (False, True):
-        p = _small_params(graph_capture=cap, save_dir=str(tmp_path), compute_dtype=dtype)
+        if which == "mnist":
+            p = _small_params(graph_capture=cap, save_dir=str(tmp_path))
+            rounds = (11, 12)    # attacker 41 poisons in round 12
+        else:
+            p = _cifar_small(tmp_path, graph_capture=cap, synthetic_train_size=3000)
+            rounds = (203,)
         s = Server(p, DistCtx(device=dev), write_outputs=False)
-        s.run_round(11)
-        s.run_round(12)          # attacker 41 poisons in round 12
+        for r in rounds:
+            s.run_round(r)
         outs.append(s.global_state.clone())
-    if dtype == "fp32":
-        assert torch.equal(outs[1], outs[0])
-    else:
-        assert _rel(outs[1], outs[0]) < 2e-2
+    assert torch.equal(outs[1], outs[0])
 
 
-@pytest.mark.parametrize("dtype,agg", [("fp32", "mean"), ("bf16", "mean"), ("fp32", "foolsgold")])
-def test_solo_tail_bitwise(dev, tmp_path, dtype, agg):
+@pytest.mark.parametrize("which,agg", [("mnist", "mean"), ("mnist", "foolsgold"), ("cifar", "mean")])
+def test_solo_tail_bitwise(dev, tmp_path, which, agg):
     """The solo tail (the long attacker's last steps move from the G-replica graph to the
     one-replica graph mid-wave, fl/trainer.py _solo_enter/_solo_leave) changes no bit: every
     snapshot, the per-epoch stats and the FoolsGold gradient sums equal a run without it.
-    The bf16 family picks split-K / tiles from the replica count, so it never takes the solo
-    tail (it would change the rounding), and its kernels use float atomics (not bitwise
-    run to run): there the test checks that the solo tail stays off."""
+    The CIFAR case (ResNet-18, batch 64) covers the fused training BN, whose statistics must not
+    depend on the launch's replica count (split-K in-launch combine at G = 1, separate reduce +
+    the standalone pass at G > 1: ADVICE r3)."""
     from dba_mod_amd.fl.server import Server
     from dba_mod_amd.parallel.dist import DistCtx
     got = []
     for solo in (0, 4):
-        p = _small_params(save_dir=str(tmp_path / f"s{solo}"), compute_dtype=dtype, aggregation_methods=agg)
+        if which == "mnist":
+            p = _small_params(save_dir=str(tmp_path / f"s{solo}"), aggregation_methods=agg)
+            epoch = 12                              # attacker 41: 10 poison epochs vs 1 benign
+        else:
+            p = _cifar_small(tmp_path / f"s{solo}", synthetic_train_size=5000, aggregation_methods=agg)
+            epoch = 203                             # attacker 17: 6 poison epochs vs 2 benign
         s = Server(p, DistCtx(device=dev), write_outputs=False)
         s.trainer.SOLO_MIN_STEPS = solo
-        st = s._train_begin(12)                     # attacker 41: 10 poison epochs vs 1 benign
+        st = s._train_begin(epoch)
         if solo:
             engaged = s.trainer._solo_tail(st["plan"].clients, max(len(c.steps) for c in st["plan"].clients))
-            assert bool(engaged) == (dtype == "fp32")
+            assert engaged
         got.append({r.name: r for r in st["handle"].collect()})
-    if dtype != "fp32":
-        return
     a, b = got
     assert a.keys() == b.keys()
     for name in a:

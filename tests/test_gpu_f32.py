@@ -19,8 +19,9 @@ def H():
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     from dba_mod_amd.ops import hip
-    hip.set_fp32_planes(3)
-    return hip
+    prev = hip.set_fp32_planes(3)
+    yield hip
+    hip.set_fp32_planes(prev)
 
 
 @pytest.fixture()
@@ -487,8 +488,9 @@ def test_fp32_train_step_vs_fp64(H, R64, arch, shp):
 
     from dba_mod_amd.ops.branches import BranchReplay
     br = BranchReplay(nval)
-    lh, gh, sh = run(H, dev, torch.float32, br.wrap(H))
-    lh2, gh2, sh2 = run(H, dev, torch.float32)
+    with H.fp32_split(H.F16_PAIR):   # the training step's split (fused BN: fp16 pair)
+        lh, gh, sh = run(H, dev, torch.float32, br.wrap(H))
+        lh2, gh2, sh2 = run(H, dev, torch.float32)
     assert torch.equal(gh, gh2) and torch.equal(sh, sh2) and torch.equal(lh, lh2), "not bitwise reproducible"
     br.start_replay()
     lr_, gr, sr = run(R64, torch.device("cpu"), torch.float64, br.wrap(R64))
