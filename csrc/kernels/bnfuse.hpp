@@ -9,10 +9,8 @@
 // Forward.  The producing conv's epilogue (xgemm.hip xconv / xhalo, stem.hip) reduces its
 // tile of the raw output y into LEVEL-0 records, one per (32-row group, channel):
 //     {sum y, sum y^2, max y, min y}        (sums in fp64, sequential over the 32 rows)
-// Every 512 rows (16 groups) form a super group (SG); the tile blocks of an SG draw tickets on
-// the SG's counter and the last one sums the SG's 16 records in group order into a LEVEL-1
-// record; those SG finalisers draw tickets on the replica's counter and the last one sums the
-// SG records in order and finalises: mean, 1/std, the running-stat update, the affine form
+// and one small launch (bnx_finalize_kernel, a block per (channel, replica)) sums a channel's
+// records in a fixed order and finalises: mean, 1/std, the running-stat update, the affine form
 // scale = gamma/std, shift = beta - mean*scale of the BN (+ReLU) output, and an exact bound of
 // that output's max |.| (from the per-channel max / min of y) for the fp16-pair operand scale
 // of its consumers.  The output itself is never stored when its only consumers are convs: the
@@ -23,7 +21,7 @@
 // it (d = g where the output is > 0), stores d, and reduces level-0 records
 //     {sum d, sum d*xhat_a, sum d*xhat_b, max |d|}     (xhat = (y - mean) * invstd, fp32)
 // for the BN a of the output and, when the output is a residual sum of two BNs (a shortcut
-// conv), the BN b of the other branch; the same two-level tickets finalise dbeta += sum d,
+// conv), the BN b of the other branch; the finalize launch accumulates dbeta += sum d,
 // dgamma += sum d*xhat and the affine form of the BN input gradient
 //     dy = fma(A, d, fma(B, y, K)),  A = gamma*invstd, B = -A*invstd*sum(d*xhat)/n,
 //     K = -A*sum(d)/n - B*mean
@@ -31,36 +29,26 @@
 // the conv below stages dy from (d, y) on the fly and stores it once for that conv's data
 // gradient.
 //
-// Every order is fixed (groups of 32 rows, SGs of 16 groups, SGs in order) and independent of
-// the tile shape of the launch, so the bits do not depend on how many replicas share a launch:
-// a tile (32 / 64 / 128 rows, 512 % rows == 0) always covers whole groups of one SG; split-K
-// launches, the separate split-K reduce and the standalone kernels (bn.hip bnx_*) produce the
-// same records.  Hand-offs between the blocks of one launch: every record is stored
-// write-through (sc1) and drained by every storing wave (vmcnt(0)) before a workgroup barrier
-// and ONE agent-scope atomic add per workgroup; the workgroup whose add returns expected-1
-// reads the records with sc1 loads only — the first row of MI355X_MICROARCH.md's hand-off table
-// (§ visibility: "ONE lane of each storing workgroup, for ALL that workgroup's stores: an
-// agent-scope atomic add ... the workgroup whose add came last, told by the value its add
-// returned ... loads, all sc1").  No block waits for another, so the grid always drains.
+// Every order is fixed (groups of 32 rows; the finalize's per-thread strides and LDS tree depend
+// on the replica's group count only) and independent of the tile shape of the launch, so the
+// bits do not depend on how many replicas share a launch: a tile (32 / 64 / 128 rows) always
+// covers whole groups; split-K launches, the standalone pass (xgemm.hip bnx_tile_kernel) and the
+// epilogues produce the same records.  (An in-kernel two-level ticket finalisation was measured
+// first: its serial tail after the last tile cost 12-20 us per conv — more than this launch.)
 #pragma once
 #include "common.hpp"
 
 __host__ __device__ __forceinline__ int ceil_div_d(int a, int b) { return (a + b - 1) / b; }
 
 constexpr int kBnGrp = 32;                 // rows per level-0 group
-constexpr int kBnSg = 512;                 // rows per super group
-constexpr int kBnGpS = kBnSg / kBnGrp;     // groups per super group
 // per-BN coefficient rows [G][kBnRows][C] (fp32)
 enum { kCMean = 0, kCInv, kCScale, kCShift, kCYmax, kCYmin, kCA, kCB, kCK, kBnRows };
 
 struct BnFuse {
   int mode;                 // 0 none, 1 forward statistics of the output, 2 backward (mask + reduce)
   int C;                    // channels of the output (= the conv's Ncol)
-  int ngrp, nsg;            // groups / super groups per replica (from the replica's row count)
-  double* rec0;             // [G][ngrp][C][4]
-  double* rec1;             // [G][nsg][C][4]
-  int* cnt1;                // [G][nsg] zeroed
-  int* cnt2;                // [G] zeroed
+  int ngrp;                 // 32-row groups per replica (from the replica's row count)
+  double* rec0;             // [G][C][ngrp][4] level-0 records (channel-major: the finalize reads a channel's run)
   // BN a: forward — the BN of this output; backward — the BN whose output's gradient this is
   float* coef_a;            // [G][kBnRows][C]
   const float* gamma_a; const float* beta_a; float* rm_a; float* rv_a;
@@ -76,42 +64,9 @@ struct BnFuse {
   int mask_lazy;            //   where fma(ya, scale_a, shift_a) > 0 (mask_lazy), else d = g
 };
 
-// ---- write-through record stores / loads (aux 16 = sc1)
-typedef __attribute__((ext_vector_type(4))) unsigned int bnf_u32x4;
-__device__ __forceinline__ void bnf_store_rec(double* base, long long rec_index, long long nrec, double a, double b,
-                                              double c, double d) {
-  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(base, (short)0, (int)0x7fffffff, 0x00020000);
-  const int off = (int)(rec_index * 32);
-  (void)nrec;
-  const double2 lo = make_double2(a, b), hi = make_double2(c, d);
-  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(bnf_u32x4, lo), r, off, 0, 16);
-  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(bnf_u32x4, hi), r, off + 16, 0, 16);
-}
-__device__ __forceinline__ void bnf_load_rec(const double* base, long long rec_index, double (&v)[4]) {
-  const __amdgpu_buffer_rsrc_t r =
-      __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(base), (short)0, (int)0x7fffffff, 0x00020000);
-  const int off = (int)(rec_index * 32);
-  const double2 lo = __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 16));
-  const double2 hi = __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(r, off + 16, 0, 16));
-  v[0] = lo.x; v[1] = lo.y; v[2] = hi.x; v[3] = hi.y;
-}
-
-// block-level ticket: every thread calls; true in every thread of the block whose add was the
-// expected-th.  The counter is reset by that block (reusable by the next launch / replay).
-__device__ __forceinline__ bool bnf_arrive(int* cnt, int expected) {
-  __shared__ int bnf_last;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave drains its sc1 stores
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const int t = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int last = t == expected - 1;
-    if (last) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    bnf_last = last;
-  }
-  __syncthreads();
-  const bool last = bnf_last;
-  if (last) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // compiler: loads stay below
-  return last;
+__device__ __forceinline__ void bnf_store_rec(double* p, double a, double b, double c, double d) {
+  ((double2*)p)[0] = make_double2(a, b);
+  ((double2*)p)[1] = make_double2(c, d);
 }
 
 // combine record v into accumulator a (sums in order; max / min or max |d|)
@@ -184,62 +139,6 @@ __device__ __forceinline__ float bnf_finalize_channel(const BnFuse& f, int g, in
   return ba;
 }
 
-// the replica finaliser (one block): sums the nsg_v level-1 records of every channel in SG order
-__device__ __forceinline__ void bnf_finalize_replica(const BnFuse& f, int g, int nsg_v, double n) {
-  __shared__ float bnf_red[2][4];
-  float ba = 0.f, bb = 0.f;
-  for (int c = threadIdx.x; c < f.C; c += blockDim.x) {
-    double a[4];
-    bnf_init(a, f.mode);
-    for (int s = 0; s < nsg_v; ++s) {
-      double v[4];
-      bnf_load_rec(f.rec1, ((long long)g * f.nsg + s) * f.C + c, v);
-      bnf_acc(a, v, f.mode);
-    }
-    ba = fmaxf(ba, bnf_finalize_channel(f, g, c, a, n, &bb));
-  }
-  ba = wave_max(ba);
-  bb = wave_max(bb);
-  const int w = threadIdx.x >> 6;
-  if ((threadIdx.x & 63) == 0) { bnf_red[0][w] = ba; bnf_red[1][w] = bb; }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const int nw = (int)(blockDim.x + 63) >> 6;
-    float x = 0.f, y = 0.f;
-    for (int k = 0; k < nw; ++k) { x = fmaxf(x, bnf_red[0][k]); y = fmaxf(y, bnf_red[1][k]); }
-    // the slot is zeroed and this block is its only writer (sub-slot 0 of common.hpp's layout)
-    if (f.amax_a) f.amax_a[g] = __float_as_int(x);
-    if (f.amax_b) f.amax_b[g] = __float_as_int(y);
-  }
-}
-
-// the SG finaliser (one block): sums the SG's level-0 records in group order into its level-1
-// record, then the replica ticket
-__device__ __forceinline__ void bnf_finalize_sg(const BnFuse& f, int g, int s, int Mv) {
-  const int gv = ceil_div_d(Mv, kBnGrp);
-  const int b0 = s * kBnGpS, b1 = min(gv, b0 + kBnGpS);
-  for (int c = threadIdx.x; c < f.C; c += blockDim.x) {
-    double a[4];
-    bnf_init(a, f.mode);
-    for (int b = b0; b < b1; ++b) {
-      double v[4];
-      bnf_load_rec(f.rec0, ((long long)g * f.ngrp + b) * f.C + c, v);
-      bnf_acc(a, v, f.mode);
-    }
-    bnf_store_rec(f.rec1, ((long long)g * f.nsg + s) * f.C + c, 0, a[0], a[1], a[2], a[3]);
-  }
-  const int nsg_v = ceil_div_d(Mv, kBnSg);
-  if (bnf_arrive(f.cnt2 + g, nsg_v)) bnf_finalize_replica(f, g, nsg_v, (double)Mv);
-}
-
-// after a tile block stored its level-0 records (rows m0.. of the replica, BM rows, one of
-// tiles_n column tiles): the SG ticket and, for the last arriver, the SG finalisation
-__device__ __forceinline__ void bnf_tile_done(const BnFuse& f, int g, int m0, int BM, int tiles_n, int Mv) {
-  const int s = m0 / kBnSg;
-  const int rows = min(kBnSg, Mv - s * kBnSg);
-  if (bnf_arrive(f.cnt1 + (long long)g * f.nsg + s, ceil_div_d(rows, BM) * tiles_n)) bnf_finalize_sg(f, g, s, Mv);
-}
-
 // level-0 records of a tile staged in LDS: Ct [BM][BN] fp32 (forward: y; backward: d, already
 // masked) of rows m0.. / columns n0.. of replica g; orow[r] >= 0 marks a valid row and is its
 // element offset in the replica's [M][C] output (the offset of ya / yb too)
@@ -247,7 +146,7 @@ template <int BM, int BN>
 __device__ __forceinline__ void bnf_tile_records(const BnFuse& f, const float* Ct, const long long* orow, int g,
                                                  int m0, int n0, int Mv) {
   constexpr int NG = BM / kBnGrp;
-  static_assert(BM % kBnGrp == 0 && kBnSg % BM == 0, "tiles cover whole groups of one super group");
+  static_assert(BM % kBnGrp == 0, "tiles cover whole groups");
   const int gv = ceil_div_d(Mv, kBnGrp);
   const int C = f.C;
   const float* ya = f.mode == 2 ? f.ya + (long long)g * f.y_gstride : nullptr;
@@ -274,20 +173,28 @@ __device__ __forceinline__ void bnf_tile_records(const BnFuse& f, const float* C
     } else {
       const float ma = ca[kCMean * C + n], ia = ca[kCInv * C + n];
       const float mb = cb ? cb[kCMean * C + n] : 0.f, ib = cb ? cb[kCInv * C + n] : 0.f;
-#pragma unroll 4
+      // the group's BN inputs first, all loads in flight (a load per row in the ordered loop
+      // below cost one memory latency per 4 rows: +8-12 us per data-gradient launch)
+      float yav[kBnGrp], ybv[kBnGrp];
+#pragma unroll
+      for (int r = 0; r < kBnGrp; ++r) {
+        const long long o = orow[grp * kBnGrp + r];
+        yav[r] = o >= 0 ? ya[o + n] : 0.f;
+        ybv[r] = (o >= 0 && yb) ? yb[o + n] : 0.f;
+      }
+#pragma unroll
       for (int r = 0; r < kBnGrp; ++r) {
         const int row = grp * kBnGrp + r;
-        const long long o = orow[row];
-        if (o < 0) continue;
+        if (orow[row] < 0) continue;
         const float d = Ct[row * BN + cc];
-        const float xa = (ya[o + n] - ma) * ia;
+        const float xa = (yav[r] - ma) * ia;
         a[0] += (double)d;
         a[1] = fma((double)d, (double)xa, a[1]);
-        if (yb) a[2] = fma((double)d, (double)((yb[o + n] - mb) * ib), a[2]);
+        if (yb) a[2] = fma((double)d, (double)((ybv[r] - mb) * ib), a[2]);
         a[3] = fmax(a[3], (double)fabsf(d));
       }
     }
-    bnf_store_rec(f.rec0, ((long long)g * f.ngrp + b) * C + n, 0, a[0], a[1], a[2], a[3]);
+    bnf_store_rec(f.rec0 + (((long long)g * C + n) * f.ngrp + b) * 4, a[0], a[1], a[2], a[3]);
   }
 }
 
@@ -308,3 +215,53 @@ __device__ __forceinline__ float4 bnf_mask4(const BnFuse& f, int g, long long o,
   }
   return v;
 }
+
+// One block per (channel, replica): the channel's level-0 records summed in a fixed order
+// (thread t: groups t, t + 256, ... in order; then a fixed pairwise LDS tree), finalised by
+// thread 0; the bound folds into the zeroed slot with an integer atomicMax (exact, any order).
+__device__ __forceinline__ void bnf_finalize_block(const BnFuse& f, int g, int c, int Mv) {
+  __shared__ double red[256][4];
+  const int tid = threadIdx.x;
+  const int gv = ceil_div_d(Mv, kBnGrp);
+  double a[4];
+  bnf_init(a, f.mode);
+  const double* r = f.rec0 + ((long long)g * f.C + c) * f.ngrp * 4;
+  for (int b = tid; b < gv; b += 256) {
+    const double2 lo = ((const double2*)(r + b * 4))[0], hi = ((const double2*)(r + b * 4))[1];
+    const double v[4] = {lo.x, lo.y, hi.x, hi.y};
+    bnf_acc(a, v, f.mode);
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) red[tid][q] = a[q];
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (tid < w) {
+      const double v[4] = {red[tid + w][0], red[tid + w][1], red[tid + w][2], red[tid + w][3]};
+      double x[4] = {red[tid][0], red[tid][1], red[tid][2], red[tid][3]};
+      bnf_acc(x, v, f.mode);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) red[tid][q] = x[q];
+    }
+    __syncthreads();
+  }
+  if (tid != 0) return;
+  const double t[4] = {red[0][0], red[0][1], red[0][2], red[0][3]};
+  float bb = 0.f;
+  const float ba = bnf_finalize_channel(f, g, c, t, (double)Mv, &bb);
+  if (f.amax_a && ba > 0.f) atomicMax(f.amax_a + (c % kAmaxSub) * f.amax_ld + g, __float_as_int(ba));
+  if (f.amax_b && bb > 0.f) atomicMax(f.amax_b + (c % kAmaxSub) * f.amax_ld + g, __float_as_int(bb));
+}
+
+namespace {
+__global__ __launch_bounds__(256) void bnx_finalize_kernel(const BnFuse f, const int* __restrict__ nvalid, int N,
+                                                           int HW) {
+  const int Mv = valid_rows(nvalid, blockIdx.y, N) * HW;
+  if (Mv > 0) bnf_finalize_block(f, blockIdx.y, blockIdx.x, Mv);   // (inactive replicas: consumers skip them)
+}
+
+// the finalize launch of a fused BN pass (after its producer in stream order)
+inline int bnx_finalize_go(const BnFuse& f, const int* nvalid, int G, int N, int HW, hipStream_t st) {
+  hipLaunchKernelGGL(bnx_finalize_kernel, dim3(f.C, G), dim3(256), 0, st, f, nvalid, N, HW);
+  return (int)hipGetLastError();
+}
+}  // namespace

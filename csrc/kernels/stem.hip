@@ -176,7 +176,7 @@ __global__ __launch_bounds__(256) void xstem_kernel(const StemArgs a) {
             r4[2] = fmax(r4[2], v);
             r4[3] = fmin(r4[3], v);
           }
-          bnf_store_rec(a.bf.rec0, ((long long)g * a.bf.ngrp + b) * COUT + c, 0, r4[0], r4[1], r4[2], r4[3]);
+          bnf_store_rec(a.bf.rec0 + (((long long)g * COUT + c) * a.bf.ngrp + b) * 4, r4[0], r4[1], r4[2], r4[3]);
         }
       }
       for (int e = tid; e < (PIX / 32) * COUT && a.bnpart; e += 256) {
@@ -197,7 +197,6 @@ __global__ __launch_bounds__(256) void xstem_kernel(const StemArgs a) {
     }
   }
   if (a.amax_out) amax_fold(a.amax_out, a.amax_ld, g, vmax);
-  if (a.bf.mode == 1) bnf_tile_done(a.bf, g, mb, ITER * PIX, 1, Mv);
 }
 
 template <int KH, int KW, int CIN, int COUT, int CPT>
@@ -205,11 +204,12 @@ int stem_go(const StemArgs& a, int G, hipStream_t st) {
   constexpr int PIX = 256 / (COUT / CPT);
   constexpr int ITER = 4;   // pixel tiles per block: one weight load (LDS transpose) per 4 tiles
   if ((a.bnpart || a.bf.mode) && PIX % 32 != 0) return -100;
-  static_assert(kBnSg % (PIX * ITER) == 0 || PIX % 32 != 0, "a block covers whole groups of one super group");
   const long long M = (long long)a.N * a.Ho * a.Wo;
   const dim3 grid((unsigned)ceil_div(M, PIX * ITER), G);
   hipLaunchKernelGGL((xstem_kernel<KH, KW, CIN, COUT, CPT, ITER>), grid, dim3(256), 0, st, a);
-  DBA_LAUNCH_CHECK();
+  const int rc = (int)hipGetLastError();
+  if (rc != 0 || !a.bf.mode) return rc;
+  return bnx_finalize_go(a.bf, a.nvalid, G, a.N, a.Ho * a.Wo, st);   // the fused BN's finalize
 }
 
 }  // namespace

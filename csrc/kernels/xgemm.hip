@@ -767,7 +767,6 @@ __global__ __launch_bounds__(256) void xconv_kernel(const XArgs a) {
   if (bfm) {
     __syncthreads();   // d in Ct (backward)
     bnf_tile_records<BM, BN>(a.bf, Ct, orow, g, m0, n0, Mv);
-    bnf_tile_done(a.bf, g, m0, BM, a.tiles_n, Mv);
   }
 }
 
@@ -1049,7 +1048,6 @@ __global__ __launch_bounds__(256) void xhalo_kernel(const XArgs a) {
     __syncthreads();   // d in Ct (backward)
     const int Mv = nv_img * a.Ho * a.Wo;
     bnf_tile_records<BM, BN>(a.bf, Ct, orow, g, tm * BM, n0, Mv);
-    bnf_tile_done(a.bf, g, tm * BM, BM, a.tiles_n, Mv);
   }
 }
 
@@ -1307,18 +1305,16 @@ struct XWArgs {
   const int* amax_x;
   int amax_dy_ld, amax_x_ld;
   FDiv dHoWo, dWo;
-  // lazy operands (bnfuse.hpp).  DLZ: dy = fma(A, d, fma(B, y, K)) of the BN below the conv
-  // (dy points at d; dy_y: that BN's input y; dy_coef: its rows [G][kBnRows][Cout]); the k-tile-0
-  // blocks store dy once to dy_out (the data gradient's operand).  XLZ: x = relu?(fma(y, scale,
-  // shift)) of the BN that produced the conv's input (x points at y; zero in the padding).
-  const float* dy_y; const float* dy_coef; float* dy_out;
+  // lazy x operand (bnfuse.hpp, XLZ): x = relu?(fma(y, scale, shift)) of the BN that produced
+  // the conv's input (x points at y; zero in the padding).  (A lazy dy staged from (d, y) was
+  // measured slower than bnx_dy_kernel's stored dy: profiles/r4/bnx/ab_steps.md.)
   const float* x_coef; int x_relu;
 };
 
-template <int BNO, int BK, int WN_, int WK_, int P, int VEC, bool H, bool DLZ = false, bool XLZ = false>
+template <int BNO, int BK, int WN_, int WK_, int P, int VEC, bool H, bool XLZ = false>
 __global__ __launch_bounds__(256) void xwgrad_kernel(const XWArgs a) {
   static_assert(!H || P == 2, "fp16 split: 2 planes");
-  static_assert(!(DLZ || XLZ) || H, "lazy BN operands: fp16 pair");
+  static_assert(!XLZ || H, "lazy BN operand: fp16 pair");
   constexpr int TNo = BNO / WN_, TK = BK / WK_, MI = TNo / 32, NJ = TK / 32;
   static_assert(WN_ * WK_ == 4 && MI >= 1 && NJ >= 1, "wave tiling");
   static_assert(BK == 128, "x micro-tiles: one per thread");
@@ -1357,20 +1353,8 @@ __global__ __launch_bounds__(256) void xwgrad_kernel(const XWArgs a) {
   }
 
   float dv[2][4][4], xv[2][4][4];   // [stage][m][n or k]
-  float yv[DLZ ? 2 : 1][4][4];      // DLZ: the BN input y at dy's positions
-  int s_mt[2] = {0, 0};             // the m-step each stage holds (DLZ: row validity)
   unsigned s_xok[2] = {0u, 0u};     // XLZ: in-image bit (r * 4 + e) per stage
-  float cA[4], cB[4], cK[4], xsc[4], xsh[4];
-  if constexpr (DLZ) {
-    const float* cf = a.dy_coef + (long long)g * kBnRows * a.Cout;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const bool ok = dact && dn + e < a.Cout;
-      cA[e] = ok ? cf[kCA * a.Cout + dn + e] : 0.f;
-      cB[e] = ok ? cf[kCB * a.Cout + dn + e] : 0.f;
-      cK[e] = ok ? cf[kCK * a.Cout + dn + e] : 0.f;
-    }
-  }
+  float xsc[4], xsh[4];
   if constexpr (XLZ) {
     const float* cf = a.x_coef + (long long)g * kBnRows * a.Cin;
 #pragma unroll
@@ -1379,8 +1363,7 @@ __global__ __launch_bounds__(256) void xwgrad_kernel(const XWArgs a) {
       xsh[e] = xkv[e] ? cf[kCShift * a.Cin + xc[e]] : 0.f;
     }
   }
-  const __amdgpu_buffer_rsrc_t rY = rsrc(DLZ ? a.dy_y + (long long)g * a.dy_gstride : nullptr,
-                                         (long long)a.N * HoWo * a.Cout * 4);
+
   // bounds-checked buffer loads (32-bit in-replica offsets: checked on the host)
   const __amdgpu_buffer_rsrc_t rD = rsrc(dy, (long long)a.N * HoWo * a.Cout * 4);
   const __amdgpu_buffer_rsrc_t rX = rsrc(x, (long long)a.N * a.H * a.W * a.Cin * 4);
@@ -1389,17 +1372,11 @@ __global__ __launch_bounds__(256) void xwgrad_kernel(const XWArgs a) {
     const int m0 = mt + m4 * 4;
     if constexpr (VEC == 4) {
       if (part == 0) {
-        s_mt[st] = mt;
         if (dact) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const int off = (m0 + r < me && dn < a.Cout) ? ((m0 + r) * a.Cout + dn) * 4 : kOOB;
-            const float4 v = bload4(rD, off);
+            const float4 v = bload4(rD, (m0 + r < me && dn < a.Cout) ? ((m0 + r) * a.Cout + dn) * 4 : kOOB);
             dv[st][r][0] = v.x; dv[st][r][1] = v.y; dv[st][r][2] = v.z; dv[st][r][3] = v.w;
-            if constexpr (DLZ) {
-              const float4 u = bload4(rY, off);
-              yv[st][r][0] = u.x; yv[st][r][1] = u.y; yv[st][r][2] = u.z; yv[st][r][3] = u.w;
-            }
           }
         }
         return;
@@ -1431,14 +1408,10 @@ __global__ __launch_bounds__(256) void xwgrad_kernel(const XWArgs a) {
         const int m = m0 + r;
         const bool mv = m < me;
         if (part == 0) {
-          s_mt[st] = mt;
           if (dact) {
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              const int off = (mv && dn + e < a.Cout) ? (m * a.Cout + dn + e) * 4 : kOOB;
-              dv[st][r][e] = bload1(rD, off);
-              if constexpr (DLZ) yv[st][r][e] = bload1(rY, off);
-            }
+            for (int e = 0; e < 4; ++e)
+              dv[st][r][e] = bload1(rD, (mv && dn + e < a.Cout) ? (m * a.Cout + dn + e) * 4 : kOOB);
           }
           continue;
         }
@@ -1470,26 +1443,9 @@ __global__ __launch_bounds__(256) void xwgrad_kernel(const XWArgs a) {
   // piece q of stage st -> LDS buffer buf: q < 4 transposes dy column e = q, q >= 4 x column q-4
   HScale hs;
   if constexpr (H) hs.init(amax_read(a.amax_dy, a.amax_dy_ld, g), amax_read(a.amax_x, a.amax_x_ld, g));
-  const bool dy_store = DLZ && a.dy_out != nullptr && tk == 0;
-  float* __restrict__ dyo = DLZ && a.dy_out ? a.dy_out + (long long)g * a.dy_gstride : nullptr;
   auto lput_q = [&](int buf, int st, int q) __attribute__((always_inline)) {
     uint4* L = lds + buf * P * PL;
     uint2 sp[P];
-    if constexpr (DLZ) {
-      if (q == 0 && dact) {   // dy of the stage's 4 x 4 micro tile (0 past the rows / channels)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int m = s_mt[st] + m4 * 4 + r;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const bool ok = m < me && dn + e < a.Cout;
-            const float v = fmaf(cA[e], dv[st][r][e], fmaf(cB[e], yv[st][r][e], cK[e]));
-            dv[st][r][e] = ok ? v : 0.f;
-            if (dy_store && ok) dyo[(long long)m * a.Cout + dn + e] = v;
-          }
-        }
-      }
-    }
     if constexpr (XLZ) {
       if (q >= 4) {
         const int e = q - 4;
@@ -1837,82 +1793,59 @@ __global__ __launch_bounds__(256) void xcolsum_kernel(const float* __restrict__ 
 }
 
 // ===================================================== fused training BN: standalone pass
-// One block per (super group, replica) over a MATERIALISED tensor, for the producers whose
-// epilogue cannot reduce (the separate split-K reduce of multi-replica launches, stride-s data
-// gradients, the global average pool's gradient, max-pool gradients): the same level-0 records
-// in the same order as bnf_tile_records, summed into the SG record in group order, then the
-// replica ticket (bnfuse.hpp).  mode 1: statistics of src; mode 2: d = mask(g) -> dst (may alias
-// src), g = src or, with pool, pool[g][img][c] * pool_scale (the global average pool's gradient,
-// elementwise.hip avgpool_bwd's value).
-__global__ __launch_bounds__(256) void bnx_rows_kernel(const BnFuse f, const float* __restrict__ src, float* dst,
-                                                       long long gstride, const int* __restrict__ nvalid, int N, int HW,
-                                                       const float* __restrict__ pool, float pool_scale) {
-  __shared__ double rec[kBnGpS][64][4];   // one 64-channel chunk of the SG's group records
-  const int s = blockIdx.x, g = blockIdx.y, tid = threadIdx.x;
+// A tile pass over a MATERIALISED tensor, for the producers whose epilogue cannot reduce: the
+// split-K slabs of multi-replica launches (summed here in z order, xsplitk_reduce's order, plus
+// the dgrad's accumulated branch), stride-s data gradients, the global average pool's gradient,
+// max-pool gradients.  Same 128-row tiles of whole groups, same level-0 records
+// (bnf_tile_records) and finalize launch as the conv epilogues, so the statistics are
+// the same bits whichever kernel produced them.  mode 1: statistics of the value (stored to dst
+// when dst is given); mode 2: d = mask(value) -> dst (may alias src).  value = src, or the sum of
+// S slabs ws[z] (+ accum), or pool[g][img][c] * pool_scale (elementwise.hip avgpool_bwd's value).
+__global__ __launch_bounds__(256) void bnx_tile_kernel(const BnFuse f, const float* src, float* dst,
+                                                       long long gstride, const int* __restrict__ nvalid, int N,
+                                                       int HW, const float* __restrict__ pool, float pool_scale,
+                                                       const float* __restrict__ ws, int S, long long zstride,
+                                                       const float* __restrict__ accum) {
+  constexpr int BM = 128, BN = 64, C4 = BN / 4;
+  __shared__ __attribute__((aligned(16))) float Ct[BM * BN];
+  __shared__ long long orow[BM];
+  const int g = blockIdx.y, tid = threadIdx.x, C = f.C;
+  const int tiles_n = ceil_div_d(C, BN);
+  const int tn = blockIdx.x % tiles_n, tm = blockIdx.x / tiles_n;
   const int Mv = valid_rows(nvalid, g, N) * HW;
-  const int r0 = s * kBnSg;
-  if (r0 >= Mv) return;
-  const int r1 = min(Mv, r0 + kBnSg);
-  const int C = f.C;
-  const float* sgp = pool ? nullptr : src + (long long)g * gstride;
-  float* dg = dst ? dst + (long long)g * gstride : nullptr;
-  const float* ya = f.mode == 2 && f.ya ? f.ya + (long long)g * gstride : nullptr;
-  const float* yb = f.mode == 2 && f.yb ? f.yb + (long long)g * gstride : nullptr;
-  const float* mo = f.mask_out ? f.mask_out + (long long)g * gstride : nullptr;
-  const float* ca = f.coef_a + (long long)g * kBnRows * C;
-  const float* cb = f.coef_b ? f.coef_b + (long long)g * kBnRows * C : nullptr;
-  const int ngv = ceil_div_d(r1 - r0, kBnGrp);
-  for (int c0 = 0; c0 < C; c0 += 64) {
-    const int cw = min(64, C - c0);
-    for (int e = tid; e < kBnGpS * 64; e += 256) {
-      const int j = e / 64, cc = e - j * 64, c = c0 + cc;
-      const int b0 = r0 + j * kBnGrp;
-      double a[4];
-      bnf_init(a, f.mode);
-      if (cc < cw && b0 < r1) {
-        if (f.mode == 1) {
-          for (int m = b0; m < min(r1, b0 + kBnGrp); ++m) {
-            const double v = (double)sgp[(long long)m * C + c];
-            a[0] += v;
-            a[1] = fma(v, v, a[1]);
-            a[2] = fmax(a[2], v);
-            a[3] = fmin(a[3], v);
-          }
-        } else {
-          const float ma = ca[kCMean * C + c], ia = ca[kCInv * C + c];
-          const float sc = ca[kCScale * C + c], sh = ca[kCShift * C + c];
-          const float mb = cb ? cb[kCMean * C + c] : 0.f, ib = cb ? cb[kCInv * C + c] : 0.f;
-          for (int m = b0; m < min(r1, b0 + kBnGrp); ++m) {
-            const long long o = (long long)m * C + c;
-            const float gv = pool ? pool[((long long)g * N + m / HW) * C + c] * pool_scale : sgp[o];
-            const float y = ya[o];
-            const bool keep = mo ? mo[o] > 0.f : (f.mask_lazy ? fmaf(y, sc, sh) > 0.f : true);
-            const float d = keep ? gv : 0.f;
-            dg[o] = d;
-            a[0] += (double)d;
-            a[1] = fma((double)d, (double)((y - ma) * ia), a[1]);
-            if (yb) a[2] = fma((double)d, (double)((yb[o] - mb) * ib), a[2]);
-            a[3] = fmax(a[3], (double)fabsf(d));
-          }
+  const int m0 = tm * BM, n0 = tn * BN;
+  if (m0 >= Mv) return;
+  if (tid < BM) orow[tid] = m0 + tid < Mv ? (long long)(m0 + tid) * C : -1;
+  __syncthreads();
+  const long long base = (long long)g * gstride;
+  for (int e = tid; e < BM * C4; e += 256) {
+    const int row = e / C4, cc = (e - row * C4) * 4, n = n0 + cc;
+    const long long o = orow[row];
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (o >= 0 && n < C) {
+      if (ws) {
+        v = *(const float4*)(ws + base + o + n);
+        for (int z = 1; z < S; ++z) {
+          const float4 u = *(const float4*)(ws + z * zstride + base + o + n);
+          v.x += u.x; v.y += u.y; v.z += u.z; v.w += u.w;
         }
+      } else if (pool) {
+        const float4 u = *(const float4*)(pool + ((long long)g * N + (m0 + row) / HW) * C + n);
+        v = make_float4(u.x * pool_scale, u.y * pool_scale, u.z * pool_scale, u.w * pool_scale);
+      } else {
+        v = *(const float4*)(src + base + o + n);
       }
-#pragma unroll
-      for (int k = 0; k < 4; ++k) rec[j][cc][k] = a[k];
-    }
-    __syncthreads();
-    if (tid < cw) {
-      double a[4];
-      bnf_init(a, f.mode);
-      for (int j = 0; j < ngv; ++j) {
-        const double v[4] = {rec[j][tid][0], rec[j][tid][1], rec[j][tid][2], rec[j][tid][3]};
-        bnf_acc(a, v, f.mode);
+      if (accum) {
+        const float4 r = *(const float4*)(accum + base + o + n);
+        v.x += r.x; v.y += r.y; v.z += r.z; v.w += r.w;
       }
-      bnf_store_rec(f.rec1, ((long long)g * f.nsg + s) * C + c0 + tid, 0, a[0], a[1], a[2], a[3]);
+      if (f.mode == 2) v = bnf_mask4(f, g, o, n, v);
+      if (dst) *(float4*)(dst + base + o + n) = v;
     }
-    __syncthreads();
+    *(float4*)&Ct[row * BN + cc] = v;
   }
-  const int nsg_v = ceil_div_d(Mv, kBnSg);
-  if (bnf_arrive(f.cnt2 + g, nsg_v)) bnf_finalize_replica(f, g, nsg_v, (double)Mv);
+  __syncthreads();
+  bnf_tile_records<BM, BN>(f, Ct, orow, g, m0, n0, Mv);
 }
 
 // The materialised output of a training BN (+ residual) (+ ReLU) (bnfuse.hpp): out =
@@ -1956,12 +1889,44 @@ __global__ __launch_bounds__(256) void bnx_apply_kernel(const float* __restrict_
   if (amax) amax_fold(amax, amax_ld, g, vmax);
 }
 
+// The input gradient of a training BN, stored: dy = fma(A, d, fma(B, y, K)) per channel
+// (bnfuse.hpp; bn.hip bn_bwd_apply's arithmetic) over the valid rows, and the max |dy| slot
+// folded for its fp16-pair consumers (DBA_BNX_DY=1: instead of the weight gradient staging dy
+// from (d, y) on the fly).
+__global__ __launch_bounds__(256) void bnx_dy_kernel(const float* __restrict__ d, const float* __restrict__ y,
+                                                     const float* __restrict__ coef, float* __restrict__ dy,
+                                                     long long gstride, const int* __restrict__ nvalid, int N, int HW,
+                                                     int C, int* __restrict__ amax, int amax_ld) {
+  const int g = blockIdx.y;
+  const int C4 = C >> 2;
+  const long long total = (long long)valid_rows(nvalid, g, N) * HW * C4;
+  const long long base = (long long)g * gstride;
+  const float* cf = coef + (long long)g * kBnRows * C;
+  float vmax = 0.f;
+  for (long long t = blockIdx.x * 256LL + threadIdx.x; t < total; t += (long long)gridDim.x * 256) {
+    const int c = (int)(t % C4) * 4;
+    const long long o = base + t * 4;
+    const float4 dv = *(const float4*)(d + o), yv = *(const float4*)(y + o);
+    const float4 A = *(const float4*)(cf + kCA * C + c), B = *(const float4*)(cf + kCB * C + c),
+                 K = *(const float4*)(cf + kCK * C + c);
+    const float4 v = make_float4(fmaf(A.x, dv.x, fmaf(B.x, yv.x, K.x)), fmaf(A.y, dv.y, fmaf(B.y, yv.y, K.y)),
+                                 fmaf(A.z, dv.z, fmaf(B.z, yv.z, K.z)), fmaf(A.w, dv.w, fmaf(B.w, yv.w, K.w)));
+    vmax = fmaxf(vmax, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+    *(float4*)(dy + o) = v;
+  }
+  if (amax) amax_fold(amax, amax_ld, g, vmax);
+}
+
 // ============================================================================ host
-int bnx_rows_go(const BnFuse& f, const float* src, float* dst, long long gstride, const int* nvalid, int G, int N,
-                int HW, const float* pool, float pool_scale, hipStream_t st) {
-  const dim3 grid((unsigned)ceil_div((long long)N * HW, kBnSg), G);
-  hipLaunchKernelGGL(bnx_rows_kernel, grid, dim3(256), 0, st, f, src, dst, gstride, nvalid, N, HW, pool, pool_scale);
-  DBA_LAUNCH_CHECK();
+int bnx_tile_go(const BnFuse& f, const float* src, float* dst, long long gstride, const int* nvalid, int G, int N,
+                int HW, const float* pool, float pool_scale, const float* ws, int S, long long zstride,
+                const float* accum, hipStream_t st) {
+  if (f.C & 3) return -102;
+  const dim3 grid((unsigned)(ceil_div((long long)N * HW, 128) * ceil_div(f.C, 64)), G);
+  hipLaunchKernelGGL(bnx_tile_kernel, grid, dim3(256), 0, st, f, src, dst, gstride, nvalid, N, HW, pool, pool_scale, ws,
+                     S, zstride, accum);
+  const int rc = (int)hipGetLastError();
+  return rc != 0 ? rc : bnx_finalize_go(f, nvalid, G, N, HW, st);
 }
 
 int env_int(const char* name, int dflt) {
@@ -2266,9 +2231,11 @@ DBA_EXPORT int dba_xconv_fwd(const float* x, long long x_gstride, const float* w
     if (!amax_x || wp || pairs || vec < 4 || Cin > 512) return -108;
     a.lz_coef = lz_coef; a.lz_relu = lz_relu;
   }
+  // a fused BN's finalize launch follows its producer (bnx_tile_go launches its own)
+  auto fin = [&](int rc) { return (rc == 0 && a.bf.mode) ? bnx_finalize_go(a.bf, nvalid, G, N, Ho * Wo, st) : rc; };
   if (stride == 1) {
     const int rc = xhalo_try(a, G, KH, KW, st);
-    if (rc != -100) return rc;
+    if (rc != -100) return fin(rc);
   }
   const int s = pairs ? 1 : xsplitk(M, G, Cout, K);
   const bool ws_ok = s > 1 && ws != nullptr && ws_floats >= (long long)s * G * M * Cout;
@@ -2278,7 +2245,7 @@ DBA_EXPORT int dba_xconv_fwd(const float* x, long long x_gstride, const float* w
     b.splitk = s;
     b.zstride = (long long)G * M * Cout;
     b.sk_ws = ws; b.sk_gstride = M * Cout; b.sk_cnt = sk_cnt;
-    return xconv_dispatch(b, M, G, 1, vec, st);
+    return fin(xconv_dispatch(b, M, G, 1, vec, st));
   }
   if (bnpart && s > 1) return -106;   // separate reduce launch: BN statistics by the BN kernels
   if (ws_ok) {
@@ -2289,18 +2256,16 @@ DBA_EXPORT int dba_xconv_fwd(const float* x, long long x_gstride, const float* w
     b.zstride = (long long)G * M * Cout;
     const int rc = xconv_dispatch(b, M, G, 1, vec, st);
     if (rc != 0) return rc;
+    if (a.bf.mode)   // the slabs summed + the statistics in one pass, the epilogue's records (bnfuse.hpp)
+      return bnx_tile_go(a.bf, nullptr, out, out_gstride, nvalid, G, N, Ho * Wo, nullptr, 0.f, ws, s, b.zstride,
+                         nullptr, st);
     const long long per = M * Cout;
     const dim3 grid((unsigned)std::max(1LL, std::min(1024LL, (per + 255) / 256)), G);
     hipLaunchKernelGGL(xsplitk_reduce_kernel, grid, dim3(256), 0, st, (const float*)ws, s, b.zstride, per, nvalid, N,
                        Ho * Wo, Cout, bias, b_sstride, wsel, res, relu, out, amax_out, amax_out_ld);
-    if (a.bf.mode) {   // the statistics from the reduced output, same records (bnfuse.hpp)
-      const int rc = (int)hipGetLastError();
-      if (rc != 0) return rc;
-      return bnx_rows_go(a.bf, out, nullptr, out_gstride, nvalid, G, N, Ho * Wo, nullptr, 0.f, st);
-    }
     DBA_LAUNCH_CHECK();
   }
-  return xconv_dispatch(a, M, G, 1, vec, st);
+  return fin(xconv_dispatch(a, M, G, 1, vec, st));
 }
 
 // dX of a conv from class-packed transposed weights (dba_xtranspose); accum (optional) is
@@ -2332,9 +2297,10 @@ DBA_EXPORT int dba_xconv_dgrad(const float* dy, long long dy_gstride, const floa
     a.cls[i] = cg.c[i];
     Mmax = std::max(Mmax, (long long)N * cg.c[i].Hq * cg.c[i].Wq);
   }
+  auto fin = [&](int rc) { return (rc == 0 && a.bf.mode) ? bnx_finalize_go(a.bf, nvalid, G, N, H * W, st) : rc; };
   if (stride == 1) {
     const int rc = xhalo_try(a, G, KH, KW, st);
-    if (rc != -100) return rc;
+    if (rc != -100) return fin(rc);
     const long long M = (long long)N * H * W;
     const int s = xsplitk(M, G, Cin, KH * KW * Cout);
     const bool ws_ok = s > 1 && ws != nullptr && ws_floats >= (long long)s * G * M * Cin;
@@ -2343,7 +2309,7 @@ DBA_EXPORT int dba_xconv_dgrad(const float* dy, long long dy_gstride, const floa
       b.splitk = s;
       b.zstride = (long long)G * M * Cin;
       b.sk_ws = ws; b.sk_gstride = M * Cin; b.sk_cnt = sk_cnt;
-      return xconv_dispatch(b, M, G, 1, vec, st);
+      return fin(xconv_dispatch(b, M, G, 1, vec, st));
     }
     if (ws_ok) {
       XArgs b = a;
@@ -2353,19 +2319,17 @@ DBA_EXPORT int dba_xconv_dgrad(const float* dy, long long dy_gstride, const floa
       b.zstride = (long long)G * M * Cin;
       const int rc = xconv_dispatch(b, M, G, 1, vec, st);
       if (rc != 0) return rc;
+      if (a.bf.mode)   // slabs + accum summed, masked and reduced in one pass (bnfuse.hpp)
+        return bnx_tile_go(a.bf, nullptr, dx, dx_gstride, nvalid, G, N, H * W, nullptr, 0.f, ws, s, b.zstride, accum,
+                           st);
       const long long per = M * Cin;
       const dim3 grid((unsigned)std::max(1LL, std::min(1024LL, (per + 255) / 256)), G);
       hipLaunchKernelGGL(xsplitk_reduce_kernel, grid, dim3(256), 0, st, (const float*)ws, s, b.zstride, per, nvalid,
                          N, H * W, Cin, nullptr, 0LL, wsel, accum, 0, dx, (int*)nullptr, 0);
-      if (a.bf.mode) {   // mask + reduce the reduced gradient in place, same records (bnfuse.hpp)
-        const int rc = (int)hipGetLastError();
-        if (rc != 0) return rc;
-        return bnx_rows_go(a.bf, dx, dx, dx_gstride, nvalid, G, N, H * W, nullptr, 0.f, st);
-      }
       DBA_LAUNCH_CHECK();
     }
   }
-  return xconv_dispatch(a, Mmax, G, cg.n, vec, st);
+  return fin(xconv_dispatch(a, Mmax, G, cg.n, vec, st));
 }
 
 // class-packed data-gradient weights for n convs.  desc: n x XTDesc in HOST memory, read
@@ -2411,11 +2375,9 @@ DBA_EXPORT int dba_xwgrad(const float* dy, long long dy_gstride, const float* x,
                           long long dw_gstride, const int* nvalid, int G, int N, int H, int W, int Cin, int Ho,
                           int Wo, int Cout, int KH, int KW, int stride, int pad, const int* amax_dy,
                           int amax_dy_ld, const int* amax_x, int amax_x_ld, float* ws, long long ws_floats, int defer,
-                          const float* dy_y, const float* dy_coef, float* dy_out, const float* x_coef, int x_relu,
-                          void* stream) {
+                          const float* x_coef, int x_relu, void* stream) {
   hipStream_t st = (hipStream_t)stream;
-  if ((dy_y || x_coef) && !amax_dy) return -108;   // lazy BN operands: fp16-pair launches only
-  if (dy_y && !dy_coef) return -108;
+  if (x_coef && !amax_dy) return -108;   // lazy BN operand: fp16-pair launches only
   int mchunk = 0;
   const long long need = dba_xwgrad_ws_floats(G, N, Ho, Wo, Cin, Cout, KH, KW, &mchunk);
   if (need > 0 && (ws == nullptr || ws_floats < need)) return -101;
@@ -2428,7 +2390,7 @@ DBA_EXPORT int dba_xwgrad(const float* dy, long long dy_gstride, const float* x,
   a.mchunk = mchunk;
   a.amax_dy = amax_dy; a.amax_x = amax_x;
   a.amax_dy_ld = amax_dy_ld; a.amax_x_ld = amax_x_ld;
-  a.dy_y = dy_y; a.dy_coef = dy_coef; a.dy_out = dy_out; a.x_coef = x_coef; a.x_relu = x_relu;
+  a.x_coef = x_coef; a.x_relu = x_relu;
   a.dHoWo = FDiv{Ho * Wo, 1.0f / (float)(Ho * Wo)};
   a.dWo = FDiv{Wo, 1.0f / (float)Wo};
   a.tiles_k = ceil_div(a.K, 128);
@@ -2444,26 +2406,22 @@ DBA_EXPORT int dba_xwgrad(const float* dy, long long dy_gstride, const float* x,
   int bno = Cout <= 32 ? 32 : Cout <= 64 ? 64 : 128;
   if (bno == 128 && (long long)ceil_div(Cout, 128) * a.tiles_k * G * Z < bno64_below) bno = 64;
   const dim3 grid((unsigned)(ceil_div(Cout, bno) * a.tiles_k), G, Z);
-#define XW_GO(BNO_, WN__, WK__, P_, V_, H_, D_, X_) \
-  hipLaunchKernelGGL((xwgrad_kernel<BNO_, 128, WN__, WK__, P_, V_, H_, D_, X_>), grid, dim3(256), 0, st, a)
-#define XW_P(P_, V_, H_, D_, X_)                                  \
-  do {                                                            \
-    if (bno == 32) XW_GO(32, 1, 4, P_, V_, H_, D_, X_);           \
-    else if (bno == 64) XW_GO(64, 2, 2, P_, V_, H_, D_, X_);      \
-    else XW_GO(128, 2, 2, P_, V_, H_, D_, X_);                    \
+#define XW_GO(BNO_, WN__, WK__, P_, V_, H_, X_) \
+  hipLaunchKernelGGL((xwgrad_kernel<BNO_, 128, WN__, WK__, P_, V_, H_, X_>), grid, dim3(256), 0, st, a)
+#define XW_P(P_, V_, H_, X_)                                  \
+  do {                                                        \
+    if (bno == 32) XW_GO(32, 1, 4, P_, V_, H_, X_);           \
+    else if (bno == 64) XW_GO(64, 2, 2, P_, V_, H_, X_);      \
+    else XW_GO(128, 2, 2, P_, V_, H_, X_);                    \
   } while (0)
-  if (amax_dy && dy_y && x_coef) {
-    if (v4) XW_P(2, 4, true, true, true); else XW_P(2, 1, true, true, true);
-  } else if (amax_dy && dy_y) {
-    if (v4) XW_P(2, 4, true, true, false); else XW_P(2, 1, true, true, false);
-  } else if (amax_dy && x_coef) {
-    if (v4) XW_P(2, 4, true, false, true); else XW_P(2, 1, true, false, true);
+  if (amax_dy && x_coef) {
+    if (v4) XW_P(2, 4, true, true); else XW_P(2, 1, true, true);
   } else if (amax_dy) {
-    if (v4) XW_P(2, 4, true, false, false); else XW_P(2, 1, true, false, false);
+    if (v4) XW_P(2, 4, true, false); else XW_P(2, 1, true, false);
   } else if (planes() == 2) {
-    if (v4) XW_P(2, 4, false, false, false); else XW_P(2, 1, false, false, false);
+    if (v4) XW_P(2, 4, false, false); else XW_P(2, 1, false, false);
   } else {
-    if (v4) XW_P(3, 4, false, false, false); else XW_P(3, 1, false, false, false);
+    if (v4) XW_P(3, 4, false, false); else XW_P(3, 1, false, false);
   }
 #undef XW_P
 #undef XW_GO
@@ -2546,13 +2504,14 @@ DBA_EXPORT int dba_xwgrad_reduce_batch(const void* desc, int n, int Gmax, long l
   return 0;
 }
 
-// the fused-BN standalone pass (bnx_rows_kernel) over a materialised tensor; bnf: a BnFuse in
-// host memory (passed by value: graph-capture safe)
+// the fused-BN standalone pass (bnx_tile_kernel) over a materialised tensor or a pooled gradient;
+// bnf: a BnFuse in host memory (passed by value: graph-capture safe)
 DBA_EXPORT int dba_bnx_rows(const void* bnf, const float* src, float* dst, long long gstride, const int* nvalid, int G,
                             int N, int HW, const float* pool, float pool_scale, void* stream) {
   const BnFuse f = *(const BnFuse*)bnf;
   if (f.mode < 1 || f.mode > 2 || (f.mode == 2 && (!dst || !f.ya))) return -108;
-  return bnx_rows_go(f, src, dst, gstride, nvalid, G, N, HW, pool, pool_scale, (hipStream_t)stream);
+  return bnx_tile_go(f, src, dst, gstride, nvalid, G, N, HW, pool, pool_scale, nullptr, 1, 0, nullptr,
+                     (hipStream_t)stream);
 }
 
 // sizeof(BnFuse) (the Python ctypes mirror checks its layout against it)
@@ -2568,5 +2527,16 @@ DBA_EXPORT int dba_bnx_apply(const float* ya, const float* ca, const float* res,
   hipLaunchKernelGGL(bnx_apply_kernel, grid, dim3(256), 0, (hipStream_t)stream, ya, ca, res, yb, cb, relu_b, relu, out,
                      gstride,
                      nvalid, N, HW, C, amax, amax_ld);
+  DBA_LAUNCH_CHECK();
+}
+
+DBA_EXPORT int dba_bnx_dy(const float* d, const float* y, const float* coef, float* dy, long long gstride,
+                          const int* nvalid, int G, int N, int HW, int C, int* amax, int amax_ld, void* stream) {
+  if (C & 3) return -102;
+  const long long per = (long long)N * HW * (C / 4);
+  const long long cap = std::max(1LL, 8192LL / std::max(1, G));
+  const dim3 grid((unsigned)std::max(1LL, std::min(cap, (per + 255) / 256)), G);
+  hipLaunchKernelGGL(bnx_dy_kernel, grid, dim3(256), 0, (hipStream_t)stream, d, y, coef, dy, gstride, nvalid, N, HW, C,
+                     amax, amax_ld);
   DBA_LAUNCH_CHECK();
 }

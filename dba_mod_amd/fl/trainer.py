@@ -35,11 +35,10 @@ from .workload import Workload
 
 log = logging.getLogger("logger")
 
-# arrival counters per training step for the in-launch split-K combines of the fp32 convs and the
-# fused training-BN tickets (bnfuse.hpp: G x (super groups + 1) per BN pass)
+# arrival counters per training step for the in-launch split-K combines of the fp32 convs
 # (xgemm.hip sk_combine, lone-client launches): a ResNet-18 step needs 14 launches x <= 128;
 # zeroed with the step's operand-max arena (no extra launch).  0: separate reduce launches
-SK_COUNTERS = int(os.environ.get("DBA_SK_COUNTERS", str(1 << 16)))
+SK_COUNTERS = int(os.environ.get("DBA_SK_COUNTERS", str(1 << 15)))
 
 
 @dataclass

@@ -32,6 +32,9 @@ from .mirror import CIFAR_RESNETS
 from .spec import ModelSpec
 
 Tensor = torch.Tensor
+# DBA_BNX_LAZY=0: training BN+ReLU outputs are stored by an apply pass instead of being applied
+# by their consuming convs (A/B of the lazy operands)
+_LAZY_BN = os.environ.get("DBA_BNX_LAZY", "1") != "0"
 BN_EPS = 1e-5
 BN_MOMENTUM = 0.1
 
@@ -248,6 +251,13 @@ class Ctx:
         w = self.w(conv)
         y, st = ops.conv_bn_stats(x, w, self.wsel, stride, pad, self.nvalid, self._bnp(bn), relu)
         a = bs.LazyBN(y, st, relu)
+        if relu and not _LAZY_BN:   # DBA_BNX_LAZY=0: BN+ReLU outputs stored (A/B of the lazy operands)
+            self.tape.record((a,), (x,), self._bn_conv_bwd(x, w, y, st, conv, stride, pad))
+            return self.bn_out(a, None, relu=True, lazy_relu=True)
+        self.tape.record((a,), (x,), self._bn_conv_bwd(x, w, y, st, conv, stride, pad))
+        return a
+
+    def _bn_conv_bwd(self, x, w, y, st, conv: str, stride: int, pad: int):
         in_hw = (x.shape[2], x.shape[3])
         kh, kw = w.shape[2], w.shape[3]
         need_dx = self.tape.needs_grad(x)
@@ -263,16 +273,15 @@ class Ctx:
             fin = self.tape.finish_spec(x) if self.tape.is_last(x) else None
             return (ops.conv2d_dgrad(dy, w, self.wsel, stride, pad, in_hw, nvalid=self.nvalid, accum=acc,
                                      wt=self._wt.get(k), finish=fin),)
+        return bwd
 
-        self.tape.record((a,), (x,), bwd)
-        return a
-
-    def bn_out(self, a, residual=None, relu: bool = True) -> Tensor:
+    def bn_out(self, a, residual=None, relu: bool = True, lazy_relu: bool = False) -> Tensor:
         """Training: the stored output relu?(BN(a) + residual) of a block (one pass); ``a`` a
         lazy BN output without ReLU, ``residual`` a tensor, a lazy BN output or None.  Its
         gradient is finished (ReLU mask, the sums of a's BN and of a residual BN branch) by
         whoever produces it last."""
-        out = ops.bn_apply(a, residual, relu, self.nvalid)
+        # lazy_relu: ``a`` is a BN+ReLU output stored here (its affine form, the ReLU below)
+        out = ops.bn_apply(bs.LazyBN(a.y, a.stat, False) if lazy_relu else a, residual, relu, self.nvalid)
         branch = isinstance(residual, bs.LazyBN) and not residual.relu
         out._dba_finish = bs.Finish(ya=a.y, sa=a.stat, mask_out=out if relu else None,
                                     yb=residual.y if branch else None, sb=residual.stat if branch else None)

@@ -53,11 +53,13 @@ class BranchReplay:
             if relu:
                 C = y.shape[-1]
                 sh = (y.shape[0],) + (1,) * (y.dim() - 2) + (C,)
-                pre = y * st.coef[:, 2].reshape(sh).to(y.dtype) + st.coef[:, 3].reshape(sh).to(y.dtype)
+                # fp64: the exact sign of y * scale + shift, which is the sign of the kernels'
+                # fmaf (a correctly rounded fma never crosses zero); fp32 mul-then-add can
+                pre = (y.double() * st.coef[:, 2].reshape(sh).double() + st.coef[:, 3].reshape(sh).double())
                 if not self.replay:
                     self.rec.append((pre > 0).cpu())
                 else:
-                    st.relu_mask = self._decide(pre)
+                    st.relu_mask = self._decide(pre.to(y.dtype) if y.dtype == torch.float64 else pre)
             return y, st
 
         def bn_apply(a, residual, relu, nvalid=None):

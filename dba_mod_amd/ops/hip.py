@@ -91,11 +91,12 @@ _SIGS = {
     "dba_amax": [_P, _LL, _LL, _P, _LL, _I, _P, _I, _P],
     "dba_xtranspose": [_P, _I, _I, _LL, _P, _P],
     "dba_xwgrad_ws_floats": [_I] * 8 + [_P],
-    "dba_xwgrad": [_P, _LL, _P, _LL, _P, _LL, _P] + [_I] * 12 + [_P, _I] * 2 + [_P, _LL, _I] + [_P] * 4 + [_I, _P],
+    "dba_xwgrad": [_P, _LL, _P, _LL, _P, _LL, _P] + [_I] * 12 + [_P, _I] * 2 + [_P, _LL, _I] + [_P, _I, _P],
     # fused training BN (csrc/kernels/bnfuse.hpp)
     "dba_bnx_rows": [_P, _P, _P, _LL, _P, _I, _I, _I, _P, _F, _P],
     "dba_bnx_apply": [_P, _P, _P, _P, _P, _I, _I, _P, _LL, _P, _I, _I, _I, _I, _P, _I, _P],
     "dba_bnfuse_size": [],
+    "dba_bnx_dy": [_P, _P, _P, _P, _LL, _P, _I, _I, _I, _I, _P, _I, _P],
     "dba_xwgrad_reduce_batch": [_P, _I, _I, _LL, _P],
     # image stems in exact fp32 (csrc/kernels/stem.hip)
     "dba_xstem_fwd": [_P, _LL, _P, _LL, _P, _P, _LL, _P, _P, _LL, _P] + [_I] * 13 + [_P, _I, _P, _P, _I, _P, _P, _P, _P],
@@ -114,8 +115,8 @@ _MODE = int(_L.dba_xgemm_set_planes(0))   # fp32 split mode (0: query only; DBA_
 class _BnFuse(ctypes.Structure):
     """Mirror of csrc/kernels/bnfuse.hpp ``BnFuse`` (passed by host pointer, copied by value
     into the kernel arguments at launch: graph-capture safe)."""
-    _fields_ = [("mode", _I), ("C", _I), ("ngrp", _I), ("nsg", _I),
-                ("rec0", _P), ("rec1", _P), ("cnt1", _P), ("cnt2", _P),
+    _fields_ = [("mode", _I), ("C", _I), ("ngrp", _I),
+                ("rec0", _P),
                 ("coef_a", _P), ("gamma_a", _P), ("beta_a", _P), ("rm_a", _P), ("rv_a", _P),
                 ("p_gstride", _LL), ("momentum", _F), ("eps", _F), ("relu", _I),
                 ("amax_a", _P), ("amax_ld", _I),
@@ -845,19 +846,18 @@ def conv2d_wgrad(dy, x, stride, pad, kh, kw, dw, dbias=None, nvalid=None, defer=
     ``LazyGrad`` (a training BN's input gradient, staged from (d, y); its value is stored once
     and returned for the data gradient) and ``x`` a ``LazyBN`` (a training BN's output, staged
     from y)."""
-    lg = dy if isinstance(dy, bs.LazyGrad) else None
+    if isinstance(dy, bs.LazyGrad):
+        # the BN input gradient stored by one elementwise pass (bnx_dy_kernel; staging it from
+        # (d, y) in the weight gradient was slower: profiles/r4/bnx/ab_steps.md), then the plain
+        # weight gradient; returned for the data gradient
+        dy = _bnx_dy(dy, nvalid)
+        conv2d_wgrad(dy, x, stride, pad, kh, kw, dw, dbias, nvalid, defer)
+        return dy
     lx = x if isinstance(x, bs.LazyBN) else None
-    dy = _act(lg.d if lg is not None else dy, None, "wgrad dy")
+    dy = _act(dy, None, "wgrad dy")
     x = _act(lx.y if lx is not None else x, dy.dtype, "wgrad x")
-    dy_out = None
-    if lg is not None or lx is not None:
-        if dy.dtype != _F32 or _MODE != F16_PAIR or "wgrad" not in _H_OPS or dbias is not None:
-            raise RuntimeError("fused training BN: fp32 family, fp16-pair weight gradient, no bias")
-        if lg is not None:
-            y_ = _act(lg.y, _F32, "wgrad BN input")
-            assert y_.shape == dy.shape and y_.stride(0) == dy.stride(0)
-            dy_out = torch.empty_like(dy)
-            dy_out._dba_amax = lg.stat.dbound
+    if lx is not None and (dy.dtype != _F32 or _MODE != F16_PAIR or "wgrad" not in _H_OPS):
+        raise RuntimeError("fused training BN: fp32 family, fp16-pair weight gradient")
     G, N, Ho, Wo, Cout = dy.shape
     _, _, H, W, Cin = x.shape
     assert dw.dtype == torch.float32 and _inner_contig(dw)
@@ -868,12 +868,11 @@ def conv2d_wgrad(dy, x, stride, pad, kh, kw, dw, dbias=None, nvalid=None, defer=
         nv = _i32(nvalid)
         ad = ax = None
         if _MODE == F16_PAIR and "wgrad" in _H_OPS:
-            ad = lg.stat.dbound if lg is not None else _amax_act(dy, nvalid)
+            ad = _amax_act(dy, nvalid)
             ax = lx.stat.bound if lx is not None else _amax_act(x, nvalid)
         _call("dba_xwgrad", dy.data_ptr(), N * Ho * Wo * Cout, x.data_ptr(), N * H * W * Cin, dw.data_ptr(),
               dw.stride(0), _ptr(nv), G, N, H, W, Cin, Ho, Wo, Cout, kh, kw, stride, pad, *_aptr(ad), *_aptr(ax),
               _ptr(wsb), n, int(defer is not None and n > 0),
-              _ptr(lg.y) if lg is not None else None, _ptr(lg.stat.coef) if lg is not None else None, _ptr(dy_out),
               _ptr(lx.stat.coef) if lx is not None else None, int(lx.relu) if lx is not None else 0, _stream())
         if defer is not None and n > 0:
             per = Cout * kh * kw * Cin
@@ -884,7 +883,7 @@ def conv2d_wgrad(dy, x, stride, pad, kh, kw, dw, dbias=None, nvalid=None, defer=
             assert dbias.dtype == torch.float32 and dbias.stride(1) == 1
             _call("dba_xcolsum", dy.data_ptr(), N * Ho * Wo * Cout, Ho * Wo, _ptr(_i32(nvalid)), G, N, Cout,
                   dbias.data_ptr(), dbias.stride(0), _stream())
-        return dy_out
+        return None
     rc = NOT_HANDLED
     if _PCONV and stride == 1 and kh == 3 and kw == 3 and pad == 1 and H == W and Ho == H:
         # halo-tiled transposed-read wgrad (csrc/kernels/pwgrad.hip)
@@ -905,25 +904,13 @@ def conv2d_wgrad(dy, x, stride, pad, kh, kw, dw, dbias=None, nvalid=None, defer=
 
 
 # ------------------------------------------------------------ fused training BN (bnfuse.hpp)
-def _bn_workspace(G: int, M: int, C: int, device):
-    """Level-0 / level-1 records and the zeroed tickets of one fused BN pass (M rows per
-    replica): the counters come from the step's arena (no fill launch) when it has room."""
-    ngrp, nsg = (M + 31) // 32, (M + 511) // 512
-    rec0 = torch.empty(G * ngrp * C * 4, dtype=torch.float64, device=device)
-    rec1 = torch.empty(G * nsg * C * 4, dtype=torch.float64, device=device)
-    cnt = _sk_counters(G * nsg + G, device)
-    if cnt is None:
-        cnt = torch.zeros(G * nsg + G, dtype=torch.int32, device=device)
-    return ngrp, nsg, rec0, rec1, cnt
-
-
 def _bnf_common(mode: int, G: int, M: int, C: int, device):
-    ngrp, nsg, rec0, rec1, cnt = _bn_workspace(G, M, C, device)
+    """A fused BN pass (bnfuse.hpp) over M rows per replica: its level-0 record workspace."""
+    ngrp = (M + 31) // 32
+    rec0 = torch.empty(G * C * ngrp * 4, dtype=torch.float64, device=device)
     f = _BnFuse()
-    f.mode, f.C, f.ngrp, f.nsg = mode, C, ngrp, nsg
-    f.rec0, f.rec1 = rec0.data_ptr(), rec1.data_ptr()
-    f.cnt1, f.cnt2 = cnt.data_ptr(), cnt.data_ptr() + 4 * G * nsg
-    f._keep = (rec0, rec1, cnt)   # alive until the launch has been enqueued
+    f.mode, f.C, f.ngrp, f.rec0 = mode, C, ngrp, rec0.data_ptr()
+    f._keep = (rec0,)   # alive until the launches have been enqueued
     return f
 
 
@@ -973,6 +960,20 @@ def _bnf_bwd(fin: "bs.Finish", G: int, M: int, device):
     f.mask_lazy = int(bool(fin.lazy))
     f._keep = f._keep + tuple(keep)
     return f
+
+
+def _bnx_dy(lg, nvalid):
+    """dy = A d + B y + K of a training BN's input, stored (its max slot: the finalize's bound)."""
+    d = _act(lg.d, _F32, "BN output gradient")
+    y = _act(lg.y, _F32, "BN input")
+    G, N, H, W, C = d.shape
+    assert y.shape == d.shape
+    dy = torch.empty_like(d)
+    am = lg.stat.dbound
+    _call("dba_bnx_dy", d.data_ptr(), y.data_ptr(), lg.stat.coef.data_ptr(), dy.data_ptr(), d.stride(0),
+          _ptr(_i32(nvalid)), G, N, H * W, C, *_aptr(None), _stream())
+    dy._dba_amax = am
+    return dy
 
 
 def conv_bn_stats(x, w, wsel, stride, pad, nvalid, p, relu):
