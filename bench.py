@@ -15,7 +15,7 @@ not shipped; the bench builds the equivalent starting point with ``--pretrain-ro
 Rounds then start at 201, so with the default ``--warmup 2`` the timed window 203..210
 contains all four poison rounds.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--dtype fp32|bf16]
+    python bench.py [--gpus N] [--steps K] [--warmup W]
     torchrun --nproc-per-node N bench.py --gpus N ...     # one rank per GPU over RCCL
     python bench.py --emulate-rank R --emulate-world N    # rank R's share of N, on one GPU
 
@@ -116,9 +116,8 @@ def _args(argv=None):
                          "pretrained checkpoint; untimed)")
     ap.add_argument("--start-epoch", type=int, default=None,
                     help="first (warmup) round; default: first poison round - warmup")
-    ap.add_argument("--dtype", choices=("fp32", "bf16"), default="fp32",
-                    help="compute precision: fp32 = the reference's (split-bf16 MFMA kernels, default); "
-                         "bf16 = fast mode (bf16 activations, fp32 master weights)")
+    ap.add_argument("--dtype", choices=("fp32",), default="fp32",
+                    help="compute precision: fp32, the reference's (fp32 operands split for the 16-bit MFMA)")
     ap.add_argument("--set", dest="overrides", nargs="*", default=[])
     ap.add_argument("--emulate-rank", type=int, default=None,
                     help="run only rank R's share of an --emulate-world N round on one device "

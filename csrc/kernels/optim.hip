@@ -2,8 +2,8 @@
 // flat [G, P] buffers of all concurrently-training clients in ONE launch, with per-client
 // learning rate (benign lr / poison lr with the MultiStepLR schedule), per-client
 // "fresh optimizer" flag (momentum buffer := d_p on its first step), per-client activity
-// mask, the FoolsGold raw-gradient accumulation (image_train.py:94-100) and the bf16 weight
-// shadow the MFMA kernels read — all in the same pass over the parameters.
+// mask and the FoolsGold raw-gradient accumulation (image_train.py:94-100), all in the same
+// pass over the parameters.
 #include "common.hpp"
 #include <algorithm>
 
@@ -13,7 +13,7 @@ __global__ __launch_bounds__(256) void sgd_kernel(float* __restrict__ params, lo
                                                   const float* __restrict__ grads, float* __restrict__ mom,
                                                   const float* __restrict__ lr, const int* __restrict__ first,
                                                   const int* __restrict__ active, float momentum, float wd,
-                                                  uint16_t* __restrict__ shadow, float* __restrict__ fg, int P) {
+                                                  float* __restrict__ fg, int P) {
   const int g = blockIdx.y;
   if (!active[g]) return;
   const float l = lr[g];
@@ -21,7 +21,6 @@ __global__ __launch_bounds__(256) void sgd_kernel(float* __restrict__ params, lo
   float* p = params + (long long)g * p_gstride;
   const float* gr = grads + (long long)g * P;
   float* m = mom + (long long)g * P;
-  uint16_t* sh = shadow ? shadow + (long long)g * P : nullptr;
   float* fa = fg ? fg + (long long)g * P : nullptr;
   for (int i4 = blockIdx.x * blockDim.x + threadIdx.x; i4 < P / 4; i4 += gridDim.x * blockDim.x) {
     const int i = i4 * 4;
@@ -44,22 +43,16 @@ __global__ __launch_bounds__(256) void sgd_kernel(float* __restrict__ params, lo
     }
     *(float4*)(p + i) = pv;
     *(float4*)(m + i) = mv;
-    if (sh) {
-      uint2 s;
-      s.x = (uint32_t)f2bf(pp[0]) | ((uint32_t)f2bf(pp[1]) << 16);
-      s.y = (uint32_t)f2bf(pp[2]) | ((uint32_t)f2bf(pp[3]) << 16);
-      *(uint2*)(sh + i) = s;
-    }
   }
 }
 
 }  // namespace
 
 DBA_EXPORT int dba_sgd_step(float* params, long long p_gstride, const float* grads, float* mom, const float* lr,
-                            const int* first, const int* active, float momentum, float wd, void* shadow, float* fg,
+                            const int* first, const int* active, float momentum, float wd, float* fg,
                             int G, int P, void* stream) {
   const int blocks = std::max(1, std::min(1024, (P / 4 + 255) / 256));
   hipLaunchKernelGGL(sgd_kernel, dim3(blocks, G), dim3(256), 0, (hipStream_t)stream, params, p_gstride, grads, mom, lr,
-                     first, active, momentum, wd, (uint16_t*)shadow, fg, P);
+                     first, active, momentum, wd, fg, P);
   DBA_LAUNCH_CHECK();
 }

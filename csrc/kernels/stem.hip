@@ -12,8 +12,8 @@
 // slots); the pixel's receptive field streams through registers one kernel row at a time.
 // Every output is an fp32 FMA chain in fixed (kh, kw, ci) order: exact fp32 arithmetic and
 // deterministic.  Epilogue: bias, residual, ReLU, the fp16-pair max slot of the output
-// (common.hpp amax_fold) and, for a training BN, the fixed 32-row fp64 column sums / sums of
-// squares (same layout and definition as xgemm.hip bn_tile_stats).
+// (common.hpp amax_fold) and, for a training BN, the level-0 records of the fused BN statistics
+// (bnfuse.hpp bnf_tile_records' definition).
 #include "common.hpp"
 #include "bnfuse.hpp"
 #include <cstdlib>
@@ -35,7 +35,6 @@ struct StemArgs {
   const int* nvalid;
   int N, H, W, Ho, Wo, stride, pad, relu;
   int* amax_out; int amax_ld;
-  double* bnpart; int bnpart_nblk;          // [G][COUT][2][nblk] (optional)
   // fp16-pair output (xgemm.hip PairAct): per-replica exponent from the bound
   // L1max(w) * max|x| + max|b|; x's max slot, the slot's {L1max, bmax}
   int* out_sexp; const float* bound; const int* amax_x; int amax_x_ld;
@@ -69,20 +68,9 @@ __global__ __launch_bounds__(256) void xstem_kernel(const StemArgs a) {
   const int tid = threadIdx.x;
   const int HoWo = a.Ho * a.Wo;
   const int Mv = valid_rows(a.nvalid, g, a.N) * HoWo;
-  const bool want_stats = a.bnpart != nullptr || a.bf.mode == 1;
+  const bool want_stats = a.bf.mode == 1;
   const int mb = blockIdx.x * (ITER * PIX);
-  if (mb >= Mv) {   // no valid pixel in the block's tiles: zero BN partials only
-    if (a.bnpart) {
-      for (int e = tid; e < ITER * (PIX / 32) * COUT; e += 256) {
-        const int grp = e / COUT, c = e - grp * COUT, b = mb / 32 + grp;
-        if (b >= a.bnpart_nblk) continue;
-        double* p = a.bnpart + ((long long)g * COUT + c) * 2 * a.bnpart_nblk + b;
-        p[0] = 0.0;
-        p[a.bnpart_nblk] = 0.0;
-      }
-    }
-    return;
-  }
+  if (mb >= Mv) return;   // no valid pixel in the block's tiles
   const int slot = a.wsel ? a.wsel[g] : g;
   const float* __restrict__ wg = a.w + (long long)slot * a.w_sstride;
   for (int e = tid; e < K * COUT; e += 256) {   // conflict-free LDS writes (the reads hit L1)
@@ -155,7 +143,7 @@ __global__ __launch_bounds__(256) void xstem_kernel(const StemArgs a) {
         acc[c4 * 4] = v.x; acc[c4 * 4 + 1] = v.y; acc[c4 * 4 + 2] = v.z; acc[c4 * 4 + 3] = v.w;
       }
     }
-    if (want_stats) {   // statistics of the raw output (bnpart implies no bias / residual / ReLU)
+    if (want_stats) {   // statistics of the raw output (fused BN implies no bias / residual / ReLU)
       if (pl < PIX) {
 #pragma unroll
         for (int c = 0; c < CPT; ++c) tile[pl * COUT + c0 + c] = live ? acc[c] : 0.f;
@@ -179,20 +167,6 @@ __global__ __launch_bounds__(256) void xstem_kernel(const StemArgs a) {
           bnf_store_rec(a.bf.rec0 + (((long long)g * COUT + c) * a.bf.ngrp + b) * 4, r4[0], r4[1], r4[2], r4[3]);
         }
       }
-      for (int e = tid; e < (PIX / 32) * COUT && a.bnpart; e += 256) {
-        const int grp = e / COUT, c = e - grp * COUT, b = m0 / 32 + grp;
-        if (b >= a.bnpart_nblk) continue;
-        double s0 = 0.0, s1 = 0.0;
-#pragma unroll 8
-        for (int r = 0; r < 32; ++r) {
-          const double v = (double)tile[(grp * 32 + r) * COUT + c];
-          s0 += v;
-          s1 = fma(v, v, s1);
-        }
-        double* pp = a.bnpart + ((long long)g * COUT + c) * 2 * a.bnpart_nblk + b;
-        pp[0] = s0;
-        pp[a.bnpart_nblk] = s1;
-      }
       __syncthreads();
     }
   }
@@ -203,7 +177,7 @@ template <int KH, int KW, int CIN, int COUT, int CPT>
 int stem_go(const StemArgs& a, int G, hipStream_t st) {
   constexpr int PIX = 256 / (COUT / CPT);
   constexpr int ITER = 4;   // pixel tiles per block: one weight load (LDS transpose) per 4 tiles
-  if ((a.bnpart || a.bf.mode) && PIX % 32 != 0) return -100;
+  if (a.bf.mode && PIX % 32 != 0) return -100;
   const long long M = (long long)a.N * a.Ho * a.Wo;
   const dim3 grid((unsigned)ceil_div(M, PIX * ITER), G);
   hipLaunchKernelGGL((xstem_kernel<KH, KW, CIN, COUT, CPT, ITER>), grid, dim3(256), 0, st, a);
@@ -220,18 +194,16 @@ DBA_EXPORT int dba_xstem_fwd(const float* x, long long x_gstride, const float* w
                              const float* bias, long long b_sstride, const float* res, float* out,
                              long long out_gstride, const int* nvalid, int G, int N, int H, int W, int Cin, int Ho,
                              int Wo, int Cout, int KH, int KW, int stride, int pad, int relu, int* amax_out,
-                             int amax_ld, double* bnpart, const int* amax_x, int amax_x_ld, int* out_sexp,
+                             int amax_ld, const int* amax_x, int amax_x_ld, int* out_sexp,
                              const float* bound, const void* bnf, void* stream) {
   if (env_off()) return -100;
-  if (out_sexp && (!bound || !amax_x || bnpart || res)) return -107;
+  if (out_sexp && (!bound || !amax_x || res)) return -107;
   if (((uintptr_t)out & 15) || (out_gstride & 3) || (res && ((uintptr_t)res & 15))) return -100;
-  if (bnpart && (bias || res || relu)) return -106;
   StemArgs a{};
   a.x = x; a.x_gstride = x_gstride; a.w = w; a.w_sstride = w_sstride; a.wsel = wsel;
   a.bias = bias; a.b_sstride = b_sstride; a.res = res; a.out = out; a.out_gstride = out_gstride;
   a.nvalid = nvalid; a.N = N; a.H = H; a.W = W; a.Ho = Ho; a.Wo = Wo; a.stride = stride; a.pad = pad;
   a.relu = relu; a.amax_out = amax_out; a.amax_ld = amax_ld;
-  a.bnpart = bnpart; a.bnpart_nblk = (int)ceil_div((long long)N * Ho * Wo, 32);
   a.out_sexp = out_sexp; a.bound = bound; a.amax_x = amax_x; a.amax_x_ld = amax_x_ld;
   if (bnf) {
     a.bf = *(const BnFuse*)bnf;
@@ -240,6 +212,6 @@ DBA_EXPORT int dba_xstem_fwd(const float* x, long long x_gstride, const float* w
   hipStream_t st = (hipStream_t)stream;
   if (KH == 3 && KW == 3 && Cin == 3 && Cout == 32) return stem_go<3, 3, 3, 32, 8>(a, G, st);
   if (KH == 7 && KW == 7 && Cin == 3 && Cout == 64) return stem_go<7, 7, 3, 64, 8>(a, G, st);
-  if (KH == 5 && KW == 5 && Cin == 1 && Cout == 20 && !bnpart) return stem_go<5, 5, 1, 20, 4>(a, G, st);
+  if (KH == 5 && KW == 5 && Cin == 1 && Cout == 20 && !a.bf.mode) return stem_go<5, 5, 1, 20, 4>(a, G, st);
   return -100;
 }

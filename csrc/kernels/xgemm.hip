@@ -284,8 +284,6 @@ struct XArgs {
   int amax_src_ld, amax_w_ld, amax_out_ld;
   const uint16_t* wp;                        // H: the weights pre-split (xsplit_w_kernel): per slot
   long long wp_sstride;                      //    2 planes of wp_sstride/2 fp16, scaled like amax_w
-  double* bnpart;                            // optional: BN statistics of the output (bn_tile_stats)
-  int bnpart_nblk;                           //    32-row groups per replica
   // fp16-pair activations (PairAct below): the A operand arrives pre-split (in_sexp: its
   // per-replica scale exponent), the output leaves pre-split (out_sexp: written per replica;
   // bound: per weight slot {max row L1 of w, max |bias|}; amax_res: the residual's max), the
@@ -397,39 +395,6 @@ __device__ __forceinline__ int pair_out_exp(const XArgs& a, int g, int slot) {
   return hexp(__float_as_int(2.f * b));
 }
 
-// Training-BN statistics of a conv's output, folded into its epilogue (the separate BN
-// reduce pass over y is gone): for every 32-row group of GEMM rows (pixels) of the tile
-// staged in LDS (Ct, BM x BN, rows of invalid pixels are exact zeros: their A rows were
-// zero-filled), the column sum and sum of squares, summed over the 32 rows in order.  The
-// group is fixed at 32 rows whatever the tile height, so the partials — and the BN
-// statistics finalised from them — do not depend on the tile shape (which follows the
-// launch's replica count): world-size independent bits.  The sums run in fp64 (a square of
-// an fp32 value is exact there, and 32 of them sum exactly in all but extreme spreads), so the
-// statistics are fp64-accurate before the final rounding: E[x^2] - mean^2 keeps no fp32
-// cancellation error.  part[g][c][2][nblk] (fp64); zero: the tile has no valid row.
-template <int BM, int BN>
-__device__ __forceinline__ void bn_tile_stats(const float* Ct, double* __restrict__ part, int nblk, int g, int C,
-                                              int m0, int n0, bool zero) {
-  constexpr int NG = BM / 32;
-  for (int e = threadIdx.x; e < NG * BN; e += 256) {
-    const int grp = e / BN, cc = e - grp * BN, n = n0 + cc;
-    const int b = m0 / 32 + grp;
-    if (n >= C || b >= nblk) continue;
-    double s0 = 0.0, s1 = 0.0;
-    if (!zero) {
-#pragma unroll 8
-      for (int r = 0; r < 32; ++r) {
-        const double v = (double)Ct[(grp * 32 + r) * BN + cc];
-        s0 += v;
-        s1 = fma(v, v, s1);
-      }
-    }
-    double* p = part + ((long long)g * C + n) * 2 * nblk + b;
-    p[0] = s0;
-    p[nblk] = s1;
-  }
-}
-
 template <int BM, int BN, int WM, int WN, int P, int VEC, bool H, bool PW = false, bool PA = false, bool LZ = false>
 __global__ __launch_bounds__(256) void xconv_kernel(const XArgs a) {
   static_assert(!H || P == 2, "fp16 split: 2 planes");
@@ -452,11 +417,7 @@ __global__ __launch_bounds__(256) void xconv_kernel(const XArgs a) {
   const int Mv = valid_rows(a.nvalid, g, a.N) * HqWq;
   const int tn = blockIdx.x % a.tiles_n, tm = blockIdx.x / a.tiles_n;
   const int m0 = tm * BM, n0 = tn * BN;
-  if (m0 >= Mv) {
-    if (a.bnpart && (a.splitk == 1 || (a.sk_cnt && kz == 0)))
-      bn_tile_stats<BM, BN>(nullptr, a.bnpart, a.bnpart_nblk, g, a.Ncol, m0, n0, true);
-    return;
-  }
+  if (m0 >= Mv) return;
   const int slot = a.wsel ? a.wsel[g] : g;
   const int Cs = a.Cs;
   if constexpr (LZ) {   // the source BN's scale / shift (Cs <= 512: checked on the host)
@@ -711,7 +672,6 @@ __global__ __launch_bounds__(256) void xconv_kernel(const XArgs a) {
       fin = true;
     }
   }
-  if (fin && a.bnpart) bn_tile_stats<BM, BN>(Ct, a.bnpart, a.bnpart_nblk, g, a.Ncol, m0, n0, false);
   const int bfm = fin ? a.bf.mode : 0;   // fused training BN of the output (bnfuse.hpp)
   float* out = a.out + (long long)g * a.out_gstride + (fin ? 0 : (long long)kz * a.zstride);
   const float* bias = (fin && a.bias) ? a.bias + (long long)slot * a.b_sstride : nullptr;
@@ -819,10 +779,7 @@ __global__ __launch_bounds__(256) void xhalo_kernel(const XArgs a) {
   const int img = tm / HT, h0 = (tm - img * HT) * TR;
   const int n0 = tn * BN;
   const int nv_img = valid_rows(a.nvalid, g, a.N);
-  if (img >= nv_img) {
-    if (a.bnpart) bn_tile_stats<BM, BN>(nullptr, a.bnpart, a.bnpart_nblk, g, a.Ncol, tm * BM, n0, true);
-    return;
-  }
+  if (img >= nv_img) return;
   const int slot = a.wsel ? a.wsel[g] : g;
   const int K = 9 * CS;
   const float* __restrict__ src = a.src + (long long)g * a.src_gstride;
@@ -1009,7 +966,6 @@ __global__ __launch_bounds__(256) void xhalo_kernel(const XArgs a) {
       for (int r = 0; r < 16; ++r)
         Ct[(wm * TM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * hf) * BN + wn * TN + j * 32 + fr] = acc[i][j][r];
   __syncthreads();
-  if (a.bnpart) bn_tile_stats<BM, BN>(Ct, a.bnpart, a.bnpart_nblk, g, a.Ncol, tm * BM, n0, false);
   float* out = a.out + (long long)g * a.out_gstride;
   const float* bias = a.bias ? a.bias + (long long)slot * a.b_sstride : nullptr;
   const float* res = a.res ? a.res + (long long)g * a.out_gstride : nullptr;
@@ -1086,19 +1042,6 @@ __global__ __launch_bounds__(256, 2) void xhalo_ws_kernel(const XArgs a, int G) 
   const bool flip = a.dsg < 0;
   int total = 0;
   for (int gg = 0; gg < G; ++gg) total += valid_rows(a.nvalid, gg, a.N) * HT;
-  if (a.bnpart) {   // BN partials of the invalid images' 32-row groups are zeros (the finalize sums all)
-    const int HoWo = a.Ho * a.Wo;
-    for (int gg = 0; gg < G; ++gg) {
-      const int b0 = valid_rows(a.nvalid, gg, a.N) * HoWo / 32;
-      for (long long e = b0 * (long long)NC + blockIdx.x * 256LL + tid; e < (long long)a.bnpart_nblk * NC;
-           e += (long long)gridDim.x * 256) {
-        const int c = (int)(e % NC), b = (int)(e / NC);
-        double* p = a.bnpart + ((long long)gg * NC + c) * 2 * a.bnpart_nblk + b;
-        p[0] = 0.0;
-        p[a.bnpart_nblk] = 0.0;
-      }
-    }
-  }
   // the valid items, split evenly over the grid (inactive replicas leave no idle blocks)
   const int per = (total + gridDim.x - 1) / gridDim.x;
   int item = blockIdx.x * per;
@@ -1233,7 +1176,6 @@ __global__ __launch_bounds__(256, 2) void xhalo_ws_kernel(const XArgs a, int G) 
       for (int r = 0; r < 16; ++r) Ct[(wm * TM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * hf) * NC + fr] = acc[i][0][r];
     __syncthreads();
     const int tm = iimg * HT + ih0 / TR;
-    if (a.bnpart) bn_tile_stats<BM, NC>(Ct, a.bnpart, a.bnpart_nblk, ig, NC, tm * BM, 0, false);
     float* out = a.out + (long long)ig * a.out_gstride;
     const float* bias = a.bias ? a.bias + (long long)slot * a.b_sstride : nullptr;
     const float* res = a.res ? a.res + (long long)ig * a.out_gstride : nullptr;
@@ -2200,7 +2142,7 @@ DBA_EXPORT int dba_xconv_fwd(const float* x, long long x_gstride, const float* w
                              int Wo, int Cout, int KH, int KW, int stride, int pad, int relu, const int* amax_x,
                              int amax_x_ld, const int* amax_w, int amax_w_ld, int* amax_out, int amax_out_ld,
                              const uint16_t* wp, long long wp_sstride, float* ws, long long ws_floats,
-                             double* bnpart, const int* in_sexp, int* out_sexp, const float* bound,
+                             const int* in_sexp, int* out_sexp, const float* bound,
                              const int* amax_res, int amax_res_ld, const int* res_sexp, int* sk_cnt,
                              long long sk_cnt_n, const void* bnf, const float* lz_coef, int lz_relu, void* stream) {
   hipStream_t st = (hipStream_t)stream;
@@ -2216,16 +2158,14 @@ DBA_EXPORT int dba_xconv_fwd(const float* x, long long x_gstride, const float* w
   a.amax_src = amax_x; a.amax_w = amax_w; a.amax_out = amax_out;
   a.amax_src_ld = amax_x_ld; a.amax_w_ld = amax_w_ld; a.amax_out_ld = amax_out_ld;
   a.wp = wp; a.wp_sstride = wp_sstride;
-  a.bnpart = bnpart; a.bnpart_nblk = (int)ceil_div(M, 32);
   a.in_sexp = in_sexp; a.out_sexp = out_sexp; a.bound = bound;
   a.amax_res = amax_res; a.amax_res_ld = amax_res_ld; a.res_sexp = res_sexp;
   a.cls[0] = XClass{KH, KW, -pad, -pad, 0, 0, Ho, Wo, 0};
-  if (bnpart && (bias || res || relu)) return -106;   // statistics of the raw conv output only
   const bool pairs = in_sexp || out_sexp || res_sexp;
-  if (pairs && (!amax_x || !wp || vec < 4 || (Cout & 3) || bnpart || (out_sexp && !bound))) return -107;
+  if (pairs && (!amax_x || !wp || vec < 4 || (Cout & 3) || (out_sexp && !bound))) return -107;
   if (bnf) {
     a.bf = *(const BnFuse*)bnf;
-    if (a.bf.mode != 1 || bias || res || relu || pairs || bnpart || (Cout & 3) || a.bf.C != Cout) return -108;
+    if (a.bf.mode != 1 || bias || res || relu || pairs || (Cout & 3) || a.bf.C != Cout) return -108;
   }
   if (lz_coef) {
     if (!amax_x || wp || pairs || vec < 4 || Cin > 512) return -108;
@@ -2247,7 +2187,6 @@ DBA_EXPORT int dba_xconv_fwd(const float* x, long long x_gstride, const float* w
     b.sk_ws = ws; b.sk_gstride = M * Cout; b.sk_cnt = sk_cnt;
     return fin(xconv_dispatch(b, M, G, 1, vec, st));
   }
-  if (bnpart && s > 1) return -106;   // separate reduce launch: BN statistics by the BN kernels
   if (ws_ok) {
     XArgs b = a;
     b.splitk = s;

@@ -93,7 +93,7 @@ _DEFAULTS: Dict[str, Any] = {
     "synthetic_noise": None,       # synthetic image pixel-noise sigma (None: per-dataset default)
     "synthetic_shared": None,      # fraction of the class template shared by all classes
     "synthetic_clutter": None,     # weight of the per-image random background field
-    "compute_dtype": "fp32",      # fp32 = reference precision (split-bf16 MFMA on GPU); bf16 = fast mode
+    "compute_dtype": "fp32",      # fp32 = reference precision (split fp32 operands on the 16-bit MFMA)
     "eval_batch_size": 1024,      # per-model eval chunk (reference: 64; a free parameter, D13)
     "aggregate_bn_buffers": True,  # D2: deltas/aggregation include BN running stats
     "best_on_clean_loss": False,   # D6: reference keys .best on the poison-test loss

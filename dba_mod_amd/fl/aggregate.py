@@ -99,7 +99,9 @@ def geometric_median(global_state: torch.Tensor, finals: torch.Tensor, num_sampl
     alphas = a / a.sum()
 
     def avg(w: torch.Tensor) -> torch.Tensor:
-        return ops.weighted_sum(points, (w / w.sum()).float())
+        # fp64 accumulation of the (exact in fp64) fp32 products, rounded once: the same
+        # numbers the distributed form reaches from rank partial sums, up to fp64 order
+        return ops.weighted_sum(points, (w / w.sum()).float(), out_dtype=torch.float64).float()
 
     def dists(m: torch.Tensor) -> torch.Tensor:
         return ops.sq_dists(points, m).double().clamp(min=0.0).sqrt()

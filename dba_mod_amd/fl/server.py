@@ -87,15 +87,15 @@ class _EarlyEval:
 
 
 def compute_dtype_for(params: C.Params, device: torch.device) -> torch.dtype:
-    """Activation / GEMM precision.  ``fp32`` (the default, = the reference's precision) runs
-    the split-bf16 fp32 kernel family on GPU (csrc/kernels/xgemm.hip); ``bf16`` opts into the
-    bf16 MFMA family (fp32 master weights, bf16 activations)."""
+    """Activation / GEMM precision: fp32, the reference's precision (the fp32 kernel family on
+    GPU, csrc/kernels/xgemm.hip).  The round-1 bf16 fast mode and its kernel family were removed
+    in round 4 (one deterministic conv family)."""
     cd = str(params["compute_dtype"]).lower()
-    table = {"auto": torch.float32, "bf16": torch.bfloat16, "bfloat16": torch.bfloat16, "fp32": torch.float32,
-             "float32": torch.float32}
-    if cd not in table:
-        raise ValueError(f"compute_dtype {cd!r}: expected fp32 or bf16")
-    return table[cd]
+    if cd in ("bf16", "bfloat16"):
+        raise ValueError("compute_dtype bf16 was removed (round 4): the kernels are the fp32 family")
+    if cd not in ("auto", "fp32", "float32"):
+        raise ValueError(f"compute_dtype {cd!r}: expected fp32")
+    return torch.float32
 
 
 class Server:

@@ -63,11 +63,10 @@ class _GroupBuffers:
     """Static per-G buffers (and the captured graph) reused across rounds."""
 
     def __init__(self, spec: ModelSpec, G: int, B: int, max_slots: int, device: torch.device,
-                 wdtype: torch.dtype, fg: bool) -> None:
+                 fg: bool) -> None:
         S, P = spec.S, spec.P
         self.G, self.B, self.max_slots = G, B, max_slots
         self.state = torch.zeros(G, S, dtype=torch.float32, device=device)
-        self.wcomp = self.state if wdtype == torch.float32 else torch.zeros(G, P, dtype=wdtype, device=device)
         self.grads = torch.zeros(G, P, dtype=torch.float32, device=device)
         self.mom = torch.zeros(G, P, dtype=torch.float32, device=device)
         self.fg = torch.zeros(G, P, dtype=torch.float32, device=device) if fg else None
@@ -144,7 +143,7 @@ class GroupTrainer:
         else:
             x, y = ops.gather_rows(wl.train_store.rows, wl.train_store.labels, b.idx, wl.trig_cols,
                                    wl.trig_vals, b.trig, b.poison_n, self.target, self.dtype)
-        ctx = prog.Ctx(self.spec, b.state, b.wcomp, None, train=True, grads=b.grads,
+        ctx = prog.Ctx(self.spec, b.state, b.state, None, train=True, grads=b.grads,
                        nvalid=b.nvalid, dropout_seed=b.seed, act_dtype=self.dtype)
         logits = prog.forward(ctx, x)
         fused = self.alpha == 1.0     # stats straight from the loss kernel (no extra launches)
@@ -160,7 +159,7 @@ class GroupTrainer:
             dist = ops.dist_loss_grad(b.state, b.base, b.grads, b.trig, b.active, self.alpha)
             loss = torch.where(b.trig >= 0, self.alpha * loss + (1.0 - self.alpha) * dist, loss)
         ops.sgd_step(b.state[:, :self.spec.P], b.grads, b.mom, b.lr, b.first, b.active, self.momentum,
-                     self.wd, shadow=(b.wcomp if b.wcomp is not b.state else None), fg_accum=b.fg)
+                     self.wd, fg_accum=b.fg)
         if not fused:
             ref_ops.accumulate_step_stats(b.stats, b.slot, loss, correct, b.nvalid)
         self._last_loss = loss
@@ -168,8 +167,7 @@ class GroupTrainer:
     def _buffers(self, G: int, max_slots: int) -> _GroupBuffers:
         key = (G, max_slots)
         if key not in self._bufs:
-            wdt = self.dtype if self.device.type == "cuda" else torch.float32
-            self._bufs[key] = _GroupBuffers(self.spec, G, self.B, max_slots, self.device, wdt, self.fg)
+            self._bufs[key] = _GroupBuffers(self.spec, G, self.B, max_slots, self.device, self.fg)
         return self._bufs[key]
 
     def _run_step(self, b: _GroupBuffers) -> None:
@@ -272,12 +270,9 @@ class GroupTrainer:
         2-epoch clients finished) for at least SOLO_MIN_STEPS steps; graph mode, G > 1 only."""
         if not self.use_graph or len(clients) < 2 or self.SOLO_MIN_STEPS <= 0:
             return None
-        # only where it is bit-identical: the fp32 family decides every kernel parameter from
-        # the per-replica geometry; the bf16 family's split-K / tile choices depend on the
-        # launch's replica count, so moving a client to the one-replica graph would change its
-        # rounding (tests/test_gpu_e2e.py test_solo_tail_bitwise)
-        if self.dtype != torch.float32:
-            return None
+        # bit-identical: the fp32 family decides every summation order from the per-replica
+        # geometry (split-K, fused BN groups), so moving a client to the one-replica graph
+        # changes no rounding (tests/test_gpu_e2e.py test_solo_tail_bitwise)
         lens = sorted(((len(c.steps), g) for g, c in enumerate(clients)), reverse=True)
         (n0, g0), (n1, _) = lens[0], lens[1]
         if n0 != T or n0 - n1 < self.SOLO_MIN_STEPS:
@@ -305,8 +300,6 @@ class GroupTrainer:
         dst.state[j].copy_(src.state[i])
         dst.base[j].copy_(src.base[i])
         dst.mom[j].copy_(src.mom[i])
-        if dst.wcomp is not dst.state:
-            dst.wcomp[j].copy_(src.wcomp[i])
         if dst.fg is not None:
             dst.fg[j].copy_(src.fg[i])
         ms = dst.max_slots
@@ -338,8 +331,6 @@ class GroupTrainer:
     def _reset(self, b: _GroupBuffers, global_state: torch.Tensor) -> None:
         b.state.copy_(global_state[None].expand_as(b.state))
         b.base.copy_(b.state)
-        if b.wcomp is not b.state:
-            b.wcomp.copy_(b.state[:, :self.spec.P])
         b.mom.zero_()
         b.stats.zero_()
         b.nan_flag.zero_()
@@ -373,8 +364,6 @@ class GroupTrainer:
             gamma = float(self.params["scale_weights_poison"])
             scaled = ops.scale_from_base(b.state[g], b.base[g], gamma)
             b.state[g].copy_(scaled)
-            if b.wcomp is not b.state:
-                b.wcomp[g].copy_(b.state[g, :P])
             # norms / distances over parameters only (helper.model_global_norm /
             # model_dist_norm, helper.py:59-71): scaled distance, the round's global model norm,
             # norm and distance before scaling, scaled norm — squared, on device, read once at

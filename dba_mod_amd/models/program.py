@@ -121,7 +121,7 @@ class Ctx:
     """Per-forward context: where the weights live, which mode, the tape.
 
     ``state``   fp32 ``[Gm, S]`` (params | BN buffers) — master weights and running stats.
-    ``wcomp``   weights in compute dtype ``[Gm, >=P]`` (bf16 shadow on GPU; = state on CPU).
+    ``wcomp``   the weights the convs read ``[Gm, >=P]`` (fp32; the trainer passes ``state``).
     ``grads``   fp32 ``[G, P]`` gradient buffer (train mode only).
     ``folded``  eval mode: {conv name: (w', b')} from :func:`fold_bank`.
     """

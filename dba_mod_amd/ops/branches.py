@@ -28,7 +28,8 @@ TIE_TOL = 1e-4
 
 
 class BranchReplay:
-    """Records ``bn_train`` / ``conv2d`` ReLU masks and ``maxpool2d`` indices of one run
+    """Records the ReLU masks of the fused training BN (``conv_bn_stats`` lazy outputs,
+    ``bn_apply``) and of ``conv2d`` and the ``maxpool2d`` indices of one run
     (``wrap(module)`` overrides, ``replay = False``) and replays them near ties in every
     later run (``replay = True``; :meth:`start_replay` before each).  Only valid images
     (``nval``) are compared."""
@@ -43,7 +44,7 @@ class BranchReplay:
         self.flips = self.hard = self.elements = 0
 
     def wrap(self, mod):
-        o_bn, o_conv, o_mp = mod.bn_train, mod.conv2d, mod.maxpool2d
+        o_conv, o_mp = mod.conv2d, mod.maxpool2d
         o_cbs, o_apply = mod.conv_bn_stats, mod.bn_apply
 
         def conv_bn_stats(x, w, wsel, stride, pad, nvalid, p, relu):
@@ -68,13 +69,6 @@ class BranchReplay:
                 return self._record(out) if relu else out
             return self._relu(o_apply(a, residual, False, nvalid))
 
-        def bn_train(y, gamma, beta, rmean, rvar, nvalid, momentum, eps, relu, residual):
-            if not (relu and self.replay):
-                out, m, s = o_bn(y, gamma, beta, rmean, rvar, nvalid, momentum, eps, relu, residual)
-                return (self._record(out) if relu else out), m, s
-            pre, m, s = o_bn(y, gamma, beta, rmean, rvar, nvalid, momentum, eps, False, residual)
-            return self._relu(pre), m, s
-
         def conv2d(*a, **k):
             relu = k.get("relu", a[7] if len(a) > 7 else False)
             if not (relu and self.replay):
@@ -89,8 +83,7 @@ class BranchReplay:
         def maxpool2d(x, kk, st, p):
             y, ind = o_mp(x, kk, st, p)
             return self._pool(x, y, ind)
-        return {"bn_train": bn_train, "conv2d": conv2d, "maxpool2d": maxpool2d, "conv_bn_stats": conv_bn_stats,
-                "bn_apply": bn_apply}
+        return {"conv2d": conv2d, "maxpool2d": maxpool2d, "conv_bn_stats": conv_bn_stats, "bn_apply": bn_apply}
 
     def _valid(self, t):
         v = torch.zeros(t.shape[:2], dtype=torch.bool)

@@ -17,7 +17,6 @@ from . import bnstate as bs
 from . import build
 
 Tensor = torch.Tensor
-_BF16 = torch.bfloat16
 _F32 = torch.float32
 
 if not os.path.exists(build.kernels_path()):
@@ -34,23 +33,7 @@ _U = ctypes.c_uint
 _SIGS = {
     "dba_gather_images": [_P, _P, _P, _P, _P, _P, _I, _P, _P, _I, _P, _I, _I, _I, _I, _I, _P],
     "dba_gather_rows": [_P, _P, _P, _P, _P, _I, _P, _P, _I, _P, _I, _P, _I, _I, _I, _P],
-    "dba_conv_fwd": [_P, _LL, _P, _LL, _P, _P, _LL, _P, _LL, _P, _LL, _I, _P] + [_I] * 13 + [_P],
-    "dba_conv_dgrad": [_P, _LL, _P, _LL, _P, _P, _LL, _P] + [_I] * 12 + [_P],
-    "dba_conv_wgrad": [_P, _LL, _P, _LL, _P, _LL, _P] + [_I] * 12 + [_P],
-    "dba_conv2_fwd": [_P, _LL, _P, _LL, _P, _P, _LL, _P, _P, _LL, _I, _P] + [_I] * 13 + [_P],
-    "dba_conv2_dgrad_w": [_P, _LL, _P, _LL, _P, _P, _P, _LL, _P] + [_I] * 12 + [_P],
-    "dba_conv2_dgrad": [_P, _LL, _P, _LL, _P, _P, _P, _LL, _P] + [_I] * 12 + [_P],
-    "dba_transpose_w": [_P, _LL, _P, _I, _I, _I, _I, _I, _P, _P],
-    "dba_transpose_w_batch": [_P, _I, _I, _P, _P],
-    "dba_halo_conv": [_P, _LL, _P, _LL, _P, _P, _LL, _P, _P, _LL, _I, _P] + [_I] * 9 + [_P],
-    "dba_colsum": [_P, _LL, _I, _P, _I, _I, _I, _P, _LL, _P],
     "dba_xcolsum": [_P, _LL, _I, _P, _I, _I, _I, _P, _LL, _P],
-    "dba_bn_stats": [_P, _P, _I, _I, _I, _I, _P, _P, _P, _LL, _F, _F, _P, _P, _I, _P, _P],
-    "dba_bn_partial_blocks": [_I, _I, _I],
-    "dba_bn_apply": [_P, _P, _P, _P, _P, _LL, _P, _I, _P, _P, _I, _I, _I, _I, _I, _P, _I, _P],
-    "dba_bn_bwd": [_P, _P, _P, _P, _P, _P, _LL, _I, _P, _P, _LL, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _I, _P, _P],
-    "dba_bn_small_fwd": [_P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _LL, _F, _F, _P, _I, _P, _P, _P, _I, _P, _I, _P],
-    "dba_bn_small_bwd": [_P, _P, _P, _P, _P, _P, _LL, _I, _P, _P, _LL, _P, _P, _P, _I, _I, _I, _I, _I, _P, _I, _P],
     "dba_amax_segments": [_P, _LL, _P, _I, _I, _P, _I, _P],
     "dba_bn_fold": [_P, _LL, _P, _P, _P, _P, _P, _LL, _F, _P, _P, _I, _I, _I, _I, _P],
     "dba_relu_mask_bwd": [_P, _P, _P, _LL, _I, _P],
@@ -60,7 +43,7 @@ _SIGS = {
     "dba_avgpool_bwd": [_P, _P, _LL, _I, _I, _I, _P],
     "dba_dropout": [_P, _P, _I, _P, _U, _F, _LL, _I, _P],
     "dba_softmax_xent": [_P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _LL, _P, _I, _P, _I, _P, _P],
-    "dba_sgd_step": [_P, _LL, _P, _P, _P, _P, _P, _F, _F, _P, _P, _I, _I, _P],
+    "dba_sgd_step": [_P, _LL, _P, _P, _P, _P, _P, _F, _F, _P, _I, _I, _P],
     "dba_scale_from_base": [_P, _P, _F, _P, _LL, _P],
     "dba_add_noise_scaled": [_P, _P, _LL, _F, _F, _U, _I, _I, _P],
     "dba_delta_sum": [_P, _LL, _I, _P, _LL, _P, _P],
@@ -69,23 +52,15 @@ _SIGS = {
     "dba_sq_dists": [_P, _LL, _P, _I, _LL, _P, _P, _P],
     "dba_weighted_sum": [_P, _LL, _P, _I, _P, _LL, _I, _P],
     "dba_gram": [_P, _LL, _I, _I, _P, _P, _P],
-    "dba_conv3_fwd": [_P, _LL, _P, _LL, _P, _P, _LL, _P, _P, _LL, _I, _P, _P] + [_I] * 13 + [_P, _LL, _P],
-    "dba_conv3_splitk_floats": [_I] * 9,
-    "dba_conv3_set_tiles": [_I, _I],
-    "dba_pconv": [_P, _LL, _P, _LL, _P, _P, _LL, _P, _P, _LL, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P],
-    "dba_pwgrad": [_P, _LL, _P, _LL, _P, _LL, _P, _P, _I, _I, _I, _I, _I, _I, _P],
-    "dba_wgrad3": [_P, _LL, _P, _LL, _P, _LL, _P, _P] + [_I] * 12 + [_P],
     "dba_dist_loss_grad": [_P, _LL, _P, _LL, _P, _LL, _I, _P, _P, _F, _P, _P, _P],
     # reference-precision (fp32) family: csrc/kernels/xgemm.hip
     "dba_xgemm_set_planes": [_I],
     "dba_xhalo_ws_set": [_I],
-    "dba_bn_bwd_fuse_set": [_I],
     "dba_xconv_ws_floats": [_I] * 8,
     "dba_xconv_fwd": [_P, _LL, _P, _LL, _P, _P, _LL, _P, _P, _LL, _P] + [_I] * 13 + [_P, _I] * 3 + [_P, _LL] * 2
-    + [_P, _P, _P, _P, _P, _I, _P, _P, _LL, _P, _P, _I, _P],
+    + [_P, _P, _P, _P, _I, _P, _P, _LL, _P, _P, _I, _P],
     "dba_xconv_sk_ints": [_I] * 8,
     "dba_row_bound": [_P, _LL, _I, _I, _P, _LL, _I, _P, _P],
-    "dba_bn_finalize_part": [_P, _I, _P, _I, _I, _I, _I, _P, _P, _LL, _F, _F, _P, _P, _P],
     "dba_xconv_dgrad": [_P, _LL, _P, _LL, _P, _P, _P, _LL, _P] + [_I] * 12 + [_P, _I] * 2 + [_P, _LL] * 3 + [_P, _P],
     "dba_xsplit_w": [_P, _LL, _LL, _I, _P, _I, _P, _P],
     "dba_amax": [_P, _LL, _LL, _P, _LL, _I, _P, _I, _P],
@@ -99,13 +74,12 @@ _SIGS = {
     "dba_bnx_dy": [_P, _P, _P, _P, _LL, _P, _I, _I, _I, _I, _P, _I, _P],
     "dba_xwgrad_reduce_batch": [_P, _I, _I, _LL, _P],
     # image stems in exact fp32 (csrc/kernels/stem.hip)
-    "dba_xstem_fwd": [_P, _LL, _P, _LL, _P, _P, _LL, _P, _P, _LL, _P] + [_I] * 13 + [_P, _I, _P, _P, _I, _P, _P, _P, _P],
+    "dba_xstem_fwd": [_P, _LL, _P, _LL, _P, _P, _LL, _P, _P, _LL, _P] + [_I] * 13 + [_P, _I, _P, _I, _P, _P, _P, _P],
 }
 for _name, _args in _SIGS.items():
     _fn = getattr(_L, _name)
     _fn.argtypes = _args
     _fn.restype = ctypes.c_int
-_L.dba_conv3_splitk_floats.restype = ctypes.c_longlong
 _L.dba_xconv_ws_floats.restype = ctypes.c_longlong
 _L.dba_xconv_sk_ints.restype = ctypes.c_longlong
 _L.dba_xwgrad_ws_floats.restype = ctypes.c_longlong
@@ -129,7 +103,7 @@ class _BnFuse(ctypes.Structure):
 assert ctypes.sizeof(_BnFuse) == int(_L.dba_bnfuse_size()), "BnFuse layout mismatch (rebuild the kernels)"
 
 
-NOT_HANDLED = -100   # a conv2 entry point declining a shape (odd channel counts)
+NOT_HANDLED = -100   # an entry point declining a shape (the stem kernel: not a stem)
 
 
 def _call(name: str, *args) -> int:
@@ -170,11 +144,11 @@ def _rowview(t: Tensor) -> Tuple[Tensor, int]:
 
 
 def _act(t: Tensor, dt: Optional[torch.dtype] = None, what: str = "activation") -> Tensor:
-    """An activation operand, contiguous and NEVER converted: the kernels run in the dtype
-    the caller computes in (bf16 -> bf16 MFMA family, fp32 -> split-bf16 reference-precision
-    family).  ``dt`` pins the dtype (every operand of one op must agree)."""
-    if t.dtype not in (_BF16, _F32):
-        raise TypeError(f"{what}: unsupported dtype {t.dtype} (bf16 or fp32)")
+    """An activation operand, contiguous and NEVER converted: every kernel computes in fp32
+    (split into fp16 pairs for the MFMA family).  ``dt`` pins the dtype (every operand of
+    one op must agree)."""
+    if t.dtype != _F32:
+        raise TypeError(f"{what}: unsupported dtype {t.dtype} (fp32 only)")
     if dt is not None and t.dtype != dt:
         raise TypeError(f"{what}: dtype {t.dtype} does not match the op's {dt} operands "
                         f"(no silent precision conversion)")
@@ -229,53 +203,11 @@ def gather_rows(src, labels, idx, trig_cols, trig_vals, trig_id, poison_n, targe
 
 
 # ------------------------------------------------------------------------------ conv
-def _check_w(w: Tensor, dt: torch.dtype = _BF16) -> Tuple[Tensor, int]:
+def _check_w(w: Tensor, dt: torch.dtype = _F32) -> Tuple[Tensor, int]:
     if w.dtype != dt:
         raise TypeError(f"conv weights: dtype {w.dtype} does not match the {dt} activations "
                         f"(no silent precision conversion)")
     return _rowview(w)
-
-
-_PCONV = os.environ.get("DBA_PCONV", "1") != "0"
-_DGRAD_W = os.environ.get("DBA_DGRAD_W", "0") == "1"
-_GEMM3 = os.environ.get("DBA_GEMM3", "1") != "0"
-_WGRAD3 = os.environ.get("DBA_WGRAD3", "1") != "0"
-# (Cin, Cout, input W, stride): see csrc/kernels/pconv.hip
-_PCONV_SHAPES = {(32, 32, 32, 1), (64, 64, 16, 1), (32, 64, 32, 2), (64, 128, 16, 2)}
-_ZEROS = {}
-
-
-def _zeros(dev) -> Tensor:
-    """A small persistent zero page (halo padding source of the LDS-DMA conv kernels)."""
-    z = _ZEROS.get(dev)
-    if z is None:
-        z = _ZEROS[dev] = torch.zeros(256, dtype=torch.uint8, device=dev)
-    return z
-
-
-def _conv3(x_ptr, x_gs, w_ptr, w_ss, wsel_, bias_ptr, bs, res_ptr, out_ptr, out_gs, f32, nv_, dev,
-           G, N, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, relu) -> int:
-    """Gen-3 implicit GEMM (csrc/kernels/gemm3.hip); small launches get an fp32 split-K
-    workspace (allocated here, stream-ordered) when the kernel asks for one."""
-    n = int(_L.dba_conv3_splitk_floats(G, N, Ho, Wo, Cin, Cout, KH, KW, f32))
-    wsb = torch.empty(n, dtype=torch.float32, device=dev) if n > 0 else None
-    return _call("dba_conv3_fwd", x_ptr, x_gs, w_ptr, w_ss, wsel_, bias_ptr, bs, res_ptr, out_ptr, out_gs, f32, nv_,
-                 _zeros(dev).data_ptr(), G, N, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, relu, _ptr(wsb), n,
-                 _stream())
-
-
-GEMM3_TILES = {0: "64x128/4", 1: "64x64/4", 2: "64x128/3", 3: "128x64/3", 4: "128x128/2", 5: "128x128/3",
-               6: "64x64/3"}   # code -> BMxBN / LDS ring depth (gemm3.hip launch3_tile)
-
-
-def set_gemm3_tiles(small: int = -1, big: int = -1) -> Tuple[int, int]:
-    """Pick the gen-3 GEMM tile of the small (< DBA_G3_SMALL_LIMIT 128x128 tiles) and large
-    launch classes; -1 keeps the current one.  Returns the previous (small, big) codes."""
-    for c in (small, big):
-        if c != -1 and c not in GEMM3_TILES:
-            raise ValueError(f"unknown gemm3 tile code {c}")
-    prev = int(_L.dba_conv3_set_tiles(int(small), int(big)))
-    return prev // 16, prev % 16
 
 
 F16_PAIR = 16
@@ -306,12 +238,6 @@ def set_halo_ws(on: int) -> int:
     """Persistent weight-stationary stage-1 halo conv (xgemm.hip xhalo_ws_kernel) on / off;
     -1 queries.  Returns the previous setting."""
     return int(_L.dba_xhalo_ws_set(int(on)))
-
-
-def set_bn_bwd_fuse(g: int) -> int:
-    """Backward BN finalize folded into the apply for launches of <= ``g`` replicas (0: off;
-    -1 queries; bn.hip bn_bwd_apply_fin_kernel).  Returns the previous setting."""
-    return int(_L.dba_bn_bwd_fuse_set(int(g)))
 
 
 def fp32_mode() -> int:
@@ -403,23 +329,6 @@ def _sk_counters(n: int, device):
     return _ARENA[-1].counters(n, device)
 
 
-def _bn_counter(G: int, device):
-    """[G] zeroed arrival counters for a last-block BN finalize (bn.hip BnFin), carved from the
-    step's zeroed arena (16 per slot); None outside an arena — the BN passes then launch their
-    separate finalize (no extra zero-fill launch)."""
-    if not _BN_LAST_BLOCK or not _ARENA:
-        return None
-    ar = _ARENA[-1]
-    slot, used = getattr(ar, "_cnt", (None, AMAX_SUB))
-    if used >= AMAX_SUB:
-        slot = ar.take(G, device)
-        if slot is None:
-            return None
-        used = 0
-    ar._cnt = (slot, used + 1)
-    return slot[used, :G]
-
-
 def _aptr(a):
     """(pointer, leading dimension) of an amax slot (None: no slot)."""
     return (None, 0) if a is None else (a.data_ptr(), a.shape[-1])
@@ -500,12 +409,6 @@ def _amax_act(t, nvalid):
     return a
 
 
-def _pconv_ok(Cin, Cout, H, W, KH, KW, stride, pad) -> bool:
-    """H, W = input size."""
-    return (_PCONV and KH == 3 and KW == 3 and pad == 1 and H == W
-            and (Cin, Cout, W, stride) in _PCONV_SHAPES)
-
-
 def decode_pairs(t: Tensor) -> Tensor:
     """fp32 values of an fp16-pair activation (PairAct layout: every 4 channels = 4 fp16 hi +
     4 fp16 lo of x * 2^s[g]) — for oracles and diagnostics; the kernels decode in-register."""
@@ -524,12 +427,10 @@ def _pair_sexp(t):
     return getattr(t, "_dba_pair", None)
 
 
-def _xconv_fwd(x, w, wsel, stride, pad, bias, residual, relu, nvalid, out_dtype, bn_stats=False, out_pairs=False,
-               bnf=None, lz=None):
-    """Reference-precision conv (fp32 in / fp32 out, split MFMA: xgemm.hip).  ``bn_stats``:
-    the output feeds a training BN — the epilogue also folds its per-32-pixel column sums /
-    sums of squares (``y._dba_bnpart``), which :func:`bn_train` finalises instead of
-    re-reading y (not for split-K launches or BN layers on the single-launch path)."""
+def _xconv_fwd(x, w, wsel, stride, pad, bias, residual, relu, nvalid, out_dtype, out_pairs=False, bnf=None, lz=None):
+    """Reference-precision conv (fp32 in / fp32 out, split MFMA: xgemm.hip).  ``bnf``: the
+    fused training-BN statistics of the output (bnfuse.hpp); ``lz``: the input is a lazy BN
+    output (its coefficients, ReLU, bound slot)."""
     if out_dtype not in (None, _F32):
         raise TypeError(f"fp32 conv cannot emit {out_dtype} (no silent precision conversion)")
     G, N, H, W, Cin = x.shape
@@ -567,7 +468,7 @@ def _xconv_fwd(x, w, wsel, stride, pad, bias, residual, relu, nvalid, out_dtype,
     # the input may arrive split, the output may leave split; every user of such a tensor is a
     # conv of this family (A operand or residual)
     in_sexp, res_sexp = _pair_sexp(x), (_pair_sexp(residual) if residual is not None else None)
-    pairs_ok = (ax is not None and getattr(w, "_dba_planes", None) is not None and Cin % 4 == 0 and not bn_stats)
+    pairs_ok = (ax is not None and getattr(w, "_dba_planes", None) is not None and Cin % 4 == 0 and bnf is None)
     if (in_sexp is not None or res_sexp is not None) and not pairs_ok:
         raise RuntimeError("fp16-pair activation fed to a conv outside the evaluation pair path")
     out_sexp = None
@@ -575,34 +476,19 @@ def _xconv_fwd(x, w, wsel, stride, pad, bias, residual, relu, nvalid, out_dtype,
         out_sexp = torch.empty(G, dtype=torch.int32, device=x.device)   # every block with rows writes it
     bound = getattr(w, "_dba_bound", None)
     ares = _amax_act(residual, nvalid) if (residual is not None and out_sexp is not None) else None
-    part = None
-    want_part = (bn_stats and _BN_FUSED_STATS and bias is None and res is None and not relu
-                 and N * Ho * Wo > _BN_SMALL_ROWS)
     if Cin <= 4 and out_dtype in (None, _F32):
         # few-channel image stems: exact-fp32 direct conv (stem.hip), -100 = not a stem shape
-        if want_part:
-            nblk = (N * Ho * Wo + 31) // 32
-            part = torch.empty(G * Cout * 2 * nblk, dtype=torch.float64, device=x.device)
         rc = _call("dba_xstem_fwd", x.data_ptr(), N * H * W * Cin, w.data_ptr(), ws, _ptr(_i32(wsel)), _ptr(bias), bs,
                    _ptr(res), y.data_ptr(), N * Ho * Wo * Cout, _ptr(_i32(nvalid)), G, N, H, W, Cin, Ho, Wo, Cout,
-                   KH, KW, stride, pad, int(relu), *_aptr(ay), _ptr(part), *_aptr(ax if out_sexp is not None else None),
+                   KH, KW, stride, pad, int(relu), *_aptr(ay), *_aptr(ax if out_sexp is not None else None),
                    _ptr(out_sexp), _ptr(bound if out_sexp is not None else None), bnf_p, _stream())
         if rc != NOT_HANDLED:
-            if part is not None:
-                y._dba_bnpart = (part, nblk)
             if out_sexp is not None:
                 y._dba_pair = out_sexp
             return y
-        part = None
-    if want_part and (n == 0 or cnt is not None):
-        nblk = (N * Ho * Wo + 31) // 32
-        part = torch.empty(G * Cout * 2 * nblk, dtype=torch.float64, device=x.device)
-        if os.environ.get("DBA_BN_FUSED_POISON") == "1":   # diagnostics: unwritten slots -> NaN
-            part.fill_(float("nan"))
-        y._dba_bnpart = (part, nblk)
     _call("dba_xconv_fwd", x.data_ptr(), N * H * W * Cin, w.data_ptr(), ws, _ptr(_i32(wsel)), _ptr(bias), bs,
           _ptr(res), y.data_ptr(), N * Ho * Wo * Cout, _ptr(_i32(nvalid)), G, N, H, W, Cin, Ho, Wo, Cout, KH, KW,
-          stride, pad, int(relu), *_aptr(ax), *_aptr(aw), *_aptr(ay), *_wplanes(w), _ptr(wsb), n, _ptr(part),
+          stride, pad, int(relu), *_aptr(ax), *_aptr(aw), *_aptr(ay), *_wplanes(w), _ptr(wsb), n,
           _ptr(in_sexp), _ptr(out_sexp), _ptr(bound if out_sexp is not None else None), *_aptr(ares), _ptr(res_sexp),
           _ptr(cnt), 0 if cnt is None else cnt.numel(), bnf_p, lz_coef, lz_relu, _stream())
     if out_sexp is not None:
@@ -613,72 +499,13 @@ def _xconv_fwd(x, w, wsel, stride, pad, bias, residual, relu, nvalid, out_dtype,
 def conv2d(x, w, wsel, stride, pad, bias=None, residual=None, relu=False, nvalid=None, out_dtype=None,
            bn_stats=False, out_pairs=False):
     """``out_pairs``: the output may be emitted as fp16-pair activations (fp32 family,
-    evaluation with pre-split weights; y._dba_pair set) — only for outputs consumed by convs."""
+    evaluation with pre-split weights; y._dba_pair set) — only for outputs consumed by convs.
+    ``bn_stats`` is a reference-API hint (training BN goes through :func:`conv_bn_stats`)."""
     sx = _pair_sexp(x)
-    x = _act(x, None, "conv input")
+    x = _act(x, _F32, "conv input")
     if sx is not None:
         x._dba_pair = sx
-    if x.dtype == _F32:
-        return _xconv_fwd(x, w, wsel, stride, pad, bias, residual, relu, nvalid, out_dtype, bn_stats, out_pairs)
-    G, N, H, W, Cin = x.shape
-    w, ws = _check_w(w)
-    Cout, KH, KW = w.shape[1], w.shape[2], w.shape[3]
-    assert w.shape[4] == Cin, (w.shape, x.shape)
-    Ho = (H + 2 * pad - KH) // stride + 1
-    Wo = (W + 2 * pad - KW) // stride + 1
-    out_dtype = out_dtype or _BF16
-    y = torch.empty(G, N, Ho, Wo, Cout, dtype=out_dtype, device=x.device)
-    bs = 0
-    if bias is not None:
-        if bias.dtype != _F32:
-            raise TypeError(f"conv bias must be fp32 (got {bias.dtype})")
-        bias, bs = _rowview(bias)
-    if residual is not None:
-        residual = _act(residual, _BF16, "residual")
-    wsel_, nv_, f32 = _ptr(_i32(wsel)), _ptr(_i32(nvalid)), int(out_dtype == torch.float32)
-    # kernel selection by shape: halo-tiled direct conv (stride 1), gen-2 implicit GEMM
-    # (Cin % 8 == 0 or small-Cin stems), gen-1 implicit GEMM (odd channel counts)
-    rc = NOT_HANDLED
-    if (not f32 and _pconv_ok(Cin, Cout, H, W, KH, KW, stride, pad)
-            and (bias is None or (bs % 4 == 0 and bias.data_ptr() % 16 == 0))):
-        rc = _call("dba_pconv", x.data_ptr(), N * H * W * Cin, w.data_ptr(), ws, wsel_, _ptr(bias), bs,
-                   _ptr(residual), y.data_ptr(), N * Ho * Wo * Cout, nv_, _zeros(x.device).data_ptr(), G, N, Ho, Wo,
-                   Cin, Cout, 0, int(relu), stride, _stream())
-    if rc == NOT_HANDLED and _GEMM3:
-        rc = _conv3(x.data_ptr(), N * H * W * Cin, w.data_ptr(), ws, wsel_, _ptr(bias), bs, _ptr(residual),
-                    y.data_ptr(), N * Ho * Wo * Cout, f32, nv_, x.device, G, N, H, W, Cin, Ho, Wo, Cout, KH, KW,
-                    stride, pad, int(relu))
-    if rc == NOT_HANDLED and stride == 1 and KH == KW:
-        rc = _call("dba_halo_conv", x.data_ptr(), N * H * W * Cin, w.data_ptr(), ws, wsel_, _ptr(bias), bs,
-                   _ptr(residual), y.data_ptr(), N * Ho * Wo * Cout, f32, nv_, G, N, H, W, Cin, Cout, KH, pad,
-                   int(relu), _stream())
-    if rc == NOT_HANDLED:
-        rc = _call("dba_conv2_fwd", x.data_ptr(), N * H * W * Cin, w.data_ptr(), ws, wsel_, _ptr(bias), bs,
-               _ptr(residual), y.data_ptr(), N * Ho * Wo * Cout, f32, nv_, G, N, H, W, Cin, Ho, Wo, Cout, KH, KW,
-               stride, pad, int(relu), _stream())
-    if rc == NOT_HANDLED:
-        _call("dba_conv_fwd", x.data_ptr(), N * H * W * Cin, w.data_ptr(), ws, wsel_, _ptr(bias), bs,
-              _ptr(residual), N * Ho * Wo * Cout, y.data_ptr(), N * Ho * Wo * Cout, f32, nv_, G, N, H, W, Cin, Ho,
-              Wo, Cout, KH, KW, stride, pad, int(relu), _stream())
-    return y
-
-
-def _dgrad_flip(w_shape, stride, pad, in_hw) -> Optional[int]:
-    """Which transposed weight copy :func:`conv2d_dgrad` reads: None (none: the persistent
-    kernel gathers transposed fragments in-kernel), 1 (tap-flipped, stride-1 convs run as a
-    forward conv of dY) or 0 (plain transpose, strided / generic dgrad)."""
-    _, Cout, KH, KW, Cin = w_shape
-    H, W = in_hw
-    if stride == 1 and _pconv_ok(Cout, Cin, H, W, KH, KW, stride, pad):
-        return None
-    if _DGRAD_W:
-        return None
-    if stride == 1 and KH == KW and pad == (KH - 1) // 2:
-        return 1
-    return 0
-
-
-_TBATCH_MAX = 32
+    return _xconv_fwd(x, w, wsel, stride, pad, bias, residual, relu, nvalid, out_dtype, out_pairs)
 
 
 def _xtranspose(items) -> list:
@@ -705,38 +532,16 @@ def prepare_dgrad_weights(ref, items):
 
     ``items``: list of ``(w, wsel, stride, pad, in_hw, nvalid, G)`` for every conv whose input
     gradient the backward pass will compute.  Returns ``{index: wt}`` to be handed to
-    :func:`conv2d_dgrad` as ``wt=`` (items that need no transpose are absent)."""
-    if items and items[0][0].dtype == _F32:
-        # fp32 family: every data gradient reads class-packed transposed weights
-        slots = items[0][0].shape[0]
-        sel = [k for k, it in enumerate(items) if it[0].shape[0] == slots]
-        if not sel:
-            return {}
-        it0 = items[sel[0]]
-        nv = it0[5] if (it0[1] is None and it0[5] is not None and slots == it0[6]) else None
-        wts = _xtranspose([(items[k][0], items[k][2], items[k][3], nv) for k in sel])
-        return dict(zip(sel, wts))
-    out = {}
-    desc = []
-    nv_ptr, slots_all = None, None
-    for k, (w, wsel, stride, pad, in_hw, nvalid, G) in enumerate(items):
-        wv, ws = _check_w(w)
-        slots, Cout, KH, KW, Cin = wv.shape
-        flip = _dgrad_flip(wv.shape, stride, pad, in_hw)
-        if flip is None:
-            continue
-        if slots_all is None:
-            slots_all = slots
-            nv_ptr = _ptr(_i32(nvalid)) if (wsel is None and nvalid is not None and slots == G) else None
-        if slots != slots_all or len(desc) >= _TBATCH_MAX:
-            continue                         # left to conv2d_dgrad's own transpose
-        wt = torch.empty(slots, Cin, KH, KW, Cout, dtype=_BF16, device=wv.device)
-        out[k] = wt
-        desc.append([wv.data_ptr(), wt.data_ptr(), ws, Cout, KH * KW, Cin, flip, 0, 0])
-    if desc:
-        d = torch.tensor(desc, dtype=torch.int64)
-        _call("dba_transpose_w_batch", d.data_ptr(), len(desc), slots_all, nv_ptr, _stream())
-    return out
+    :func:`conv2d_dgrad` as ``wt=`` (every data gradient reads class-packed transposed weights;
+    items of another slot count are transposed by their own dgrad)."""
+    if not items:
+        return {}
+    slots = items[0][0].shape[0]
+    sel = [k for k, it in enumerate(items) if it[0].shape[0] == slots]
+    it0 = items[sel[0]]
+    nv = it0[5] if (it0[1] is None and it0[5] is not None and slots == it0[6]) else None
+    wts = _xtranspose([(items[k][0], items[k][2], items[k][3], nv) for k in sel])
+    return dict(zip(sel, wts))
 
 
 def _xconv_dgrad(dy, w, wsel, stride, pad, in_hw, nvalid, out_dtype, accum, wt, finish=None):
@@ -775,69 +580,7 @@ def _xconv_dgrad(dy, w, wsel, stride, pad, in_hw, nvalid, out_dtype, accum, wt, 
 
 
 def conv2d_dgrad(dy, w, wsel, stride, pad, in_hw, nvalid=None, out_dtype=None, accum=None, wt=None, finish=None):
-    dy = _act(dy, None, "dgrad dy")
-    if dy.dtype == _F32:
-        return _xconv_dgrad(dy, w, wsel, stride, pad, in_hw, nvalid, out_dtype, accum, wt, finish)
-    if finish is not None:
-        raise RuntimeError("fused training BN: fp32 family only")
-    G, N, Ho, Wo, Cout = dy.shape
-    w, ws = _check_w(w)
-    slots, _, KH, KW, Cin = w.shape
-    H, W = in_hw
-    have_wt = wt is not None
-    dx = torch.empty(G, N, H, W, Cin, dtype=_BF16, device=dy.device)
-    acc = _act(accum, _BF16, "dgrad accum") if accum is not None else None
-    if acc is not None:
-        assert acc.shape == dx.shape
-    if out_dtype not in (None, _BF16):
-        raise TypeError(f"bf16 dgrad cannot emit {out_dtype}")
-
-    if stride == 1 and _pconv_ok(Cout, Cin, H, W, KH, KW, stride, pad):
-        # stride-1 3x3 dgrad on the persistent kernel: transposed + flipped weight fragments
-        # are gathered in-kernel from the forward weights (no transpose pass)
-        rc = _call("dba_pconv", dy.data_ptr(), N * Ho * Wo * Cout, w.data_ptr(), ws, _ptr(_i32(wsel)), None, 0,
-                   _ptr(acc), dx.data_ptr(), N * H * W * Cin, _ptr(_i32(nvalid)), _zeros(dy.device).data_ptr(), G,
-                   N, H, W, Cout, Cin, 1, 0, 1, _stream())
-        if rc != NOT_HANDLED:
-            return dx
-    if _DGRAD_W:
-        # implicit GEMM reading the forward weights K-major with transposed LDS reads
-        # (experimental: measured slower than transpose + gen-2 GEMM on the ResNet shapes)
-        rc = _call("dba_conv2_dgrad_w", dy.data_ptr(), N * Ho * Wo * Cout, w.data_ptr(), ws, _ptr(_i32(wsel)),
-                   _ptr(acc), dx.data_ptr(), N * H * W * Cin, _ptr(_i32(nvalid)), G, N, H, W, Cin, Ho, Wo, Cout, KH,
-                   KW, stride, pad, _stream())
-        if rc != NOT_HANDLED:
-            return dx
-    if not have_wt:
-        wt = torch.empty(slots, Cin, KH, KW, Cout, dtype=_BF16, device=dy.device)
-    # slot == replica when there is no slot map: inactive replicas' slots need no transpose
-    skip = _ptr(_i32(nvalid)) if (wsel is None and nvalid is not None and slots == G) else None
-    if stride == 1 and KH == KW and pad == (KH - 1) // 2:
-        # stride-1 dgrad == forward conv of dY with tap-flipped, transposed weights
-        if not have_wt:
-            _call("dba_transpose_w", w.data_ptr(), ws, wt.data_ptr(), slots, Cout, KH * KW, Cin, 1, skip, _stream())
-        rc = NOT_HANDLED
-        if _GEMM3:
-            rc = _conv3(dy.data_ptr(), N * Ho * Wo * Cout, wt.data_ptr(), Cin * KH * KW * Cout, _ptr(_i32(wsel)),
-                        None, 0, _ptr(acc), dx.data_ptr(), N * H * W * Cin, 0, _ptr(_i32(nvalid)), dy.device, G, N,
-                        Ho, Wo, Cout, H, W, Cin, KH, KH, 1, KH - 1 - pad, 0)
-        if rc != NOT_HANDLED:
-            return dx
-        rc = _call("dba_halo_conv", dy.data_ptr(), N * Ho * Wo * Cout, wt.data_ptr(), Cin * KH * KW * Cout,
-                   _ptr(_i32(wsel)), None, 0, _ptr(acc), dx.data_ptr(), N * H * W * Cin, 0, _ptr(_i32(nvalid)), G,
-                   N, Ho, Wo, Cout, Cin, KH, KH - 1 - pad, 0, _stream())
-        if rc != NOT_HANDLED:
-            return dx
-    if not have_wt:
-        _call("dba_transpose_w", w.data_ptr(), ws, wt.data_ptr(), slots, Cout, KH * KW, Cin, 0, skip, _stream())
-    args = (dy.data_ptr(), N * Ho * Wo * Cout, wt.data_ptr(), Cin * KH * KW * Cout, _ptr(_i32(wsel)))
-    tail = (dx.data_ptr(), N * H * W * Cin, _ptr(_i32(nvalid)), G, N, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad,
-            _stream())
-    if _call("dba_conv2_dgrad", *args, _ptr(acc), *tail) == NOT_HANDLED:
-        _call("dba_conv_dgrad", *args, *tail)
-        if acc is not None:
-            dx += acc
-    return dx
+    return _xconv_dgrad(_act(dy, _F32, "dgrad dy"), w, wsel, stride, pad, in_hw, nvalid, out_dtype, accum, wt, finish)
 
 
 def conv2d_wgrad(dy, x, stride, pad, kh, kw, dw, dbias=None, nvalid=None, defer=None):
@@ -854,53 +597,35 @@ def conv2d_wgrad(dy, x, stride, pad, kh, kw, dw, dbias=None, nvalid=None, defer=
         conv2d_wgrad(dy, x, stride, pad, kh, kw, dw, dbias, nvalid, defer)
         return dy
     lx = x if isinstance(x, bs.LazyBN) else None
-    dy = _act(dy, None, "wgrad dy")
-    x = _act(lx.y if lx is not None else x, dy.dtype, "wgrad x")
-    if lx is not None and (dy.dtype != _F32 or _MODE != F16_PAIR or "wgrad" not in _H_OPS):
-        raise RuntimeError("fused training BN: fp32 family, fp16-pair weight gradient")
+    dy = _act(dy, _F32, "wgrad dy")
+    x = _act(lx.y if lx is not None else x, _F32, "wgrad x")
+    if lx is not None and (_MODE != F16_PAIR or "wgrad" not in _H_OPS):
+        raise RuntimeError("fused training BN: fp16-pair weight gradient")
     G, N, Ho, Wo, Cout = dy.shape
     _, _, H, W, Cin = x.shape
     assert dw.dtype == torch.float32 and _inner_contig(dw)
-    if dy.dtype == _F32:
-        mchunk = ctypes.c_int(0)
-        n = int(_L.dba_xwgrad_ws_floats(G, N, Ho, Wo, Cin, Cout, kh, kw, ctypes.byref(mchunk)))
-        wsb = torch.empty(n, dtype=_F32, device=dy.device) if n > 0 else None
-        nv = _i32(nvalid)
-        ad = ax = None
-        if _MODE == F16_PAIR and "wgrad" in _H_OPS:
-            ad = _amax_act(dy, nvalid)
-            ax = lx.stat.bound if lx is not None else _amax_act(x, nvalid)
-        _call("dba_xwgrad", dy.data_ptr(), N * Ho * Wo * Cout, x.data_ptr(), N * H * W * Cin, dw.data_ptr(),
-              dw.stride(0), _ptr(nv), G, N, H, W, Cin, Ho, Wo, Cout, kh, kw, stride, pad, *_aptr(ad), *_aptr(ax),
-              _ptr(wsb), n, int(defer is not None and n > 0),
-              _ptr(lx.stat.coef) if lx is not None else None, int(lx.relu) if lx is not None else 0, _stream())
-        if defer is not None and n > 0:
-            per = Cout * kh * kw * Cin
-            # (keeps the slab workspace and nvalid alive until the flush)
-            defer.append(([wsb.data_ptr(), dw.data_ptr(), dw.stride(0), per, _ptr(nv) or 0, N, Ho * Wo,
-                           mchunk.value, G, 0], wsb, nv))
-        if dbias is not None:
-            assert dbias.dtype == torch.float32 and dbias.stride(1) == 1
-            _call("dba_xcolsum", dy.data_ptr(), N * Ho * Wo * Cout, Ho * Wo, _ptr(_i32(nvalid)), G, N, Cout,
-                  dbias.data_ptr(), dbias.stride(0), _stream())
-        return None
-    rc = NOT_HANDLED
-    if _PCONV and stride == 1 and kh == 3 and kw == 3 and pad == 1 and H == W and Ho == H:
-        # halo-tiled transposed-read wgrad (csrc/kernels/pwgrad.hip)
-        rc = _call("dba_pwgrad", dy.data_ptr(), N * Ho * Wo * Cout, x.data_ptr(), N * H * W * Cin, dw.data_ptr(),
-                   dw.stride(0), _ptr(_i32(nvalid)), _zeros(dy.device).data_ptr(), G, N, H, W, Cin, Cout, _stream())
-    if rc == NOT_HANDLED and _WGRAD3:
-        # generation-3 im2col wgrad: strided convs, shortcuts, stem (csrc/kernels/wgrad3.hip)
-        rc = _call("dba_wgrad3", dy.data_ptr(), N * Ho * Wo * Cout, x.data_ptr(), N * H * W * Cin, dw.data_ptr(),
-                   dw.stride(0), _ptr(_i32(nvalid)), _zeros(dy.device).data_ptr(), G, N, H, W, Cin, Ho, Wo, Cout,
-                   kh, kw, stride, pad, _stream())
-    if rc == NOT_HANDLED:
-        _call("dba_conv_wgrad", dy.data_ptr(), N * Ho * Wo * Cout, x.data_ptr(), N * H * W * Cin, dw.data_ptr(),
-              dw.stride(0), _ptr(_i32(nvalid)), G, N, H, W, Cin, Ho, Wo, Cout, kh, kw, stride, pad, _stream())
+    mchunk = ctypes.c_int(0)
+    n = int(_L.dba_xwgrad_ws_floats(G, N, Ho, Wo, Cin, Cout, kh, kw, ctypes.byref(mchunk)))
+    wsb = torch.empty(n, dtype=_F32, device=dy.device) if n > 0 else None
+    nv = _i32(nvalid)
+    ad = ax = None
+    if _MODE == F16_PAIR and "wgrad" in _H_OPS:
+        ad = _amax_act(dy, nvalid)
+        ax = lx.stat.bound if lx is not None else _amax_act(x, nvalid)
+    _call("dba_xwgrad", dy.data_ptr(), N * Ho * Wo * Cout, x.data_ptr(), N * H * W * Cin, dw.data_ptr(),
+          dw.stride(0), _ptr(nv), G, N, H, W, Cin, Ho, Wo, Cout, kh, kw, stride, pad, *_aptr(ad), *_aptr(ax),
+          _ptr(wsb), n, int(defer is not None and n > 0),
+          _ptr(lx.stat.coef) if lx is not None else None, int(lx.relu) if lx is not None else 0, _stream())
+    if defer is not None and n > 0:
+        per = Cout * kh * kw * Cin
+        # (keeps the slab workspace and nvalid alive until the flush)
+        defer.append(([wsb.data_ptr(), dw.data_ptr(), dw.stride(0), per, _ptr(nv) or 0, N, Ho * Wo,
+                       mchunk.value, G, 0], wsb, nv))
     if dbias is not None:
         assert dbias.dtype == torch.float32 and dbias.stride(1) == 1
-        _call("dba_colsum", dy.data_ptr(), N * Ho * Wo * Cout, Ho * Wo, _ptr(_i32(nvalid)), G, N, Cout,
+        _call("dba_xcolsum", dy.data_ptr(), N * Ho * Wo * Cout, Ho * Wo, _ptr(_i32(nvalid)), G, N, Cout,
               dbias.data_ptr(), dbias.stride(0), _stream())
+    return None
 
 
 # ------------------------------------------------------------ fused training BN (bnfuse.hpp)
@@ -1066,85 +791,6 @@ def _same_stride(*ts: Tensor) -> int:
     return s
 
 
-# rows per replica up to which BN runs as one launch (bn_small_*: ResNet stage 4 at batch 64)
-_BN_SMALL_ROWS = int(os.environ.get("DBA_BN_SMALL_ROWS", "1024"))
-# BN statistics finalised by the last reduce block instead of a separate launch
-# (DBA_BN_LAST_BLOCK=1: on).  Off: measured slower — lone step 1.84 -> 1.94 ms, 10-client
-# step 6.72 -> 9.40 ms (profiles/r2c_bn_last_block_rejected.md): the device-scope release
-# fence every block issues before its arrival writes back its XCD's L2
-_BN_LAST_BLOCK = os.environ.get("DBA_BN_LAST_BLOCK", "0") == "1"
-# fp32 training BN statistics folded into the producing conv's epilogue (DBA_BN_FUSED=0: off)
-_BN_FUSED_STATS = os.environ.get("DBA_BN_FUSED", "1") != "0"
-
-
-def _bn_layout(C: int) -> None:
-    # the kernels' channel contract (bn.hip bn_layout_ok): 8-channel vectors, and a thread of
-    # the grid-stride passes always owns the same 8 channels
-    if C % 8 != 0 or C > 2048 or 256 % (C // 8) != 0:
-        raise ValueError(f"BN over {C} channels: need C % 8 == 0, C <= 2048 and 256 % (C/8) == 0")
-
-
-def bn_train(y, gamma, beta, rmean, rvar, nvalid, momentum, eps, relu, residual):
-    y = _act(y, None, "bn input")
-    G, N, H, W, C = y.shape
-    _bn_layout(C)
-    f32 = _f32(y)
-    ps = _same_stride(gamma, beta, rmean, rvar)
-    mean = torch.empty(G, C, dtype=torch.float32, device=y.device)
-    invstd = torch.empty(G, C, dtype=torch.float32, device=y.device)
-    nv = _ptr(_i32(nvalid))
-    out = torch.empty_like(y)
-    res = _act(residual, y.dtype, "bn residual") if residual is not None else None
-    am = _amax_out(out)
-    if N * H * W <= _BN_SMALL_ROWS:
-        # one launch: a block owns 8 channels of a replica for all its rows
-        _call("dba_bn_small_fwd", y.data_ptr(), nv, G, N, H * W, C, gamma.data_ptr(), beta.data_ptr(),
-              rmean.data_ptr(), rvar.data_ptr(), ps, float(momentum), float(eps), _ptr(res), int(relu),
-              out.data_ptr(), mean.data_ptr(), invstd.data_ptr(), f32, *_aptr(am), _stream())
-        return out, mean, invstd
-    fused = getattr(y, "_dba_bnpart", None)
-    if fused is not None and os.environ.get("DBA_BN_FUSED_DRY") != "1":
-        # statistics already folded by the conv epilogue: finalise them (no pass over y)
-        part, nblk = fused
-        _call("dba_bn_finalize_part", part.data_ptr(), nblk, nv, G, N, H * W, C, rmean.data_ptr(), rvar.data_ptr(),
-              ps, float(momentum), float(eps), mean.data_ptr(), invstd.data_ptr(), _stream())
-    else:
-        nblk = _L.dba_bn_partial_blocks(N, H * W, C)
-        part = torch.empty(G * nblk * 2 * C, dtype=torch.float32, device=y.device)
-        _call("dba_bn_stats", y.data_ptr(), nv, G, N, H * W, C, part.data_ptr(), rmean.data_ptr(), rvar.data_ptr(),
-              ps, float(momentum), float(eps), mean.data_ptr(), invstd.data_ptr(), f32,
-              _ptr(_bn_counter(G, y.device)), _stream())
-    _call("dba_bn_apply", y.data_ptr(), mean.data_ptr(), invstd.data_ptr(), gamma.data_ptr(), beta.data_ptr(), ps,
-          _ptr(res), int(relu), out.data_ptr(), nv, G, N, H * W, C, f32, *_aptr(am), _stream())
-    return out, mean, invstd
-
-
-def bn_train_bwd(dout, y, out, mean, invstd, gamma, nvalid, relu, dgamma, dbeta, want_dres=False):
-    y = _act(y, None, "bn input")
-    dout = _act(dout, y.dtype, "bn dout")
-    out = _act(out, y.dtype, "bn output")
-    G, N, H, W, C = y.shape
-    _bn_layout(C)
-    f32 = _f32(y)
-    ps = _same_stride(gamma)
-    gs = _same_stride(dgamma, dbeta)
-    dy = torch.empty_like(y)
-    dres = torch.empty_like(y) if want_dres else None
-    am = _amax_out(dy)
-    if N * H * W <= _BN_SMALL_ROWS:
-        _call("dba_bn_small_bwd", dout.data_ptr(), out.data_ptr(), y.data_ptr(), mean.data_ptr(), invstd.data_ptr(),
-              gamma.data_ptr(), ps, int(relu), dgamma.data_ptr(), dbeta.data_ptr(), gs, dy.data_ptr(), _ptr(dres),
-              _ptr(_i32(nvalid)), G, N, H * W, C, f32, *_aptr(am), _stream())
-        return (dy, dres) if want_dres else dy
-    nblk = _L.dba_bn_partial_blocks(N, H * W, C)
-    part = torch.empty(G * (nblk + 1) * 2 * C, dtype=torch.float32, device=y.device)
-    _call("dba_bn_bwd", dout.data_ptr(), out.data_ptr(), y.data_ptr(), mean.data_ptr(), invstd.data_ptr(),
-          gamma.data_ptr(), ps, int(relu), dgamma.data_ptr(), dbeta.data_ptr(), gs, dy.data_ptr(), _ptr(dres),
-          part.data_ptr(), _ptr(_i32(nvalid)), G, N, H * W, C, f32, *_aptr(am), _ptr(_bn_counter(G, y.device)),
-          _stream())
-    return (dy, dres) if want_dres else dy
-
-
 def relu_mask_bwd(dout, out):
     dout = _act(dout, None, "relu dout")
     out = _act(out, dout.dtype, "relu output")
@@ -1155,8 +801,8 @@ def relu_mask_bwd(dout, out):
 
 def bn_fold(w, conv_bias, gamma, beta, rmean, rvar, eps, out_dtype):
     assert w.dtype == torch.float32 and _inner_contig(w)
-    if out_dtype not in (_BF16, _F32):
-        raise TypeError(f"bn_fold: unsupported weight dtype {out_dtype}")
+    if out_dtype != _F32:
+        raise TypeError(f"bn_fold: fp32 weights only (got {out_dtype})")
     slots, Cout = w.shape[0], w.shape[1]
     K = int(torch.tensor(w.shape[2:]).prod())
     ss = _same_stride(gamma, beta, rmean, rvar)
@@ -1247,14 +893,13 @@ def dropout_bwd(dy, p, seeds, salt):
 # ---------------------------------------------------------------------------- loss
 def softmax_xent(logits, labels, mean, want_grad, stats=None, slot=None, nvalid=None, grad_dtype=None,
                  loss_dtype=None):
-    """``grad_dtype``: dtype of dlogits (the compute dtype of the backward pass; bf16 if
-    unset).  ``loss_dtype`` fp64 returns the per-group loss unrounded (evaluation sums)."""
+    """``grad_dtype``: dtype of dlogits (fp32, the compute dtype of the backward pass).  ``loss_dtype`` fp64 returns the per-group loss unrounded (evaluation sums)."""
     if logits.dtype != _F32:
         raise TypeError("softmax_xent: logits must be fp32 (the final layer emits fp32)")
     lf = logits.contiguous()
     G, B, C = lf.shape
-    gdt = grad_dtype or _BF16
-    if gdt not in (_BF16, _F32):
+    gdt = grad_dtype or _F32
+    if gdt != _F32:
         raise TypeError(f"softmax_xent: unsupported grad dtype {gdt}")
     loss = torch.empty(G, dtype=torch.float32, device=lf.device)
     loss64 = torch.empty(G, dtype=torch.float64, device=lf.device) if loss_dtype == torch.float64 else None
@@ -1273,15 +918,13 @@ def softmax_xent(logits, labels, mean, want_grad, stats=None, slot=None, nvalid=
 
 
 # ------------------------------------------------------------------------- optimizer
-def sgd_step(params, grads, mom, lr, first, active, momentum, wd, shadow=None, fg_accum=None):
+def sgd_step(params, grads, mom, lr, first, active, momentum, wd, fg_accum=None):
     G, P = grads.shape
     assert params.dtype == torch.float32 and params.stride(1) == 1 and params.stride(0) % 4 == 0
     assert grads.is_contiguous() and mom.is_contiguous() and P % 4 == 0
-    if shadow is not None:
-        assert shadow.is_contiguous() and shadow.dtype == _BF16
     _call("dba_sgd_step", params.data_ptr(), params.stride(0), grads.data_ptr(), mom.data_ptr(),
           lr.float().contiguous().data_ptr(), _i32(first).data_ptr(), _i32(active).data_ptr(), float(momentum),
-          float(wd), _ptr(shadow), _ptr(fg_accum), G, P, _stream())
+          float(wd), _ptr(fg_accum), G, P, _stream())
 
 
 def dist_loss_grad(w, base, grads, trig, active, alpha):

@@ -8,11 +8,14 @@ reference (:mod:`dba_mod_amd.ops.reference`), so ``torch.ops.dba.conv2d(x, w, ..
 the MFMA kernel for a GPU tensor and the reference for a CPU tensor — one call site, no
 duplicated model code.  Mutating ops declare what they write (``mutates_args``).
 
-The framework's own hot path (``models/program.py`` via :mod:`dba_mod_amd.ops`) dispatches
-to the same two implementations directly: inside a captured HIP graph of a training step
-the per-call dispatcher overhead buys nothing.  ``tests/test_library.py`` (CPU) and
-``tests/test_gpu_kernels.py::test_torch_library_ops_run_hip`` check that both entry points
-give the same results.
+This registration is the framework's EXTERNAL tensor API: the model programs
+(``models/program.py`` via :mod:`dba_mod_amd.ops`) call the same two implementations directly,
+because their training path passes values a schema cannot carry — lazy BN outputs and finished
+gradients (:mod:`dba_mod_amd.ops.bnstate`), operand-max slots and fp16-pair activations attached
+to tensors — so a ``torch.ops.dba`` call there would have to materialise what the fused kernels
+never store.  ``tests/test_library.py`` (CPU) and
+``tests/test_gpu_kernels.py::test_torch_library_ops_run_hip`` check that both entry points give
+the same results.
 
 Reference call sites of the ops (stock PyTorch there): conv ``models/resnet_cifar.py:19-33``,
 BN ``:32-35``, CE ``image_train.py:85``, SGD ``image_train.py:33-35,102``, trigger
@@ -102,17 +105,43 @@ conv2d_wgrad = _both(
 
 
 # ------------------------------------------------------------------------ batch norm
-def _bn_train(y: Tensor, gamma: Tensor, beta: Tensor, rmean: Tensor, rvar: Tensor, nvalid: Optional[Tensor],
-              momentum: float, eps: float, relu: bool, residual: Optional[Tensor]) -> Tuple[Tensor, Tensor, Tensor]:
-    """Training BatchNorm (+residual, +ReLU) over the valid rows (K5/K6); running stats in place."""
-    return _impl("bn_train", y)(y, gamma, beta, rmean, rvar, nvalid, momentum, eps, relu, residual)
+def _bn_params(gamma, beta, rmean, rvar, momentum, eps):
+    from .bnstate import BnParams
+    z = torch.zeros_like(gamma)
+    return BnParams(gamma, beta, rmean, rvar, z, z.clone(), momentum, eps)
 
 
-bn_train = _both(
-    "bn_train",
-    lambda *a: tuple(t.clone() for t in _ref.bn_train(*a)),
-    lambda *a: tuple(_hip().bn_train(*a)),
-    _bn_train, mutates=("rmean", "rvar"))
+def _conv_bn_stats(x: Tensor, w: Tensor, wsel: Optional[Tensor], stride: int, pad: int, nvalid: Optional[Tensor],
+                   gamma: Tensor, beta: Tensor, rmean: Tensor, rvar: Tensor, momentum: float,
+                   eps: float) -> Tuple[Tensor, Tensor]:
+    """Training conv + BatchNorm statistics in one pass (K1/K5, csrc/kernels/bnfuse.hpp):
+    y = conv(x, w[wsel]) and the BN's coefficient rows [G, 9, C] (mean, 1/std, scale, shift,
+    max y, min y, ...); running stats updated in place.  The BN output is
+    relu?(y * scale + shift) (``bn_apply``)."""
+    return _impl("conv_bn_stats", x)(x, w, wsel, stride, pad, nvalid, gamma, beta, rmean, rvar, momentum, eps)
+
+
+def _cbs(mod, x, w, wsel, stride, pad, nvalid, gamma, beta, rmean, rvar, momentum, eps):
+    y, st = mod.conv_bn_stats(x, w, wsel, stride, pad, nvalid, _bn_params(gamma, beta, rmean, rvar, momentum, eps),
+                              False)
+    return y, st.coef.float().clone()
+
+
+conv_bn_stats = _both("conv_bn_stats", lambda *a: _cbs(_ref, *a), lambda *a: _cbs(_hip(), *a), _conv_bn_stats,
+                      mutates=("rmean", "rvar"))
+
+
+def _bn_apply(y: Tensor, coef: Tensor, residual: Optional[Tensor], relu: bool, nvalid: Optional[Tensor]) -> Tensor:
+    """relu?(y * scale + shift + residual) of a training BN from its coefficient rows (K6)."""
+    return _impl("bn_apply", y)(y, coef, residual, relu, nvalid)
+
+
+def _bapp(mod, y, coef, residual, relu, nvalid):
+    from .bnstate import BnStat, LazyBN
+    return mod.bn_apply(LazyBN(y, BnStat(coef.to(y.dtype), None), False), residual, relu, nvalid)
+
+
+bn_apply = _both("bn_apply", lambda *a: _bapp(_ref, *a), lambda *a: _bapp(_hip(), *a), _bn_apply)
 
 
 # ------------------------------------------------------------------ data / loss / optim
@@ -190,5 +219,5 @@ def _gram(feats: Tensor) -> Tensor:
 gram = _both("gram", lambda f: _ref.gram(f), lambda f: _hip().gram(f), _gram)
 
 
-OPS: List[str] = ["conv2d", "conv2d_dgrad", "conv2d_wgrad", "bn_train", "gather_images", "softmax_xent",
-                  "sgd_step", "delta_sum", "sq_dists", "weighted_sum", "gram"]
+OPS: List[str] = ["conv2d", "conv2d_dgrad", "conv2d_wgrad", "conv_bn_stats", "bn_apply", "gather_images",
+                  "softmax_xent", "sgd_step", "delta_sum", "sq_dists", "weighted_sum", "gram"]

@@ -315,70 +315,6 @@ def conv2d_wgrad(dy, x, stride: int, pad: int, kh: int, kw: int,
 
 
 # ------------------------------------------------------------------------ batch norm
-def bn_train(y: Tensor, gamma: Tensor, beta: Tensor, rmean: Tensor, rvar: Tensor,
-             nvalid: Optional[Tensor], momentum: float, eps: float, relu: bool,
-             residual: Optional[Tensor]) -> Tuple[Tensor, Tensor, Tensor]:
-    """Training-mode BN over valid rows (+residual, +ReLU); updates running stats in place."""
-    G, N = y.shape[:2]
-    C = y.shape[-1]
-    out = torch.zeros_like(y)
-    means = torch.zeros(G, C, dtype=_cdt(), device=y.device)
-    invstds = torch.zeros(G, C, dtype=_cdt(), device=y.device)
-    for g in range(G):
-        n = _rows_valid(nvalid, g, N)
-        if n == 0:
-            continue
-        yg = y[g, :n].to(_cdt())
-        flat = yg.reshape(-1, C)
-        cnt = flat.shape[0]
-        mean = flat.mean(0)
-        var = flat.var(0, unbiased=False)
-        invstd = torch.rsqrt(var + eps)
-        o = (yg - mean) * invstd * gamma[g].to(_cdt()) + beta[g].to(_cdt())
-        if residual is not None:
-            o = o + residual[g, :n].to(_cdt())
-        if relu:
-            o = torch.relu(o)
-        out[g, :n] = o.to(out.dtype)
-        unbiased = var * (cnt / max(cnt - 1, 1))
-        rmean[g] = (1 - momentum) * rmean[g] + momentum * mean
-        rvar[g] = (1 - momentum) * rvar[g] + momentum * unbiased
-        means[g] = mean
-        invstds[g] = invstd
-    return out, means, invstds
-
-
-def bn_train_bwd(dout: Tensor, y: Tensor, out: Tensor, mean: Tensor, invstd: Tensor,
-                 gamma: Tensor, nvalid: Optional[Tensor], relu: bool, dgamma: Tensor,
-                 dbeta: Tensor, want_dres: bool = False):
-    """Backward of bn_train: d(pre-BN input); with ``want_dres`` also the grad flowing into
-    the residual branch (the ReLU-masked ``dout``)."""
-    G, N = y.shape[:2]
-    C = y.shape[-1]
-    dy = torch.zeros_like(y)
-    dres = None
-    if want_dres:
-        dres = relu_mask_bwd(dout, out) if relu else dout.clone()
-    for g in range(G):
-        n = _rows_valid(nvalid, g, N)
-        if n == 0:
-            continue
-        d = dout[g, :n].to(_cdt())
-        if relu:
-            d = d * (out[g, :n].to(_cdt()) > 0)
-        xhat = (y[g, :n].to(_cdt()) - mean[g]) * invstd[g]
-        cnt = d.numel() // C
-        sd = d.reshape(-1, C).sum(0)
-        sdx = (d * xhat).reshape(-1, C).sum(0)
-        dgamma[g] += sdx
-        dbeta[g] += sd
-        dx = gamma[g].to(_cdt()) * invstd[g] / cnt * (cnt * d - sd - xhat * sdx)
-        dy[g, :n] = dx.to(dy.dtype)
-    if want_dres:
-        return dy, dres
-    return dy
-
-
 def relu_mask_bwd(dout: Tensor, out: Tensor) -> Tensor:
     return (dout.to(_cdt()) * (out.to(_cdt()) > 0)).to(dout.dtype)
 
@@ -490,8 +426,7 @@ def accumulate_step_stats(stats: Tensor, slot: Tensor, loss: Tensor, correct: Te
 
 # ------------------------------------------------------------------------- optimizer
 def sgd_step(params: Tensor, grads: Tensor, mom: Tensor, lr: Tensor, first: Tensor, active: Tensor,
-             momentum: float, wd: float, shadow: Optional[Tensor] = None,
-             fg_accum: Optional[Tensor] = None) -> None:
+             momentum: float, wd: float, fg_accum: Optional[Tensor] = None) -> None:
     """torch.optim.SGD(momentum, weight_decay) on [G, P] flat buffers (K10).
 
     ``first[g]`` marks the first step of a freshly created optimizer (buffer := d_p).
@@ -509,8 +444,6 @@ def sgd_step(params: Tensor, grads: Tensor, mom: Tensor, lr: Tensor, first: Tens
         else:
             mom[g] = momentum * mom[g] + dp
         params[g] -= float(lr[g]) * mom[g]
-        if shadow is not None:
-            shadow[g] = params[g].to(shadow.dtype)
 
 
 def dist_loss_grad(w: Tensor, base: Tensor, grads: Tensor, trig: Tensor, active: Tensor,

@@ -101,49 +101,16 @@ def main(argv=None) -> int:
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--json", default=None)
     ap.add_argument("--only", default="", help="substring filter on shape names")
-    ap.add_argument("--dtype", choices=("bf16", "fp32"), default="bf16",
-                    help="fp32: the reference-precision family (xgemm.hip)")
-    ap.add_argument("--planes", type=int, default=3, help="fp32 split: 2 / 3 bf16 planes or 16 (fp16 pair)")
+    ap.add_argument("--planes", type=int, default=16, help="fp32 split: 2 / 3 bf16 planes or 16 (fp16 pair)")
     args = ap.parse_args(argv)
     dev = torch.device("cuda")
     rows = []
-    if args.dtype == "fp32":
-        H.set_fp32_planes(args.planes)
+    H.set_fp32_planes(args.planes)
     for name, G, N, Hh, Cin, Cout, k, s, p in SHAPES:
         if args.only not in name:
             continue
-        if args.dtype == "fp32":
-            rows.append(_bench_fp32(name, G, N, Hh, Cin, Cout, k, s, p, args.reps, dev))
-            print(json.dumps(rows[-1]), flush=True)
-            continue
-        torch.manual_seed(0)
-        x = torch.randn(G, N, Hh, Hh, Cin, device=dev).bfloat16()
-        w = (torch.randn(G, Cout, k, k, Cin, device=dev) * 0.05).bfloat16()
-        Ho = (Hh + 2 * p - k) // s + 1
-        dy = torch.randn(G, N, Ho, Ho, Cout, device=dev).bfloat16()
-        flops = 2.0 * G * N * Ho * Ho * Cout * k * k * Cin
-        rec = {"shape": name}
-        for tag, pc, g3 in (("fwd", True, True), ("fwd_nopconv", False, True), ("fwd_nogemm3", True, False)):
-            H._PCONV, H._GEMM3 = pc, g3
-            t = _time(lambda: H.conv2d(x, w, None, s, p, relu=True), args.reps)
-            rec[tag + "_us"] = round(t * 1e6, 1)
-            rec[tag + "_tflops"] = round(flops / t / 1e12, 1)
-        H._GEMM3 = True
-        for tag, pc in (("dgrad", True), ("dgrad_nopconv", False)):
-            H._PCONV = pc
-            t = _time(lambda: H.conv2d_dgrad(dy, w, None, s, p, (Hh, Hh)), args.reps)
-            rec[tag + "_us"] = round(t * 1e6, 1)
-            rec[tag + "_tflops"] = round(flops / t / 1e12, 1)
-        if name.startswith("train"):
-            dw = torch.zeros(G, Cout, k, k, Cin, device=dev)
-            for tag, pc, w3 in (("wgrad", True, True), ("wgrad_nowg3", True, False), ("wgrad_old", False, False)):
-                H._PCONV, H._WGRAD3 = pc, w3
-                t = _time(lambda: H.conv2d_wgrad(dy, x, s, p, k, k, dw), args.reps)
-                rec[tag + "_us"] = round(t * 1e6, 1)
-                rec[tag + "_tflops"] = round(flops / t / 1e12, 1)
-        H._PCONV, H._WGRAD3 = True, True
-        rows.append(rec)
-        print(json.dumps(rec), flush=True)
+        rows.append(_bench_fp32(name, G, N, Hh, Cin, Cout, k, s, p, args.reps, dev))
+        print(json.dumps(rows[-1]), flush=True)
     if args.json:
         with open(args.json, "w") as f:
             json.dump(rows, f, indent=1)

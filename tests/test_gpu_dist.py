@@ -5,8 +5,9 @@ global tests with owner broadcasts of the sharded clients' snapshots, the reduct
 aggregations (fp64 FedAvg delta all-reduce, distributed Weiszfeld, FoolsGold feature +
 weighted-sum all-reduces) and the counter all-reduce exactly as the 8-GPU run does, and checks
 the world-2 run against a world-1 run of the same rounds: FedAvg's global model BITWISE (its
-hash) and every round's metrics; RFA / FoolsGold combine rank partial sums in a world-dependent
-order (tests/test_distributed.py), so their models agree to fp32 rounding.  Also the launch forms the round driver uses for the scaling bench:
+hash) and every round's metrics; RFA / FoolsGold add fp64 rank partial sums in a world-dependent
+order (tests/test_distributed.py) and round once to fp32, so their models agree to within an
+occasional last-bit difference.  Also the launch forms the round driver uses for the scaling bench:
 ``python bench.py --gpus N`` (self-spawn) and a --gpus / WORLD_SIZE mismatch."""
 import json
 import os
@@ -70,7 +71,8 @@ def test_two_ranks_share_one_gpu():
 def test_cifar_world2(tmp_path, agg, extra):
     """The flagship CIFAR ResNet-18 rounds (fused training BN, attacker 17's model replacement)
     at world 2 (gloo on the shared GPU) vs world 1: FedAvg bitwise; distributed RFA and
-    FoolsGold to fp32 rounding (their rank partial sums meet in a world-dependent order)."""
+    FoolsGold to an occasional last-bit difference (fp64 rank partial sums meet in a
+    world-dependent order, then round once to fp32)."""
     import torch
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
@@ -83,7 +85,7 @@ def test_cifar_world2(tmp_path, agg, extra):
     assert two["world"] == 2 and one["dtype"] == two["dtype"] == "fp32"
     s1 = torch.load(tmp_path / "w1.pt", weights_only=True)
     s2 = torch.load(tmp_path / "w2.pt", weights_only=True)
-    assert ((s1 - s2).norm() / s1.norm()).item() < 1e-5
+    assert ((s1 - s2).norm() / s1.norm()).item() < 1e-6
     for (e1, a1, _), (e2, a2, _) in zip(one["rounds"], two["rounds"]):
         assert e1 == e2 and abs(a1 - a2) <= 0.5
 

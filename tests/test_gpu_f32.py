@@ -278,92 +278,6 @@ def test_fp32_group_size_independent_bits(H, planes, case):
         H.set_fp32_planes(prev)
 
 
-@pytest.mark.parametrize("case", [(3, 8, 32, 32, 32, 32, 3, 1, 1), (2, 8, 32, 32, 32, 64, 3, 2, 1),
-                                  (2, 16, 16, 16, 64, 64, 3, 1, 1), (1, 64, 16, 16, 64, 64, 3, 1, 1)])
-def test_fp32_bn_stats_folded_in_conv_epilogue(H, R64, case):
-    """Training BN statistics folded into the conv epilogue (per-32-pixel partials, finalised
-    without a pass over y) match the fp64 oracle's batch statistics and running-stat update,
-    and the BN output matches the separate-reduction path to fp32 rounding."""
-    dev = torch.device("cuda")
-    G, N, Hh, Ww, Cin, Cout, k, s, p = case
-    x, w, wsel, bias, nvalid, res, dy, acc = _inputs(case, dev, seed=11)
-    gamma = (1 + 0.1 * torch.randn(G, Cout)).to(dev)
-    beta = (0.1 * torch.randn(G, Cout)).to(dev)
-    prev = H._BN_FUSED_STATS
-    H._BN_FUSED_STATS = True
-    try:
-        y = H.conv2d(x, w, wsel, s, p, nvalid=nvalid, bn_stats=True)
-    finally:
-        H._BN_FUSED_STATS = prev
-    fused = hasattr(y, "_dba_bnpart")
-    y2 = y.clone()                                    # same values, no folded partials
-    outs = []
-    for t in (y, y2):
-        rm, rv = torch.zeros(G, Cout, device=dev), torch.ones(G, Cout, device=dev)
-        out, mean, invstd = H.bn_train(t, gamma, beta, rm, rv, nvalid, 0.1, 1e-5, True, None)
-        outs.append((out, mean, invstd, rm, rv))
-    for g in range(G):
-        n = int(nvalid[g])
-        yv = y[g, :n].double().cpu().reshape(-1, Cout)
-        m = yv.mean(0)
-        var = yv.var(0, unbiased=False)
-        for out, mean, invstd, rm, rv in outs:
-            assert _rel(mean[g], m) < 1e-6 and _rel(invstd[g], 1 / (var + 1e-5).sqrt()) < 1e-6, (case, g, fused)
-            assert _rel(rm[g], 0.1 * m) < 1e-6
-            assert _rel(rv[g], 0.9 + 0.1 * yv.var(0, unbiased=True)) < 1e-6
-        assert _rel(outs[0][0][g, :n], outs[1][0][g, :n]) < 1e-6
-    Ho = (Hh + 2 * p - k) // s + 1
-    split = int(H._L.dba_xconv_ws_floats(G, N, Ho, Ho, Cin, Cout, k, k)) > 0
-    if N * Ho * Ho > 1024 and not split:
-        assert fused, "the conv did not fold BN statistics"
-
-
-@pytest.mark.parametrize("shape", [(3, 16, 32, 32, 32), (3, 16, 16, 16, 64), (2, 64, 8, 8, 128), (3, 8, 8, 8, 512)])
-def test_bn_last_block_finalize(H, shape):
-    """BN statistics finalised by the last reduce block (inside a training step's zeroed
-    arena: one launch per BN pass) match the separate finalize launch to fp32 rounding —
-    forward statistics, running stats, backward dgamma / dbeta / dy — for a full, a partly
-    valid and an inactive replica, and are bitwise reproducible."""
-    dev = torch.device("cuda")
-    G, N, Hh, Ww, C = shape
-    gen = torch.Generator().manual_seed(3)
-    y = (torch.randn(G, N, Hh, Ww, C, generator=gen) * 2 + 0.5).to(dev)
-    dout = torch.randn(G, N, Hh, Ww, C, generator=gen).to(dev)
-    gamma = (1 + 0.1 * torch.randn(G, C, generator=gen)).to(dev)
-    beta = (0.1 * torch.randn(G, C, generator=gen)).to(dev)
-    nvalid = torch.tensor([N, N // 2 + 1, 0][:G], dtype=torch.int32, device=dev)
-    prev = H.set_fp32_planes(16)
-    prev_lb = H._BN_LAST_BLOCK
-    H._BN_LAST_BLOCK = True   # opt-in path (measured slower, kept correct)
-
-    def run(arena):
-        rm, rv = torch.zeros(G, C, device=dev), torch.ones(G, C, device=dev)
-        dg, db = torch.zeros(G, C, device=dev), torch.zeros(G, C, device=dev)
-        ctx = H.amax_arena(G, dev) if arena else __import__("contextlib").nullcontext()
-        with ctx:
-            out, mean, invstd = H.bn_train(y, gamma, beta, rm, rv, nvalid, 0.1, 1e-5, True, None)
-            dy = H.bn_train_bwd(dout, y, out, mean, invstd, gamma, nvalid, True, dg, db)
-        return out, mean, invstd, rm, rv, dg, db, dy
-    try:
-        a, b, c = run(False), run(True), run(True)
-    finally:
-        H.set_fp32_planes(prev)
-        H._BN_LAST_BLOCK = prev_lb
-    for g in range(G):
-        n = int(nvalid[g])
-        if n == 0:
-            assert b[5][g].abs().max().item() == 0 and torch.equal(b[3][g], a[3][g]) and torch.equal(b[4][g], a[4][g])
-            continue
-        for k, (u, v) in enumerate(zip(a, b)):
-            rows = u[g, :n] if u.dim() > 2 else u[g]
-            assert _rel(v[g, :n] if v.dim() > 2 else v[g], rows) < 2e-6, (shape, g, k)
-    for u, v in zip(b, c):
-        for g in range(G):
-            n = int(nvalid[g])
-            if n:
-                assert torch.equal(u[g, :n] if u.dim() > 2 else u[g], v[g, :n] if v.dim() > 2 else v[g])
-
-
 def test_fp32_no_silent_downcast(H):
     """fp32 activations never reach a bf16 kernel, and mixed operands are refused."""
     dev = torch.device("cuda")
@@ -375,43 +289,6 @@ def test_fp32_no_silent_downcast(H):
         H.conv2d(x.bfloat16(), w16.float(), None, 1, 1)
     with pytest.raises(TypeError):
         H.conv2d(x, w16.float(), None, 1, 1, out_dtype=torch.bfloat16)
-
-
-@pytest.mark.parametrize("C,Hh,N", [(32, 32, 6), (64, 16, 20), (256, 4, 64), (128, 8, 9)])
-@pytest.mark.parametrize("relu,with_res", [(True, False), (True, True), (False, False)])
-def test_fp32_bn_train(H, R64, C, Hh, N, relu, with_res):
-    dev = torch.device("cuda")
-    G = 3
-    torch.manual_seed(1)
-    y = torch.randn(G, N, Hh, Hh, C, device=dev) * 2 + 0.5
-    nvalid = torch.tensor([N, max(1, N - 3), 0], dtype=torch.int32, device=dev)
-    gamma = torch.rand(G, C, device=dev) + 0.5
-    beta = torch.randn(G, C, device=dev)
-    rm = torch.randn(G, C, device=dev)
-    rv = torch.rand(G, C, device=dev) + 0.5
-    rm_r, rv_r = _c(rm), _c(rv)
-    res = torch.randn_like(y) if with_res else None
-    out, mean, invstd = H.bn_train(y, gamma, beta, rm, rv, nvalid, 0.1, 1e-5, relu, res)
-    out_r, mean_r, inv_r = R64.bn_train(_c(y), _c(gamma), _c(beta), rm_r, rv_r, nvalid.cpu(), 0.1, 1e-5, relu,
-                                        _c(res))
-    for g in range(2):
-        n = int(nvalid[g])
-        assert _rel(out[g, :n], out_r[g, :n]) < 2e-6
-        assert _rel(mean[g], mean_r[g]) < 2e-6 and _rel(invstd[g], inv_r[g]) < 2e-6
-        assert _rel(rm[g], rm_r[g]) < 2e-6 and _rel(rv[g], rv_r[g]) < 2e-6
-    dout = torch.randn_like(y)
-    dg, dbt = torch.zeros(G, C, device=dev), torch.zeros(G, C, device=dev)
-    r = H.bn_train_bwd(dout, y, out, mean, invstd, gamma, nvalid, relu, dg, dbt, want_dres=with_res)
-    dg_r, db_r = torch.zeros(G, C, dtype=torch.float64), torch.zeros(G, C, dtype=torch.float64)
-    rr = R64.bn_train_bwd(_c(dout), _c(y), out_r, mean_r, inv_r, _c(gamma), nvalid.cpu(), relu, dg_r, db_r,
-                          want_dres=with_res)
-    dyh, dyr = (r[0], rr[0]) if with_res else (r, rr)
-    for g in range(2):
-        n = int(nvalid[g])
-        assert _rel(dyh[g, :n], dyr[g, :n]) < 1e-5
-        assert _rel(dg[g], dg_r[g]) < 1e-5 and _rel(dbt[g], db_r[g]) < 1e-5
-        if with_res:
-            assert _rel(r[1][g, :n], rr[1][g, :n]) < 1e-6
 
 
 def test_fp32_pool_relu_loss_fold(H, R64):
@@ -559,45 +436,6 @@ def test_halo_ws_bitwise_vs_tiled(H, R64, case, presplit):
         H.set_fp32_planes(prev)
 
 
-@pytest.mark.parametrize("G,C,Hh,N", [(1, 32, 32, 64), (3, 64, 16, 20), (2, 128, 8, 64), (4, 256, 8, 9)])
-@pytest.mark.parametrize("relu,with_res", [(True, False), (True, True), (False, False)])
-def test_bn_bwd_folded_finalize_bitwise(H, G, C, Hh, N, relu, with_res):
-    """Backward BN with the finalize folded into the apply (bn_bwd_apply_fin_kernel, small
-    launches) is bit-identical to reduce / finalize / apply: dy, the residual gradient, the
-    accumulated dgamma / dbeta and the fp16-pair max slot."""
-    dev = torch.device("cuda")
-    torch.manual_seed(3)
-    y = torch.randn(G, N, Hh, Hh, C, device=dev) * 1.7 - 0.2
-    nvalid = torch.tensor([N, max(1, N - 5), 0, N][:G], dtype=torch.int32, device=dev)
-    gamma = torch.rand(G, C, device=dev) + 0.5
-    beta = torch.randn(G, C, device=dev)
-    rm, rv = torch.zeros(G, C, device=dev), torch.ones(G, C, device=dev)
-    res = torch.randn_like(y) if with_res else None
-    out, mean, invstd = H.bn_train(y, gamma, beta, rm, rv, nvalid, 0.1, 1e-5, relu, res)
-    dout = torch.randn_like(y)
-    seed_g, seed_b = torch.randn(G, C, device=dev), torch.randn(G, C, device=dev)
-    res_by = []
-    prev = H.set_bn_bwd_fuse(-1)
-    try:
-        for fuse in (8, 0):
-            H.set_bn_bwd_fuse(fuse)
-            dg, db = seed_g.clone(), seed_b.clone()
-            r = H.bn_train_bwd(dout, y, out, mean, invstd, gamma, nvalid, relu, dg, db, want_dres=with_res)
-            dyh, dres = r if with_res else (r, None)
-            res_by.append((dyh, dres, dg, db, getattr(dyh, "_dba_amax", None)))
-    finally:
-        H.set_bn_bwd_fuse(prev)
-    (a, ra, ga, ba, ma), (b, rb, gb, bb, mb) = res_by
-    for g in range(G):
-        n = int(nvalid[g])
-        assert torch.equal(a[g, :n], b[g, :n])
-        if with_res:
-            assert torch.equal(ra[g, :n], rb[g, :n])
-    assert torch.equal(ga, gb) and torch.equal(ba, bb)
-    if ma is not None:
-        assert torch.equal(ma, mb)
-
-
 @pytest.mark.parametrize("slots,Cout,K", [(1, 32, 27), (17, 32, 288), (5, 256, 2304), (3, 10, 256), (2, 70, 33)])
 def test_row_bound(H, slots, Cout, K):
     """PairAct output bound per weight slot: {max row L1 of w, max |bias|} — an upper bound
@@ -612,35 +450,6 @@ def test_row_bound(H, slots, Cout, K):
     assert torch.equal(out[:, 1], b.abs().amax(1))
     assert torch.equal(H.row_bound(w, b), out)
     assert torch.equal(H.row_bound(w, None)[:, 1], torch.zeros(slots, device=dev))
-
-
-def test_halo_ws_bn_partials_bitwise(H):
-    """Training forward with fused BN statistics through the persistent halo conv: the fp64
-    partials (incl. the zeroed groups of invalid images) equal the per-tile kernel's."""
-    prev = H.set_fp32_planes(16)
-    prev_ws = H.set_halo_ws(-1)
-    try:
-        dev = torch.device("cuda")
-        g0 = torch.Generator().manual_seed(5)
-        G, N = 3, 12
-        x = torch.randn(G, N, 32, 32, 32, generator=g0).to(dev)
-        w = (torch.randn(G, 32, 3, 3, 32, generator=g0) * 0.06).to(dev)
-        nvalid = torch.tensor([N, 7, 0], dtype=torch.int32, device=dev)
-        parts = []
-        for on in (1, 0):
-            H.set_halo_ws(on)
-            y = H.conv2d(x.clone(), w, None, 1, 1, nvalid=nvalid, bn_stats=True)
-            part, nblk = y._dba_bnpart
-            parts.append((y, part.view(G, 32, 2, nblk).clone()))
-        (ya, pa), (yb, pb) = parts
-        for g in range(G):
-            n = int(nvalid[g])
-            assert torch.equal(ya[g, :n], yb[g, :n])
-        assert torch.equal(pa, pb)
-        assert pa[2].abs().max().item() == 0.0 and pa[1, :, :, 7 * 32:].abs().max().item() == 0.0
-    finally:
-        H.set_halo_ws(prev_ws)
-        H.set_fp32_planes(prev)
 
 
 @pytest.mark.parametrize("arch,shp", [("resnet18_cifar", (32, 32, 3)), ("resnet18_tiny", (64, 64, 3)),

@@ -119,29 +119,50 @@ def test_inlaunch_combine_graph_replay(H):
         assert torch.equal(out, ref)
 
 
-@pytest.mark.parametrize("shape", [(1, 64, 8, 128, 128, 64), (1, 64, 8, 128, 128, 37)])
-def test_inlaunch_combine_bn_stats(H, shape):
-    """A split conv feeding a training BN folds the statistics in the reducing block:
-    bn_train finalises them (no pass over y) to fp64 accuracy."""
-    G, N, Hh, Cin, Cout, nv = shape
+def test_inlaunch_combine_many_launches_in_one_graph(H):
+    """Eight consecutive in-launch split-K combines (a chain of lone-client stage-3/4 convs and
+    their data gradients, each reading the previous output) captured in ONE graph and replayed
+    repeatedly: every replay is bitwise equal to the same chain on the separate reduce kernel.
+    Each launch's hand-off (sc1 slab stores, vmcnt(0), a relaxed agent ticket, sc1 loads) must
+    hold while the previous launch's blocks drain and the next one's start (xgemm.hip
+    sk_combine; MI355X_MICROARCH.md § visibility, hand-off table row 1)."""
+    G, N = 1, 64
     dev = torch.device("cuda")
-    x, w, _, _, _, _, nvalid = _data(G, N, Hh, Cin, Cout, dev, seed=2, nv=nv)
-    gamma = torch.ones(G, Cout, device=dev)
-    beta = torch.zeros(G, Cout, device=dev)
-    with H.amax_arena(G, dev, counters=1 << 15):
-        y = H.conv2d(x, w, None, 1, 1, nvalid=nvalid, bn_stats=True)
-        assert hasattr(y, "_dba_bnpart"), "split conv did not fold BN statistics"
-        rm, rv = torch.zeros(G, Cout, device=dev), torch.ones(G, Cout, device=dev)
-        out, mean, invstd = H.bn_train(y, gamma, beta, rm, rv, nvalid, 0.1, 1e-5, False, None)
-    torch.cuda.synchronize()
-    for g in range(G):
-        n = int(nvalid[g])
-        if n == 0:
-            assert torch.all(mean[g] == 0) and torch.all(invstd[g] == 0)
-            continue
-        yv = y[g, :n].double().cpu().reshape(-1, Cout)
-        m, var = yv.mean(0), yv.var(0, unbiased=False)
-        assert ((mean[g].double().cpu() - m).norm() / m.norm()).item() < 1e-6
-        ist = 1 / (var + 1e-5).sqrt()
-        assert ((invstd[g].double().cpu() - ist).norm() / ist.norm()).item() < 1e-6
-        assert ((rv[g].double().cpu() - (0.9 + 0.1 * yv.var(0, unbiased=True))).norm()).item() < 1e-5
+    layers = []
+    g = torch.Generator().manual_seed(3)
+    for Hh, C in ((8, 128), (8, 128), (4, 256), (4, 256)):
+        w = (torch.randn(G, C, 3, 3, C, generator=g) / (9 * C) ** 0.5).to(dev)
+        layers.append((Hh, C, w))
+    x0 = torch.randn(G, N, 8, 8, 128, generator=g).to(dev)
+    x1 = torch.randn(G, N, 4, 4, 256, generator=g).to(dev)
+    nvalid = torch.tensor([N], dtype=torch.int32, device=dev)
+
+    def chain(counters):
+        outs = []
+        with H.amax_arena(G, dev, counters=counters):
+            for i, (Hh, C, w) in enumerate(layers):
+                src = (x0 if Hh == 8 else x1) if i in (0, 2) else outs[-1]
+                y = H.conv2d(src, w, None, 1, 1, relu=True, nvalid=nvalid)
+                dx = H.conv2d_dgrad(y, w, None, 1, 1, (Hh, Hh), nvalid=nvalid)
+                outs += [y, dx]
+        return outs
+
+    for Hh, C, _ in layers:
+        assert int(H._L.dba_xconv_sk_ints(G, N, Hh, Hh, C, C, 3, 3)) > 0, "shape does not split"
+    ref = [t.clone() for t in chain(0)]          # separate reduce launches
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for _ in range(2):
+            chain(1 << 14)
+    torch.cuda.current_stream().wait_stream(s)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        outs = chain(1 << 14)
+    for _ in range(6):
+        for t in outs:
+            t.fill_(float("nan"))
+        graph.replay()
+        torch.cuda.synchronize()
+        for a, b in zip(outs, ref):
+            assert torch.equal(a, b)

@@ -54,11 +54,17 @@ def test_mutating_ops():
     torch.ops.dba.sgd_step(p1, grads, m1, lr, one, one, 0.9, 5e-4)
     R.sgd_step(p2, grads, m2, lr, one, one, 0.9, 5e-4)
     assert torch.equal(p1, p2) and torch.equal(m1, m2)
-    y = torch.randn(2, 4, 4, 4, 8, generator=g)
-    gamma, beta = torch.ones(2, 8), torch.zeros(2, 8)
+    x = torch.randn(2, 3, 4, 4, 8, generator=g)
+    w = torch.randn(2, 8, 3, 3, 8, generator=g) * 0.2
+    gamma, beta = torch.rand(2, 8, generator=g) + 0.5, torch.randn(2, 8, generator=g) * 0.1
     rm1, rv1, rm2, rv2 = torch.zeros(2, 8), torch.ones(2, 8), torch.zeros(2, 8), torch.ones(2, 8)
-    out1 = torch.ops.dba.bn_train(y, gamma, beta, rm1, rv1, None, 0.1, 1e-5, True, None)
-    out2 = R.bn_train(y, gamma, beta, rm2, rv2, None, 0.1, 1e-5, True, None)
-    for a, b in zip(out1, out2):
-        assert torch.equal(a, b)
+    nv = torch.tensor([3, 2], dtype=torch.int32)
+    y1, c1 = torch.ops.dba.conv_bn_stats(x, w, None, 1, 1, nv, gamma, beta, rm1, rv1, 0.1, 1e-5)
+    from dba_mod_amd.ops.bnstate import BnParams, BnStat, LazyBN
+    z = torch.zeros(2, 8)
+    y2, st2 = R.conv_bn_stats(x, w, None, 1, 1, nv, BnParams(gamma, beta, rm2, rv2, z, z.clone(), 0.1, 1e-5), False)
+    assert torch.equal(y1, y2) and torch.equal(c1, st2.coef)
     assert torch.equal(rm1, rm2) and torch.equal(rv1, rv2) and rm1.abs().sum() > 0
+    o1 = torch.ops.dba.bn_apply(y1, c1, None, True, nv)
+    o2 = R.bn_apply(LazyBN(y2, BnStat(st2.coef, None), False), None, True, nv)
+    assert torch.equal(o1, o2)

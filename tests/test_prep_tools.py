@@ -74,11 +74,11 @@ def test_trace_streams_summary(tmp_path):
     from dba_mod_amd.tools.trace_streams import summarize
     p = tmp_path / "k.csv"
     hdr = '"Kind","Stream_Id","Kernel_Name","Start_Timestamp","End_Timestamp"\n'
-    rows = [("1", "void (anonymous namespace)::igemm3_kernel<64, 128, 3, unsigned short>(G3Args)", 0, 2_000_000),
-            ("1", "(anonymous namespace)::bn_reduce_kernel(float const*)", 2_000_000, 3_000_000),
-            ("4", "void (anonymous namespace)::pconv_kernel<32, 32>(PconvArgs)", 1_000_000, 5_000_000)]
+    rows = [("1", "void (anonymous namespace)::xconv_kernel<32, 128, 1, 4, 2, 32, true, false>(XArgs)", 0, 2_000_000),
+            ("1", "(anonymous namespace)::bnx_finalize_kernel(BnFuse)", 2_000_000, 3_000_000),
+            ("4", "void (anonymous namespace)::xhalo_kernel<32, 32, 128, 32>(XArgs)", 1_000_000, 5_000_000)]
     p.write_text(hdr + "".join(f'"KERNEL_DISPATCH",{s},"{k}",{a},{b}\n' for s, k, a, b in rows))
     md = summarize(str(p), last_ms=100)
     assert "## stream 1: 3.0 ms" in md and "## stream 4: 4.0 ms" in md
-    assert "`igemm3_kernel<64, 128, 3, unsigned short>` | 2.0 | 66.7 | 1 |" in md
+    assert "`xconv_kernel<32, 128, 1, 4, 2, 32, true, false>` | 2.0 | 66.7 | 1 |" in md
     assert "Union of kernel intervals: 5 ms of 5 ms" in md

@@ -30,9 +30,3 @@ def test_solo_tail_off_without_graphs_or_group():
     assert _tail([18, 54], use_graph=False) is None
     assert _tail([54]) is None
     assert _tail([18, 54], min_steps=0) is None
-
-
-def test_solo_tail_fp32_family_only():
-    # the bf16 family's tile / split-K choices follow the launch's replica count, so moving a
-    # client to the one-replica graph would change its rounding: no solo tail there
-    assert _tail([18, 54], dtype=torch.bfloat16) is None
