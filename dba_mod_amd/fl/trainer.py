@@ -125,6 +125,12 @@ class GroupTrainer:
         # the BN / conv producers fold on the fly)
         sm = os.environ.get("DBA_F32_TRAIN_PLANES")
         self.split_mode: Optional[int] = int(sm) if sm else None
+        # LoanNet: every client's steps between two phase events run in ONE persistent launch
+        # (csrc/kernels/mlp.hip, one workgroup per client) instead of a graph replay per step;
+        # DBA_MLP_PERSIST=0 keeps the per-step graph
+        self.persistent = (self.spec.arch == "loan" and self.device.type == "cuda" and self.alpha == 1.0
+                           and not self.trace and ops.backend_name(self.device) == "hip"
+                           and os.environ.get("DBA_MLP_PERSIST", "1") != "0")
 
     # ------------------------------------------------------------------ step
     def _step(self, b: _GroupBuffers) -> None:
@@ -224,6 +230,8 @@ class GroupTrainer:
         T = max(len(c.steps) for c in clients)
         host = native.pack_steps(clients, G, self.B, T, max_slots)   # [T, D] int32 (C++ runtime)
         sched = to_device(host, self.device)
+        if self.persistent:
+            return self._persistent_enqueue(clients, b, sched, T, global_state, on_client_done)
         if self.use_graph and b.graph is None:
             b._cur = sched[0]
             self._reset(b, global_state)
@@ -261,6 +269,35 @@ class GroupTrainer:
             self._solo_leave(cur, b, solo[1])
         return {"b": b, "clients": clients, "snaps": snaps, "pend_dist": pend_dist, "sched": sched,
                 "trace": torch.stack(trace) if trace else None}
+
+    def _persistent_enqueue(self, clients: List[ClientPlan], b: _GroupBuffers, sched: torch.Tensor, T: int,
+                            global_state: torch.Tensor, on_client_done=None) -> Dict[str, Any]:
+        """LoanNet: one persistent launch per segment of steps between phase events (the
+        snapshots / scaling of :meth:`_phase_end` run between launches, as between graph
+        replays)."""
+        self._reset(b, global_state)
+        G = len(clients)
+        events = self._events(clients)
+        snaps: Dict[int, Dict[int, torch.Tensor]] = {g: {} for g in range(G)}
+        pend_dist: List[Tuple[int, int, torch.Tensor]] = []
+        gn2 = (ops.sq_dists(global_state[None, :self.spec.P], self._zeros_p())[0]
+               if any(ph.pre_scale_snap is not None for c in clients for ph in c.phases) else None)
+        wl = self.wl
+        hip = ops.hip_module()
+        t0 = 0
+        for t1 in sorted(set(events) | {T}):
+            if t1 > t0:
+                rc = hip.mlp_train(self.spec, sched, t0, t1, self.B, b.state, b.mom, b.fg, wl.train_store.rows,
+                                   wl.train_store.labels, wl.trig_cols, wl.trig_vals, self.target, b.stats,
+                                   b.max_slots, b.nan_flag, self.momentum, self.wd)
+                if rc != 0:
+                    raise RuntimeError(f"persistent LoanNet trainer declined the shape ({rc})")
+                t0 = t1
+            for (g, ph) in events.get(t1, []):
+                self._phase_end(b, g, ph, snaps[g], pend_dist, g, gn2)
+                if on_client_done is not None and ph is clients[g].phases[-1]:
+                    on_client_done(clients[g], snaps[g])
+        return {"b": b, "clients": clients, "snaps": snaps, "pend_dist": pend_dist, "sched": sched, "trace": None}
 
     # a lone client's tail shorter than this stays in the group graph
     SOLO_MIN_STEPS = int(os.environ.get("DBA_SOLO_MIN_STEPS", "4"))

@@ -201,41 +201,29 @@ class Ctx:
     # ------------------------------------------------------------------ layers
     def conv_bn(self, x: Tensor, conv: str, bn: str, stride: int, pad: int, relu: bool,
                 residual: Optional[Tensor] = None, to_conv: bool = True) -> Tensor:
-        """``to_conv``: the output only feeds convs (A operand or residual), so an evaluation
-        forward may keep it as fp16-pair activations (ops.hip PairAct); False where a pooling
-        or a linear layer reads it."""
-        if not self.train:
-            wf, bf = self.folded[conv]
-            kw = {"out_pairs": True} if (to_conv and self.eval_pairs) else {}
-            return ops.conv2d(x, wf, self.wsel, stride, pad, bias=bf, residual=residual, relu=relu,
-                              nvalid=self.nvalid, **kw)
-        w = self.w(conv)
-        y = ops.conv2d(x, w, self.wsel, stride, pad, nvalid=self.nvalid, bn_stats=True)
-        gamma, beta = self.m(bn + ".weight"), self.m(bn + ".bias")
-        out, mean, invstd = ops.bn_train(y, gamma, beta, self.m(bn + ".running_mean"),
-                                         self.m(bn + ".running_var"), self.nvalid, BN_MOMENTUM,
-                                         BN_EPS, relu, residual)
-        in_hw = (x.shape[2], x.shape[3])
-        kh, kw = w.shape[2], w.shape[3]
-        need_dx = self.tape.needs_grad(x)
-        k = self._want_dgrad(w, stride, pad, in_hw, x.shape[0]) if need_dx else -1
+        """Evaluation: the BN-folded conv (+ bias, residual, ReLU in its epilogue).  ``to_conv``:
+        the output only feeds convs (A operand or residual), so it may stay as fp16-pair
+        activations (ops.hip PairAct); False where a pooling or a linear layer reads it.
+        Training goes through :meth:`bn_conv` / :meth:`bn_out` (fused BN)."""
+        if self.train:
+            raise RuntimeError("conv_bn is the evaluation form; training uses bn_conv / bn_out")
+        wf, bf = self.folded[conv]
+        kw = {"out_pairs": True} if (to_conv and self.eval_pairs) else {}
+        return ops.conv2d(x, wf, self.wsel, stride, pad, bias=bf, residual=residual, relu=relu,
+                          nvalid=self.nvalid, **kw)
 
-        def bwd(dout: Tensor):
-            r = ops.bn_train_bwd(dout, y, out, mean, invstd, gamma, self.nvalid, relu,
-                                 self.g(bn + ".weight"), self.g(bn + ".bias"),
-                                 want_dres=residual is not None)
-            dy, dres = r if residual is not None else (r, None)
-            ops.conv2d_wgrad(dy, x, stride, pad, kh, kw, self.g(conv), nvalid=self.nvalid, defer=self._wdefer)
-            dx = None
-            if need_dx:
-                # the other consumer of x (shortcut branch) already delivered its gradient
-                acc = self.tape.pop_grad(x)
-                dx = ops.conv2d_dgrad(dy, w, self.wsel, stride, pad, in_hw, nvalid=self.nvalid, accum=acc,
-                                      wt=self._wt.get(k))
-            return dx, dres
-
-        self.tape.record((out,), (x, residual), bwd)
-        return out
+    def basic_block(self, x: Tensor, pre: str, to_conv: bool = True) -> Tensor:
+        """Evaluation of an identity BasicBlock, relu(bn2(conv2(relu(bn1(conv1(x))))) + x), BN
+        folded: ONE fused launch where the backend has it (ops.hip.basic_block_eval: the
+        32-wide stage; the mid activation stays in LDS), else the two folded convs."""
+        w1, b1 = self.folded[pre + "conv1.weight"]
+        w2, b2 = self.folded[pre + "conv2.weight"]
+        if not self.eval_pairs and ops.basic_block_ok(x, w1, w2):
+            return ops.basic_block_eval(x, w1, b1, w2, b2, self.wsel, self.nvalid)
+        a = ops.conv2d(x, w1, self.wsel, 1, 1, bias=b1, relu=True, nvalid=self.nvalid,
+                       **({"out_pairs": True} if self.eval_pairs else {}))
+        return ops.conv2d(a, w2, self.wsel, 1, 1, bias=b2, residual=x, relu=True, nvalid=self.nvalid,
+                          **({"out_pairs": True} if (self.eval_pairs and to_conv) else {}))
 
     # ---------------------------------------------------------- fused training BN
     def _bnp(self, bn: str) -> bs.BnParams:
@@ -415,6 +403,11 @@ def _resnet_cifar(ctx: Ctx, x: Tensor) -> Tensor:
         for bi in range(blocks[li]):
             stride = 2 if (li > 0 and bi == 0) else 1
             pre = f"layer{li + 1}.{bi}."
+            final = li == 3 and bi == blocks[li] - 1
+            if not ctx.train and not bottleneck and stride == 1 and cin == w:
+                out = ctx.basic_block(out, pre, to_conv=not final)
+                cin = w
+                continue
             if bottleneck:
                 a = ctx.bn_conv(out, pre + "conv1.weight", pre + "bn1", 1, 0, relu=True)
                 a = ctx.bn_conv(a, pre + "conv2.weight", pre + "bn2", stride, 1, relu=True)
@@ -426,7 +419,6 @@ def _resnet_cifar(ctx: Ctx, x: Tensor) -> Tensor:
                 sc = ctx.bn_conv(out, pre + "shortcut.0.weight", pre + "shortcut.1", stride, 0, relu=False)
             else:
                 sc = out
-            final = li == 3 and bi == blocks[li] - 1
             out = _block_out(ctx, a, pre + f"conv{last}.weight", pre + f"bn{last}", p, sc, to_conv=not final)
             cin = w * exp
     out = ctx.gap(out)

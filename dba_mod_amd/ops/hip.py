@@ -74,6 +74,10 @@ _SIGS = {
     "dba_bnx_dy": [_P, _P, _P, _P, _LL, _P, _I, _I, _I, _I, _P, _I, _P],
     "dba_xwgrad_reduce_batch": [_P, _I, _I, _LL, _P],
     # image stems in exact fp32 (csrc/kernels/stem.hip)
+    "dba_xblock_fwd": [_P, _LL, _P, _LL, _P, _P, _P, _LL, _P, _P, _LL, _P] + [_I] * 6
+    + [_P, _I, _P, _P, _I, _P, _I, _P],
+    "dba_mlp_train": [_P, _I, _I, _I, _I, _I, _P, _LL, _P, _P, _I, _P, _I, _I, _I, _I, _P, _P, _P, _P, _I, _I,
+                      _P, _LL, _I, _P, _F, _F, _P],
     "dba_xstem_fwd": [_P, _LL, _P, _LL, _P, _P, _LL, _P, _P, _LL, _P] + [_I] * 13 + [_P, _I, _P, _I, _P, _P, _P, _P],
 }
 for _name, _args in _SIGS.items():
@@ -200,6 +204,29 @@ def gather_rows(src, labels, idx, trig_cols, trig_vals, trig_id, poison_n, targe
           _i32(poison_n).data_ptr(), int(target), x.data_ptr(), int(out_dtype == torch.float32), y.data_ptr(),
           G, B, Fd, _stream())
     return x, y
+
+
+_MLP_LAYERS = ("layer1.0.weight", "layer1.0.bias", "layer2.0.weight", "layer2.0.bias", "layer3.0.weight",
+               "layer3.0.bias")
+
+
+def mlp_train(spec, sched, t0, t1, B, state, mom, fg, rows, labels, trig_cols, trig_vals, target, stats,
+              max_slots, nan_flag, momentum, wd) -> int:
+    """Steps [t0, t1) of the step table ``sched`` [T, G*B + 8G] for every client of a LoanNet
+    group in ONE launch, one workgroup per client (csrc/kernels/mlp.hip): parameters and
+    momentum LDS-resident, written back to ``state`` / ``mom`` at the end.  Returns -100
+    (nothing launched) for other shapes."""
+    G = state.shape[0]
+    es = [spec.by_name[n] for n in _MLP_LAYERS]
+    offs = torch.tensor([e.offset for e in es], dtype=torch.int32)   # host table, read at launch
+    (H1, F), (H2, _), (C, _) = es[0].k_shape[:2], es[2].k_shape[:2], es[4].k_shape[:2]
+    assert sched.dtype == torch.int32 and sched.is_contiguous() and state.stride(1) == 1
+    tc = _i32(trig_cols)
+    return _call("dba_mlp_train", sched.data_ptr(), sched.shape[1], int(t0), int(t1), G, B, state.data_ptr(),
+                 state.stride(0), mom.data_ptr(), _ptr(fg), spec.P, offs.data_ptr(), F, H1, H2, C,
+                 rows.contiguous().data_ptr(), _i32(labels).data_ptr(), tc.data_ptr(),
+                 trig_vals.float().contiguous().data_ptr(), int(tc.shape[1]), int(target), stats.data_ptr(),
+                 stats.shape[1], max_slots, nan_flag.data_ptr(), float(momentum), float(wd), _stream())
 
 
 # ------------------------------------------------------------------------------ conv
@@ -493,6 +520,42 @@ def _xconv_fwd(x, w, wsel, stride, pad, bias, residual, relu, nvalid, out_dtype,
           _ptr(cnt), 0 if cnt is None else cnt.numel(), bnf_p, lz_coef, lz_relu, _stream())
     if out_sexp is not None:
         y._dba_pair = out_sexp
+    return y
+
+
+_EVAL_BLOCK = os.environ.get("DBA_EVAL_BLOCK", "1") != "0"
+
+
+def basic_block_ok(x, w1, w2) -> bool:
+    """The fused evaluation BasicBlock (csrc/kernels/xblock.hip) takes this block: fp16-pair
+    forwards, fp32 [G, N, 32, 32, 32] input (not PairAct), 32 -> 32 3x3 weights pre-split at
+    the eval fold.  ``DBA_EVAL_BLOCK=0``: off (the two convs run)."""
+    return (_EVAL_BLOCK and _MODE == F16_PAIR and "fwd" in _H_OPS and x.dtype == _F32 and x.dim() == 5
+            and tuple(x.shape[2:]) == (32, 32, 32) and _pair_sexp(x) is None
+            and all(w.dtype == _F32 and tuple(w.shape[1:]) == (32, 3, 3, 32)
+                    and getattr(w, "_dba_planes", None) is not None for w in (w1, w2)))
+
+
+def basic_block_eval(x, w1, b1, w2, b2, wsel=None, nvalid=None):
+    """relu(conv2(relu(conv1(x) + b1)) + b2 + x) in one launch (BN folded into w / b; the mid
+    activation stays in LDS): xblock.hip.  Callers check :func:`basic_block_ok` first."""
+    x = _act(x, _F32, "conv input")
+    G, N = x.shape[:2]
+    per = 32 * 9 * 32
+    (w1c, ws1), (w2c, ws2) = _check_w(w1), _check_w(w2)
+    aw1, aw2 = _amax_w(w1, ws1, per), _amax_w(w2, ws2, per)
+    p1, p2 = w1._dba_planes, w2._dba_planes
+    assert p1.stride(0) == p2.stride(0) and aw1.shape[1] == aw2.shape[1]
+    (b1c, bs1), (b2c, bs2) = _rowview(b1), _rowview(b2)
+    assert bs1 == bs2 and b1c.dtype == b2c.dtype == _F32
+    ax = _amax_act(x, nvalid)
+    y = torch.empty_like(x)
+    ay = _amax_out(y)
+    rc = _call("dba_xblock_fwd", x.data_ptr(), x.stride(0), y.data_ptr(), y.stride(0), _ptr(_i32(wsel)),
+               p1.data_ptr(), p2.data_ptr(), p1.stride(0), b1c.data_ptr(), b2c.data_ptr(), bs1, _ptr(_i32(nvalid)),
+               G, N, 32, 32, 32, 32, *_aptr(ax), aw1.data_ptr(), aw2.data_ptr(), aw1.shape[1], *_aptr(ay), _stream())
+    if rc == NOT_HANDLED:
+        raise RuntimeError("xblock_fwd declined a shape basic_block_ok accepted")
     return y
 
 

@@ -135,6 +135,20 @@ def conv2d(x: Tensor, w: Tensor, wsel: Optional[Tensor], stride: int, pad: int,
     return torch.stack(outs).to(out_dtype or x.dtype)
 
 
+def basic_block_ok(x: Tensor, w1: Tensor, w2: Tensor) -> bool:
+    """Whether the backend runs an evaluation BasicBlock as one fused op (HIP: xblock.hip);
+    the reference runs the two convs."""
+    return False
+
+
+def basic_block_eval(x: Tensor, w1: Tensor, b1: Tensor, w2: Tensor, b2: Tensor,
+                     wsel: Optional[Tensor] = None, nvalid: Optional[Tensor] = None) -> Tensor:
+    """relu(conv2(relu(conv1(x) + b1)) + b2 + x), 3x3 stride-1 convs with BN folded into w / b
+    (the identity BasicBlock of the reference models/resnet_cifar.py:14-37, evaluated)."""
+    h = conv2d(x, w1, wsel, 1, 1, bias=b1, relu=True, nvalid=nvalid)
+    return conv2d(h, w2, wsel, 1, 1, bias=b2, residual=x, relu=True, nvalid=nvalid)
+
+
 def _valid_mask(t: Tensor, nvalid: Optional[Tensor]) -> Tensor:
     """[G, N, 1, 1, 1] (bool) of the valid images of each replica."""
     G, N = t.shape[:2]

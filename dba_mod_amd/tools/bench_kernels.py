@@ -84,6 +84,17 @@ def _bench_fp32(name, G, N, Hh, Cin, Cout, k, s, p, reps, dev):
         xp = H.conv2d(x, w, None, s, p, relu=True, out_pairs=True)
         assert getattr(xp, "_dba_pair", None) is not None
         ops.append(("fwd_pairs", lambda: H.conv2d(xp, w, None, s, p, relu=True, out_pairs=True)))
+    block_flops = None
+    if name.startswith("eval") and H.fp32_mode() == H.F16_PAIR and H.basic_block_ok(x, w, w):
+        # the whole identity BasicBlock (two convs, the mid activation in LDS: xblock.hip); its
+        # TFLOP/s counts both convs' fp32 work
+        xb = torch.relu(x)
+        w2 = torch.randn(G, Cout, k, k, Cin, device=dev) * 0.05
+        H.split_weights(w2, per, per, H._amax_w(w2, per, per))
+        b1, b2 = torch.randn(G, Cout, device=dev) * 0.1, torch.randn(G, Cout, device=dev) * 0.1
+        xb._dba_amax = H._amax_act(xb, None)
+        block_flops = 2 * flops
+        ops.append(("block", lambda: H.basic_block_eval(xb, w, b1, w2, b2)))
     if name.startswith("train"):
         wt = H.prepare_dgrad_weights(w, [(w, None, s, p, (Hh, Hh), None, G)])[0]
         dw = torch.zeros(G, Cout, k, k, Cin, device=dev)
@@ -92,7 +103,7 @@ def _bench_fp32(name, G, N, Hh, Cin, Cout, k, s, p, reps, dev):
     for tag, fn in ops:
         t = _time(fn, reps)
         rec[tag + "_us"] = round(t * 1e6, 1)
-        rec[tag + "_tflops"] = round(flops / t / 1e12, 1)
+        rec[tag + "_tflops"] = round((block_flops if tag == "block" else flops) / t / 1e12, 1)
     return rec
 
 

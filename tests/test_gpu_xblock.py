@@ -1,0 +1,90 @@
+"""The fused evaluation BasicBlock (``csrc/kernels/xblock.hip``) vs an fp64 oracle and vs the
+two-launch form it replaces (GPU only).
+
+relu(conv2(relu(conv1(x) + b1)) + b2 + x) for the 32-wide stage with BN folded into the
+weights — the identity BasicBlock of the reference ``models/resnet_cifar.py:14-37`` in
+evaluation.  The kernel keeps the mid activation in LDS (split with the block's own scale), so
+it is compared to the fp64 reference at fp32 level and to the two halo-conv launches to the
+same level, not bitwise.
+"""
+import struct
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def H():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from dba_mod_amd.ops import hip
+    prev = hip.set_fp32_planes(hip.F16_PAIR)
+    yield hip
+    hip.set_fp32_planes(prev)
+
+
+@pytest.fixture()
+def R64():
+    from dba_mod_amd.ops import reference
+    old = reference.COMPUTE_DTYPE
+    reference.COMPUTE_DTYPE = torch.float64
+    yield reference
+    reference.COMPUTE_DTYPE = old
+
+
+def _rel(a, b):
+    a, b = a.double().cpu(), b.double().cpu()
+    return ((a - b).norm() / b.norm().clamp(min=1e-30)).item()
+
+
+def _weights(H, slots, dev, g, scale):
+    w = (torch.randn(slots, 32, 3, 3, 32, generator=g) * scale).to(dev)
+    per = 32 * 9 * 32
+    H.split_weights(w, per, per, H._amax_w(w, per, per))
+    return w
+
+
+@pytest.mark.parametrize("G,N,nv,scale", [(3, 5, (5, 3, 5), 1.0), (2, 4, (4, 1), 1e-3), (1, 9, (9,), 30.0)])
+def test_basic_block_eval_vs_fp64_and_two_launches(H, R64, G, N, nv, scale):
+    dev = torch.device("cuda")
+    g = torch.Generator().manual_seed(G * 100 + N)
+    slots = 2
+    x = torch.relu(torch.randn(G, N, 32, 32, 32, generator=g) * scale).to(dev)
+    w1 = _weights(H, slots, dev, g, 1.0 / 17)
+    w2 = _weights(H, slots, dev, g, 1.0 / 17)
+    b1 = (torch.randn(slots, 32, generator=g) * 0.1 * scale).to(dev)
+    b2 = (torch.randn(slots, 32, generator=g) * 0.1 * scale).to(dev)
+    wsel = torch.tensor([min(i, slots - 1) for i in range(G)], dtype=torch.int32, device=dev)
+    nvalid = torch.tensor(nv, dtype=torch.int32, device=dev)
+    assert H.basic_block_ok(x, w1, w2)
+    with H.amax_arena(G, dev):
+        y = H.basic_block_eval(x, w1, b1, w2, b2, wsel, nvalid)
+        h = H.conv2d(x, w1, wsel, 1, 1, bias=b1, relu=True, nvalid=nvalid)
+        y2 = H.conv2d(h, w2, wsel, 1, 1, bias=b2, residual=x, relu=True, nvalid=nvalid)
+        amax = y._dba_amax.clone()
+    torch.cuda.synchronize()
+    yr = R64.basic_block_eval(x.double().cpu(), w1.double().cpu(), b1.double().cpu(), w2.double().cpu(),
+                              b2.double().cpu(), wsel.cpu())
+    for i in range(G):
+        n = nv[i]
+        e, e2 = _rel(y[i, :n], yr[i, :n]), _rel(y2[i, :n], yr[i, :n])
+        assert e < 2e-6, f"replica {i}: fused {e:.2e} (two launches {e2:.2e})"
+        assert e < max(2e-6, 2 * e2), f"replica {i}: fused {e:.2e} vs two launches {e2:.2e}"
+        # the output's max |y| folded for its consumers (exact integer max of float bits)
+        m = y[i, :n].abs().max().item()
+        assert struct.unpack("<f", struct.pack("<i", int(amax[:, i].max().item())))[0] == m
+
+
+def test_basic_block_eval_is_deterministic(H):
+    dev = torch.device("cuda")
+    g = torch.Generator().manual_seed(7)
+    x = torch.relu(torch.randn(2, 6, 32, 32, 32, generator=g)).to(dev)
+    w1, w2 = _weights(H, 2, dev, g, 0.06), _weights(H, 2, dev, g, 0.06)
+    b1, b2 = torch.randn(2, 32, generator=g).to(dev) * 0.1, torch.randn(2, 32, generator=g).to(dev) * 0.1
+    outs = []
+    for _ in range(3):
+        with H.amax_arena(2, dev):
+            outs.append(H.basic_block_eval(x, w1, b1, w2, b2))
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
