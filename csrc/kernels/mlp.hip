@@ -30,6 +30,11 @@ namespace {
 constexpr int kB = 64, kF = 91, kH1 = 46, kH2 = 23, kC = 9;   // batch, LoanNet dims
 constexpr int kH1p = 48, kH2p = 24, kCp = 12;                 // padded to 4-wide blocks
 constexpr int kPmax = 6144;                                   // flat parameter floats (aligned entries)
+// row stride of the feature-major activation images: 68 floats (272 B) puts consecutive rows
+// one 16-B bank slot apart, so lanes walking rows (the weight-gradient loops) read without
+// LDS bank conflicts (a 64-float stride put every lane on the same slot)
+constexpr int kLD = kB + 4;
+constexpr int kLG = kC + 4;                                   // dlogits row stride (odd: conflict-free)
 
 struct MlpArgs {
   const int* sched; int D, t0, t1, G;        // step descriptors [T][D] (fl/trainer.py _GroupBuffers)
@@ -47,10 +52,10 @@ struct MlpArgs {
 struct MlpLds {
   float prm[kPmax], mom[kPmax];
   float w1t[kF * kH1p], w2t[kH1 * kH2p], w3t[kH2 * kCp];   // transposed weights [in][out]
-  float xT[kF * kB];                                       // batch, feature-major
-  float a1T[kH1p * kB], a2T[kH2p * kB];                    // post-dropout activations
-  float lg[kB * kCp];                                      // dlogits
-  float d1T[kH1p * kB], d2T[kH2p * kB];                    // pre-activation gradients
+  float xT[kF * kLD];                                      // batch, feature-major
+  float a1T[kH1p * kLD], a2T[kH2p * kLD];                  // post-dropout activations
+  float lg[kB * kLG];                                      // dlogits
+  float d1T[kH1p * kLD], d2T[kH2p * kLD];                  // pre-activation gradients
   int y[kB];
   double wl[4];
   float wc[4];
@@ -83,10 +88,9 @@ __global__ __launch_bounds__(256) void mlp_train_kernel(const MlpArgs a) {
     s.prm[i] = st[i];
     s.mom[i] = mg[i];
   }
-  for (int i = tid; i < kH1p * kB; i += 256) s.a1T[i] = 0.f;
-  for (int i = tid; i < kH2p * kB; i += 256) s.a2T[i] = s.d2T[i] = 0.f;
-  for (int i = tid; i < kH1p * kB; i += 256) s.d1T[i] = 0.f;
-  for (int i = tid; i < kB * kCp; i += 256) s.lg[i] = 0.f;
+  for (int i = tid; i < kH1p * kLD; i += 256) s.a1T[i] = s.d1T[i] = 0.f;
+  for (int i = tid; i < kH2p * kLD; i += 256) s.a2T[i] = s.d2T[i] = 0.f;
+  for (int i = tid; i < kB * kLG; i += 256) s.lg[i] = 0.f;
   __syncthreads();
   auto transpose_w = [&]() __attribute__((always_inline)) {
     for (int e = tid; e < kF * kH1p; e += 256) {
@@ -126,7 +130,7 @@ __global__ __launch_bounds__(256) void mlp_train_kernel(const MlpArgs a) {
           for (int k = 0; k < a.K; ++k)
             if (a.tcols[trig * a.K + k] == f) v = a.tvals[trig * a.K + k];
       }
-      s.xT[f * kB + b] = v;
+      s.xT[f * kLD + b] = v;
     }
     if (tid < kB) {
       const int r = idx[tid];
@@ -139,7 +143,7 @@ __global__ __launch_bounds__(256) void mlp_train_kernel(const MlpArgs a) {
       const int b0 = (tid & 15) * 4, j0 = (tid >> 4) * 4;
       float acc[4][4] = {};
       for (int f = 0; f < kF; ++f) {
-        const float4 xv = *(const float4*)&s.xT[f * kB + b0];
+        const float4 xv = *(const float4*)&s.xT[f * kLD + b0];
         const float4 wv = *(const float4*)&s.w1t[f * kH1p + j0];
         const float xs[4] = {xv.x, xv.y, xv.z, xv.w}, ws[4] = {wv.x, wv.y, wv.z, wv.w};
 #pragma unroll
@@ -156,7 +160,7 @@ __global__ __launch_bounds__(256) void mlp_train_kernel(const MlpArgs a) {
         for (int i = 0; i < 4; ++i) {
           const int b = b0 + i;
           const bool keep = uniform01(seed, (uint32_t)(b * kH1 + j)) >= 0.5f;
-          s.a1T[j * kB + b] = keep ? fmaxf(acc[i][k] + bj, 0.f) * 2.0f : 0.f;
+          s.a1T[j * kLD + b] = keep ? fmaxf(acc[i][k] + bj, 0.f) * 2.0f : 0.f;
         }
       }
     }
@@ -167,7 +171,7 @@ __global__ __launch_bounds__(256) void mlp_train_kernel(const MlpArgs a) {
       const int b0 = (tid & 15) * 4, j0 = (tid >> 4) * 4;
       float acc[4][4] = {};
       for (int k = 0; k < kH1; ++k) {
-        const float4 xv = *(const float4*)&s.a1T[k * kB + b0];
+        const float4 xv = *(const float4*)&s.a1T[k * kLD + b0];
         const float4 wv = *(const float4*)&s.w2t[k * kH2p + j0];
         const float xs[4] = {xv.x, xv.y, xv.z, xv.w}, ws[4] = {wv.x, wv.y, wv.z, wv.w};
 #pragma unroll
@@ -185,7 +189,7 @@ __global__ __launch_bounds__(256) void mlp_train_kernel(const MlpArgs a) {
         for (int i = 0; i < 4; ++i) {
           const int b = b0 + i;
           const bool keep = uniform01(sd1, (uint32_t)(b * kH2 + j)) >= 0.5f;
-          s.a2T[j * kB + b] = keep ? fmaxf(acc[i][q] + bj, 0.f) * 2.0f : 0.f;
+          s.a2T[j * kLD + b] = keep ? fmaxf(acc[i][q] + bj, 0.f) * 2.0f : 0.f;
         }
       }
     }
@@ -198,7 +202,7 @@ __global__ __launch_bounds__(256) void mlp_train_kernel(const MlpArgs a) {
 #pragma unroll
       for (int c = 0; c < kC; ++c) x[c] = 0.f;
       for (int k = 0; k < kH2; ++k) {
-        const float av = s.a2T[k * kB + b];
+        const float av = s.a2T[k * kLD + b];
 #pragma unroll
         for (int c = 0; c < kC; ++c) x[c] = fmaf(av, s.w3t[k * kCp + c], x[c]);
       }
@@ -210,7 +214,7 @@ __global__ __launch_bounds__(256) void mlp_train_kernel(const MlpArgs a) {
       float wc = 0.f;
       if (y < 0) {
 #pragma unroll
-        for (int c = 0; c < kC; ++c) s.lg[b * kCp + c] = 0.f;
+        for (int c = 0; c < kC; ++c) s.lg[b * kLG + c] = 0.f;
       } else {
         float mx = x[0];
         int am = 0;
@@ -228,7 +232,7 @@ __global__ __launch_bounds__(256) void mlp_train_kernel(const MlpArgs a) {
         wl = (double)(lse - xy);
         wc = am == y ? 1.f : 0.f;
 #pragma unroll
-        for (int c = 0; c < kC; ++c) s.lg[b * kCp + c] = (__expf(x[c] - lse) - (c == y ? 1.f : 0.f)) * scale;
+        for (int c = 0; c < kC; ++c) s.lg[b * kLG + c] = (__expf(x[c] - lse) - (c == y ? 1.f : 0.f)) * scale;
       }
 #pragma unroll
       for (int o = 32; o > 0; o >>= 1) wl += __shfl_xor(wl, o, kWave);
@@ -250,8 +254,8 @@ __global__ __launch_bounds__(256) void mlp_train_kernel(const MlpArgs a) {
       const int j = e / kB, b = e - j * kB;
       float acc = 0.f;
 #pragma unroll
-      for (int c = 0; c < kC; ++c) acc = fmaf(s.lg[b * kCp + c], s.prm[a.o_w3 + c * kH2 + j], acc);
-      s.d2T[j * kB + b] = s.a2T[j * kB + b] > 0.f ? acc * 2.0f : 0.f;
+      for (int c = 0; c < kC; ++c) acc = fmaf(s.lg[b * kLG + c], s.prm[a.o_w3 + c * kH2 + j], acc);
+      s.d2T[j * kLD + b] = s.a2T[j * kLD + b] > 0.f ? acc * 2.0f : 0.f;
     }
     __syncthreads();
 
@@ -259,19 +263,19 @@ __global__ __launch_bounds__(256) void mlp_train_kernel(const MlpArgs a) {
     for (int e = tid; e < kB * kH1; e += 256) {
       const int k = e / kB, b = e - k * kB;
       float acc = 0.f;
-      for (int j = 0; j < kH2; ++j) acc = fmaf(s.d2T[j * kB + b], s.prm[a.o_w2 + j * kH1 + k], acc);
-      s.d1T[k * kB + b] = s.a1T[k * kB + b] > 0.f ? acc * 2.0f : 0.f;
+      for (int j = 0; j < kH2; ++j) acc = fmaf(s.d2T[j * kLD + b], s.prm[a.o_w2 + j * kH1 + k], acc);
+      s.d1T[k * kLD + b] = s.a1T[k * kLD + b] > 0.f ? acc * 2.0f : 0.f;
     }
     for (int e = tid; e < kC * kH2 + kC; e += 256) {
       float gr = 0.f;
       if (e < kC * kH2) {
         const int c = e / kH2, j = e - c * kH2;
-        for (int b = 0; b < kB; ++b) gr = fmaf(s.lg[b * kCp + c], s.a2T[j * kB + b], gr);
+        for (int b = 0; b < kB; ++b) gr = fmaf(s.lg[b * kLG + c], s.a2T[j * kLD + b], gr);
         sgd1(s, a, fgr, a.o_w3 + e, gr, lr, first);
         s.w3t[j * kCp + c] = s.prm[a.o_w3 + e];
       } else {
         const int c = e - kC * kH2;
-        for (int b = 0; b < kB; ++b) gr += s.lg[b * kCp + c];
+        for (int b = 0; b < kB; ++b) gr += s.lg[b * kLG + c];
         sgd1(s, a, fgr, a.o_b3 + c, gr, lr, first);
       }
     }
@@ -284,17 +288,17 @@ __global__ __launch_bounds__(256) void mlp_train_kernel(const MlpArgs a) {
         const bool l1 = e < N1;
         const int e2 = l1 ? e : e - N1;
         const int nin = l1 ? kF : kH1, nout = l1 ? kH1 : kH2;
-        const int npair = (nin + 1) / 2;
-        const int j0 = (e2 / npair) * 2, f0 = (e2 % npair) * 2;
+        const int npair = (nin + 1) / 2;   // inputs {q, q + npair}: lanes walk consecutive rows
+        const int j0 = (e2 / npair) * 2, f0 = e2 % npair, f1 = f0 + npair;
         const float* dT = l1 ? s.d1T : s.d2T;
         const float* inT = l1 ? s.xT : s.a1T;
-        const bool f1ok = f0 + 1 < nin, j1ok = j0 + 1 < nout;
+        const bool f1ok = f1 < nin, j1ok = j0 + 1 < nout;
         float g00 = 0.f, g01 = 0.f, g10 = 0.f, g11 = 0.f;
         for (int b = 0; b < kB; b += 4) {
-          const float4 d0 = *(const float4*)&dT[j0 * kB + b];
-          const float4 d1 = *(const float4*)&dT[(j0 + (j1ok ? 1 : 0)) * kB + b];
-          const float4 x0 = *(const float4*)&inT[f0 * kB + b];
-          const float4 x1 = *(const float4*)&inT[(f0 + (f1ok ? 1 : 0)) * kB + b];
+          const float4 d0 = *(const float4*)&dT[j0 * kLD + b];
+          const float4 d1 = *(const float4*)&dT[(j0 + (j1ok ? 1 : 0)) * kLD + b];
+          const float4 x0 = *(const float4*)&inT[f0 * kLD + b];
+          const float4 x1 = *(const float4*)&inT[(f1ok ? f1 : f0) * kLD + b];
           g00 = fmaf(d0.x, x0.x, g00); g00 = fmaf(d0.y, x0.y, g00); g00 = fmaf(d0.z, x0.z, g00); g00 = fmaf(d0.w, x0.w, g00);
           g01 = fmaf(d0.x, x1.x, g01); g01 = fmaf(d0.y, x1.y, g01); g01 = fmaf(d0.z, x1.z, g01); g01 = fmaf(d0.w, x1.w, g01);
           g10 = fmaf(d1.x, x0.x, g10); g10 = fmaf(d1.y, x0.y, g10); g10 = fmaf(d1.z, x0.z, g10); g10 = fmaf(d1.w, x0.w, g10);
@@ -306,15 +310,15 @@ __global__ __launch_bounds__(256) void mlp_train_kernel(const MlpArgs a) {
         sgd1(s, a, fgr, ow + j0 * nin + f0, g00, lr, first);
         wt[f0 * ldt + j0] = s.prm[ow + j0 * nin + f0];
         if (f1ok) {
-          sgd1(s, a, fgr, ow + j0 * nin + f0 + 1, g01, lr, first);
-          wt[(f0 + 1) * ldt + j0] = s.prm[ow + j0 * nin + f0 + 1];
+          sgd1(s, a, fgr, ow + j0 * nin + f1, g01, lr, first);
+          wt[f1 * ldt + j0] = s.prm[ow + j0 * nin + f1];
         }
         if (j1ok) {
           sgd1(s, a, fgr, ow + (j0 + 1) * nin + f0, g10, lr, first);
           wt[f0 * ldt + j0 + 1] = s.prm[ow + (j0 + 1) * nin + f0];
           if (f1ok) {
-            sgd1(s, a, fgr, ow + (j0 + 1) * nin + f0 + 1, g11, lr, first);
-            wt[(f0 + 1) * ldt + j0 + 1] = s.prm[ow + (j0 + 1) * nin + f0 + 1];
+            sgd1(s, a, fgr, ow + (j0 + 1) * nin + f1, g11, lr, first);
+            wt[f1 * ldt + j0 + 1] = s.prm[ow + (j0 + 1) * nin + f1];
           }
         }
       } else {
@@ -323,7 +327,7 @@ __global__ __launch_bounds__(256) void mlp_train_kernel(const MlpArgs a) {
         const int u = l1 ? j : j - kH1;
         const float* dT = l1 ? s.d1T : s.d2T;
         float gr = 0.f;
-        for (int b = 0; b < kB; ++b) gr += dT[u * kB + b];
+        for (int b = 0; b < kB; ++b) gr += dT[u * kLD + b];
         sgd1(s, a, fgr, (l1 ? a.o_b1 : a.o_b2) + u, gr, lr, first);
       }
     }

@@ -106,8 +106,11 @@ _DEFAULTS: Dict[str, Any] = {
     "early_local_eval": True,      # enqueue a client's local tests as soon as it finishes training
     # N > 1 ranks: image-sharded tests split by water-filling over each rank's load in the
     # window (training of the next round + its local tests), in eval image-forward units:
-    # one grouped training step costs balance_step_latency + balance_step_per_client * active
-    "eval_balance": True,
+    # one grouped training step costs balance_step_latency + balance_step_per_client * active.
+    # The constants are calibrated for fp32 CIFAR ResNets on MI355X
+    # (profiles/balance_sweep_r3/); None = on for CIFAR only, the strided even split elsewhere
+    # (MNIST / LOAN / Tiny have other step-to-forward cost ratios: set both constants with it)
+    "eval_balance": None,
     "balance_step_latency": 2400.0,
     "balance_step_per_client": 420.0,
     "rfa_mode": "auto",            # RFA across ranks: gather | distributed | auto (fewer bytes)

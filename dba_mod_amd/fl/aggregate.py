@@ -45,14 +45,18 @@ def fedavg_apply(global_state: torch.Tensor, delta_sum: torch.Tensor, eta: float
     ops.add_noise_scaled(global_state[:n_update], delta_sum, eta / no_models, sigma, seed, dp)
 
 
-def _weiszfeld(avg, dists, alphas: torch.Tensor, maxiter: int, eps: float, ftol: float):
+def _weiszfeld(avg, dists, alphas: torch.Tensor, maxiter: int, eps: float, ftol: float, poll: int = 0):
     """Weiszfeld iteration control on the DEVICE (reference ``helper.py:320-352``, SURVEY
     §7.4.4): ``maxiter`` iterations are always enqueued; the stopping test
     ``|f_prev - f| < ftol * f`` clears a device flag that freezes the median, distances and
     weights from the converging iteration on (exactly the values the reference's ``break``
     leaves).  No host sync inside the loop: one read of the per-iteration objectives at the
     end (for the reference's log lines).  ``avg(w)``: weighted sum of the points for the
-    normalised fp64 weights ``w`` (device); ``dists(m)``: fp64 distances of the points to m."""
+    normalised fp64 weights ``w`` (device); ``dists(m)``: fp64 distances of the points to m.
+    ``poll`` > 0: read the flag every ``poll`` iterations and stop enqueueing once converged
+    (the distributed form: each further iteration is two all-reduces; every rank reads the
+    same all-reduced objective, so all stop at the same iteration).  Returns (median,
+    distances, weights, iterations run = the reference's num_oracle_calls - 1)."""
     dev = alphas.device
     median = avg(alphas)
     d = dists(median)
@@ -78,6 +82,8 @@ def _weiszfeld(avg, dists, alphas: torch.Tensor, maxiter: int, eps: float, ftol:
         upd = active & ~conv
         wv = torch.where(upd, w, wv) if wv is not None else torch.where(upd, w, torch.full_like(w, float("nan")))
         active = active & ~conv
+        if poll > 0 and (i + 1) % poll == 0 and i + 1 < maxiter and not bool(active.item()):
+            break
     h = hist.cpu().numpy()                       # the one host read of the aggregation
     for i in range(maxiter):
         if h[i, 2] > 0:
@@ -86,7 +92,9 @@ def _weiszfeld(avg, dists, alphas: torch.Tensor, maxiter: int, eps: float, ftol:
     wv_h = wv.cpu().numpy() if wv is not None else None
     if wv_h is None or np.isnan(wv_h).any():      # D5: converged at iteration 0
         wv_h = weights.cpu().numpy()
-    return median, d, wv_h
+    # iterations the reference runs: up to and including the converging one (its break)
+    iters = min(int((h[:, 2] > 0).sum()) + 1, maxiter)
+    return median, d, wv_h, iters
 
 
 def geometric_median(global_state: torch.Tensor, finals: torch.Tensor, num_samples: Sequence[int],
@@ -106,11 +114,11 @@ def geometric_median(global_state: torch.Tensor, finals: torch.Tensor, num_sampl
     def dists(m: torch.Tensor) -> torch.Tensor:
         return ops.sq_dists(points, m).double().clamp(min=0.0).sqrt()
 
-    median, d, wv = _weiszfeld(avg, dists, alphas, maxiter, eps, ftol)
-    return _rfa_apply(global_state, median, d, wv, eta, dp, sigma, seed, n_update, max_update_norm, maxiter)
+    median, d, wv, iters = _weiszfeld(avg, dists, alphas, maxiter, eps, ftol)
+    return _rfa_apply(global_state, median, d, wv, eta, dp, sigma, seed, n_update, max_update_norm, iters)
 
 
-def _rfa_apply(global_state, median, d, wv, eta, dp, sigma, seed, n_update, max_update_norm, maxiter):
+def _rfa_apply(global_state, median, d, wv, eta, dp, sigma, seed, n_update, max_update_norm, iters):
     upd_norm = float(torch.linalg.vector_norm(median.double()).item())
     if max_update_norm is None or upd_norm < max_update_norm:
         ops.add_noise_scaled(global_state[:n_update], median, eta, sigma, seed, dp)
@@ -118,7 +126,7 @@ def _rfa_apply(global_state, median, d, wv, eta, dp, sigma, seed, n_update, max_
     else:
         log.info(f"\t\t\tUpdate norm = {upd_norm} is too large. Update rejected")
         updated = False
-    return updated, [float(x) for x in wv], [float(x) for x in d.cpu().tolist()], maxiter + 1
+    return updated, [float(x) for x in wv], [float(x) for x in d.cpu().tolist()], 1 + iters
 
 
 def geometric_median_distributed(global_state: torch.Tensor, local_finals: torch.Tensor, local_idx: Sequence[int],
@@ -153,8 +161,8 @@ def geometric_median_distributed(global_state: torch.Tensor, local_finals: torch
             full[idx_t] = ops.sq_dists(points, m).double()
         return reduce(full).clamp(min=0.0).sqrt()
 
-    median, d, wv = _weiszfeld(avg, dists, alphas, maxiter, eps, ftol)
-    return _rfa_apply(global_state, median, d, wv, eta, dp, sigma, seed, n_update, max_update_norm, maxiter)
+    median, d, wv, iters = _weiszfeld(avg, dists, alphas, maxiter, eps, ftol, poll=2)
+    return _rfa_apply(global_state, median, d, wv, eta, dp, sigma, seed, n_update, max_update_norm, iters)
 
 
 class FoolsGold:

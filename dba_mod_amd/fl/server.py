@@ -327,10 +327,16 @@ class Server:
                 load[owner_of[name]] += sum(self._job_images(plan.jobs[j]) for j in js)
         return load
 
+    def _eval_balance(self) -> bool:
+        """Water-filled eval shares (config ``eval_balance``; None: on where the step-cost
+        constants are calibrated — the CIFAR ResNets)."""
+        eb = self.params["eval_balance"]
+        return self.params["type"] == C.TYPE_CIFAR if eb is None else bool(eb)
+
     def _eval_shares(self, jobs, base: Optional[List[float]]) -> Optional[List[float]]:
         """Per-rank shares of the image-sharded tests ``jobs``: water-filling over ``base``
         (None: the strided even split)."""
-        if self.d.world <= 1 or base is None or not self.params["eval_balance"]:
+        if self.d.world <= 1 or base is None or not self._eval_balance():
             return None
         work = float(sum(self._job_images(j) for j in jobs))
         return native.balance_shares(base, work)

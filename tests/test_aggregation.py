@@ -29,8 +29,10 @@ def _weiszfeld_oracle(points, alphas, maxiter, eps=1e-5, ftol=1e-6):
     med = (alphas[:, None] * points).sum(0) / alphas.sum()
     obj = sum(a * np.linalg.norm(med - p) for a, p in zip(alphas, points))
     wv = None
+    calls = 1
     for _ in range(maxiter):
         prev = obj
+        calls += 1
         w = np.array([a / max(eps, np.linalg.norm(med - p)) for a, p in zip(alphas, points)])
         w = w / w.sum()
         med = (w[:, None] * points).sum(0) / w.sum()
@@ -38,7 +40,7 @@ def _weiszfeld_oracle(points, alphas, maxiter, eps=1e-5, ftol=1e-6):
         if abs(prev - obj) < ftol * obj:
             break
         wv = w
-    return med, wv, [np.linalg.norm(med - p) for p in points]
+    return med, wv, [np.linalg.norm(med - p) for p in points], calls
 
 
 def test_geometric_median_matches_oracle():
@@ -50,7 +52,12 @@ def test_geometric_median_matches_oracle():
     finals = torch.from_numpy(pts).float()
     updated, wv, alphas, calls = agg.geometric_median(g, finals, ns, eta=1.0, maxiter=10, dp=False, sigma=0,
                                                       seed=0, n_update=50)
-    med, wv_ref, al_ref = _weiszfeld_oracle(pts, ns, 10)
+    med, wv_ref, al_ref, calls_ref = _weiszfeld_oracle(pts, ns, 10)
+    # the reference's num_oracle_calls: 1 + the iterations up to its break (helper.py:321-349)
+    assert calls == calls_ref
+    g2 = torch.zeros(50)
+    calls2 = agg.geometric_median(g2, finals, ns, eta=1.0, maxiter=200, dp=False, sigma=0, seed=0, n_update=50)[3]
+    assert calls2 == _weiszfeld_oracle(pts, ns, 200)[3] < 201   # converged early: the break's count
     np.testing.assert_allclose(g.numpy(), med, rtol=1e-4, atol=1e-4)
     np.testing.assert_allclose(wv, wv_ref, rtol=1e-4, atol=1e-6)
     np.testing.assert_allclose(alphas, al_ref, rtol=1e-4)
