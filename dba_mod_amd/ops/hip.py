@@ -77,7 +77,7 @@ _SIGS = {
     "dba_xblock_fwd": [_P, _LL, _P, _LL, _P, _P, _P, _LL, _P, _P, _LL, _P] + [_I] * 6
     + [_P, _I, _P, _P, _I, _P, _I, _P],
     "dba_mlp_train": [_P, _I, _I, _I, _I, _I, _P, _LL, _P, _P, _I, _P, _I, _I, _I, _I, _P, _P, _P, _P, _I, _I,
-                      _P, _LL, _I, _P, _F, _F, _P],
+                      _P, _LL, _I, _P, _F, _F, _P, _P],
     "dba_xstem_fwd": [_P, _LL, _P, _LL, _P, _P, _LL, _P, _P, _LL, _P] + [_I] * 13 + [_P, _I, _P, _I, _P, _P, _P, _P],
 }
 for _name, _args in _SIGS.items():
@@ -211,7 +211,7 @@ _MLP_LAYERS = ("layer1.0.weight", "layer1.0.bias", "layer2.0.weight", "layer2.0.
 
 
 def mlp_train(spec, sched, t0, t1, B, state, mom, fg, rows, labels, trig_cols, trig_vals, target, stats,
-              max_slots, nan_flag, momentum, wd) -> int:
+              max_slots, nan_flag, momentum, wd, prof=None) -> int:
     """Steps [t0, t1) of the step table ``sched`` [T, G*B + 8G] for every client of a LoanNet
     group in ONE launch, one workgroup per client (csrc/kernels/mlp.hip): parameters and
     momentum LDS-resident, written back to ``state`` / ``mom`` at the end.  Returns -100
@@ -226,7 +226,7 @@ def mlp_train(spec, sched, t0, t1, B, state, mom, fg, rows, labels, trig_cols, t
                  state.stride(0), mom.data_ptr(), _ptr(fg), spec.P, offs.data_ptr(), F, H1, H2, C,
                  rows.contiguous().data_ptr(), _i32(labels).data_ptr(), tc.data_ptr(),
                  trig_vals.float().contiguous().data_ptr(), int(tc.shape[1]), int(target), stats.data_ptr(),
-                 stats.shape[1], max_slots, nan_flag.data_ptr(), float(momentum), float(wd), _stream())
+                 stats.shape[1], max_slots, nan_flag.data_ptr(), float(momentum), float(wd), _ptr(prof), _stream())
 
 
 # ------------------------------------------------------------------------------ conv
@@ -524,15 +524,23 @@ def _xconv_fwd(x, w, wsel, stride, pad, bias, residual, relu, nvalid, out_dtype,
 
 
 _EVAL_BLOCK = os.environ.get("DBA_EVAL_BLOCK", "1") != "0"
+# (width, channels) of the fused BasicBlock kernel (xblock.hip): the 32-wide stage.  Whole-image
+# forms for the 16 / 8 / 4-wide stages were measured slower than the two launches (block /
+# 2 x conv: 1.13, 1.07, 2.15 — per-workgroup row counts of 256 / 64 / 32 re-read the weights
+# from L2 far more often than the 128-row implicit GEMM tiles: profiles/r4/xblock/README.md)
+_BLOCK_SHAPES = {(32, 32)}
 
 
 def basic_block_ok(x, w1, w2) -> bool:
     """The fused evaluation BasicBlock (csrc/kernels/xblock.hip) takes this block: fp16-pair
-    forwards, fp32 [G, N, 32, 32, 32] input (not PairAct), 32 -> 32 3x3 weights pre-split at
-    the eval fold.  ``DBA_EVAL_BLOCK=0``: off (the two convs run)."""
-    return (_EVAL_BLOCK and _MODE == F16_PAIR and "fwd" in _H_OPS and x.dtype == _F32 and x.dim() == 5
-            and tuple(x.shape[2:]) == (32, 32, 32) and _pair_sexp(x) is None
-            and all(w.dtype == _F32 and tuple(w.shape[1:]) == (32, 3, 3, 32)
+    forwards, fp32 [G, N, W, W, C] input (not PairAct) of a CIFAR ResNet stage, C -> C 3x3
+    weights pre-split at the eval fold.  ``DBA_EVAL_BLOCK=0``: off (the two convs run)."""
+    if not (_EVAL_BLOCK and _MODE == F16_PAIR and "fwd" in _H_OPS and x.dtype == _F32 and x.dim() == 5
+            and _pair_sexp(x) is None):
+        return False
+    H, W, C = x.shape[2:]
+    return (H == W and (W, C) in _BLOCK_SHAPES
+            and all(w.dtype == _F32 and tuple(w.shape[1:]) == (C, 3, 3, C)
                     and getattr(w, "_dba_planes", None) is not None for w in (w1, w2)))
 
 
@@ -540,8 +548,8 @@ def basic_block_eval(x, w1, b1, w2, b2, wsel=None, nvalid=None):
     """relu(conv2(relu(conv1(x) + b1)) + b2 + x) in one launch (BN folded into w / b; the mid
     activation stays in LDS): xblock.hip.  Callers check :func:`basic_block_ok` first."""
     x = _act(x, _F32, "conv input")
-    G, N = x.shape[:2]
-    per = 32 * 9 * 32
+    G, N, _, W, C = x.shape
+    per = C * 9 * C
     (w1c, ws1), (w2c, ws2) = _check_w(w1), _check_w(w2)
     aw1, aw2 = _amax_w(w1, ws1, per), _amax_w(w2, ws2, per)
     p1, p2 = w1._dba_planes, w2._dba_planes
@@ -553,7 +561,7 @@ def basic_block_eval(x, w1, b1, w2, b2, wsel=None, nvalid=None):
     ay = _amax_out(y)
     rc = _call("dba_xblock_fwd", x.data_ptr(), x.stride(0), y.data_ptr(), y.stride(0), _ptr(_i32(wsel)),
                p1.data_ptr(), p2.data_ptr(), p1.stride(0), b1c.data_ptr(), b2c.data_ptr(), bs1, _ptr(_i32(nvalid)),
-               G, N, 32, 32, 32, 32, *_aptr(ax), aw1.data_ptr(), aw2.data_ptr(), aw1.shape[1], *_aptr(ay), _stream())
+               G, N, W, W, C, C, *_aptr(ax), aw1.data_ptr(), aw2.data_ptr(), aw1.shape[1], *_aptr(ay), _stream())
     if rc == NOT_HANDLED:
         raise RuntimeError("xblock_fwd declined a shape basic_block_ok accepted")
     return y

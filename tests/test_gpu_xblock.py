@@ -39,23 +39,26 @@ def _rel(a, b):
     return ((a - b).norm() / b.norm().clamp(min=1e-30)).item()
 
 
-def _weights(H, slots, dev, g, scale):
-    w = (torch.randn(slots, 32, 3, 3, 32, generator=g) * scale).to(dev)
-    per = 32 * 9 * 32
+def _weights(H, slots, dev, g, scale, C=32):
+    w = (torch.randn(slots, C, 3, 3, C, generator=g) * scale).to(dev)
+    per = C * 9 * C
     H.split_weights(w, per, per, H._amax_w(w, per, per))
     return w
 
 
-@pytest.mark.parametrize("G,N,nv,scale", [(3, 5, (5, 3, 5), 1.0), (2, 4, (4, 1), 1e-3), (1, 9, (9,), 30.0)])
-def test_basic_block_eval_vs_fp64_and_two_launches(H, R64, G, N, nv, scale):
+@pytest.mark.parametrize("G,N,nv,scale,W,C", [
+    (3, 5, (5, 3, 5), 1.0, 32, 32), (2, 4, (4, 1), 1e-3, 32, 32), (1, 9, (9,), 30.0, 32, 32)])
+def test_basic_block_eval_vs_fp64_and_two_launches(H, R64, G, N, nv, scale, W, C):
+    """The 32-wide stage (8 output rows per workgroup, halo rows recomputed), partly valid
+    replicas, a slot map and wide dynamic range."""
     dev = torch.device("cuda")
-    g = torch.Generator().manual_seed(G * 100 + N)
+    g = torch.Generator().manual_seed(G * 100 + N + W)
     slots = 2
-    x = torch.relu(torch.randn(G, N, 32, 32, 32, generator=g) * scale).to(dev)
-    w1 = _weights(H, slots, dev, g, 1.0 / 17)
-    w2 = _weights(H, slots, dev, g, 1.0 / 17)
-    b1 = (torch.randn(slots, 32, generator=g) * 0.1 * scale).to(dev)
-    b2 = (torch.randn(slots, 32, generator=g) * 0.1 * scale).to(dev)
+    x = torch.relu(torch.randn(G, N, W, W, C, generator=g) * scale).to(dev)
+    w1 = _weights(H, slots, dev, g, 1.0 / (3 * C ** 0.5), C)
+    w2 = _weights(H, slots, dev, g, 1.0 / (3 * C ** 0.5), C)
+    b1 = (torch.randn(slots, C, generator=g) * 0.1 * scale).to(dev)
+    b2 = (torch.randn(slots, C, generator=g) * 0.1 * scale).to(dev)
     wsel = torch.tensor([min(i, slots - 1) for i in range(G)], dtype=torch.int32, device=dev)
     nvalid = torch.tensor(nv, dtype=torch.int32, device=dev)
     assert H.basic_block_ok(x, w1, w2)
