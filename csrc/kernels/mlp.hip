@@ -28,7 +28,7 @@
 namespace {
 
 constexpr int kB = 64, kF = 91, kH1 = 46, kH2 = 23, kC = 9;   // batch, LoanNet dims
-constexpr int kH1p = 48, kH2p = 24, kCp = 12;                 // padded to 4-wide blocks
+constexpr int kH1p = 48, kH2p = 24, kFp = 96;                 // zero-padded row counts
 constexpr int kPmax = 6144;                                   // flat parameter floats (aligned entries)
 constexpr int kT = 512;                                       // threads: 8 waves, 2 per SIMD
 // row stride of the feature-major activation images: 68 floats (272 B) puts consecutive rows
@@ -53,8 +53,7 @@ struct MlpArgs {
 
 struct MlpLds {
   float prm[kPmax], mom[kPmax];
-  float w1t[kF * kH1p], w2t[kH1 * kH2p], w3t[kH2 * kCp];   // transposed weights [in][out]
-  float xT[kF * kLD];                                      // batch, feature-major
+  float xT[kFp * kLD];                                     // batch, feature-major (rows >= kF zero)
   float a1T[kH1p * kLD], a2T[kH2p * kLD];                  // post-dropout activations
   float lg[kB * kLG];                                      // dlogits
   float d1T[kH1p * kLD], d2T[kH2p * kLD];                  // pre-activation gradients
@@ -71,6 +70,35 @@ __device__ __forceinline__ void sgd1(MlpLds& s, const MlpArgs& a, float* fgr, in
   s.mom[o] = m;
   s.prm[o] = p - lr * m;
 }
+
+// One 32 x 32 fp32 output tile D[i][j] = sum_k A(i, k) B(k, j), k < 2 nks, on the exact-fp32
+// MFMA (v_mfma_f32_32x32x2_f32: lane l supplies A(l % 32, l / 32) and B(l / 32, l % 32) of
+// each 2-deep step; it holds D rows (r & 3) + 8 (r >> 2) + 4 (l / 32), column l % 32).  The
+// fp32 matrix rate is twice the VALU FMA rate, and each operand value read from LDS feeds a
+// 32-wide outer product instead of 2-4 register-blocked FMAs (the VALU version was bound by
+// LDS return bandwidth and load latency: tools/bench_mlp --prof).
+template <typename FA, typename FB>
+__device__ __forceinline__ f32x16_t mm_tile(int nks, FA fa, FB fb) {
+  f32x16_t acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  const int lane = threadIdx.x & 63, r32 = lane & 31, kh = lane >> 5;
+#pragma unroll 4
+  for (int ks = 0; ks < nks; ++ks) {
+    const int k = 2 * ks + kh;
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fa(r32, k), fb(k, r32), acc, 0, 0, 0);
+  }
+  return acc;
+}
+// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS operations, not for its
+// outstanding global loads (__syncthreads' workgroup release fence would also wait vmcnt(0),
+// i.e. for the next step's prefetched batch rows, which must stay in flight across the step)
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+__device__ __forceinline__ int tile_row(int r) { return (r & 3) + 8 * (r >> 2) + 4 * ((threadIdx.x & 63) >> 5); }
 
 __global__ __launch_bounds__(kT) void mlp_train_kernel(const MlpArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -89,24 +117,10 @@ __global__ __launch_bounds__(kT) void mlp_train_kernel(const MlpArgs a) {
     s.mom[i] = mg[i];
   }
   for (int i = tid; i < kH1p * kLD; i += kT) s.a1T[i] = s.d1T[i] = 0.f;
+  for (int i = tid; i < kFp * kLD; i += kT) s.xT[i] = 0.f;
   for (int i = tid; i < kH2p * kLD; i += kT) s.a2T[i] = s.d2T[i] = 0.f;
   for (int i = tid; i < kB * kLG; i += kT) s.lg[i] = 0.f;
   __syncthreads();
-  auto transpose_w = [&]() __attribute__((always_inline)) {
-    for (int e = tid; e < kF * kH1p; e += kT) {
-      const int f = e / kH1p, j = e - f * kH1p;
-      s.w1t[e] = j < kH1 ? s.prm[a.o_w1 + j * kF + f] : 0.f;
-    }
-    for (int e = tid; e < kH1 * kH2p; e += kT) {
-      const int k = e / kH2p, j = e - k * kH2p;
-      s.w2t[e] = j < kH2 ? s.prm[a.o_w2 + j * kH1 + k] : 0.f;
-    }
-    for (int e = tid; e < kH2 * kCp; e += kT) {
-      const int k = e / kCp, c = e - k * kCp;
-      s.w3t[e] = c < kC ? s.prm[a.o_w3 + c * kH2 + k] : 0.f;
-    }
-  };
-  transpose_w();
 
   // Step descriptors and batch rows are fetched ONE STEP AHEAD into registers (the HBM
   // latency of the random row gather and of the descriptor reads overlaps the current step's
@@ -126,43 +140,55 @@ __global__ __launch_bounds__(kT) void mlp_train_kernel(const MlpArgs a) {
   };
   float gv[NG];
   int gy = -1;
-  auto gather = [&](int t, const Desc& q, int tid) __attribute__((always_inline)) {   // step t's rows -> registers
+  // the gather in two halves, so no wave waits on a global load mid-step: the row indices
+  // (and the label-row index) are loaded first, the rows themselves one phase later, once the
+  // indices have landed; the values are consumed by stage() at the end of the step
+  int gi[NG];
+  int gl = -1;
+  auto gather_idx = [&](int t, const Desc& q, int tid) __attribute__((always_inline)) {
     if (!q.active) return;
     const int* idx = a.sched + (long long)t * a.D + g * kB;
 #pragma unroll
     for (int u = 0; u < NG; ++u) {
       const int e = tid + kT * u;
-      const int b = e / kF, f = e - b * kF;
-      const int r = e < kB * kF ? idx[b] : -1;
-      float v = 0.f;
-      if (r >= 0) {
-        v = a.rows[(long long)r * kF + f];
-        if (q.trig >= 0 && b < q.poison_n)
-          for (int k = 0; k < a.K; ++k)
-            if (a.tcols[q.trig * a.K + k] == f) v = a.tvals[q.trig * a.K + k];
-      }
-      gv[u] = v;
+      gi[u] = e < kB * kF ? idx[e / kF] : -1;
     }
-    if (tid < kB) {
-      const int r = idx[tid];
-      gy = r < 0 ? -1 : ((q.trig >= 0 && tid < q.poison_n) ? a.target : a.labels[r]);
-    }
+    if (tid < kB) gl = idx[tid];
   };
-  auto stage = [&](int tid) __attribute__((always_inline)) {   // registers -> xT / y (no reader in flight)
+  auto gather_rows = [&](const Desc& q, int tid) __attribute__((always_inline)) {
+    if (!q.active) return;
+    // raw row values only: selecting on them here (zero for padded rows, trigger values)
+    // would make the wave wait for the loads mid-step; stage() applies both
+#pragma unroll
+    for (int u = 0; u < NG; ++u) {
+      const int e = tid + kT * u;
+      gv[u] = a.rows[(long long)max(gi[u], 0) * kF + e % kF];
+    }
+    if (tid < kB && gl >= 0) gy = a.labels[gl];
+  };
+  auto gather = [&](int t, const Desc& q, int tid) __attribute__((always_inline)) {
+    gather_idx(t, q, tid);
+    gather_rows(q, tid);
+  };
+  auto stage = [&](const Desc& q, int tid) __attribute__((always_inline)) {   // registers -> xT / y
 #pragma unroll
     for (int u = 0; u < NG; ++u) {
       const int e = tid + kT * u;
       if (e < kB * kF) {
         const int b = e / kF, f = e - b * kF;
-        s.xT[f * kLD + b] = gv[u];
+        float v = gi[u] < 0 ? 0.f : gv[u];
+        if (gi[u] >= 0 && q.trig >= 0 && b < q.poison_n)   // feature trigger of the poisoned rows
+          for (int k = 0; k < a.K; ++k)
+            if (a.tcols[q.trig * a.K + k] == f) v = a.tvals[q.trig * a.K + k];
+        s.xT[f * kLD + b] = v;
       }
     }
-    if (tid < kB) s.y[tid] = gy;
+    if (tid < kB) s.y[tid] = gl < 0 ? -1 : ((q.trig >= 0 && tid < q.poison_n) ? a.target : gy);
   };
 
   Desc cur = desc(a.t0);
   gather(a.t0, cur, tid);
-  stage(tid);
+  stage(cur, tid);
   for (int t = a.t0; t < a.t1; ++t) {
     if (!cur.active) break;
     // an opaque per-step copy of the thread index: everything derived from it (a step's
@@ -178,83 +204,75 @@ __global__ __launch_bounds__(kT) void mlp_train_kernel(const MlpArgs a) {
     const Desc nxt = desc(t + 1);
 #define PROF(k) if (a.prof && tid == 0) a.prof[(long long)(t - a.t0) * 8 + (k)] = (long long)__builtin_readcyclecounter()
     PROF(0);
-    __syncthreads();   // xT / y of step t staged
-    gather(t + 1, nxt, tid);   // lands while this step computes
+    lds_barrier();   // xT / y of step t staged
+    gather_idx(t + 1, nxt, tid);   // the next step's batch: indices now, rows after layer 1
 
-    // ---- layer 1: 2 x 4 (row, unit) blocks, 384 threads
-    if (tid < (kB / 2) * (kH1p / 4)) {
-      const int b0 = (tid & 31) * 2, j0 = (tid >> 5) * 4;
-      float acc[2][4] = {};
-#pragma unroll 7
-      for (int f = 0; f < kF; ++f) {
-        const float2 xv = *(const float2*)&s.xT[f * kLD + b0];
-        const float4 wv = *(const float4*)&s.w1t[f * kH1p + j0];
-        const float xs[2] = {xv.x, xv.y}, ws[4] = {wv.x, wv.y, wv.z, wv.w};
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-          for (int k = 0; k < 4; ++k) acc[i][k] = fmaf(xs[i], ws[k], acc[i][k]);
-      }
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const int j = j0 + k;
-        if (j >= kH1) break;
+    const int c32 = lane & 31;
+    // ---- layer 1: [64 x 91] x W1^T -> 2 x 2 tiles (waves 0-3), + b1, ReLU, dropout (salt 0)
+    if (wid < 4) {
+      const int mt = wid & 1, nt = wid >> 1;
+      const f32x16_t z = mm_tile(
+          (kF + 1) / 2, [&](int i, int k) { return s.xT[k * kLD + mt * 32 + i]; },
+          [&](int k, int j) {
+            const int u = nt * 32 + j;
+            return (u < kH1 && k < kF) ? s.prm[a.o_w1 + u * kF + k] : 0.f;
+          });
+      const int j = nt * 32 + c32;
+      if (j < kH1) {
         const float bj = s.prm[a.o_b1 + j];
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
-          const int b = b0 + i;
+        for (int r = 0; r < 16; ++r) {
+          const int b = mt * 32 + tile_row(r);
           const bool keep = uniform01(seed, (uint32_t)(b * kH1 + j)) >= 0.5f;
-          s.a1T[j * kLD + b] = keep ? fmaxf(acc[i][k] + bj, 0.f) * 2.0f : 0.f;
+          s.a1T[j * kLD + b] = keep ? fmaxf(z[r] + bj, 0.f) * 2.0f : 0.f;
         }
       }
     }
+    gather_rows(nxt, tid);   // lands while this step computes
     PROF(1);
-    __syncthreads();
+    lds_barrier();
 
-    // ---- layer 2: 2 x 4 blocks, 192 threads
-    if (tid < (kB / 2) * (kH2p / 4)) {
-      const int b0 = (tid & 31) * 2, j0 = (tid >> 5) * 4;
-      float acc[2][4] = {};
-#pragma unroll 2
-      for (int k = 0; k < kH1; ++k) {
-        const float2 xv = *(const float2*)&s.a1T[k * kLD + b0];
-        const float4 wv = *(const float4*)&s.w2t[k * kH2p + j0];
-        const float xs[2] = {xv.x, xv.y}, ws[4] = {wv.x, wv.y, wv.z, wv.w};
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-          for (int q = 0; q < 4; ++q) acc[i][q] = fmaf(xs[i], ws[q], acc[i][q]);
-      }
-      const uint32_t sd1 = seed + 0x9E3779B9u;   // salt 1
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int j = j0 + q;
-        if (j >= kH2) break;
+    // ---- layer 2: 2 tiles (waves 0-1), + b2, ReLU, dropout (salt 1)
+    if (wid < 2) {
+      const int mt = wid;
+      const f32x16_t z = mm_tile(
+          kH1 / 2, [&](int i, int k) { return s.a1T[k * kLD + mt * 32 + i]; },
+          [&](int k, int j) { return j < kH2 ? s.prm[a.o_w2 + j * kH1 + k] : 0.f; });
+      const int j = c32;
+      if (j < kH2) {
         const float bj = s.prm[a.o_b2 + j];
+        const uint32_t sd1 = seed + 0x9E3779B9u;
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
-          const int b = b0 + i;
+        for (int r = 0; r < 16; ++r) {
+          const int b = mt * 32 + tile_row(r);
           const bool keep = uniform01(sd1, (uint32_t)(b * kH2 + j)) >= 0.5f;
-          s.a2T[j * kLD + b] = keep ? fmaxf(acc[i][q] + bj, 0.f) * 2.0f : 0.f;
+          s.a2T[j * kLD + b] = keep ? fmaxf(z[r] + bj, 0.f) * 2.0f : 0.f;
         }
       }
     }
     PROF(2);
-    __syncthreads();
+    lds_barrier();
 
-    // ---- layer 3 + softmax cross-entropy (one row per thread of wave 0)
+    // ---- layer 3 logits: 2 tiles (waves 0-1) -> lg
+    if (wid < 2) {
+      const int mt = wid;
+      const f32x16_t z = mm_tile(
+          kH2p / 2, [&](int i, int k) { return s.a2T[k * kLD + mt * 32 + i]; },
+          [&](int k, int c) { return (c < kC && k < kH2) ? s.prm[a.o_w3 + c * kH2 + k] : 0.f; });
+      if (c32 < kC) {
+        const float bc = s.prm[a.o_b3 + c32];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) s.lg[(mt * 32 + tile_row(r)) * kLG + c32] = z[r] + bc;
+      }
+    }
+    lds_barrier();
+
+    // ---- softmax cross-entropy (one row per thread of wave 0): dlogits into lg
     if (wid == 0) {
       const int b = lane;
       float x[kC];
 #pragma unroll
-      for (int c = 0; c < kC; ++c) x[c] = 0.f;
-      for (int k = 0; k < kH2; ++k) {
-        const float av = s.a2T[k * kLD + b];
-#pragma unroll
-        for (int c = 0; c < kC; ++c) x[c] = fmaf(av, s.w3t[k * kCp + c], x[c]);
-      }
-#pragma unroll
-      for (int c = 0; c < kC; ++c) x[c] += s.prm[a.o_b3 + c];
+      for (int c = 0; c < kC; ++c) x[c] = s.lg[b * kLG + c];
       const int y = s.y[b];
       const float scale = nvalid > 0 ? 1.0f / (float)nvalid : 1.0f;
       double wl = 0.0;
@@ -295,109 +313,108 @@ __global__ __launch_bounds__(kT) void mlp_train_kernel(const MlpArgs a) {
       }
     }
     PROF(3);
-    __syncthreads();
+    lds_barrier();
 
-    // ---- d(layer-2 output): dlogits W3, masked by the dropout / ReLU of a2
-    for (int e = tid; e < kB * kH2; e += kT) {
-      const int j = e / kB, b = e - j * kB;
-      float acc = 0.f;
+    // ---- d(layer-2 output) = dlogits W3, masked by a2's dropout / ReLU: 2 tiles (waves 0-1)
+    if (wid < 2) {
+      const int mt = wid;
+      const f32x16_t z = mm_tile(
+          (kC + 1) / 2, [&](int i, int k) { return k < kC ? s.lg[(mt * 32 + i) * kLG + k] : 0.f; },
+          [&](int k, int j) { return (k < kC && j < kH2) ? s.prm[a.o_w3 + k * kH2 + j] : 0.f; });
+      const int j = c32;
+      if (j < kH2) {
 #pragma unroll
-      for (int c = 0; c < kC; ++c) acc = fmaf(s.lg[b * kLG + c], s.prm[a.o_w3 + c * kH2 + j], acc);
-      s.d2T[j * kLD + b] = s.a2T[j * kLD + b] > 0.f ? acc * 2.0f : 0.f;
+        for (int r = 0; r < 16; ++r) {
+          const int b = mt * 32 + tile_row(r);
+          s.d2T[j * kLD + b] = s.a2T[j * kLD + b] > 0.f ? z[r] * 2.0f : 0.f;
+        }
+      }
     }
     PROF(4);
-    __syncthreads();
+    lds_barrier();
 
-    // ---- d(layer-1 output) (reads W2) | layer-3 gradients + SGD (W3 no longer read)
-    for (int e = tid; e < kB * kH1; e += kT) {
-      const int k = e / kB, b = e - k * kB;
-      float acc = 0.f;
+    // ---- d(layer-1 output) = d2 W2 (waves 0-3, reads W2) | layer-3 weight gradient + SGD
+    // (wave 4: W3 is no longer read) | layer-3 bias gradient (wave 5)
+    if (wid < 4) {
+      const int mt = wid & 1, nt = wid >> 1;
+      const f32x16_t z = mm_tile(
+          kH2p / 2, [&](int i, int k) { return s.d2T[k * kLD + mt * 32 + i]; },
+          [&](int k, int j) {
+            const int u = nt * 32 + j;
+            return (u < kH1 && k < kH2) ? s.prm[a.o_w2 + k * kH1 + u] : 0.f;
+          });
+      const int k = nt * 32 + c32;
+      if (k < kH1) {
 #pragma unroll
-      for (int j = 0; j < kH2; ++j) acc = fmaf(s.d2T[j * kLD + b], s.prm[a.o_w2 + j * kH1 + k], acc);
-      s.d1T[k * kLD + b] = s.a1T[k * kLD + b] > 0.f ? acc * 2.0f : 0.f;
-    }
-    for (int e = tid; e < kC * kH2 + kC; e += kT) {
-      float gr = 0.f;
-      if (e < kC * kH2) {
-        const int c = e / kH2, j = e - c * kH2;
-        for (int b = 0; b < kB; ++b) gr = fmaf(s.lg[b * kLG + c], s.a2T[j * kLD + b], gr);
-        sgd1(s, a, fgr, a.o_w3 + e, gr, lr, first);
-        s.w3t[j * kCp + c] = s.prm[a.o_w3 + e];
-      } else {
-        const int c = e - kC * kH2;
-        for (int b = 0; b < kB; ++b) gr += s.lg[b * kLG + c];
-        sgd1(s, a, fgr, a.o_b3 + c, gr, lr, first);
+        for (int r = 0; r < 16; ++r) {
+          const int b = mt * 32 + tile_row(r);
+          s.d1T[k * kLD + b] = s.a1T[k * kLD + b] > 0.f ? z[r] * 2.0f : 0.f;
+        }
       }
+    } else if (wid == 4) {
+      const f32x16_t gw = mm_tile(
+          kB / 2, [&](int c, int b) { return c < kC ? s.lg[b * kLG + c] : 0.f; },
+          [&](int b, int j) { return j < kH2 ? s.a2T[j * kLD + b] : 0.f; });
+      const int j = c32;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int c = tile_row(r);
+        if (c < kC && j < kH2) sgd1(s, a, fgr, a.o_w3 + c * kH2 + j, gw[r], lr, first);
+      }
+    } else if (wid == 5 && lane < kC) {
+      float p0 = 0.f, p1 = 0.f, p2 = 0.f, p3 = 0.f;
+#pragma unroll
+      for (int b = 0; b < kB; b += 4) {
+        p0 += s.lg[b * kLG + lane];
+        p1 += s.lg[(b + 1) * kLG + lane];
+        p2 += s.lg[(b + 2) * kLG + lane];
+        p3 += s.lg[(b + 3) * kLG + lane];
+      }
+      sgd1(s, a, fgr, a.o_b3 + lane, (p0 + p1) + (p2 + p3), lr, first);
     }
     PROF(5);
-    __syncthreads();
+    lds_barrier();
 
-    // ---- layer-1 / layer-2 weight + bias gradients and SGD: 4 x 4 (unit, input) blocks, the
-    // block's inputs {q, q + n4, q + 2 n4, q + 3 n4} so consecutive lanes read consecutive
-    // activation rows (conflict-free), its units 4 consecutive (a broadcast per lane group)
-    constexpr int F4 = (kF + 3) / 4, K4 = (kH1 + 3) / 4;                 // 23, 12
-    constexpr int N1 = ((kH1 + 3) / 4) * F4, N2 = ((kH2 + 3) / 4) * K4, NB = kH1 + kH2;
-    static_assert(N1 + N2 + NB <= kT, "one pass");
-    if (tid < N1 + N2) {
-      const bool l1 = tid < N1;
-      const int e2 = l1 ? tid : tid - N1;
-      const int nin = l1 ? kF : kH1, nout = l1 ? kH1 : kH2, n4 = l1 ? F4 : K4;
-      const int j0 = (e2 / n4) * 4, q = e2 % n4;
-      const float* dT = l1 ? s.d1T : s.d2T;
-      const float* inT = l1 ? s.xT : s.a1T;
-      int jr[4], fr4[4];
+    // ---- layer-1 (6 tiles, waves 0-5) / layer-2 (2 tiles, waves 6-7) weight gradients + SGD,
+    // then the layer-1 / layer-2 bias gradients
+    if (wid < 6) {
+      const int jt = wid / 3, ft = wid % 3;
+      const f32x16_t gw = mm_tile(
+          kB / 2, [&](int i, int b) { const int j = jt * 32 + i; return j < kH1 ? s.d1T[j * kLD + b] : 0.f; },
+          [&](int b, int f) { const int ff = ft * 32 + f; return ff < kF ? s.xT[ff * kLD + b] : 0.f; });
+      const int f = ft * 32 + c32;
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        jr[u] = min(j0 + u, nout - 1);            // clamped rows: their sums are discarded
-        fr4[u] = min(q + u * n4, nin - 1);
+      for (int r = 0; r < 16; ++r) {
+        const int j = jt * 32 + tile_row(r);
+        if (j < kH1 && f < kF) sgd1(s, a, fgr, a.o_w1 + j * kF + f, gw[r], lr, first);
       }
-      float gw[4][4] = {};
-#pragma unroll 2
+    } else {
+      const int kt = wid - 6;
+      const f32x16_t gw = mm_tile(
+          kB / 2, [&](int j, int b) { return j < kH2 ? s.d2T[j * kLD + b] : 0.f; },
+          [&](int b, int k) { const int kk = kt * 32 + k; return kk < kH1 ? s.a1T[kk * kLD + b] : 0.f; });
+      const int k = kt * 32 + c32;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int j = tile_row(r);
+        if (j < kH2 && k < kH1) sgd1(s, a, fgr, a.o_w2 + j * kH1 + k, gw[r], lr, first);
+      }
+    }
+    if (tid < kH1 + kH2) {
+      const bool l1 = tid < kH1;
+      const int u = l1 ? tid : tid - kH1;
+      const float* dT = l1 ? s.d1T : s.d2T;
+      float4 p = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
       for (int b = 0; b < kB; b += 4) {
-        float4 dv[4], xv[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          dv[u] = *(const float4*)&dT[jr[u] * kLD + b];
-          xv[u] = *(const float4*)&inT[fr4[u] * kLD + b];
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-#pragma unroll
-          for (int v = 0; v < 4; ++v) {
-            gw[u][v] = fmaf(dv[u].x, xv[v].x, gw[u][v]);
-            gw[u][v] = fmaf(dv[u].y, xv[v].y, gw[u][v]);
-            gw[u][v] = fmaf(dv[u].z, xv[v].z, gw[u][v]);
-            gw[u][v] = fmaf(dv[u].w, xv[v].w, gw[u][v]);
-          }
+        const float4 v = *(const float4*)&dT[u * kLD + b];
+        p.x += v.x; p.y += v.y; p.z += v.z; p.w += v.w;
       }
-      const int ow = l1 ? a.o_w1 : a.o_w2;
-      float* wt = l1 ? s.w1t : s.w2t;
-      const int ldt = l1 ? kH1p : kH2p;
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int j = j0 + u;
-        if (j >= nout) break;
-#pragma unroll
-        for (int v = 0; v < 4; ++v) {
-          const int f = q + v * n4;
-          if (f >= nin) break;
-          const int o = ow + j * nin + f;
-          sgd1(s, a, fgr, o, gw[u][v], lr, first);
-          wt[f * ldt + j] = s.prm[o];
-        }
-      }
-    } else if (tid < N1 + N2 + NB) {
-      const int j = tid - N1 - N2;
-      const bool l1 = j < kH1;
-      const int u = l1 ? j : j - kH1;
-      const float* dT = l1 ? s.d1T : s.d2T;
-      float gr = 0.f;
-      for (int b = 0; b < kB; ++b) gr += dT[u * kLD + b];
-      sgd1(s, a, fgr, (l1 ? a.o_b1 : a.o_b2) + u, gr, lr, first);
+      sgd1(s, a, fgr, (l1 ? a.o_b1 : a.o_b2) + u, (p.x + p.y) + (p.z + p.w), lr, first);
     }
     PROF(6);
-    __syncthreads();   // xT and the weights of step t are no longer read
-    stage(tid);
+    lds_barrier();   // xT and the weights of step t are no longer read
+    stage(nxt, tid);
     cur = nxt;
 #undef PROF
   }
