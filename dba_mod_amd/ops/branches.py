@@ -83,7 +83,14 @@ class BranchReplay:
         def maxpool2d(x, kk, st, p):
             y, ind = o_mp(x, kk, st, p)
             return self._pool(x, y, ind)
-        return {"conv2d": conv2d, "maxpool2d": maxpool2d, "conv_bn_stats": conv_bn_stats, "bn_apply": bn_apply}
+
+        def basic_block_ok(x, w1, w2):
+            # the fused evaluation BasicBlock keeps its mid activation (and so its ReLU
+            # decisions) on chip: recorded and replayed runs both take the two convs, whose
+            # decisions this oracle sees (the fused kernel has its own fp64 test)
+            return False
+        return {"conv2d": conv2d, "maxpool2d": maxpool2d, "conv_bn_stats": conv_bn_stats, "bn_apply": bn_apply,
+                "basic_block_ok": basic_block_ok}
 
     def _valid(self, t):
         v = torch.zeros(t.shape[:2], dtype=torch.bool)
