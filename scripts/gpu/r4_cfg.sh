@@ -8,7 +8,9 @@ run() {  # $1 tag, $2 timeout, rest bench args
   timeout -k 10 $t python bench.py "$@" > $O/$tag.log 2>&1 || { tail -20 $O/$tag.log; exit 1; }
   echo "$tag: $(grep -o '"value": [0-9.]*' $O/$tag.log) $(grep -o '"rounds_timed": "[0-9.]*"' $O/$tag.log) $(grep -o '"global_acc": [0-9.]*, "global_asr": [0-9.]*' $O/$tag.log)"
 }
-for spec in ${RUNS:-"mnist_1024:--config configs/mnist_params.yaml" "mnist_10000:--config configs/mnist_params.yaml --set eval_batch_size=10000" "cifar:--steps 20 --warmup 5"}; do
+# RUNS: "tag:bench args;tag:bench args;..."
+IFS=';' read -ra SPECS <<< "${RUNS:-mnist:--config configs/mnist_params.yaml;cifar:--steps 20 --warmup 5}"
+for spec in "${SPECS[@]}"; do
   tag=${spec%%:*}; args=${spec#*:}
   run $tag 600 $args
 done
