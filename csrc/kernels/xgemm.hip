@@ -175,8 +175,15 @@ __device__ __forceinline__ int pair_out_exp(const XArgs& a, int g, int slot) {
   return hexp(__float_as_int(2.f * b));
 }
 
+// register budget: XCONV_MINB=2 fits two workgroups per CU (<= 256 registers per lane, no
+// spills) but measured no faster than one (eval / training conv TFLOP/s within 1 %, bench 3.04
+// vs 3.09 rounds/s, same box: profiles/r4/minb/) — the 128x128 eval tiles are bound by the
+// MFMA work at the DVFS-held clock, not by latency; one workgroup per CU stays the default
+#ifndef XCONV_MINB
+#define XCONV_MINB 1
+#endif
 template <int BM, int BN, int WM, int WN, int P, int VEC, bool H, bool PW = false, bool PA = false, bool LZ = false>
-__global__ __launch_bounds__(256) void xconv_kernel(const XArgs a) {
+__global__ __launch_bounds__(256, XCONV_MINB) void xconv_kernel(const XArgs a) {
   static_assert(!H || P == 2, "fp16 split: 2 planes");
   static_assert(!LZ || (H && !PA && VEC >= 4), "lazy BN operand: fp16 pair, fp32 source, 4-channel vectors");
   static_assert(!PW || (H && VEC >= 4), "pre-split weights: fp16 pair, vector loads");

@@ -25,7 +25,9 @@ ARCH = os.environ.get("DBA_OFFLOAD_ARCH", "gfx950")
 
 
 def kernels_path() -> str:
-    return os.path.join(LIBDIR, "libdba_kernels.so")
+    """The kernel library; ``DBA_KERNELS_LIB`` loads another build of it (same-box A/Bs of
+    compile-time choices, e.g. scripts/gpu/r4_minb.sh)."""
+    return os.environ.get("DBA_KERNELS_LIB") or os.path.join(LIBDIR, "libdba_kernels.so")
 
 
 def runtime_path() -> str:
