@@ -225,6 +225,18 @@ class Ctx:
         return ops.conv2d(a, w2, self.wsel, 1, 1, bias=b2, residual=x, relu=True, nvalid=self.nvalid,
                           **({"out_pairs": True} if (self.eval_pairs and to_conv) else {}))
 
+    def stem_block(self, x: Tensor, stem: str, pre: str) -> Optional[Tensor]:
+        """Evaluation of the CIFAR stem conv+BN+ReLU followed by the identity BasicBlock
+        ``pre`` as ONE launch where the backend has it (ops.hip.stem_block_eval: the stem's
+        32-channel output never leaves the chip); None where it does not (the caller runs
+        them separately)."""
+        w0, b0 = self.folded[stem]
+        w1, b1 = self.folded[pre + "conv1.weight"]
+        w2, b2 = self.folded[pre + "conv2.weight"]
+        if self.eval_pairs or not ops.stem_block_ok(x, w0, w1, w2):
+            return None
+        return ops.stem_block_eval(x, w0, b0, w1, b1, w2, b2, self.wsel, self.nvalid)
+
     # ---------------------------------------------------------- fused training BN
     def _bnp(self, bn: str) -> bs.BnParams:
         return bs.BnParams(self.m(bn + ".weight"), self.m(bn + ".bias"), self.m(bn + ".running_mean"),
@@ -397,10 +409,14 @@ def _resnet_cifar(ctx: Ctx, x: Tensor) -> Tensor:
     adds); block outputs are stored."""
     bottleneck, blocks = CIFAR_RESNETS[ctx.spec.arch]
     exp = 4 if bottleneck else 1
-    out = ctx.bn_conv(x, "conv1.weight", "bn1", 1, 1, relu=True)
+    # evaluation: the stem + layer1.0 as one fused launch where the backend has it
+    out = None if (ctx.train or bottleneck) else ctx.stem_block(x, "conv1.weight", "layer1.0.")
+    done = 0 if out is None else 1   # layer1 blocks already applied
+    if out is None:
+        out = ctx.bn_conv(x, "conv1.weight", "bn1", 1, 1, relu=True)
     cin = 32
     for li, w in enumerate((32, 64, 128, 256)):
-        for bi in range(blocks[li]):
+        for bi in range(done if li == 0 else 0, blocks[li]):
             stride = 2 if (li > 0 and bi == 0) else 1
             pre = f"layer{li + 1}.{bi}."
             final = li == 3 and bi == blocks[li] - 1

@@ -73,9 +73,11 @@ _SIGS = {
     "dba_bnfuse_size": [],
     "dba_bnx_dy": [_P, _P, _P, _P, _LL, _P, _I, _I, _I, _I, _P, _I, _P],
     "dba_xwgrad_reduce_batch": [_P, _I, _I, _LL, _P],
-    # image stems in exact fp32 (csrc/kernels/stem.hip)
+    # fused evaluation BasicBlock, with or without the image stem (csrc/kernels/xblock.hip)
     "dba_xblock_fwd": [_P, _LL, _P, _LL, _P, _P, _P, _LL, _P, _P, _LL, _P] + [_I] * 6
     + [_P, _I, _P, _P, _I, _P, _I, _P],
+    "dba_xblock_stem_fwd": [_P, _LL, _P, _LL, _P, _P, _LL, _P, _LL, _P, _P, _LL, _P, _P, _LL, _P] + [_I] * 6
+    + [_P, _P, _P, _I, _P, _I, _P],
     "dba_mlp_train": [_P, _I, _I, _I, _I, _I, _P, _LL, _P, _P, _I, _P, _I, _I, _I, _I, _P, _P, _P, _P, _I, _I,
                       _P, _LL, _I, _P, _F, _F, _P, _P],
     "dba_xstem_fwd": [_P, _LL, _P, _LL, _P, _P, _LL, _P, _P, _LL, _P] + [_I] * 13 + [_P, _I, _P, _I, _P, _P, _P, _P],
@@ -566,6 +568,47 @@ def basic_block_eval(x, w1, b1, w2, b2, wsel=None, nvalid=None):
                G, N, W, W, C, C, *_aptr(ax), aw1.data_ptr(), aw2.data_ptr(), aw1.shape[1], *_aptr(ay), _stream())
     if rc == NOT_HANDLED:
         raise RuntimeError("xblock_fwd declined a shape basic_block_ok accepted")
+    return y
+
+
+_EVAL_STEM = os.environ.get("DBA_EVAL_STEM", "1") != "0"
+
+
+def stem_block_ok(x, w0, w1, w2) -> bool:
+    """The stem + first BasicBlock of the 32-wide stage run as one launch (xblock.hip STEM
+    variant): [G, N, 32, 32, 3] fp32 images, a 3x3 3 -> 32 stem and the block's weights all
+    pre-split at the eval fold.  ``DBA_EVAL_STEM=0``: off (stem launch + fused block)."""
+    if not (_EVAL_STEM and _EVAL_BLOCK and _MODE == F16_PAIR and "fwd" in _H_OPS and x.dtype == _F32
+            and x.dim() == 5 and tuple(x.shape[2:]) == (32, 32, 3)):
+        return False
+    return (w0.dtype == _F32 and tuple(w0.shape[1:]) == (32, 3, 3, 3) and getattr(w0, "_dba_planes", None) is not None
+            and all(w.dtype == _F32 and tuple(w.shape[1:]) == (32, 3, 3, 32)
+                    and getattr(w, "_dba_planes", None) is not None for w in (w1, w2)))
+
+
+def stem_block_eval(x, w0, b0, w1, b1, w2, b2, wsel=None, nvalid=None):
+    """relu(conv2(h) + b2 + s), h = relu(conv1(s) + b1), s = relu(stem(x) + b0): the CIFAR
+    ResNet stem and layer1.0 (BN folded) in one launch; the stem output stays on chip
+    (xblock.hip).  Callers check :func:`stem_block_ok` first."""
+    x = _act(x, _F32, "image")
+    G, N, _, W, Ci = x.shape
+    C = w1.shape[1]
+    per = C * 9 * C
+    (w0c, ws0), (w1c, ws1), (w2c, ws2) = _check_w(w0), _check_w(w1), _check_w(w2)
+    aw0 = _amax_w(w0, ws0, C * 9 * Ci)
+    aw1, aw2 = _amax_w(w1, ws1, per), _amax_w(w2, ws2, per)
+    p0, p1, p2 = w0._dba_planes, w1._dba_planes, w2._dba_planes
+    assert p1.stride(0) == p2.stride(0) and aw0.shape[1] == aw1.shape[1] == aw2.shape[1]
+    (b0c, bs0), (b1c, bs1), (b2c, bs2) = _rowview(b0), _rowview(b1), _rowview(b2)
+    assert bs1 == bs2 and b0c.dtype == b1c.dtype == b2c.dtype == _F32
+    y = torch.empty(G, N, W, W, C, dtype=_F32, device=x.device)
+    ay = _amax_out(y)
+    rc = _call("dba_xblock_stem_fwd", x.data_ptr(), x.stride(0), y.data_ptr(), y.stride(0), _ptr(_i32(wsel)),
+               p0.data_ptr(), p0.stride(0), b0c.data_ptr(), bs0, p1.data_ptr(), p2.data_ptr(), p1.stride(0),
+               b1c.data_ptr(), b2c.data_ptr(), bs1, _ptr(_i32(nvalid)), G, N, W, W, Ci, C, aw0.data_ptr(),
+               aw1.data_ptr(), aw2.data_ptr(), aw1.shape[1], *_aptr(ay), _stream())
+    if rc == NOT_HANDLED:
+        raise RuntimeError("xblock_stem_fwd declined a shape stem_block_ok accepted")
     return y
 
 

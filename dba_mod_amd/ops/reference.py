@@ -149,6 +149,20 @@ def basic_block_eval(x: Tensor, w1: Tensor, b1: Tensor, w2: Tensor, b2: Tensor,
     return conv2d(h, w2, wsel, 1, 1, bias=b2, residual=x, relu=True, nvalid=nvalid)
 
 
+def stem_block_ok(x: Tensor, w0: Tensor, w1: Tensor, w2: Tensor) -> bool:
+    """Whether the backend runs the stem + first BasicBlock as one fused op (HIP: xblock.hip
+    STEM variant); the reference runs the three convs."""
+    return False
+
+
+def stem_block_eval(x: Tensor, w0: Tensor, b0: Tensor, w1: Tensor, b1: Tensor, w2: Tensor, b2: Tensor,
+                    wsel: Optional[Tensor] = None, nvalid: Optional[Tensor] = None) -> Tensor:
+    """The CIFAR ResNet stem relu(conv(x) + b0) (3x3, pad 1) followed by the identity
+    BasicBlock of :func:`basic_block_eval`, BN folded (reference models/resnet_cifar.py:80-88)."""
+    s = conv2d(x, w0, wsel, 1, 1, bias=b0, relu=True, nvalid=nvalid)
+    return basic_block_eval(s, w1, b1, w2, b2, wsel, nvalid)
+
+
 def _valid_mask(t: Tensor, nvalid: Optional[Tensor]) -> Tensor:
     """[G, N, 1, 1, 1] (bool) of the valid images of each replica."""
     G, N = t.shape[:2]

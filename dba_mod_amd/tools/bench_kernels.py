@@ -95,6 +95,18 @@ def _bench_fp32(name, G, N, Hh, Cin, Cout, k, s, p, reps, dev):
         xb._dba_amax = H._amax_act(xb, None)
         block_flops = 2 * flops
         ops.append(("block", lambda: H.basic_block_eval(xb, w, b1, w2, b2)))
+    if name == "eval.stem" and H.fp32_mode() == H.F16_PAIR:
+        # the stem + layer1.0 (xblock.hip STEM variant) vs the stem launch + fused block; their
+        # TFLOP/s count the stem's and both block convs' fp32 work
+        wb = [torch.randn(G, 32, 3, 3, 32, device=dev) * 0.05 for _ in range(2)]
+        for wi in wb:
+            H.split_weights(wi, 9216, 9216, H._amax_w(wi, 9216, 9216))
+        b0, b1, b2 = [torch.randn(G, 32, device=dev) * 0.1 for _ in range(3)]
+        if H.stem_block_ok(x, w, *wb):
+            block_flops = flops + 2 * 2.0 * G * N * 32 * 32 * 32 * 9 * 32
+            ops += [("stem_then_block", lambda: H.basic_block_eval(H.conv2d(x, w, None, 1, 1, bias=b0, relu=True),
+                                                                 wb[0], b1, wb[1], b2)),
+                    ("stem_block", lambda: H.stem_block_eval(x, w, b0, wb[0], b1, wb[1], b2))]
     if name.startswith("train"):
         wt = H.prepare_dgrad_weights(w, [(w, None, s, p, (Hh, Hh), None, G)])[0]
         dw = torch.zeros(G, Cout, k, k, Cin, device=dev)
@@ -103,7 +115,8 @@ def _bench_fp32(name, G, N, Hh, Cin, Cout, k, s, p, reps, dev):
     for tag, fn in ops:
         t = _time(fn, reps)
         rec[tag + "_us"] = round(t * 1e6, 1)
-        rec[tag + "_tflops"] = round((block_flops if tag == "block" else flops) / t / 1e12, 1)
+        rec[tag + "_tflops"] = round((block_flops if tag in ("block", "stem_block", "stem_then_block") else flops)
+                                     / t / 1e12, 1)
     return rec
 
 
