@@ -788,6 +788,223 @@ __global__ __launch_bounds__(256) void xhalo_kernel(const XArgs a) {
   }
 }
 
+// ================================================================ whole-image halo conv
+// Stride-1 3x3 pad-1 evaluation forward of the small-image stages (W 8 / 4: ResNet stages 3
+// and 4 on 32x32 inputs; fp16 pair, weights pre-split at the eval fold).  The implicit GEMM re-fetches every
+// input element once per tap, and at these shapes its operand fetch — not the MFMA — bounds
+// it (eval.layer3 / 4 ran +37 / +43 % faster with the in-loop global loads removed, against
+// +5 % without the in-loop barriers: profiles/r4/ximg).  Here a block owns IMGS whole images
+// (128 output pixels) x BN output channels; the reduction runs channel-chunk-major (chunk of
+// 32 channels, then its 9 taps): each chunk's zero-padded patch (IMGS x (W+2)^2 pixels x 32
+// channels) is loaded once, split once into the LDS patch, and read by all 9 taps at their
+// pixel offsets — (W+2)^2 / W^2 = 1.56x / 2.25x of the image bytes instead of 9x.  The next
+// chunk's patch is loaded into registers while the current chunk's 9 k-steps run (8 steps to
+// land), so the only exposed cost is its split + LDS store at the chunk boundary.  Weights:
+// the two-stage register / LDS ring of xhalo_kernel.  Epilogue straight from the
+// accumulators (a 32-lane row is 32 consecutive output channels: 128-B segments).
+// Deterministic; the chunk-major k order makes its bits differ from the tap-major implicit
+// GEMM's (both fp32 level: tests hold both to the fp64 oracle).
+template <int W, int IMGS, int BN, int WM, int WN, bool PRE>
+__global__ __launch_bounds__(256) void ximg_kernel(const XArgs a) {
+  constexpr int P = 2;
+  constexpr int PW = W + 2, PI = PW * PW, PP = IMGS * PI;   // padded pixels per image / patch
+  constexpr int CC = 32, CH = CC / 8, Q4 = CC / 4;          // chunk channels, 16-B chunks, float4 per pixel
+  constexpr int PATCH = PP * CH;                            // uint4 per plane
+  constexpr int BM = IMGS * W * W;
+  constexpr int TM = BM / WM, TN = BN / WN, MI = TM / 32, NJ = TN / 32;
+  static_assert(WM * WN == 4 && MI >= 1 && NJ >= 1 && BM == 128, "tiling");
+  constexpr int RB = BN / 32, BPL = BN * 4;
+  __shared__ __attribute__((aligned(16))) uint4 patch[P * PATCH];
+  __shared__ __attribute__((aligned(16))) uint4 bring[2 * P * BPL];
+
+  const int g = blockIdx.y;
+  const int tn = blockIdx.x % a.tiles_n, tm = blockIdx.x / a.tiles_n;
+  const int img0 = tm * IMGS, n0 = tn * BN;
+  const int nv = min(valid_rows(a.nvalid, g, a.N), a.N);
+  if (img0 >= nv) return;
+  const int slot = a.wsel ? a.wsel[g] : g;
+  const int Cs = a.Cs, K = 9 * Cs, NC = Cs / CC, NK = 9 * NC;
+  const float* __restrict__ src = a.src + (long long)g * a.src_gstride;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WN, wn = wid % WN;
+  const int kq = tid & 7, r0 = tid >> 3;
+  const int fr = lane & 31, hf = lane >> 5;
+
+  // ---- patch chunks: chunk cc of images img0 .. img0+IMGS-1, zero padding / invalid images
+  constexpr int NE = (PP * Q4 + 255) / 256;
+  float4 pv[NE];
+  const __amdgpu_buffer_rsrc_t rA = rsrc(src, (long long)a.N * W * W * Cs * 4);
+  auto pload = [&](int cc) __attribute__((always_inline)) {
+#pragma unroll
+    for (int u = 0; u < NE; ++u) {
+      const int e = tid + 256 * u;
+      const int pp = e / Q4, q = e - pp * Q4;
+      const int im = pp / PI, rem = pp - im * PI;
+      const int h = rem / PW - 1, w = rem % PW - 1, img = img0 + im;
+      const bool ok = e < PP * Q4 && img < nv && (unsigned)h < (unsigned)W && (unsigned)w < (unsigned)W;
+      pv[u] = bload4(rA, ok ? (((img * W + h) * W + w) * Cs + cc * CC + q * 4) * 4 : kOOB);
+    }
+  };
+  HScale hs;
+  auto patch_put = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int u = 0; u < NE; ++u) {
+      const int e = tid + 256 * u;
+      if (e >= PP * Q4) break;
+      const int pp = e / Q4, q = e - pp * Q4;
+      uint2 sp[P];
+      split4h(pv[u].x, pv[u].y, pv[u].z, pv[u].w, hs.ma, sp);
+      const int o = pp * CH + ((q >> 1) ^ hswz<W, CC>(pp, 0));
+#pragma unroll
+      for (int p = 0; p < P; ++p) ((uint2*)&patch[p * PATCH + o])[q & 1] = sp[p];
+    }
+  };
+
+  // ---- weights (pre-split planes, or fp32 split while staging: the same bits): two-stage
+  // pipeline, k-step t = chunk t / 9, tap t % 9
+  int boffs[RB];
+#pragma unroll
+  for (int j = 0; j < RB; ++j) {
+    const int n = n0 + r0 + 32 * j;
+    boffs[j] = n < a.Ncol ? n * K : -1;
+  }
+  const uint16_t* Bh = PRE ? a.wp + (long long)slot * a.wp_sstride : nullptr;
+  const __amdgpu_buffer_rsrc_t rBh = rsrc(Bh, (long long)a.Ncol * K * 2);
+  const __amdgpu_buffer_rsrc_t rBl = rsrc(PRE ? Bh + (a.wp_sstride >> 1) : nullptr, (long long)a.Ncol * K * 2);
+  const __amdgpu_buffer_rsrc_t rB = rsrc(a.w + (long long)slot * a.w_sstride, (long long)a.Ncol * K * 4);
+  uint4 rb[2][RB];
+  auto gq = [&](int t, int st, int j) __attribute__((always_inline)) {
+    const int cc = t / 9, tap = t - cc * 9;
+    const int kb = boffs[j] + tap * Cs + cc * CC + kq * 4;
+    const bool ok = boffs[j] >= 0 && t < NK;
+    if constexpr (PRE) {
+      const uint2 h = bload8(rBh, ok ? kb * 2 : kOOB), l = bload8(rBl, ok ? kb * 2 : kOOB);
+      rb[st][j] = make_uint4(h.x, h.y, l.x, l.y);
+    } else {
+      rb[st][j] = __builtin_bit_cast(uint4, bload4(rB, ok ? kb * 4 : kOOB));
+    }
+  };
+  auto lput_q = [&](int buf, int st, int q) __attribute__((always_inline)) {
+    if (q >= RB) return;
+    uint2 sp[P];
+    if constexpr (PRE) {
+      sp[0] = make_uint2(rb[st][q].x, rb[st][q].y);
+      sp[1] = make_uint2(rb[st][q].z, rb[st][q].w);
+    } else {
+      const float4 v = __builtin_bit_cast(float4, rb[st][q]);
+      split4h(v.x, v.y, v.z, v.w, hs.mb, sp);
+    }
+    lds_put<P, false, BN>(bring + buf * P * BPL, BPL, 0, r0 + 32 * q, kq, sp);
+  };
+
+  f32x16_t acc[MI][NJ];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  int apix[MI];   // patch pixel of each A fragment row at tap (0, 0)
+#pragma unroll
+  for (int i = 0; i < MI; ++i) {
+    const int m = wm * TM + i * 32 + fr;
+    const int im = m / (W * W), rem = m - im * (W * W);
+    apix[i] = im * PI + (rem / W) * PW + rem % W;
+  }
+  auto mma = [&](int t, int buf, int stn) __attribute__((always_inline)) {
+    const int tap = t % 9, ti = tap / 3, tj = tap - ti * 3;
+    const int toff = ti * PW + tj;
+    const uint4* L = bring + buf * P * BPL;
+    sfor<2>([&](auto KK) __attribute__((always_inline)) {
+      const int ch = decltype(KK)::value * 2 + hf;
+      uint4 af[P][MI], bfr[P][NJ];
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        const int pp = apix[i] + toff;
+        const int o = pp * CH + (ch ^ hswz<W, CC>(pp, 0));
+#pragma unroll
+        for (int p = 0; p < P; ++p) af[p][i] = patch[p * PATCH + o];
+      }
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int n = wn * TN + j * 32 + fr;
+        const int o = n * 4 + (ch ^ ((n >> 2) & 3));
+#pragma unroll
+        for (int p = 0; p < P; ++p) bfr[p][j] = L[p * BPL + o];
+      }
+      mma_half<MI, NJ, P, true, RB, decltype(KK)::value>(af, bfr, acc, [&](int q) __attribute__((always_inline)) {
+        lput_q(buf ^ 1, stn, q);
+        gq(t + 3, stn, q);   // reload: step t+3 (past NK: zero-filled, never read)
+      });
+    });
+  };
+  // after step t's barrier: at a chunk boundary the next chunk's patch replaces the old one
+  // (every read of it is done) and the chunk after it starts loading
+  auto boundary = [&](int t) __attribute__((always_inline)) {
+    if (t % 9 == 8 && t + 1 < NK) {
+      patch_put();
+      const int nc = (t + 1) / 9 + 1;
+      if (nc < NC) pload(nc);
+      __syncthreads();
+    }
+  };
+
+  hs.init(amax_read(a.amax_src, a.amax_src_ld, g), amax_read(a.amax_w, a.amax_w_ld, slot));
+#pragma unroll
+  for (int q = 0; q < RB; ++q) {
+    gq(0, 0, q);
+    gq(1, 1, q);
+  }
+  pload(0);
+  patch_put();
+  if (NC > 1) pload(1);
+#pragma unroll
+  for (int q = 0; q < RB; ++q) {
+    lput_q(0, 0, q);
+    gq(2, 0, q);
+  }
+  __syncthreads();   // patch (chunk 0) + first weight step
+  int t = 0;
+  for (; t + 1 < NK; t += 2) {
+    mma(t, 0, 1);
+    __syncthreads();
+    boundary(t);
+    mma(t + 1, 1, 0);
+    __syncthreads();
+    boundary(t + 1);
+  }
+  if (t < NK) mma(t, 0, 1);
+  hs.finish(acc);
+
+  // ---- epilogue from the accumulators: bias, residual, ReLU, max
+  float* out = a.out + (long long)g * a.out_gstride;
+  const float* bias = a.bias ? a.bias + (long long)slot * a.b_sstride : nullptr;
+  const float* res = a.res ? a.res + (long long)g * a.out_gstride : nullptr;
+  float vmax = 0.f;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int n = n0 + wn * TN + j * 32 + fr;
+    if (n >= a.Ncol) continue;
+    const float bv = bias ? bias[n] : 0.f;
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = wm * TM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * hf;
+        if (img0 + m / (W * W) >= nv) continue;
+        const long long o = (long long)(img0 * W * W + m) * a.Ncol + n;
+        float v = acc[i][j][r];
+        if (bias) v += bv;
+        if (res) v += res[o];
+        if (a.relu) v = fmaxf(v, 0.f);
+        vmax = fmaxf(vmax, fabsf(v));
+        out[o] = v;
+      }
+  }
+  if (a.amax_out) amax_fold(a.amax_out, a.amax_out_ld, g, vmax);
+}
+
 // ============================================================ persistent halo conv
 // Weight-stationary, persistent form of xhalo_kernel for the stage-1 shape (W 32, Cs 32,
 // Ncol 32, fp16 pair): the same per-element MFMA sequence (tap-major k-steps, plane products in
@@ -1724,6 +1941,36 @@ int xhalo_ws_try(const XArgs& a, int G, hipStream_t st) {
   DBA_LAUNCH_CHECK();
 }
 
+// the whole-image halo conv (ximg_kernel): evaluation forward, 3x3 stride-1 pad-1, square
+// W 8 / 4, Cs % 32 == 0, fp16 pair (weights pre-split or not), no fused BN / lazy / pair operands
+// (DBA_F32_XIMG=0: off — the implicit GEMM runs)
+template <int W, int IMGS, int BN, int WM, int WN>
+int ximg_go(const XArgs& a, int G, hipStream_t st) {
+  XArgs b = a;
+  b.tiles_n = ceil_div(a.Ncol, BN);
+  const dim3 grid((unsigned)(ceil_div(a.N, IMGS) * b.tiles_n), G, 1);
+  if (a.wp) hipLaunchKernelGGL((ximg_kernel<W, IMGS, BN, WM, WN, true>), grid, dim3(256), 0, st, b);
+  else hipLaunchKernelGGL((ximg_kernel<W, IMGS, BN, WM, WN, false>), grid, dim3(256), 0, st, b);
+  DBA_LAUNCH_CHECK();
+}
+int& ximg_on() {
+  static int on = env_int("DBA_F32_XIMG", 1);
+  return on;
+}
+int ximg_try(const XArgs& a, int G, int KH, int KW, hipStream_t st) {
+  const XClass& c = a.cls[0];
+  if (!ximg_on() || KH != 3 || KW != 3 || a.sp != 1 || a.os != 1 || a.dsg != 1 || a.splitk != 1 || c.nI != 3 ||
+      c.nJ != 3 || c.bh != -1 || c.bw != -1)
+    return -100;
+  if (a.Hs != a.Ho || a.Ws != a.Wo || a.Ho != a.Wo || a.Cs % 32 != 0 || a.Ncol % 32 != 0) return -100;
+  if (!a.amax_src || a.in_sexp || a.out_sexp || a.res_sexp || a.bf.mode || a.lz_coef) return -100;
+  if (!aligned16(a.src) || a.src_gstride % 4 || !aligned16(a.w) || a.w_sstride % 4) return -100;
+  if (a.wp && (((uintptr_t)a.wp & 15) || a.wp_sstride % 8)) return -100;
+  if (a.Wo == 8) return a.Ncol >= 128 ? ximg_go<8, 2, 128, 2, 2>(a, G, st) : ximg_go<8, 2, 64, 2, 2>(a, G, st);
+  if (a.Wo == 4) return a.Ncol >= 128 ? ximg_go<4, 8, 128, 2, 2>(a, G, st) : ximg_go<4, 8, 64, 2, 2>(a, G, st);
+  return -100;
+}
+
 bool flip_dgrad(const XArgs& a) { return a.dsg < 0; }
 
 // the halo kernel's shapes: 3x3 stride-1 pad-1 (fwd) or its stride-1 data gradient, one class,
@@ -1894,6 +2141,13 @@ DBA_EXPORT int dba_xhalo_ws_set(int on) {
   return prev;
 }
 
+// whole-image halo conv (ximg_kernel) on / off (tests: A/B against the implicit GEMM); returns the previous
+DBA_EXPORT int dba_ximg_set(int on) {
+  const int prev = ximg_on();
+  if (on >= 0) ximg_on() = on;
+  return prev;
+}
+
 DBA_EXPORT int dba_xgemm_set_planes(int p) {
   const int prev = planes();
   if (p == 2 || p == 3 || p == kF16) planes() = p;
@@ -1955,7 +2209,8 @@ DBA_EXPORT int dba_xconv_fwd(const float* x, long long x_gstride, const float* w
   // a fused BN's finalize launch follows its producer (bnx_tile_go launches its own)
   auto fin = [&](int rc) { return (rc == 0 && a.bf.mode) ? bnx_finalize_go(a.bf, nvalid, G, N, Ho * Wo, st) : rc; };
   if (stride == 1) {
-    const int rc = xhalo_try(a, G, KH, KW, st);
+    int rc = ximg_try(a, G, KH, KW, st);
+    if (rc == -100) rc = xhalo_try(a, G, KH, KW, st);
     if (rc != -100) return fin(rc);
   }
   const int s = pairs ? 1 : xsplitk(M, G, Cout, K);

@@ -56,6 +56,7 @@ _SIGS = {
     # reference-precision (fp32) family: csrc/kernels/xgemm.hip
     "dba_xgemm_set_planes": [_I],
     "dba_xhalo_ws_set": [_I],
+    "dba_ximg_set": [_I],
     "dba_xconv_ws_floats": [_I] * 8,
     "dba_xconv_fwd": [_P, _LL, _P, _LL, _P, _P, _LL, _P, _P, _LL, _P] + [_I] * 13 + [_P, _I] * 3 + [_P, _LL] * 2
     + [_P, _P, _P, _P, _I, _P, _P, _LL, _P, _P, _I, _P],
@@ -267,6 +268,12 @@ def set_halo_ws(on: int) -> int:
     """Persistent weight-stationary stage-1 halo conv (xgemm.hip xhalo_ws_kernel) on / off;
     -1 queries.  Returns the previous setting."""
     return int(_L.dba_xhalo_ws_set(int(on)))
+
+
+def set_ximg(on: int) -> int:
+    """Whole-image halo conv of the 8 / 4-wide evaluation stages (xgemm.hip ximg_kernel) on /
+    off; -1 queries.  Returns the previous setting."""
+    return int(_L.dba_ximg_set(int(on)))
 
 
 def fp32_mode() -> int:
