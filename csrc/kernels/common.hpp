@@ -100,7 +100,7 @@ constexpr int kAmaxSub = 16;
 
 // every thread of the block must call it (block-level reduction, then one atomic per block)
 __device__ __forceinline__ void amax_fold(int* amax, int ld, int g, float m) {
-  __shared__ float amax_red[4];
+  __shared__ float amax_red[16];   // up to 1024 threads
   m = wave_max(m);
   if ((threadIdx.x & 63) == 0) amax_red[threadIdx.x >> 6] = m;
   __syncthreads();

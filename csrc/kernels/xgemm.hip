@@ -789,32 +789,40 @@ __global__ __launch_bounds__(256) void xhalo_kernel(const XArgs a) {
 }
 
 // ================================================================ whole-image halo conv
-// Stride-1 3x3 pad-1 evaluation forward of the small-image stages (W 8 / 4: ResNet stages 3
-// and 4 on 32x32 inputs; fp16 pair, weights pre-split at the eval fold).  The implicit GEMM re-fetches every
-// input element once per tap, and at these shapes its operand fetch — not the MFMA — bounds
-// it (eval.layer3 / 4 ran +37 / +43 % faster with the in-loop global loads removed, against
-// +5 % without the in-loop barriers: profiles/r4/ximg).  Here a block owns IMGS whole images
-// (128 output pixels) x BN output channels; the reduction runs channel-chunk-major (chunk of
-// 32 channels, then its 9 taps): each chunk's zero-padded patch (IMGS x (W+2)^2 pixels x 32
-// channels) is loaded once, split once into the LDS patch, and read by all 9 taps at their
-// pixel offsets — (W+2)^2 / W^2 = 1.56x / 2.25x of the image bytes instead of 9x.  The next
-// chunk's patch is loaded into registers while the current chunk's 9 k-steps run (8 steps to
-// land), so the only exposed cost is its split + LDS store at the chunk boundary.  Weights:
-// the two-stage register / LDS ring of xhalo_kernel.  Epilogue straight from the
+// Stride-1 3x3 pad-1 evaluation forward of the small-image stages (W 16 / 8 / 4: ResNet stages
+// 2-4 on 32x32 inputs; fp16 pair, weights pre-split at the eval fold).  The implicit GEMM
+// re-fetches every input element once per tap, and at these shapes its operand fetch — not
+// the MFMA — bounds it (eval.layer3 / 4 ran +37 / +43 % faster with the in-loop global loads
+// removed, against +5 % without the in-loop barriers: profiles/r4/ximg).  Here a block owns
+// IMGS whole images (BM = 128 or 256 output pixels) x BN output channels; the reduction runs
+// channel-chunk-major (chunk of 32 channels, then its 9 taps): each chunk's zero-padded patch
+// (IMGS x (W+2)^2 pixels x 32 channels) is loaded once, split once into the LDS patch, and
+// read by all 9 taps at their pixel offsets — (W+2)^2 / W^2 = 1.27x / 1.56x / 2.25x of the
+// image bytes instead of 9x.  The next chunk's patch is loaded into registers while the
+// current chunk's 9 k-steps run (8 steps to land).
+//   NT = 256 (4 waves, 2 blocks per CU): one patch buffer, the next chunk is split + stored
+//     after the chunk's last barrier (one more barrier per chunk);
+//   NT = 512 (8 waves, BM 256, one block per CU; DBA_F32_XIMG_V=2, measured slower): two
+//     patch buffers, the next chunk's split + stores ride in the MFMA gaps of the chunk's last
+//     k-step (no extra barrier), and each weight k-step feeds twice the pixels.
+// Weights: the two-stage register / LDS ring of xhalo_kernel.  Epilogue straight from the
 // accumulators (a 32-lane row is 32 consecutive output channels: 128-B segments).
 // Deterministic; the chunk-major k order makes its bits differ from the tap-major implicit
 // GEMM's (both fp32 level: tests hold both to the fp64 oracle).
-template <int W, int IMGS, int BN, int WM, int WN, bool PRE>
-__global__ __launch_bounds__(256) void ximg_kernel(const XArgs a) {
+template <int W, int IMGS, int BN, int WM, int WN, bool PRE, int NT>
+__global__ __launch_bounds__(NT) void ximg_kernel(const XArgs a) {
   constexpr int P = 2;
+  constexpr bool DB = NT == 512;                            // double-buffered patch
   constexpr int PW = W + 2, PI = PW * PW, PP = IMGS * PI;   // padded pixels per image / patch
   constexpr int CC = 32, CH = CC / 8, Q4 = CC / 4;          // chunk channels, 16-B chunks, float4 per pixel
   constexpr int PATCH = PP * CH;                            // uint4 per plane
   constexpr int BM = IMGS * W * W;
   constexpr int TM = BM / WM, TN = BN / WN, MI = TM / 32, NJ = TN / 32;
-  static_assert(WM * WN == 4 && MI >= 1 && NJ >= 1 && BM == 128, "tiling");
-  constexpr int RB = BN / 32, BPL = BN * 4;
-  __shared__ __attribute__((aligned(16))) uint4 patch[P * PATCH];
+  static_assert(WM * WN == NT / 64 && MI >= 1 && NJ >= 1 && (BM == 128 || BM == 256), "tiling");
+  constexpr int RPT = NT / 8;                               // weight rows staged per pass
+  static_assert(BN % RPT == 0, "weight rows");
+  constexpr int RB = BN / RPT, BPL = BN * 4;
+  __shared__ __attribute__((aligned(16))) uint4 patch[(DB ? 2 : 1) * P * PATCH];
   __shared__ __attribute__((aligned(16))) uint4 bring[2 * P * BPL];
 
   const int g = blockIdx.y;
@@ -831,13 +839,13 @@ __global__ __launch_bounds__(256) void ximg_kernel(const XArgs a) {
   const int fr = lane & 31, hf = lane >> 5;
 
   // ---- patch chunks: chunk cc of images img0 .. img0+IMGS-1, zero padding / invalid images
-  constexpr int NE = (PP * Q4 + 255) / 256;
+  constexpr int NE = (PP * Q4 + NT - 1) / NT;
   float4 pv[NE];
   const __amdgpu_buffer_rsrc_t rA = rsrc(src, (long long)a.N * W * W * Cs * 4);
   auto pload = [&](int cc) __attribute__((always_inline)) {
 #pragma unroll
     for (int u = 0; u < NE; ++u) {
-      const int e = tid + 256 * u;
+      const int e = tid + NT * u;
       const int pp = e / Q4, q = e - pp * Q4;
       const int im = pp / PI, rem = pp - im * PI;
       const int h = rem / PW - 1, w = rem % PW - 1, img = img0 + im;
@@ -846,18 +854,15 @@ __global__ __launch_bounds__(256) void ximg_kernel(const XArgs a) {
     }
   };
   HScale hs;
-  auto patch_put = [&]() __attribute__((always_inline)) {
+  auto ppiece = [&](int u, int pb) __attribute__((always_inline)) {   // piece u of pv -> patch buffer pb
+    const int e = tid + NT * u;
+    if (e >= PP * Q4) return;
+    const int pp = e / Q4, q = e - pp * Q4;
+    uint2 sp[P];
+    split4h(pv[u].x, pv[u].y, pv[u].z, pv[u].w, hs.ma, sp);
+    const int o = pb * P * PATCH + pp * CH + ((q >> 1) ^ hswz<W, CC>(pp, 0));
 #pragma unroll
-    for (int u = 0; u < NE; ++u) {
-      const int e = tid + 256 * u;
-      if (e >= PP * Q4) break;
-      const int pp = e / Q4, q = e - pp * Q4;
-      uint2 sp[P];
-      split4h(pv[u].x, pv[u].y, pv[u].z, pv[u].w, hs.ma, sp);
-      const int o = pp * CH + ((q >> 1) ^ hswz<W, CC>(pp, 0));
-#pragma unroll
-      for (int p = 0; p < P; ++p) ((uint2*)&patch[p * PATCH + o])[q & 1] = sp[p];
-    }
+    for (int p = 0; p < P; ++p) ((uint2*)&patch[p * PATCH + o])[q & 1] = sp[p];
   };
 
   // ---- weights (pre-split planes, or fp32 split while staging: the same bits): two-stage
@@ -865,7 +870,7 @@ __global__ __launch_bounds__(256) void ximg_kernel(const XArgs a) {
   int boffs[RB];
 #pragma unroll
   for (int j = 0; j < RB; ++j) {
-    const int n = n0 + r0 + 32 * j;
+    const int n = n0 + r0 + RPT * j;
     boffs[j] = n < a.Ncol ? n * K : -1;
   }
   const uint16_t* Bh = PRE ? a.wp + (long long)slot * a.wp_sstride : nullptr;
@@ -885,7 +890,6 @@ __global__ __launch_bounds__(256) void ximg_kernel(const XArgs a) {
     }
   };
   auto lput_q = [&](int buf, int st, int q) __attribute__((always_inline)) {
-    if (q >= RB) return;
     uint2 sp[P];
     if constexpr (PRE) {
       sp[0] = make_uint2(rb[st][q].x, rb[st][q].y);
@@ -894,7 +898,7 @@ __global__ __launch_bounds__(256) void ximg_kernel(const XArgs a) {
       const float4 v = __builtin_bit_cast(float4, rb[st][q]);
       split4h(v.x, v.y, v.z, v.w, hs.mb, sp);
     }
-    lds_put<P, false, BN>(bring + buf * P * BPL, BPL, 0, r0 + 32 * q, kq, sp);
+    lds_put<P, false, BN>(bring + buf * P * BPL, BPL, 0, r0 + RPT * q, kq, sp);
   };
 
   f32x16_t acc[MI][NJ];
@@ -912,10 +916,15 @@ __global__ __launch_bounds__(256) void ximg_kernel(const XArgs a) {
     const int im = m / (W * W), rem = m - im * (W * W);
     apix[i] = im * PI + (rem / W) * PW + rem % W;
   }
-  auto mma = [&](int t, int buf, int stn) __attribute__((always_inline)) {
+  // k-step t from patch buffer pb and weight buffer buf; fills: the weight ring's next step
+  // and (PT) the next chunk's patch into buffer pb ^ 1
+  auto mma = [&](auto PTc, int t, int buf, int stn, int pb) __attribute__((always_inline)) {
+    constexpr bool PT = decltype(PTc)::value;
+    constexpr int NQ = RB + (PT ? NE : 0);
     const int tap = t % 9, ti = tap / 3, tj = tap - ti * 3;
     const int toff = ti * PW + tj;
     const uint4* L = bring + buf * P * BPL;
+    const uint4* A = patch + pb * P * PATCH;
     sfor<2>([&](auto KK) __attribute__((always_inline)) {
       const int ch = decltype(KK)::value * 2 + hf;
       uint4 af[P][MI], bfr[P][NJ];
@@ -924,7 +933,7 @@ __global__ __launch_bounds__(256) void ximg_kernel(const XArgs a) {
         const int pp = apix[i] + toff;
         const int o = pp * CH + (ch ^ hswz<W, CC>(pp, 0));
 #pragma unroll
-        for (int p = 0; p < P; ++p) af[p][i] = patch[p * PATCH + o];
+        for (int p = 0; p < P; ++p) af[p][i] = A[p * PATCH + o];
       }
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
@@ -933,20 +942,30 @@ __global__ __launch_bounds__(256) void ximg_kernel(const XArgs a) {
 #pragma unroll
         for (int p = 0; p < P; ++p) bfr[p][j] = L[p * BPL + o];
       }
-      mma_half<MI, NJ, P, true, RB, decltype(KK)::value>(af, bfr, acc, [&](int q) __attribute__((always_inline)) {
-        lput_q(buf ^ 1, stn, q);
-        gq(t + 3, stn, q);   // reload: step t+3 (past NK: zero-filled, never read)
+      mma_half<MI, NJ, P, true, NQ, decltype(KK)::value>(af, bfr, acc, [&](int q) __attribute__((always_inline)) {
+        if (q < RB) {
+          lput_q(buf ^ 1, stn, q);
+          gq(t + 3, stn, q);   // reload: step t+3 (past NK: zero-filled, never read)
+        } else {
+          ppiece(q - RB, pb ^ 1);
+        }
       });
     });
   };
-  // after step t's barrier: at a chunk boundary the next chunk's patch replaces the old one
-  // (every read of it is done) and the chunk after it starts loading
-  auto boundary = [&](int t) __attribute__((always_inline)) {
-    if (t % 9 == 8 && t + 1 < NK) {
-      patch_put();
-      const int nc = (t + 1) / 9 + 1;
-      if (nc < NC) pload(nc);
-      __syncthreads();
+  auto step = [&](int t, int buf, int stn) __attribute__((always_inline)) {
+    const int c = t / 9;
+    const bool last = t - 9 * c == 8 && c + 1 < NC;   // the chunk's last k-step, another follows
+    const int pb = DB ? (c & 1) : 0;
+    if (DB && last) mma(std::true_type{}, t, buf, stn, pb);
+    else mma(std::false_type{}, t, buf, stn, pb);
+    __syncthreads();
+    if (last) {
+      if constexpr (!DB) {   // every read of the old patch is done: the next chunk replaces it
+#pragma unroll
+        for (int u = 0; u < NE; ++u) ppiece(u, 0);
+      }
+      if (c + 2 < NC) pload(c + 2);
+      if constexpr (!DB) __syncthreads();
     }
   };
 
@@ -957,7 +976,8 @@ __global__ __launch_bounds__(256) void ximg_kernel(const XArgs a) {
     gq(1, 1, q);
   }
   pload(0);
-  patch_put();
+#pragma unroll
+  for (int u = 0; u < NE; ++u) ppiece(u, 0);
   if (NC > 1) pload(1);
 #pragma unroll
   for (int q = 0; q < RB; ++q) {
@@ -967,14 +987,10 @@ __global__ __launch_bounds__(256) void ximg_kernel(const XArgs a) {
   __syncthreads();   // patch (chunk 0) + first weight step
   int t = 0;
   for (; t + 1 < NK; t += 2) {
-    mma(t, 0, 1);
-    __syncthreads();
-    boundary(t);
-    mma(t + 1, 1, 0);
-    __syncthreads();
-    boundary(t + 1);
+    step(t, 0, 1);
+    step(t + 1, 1, 0);
   }
-  if (t < NK) mma(t, 0, 1);
+  if (t < NK) step(t, 0, 1);
   hs.finish(acc);
 
   // ---- epilogue from the accumulators: bias, residual, ReLU, max
@@ -1942,15 +1958,15 @@ int xhalo_ws_try(const XArgs& a, int G, hipStream_t st) {
 }
 
 // the whole-image halo conv (ximg_kernel): evaluation forward, 3x3 stride-1 pad-1, square
-// W 8 / 4, Cs % 32 == 0, fp16 pair (weights pre-split or not), no fused BN / lazy / pair operands
+// W 16 / 8 / 4, Cs % 32 == 0, fp16 pair (weights pre-split or not), no fused BN / lazy / pair operands
 // (DBA_F32_XIMG=0: off — the implicit GEMM runs)
-template <int W, int IMGS, int BN, int WM, int WN>
+template <int W, int IMGS, int BN, int WM, int WN, int NT>
 int ximg_go(const XArgs& a, int G, hipStream_t st) {
   XArgs b = a;
   b.tiles_n = ceil_div(a.Ncol, BN);
   const dim3 grid((unsigned)(ceil_div(a.N, IMGS) * b.tiles_n), G, 1);
-  if (a.wp) hipLaunchKernelGGL((ximg_kernel<W, IMGS, BN, WM, WN, true>), grid, dim3(256), 0, st, b);
-  else hipLaunchKernelGGL((ximg_kernel<W, IMGS, BN, WM, WN, false>), grid, dim3(256), 0, st, b);
+  if (a.wp) hipLaunchKernelGGL((ximg_kernel<W, IMGS, BN, WM, WN, true, NT>), grid, dim3(NT), 0, st, b);
+  else hipLaunchKernelGGL((ximg_kernel<W, IMGS, BN, WM, WN, false, NT>), grid, dim3(NT), 0, st, b);
   DBA_LAUNCH_CHECK();
 }
 int& ximg_on() {
@@ -1966,8 +1982,19 @@ int ximg_try(const XArgs& a, int G, int KH, int KW, hipStream_t st) {
   if (!a.amax_src || a.in_sexp || a.out_sexp || a.res_sexp || a.bf.mode || a.lz_coef) return -100;
   if (!aligned16(a.src) || a.src_gstride % 4 || !aligned16(a.w) || a.w_sstride % 4) return -100;
   if (a.wp && (((uintptr_t)a.wp & 15) || a.wp_sstride % 8)) return -100;
-  if (a.Wo == 8) return a.Ncol >= 128 ? ximg_go<8, 2, 128, 2, 2>(a, G, st) : ximg_go<8, 2, 64, 2, 2>(a, G, st);
-  if (a.Wo == 4) return a.Ncol >= 128 ? ximg_go<4, 8, 128, 2, 2>(a, G, st) : ximg_go<4, 8, 64, 2, 2>(a, G, st);
+  // 4 waves, BM 128, one patch buffer, 2 blocks per CU (one block's prologue / epilogue runs
+  // under the other's MFMAs).  DBA_F32_XIMG_V=2: 8 waves, BM 256 x BN 64, double-buffered
+  // patches (W 16: 83 + 16 KB, W 8: 102 + 16 KB of LDS; BN 128 spills at the 256 registers of
+  // 2 waves per SIMD), one block per CU — measured slower (eval.layer2 221 vs 282 TF, layer3
+  // 254 vs 314, headline 3.11 vs 3.45 rounds/s same box: profiles/r4/ximg/README.md): the
+  // lone block's prologue and epilogue are exposed
+  static const int v = env_int("DBA_F32_XIMG_V", 1);
+  if (a.Wo == 16 && a.Ncol <= 64 && v >= 2) return ximg_go<16, 1, 64, 4, 2, 512>(a, G, st);
+  if (a.Wo == 8) {
+    if (v >= 2) return ximg_go<8, 4, 64, 4, 2, 512>(a, G, st);
+    return a.Ncol >= 128 ? ximg_go<8, 2, 128, 2, 2, 256>(a, G, st) : ximg_go<8, 2, 64, 2, 2, 256>(a, G, st);
+  }
+  if (a.Wo == 4) return a.Ncol >= 128 ? ximg_go<4, 8, 128, 2, 2, 256>(a, G, st) : ximg_go<4, 8, 64, 2, 2, 256>(a, G, st);
   return -100;
 }
 

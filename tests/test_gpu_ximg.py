@@ -1,7 +1,7 @@
-"""The whole-image halo conv of the 8 / 4-wide evaluation stages (``xgemm.hip ximg_kernel``)
+"""The whole-image halo conv of the 16 / 8 / 4-wide evaluation stages (``xgemm.hip ximg_kernel``)
 vs an fp64 oracle and vs the implicit GEMM it replaces (GPU only).
 
-3x3 stride-1 pad-1 forwards with BN-folded, pre-split weights (the stage-3 / 4 convs of the
+3x3 stride-1 pad-1 forwards with BN-folded, pre-split weights (the stage-2 / 3 / 4 convs of the
 reference ``models/resnet_cifar.py`` in evaluation): bias, residual and ReLU in the epilogue,
 partly valid replicas, image counts that leave a partial tile, a slot map.  The kernel runs
 the reduction chunk-major (32 channels x 9 taps per chunk) where the implicit GEMM runs it
@@ -42,7 +42,8 @@ def _rel(a, b):
 
 @pytest.mark.parametrize("G,N,nv,W,Cin,Cout,res", [
     (3, 5, (5, 2, 4), 8, 128, 128, True), (2, 9, (9, 6), 4, 256, 256, True),
-    (2, 7, (7, 3), 8, 64, 64, False), (1, 11, (11,), 4, 128, 64, False)])
+    (2, 7, (7, 3), 8, 64, 64, False), (1, 11, (11,), 4, 128, 64, False),
+    (2, 5, (5, 3), 16, 64, 64, True), (1, 3, (3,), 16, 32, 32, False)])
 def test_ximg_vs_fp64_and_implicit_gemm(H, R64, G, N, nv, W, Cin, Cout, res):
     dev = torch.device("cuda")
     g = torch.Generator().manual_seed(G * 1000 + N * 10 + W)
