@@ -175,12 +175,15 @@ __device__ __forceinline__ int pair_out_exp(const XArgs& a, int g, int slot) {
   return hexp(__float_as_int(2.f * b));
 }
 
-// register budget: XCONV_MINB=2 fits two workgroups per CU (<= 256 registers per lane, no
-// spills) but measured no faster than one (eval / training conv TFLOP/s within 1 %, bench 3.04
-// vs 3.09 rounds/s, same box: profiles/r4/minb/) — the 128x128 eval tiles are bound by the
-// MFMA work at the DVFS-held clock, not by latency; one workgroup per CU stays the default
+// register budget (minimum workgroups per CU): 3 lets the 128x64 / 64x128 / 32x128 tiles keep
+// their accumulators in VGPRs within 168 registers (3 waves per SIMD, no spills; the 128x128
+// tiles stay at 2, LDS-bound).  Those tiles run the short-K stride-2 and 1x1 convs, whose
+// prologue / epilogue a third resident workgroup hides: eval.l2.0.conv1 163 vs 156 TF,
+// l2.0.sc 43 vs 33, training l2.0.conv1 fwd 134 vs 120, l3/l4 dgrad +7 %, headline 3.25 vs
+// 3.16 rounds/s same box (profiles/r4/minb3/).  (1 -> 2 changed nothing: profiles/r4/minb/.)
+// The 128x128 eval tiles are operand-fetch bound (profiles/r4/ximg/README.md), not MFMA bound.
 #ifndef XCONV_MINB
-#define XCONV_MINB 1
+#define XCONV_MINB 3
 #endif
 template <int BM, int BN, int WM, int WN, int P, int VEC, bool H, bool PW = false, bool PA = false, bool LZ = false>
 __global__ __launch_bounds__(256, XCONV_MINB) void xconv_kernel(const XArgs a) {

@@ -22,6 +22,11 @@ SHAPES = [
     ("eval.layer3", 17, 1024, 8, 128, 128, 3, 1, 1),
     ("eval.layer4", 17, 1024, 4, 256, 256, 3, 1, 1),
     ("eval.l2.0.conv1", 17, 1024, 32, 32, 64, 3, 2, 1),
+    ("eval.l3.0.conv1", 17, 1024, 16, 64, 128, 3, 2, 1),
+    ("eval.l4.0.conv1", 17, 1024, 8, 128, 256, 3, 2, 1),
+    ("eval.l2.0.sc", 17, 1024, 32, 32, 64, 1, 2, 0),
+    ("eval.l3.0.sc", 17, 1024, 16, 64, 128, 1, 2, 0),
+    ("eval.l4.0.sc", 17, 1024, 8, 128, 256, 1, 2, 0),
     ("eval.stem", 17, 1024, 32, 3, 32, 3, 1, 1),
     ("train.layer1", 10, 64, 32, 32, 32, 3, 1, 1),
     ("train.layer2", 10, 64, 16, 64, 64, 3, 1, 1),
