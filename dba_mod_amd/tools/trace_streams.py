@@ -44,18 +44,31 @@ def summarize(path: str, last_ms: float = 750.0, top: int = 12) -> str:
         out.append(f"\n## stream {st}: {tot:.1f} ms of kernels\n\n| kernel | ms | % | launches |\n|---|---|---|---|")
         for k, (ms, n) in sorted(per[st].items(), key=lambda kv: -kv[1][0])[:top]:
             out.append(f"| `{k}` | {ms:.1f} | {100 * ms / max(tot, 1e-9):.1f} | {n} |")
-    iv = sorted((s, e) for s, e, _, _ in win)
-    busy, cur_s, cur_e = 0, iv[0][0], iv[0][1]
-    for s, e in iv[1:]:
+    iv = sorted((s, e, k) for s, e, _, k in win)
+    busy, cur_s, cur_e, last_k = 0, iv[0][0], iv[0][1], iv[0][2]
+    gaps: List[Tuple[int, str, str]] = []   # (idle ns, kernel ending before, kernel starting after)
+    for s, e, k in iv[1:]:
         if s > cur_e:
             busy += cur_e - cur_s
+            gaps.append((s - cur_e, last_k, k))
             cur_s, cur_e = s, e
         else:
             cur_e = max(cur_e, e)
+        if e >= cur_e:
+            last_k = k
     busy += cur_e - cur_s
-    span = (t_end - min(s for s, _ in iv)) / 1e6
+    span = (t_end - min(s for s, _, _ in iv)) / 1e6
     out.append(f"\nUnion of kernel intervals: {busy / 1e6:.0f} ms of {span:.0f} ms "
                f"({100 * busy / 1e6 / max(span, 1e-9):.0f} % of the window has a kernel in flight).\n")
+    if gaps:
+        big = sorted(gaps, reverse=True)[:top]
+        idle = sum(g for g, _, _ in gaps) / 1e6
+        n1 = sum(1 for g, _, _ in gaps if g >= 1e6)
+        out.append(f"Idle: {idle:.1f} ms in {len(gaps)} gaps ({n1} of >= 1 ms, "
+                   f"{sum(g for g, _, _ in gaps if g >= 1e6) / 1e6:.1f} ms).  Largest:\n\n"
+                   "| idle ms | last kernel before | first kernel after |\n|---|---|---|")
+        for g, a, b in big:
+            out.append(f"| {g / 1e6:.2f} | `{a}` | `{b}` |")
     return "\n".join(out) + "\n"
 
 
