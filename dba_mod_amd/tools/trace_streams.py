@@ -46,11 +46,11 @@ def summarize(path: str, last_ms: float = 750.0, top: int = 12) -> str:
             out.append(f"| `{k}` | {ms:.1f} | {100 * ms / max(tot, 1e-9):.1f} | {n} |")
     iv = sorted((s, e, k) for s, e, _, k in win)
     busy, cur_s, cur_e, last_k = 0, iv[0][0], iv[0][1], iv[0][2]
-    gaps: List[Tuple[int, str, str]] = []   # (idle ns, kernel ending before, kernel starting after)
+    gaps: List[Tuple[int, str, str, int]] = []   # (idle ns, kernel before, kernel after, start ns)
     for s, e, k in iv[1:]:
         if s > cur_e:
             busy += cur_e - cur_s
-            gaps.append((s - cur_e, last_k, k))
+            gaps.append((s - cur_e, last_k, k, cur_e))
             cur_s, cur_e = s, e
         else:
             cur_e = max(cur_e, e)
@@ -62,13 +62,14 @@ def summarize(path: str, last_ms: float = 750.0, top: int = 12) -> str:
                f"({100 * busy / 1e6 / max(span, 1e-9):.0f} % of the window has a kernel in flight).\n")
     if gaps:
         big = sorted(gaps, reverse=True)[:top]
-        idle = sum(g for g, _, _ in gaps) / 1e6
-        n1 = sum(1 for g, _, _ in gaps if g >= 1e6)
+        idle = sum(g[0] for g in gaps) / 1e6
+        n1 = sum(1 for g in gaps if g[0] >= 1e6)
         out.append(f"Idle: {idle:.1f} ms in {len(gaps)} gaps ({n1} of >= 1 ms, "
-                   f"{sum(g for g, _, _ in gaps if g >= 1e6) / 1e6:.1f} ms).  Largest:\n\n"
-                   "| idle ms | last kernel before | first kernel after |\n|---|---|---|")
-        for g, a, b in big:
-            out.append(f"| {g / 1e6:.2f} | `{a}` | `{b}` |")
+                   f"{sum(g[0] for g in gaps if g[0] >= 1e6) / 1e6:.1f} ms).  Largest:\n\n"
+                   "| idle ms | starts, ms before the trace end | last kernel before | first kernel after |\n"
+                   "|---|---|---|---|")
+        for g, a, b, t in big:
+            out.append(f"| {g / 1e6:.2f} | {(t_end - t) / 1e6:.1f} | `{a}` | `{b}` |")
     return "\n".join(out) + "\n"
 
 

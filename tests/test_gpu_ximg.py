@@ -89,3 +89,25 @@ def test_ximg_is_deterministic(H):
         with H.amax_arena(2, dev):
             outs.append(H.conv2d(x, w, None, 1, 1, relu=True))
     assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
+
+
+@pytest.mark.parametrize("W,C", [(8, 128), (4, 256)])
+def test_ximg_group_size_independent_bits(H, W, C):
+    """A replica's output bits do not depend on how many replicas share the launch (world-1 vs
+    world-N runs group models differently)."""
+    dev = torch.device("cuda")
+    g = torch.Generator().manual_seed(W + C)
+    G = 3
+    x = torch.relu(torch.randn(G, 5, W, W, C, generator=g)).to(dev)
+    w = (torch.randn(G, C, 3, 3, C, generator=g) / (3 * C ** 0.5)).to(dev)
+    per = C * 9 * C
+    H.split_weights(w, per, per, H._amax_w(w, per, per))
+    b = (torch.randn(G, C, generator=g) * 0.1).to(dev)
+    with H.amax_arena(G, dev):
+        yall = H.conv2d(x, w, None, 1, 1, bias=b, relu=True)
+    for i in range(G):
+        wi = w[i:i + 1].clone()
+        H.split_weights(wi, per, per, H._amax_w(wi, per, per))
+        with H.amax_arena(1, dev):
+            yi = H.conv2d(x[i:i + 1].contiguous(), wi, None, 1, 1, bias=b[i:i + 1].contiguous(), relu=True)
+        assert torch.equal(yi[0], yall[i]), i
