@@ -57,6 +57,7 @@ struct XArgs {
   int N, Hs, Ws, Cs, Ncol, Ho, Wo;
   int sp, os, dsg, relu;
   int splitk, tiles_n;
+  int kslab;                                 // xconv KS: split-K slabs summed in the block (1: none)
   long long zstride;                         // split-K: slab z at out + z * zstride
   const int* amax_src;                       // H: max |src| slot [kAmaxSub][amax_src_ld] (common.hpp)
   const int* amax_w;                         // H: max |w| slot, indexed by weight slot
@@ -185,8 +186,14 @@ __device__ __forceinline__ int pair_out_exp(const XArgs& a, int g, int slot) {
 #ifndef XCONV_MINB
 #define XCONV_MINB 3
 #endif
-template <int BM, int BN, int WM, int WN, int P, int VEC, bool H, bool PW = false, bool PA = false, bool LZ = false>
-__global__ __launch_bounds__(256, XCONV_MINB) void xconv_kernel(const XArgs a) {
+// KS: the K range runs as a.kslab slabs inside the block — each slab's MFMAs accumulate from
+// zero, are scaled back (HScale) and added to a running fp32 sum in slab order — the exact
+// arithmetic of a.kslab split-K launches summed in z order (xsplitk_reduce / sk_combine), so a
+// grouped launch reproduces a lone client's split-K bits without the slab round trip through
+// HBM or the separate reduce / statistics pass
+template <int BM, int BN, int WM, int WN, int P, int VEC, bool H, bool PW = false, bool PA = false, bool LZ = false,
+          bool KS = false>
+__global__ __launch_bounds__(256, KS ? 2 : XCONV_MINB) void xconv_kernel(const XArgs a) {
   static_assert(!H || P == 2, "fp16 split: 2 planes");
   static_assert(!LZ || (H && !PA && VEC >= 4), "lazy BN operand: fp16 pair, fp32 source, 4-channel vectors");
   static_assert(!PW || (H && VEC >= 4), "pre-split weights: fp16 pair, vector loads");
@@ -410,6 +417,27 @@ __global__ __launch_bounds__(256, XCONV_MINB) void xconv_kernel(const XArgs a) {
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
   if constexpr (LZ) __syncthreads();   // lzc
+  // KS: the running sum of the finished slabs, the next slab boundary
+  [[maybe_unused]] f32x16_t ssum[KS ? MI : 1][KS ? NJ : 1];
+  [[maybe_unused]] int zs = 1, kb_next = KS ? (int)((long long)nkt / a.kslab) : 0;
+  auto slab_end = [&](int kt_done) __attribute__((always_inline)) {   // after step kt_done
+    if constexpr (KS) {
+      if (kt_done + 1 == kb_next) {
+        if constexpr (H) hs.finish(acc);
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+          for (int j = 0; j < NJ; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              ssum[i][j][r] = zs == 1 ? acc[i][j][r] : ssum[i][j][r] + acc[i][j][r];
+              acc[i][j][r] = 0.f;
+            }
+        ++zs;
+        kb_next = (int)((long long)nkt * zs / a.kslab);
+      }
+    }
+  };
   if (kt0 < kt1) {
     // loads past the slice's last step are harmless (past K they zero-fill), so the loop body
     // has no branches and the accumulators stay in place across iterations
@@ -430,17 +458,29 @@ __global__ __launch_bounds__(256, XCONV_MINB) void xconv_kernel(const XArgs a) {
         lput_q(1, 1, q);
         gq(1, q);
       });
+      slab_end(kt);
       __syncthreads();
       gprep();   // step kt+4
       mma_step<MI, NJ, P, H, false, BM, BN, RA + RB>(lds + P * PL, PL, wm * TM, wn * TN, acc, lane, [&](int q) __attribute__((always_inline)) {
         lput_q(0, 0, q);
         gq(0, q);
       });
+      slab_end(kt + 1);
       __syncthreads();
     }
-    if (kt < kt1) mma_step<MI, NJ, P, H, false, BM, BN, 0>(lds, PL, wm * TM, wn * TN, acc, lane, [&](int) {});
+    if (kt < kt1) {
+      mma_step<MI, NJ, P, H, false, BM, BN, 0>(lds, PL, wm * TM, wn * TN, acc, lane, [&](int) {});
+      slab_end(kt);
+    }
   }
-  if constexpr (H) hs.finish(acc);
+  if constexpr (KS) {
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) acc[i][j] = ssum[i][j];
+  } else if constexpr (H) {
+    hs.finish(acc);
+  }
 
   // ---- epilogue: fp32 tile through LDS, row-contiguous stores with bias / residual / ReLU
   __syncthreads();
@@ -1902,13 +1942,32 @@ int& planes() {
   return p;
 }
 
-template <int BM, int BN, int WM, int WN, int P, int VEC, bool H, bool PW, bool PA = false, bool LZ = false>
+template <int BM, int BN, int WM, int WN, int P, int VEC, bool H, bool PW, bool PA = false, bool LZ = false,
+          bool KS = false>
 int xconv_go(const XArgs& a, long long Mmax, int G, int nclass, hipStream_t st) {
   XArgs b = a;
   b.tiles_n = ceil_div(a.Ncol, BN);
   const dim3 grid((unsigned)(ceil_div(Mmax, BM) * b.tiles_n), G, nclass * a.splitk);
-  hipLaunchKernelGGL((xconv_kernel<BM, BN, WM, WN, P, VEC, H, PW, PA, LZ>), grid, dim3(256), 0, st, b);
+  hipLaunchKernelGGL((xconv_kernel<BM, BN, WM, WN, P, VEC, H, PW, PA, LZ, KS>), grid, dim3(256), 0, st, b);
   DBA_LAUNCH_CHECK();
+}
+
+// a split forward of a grouped launch as in-block slabs (xconv_kernel KS): fp16 pair, 32-channel
+// vectors, Ncol > 64 (the stage-3 / 4 convs xsplitk splits), 64 x 128 tiles (the running sum
+// doubles the accumulators), at most DBA_F32_KSLAB slabs (0: off — slabs through HBM + the
+// reduce / BN pass).  Serial slabs cost the launch its split-K parallelism: at 8 slabs (stage 4)
+// the 10-client step's split convs took 385 vs 352 us with the reduce passes included.
+int kslab_max() {
+  static const int m = env_int("DBA_F32_KSLAB", 2);
+  return m;
+}
+int xconv_ks(const XArgs& a, long long M, int G, int vec, hipStream_t st) {
+  if (a.kslab > kslab_max() || !a.amax_src || a.Ncol <= 64 || a.Cs % 32 || vec < 4 || a.in_sexp || a.out_sexp || a.res_sexp ||
+      a.splitk != 1 || a.kslab < 2)
+    return -100;
+  if (a.lz_coef) return xconv_go<64, 128, 2, 2, 2, 32, true, false, false, true, true>(a, M, G, 1, st);
+  if (a.wp) return xconv_go<64, 128, 2, 2, 2, 32, true, true, false, false, true>(a, M, G, 1, st);
+  return xconv_go<64, 128, 2, 2, 2, 32, true, false, false, false, true>(a, M, G, 1, st);
 }
 
 template <int P, int VEC, bool H, bool PW = false, bool PA = false, bool LZ = false>
@@ -2245,6 +2304,13 @@ DBA_EXPORT int dba_xconv_fwd(const float* x, long long x_gstride, const float* w
   }
   const int s = pairs ? 1 : xsplitk(M, G, Cout, K);
   const bool ws_ok = s > 1 && ws != nullptr && ws_floats >= (long long)s * G * M * Cout;
+  if (s > 1 && !(ws_ok && sk_ok(sk_cnt, sk_cnt_n, M, Cout, G, 1, s))) {
+    // grouped launch: the slabs summed inside each block (same bits as the split launches)
+    XArgs b = a;
+    b.kslab = s;
+    const int rc = xconv_ks(b, M, G, vec, st);
+    if (rc != -100) return fin(rc);
+  }
   if (ws_ok && sk_ok(sk_cnt, sk_cnt_n, M, Cout, G, 1, s)) {
     // in-launch combine (sk_combine): one launch, BN statistics folded by the reducing block
     XArgs b = a;
