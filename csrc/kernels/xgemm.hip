@@ -901,9 +901,10 @@ __global__ __launch_bounds__(NT) void ximg_kernel(const XArgs a) {
     const int e = tid + NT * u;
     if (e >= PP * Q4) return;
     const int pp = e / Q4, q = e - pp * Q4;
+    const int prow = (pp % PI) / PW;   // patch row: the swizzle key
     uint2 sp[P];
     split4h(pv[u].x, pv[u].y, pv[u].z, pv[u].w, hs.ma, sp);
-    const int o = pb * P * PATCH + pp * CH + ((q >> 1) ^ hswz<W, CC>(pp, 0));
+    const int o = pb * P * PATCH + pp * CH + ((q >> 1) ^ (prow & 3));
 #pragma unroll
     for (int p = 0; p < P; ++p) ((uint2*)&patch[p * PATCH + o])[q & 1] = sp[p];
   };
@@ -952,12 +953,18 @@ __global__ __launch_bounds__(NT) void ximg_kernel(const XArgs a) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  int apix[MI];   // patch pixel of each A fragment row at tap (0, 0)
+  // patch pixel and patch row of each A fragment row at tap (0, 0).  LDS image: pixel pp holds
+  // 4 16-B chunks, chunk c at c ^ (patch row & 3) — the rows of a 32-lane fragment read (W 8: 4
+  // rows of 8 pixels, W 4: 2 images x 4 rows of 4) then hit 16 distinct 16-B bank slots in each
+  // ds_read_b128 lane group at every tap (the 32-wide halo conv's (pp >> 2) & 3 left 2-way
+  // conflicts here: SQ_LDS_BANK_CONFLICT 8.0e7 per launch, profiles/r4/final2/)
+  int apix[MI], arow[MI];
 #pragma unroll
   for (int i = 0; i < MI; ++i) {
     const int m = wm * TM + i * 32 + fr;
     const int im = m / (W * W), rem = m - im * (W * W);
     apix[i] = im * PI + (rem / W) * PW + rem % W;
+    arow[i] = rem / W;
   }
   // k-step t from patch buffer pb and weight buffer buf; fills: the weight ring's next step
   // and (PT) the next chunk's patch into buffer pb ^ 1
@@ -974,7 +981,7 @@ __global__ __launch_bounds__(NT) void ximg_kernel(const XArgs a) {
 #pragma unroll
       for (int i = 0; i < MI; ++i) {
         const int pp = apix[i] + toff;
-        const int o = pp * CH + (ch ^ hswz<W, CC>(pp, 0));
+        const int o = pp * CH + (ch ^ ((arow[i] + ti) & 3));
 #pragma unroll
         for (int p = 0; p < P; ++p) af[p][i] = A[p * PATCH + o];
       }
