@@ -91,16 +91,14 @@ def _spawn_ranks(n: int, argv) -> int:
 
 
 def _split_label(server) -> Optional[dict]:
-    """How the fp32 kernels carry fp32 operands on the bf16/fp16 MFMA (csrc/kernels/xgemm.hip):
-    both modes reach fp32-level error (tests/test_gpu_f32.py)."""
+    """The fp32 family's operand split on the HIP backend: the scaled fp16 pair (3 MFMAs per
+    product, fp32-level error: tests/test_gpu_f32.py) on every conv pass, training and
+    evaluation."""
     import torch
     from dba_mod_amd import ops
     if server.dtype != torch.float32 or ops.backend_name(server.device) != "hip":
         return None
-    names = {2: "bf16x2 (3 MFMA)", 3: "bf16x3 (6 MFMA)", 16: "scaled fp16x2 (3 MFMA)"}
-    lib = ops.hip_module().fp32_mode()
-    tr = server.trainer.split_mode if server.trainer.split_mode is not None else lib
-    return {"train": names.get(tr, str(tr)), "eval": names.get(lib, str(lib))}
+    return {"train": "scaled fp16x2 (3 MFMA)", "eval": "scaled fp16x2 (3 MFMA)"}
 
 
 def _args(argv=None):

@@ -440,12 +440,16 @@ DBA_EXPORT int dba_mlp_train(const int* sched, int D, int t0, int t1, int G, int
   if (t1 <= t0) return 0;
   MlpArgs a{sched, D, t0, t1, G, state, s_stride, mom, fg, P, offs[0], offs[1], offs[2], offs[3], offs[4], offs[5],
             rows, labels, tcols, tvals, K, target, stats, stats_stride, max_slots, nan_flag, momentum, wd, prof};
-  static bool attr = false;
-  if (!attr) {
+  // the dynamic-LDS attribute is per device: set once for every device this process launches on
+  // (a device that refuses the ~118 KB budget declines the launch: the caller keeps the graph path)
+  static unsigned long long attr_set = 0ull;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return -100;
+  if (!(attr_set >> dev & 1ull)) {
     const hipError_t e = hipFuncSetAttribute((const void*)mlp_train_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                              (int)sizeof(MlpLds));
-    if (e != hipSuccess) return (int)e;
-    attr = true;
+    if (e != hipSuccess) return -100;
+    attr_set |= 1ull << dev;
   }
   hipLaunchKernelGGL(mlp_train_kernel, dim3(G), dim3(kT), sizeof(MlpLds), (hipStream_t)stream, a);
   DBA_LAUNCH_CHECK();

@@ -16,14 +16,8 @@
 // (bnfuse.hpp bnf_tile_records' definition).
 #include "common.hpp"
 #include "bnfuse.hpp"
-#include <cstdlib>
 
 namespace {
-
-bool env_off() {   // DBA_F32_STEM=0: stems on the MFMA family (A/B)
-  static const bool off = getenv("DBA_F32_STEM") && atoi(getenv("DBA_F32_STEM")) == 0;
-  return off;
-}
 
 struct StemArgs {
   const float* x; long long x_gstride;      // [G][N][H][W][CIN]
@@ -35,25 +29,8 @@ struct StemArgs {
   const int* nvalid;
   int N, H, W, Ho, Wo, stride, pad, relu;
   int* amax_out; int amax_ld;
-  // fp16-pair output (xgemm.hip PairAct): per-replica exponent from the bound
-  // L1max(w) * max|x| + max|b|; x's max slot, the slot's {L1max, bmax}
-  int* out_sexp; const float* bound; const int* amax_x; int amax_x_ld;
   BnFuse bf;                                // fused training BN statistics (bnfuse.hpp), mode 1
 };
-
-typedef __attribute__((ext_vector_type(2))) float f32x2s;
-typedef __attribute__((ext_vector_type(2))) _Float16 f16x2s;
-__device__ __forceinline__ uint32_t pkh(float a, float b) {
-  return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2s){a, b}, f16x2s));
-}
-__device__ __forceinline__ f32x2s unpk(uint32_t u) { return __builtin_convertvector(__builtin_bit_cast(f16x2s, u), f32x2s); }
-// 4 values * 2^s -> {4 fp16 hi, 4 fp16 lo} (bit-identical to xgemm.hip split4h / PairAct::encode)
-__device__ __forceinline__ uint4 pair_encode(float4 v, float m) {
-  const float a = v.x * m, b = v.y * m, c = v.z * m, d = v.w * m;
-  const uint32_t h0 = pkh(a, b), h1 = pkh(c, d);
-  const f32x2s u0 = unpk(h0), u1 = unpk(h1);
-  return make_uint4(h0, h1, pkh(a - u0.x, b - u0.y), pkh(c - u1.x, d - u1.y));
-}
 
 template <int KH, int KW, int CIN, int COUT, int CPT, int ITER>
 __global__ __launch_bounds__(256) void xstem_kernel(const StemArgs a) {
@@ -82,14 +59,6 @@ __global__ __launch_bounds__(256) void xstem_kernel(const StemArgs a) {
   const int pl = tid / TPP, cg = tid - pl * TPP;
   const int c0 = cg * CPT;
   float vmax = 0.f;
-  float omul = 1.f;
-  if (a.out_sexp) {   // block-uniform; every lane of every wave reads the max slot
-    const float ax = __int_as_float(amax_read(a.amax_x, a.amax_x_ld, g));
-    const float bnd = a.bound[2 * slot] * ax + a.bound[2 * slot + 1];
-    const int so = min(100, 141 - (__float_as_int(2.f * bnd) >> 23));   // xgemm.hip hexp
-    omul = __uint_as_float((uint32_t)(so + 127) << 23);
-    if (tid == 0) a.out_sexp[g] = so;
-  }
   const float* bp = a.bias ? a.bias + (long long)slot * a.b_sstride + c0 : nullptr;
   for (int it = 0; it < ITER; ++it) {   // the weights in LDS serve ITER pixel tiles
     const int m0 = mb + it * PIX;
@@ -138,8 +107,7 @@ __global__ __launch_bounds__(256) void xstem_kernel(const StemArgs a) {
         }
         if (a.relu) { v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f); }
         vmax = fmaxf(vmax, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
-        if (a.out_sexp) *(uint4*)(a.out + o + c4 * 4) = pair_encode(v, omul);
-        else *(float4*)(a.out + o + c4 * 4) = v;
+        *(float4*)(a.out + o + c4 * 4) = v;
         acc[c4 * 4] = v.x; acc[c4 * 4 + 1] = v.y; acc[c4 * 4 + 2] = v.z; acc[c4 * 4 + 3] = v.w;
       }
     }
@@ -194,20 +162,16 @@ DBA_EXPORT int dba_xstem_fwd(const float* x, long long x_gstride, const float* w
                              const float* bias, long long b_sstride, const float* res, float* out,
                              long long out_gstride, const int* nvalid, int G, int N, int H, int W, int Cin, int Ho,
                              int Wo, int Cout, int KH, int KW, int stride, int pad, int relu, int* amax_out,
-                             int amax_ld, const int* amax_x, int amax_x_ld, int* out_sexp,
-                             const float* bound, const void* bnf, void* stream) {
-  if (env_off()) return -100;
-  if (out_sexp && (!bound || !amax_x || res)) return -107;
+                             int amax_ld, const void* bnf, void* stream) {
   if (((uintptr_t)out & 15) || (out_gstride & 3) || (res && ((uintptr_t)res & 15))) return -100;
   StemArgs a{};
   a.x = x; a.x_gstride = x_gstride; a.w = w; a.w_sstride = w_sstride; a.wsel = wsel;
   a.bias = bias; a.b_sstride = b_sstride; a.res = res; a.out = out; a.out_gstride = out_gstride;
   a.nvalid = nvalid; a.N = N; a.H = H; a.W = W; a.Ho = Ho; a.Wo = Wo; a.stride = stride; a.pad = pad;
   a.relu = relu; a.amax_out = amax_out; a.amax_ld = amax_ld;
-  a.out_sexp = out_sexp; a.bound = bound; a.amax_x = amax_x; a.amax_x_ld = amax_x_ld;
   if (bnf) {
     a.bf = *(const BnFuse*)bnf;
-    if (a.bf.mode != 1 || bias || res || relu || out_sexp || a.bf.C != Cout) return -108;
+    if (a.bf.mode != 1 || bias || res || relu || a.bf.C != Cout) return -108;
   }
   hipStream_t st = (hipStream_t)stream;
   if (KH == 3 && KW == 3 && Cin == 3 && Cout == 32) return stem_go<3, 3, 3, 32, 8>(a, G, st);

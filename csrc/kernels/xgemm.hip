@@ -1,19 +1,19 @@
-// Reference-precision (fp32) convolution family for gfx950: split-bf16 MFMA.
+// Reference-precision (fp32) convolution family for gfx950: scaled fp16-pair MFMA.
 //
 // The reference trains and evaluates in fp32 (image_train.py:84-91, models/resnet_cifar.py:
-// 67-104).  gfx950 has no xf32 MFMA and its exact f32-input MFMA runs at 1/16 of the bf16
-// rate, so these kernels keep fp32 operands in HBM and split every operand element x into
-// P bf16 planes while staging it into LDS:
+// 67-104).  gfx950 has no xf32 MFMA and its exact f32-input MFMA runs at 1/16 of the 16-bit
+// rate, so these kernels keep fp32 operands in HBM and split every operand element x, scaled
+// by a power of two 2^s fixed per launch from the operand's max |x| (xmfma.hpp HScale), into
+// two fp16 planes while staging it into LDS:
 //
-//     x = x0 + x1 (+ x2) + e,    x_p = bf16(x - x0 - ... - x_{p-1}),
-//     |e| <= 2^-16 |x| (P = 2)  /  2^-24 |x| (P = 3)
+//     x * 2^s = h + l + e,   h = f16(x * 2^s),   l = f16(x * 2^s - h),   |e| <= 2^-22 |x|
 //
-// and sum the plane products with total order <= P-1 on the bf16 MFMA with fp32
-// accumulation: P = 2 -> 3 MFMAs per product (x0y0 + x0y1 + x1y0, relative error ~4e-6,
-// fp32 accumulate), P = 3 -> 6 MFMAs (error at the fp32-accumulation level, ~3e-7).
-// Either is 2.7x / 5.3x the work of a bf16 GEMM but still 5x / 2.7x the peak of the exact
-// f32 MFMA (157 TF).  The split costs 2.5 VALU ops per element (v_cvt_pk_bf16_f32,
-// shift/mask, v_pk_add_f32, v_cvt_pk_bf16_f32), done once per staged element.
+// and sum the plane products hh + hl + lh (3 MFMAs per product, fp32 accumulation; the
+// dropped ll term is <= 2^-22 |xy|) on the f16 MFMA: fp32-level error (tests/test_gpu_f32.py
+// against fp64) at 1/3 of the 16-bit peak, ~5x the exact f32 MFMA's.  The operand maxima are
+// folded by the producing kernels' epilogues (common.hpp amax_fold), so the scales cost no
+// extra pass.  (Round 2-4 also carried 2- and 3-plane bf16 splits; the fp16 pair replaced
+// them on every pass, measured under the branch-matched fp64 oracle: profiles/split_policy_r3.md.)
 //
 // Kernels (all deterministic: fixed reduction orders, no float atomics; the in-launch split-K
 // combine draws integer arrival tickets that only pick WHICH block sums the slabs):
@@ -63,17 +63,8 @@ struct XArgs {
   const int* amax_w;                         // H: max |w| slot, indexed by weight slot
   int* amax_out;                             // optional: fold max |out| (zeroed slot)
   int amax_src_ld, amax_w_ld, amax_out_ld;
-  const uint16_t* wp;                        // H: the weights pre-split (xsplit_w_kernel): per slot
+  const uint16_t* wp;                        // the weights pre-split (xsplit_w_kernel): per slot
   long long wp_sstride;                      //    2 planes of wp_sstride/2 fp16, scaled like amax_w
-  // fp16-pair activations (PairAct below): the A operand arrives pre-split (in_sexp: its
-  // per-replica scale exponent), the output leaves pre-split (out_sexp: written per replica;
-  // bound: per weight slot {max row L1 of w, max |bias|}; amax_res: the residual's max), the
-  // residual arrives pre-split (res_sexp)
-  const int* in_sexp;
-  int* out_sexp;
-  const float* bound;
-  const int* amax_res; int amax_res_ld;
-  const int* res_sexp;
   // in-launch split-K combine (xconv_kernel sk_combine): slab z of replica g at
   // sk_ws + z * zstride + g * sk_gstride; sk_cnt: zeroed arrival counters, one per
   // (replica, tile, class); out / out_gstride stay the real output
@@ -86,6 +77,15 @@ struct XArgs {
   BnFuse bf;
   const float* lz_coef;
   int lz_relu;
+  // fused downsampling shortcut (evaluation, ximg_kernel / xhalo_kernel SC): out += the 1x1
+  // stride-2 conv of x2 [G][N][sc_H][sc_W][sc_C] with pre-split weights (sc_wp: per slot 2 planes
+  // of Ncol x sc_C fp16) + its bias, as extra k-steps of the same accumulators
+  const float* sc_src; long long sc_gstride;
+  int sc_H, sc_W, sc_C;
+  const uint16_t* sc_wp; long long sc_wp_sstride;
+  const int* sc_amax_src; int sc_amax_src_ld;
+  const int* sc_amax_w; int sc_amax_w_ld;
+  const float* sc_bias; long long sc_b_sstride;
   XClass cls[4];
 };
 
@@ -167,15 +167,6 @@ __device__ __forceinline__ bool sk_combine(const XArgs& a, float* Ct, const long
   return true;
 }
 
-// fp16-pair output exponent of replica g (slot: its weight slot; PairAct); every lane of the
-// wave calls it (amax_read)
-__device__ __forceinline__ int pair_out_exp(const XArgs& a, int g, int slot) {
-  const float ax = __int_as_float(amax_read(a.amax_src, a.amax_src_ld, g));
-  const float ar = a.amax_res ? __int_as_float(amax_read(a.amax_res, a.amax_res_ld, g)) : 0.f;
-  const float b = a.bound[2 * slot] * ax + a.bound[2 * slot + 1] + ar;
-  return hexp(__float_as_int(2.f * b));
-}
-
 // register budget (minimum workgroups per CU): 3 lets the 128x64 / 64x128 / 32x128 tiles keep
 // their accumulators in VGPRs within 168 registers (3 waves per SIMD, no spills; the 128x128
 // tiles stay at 2, LDS-bound).  Those tiles run the short-K stride-2 and 1x1 convs, whose
@@ -191,13 +182,11 @@ __device__ __forceinline__ int pair_out_exp(const XArgs& a, int g, int slot) {
 // arithmetic of a.kslab split-K launches summed in z order (xsplitk_reduce / sk_combine), so a
 // grouped launch reproduces a lone client's split-K bits without the slab round trip through
 // HBM or the separate reduce / statistics pass
-template <int BM, int BN, int WM, int WN, int P, int VEC, bool H, bool PW = false, bool PA = false, bool LZ = false,
-          bool KS = false>
+template <int BM, int BN, int WM, int WN, int VEC, bool PW = false, bool LZ = false, bool KS = false>
 __global__ __launch_bounds__(256, KS ? 2 : XCONV_MINB) void xconv_kernel(const XArgs a) {
-  static_assert(!H || P == 2, "fp16 split: 2 planes");
-  static_assert(!LZ || (H && !PA && VEC >= 4), "lazy BN operand: fp16 pair, fp32 source, 4-channel vectors");
-  static_assert(!PW || (H && VEC >= 4), "pre-split weights: fp16 pair, vector loads");
-  static_assert(!PA || (PW && VEC >= 4), "pre-split activations (PairAct): with pre-split weights");
+  static_assert(!LZ || VEC >= 4, "lazy BN operand: 4-channel vectors");
+  static_assert(!PW || VEC >= 4, "pre-split weights: vector loads");
+  constexpr int P = 2;
   constexpr int TM = BM / WM, TN = BN / WN, MI = TM / 32, NJ = TN / 32;
   static_assert(WM * WN == 4 && MI >= 1 && NJ >= 1, "wave tiling");
   constexpr int ROWS = BM + BN, PL = ROWS * 4;   // uint4 per plane image
@@ -368,17 +357,12 @@ __global__ __launch_bounds__(256, KS ? 2 : XCONV_MINB) void xconv_kernel(const X
   };
   // quarter q of stage st -> LDS buffer buf
   HScale hs;
-  if constexpr (H)
-    hs.init(amax_read(a.amax_src, a.amax_src_ld, g), amax_read(a.amax_w, a.amax_w_ld, slot), PA ? a.in_sexp : nullptr, g);
+  hs.init(amax_read(a.amax_src, a.amax_src_ld, g), amax_read(a.amax_w, a.amax_w_ld, slot));
   auto lput_q = [&](int buf, int st, int q) __attribute__((always_inline)) {
     uint4* L = lds + buf * P * PL;
     uint2 sp[P];
     if (q < RA) {
-      if constexpr (PA) {   // pre-split activations: the loaded bits are {4 hi, 4 lo}
-        const uint4 u = __builtin_bit_cast(uint4, ra[st][q]);
-        sp[0] = make_uint2(u.x, u.y);
-        sp[1] = make_uint2(u.z, u.w);
-      } else if constexpr (LZ) {   // relu?(fma(y, scale, shift)) in the image, 0 in the padding
+      if constexpr (LZ) {   // relu?(fma(y, scale, shift)) in the image, 0 in the padding
         const int kq4 = s_kq[st][q] & 0xffff;
         const bool ok = (s_kq[st][q] >> 16) != 0;
         const float4 sc = *(const float4*)&lzc[kq4], sh = *(const float4*)&lzc[512 + kq4];
@@ -387,10 +371,8 @@ __global__ __launch_bounds__(256, KS ? 2 : XCONV_MINB) void xconv_kernel(const X
         if (a.lz_relu) { v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f); }
         if (!ok) v = make_float4(0.f, 0.f, 0.f, 0.f);
         split4h(v.x, v.y, v.z, v.w, hs.ma, sp);
-      } else if constexpr (H) {
-        split4h(ra[st][q].x, ra[st][q].y, ra[st][q].z, ra[st][q].w, hs.ma, sp);
       } else {
-        split4<P>(ra[st][q].x, ra[st][q].y, ra[st][q].z, ra[st][q].w, sp);
+        split4h(ra[st][q].x, ra[st][q].y, ra[st][q].z, ra[st][q].w, hs.ma, sp);
       }
       lds_put<P, false, BM>(L, PL, 0, r0 + 32 * q, kq, sp);
     } else {
@@ -399,10 +381,8 @@ __global__ __launch_bounds__(256, KS ? 2 : XCONV_MINB) void xconv_kernel(const X
         const uint4 u = __builtin_bit_cast(uint4, rb[st][j]);
         sp[0] = make_uint2(u.x, u.y);
         sp[1] = make_uint2(u.z, u.w);
-      } else if constexpr (H) {
-        split4h(rb[st][j].x, rb[st][j].y, rb[st][j].z, rb[st][j].w, hs.mb, sp);
       } else {
-        split4<P>(rb[st][j].x, rb[st][j].y, rb[st][j].z, rb[st][j].w, sp);
+        split4h(rb[st][j].x, rb[st][j].y, rb[st][j].z, rb[st][j].w, hs.mb, sp);
       }
       lds_put<P, false, BN>(L, PL, BM, r0 + 32 * j, kq, sp);
     }
@@ -423,7 +403,7 @@ __global__ __launch_bounds__(256, KS ? 2 : XCONV_MINB) void xconv_kernel(const X
   auto slab_end = [&](int kt_done) __attribute__((always_inline)) {   // after step kt_done
     if constexpr (KS) {
       if (kt_done + 1 == kb_next) {
-        if constexpr (H) hs.finish(acc);
+        hs.finish(acc);
 #pragma unroll
         for (int i = 0; i < MI; ++i)
 #pragma unroll
@@ -454,14 +434,14 @@ __global__ __launch_bounds__(256, KS ? 2 : XCONV_MINB) void xconv_kernel(const X
     int kt = kt0;
     for (; kt + 1 < kt1; kt += 2) {
       gprep();   // step kt+3
-      mma_step<MI, NJ, P, H, false, BM, BN, RA + RB>(lds, PL, wm * TM, wn * TN, acc, lane, [&](int q) __attribute__((always_inline)) {
+      mma_step<MI, NJ, P, true, false, BM, BN, RA + RB>(lds, PL, wm * TM, wn * TN, acc, lane, [&](int q) __attribute__((always_inline)) {
         lput_q(1, 1, q);
         gq(1, q);
       });
       slab_end(kt);
       __syncthreads();
       gprep();   // step kt+4
-      mma_step<MI, NJ, P, H, false, BM, BN, RA + RB>(lds + P * PL, PL, wm * TM, wn * TN, acc, lane, [&](int q) __attribute__((always_inline)) {
+      mma_step<MI, NJ, P, true, false, BM, BN, RA + RB>(lds + P * PL, PL, wm * TM, wn * TN, acc, lane, [&](int q) __attribute__((always_inline)) {
         lput_q(0, 0, q);
         gq(0, q);
       });
@@ -469,7 +449,7 @@ __global__ __launch_bounds__(256, KS ? 2 : XCONV_MINB) void xconv_kernel(const X
       __syncthreads();
     }
     if (kt < kt1) {
-      mma_step<MI, NJ, P, H, false, BM, BN, 0>(lds, PL, wm * TM, wn * TN, acc, lane, [&](int) {});
+      mma_step<MI, NJ, P, true, false, BM, BN, 0>(lds, PL, wm * TM, wn * TN, acc, lane, [&](int) {});
       slab_end(kt);
     }
   }
@@ -478,7 +458,7 @@ __global__ __launch_bounds__(256, KS ? 2 : XCONV_MINB) void xconv_kernel(const X
     for (int i = 0; i < MI; ++i)
 #pragma unroll
       for (int j = 0; j < NJ; ++j) acc[i][j] = ssum[i][j];
-  } else if constexpr (H) {
+  } else {
     hs.finish(acc);
   }
 
@@ -510,14 +490,6 @@ __global__ __launch_bounds__(256, KS ? 2 : XCONV_MINB) void xconv_kernel(const X
   float vmax = 0.f;
   if ((a.Ncol & 3) == 0) {
     constexpr int C4 = BN / 4;
-    // fp16-pair residual / output (PairAct): block-uniform scales
-    const float rinv = (res && a.res_sexp) ? PairAct::mul(-a.res_sexp[g]) : 0.f;
-    int so = 0;
-    if (fin && a.out_sexp) {
-      so = pair_out_exp(a, g, slot);
-      if (tid == 0) a.out_sexp[g] = so;
-    }
-    const float omul = PairAct::mul(so);
     for (int e = tid; e < BM * C4; e += 256) {
       const int row = e / C4, cc = (e - row * C4) * 4;
       const int n = n0 + cc;
@@ -526,8 +498,7 @@ __global__ __launch_bounds__(256, KS ? 2 : XCONV_MINB) void xconv_kernel(const X
       float4 v = *(const float4*)&Ct[row * BN + cc];
       if (bias) { v.x += bias[n]; v.y += bias[n + 1]; v.z += bias[n + 2]; v.w += bias[n + 3]; }
       if (res) {
-        const float4 rv = a.res_sexp ? PairAct::decode(*(const uint4*)(res + o + n), rinv)
-                                     : *(const float4*)(res + o + n);
+        const float4 rv = *(const float4*)(res + o + n);
         v.x += rv.x; v.y += rv.y; v.z += rv.z; v.w += rv.w;
       }
       if (relu) { v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f); }
@@ -536,8 +507,7 @@ __global__ __launch_bounds__(256, KS ? 2 : XCONV_MINB) void xconv_kernel(const X
         *(float4*)&Ct[row * BN + cc] = v;
       }
       vmax = fmaxf(vmax, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
-      if (fin && a.out_sexp) *(uint4*)(out + o + n) = PairAct::encode(v, omul);
-      else *(float4*)(out + o + n) = v;
+      *(float4*)(out + o + n) = v;
     }
   } else {
     for (int e = tid; e < BM * BN; e += 256) {
@@ -577,13 +547,15 @@ __global__ __launch_bounds__(256, KS ? 2 : XCONV_MINB) void xconv_kernel(const X
 // 16 pixels to 16 distinct slots for every tap column c0 (the former (pp >> 1) & 7 put pixels
 // 16 apart on one slot: 2-way conflicts on ~29 % of the LDS cycles, profiles/pmc_eval_r3.md).
 
-template <int W, int CS, int BM, int BN, int WM, int WN, int P, bool H, bool PRE = false, bool PA = false,
-          bool LZ = false>
+// SC (evaluation, a downsampling block's conv2 at W 16): the block's 1x1 stride-2 shortcut conv
+// (32 input channels: one k-step) runs after the 18 3x3 steps from its own LDS tile
+// (x2[2h][2w] of the block's 128 output pixels, loaded and split at the start), with its own
+// fp16 scales (the accumulators are rescaled once, exactly) and pre-split weights; its output is
+// never written or read back as a residual (ximg_kernel SC: the same scheme).
+template <int W, int CS, int BM, int BN, int WM, int WN, bool PRE = false, bool LZ = false, bool SC = false>
 __global__ __launch_bounds__(256) void xhalo_kernel(const XArgs a) {
-  static_assert(!H || P == 2, "fp16 split: 2 planes");
-  static_assert(!LZ || (H && !PA), "lazy BN operand: fp16 pair, fp32 source");
-  static_assert(!PRE || H, "pre-split weights: fp16 pair");
-  static_assert(!PA || PRE, "pre-split activations (PairAct): with pre-split weights");
+  static_assert(!SC || (PRE && !LZ), "fused shortcut: evaluation, pre-split weights");
+  constexpr int P = 2;
   constexpr int TR = BM / W, PW = W + 2, PR = TR + 2, PP = PR * PW;
   constexpr int CH = CS / 8, PATCH = PP * CH;             // uint4 per plane
   constexpr int TM = BM / WM, TN = BN / WN, MI = TM / 32, NJ = TN / 32;
@@ -593,8 +565,11 @@ __global__ __launch_bounds__(256) void xhalo_kernel(const XArgs a) {
   constexpr int NK = 9 * CS / 32;                         // k-steps
   constexpr int CB = CS / 32;                             // channel blocks per tap
   static_assert(BM * BN <= P * PATCH * 4, "epilogue tile fits the patch");
+  constexpr int NKT = NK + (SC ? 1 : 0);                  // + the shortcut's k-step
+  constexpr int SPL = BM * 4;                             // SC: uint4 per plane of the shortcut tile
   __shared__ __attribute__((aligned(16))) uint4 patch[P * PATCH];
   __shared__ __attribute__((aligned(16))) uint4 bring[2 * P * BPL];
+  __shared__ __attribute__((aligned(16))) uint4 scbuf[SC ? P * SPL : 4];
   __shared__ long long orow[BM];
 
   const int g = blockIdx.y;
@@ -633,9 +608,35 @@ __global__ __launch_bounds__(256) void xhalo_kernel(const XArgs a) {
       pv[u] = bload4(rA, ok ? (((img * a.Hs + h) * a.Ws + w) * CS + q * 4) * 4 : kOOB);
     }
   }
+  // SC: the shortcut tile, x2[img][2(h0 + r)][2c][0 .. 32) of the block's BM output pixels
+  constexpr int NS = SC ? BM * 8 / 256 : 1;
+  [[maybe_unused]] float4 sv[NS];
+  if constexpr (SC) {
+    const __amdgpu_buffer_rsrc_t rS = rsrc(a.sc_src + (long long)g * a.sc_gstride,
+                                           (long long)a.N * a.sc_H * a.sc_W * 32 * 4);
+#pragma unroll
+    for (int u = 0; u < NS; ++u) {
+      const int e = tid + 256 * u, px = e >> 3, q = e & 7;
+      const int h = 2 * (h0 + px / W), w = 2 * (px % W);
+      const bool ok = h < a.sc_H && w < a.sc_W;
+      sv[u] = bload4(rS, ok ? (((img * a.sc_H + h) * a.sc_W + w) * 32 + q * 4) * 4 : kOOB);
+    }
+  }
   HScale hs;
-  if constexpr (H)
-    hs.init(amax_read(a.amax_src, a.amax_src_ld, g), amax_read(a.amax_w, a.amax_w_ld, slot), PA ? a.in_sexp : nullptr, g);
+  hs.init(amax_read(a.amax_src, a.amax_src_ld, g), amax_read(a.amax_w, a.amax_w_ld, slot));
+  [[maybe_unused]] int s_sc = 0;
+  if constexpr (SC) {
+    const int sx = hexp(amax_read(a.sc_amax_src, a.sc_amax_src_ld, g));
+    s_sc = sx + hexp(amax_read(a.sc_amax_w, a.sc_amax_w_ld, slot));
+    const float m = __uint_as_float((uint32_t)(sx + 127) << 23);
+#pragma unroll
+    for (int u = 0; u < NS; ++u) {
+      const int e = tid + 256 * u;
+      uint2 sp[P];
+      split4h(sv[u].x, sv[u].y, sv[u].z, sv[u].w, m, sp);
+      lds_put<P, false, BM>(scbuf, SPL, 0, e >> 3, e & 7, sp);
+    }
+  }
   const float* lzc = LZ ? a.lz_coef + (long long)g * kBnRows * CS : nullptr;
   auto patch_put = [&]() __attribute__((always_inline)) {
 #pragma unroll
@@ -644,11 +645,7 @@ __global__ __launch_bounds__(256) void xhalo_kernel(const XArgs a) {
       if (e >= PP * Q4) break;
       const int pp = e / Q4, q = e - pp * Q4;
       uint2 sp[P];
-      if constexpr (PA) {   // pre-split activations: the loaded bits are {4 hi, 4 lo}
-        const uint4 uu = __builtin_bit_cast(uint4, pv[u]);
-        sp[0] = make_uint2(uu.x, uu.y);
-        sp[1] = make_uint2(uu.z, uu.w);
-      } else if constexpr (LZ) {   // relu?(fma(y, scale, shift)) in the image, 0 in the padding
+      if constexpr (LZ) {   // relu?(fma(y, scale, shift)) in the image, 0 in the padding
         const int pr = pp / PW, pc = pp - pr * PW;
         const int h = h0 - 1 + pr, w = pc - 1;
         const bool ok = (unsigned)h < (unsigned)a.Hs && (unsigned)w < (unsigned)a.Ws;
@@ -658,10 +655,8 @@ __global__ __launch_bounds__(256) void xhalo_kernel(const XArgs a) {
         if (a.lz_relu) { v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f); }
         if (!ok) v = make_float4(0.f, 0.f, 0.f, 0.f);
         split4h(v.x, v.y, v.z, v.w, hs.ma, sp);
-      } else if constexpr (H) {
-        split4h(pv[u].x, pv[u].y, pv[u].z, pv[u].w, hs.ma, sp);
       } else {
-        split4<P>(pv[u].x, pv[u].y, pv[u].z, pv[u].w, sp);
+        split4h(pv[u].x, pv[u].y, pv[u].z, pv[u].w, hs.ma, sp);
       }
       const int o = pp * CH + ((q >> 1) ^ hswz<W, CS>(pp, pp % PW));
 #pragma unroll
@@ -681,8 +676,18 @@ __global__ __launch_bounds__(256) void xhalo_kernel(const XArgs a) {
   const __amdgpu_buffer_rsrc_t rBh = rsrc(Bh, (long long)a.Ncol * K * 2);
   const __amdgpu_buffer_rsrc_t rBl = rsrc(PRE ? Bh + (a.wp_sstride >> 1) : nullptr, (long long)a.Ncol * K * 2);
   float4 rb[2][RB];
+  [[maybe_unused]] const uint16_t* Sh = SC ? a.sc_wp + (long long)slot * a.sc_wp_sstride : nullptr;
+  [[maybe_unused]] const __amdgpu_buffer_rsrc_t rSh = rsrc(Sh, SC ? (long long)a.Ncol * 32 * 2 : 0);
+  [[maybe_unused]] const __amdgpu_buffer_rsrc_t rSl = rsrc(SC ? Sh + (a.sc_wp_sstride >> 1) : nullptr,
+                                                           SC ? (long long)a.Ncol * 32 * 2 : 0);
   auto gq = [&](int t, int st, int j) __attribute__((always_inline)) {   // quarter j of weight step t -> stage st
     const int kb = t * 32 + kq * 4;
+    if (SC && t >= NK) {   // the shortcut's weights [Ncol][32]
+      const int off = (boffs[j] >= 0 && t == NK) ? ((n0 + r0 + 32 * j) * 32 + kq * 4) * 2 : kOOB;
+      const uint2 h = bload8(rSh, off), l = bload8(rSl, off);
+      rb[st][j] = __builtin_bit_cast(float4, make_uint4(h.x, h.y, l.x, l.y));
+      return;
+    }
     if constexpr (PRE) {
       const int off = (boffs[j] >= 0 && kb < K) ? (boffs[j] + kb) * 2 : kOOB;
       const uint2 h = bload8(rBh, off), l = bload8(rBl, off);
@@ -702,10 +707,8 @@ __global__ __launch_bounds__(256) void xhalo_kernel(const XArgs a) {
       const uint4 u = __builtin_bit_cast(uint4, rb[st][q]);
       sp[0] = make_uint2(u.x, u.y);
       sp[1] = make_uint2(u.z, u.w);
-    } else if constexpr (H) {
-      split4h(rb[st][q].x, rb[st][q].y, rb[st][q].z, rb[st][q].w, hs.mb, sp);
     } else {
-      split4<P>(rb[st][q].x, rb[st][q].y, rb[st][q].z, rb[st][q].w, sp);
+      split4h(rb[st][q].x, rb[st][q].y, rb[st][q].z, rb[st][q].w, hs.mb, sp);
     }
     lds_put<P, false, BN>(bring + buf * P * BPL, BPL, 0, r0 + 32 * q, kq, sp);
   };
@@ -728,16 +731,33 @@ __global__ __launch_bounds__(256) void xhalo_kernel(const XArgs a) {
     acol[i] = m % W;
   }
   auto mma = [&](int t, int buf, int stn) __attribute__((always_inline)) {
+    const bool scs = SC && t >= NK;
     const int tap = t / CB, cb = t - tap * CB;
     int ti = tap / 3, tj = tap - ti * 3;
     if (flip) { ti = 2 - ti; tj = 2 - tj; }
     const int toff = ti * PW + tj;
     const uint4* L = bring + buf * P * BPL;
+    if (scs && t == NK) {   // the shortcut's products accumulate at their own scale (exact rescale)
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) acc[i][j][r] = ldexpf(acc[i][j][r], s_sc - hs.s);
+      hs.s = s_sc;
+    }
     sfor<2>([&](auto KK) __attribute__((always_inline)) {
       const int ch = decltype(KK)::value * 2 + hf;
       uint4 af[P][MI], bfr[P][NJ];
 #pragma unroll
       for (int i = 0; i < MI; ++i) {
+        if (scs) {
+          const int m = wm * TM + i * 32 + fr;
+          const int o = m * 4 + (ch ^ ((m >> 2) & 3));
+#pragma unroll
+          for (int p = 0; p < P; ++p) af[p][i] = scbuf[p * SPL + o];
+          continue;
+        }
         const int pp = apix[i] + toff;
         const int o = pp * CH + ((cb * 4 + ch) ^ hswz<W, CS>(pp, acol[i] + tj));
 #pragma unroll
@@ -750,7 +770,7 @@ __global__ __launch_bounds__(256) void xhalo_kernel(const XArgs a) {
 #pragma unroll
         for (int p = 0; p < P; ++p) bfr[p][j] = L[p * BPL + o];
       }
-      mma_half<MI, NJ, P, H, RB, decltype(KK)::value>(af, bfr, acc, [&](int q) __attribute__((always_inline)) {
+      mma_half<MI, NJ, P, true, RB, decltype(KK)::value>(af, bfr, acc, [&](int q) __attribute__((always_inline)) {
         lput_q(buf ^ 1, stn, q);
         gq(t + 3, stn, q);   // reload: step t+3 (past NK: zero-filled, never read)
       });
@@ -768,17 +788,17 @@ __global__ __launch_bounds__(256) void xhalo_kernel(const XArgs a) {
   }
   __syncthreads();   // patch + first weight step
   int t = 0;
-  for (; t + 1 < NK; t += 2) {
+  for (; t + 1 < NKT; t += 2) {
     mma(t, 0, 1);
     __syncthreads();
     mma(t + 1, 1, 0);
     __syncthreads();
   }
-  if (t < NK) {
+  if (t < NKT) {
     mma(t, 0, 1);   // (its filler writes a buffer nobody reads)
     __syncthreads();
   }
-  if constexpr (H) hs.finish(acc);
+  hs.finish(acc);
 
   // ---- epilogue through the (drained) patch memory
   float* Ct = reinterpret_cast<float*>(patch);
@@ -792,26 +812,24 @@ __global__ __launch_bounds__(256) void xhalo_kernel(const XArgs a) {
   __syncthreads();
   float* out = a.out + (long long)g * a.out_gstride;
   const float* bias = a.bias ? a.bias + (long long)slot * a.b_sstride : nullptr;
+  const float* bias2 = (SC && a.sc_bias) ? a.sc_bias + (long long)slot * a.sc_b_sstride : nullptr;
   const float* res = a.res ? a.res + (long long)g * a.out_gstride : nullptr;
   constexpr int C4 = BN / 4;
   float vmax = 0.f;
-  const float rinv = (res && a.res_sexp) ? PairAct::mul(-a.res_sexp[g]) : 0.f;
-  int so = 0;
-  if (a.out_sexp) {
-    so = pair_out_exp(a, g, slot);
-    if (tid == 0) a.out_sexp[g] = so;
-  }
-  const float omul = PairAct::mul(so);
   for (int e = tid; e < BM * C4; e += 256) {
     const int row = e / C4, cc = (e - row * C4) * 4;
     const int n = n0 + cc;
     if (n >= a.Ncol) continue;
     const long long o = orow[row];
     float4 v = *(const float4*)&Ct[row * BN + cc];
-    if (bias) { v.x += bias[n]; v.y += bias[n + 1]; v.z += bias[n + 2]; v.w += bias[n + 3]; }
+    if (bias2) {   // conv2's and the shortcut's folded biases, summed first (as ximg_kernel)
+      const float4 b1 = bias ? *(const float4*)(bias + n) : make_float4(0.f, 0.f, 0.f, 0.f);
+      v.x += b1.x + bias2[n]; v.y += b1.y + bias2[n + 1]; v.z += b1.z + bias2[n + 2]; v.w += b1.w + bias2[n + 3];
+    } else if (bias) {
+      v.x += bias[n]; v.y += bias[n + 1]; v.z += bias[n + 2]; v.w += bias[n + 3];
+    }
     if (res) {
-      const float4 rv = a.res_sexp ? PairAct::decode(*(const uint4*)(res + o + n), rinv)
-                                   : *(const float4*)(res + o + n);
+      const float4 rv = *(const float4*)(res + o + n);
       v.x += rv.x; v.y += rv.y; v.z += rv.z; v.w += rv.w;
     }
     if (a.relu) { v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f); }
@@ -820,8 +838,7 @@ __global__ __launch_bounds__(256) void xhalo_kernel(const XArgs a) {
       *(float4*)&Ct[row * BN + cc] = v;
     }
     vmax = fmaxf(vmax, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
-    if (a.out_sexp) *(uint4*)(out + o + n) = PairAct::encode(v, omul);
-    else *(float4*)(out + o + n) = v;
+    *(float4*)(out + o + n) = v;
   }
   if (a.amax_out) amax_fold(a.amax_out, a.amax_out_ld, g, vmax);
   if (a.bf.mode) {
@@ -843,29 +860,35 @@ __global__ __launch_bounds__(256) void xhalo_kernel(const XArgs a) {
 // read by all 9 taps at their pixel offsets — (W+2)^2 / W^2 = 1.27x / 1.56x / 2.25x of the
 // image bytes instead of 9x.  The next chunk's patch is loaded into registers while the
 // current chunk's 9 k-steps run (8 steps to land).
-//   NT = 256 (4 waves, 2 blocks per CU): one patch buffer, the next chunk is split + stored
-//     after the chunk's last barrier (one more barrier per chunk);
-//   NT = 512 (8 waves, BM 256, one block per CU; DBA_F32_XIMG_V=2, measured slower): two
-//     patch buffers, the next chunk's split + stores ride in the MFMA gaps of the chunk's last
-//     k-step (no extra barrier), and each weight k-step feeds twice the pixels.
+// 4 waves, 2 blocks per CU, one patch buffer: the next chunk is split + stored after the
+// chunk's last barrier (one more barrier per chunk).  (An 8-wave BM-256 form with two patch
+// buffers, the next chunk split in the MFMA gaps, was measured slower — one block per CU
+// exposes its prologue / epilogue: eval.layer3 254 vs 314 TF, profiles/r4/ximg/README.md.)
 // Weights: the two-stage register / LDS ring of xhalo_kernel.  Epilogue straight from the
 // accumulators (a 32-lane row is 32 consecutive output channels: 128-B segments).
+// SC (a downsampling block's conv2, evaluation): the block's 1x1 stride-2 shortcut conv runs as
+// sc_C / 32 more chunks of ONE tap each after the 3x3 chunks — chunk c's "patch" holds
+// x2[img][2h][2w][32 channels] at the interior pixels and the step reads it at the centre tap,
+// the weights come from the shortcut's pre-split planes — so the shortcut's output is never
+// written or read back as a residual (reference: models/resnet_cifar.py:24-36).  Its operands
+// carry their own fp16 scales: the accumulators are rescaled by 2^(s_sc - s_main) (exact) before
+// the first shortcut step, and its folded bias is added with conv2's in the epilogue.
 // Deterministic; the chunk-major k order makes its bits differ from the tap-major implicit
 // GEMM's (both fp32 level: tests hold both to the fp64 oracle).
-template <int W, int IMGS, int BN, int WM, int WN, bool PRE, int NT>
-__global__ __launch_bounds__(NT) void ximg_kernel(const XArgs a) {
-  constexpr int P = 2;
-  constexpr bool DB = NT == 512;                            // double-buffered patch
+template <int W, int IMGS, int BN, int WM, int WN, bool PRE, bool SC = false>
+__global__ __launch_bounds__(256) void ximg_kernel(const XArgs a) {
+  static_assert(!SC || PRE, "fused shortcut: pre-split weights (evaluation)");
+  constexpr int P = 2, NT = 256;
   constexpr int PW = W + 2, PI = PW * PW, PP = IMGS * PI;   // padded pixels per image / patch
   constexpr int CC = 32, CH = CC / 8, Q4 = CC / 4;          // chunk channels, 16-B chunks, float4 per pixel
   constexpr int PATCH = PP * CH;                            // uint4 per plane
   constexpr int BM = IMGS * W * W;
   constexpr int TM = BM / WM, TN = BN / WN, MI = TM / 32, NJ = TN / 32;
-  static_assert(WM * WN == NT / 64 && MI >= 1 && NJ >= 1 && (BM == 128 || BM == 256), "tiling");
+  static_assert(WM * WN == NT / 64 && MI >= 1 && NJ >= 1 && BM == 128, "tiling");
   constexpr int RPT = NT / 8;                               // weight rows staged per pass
   static_assert(BN % RPT == 0, "weight rows");
   constexpr int RB = BN / RPT, BPL = BN * 4;
-  __shared__ __attribute__((aligned(16))) uint4 patch[(DB ? 2 : 1) * P * PATCH];
+  __shared__ __attribute__((aligned(16))) uint4 patch[P * PATCH];
   __shared__ __attribute__((aligned(16))) uint4 bring[2 * P * BPL];
 
   const int g = blockIdx.y;
@@ -874,18 +897,24 @@ __global__ __launch_bounds__(NT) void ximg_kernel(const XArgs a) {
   const int nv = min(valid_rows(a.nvalid, g, a.N), a.N);
   if (img0 >= nv) return;
   const int slot = a.wsel ? a.wsel[g] : g;
-  const int Cs = a.Cs, K = 9 * Cs, NC = Cs / CC, NK = 9 * NC;
+  const int Cs = a.Cs, K = 9 * Cs, NC = Cs / CC;
+  const int NCT = NC + (SC ? a.sc_C / CC : 0);              // chunks: 3x3 ones, then the shortcut's
+  const int NK = 9 * NC + (NCT - NC);                       // k-steps
   const float* __restrict__ src = a.src + (long long)g * a.src_gstride;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WN, wn = wid % WN;
   const int kq = tid & 7, r0 = tid >> 3;
   const int fr = lane & 31, hf = lane >> 5;
 
-  // ---- patch chunks: chunk cc of images img0 .. img0+IMGS-1, zero padding / invalid images
+  // ---- patch chunks: chunk cc of images img0 .. img0+IMGS-1, zero padding / invalid images;
+  // a shortcut chunk's interior pixel (h, w) holds x2[2h][2w] (its halo is never read)
   constexpr int NE = (PP * Q4 + NT - 1) / NT;
   float4 pv[NE];
   const __amdgpu_buffer_rsrc_t rA = rsrc(src, (long long)a.N * W * W * Cs * 4);
+  [[maybe_unused]] const __amdgpu_buffer_rsrc_t rS =
+      rsrc(SC ? a.sc_src + (long long)g * a.sc_gstride : nullptr, SC ? (long long)a.N * a.sc_H * a.sc_W * a.sc_C * 4 : 0);
   auto pload = [&](int cc) __attribute__((always_inline)) {
+    const bool sc = SC && cc >= NC;
 #pragma unroll
     for (int u = 0; u < NE; ++u) {
       const int e = tid + NT * u;
@@ -893,39 +922,54 @@ __global__ __launch_bounds__(NT) void ximg_kernel(const XArgs a) {
       const int im = pp / PI, rem = pp - im * PI;
       const int h = rem / PW - 1, w = rem % PW - 1, img = img0 + im;
       const bool ok = e < PP * Q4 && img < nv && (unsigned)h < (unsigned)W && (unsigned)w < (unsigned)W;
-      pv[u] = bload4(rA, ok ? (((img * W + h) * W + w) * Cs + cc * CC + q * 4) * 4 : kOOB);
+      if (sc)
+        pv[u] = bload4(rS, ok ? (((img * a.sc_H + 2 * h) * a.sc_W + 2 * w) * a.sc_C + (cc - NC) * CC + q * 4) * 4 : kOOB);
+      else
+        pv[u] = bload4(rA, ok ? (((img * W + h) * W + w) * Cs + cc * CC + q * 4) * 4 : kOOB);
     }
   };
   HScale hs;
-  auto ppiece = [&](int u, int pb) __attribute__((always_inline)) {   // piece u of pv -> patch buffer pb
+  float ma_sc = 1.f;   // SC: the shortcut input's fill multiplier
+  int s_sc = 0;        //     and the shortcut products' accumulator exponent
+  auto ppiece = [&](int u, float m) __attribute__((always_inline)) {   // piece u of pv -> the patch
     const int e = tid + NT * u;
     if (e >= PP * Q4) return;
     const int pp = e / Q4, q = e - pp * Q4;
     const int prow = (pp % PI) / PW;   // patch row: the swizzle key
     uint2 sp[P];
-    split4h(pv[u].x, pv[u].y, pv[u].z, pv[u].w, hs.ma, sp);
-    const int o = pb * P * PATCH + pp * CH + ((q >> 1) ^ (prow & 3));
+    split4h(pv[u].x, pv[u].y, pv[u].z, pv[u].w, m, sp);
+    const int o = pp * CH + ((q >> 1) ^ (prow & 3));
 #pragma unroll
     for (int p = 0; p < P; ++p) ((uint2*)&patch[p * PATCH + o])[q & 1] = sp[p];
   };
 
   // ---- weights (pre-split planes, or fp32 split while staging: the same bits): two-stage
-  // pipeline, k-step t = chunk t / 9, tap t % 9
-  int boffs[RB];
+  // pipeline, k-step t = chunk t / 9, tap t % 9 (shortcut step t >= 9 NC: chunk NC + t - 9 NC)
+  int bn_[RB];
 #pragma unroll
   for (int j = 0; j < RB; ++j) {
     const int n = n0 + r0 + RPT * j;
-    boffs[j] = n < a.Ncol ? n * K : -1;
+    bn_[j] = n < a.Ncol ? n : -1;
   }
   const uint16_t* Bh = PRE ? a.wp + (long long)slot * a.wp_sstride : nullptr;
   const __amdgpu_buffer_rsrc_t rBh = rsrc(Bh, (long long)a.Ncol * K * 2);
   const __amdgpu_buffer_rsrc_t rBl = rsrc(PRE ? Bh + (a.wp_sstride >> 1) : nullptr, (long long)a.Ncol * K * 2);
   const __amdgpu_buffer_rsrc_t rB = rsrc(a.w + (long long)slot * a.w_sstride, (long long)a.Ncol * K * 4);
+  const uint16_t* Sh = SC ? a.sc_wp + (long long)slot * a.sc_wp_sstride : nullptr;
+  [[maybe_unused]] const __amdgpu_buffer_rsrc_t rSh = rsrc(Sh, SC ? (long long)a.Ncol * a.sc_C * 2 : 0);
+  [[maybe_unused]] const __amdgpu_buffer_rsrc_t rSl =
+      rsrc(SC ? Sh + (a.sc_wp_sstride >> 1) : nullptr, SC ? (long long)a.Ncol * a.sc_C * 2 : 0);
   uint4 rb[2][RB];
   auto gq = [&](int t, int st, int j) __attribute__((always_inline)) {
+    const bool ok = bn_[j] >= 0 && t < NK;
+    if (SC && t >= 9 * NC) {
+      const int kb = bn_[j] * a.sc_C + (t - 9 * NC) * CC + kq * 4;
+      const uint2 h = bload8(rSh, ok ? kb * 2 : kOOB), l = bload8(rSl, ok ? kb * 2 : kOOB);
+      rb[st][j] = make_uint4(h.x, h.y, l.x, l.y);
+      return;
+    }
     const int cc = t / 9, tap = t - cc * 9;
-    const int kb = boffs[j] + tap * Cs + cc * CC + kq * 4;
-    const bool ok = boffs[j] >= 0 && t < NK;
+    const int kb = bn_[j] * K + tap * Cs + cc * CC + kq * 4;
     if constexpr (PRE) {
       const uint2 h = bload8(rBh, ok ? kb * 2 : kOOB), l = bload8(rBl, ok ? kb * 2 : kOOB);
       rb[st][j] = make_uint4(h.x, h.y, l.x, l.y);
@@ -966,15 +1010,11 @@ __global__ __launch_bounds__(NT) void ximg_kernel(const XArgs a) {
     apix[i] = im * PI + (rem / W) * PW + rem % W;
     arow[i] = rem / W;
   }
-  // k-step t from patch buffer pb and weight buffer buf; fills: the weight ring's next step
-  // and (PT) the next chunk's patch into buffer pb ^ 1
-  auto mma = [&](auto PTc, int t, int buf, int stn, int pb) __attribute__((always_inline)) {
-    constexpr bool PT = decltype(PTc)::value;
-    constexpr int NQ = RB + (PT ? NE : 0);
-    const int tap = t % 9, ti = tap / 3, tj = tap - ti * 3;
+  // k-step t from weight buffer buf; fill: the weight ring's next step
+  auto mma = [&](int t, int buf, int stn) __attribute__((always_inline)) {
+    const int tap = (SC && t >= 9 * NC) ? 4 : t % 9, ti = tap / 3, tj = tap - ti * 3;
     const int toff = ti * PW + tj;
     const uint4* L = bring + buf * P * BPL;
-    const uint4* A = patch + pb * P * PATCH;
     sfor<2>([&](auto KK) __attribute__((always_inline)) {
       const int ch = decltype(KK)::value * 2 + hf;
       uint4 af[P][MI], bfr[P][NJ];
@@ -983,7 +1023,7 @@ __global__ __launch_bounds__(NT) void ximg_kernel(const XArgs a) {
         const int pp = apix[i] + toff;
         const int o = pp * CH + (ch ^ ((arow[i] + ti) & 3));
 #pragma unroll
-        for (int p = 0; p < P; ++p) af[p][i] = A[p * PATCH + o];
+        for (int p = 0; p < P; ++p) af[p][i] = patch[p * PATCH + o];
       }
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
@@ -992,34 +1032,41 @@ __global__ __launch_bounds__(NT) void ximg_kernel(const XArgs a) {
 #pragma unroll
         for (int p = 0; p < P; ++p) bfr[p][j] = L[p * BPL + o];
       }
-      mma_half<MI, NJ, P, true, NQ, decltype(KK)::value>(af, bfr, acc, [&](int q) __attribute__((always_inline)) {
-        if (q < RB) {
-          lput_q(buf ^ 1, stn, q);
-          gq(t + 3, stn, q);   // reload: step t+3 (past NK: zero-filled, never read)
-        } else {
-          ppiece(q - RB, pb ^ 1);
-        }
+      mma_half<MI, NJ, P, true, RB, decltype(KK)::value>(af, bfr, acc, [&](int q) __attribute__((always_inline)) {
+        lput_q(buf ^ 1, stn, q);
+        gq(t + 3, stn, q);   // reload: step t+3 (past NK: zero-filled, never read)
       });
     });
   };
   auto step = [&](int t, int buf, int stn) __attribute__((always_inline)) {
-    const int c = t / 9;
-    const bool last = t - 9 * c == 8 && c + 1 < NC;   // the chunk's last k-step, another follows
-    const int pb = DB ? (c & 1) : 0;
-    if (DB && last) mma(std::true_type{}, t, buf, stn, pb);
-    else mma(std::false_type{}, t, buf, stn, pb);
-    __syncthreads();
-    if (last) {
-      if constexpr (!DB) {   // every read of the old patch is done: the next chunk replaces it
+    const bool scs = SC && t >= 9 * NC;
+    const int c = scs ? NC + (t - 9 * NC) : t / 9;
+    if (SC && t == 9 * NC) {   // the shortcut's products accumulate at their own scale (exact)
 #pragma unroll
-        for (int u = 0; u < NE; ++u) ppiece(u, 0);
-      }
-      if (c + 2 < NC) pload(c + 2);
-      if constexpr (!DB) __syncthreads();
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) acc[i][j][r] = ldexpf(acc[i][j][r], s_sc - hs.s);
+      hs.s = s_sc;
+    }
+    mma(t, buf, stn);
+    __syncthreads();
+    if ((scs || t - 9 * c == 8) && c + 1 < NCT) {   // the chunk's last k-step, another follows
+      const float m = (SC && c + 1 >= NC) ? ma_sc : hs.ma;
+#pragma unroll
+      for (int u = 0; u < NE; ++u) ppiece(u, m);   // every read of the old patch is done
+      if (c + 2 < NCT) pload(c + 2);
+      __syncthreads();
     }
   };
 
   hs.init(amax_read(a.amax_src, a.amax_src_ld, g), amax_read(a.amax_w, a.amax_w_ld, slot));
+  if constexpr (SC) {
+    const int sx = hexp(amax_read(a.sc_amax_src, a.sc_amax_src_ld, g));
+    ma_sc = __uint_as_float((uint32_t)(sx + 127) << 23);
+    s_sc = sx + hexp(amax_read(a.sc_amax_w, a.sc_amax_w_ld, slot));
+  }
 #pragma unroll
   for (int q = 0; q < RB; ++q) {
     gq(0, 0, q);
@@ -1027,8 +1074,8 @@ __global__ __launch_bounds__(NT) void ximg_kernel(const XArgs a) {
   }
   pload(0);
 #pragma unroll
-  for (int u = 0; u < NE; ++u) ppiece(u, 0);
-  if (NC > 1) pload(1);
+  for (int u = 0; u < NE; ++u) ppiece(u, hs.ma);
+  if (NCT > 1) pload(1);
 #pragma unroll
   for (int q = 0; q < RB; ++q) {
     lput_q(0, 0, q);
@@ -1043,16 +1090,17 @@ __global__ __launch_bounds__(NT) void ximg_kernel(const XArgs a) {
   if (t < NK) step(t, 0, 1);
   hs.finish(acc);
 
-  // ---- epilogue from the accumulators: bias, residual, ReLU, max
+  // ---- epilogue from the accumulators: bias (+ the shortcut's), residual, ReLU, max
   float* out = a.out + (long long)g * a.out_gstride;
   const float* bias = a.bias ? a.bias + (long long)slot * a.b_sstride : nullptr;
+  const float* bias2 = (SC && a.sc_bias) ? a.sc_bias + (long long)slot * a.sc_b_sstride : nullptr;
   const float* res = a.res ? a.res + (long long)g * a.out_gstride : nullptr;
   float vmax = 0.f;
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
     const int n = n0 + wn * TN + j * 32 + fr;
     if (n >= a.Ncol) continue;
-    const float bv = bias ? bias[n] : 0.f;
+    const float bv = (bias ? bias[n] : 0.f) + (bias2 ? bias2[n] : 0.f);
 #pragma unroll
     for (int i = 0; i < MI; ++i)
 #pragma unroll
@@ -1061,7 +1109,7 @@ __global__ __launch_bounds__(NT) void ximg_kernel(const XArgs a) {
         if (img0 + m / (W * W) >= nv) continue;
         const long long o = (long long)(img0 * W * W + m) * a.Ncol + n;
         float v = acc[i][j][r];
-        if (bias) v += bv;
+        if (bias || bias2) v += bv;
         if (res) v += res[o];
         if (a.relu) v = fmaxf(v, 0.f);
         vmax = fmaxf(vmax, fabsf(v));
@@ -1069,197 +1117,6 @@ __global__ __launch_bounds__(NT) void ximg_kernel(const XArgs a) {
       }
   }
   if (a.amax_out) amax_fold(a.amax_out, a.amax_out_ld, g, vmax);
-}
-
-// ============================================================ persistent halo conv
-// Weight-stationary, persistent form of xhalo_kernel for the stage-1 shape (W 32, Cs 32,
-// Ncol 32, fp16 pair): the same per-element MFMA sequence (tap-major k-steps, plane products in
-// prod_pa/pb order) — identical bits — but
-//   * a block owns a contiguous run of (replica, image, row-tile) items and keeps its replica's
-//     split weights for ALL nine taps resident in LDS (36 KB, reloaded only when the run
-//     crosses into the next replica), instead of streaming them through a two-stage ring with a
-//     barrier per 32-deep k-step (xhalo_kernel: 9 barriers and 37 KB of weight traffic per
-//     128-pixel tile);
-//   * the next item's input patch is loaded into registers while the current item's 54 MFMAs
-//     per wave run (the patch load is the latency the per-tile kernel exposes every block);
-//   * consecutive row tiles of one image go to the same block, so the two halo rows a tile
-//     shares with its neighbour are L2 / L1 hits.
-// Weight LDS image: per plane, row n (output channel) holds its K = 288 fp16 in 36 16-B chunks,
-// chunk c at c ^ ((n >> 2) & 3): the B-fragment reads of a wave (32 rows, one k-chunk) hit 16
-// distinct bank slots per ds_read_b128 lane group (as lds_put's swizzle).  63 KB of LDS: two
-// blocks per CU.
-template <int TR, bool PRE>
-__global__ __launch_bounds__(256, 2) void xhalo_ws_kernel(const XArgs a, int G) {
-  constexpr int W = 32, CS = 32, NC = 32, P = 2;
-  constexpr int BM = TR * W, PW = W + 2, PR = TR + 2, PP = PR * PW;
-  constexpr int CH = CS / 8, PATCH = PP * CH;              // uint4 per patch plane
-  constexpr int K = 9 * CS, KC = K / 8, WPL = NC * KC;     // weight chunks per row / plane
-  constexpr int TM = BM / 4, MI = TM / 32;                 // 4 waves stacked along M
-  constexpr int Q4 = CS / 4, NE = (PP * Q4 + 255) / 256;
-  static_assert(BM * NC <= P * PATCH * 4, "epilogue tile fits the patch");
-  __shared__ __attribute__((aligned(16))) uint4 wlds[P * WPL];
-  __shared__ __attribute__((aligned(16))) uint4 patch[P * PATCH];
-
-  const int tid = threadIdx.x, lane = tid & 63, wm = tid >> 6;
-  const int fr = lane & 31, hf = lane >> 5;
-  const int HT = a.Ho / TR;
-  const bool flip = a.dsg < 0;
-  int total = 0;
-  for (int gg = 0; gg < G; ++gg) total += valid_rows(a.nvalid, gg, a.N) * HT;
-  // the valid items, split evenly over the grid (inactive replicas leave no idle blocks)
-  const int per = (total + gridDim.x - 1) / gridDim.x;
-  int item = blockIdx.x * per;
-  const int end = min(total, item + per);
-  if (item >= end) return;
-
-  // item -> (g, img, h0): items are counted over the valid images of every replica in order
-  auto decode = [&](int it, int& g, int& img, int& h0) __attribute__((always_inline)) {
-    g = 0;
-    int base = 0;
-    for (;; ++g) {
-      const int n = valid_rows(a.nvalid, g, a.N) * HT;
-      if (it < base + n) break;
-      base += n;
-    }
-    const int r = it - base;
-    img = r / HT;
-    h0 = (r - img * HT) * TR;
-  };
-  float4 pv[NE];
-  auto patch_load = [&](int g, int img, int h0) __attribute__((always_inline)) {
-    const float* __restrict__ src = a.src + (long long)g * a.src_gstride;
-    const __amdgpu_buffer_rsrc_t rA = rsrc(src, (long long)a.N * a.Hs * a.Ws * CS * 4);
-#pragma unroll
-    for (int u = 0; u < NE; ++u) {
-      const int e = tid + 256 * u;
-      const int pp = e / Q4, q = e - pp * Q4;
-      const int pr = pp / PW, pc = pp - pr * PW;
-      const int h = h0 - 1 + pr, w = pc - 1;
-      const bool ok = e < PP * Q4 && (unsigned)h < (unsigned)a.Hs && (unsigned)w < (unsigned)a.Ws;
-      pv[u] = bload4(rA, ok ? (((img * a.Hs + h) * a.Ws + w) * CS + q * 4) * 4 : kOOB);
-    }
-  };
-  auto patch_put = [&](float ma) __attribute__((always_inline)) {
-#pragma unroll
-    for (int u = 0; u < NE; ++u) {
-      const int e = tid + 256 * u;
-      if (e >= PP * Q4) break;
-      const int pp = e / Q4, q = e - pp * Q4;
-      uint2 sp[P];
-      split4h(pv[u].x, pv[u].y, pv[u].z, pv[u].w, ma, sp);
-      const int o = pp * CH + ((q >> 1) ^ hswz<W, CS>(pp, pp % PW));
-#pragma unroll
-      for (int p = 0; p < P; ++p) ((uint2*)&patch[p * PATCH + o])[q & 1] = sp[p];
-    }
-  };
-  auto weights_put = [&](int slot, float mb) __attribute__((always_inline)) {
-    for (int e = tid; e < WPL; e += 256) {       // chunk e = row n, chunk c (8 k-elements)
-      const int n = e / KC, c = e - n * KC;
-      const int o = n * KC + (c ^ ((n >> 2) & 3));
-      if constexpr (PRE) {
-        const uint16_t* Bh = a.wp + (long long)slot * a.wp_sstride;
-        const uint4* ph = (const uint4*)(Bh + (long long)n * K + c * 8);
-        const uint4* pl = (const uint4*)(Bh + (a.wp_sstride >> 1) + (long long)n * K + c * 8);
-        wlds[o] = *ph;
-        wlds[WPL + o] = *pl;
-      } else {
-        const float* Bp = a.w + (long long)slot * a.w_sstride + (long long)n * K + c * 8;
-        const float4 x0 = ((const float4*)Bp)[0], x1 = ((const float4*)Bp)[1];
-        uint2 s0[2], s1[2];
-        split4h(x0.x, x0.y, x0.z, x0.w, mb, s0);
-        split4h(x1.x, x1.y, x1.z, x1.w, mb, s1);
-        wlds[o] = make_uint4(s0[0].x, s0[0].y, s1[0].x, s1[0].y);
-        wlds[WPL + o] = make_uint4(s0[1].x, s0[1].y, s1[1].x, s1[1].y);
-      }
-    }
-  };
-
-  int g, img, h0;
-  decode(item, g, img, h0);
-  patch_load(g, img, h0);
-  int cur_g = -1, slot = 0;
-  HScale hs;
-  float vmax = 0.f;
-  int apix[MI];
-#pragma unroll
-  for (int i = 0; i < MI; ++i) {
-    const int m = wm * TM + i * 32 + fr;
-    apix[i] = (m / W) * PW + (m % W);
-  }
-  for (; item < end; ++item) {
-    if (g != cur_g) {
-      if (cur_g >= 0 && a.amax_out) {             // the previous replica's output max
-        amax_fold(a.amax_out, a.amax_out_ld, cur_g, vmax);
-        vmax = 0.f;
-      }
-      slot = a.wsel ? a.wsel[g] : g;
-      hs.init(amax_read(a.amax_src, a.amax_src_ld, g), amax_read(a.amax_w, a.amax_w_ld, slot));
-      __syncthreads();                            // previous weights no longer read
-      weights_put(slot, hs.mb);
-      cur_g = g;
-    }
-    patch_put(hs.ma);
-    __syncthreads();
-    const int ig = g, iimg = img, ih0 = h0;
-    if (item + 1 < end) {                         // next item's patch: in flight during the MFMAs
-      decode(item + 1, g, img, h0);
-      patch_load(g, img, h0);
-    }
-    f32x16_t acc[MI][1];
-#pragma unroll
-    for (int i = 0; i < MI; ++i)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][0][r] = 0.f;
-#pragma unroll 1
-    for (int tap = 0; tap < 9; ++tap) {
-      int ti = tap / 3, tj = tap - ti * 3;
-      if (flip) { ti = 2 - ti; tj = 2 - tj; }
-      const int toff = ti * PW + tj;
-      sfor<2>([&](auto KK) __attribute__((always_inline)) {
-        const int ch = decltype(KK)::value * 2 + hf;
-        uint4 af[P][MI], bfr[P][1];
-#pragma unroll
-        for (int i = 0; i < MI; ++i) {
-          const int pp = apix[i] + toff;
-          const int o = pp * CH + (ch ^ hswz<W, CS>(pp, 0));
-#pragma unroll
-          for (int p = 0; p < P; ++p) af[p][i] = patch[p * PATCH + o];
-        }
-        const int ob = fr * KC + ((tap * 4 + ch) ^ ((fr >> 2) & 3));
-#pragma unroll
-        for (int p = 0; p < P; ++p) bfr[p][0] = wlds[p * WPL + ob];
-        mma_half<MI, 1, P, true, 0, decltype(KK)::value>(af, bfr, acc, [&](int) {});
-      });
-    }
-    hs.finish(acc);
-    __syncthreads();                              // patch reads done: reuse it as the tile
-    float* Ct = reinterpret_cast<float*>(patch);
-#pragma unroll
-    for (int i = 0; i < MI; ++i)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) Ct[(wm * TM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * hf) * NC + fr] = acc[i][0][r];
-    __syncthreads();
-    const int tm = iimg * HT + ih0 / TR;
-    float* out = a.out + (long long)ig * a.out_gstride;
-    const float* bias = a.bias ? a.bias + (long long)slot * a.b_sstride : nullptr;
-    const float* res = a.res ? a.res + (long long)ig * a.out_gstride : nullptr;
-    constexpr int C4 = NC / 4;
-    for (int e = tid; e < BM * C4; e += 256) {
-      const int row = e / C4, cc = (e - row * C4) * 4;
-      const long long o = (((long long)iimg * a.Ho + ih0 + row / W) * a.Wo + row % W) * NC + cc;
-      float4 v = *(const float4*)&Ct[row * NC + cc];
-      if (bias) { v.x += bias[cc]; v.y += bias[cc + 1]; v.z += bias[cc + 2]; v.w += bias[cc + 3]; }
-      if (res) {
-        const float4 rv = *(const float4*)(res + o);
-        v.x += rv.x; v.y += rv.y; v.z += rv.z; v.w += rv.w;
-      }
-      if (a.relu) { v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f); }
-      vmax = fmaxf(vmax, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
-      *(float4*)(out + o) = v;
-    }
-    __syncthreads();                              // tile consumed before the next patch_put
-  }
-  if (a.amax_out) amax_fold(a.amax_out, a.amax_out_ld, cur_g, vmax);
 }
 
 // sum of split-K slabs ws[z][g][m][n] (fixed z order) + bias (+ residual) (ReLU), valid rows
@@ -1307,7 +1164,7 @@ struct XWArgs {
   const int* nvalid;
   int N, H, W, Cin, Ho, Wo, Cout, KW, stride, pad, K;
   int tiles_k, mchunk;
-  const int* amax_dy;                      // H: max |dy| / |x| slots (common.hpp)
+  const int* amax_dy;                      // max |dy| / |x| slots (common.hpp)
   const int* amax_x;
   int amax_dy_ld, amax_x_ld;
   FDiv dHoWo, dWo;
@@ -1317,10 +1174,9 @@ struct XWArgs {
   const float* x_coef; int x_relu;
 };
 
-template <int BNO, int BK, int WN_, int WK_, int P, int VEC, bool H, bool XLZ = false>
+template <int BNO, int BK, int WN_, int WK_, int VEC, bool XLZ = false>
 __global__ __launch_bounds__(256) void xwgrad_kernel(const XWArgs a) {
-  static_assert(!H || P == 2, "fp16 split: 2 planes");
-  static_assert(!XLZ || H, "lazy BN operand: fp16 pair");
+  constexpr int P = 2;
   constexpr int TNo = BNO / WN_, TK = BK / WK_, MI = TNo / 32, NJ = TK / 32;
   static_assert(WN_ * WK_ == 4 && MI >= 1 && NJ >= 1, "wave tiling");
   static_assert(BK == 128, "x micro-tiles: one per thread");
@@ -1448,7 +1304,7 @@ __global__ __launch_bounds__(256) void xwgrad_kernel(const XWArgs a) {
   };
   // piece q of stage st -> LDS buffer buf: q < 4 transposes dy column e = q, q >= 4 x column q-4
   HScale hs;
-  if constexpr (H) hs.init(amax_read(a.amax_dy, a.amax_dy_ld, g), amax_read(a.amax_x, a.amax_x_ld, g));
+  hs.init(amax_read(a.amax_dy, a.amax_dy_ld, g), amax_read(a.amax_x, a.amax_x_ld, g));
   auto lput_q = [&](int buf, int st, int q) __attribute__((always_inline)) {
     uint4* L = lds + buf * P * PL;
     uint2 sp[P];
@@ -1465,14 +1321,12 @@ __global__ __launch_bounds__(256) void xwgrad_kernel(const XWArgs a) {
     }
     if (q < 4) {
       if (dact) {
-        if constexpr (H) split4h(dv[st][0][q], dv[st][1][q], dv[st][2][q], dv[st][3][q], hs.ma, sp);
-        else split4<P>(dv[st][0][q], dv[st][1][q], dv[st][2][q], dv[st][3][q], sp);
+        split4h(dv[st][0][q], dv[st][1][q], dv[st][2][q], dv[st][3][q], hs.ma, sp);
         lds_put<P, true, BNO>(L, PL, 0, dn4 * 4 + q, m4, sp);
       }
     } else {
       const int e = q - 4;
-      if constexpr (H) split4h(xv[st][0][e], xv[st][1][e], xv[st][2][e], xv[st][3][e], hs.mb, sp);
-      else split4<P>(xv[st][0][e], xv[st][1][e], xv[st][2][e], xv[st][3][e], sp);
+      split4h(xv[st][0][e], xv[st][1][e], xv[st][2][e], xv[st][3][e], hs.mb, sp);
       lds_put<P, true, BK>(L, PL, BNO, xk4 * 4 + e, m4, sp);
     }
   };
@@ -1500,15 +1354,15 @@ __global__ __launch_bounds__(256) void xwgrad_kernel(const XWArgs a) {
   __syncthreads();
   int mt = mb;
   for (; mt + 32 < me; mt += 64) {
-    mma_step<MI, NJ, P, H, true, BNO, BK, 8>(lds, PL, wn * TNo, wk * TK, acc, lane,
+    mma_step<MI, NJ, P, true, true, BNO, BK, 8>(lds, PL, wn * TNo, wk * TK, acc, lane,
                                              [&](int q) __attribute__((always_inline)) { fill(1, 1, q, mt + 96); });
     __syncthreads();
-    mma_step<MI, NJ, P, H, true, BNO, BK, 8>(lds + P * PL, PL, wn * TNo, wk * TK, acc, lane,
+    mma_step<MI, NJ, P, true, true, BNO, BK, 8>(lds + P * PL, PL, wn * TNo, wk * TK, acc, lane,
                                              [&](int q) __attribute__((always_inline)) { fill(0, 0, q, mt + 128); });
     __syncthreads();
   }
-  if (mt < me) mma_step<MI, NJ, P, H, true, BNO, BK, 0>(lds, PL, wn * TNo, wk * TK, acc, lane, [&](int) {});
-  if constexpr (H) hs.finish(acc);
+  if (mt < me) mma_step<MI, NJ, P, true, true, BNO, BK, 0>(lds, PL, wn * TNo, wk * TK, acc, lane, [&](int) {});
+  hs.finish(acc);
 
   // acc[i][j][r]: cout row n = n0 + wn*TNo + i*32 + (r&3) + 8*(r>>2) + 4*hf, k col = k0 + wk*TK + j*32 + fr
   const int fr = lane & 31, hf = lane >> 5;
@@ -1701,38 +1555,6 @@ __global__ __launch_bounds__(256) void xsplit_w_kernel(const float* __restrict__
 #pragma unroll
     for (int i = 0; i < 4; ++i)
       if (e + i < per) { oh[e + i] = h[i]; ol[e + i] = l[i]; }
-  }
-}
-
-// output bound of an evaluation conv per weight slot (PairAct): out[slot] = {max over rows of
-// sum |w[row][k]|, max |bias|}; each row's L1 is an fp32 sum (relative rounding <= K * 2^-24;
-// the 2x in the exponent choice covers it), x (1 + 2^-9).
-// Grid (slots, row groups of 16): each wave
-// sums whole rows with coalesced loads (lanes stride the row, a fixed shuffle tree), the
-// block's max row goes to out[2 * slot] by an integer atomicMax on the non-negative float bits
-// (exact and order-independent, so the bound is deterministic); out must be zeroed.  The
-// former one-block-per-slot form walked each row with one thread (uncoalesced, ~95 us per
-// eval fold launch, 3.8 % of the bench's kernel time: profiles/r3_bench_kernel_stats.csv).
-__global__ __launch_bounds__(256) void row_bound_kernel(const float* __restrict__ w, long long w_sstride, int rows,
-                                                        int rowlen, const float* __restrict__ bias,
-                                                        long long b_sstride, float* __restrict__ out) {
-  const int sl = blockIdx.x, lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const float* __restrict__ ws = w + (long long)sl * w_sstride;
-  float l1 = 0.f;
-  const int r0 = blockIdx.y * 16;
-  for (int r = r0 + wv; r < min(rows, r0 + 16); r += 4) {
-    const float* __restrict__ row = ws + (long long)r * rowlen;
-    float acc = 0.f;
-    for (int k = lane; k < rowlen; k += 64) acc += fabsf(row[k]);
-    acc = wave_sum(acc);
-    l1 = fmaxf(l1, acc * (1.f + 0x1p-9f));   // covers the fp32 rounding of any summation order
-  }
-  if (lane == 0) atomicMax(reinterpret_cast<int*>(out) + 2 * sl, __float_as_int(l1));
-  if (bias && blockIdx.y == 0) {
-    float bm = 0.f;
-    for (int r = threadIdx.x; r < rows; r += 256) bm = fmaxf(bm, fabsf(bias[(long long)sl * b_sstride + r]));
-    bm = wave_max(bm);
-    if (lane == 0) atomicMax(reinterpret_cast<int*>(out) + 2 * sl + 1, __float_as_int(bm));
   }
 }
 
@@ -1935,111 +1757,66 @@ int bnx_tile_go(const BnFuse& f, const float* src, float* dst, long long gstride
   return rc != 0 ? rc : bnx_finalize_go(f, nvalid, G, N, HW, st);
 }
 
-int env_int(const char* name, int dflt) {
-  const char* e = getenv(name);
-  return e ? atoi(e) : dflt;
-}
-
-// split mode: 2 / 3 bf16 planes (3 / 6 MFMAs per product) or kF16 (scaled fp16 pair, 3
-// MFMAs); DBA_F32_PLANES / dba_xgemm_set_planes.  A launch runs the fp16 pair exactly when the
-// caller passes its operands' max |x| (amax pointers); kF16 tells the caller to do so.
-constexpr int kF16 = 16;
-int& planes() {
-  static int p = env_int("DBA_F32_PLANES", kF16);
-  return p;
-}
-
-template <int BM, int BN, int WM, int WN, int P, int VEC, bool H, bool PW, bool PA = false, bool LZ = false,
-          bool KS = false>
+template <int BM, int BN, int WM, int WN, int VEC, bool PW, bool LZ = false, bool KS = false>
 int xconv_go(const XArgs& a, long long Mmax, int G, int nclass, hipStream_t st) {
   XArgs b = a;
   b.tiles_n = ceil_div(a.Ncol, BN);
   const dim3 grid((unsigned)(ceil_div(Mmax, BM) * b.tiles_n), G, nclass * a.splitk);
-  hipLaunchKernelGGL((xconv_kernel<BM, BN, WM, WN, P, VEC, H, PW, PA, LZ, KS>), grid, dim3(256), 0, st, b);
+  hipLaunchKernelGGL((xconv_kernel<BM, BN, WM, WN, VEC, PW, LZ, KS>), grid, dim3(256), 0, st, b);
   DBA_LAUNCH_CHECK();
 }
 
-// a split forward of a grouped launch as in-block slabs (xconv_kernel KS): fp16 pair, 32-channel
-// vectors, Ncol > 64 (the stage-3 / 4 convs xsplitk splits), 64 x 128 tiles (the running sum
-// doubles the accumulators), at most DBA_F32_KSLAB slabs (0: off — slabs through HBM + the
-// reduce / BN pass).  Serial slabs cost the launch its split-K parallelism: at 8 slabs (stage 4)
-// the 10-client step's split convs took 385 vs 352 us with the reduce passes included.
-int kslab_max() {
-  static const int m = env_int("DBA_F32_KSLAB", 2);
-  return m;
-}
+// a split forward of a grouped launch as in-block slabs (xconv_kernel KS): 32-channel vectors,
+// Ncol > 64 (the stage-3 / 4 convs xsplitk splits), 64 x 128 tiles (the running sum doubles the
+// accumulators), at most kKslabMax slabs (more go through HBM + the reduce / BN pass).  Serial
+// slabs cost the launch its split-K parallelism: at 8 slabs (stage 4) the 10-client step's split
+// convs took 385 vs 352 us with the reduce passes included (profiles/r4/kslab/).
+constexpr int kKslabMax = 2;
 int xconv_ks(const XArgs& a, long long M, int G, int vec, hipStream_t st) {
-  if (a.kslab > kslab_max() || !a.amax_src || a.Ncol <= 64 || a.Cs % 32 || vec < 4 || a.in_sexp || a.out_sexp || a.res_sexp ||
-      a.splitk != 1 || a.kslab < 2)
-    return -100;
-  if (a.lz_coef) return xconv_go<64, 128, 2, 2, 2, 32, true, false, false, true, true>(a, M, G, 1, st);
-  if (a.wp) return xconv_go<64, 128, 2, 2, 2, 32, true, true, false, false, true>(a, M, G, 1, st);
-  return xconv_go<64, 128, 2, 2, 2, 32, true, false, false, false, true>(a, M, G, 1, st);
+  if (a.kslab > kKslabMax || a.Ncol <= 64 || a.Cs % 32 || vec < 4 || a.splitk != 1 || a.kslab < 2) return -100;
+  if (a.lz_coef) return xconv_go<64, 128, 2, 2, 32, false, true, true>(a, M, G, 1, st);
+  if (a.wp) return xconv_go<64, 128, 2, 2, 32, true, false, true>(a, M, G, 1, st);
+  return xconv_go<64, 128, 2, 2, 32, false, false, true>(a, M, G, 1, st);
 }
 
-template <int P, int VEC, bool H, bool PW = false, bool PA = false, bool LZ = false>
+template <int VEC, bool PW = false, bool LZ = false>
 int xconv_tile(const XArgs& a, long long Mmax, int G, int nclass, int bm, hipStream_t st) {
-  if (a.Ncol <= 32) return xconv_go<128, 32, 4, 1, P, VEC, H, PW, PA, LZ>(a, Mmax, G, nclass, st);
+  if (a.Ncol <= 32) return xconv_go<128, 32, 4, 1, VEC, PW, LZ>(a, Mmax, G, nclass, st);
   if (a.Ncol <= 64) {
-    if (bm == 64) return xconv_go<64, 64, 2, 2, P, VEC, H, PW, PA, LZ>(a, Mmax, G, nclass, st);
-    return xconv_go<128, 64, 2, 2, P, VEC, H, PW, PA, LZ>(a, Mmax, G, nclass, st);
+    if (bm == 64) return xconv_go<64, 64, 2, 2, VEC, PW, LZ>(a, Mmax, G, nclass, st);
+    return xconv_go<128, 64, 2, 2, VEC, PW, LZ>(a, Mmax, G, nclass, st);
   }
-  if (bm == 32) return xconv_go<32, 128, 1, 4, P, VEC, H, PW, PA, LZ>(a, Mmax, G, nclass, st);
-  if (bm == 64) return xconv_go<64, 128, 2, 2, P, VEC, H, PW, PA, LZ>(a, Mmax, G, nclass, st);
-  return xconv_go<128, 128, 2, 2, P, VEC, H, PW, PA, LZ>(a, Mmax, G, nclass, st);
+  if (bm == 32) return xconv_go<32, 128, 1, 4, VEC, PW, LZ>(a, Mmax, G, nclass, st);
+  if (bm == 64) return xconv_go<64, 128, 2, 2, VEC, PW, LZ>(a, Mmax, G, nclass, st);
+  return xconv_go<128, 128, 2, 2, VEC, PW, LZ>(a, Mmax, G, nclass, st);
 }
 
 bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
-template <int W, int CS, int BM, int BN, int WM, int WN, int P, bool H, bool PRE = false, bool PA = false,
-          bool LZ = false>
+template <int W, int CS, int BM, int BN, int WM, int WN, bool PRE = false, bool LZ = false, bool SC = false>
 int xhalo_go(const XArgs& a, int G, hipStream_t st) {
   XArgs b = a;
   b.tiles_n = ceil_div(a.Ncol, BN);
   const dim3 grid((unsigned)(a.N * (a.Ho / (BM / W)) * b.tiles_n), G, 1);
-  hipLaunchKernelGGL((xhalo_kernel<W, CS, BM, BN, WM, WN, P, H, PRE, PA, LZ>), grid, dim3(256), 0, st, b);
-  DBA_LAUNCH_CHECK();
-}
-
-// persistent weight-stationary stage-1 halo conv: ~2 blocks per CU.  OFF by default
-// (DBA_F32_HALO_WS=1: on): alone it matches the per-tile kernel (eval.layer1 1504 vs 1509 us:
-// the layer is HBM-bound), but its long-lived blocks hold CUs the high-priority training stream
-// needs, so the overlapped round is slower (3.06 vs 3.20 rounds/s, profiles/halo_ws_r3.md).
-// Items are (replica, image, 4-row tile); the grid never depends on G beyond the item count,
-// and every item computes the same bits as xhalo_kernel.
-int& halo_ws_on() {
-  static int on = env_int("DBA_F32_HALO_WS", 0);
-  return on;
-}
-int xhalo_ws_try(const XArgs& a, int G, hipStream_t st) {
-  static const int blocks = env_int("DBA_F32_HALO_WS_BLOCKS", 512);
-  if (!halo_ws_on() || a.Ho % 4 != 0 || a.bf.mode || a.lz_coef) return -100;
-  if (a.wp && (((uintptr_t)a.wp & 15) || (a.wp_sstride % 8))) return -100;
-  // the item count: valid images of every replica (host view: nvalid lives on the device, so
-  // size the grid for all N images; blocks past the valid items return at once)
-  const long long total = (long long)G * a.N * (a.Ho / 4);
-  if (total >= (1LL << 31)) return -100;
-  const int nb = (int)std::max(1LL, std::min<long long>(blocks, total));
-  const dim3 grid((unsigned)nb);
-  if (a.wp) hipLaunchKernelGGL((xhalo_ws_kernel<4, true>), grid, dim3(256), 0, st, a, G);
-  else hipLaunchKernelGGL((xhalo_ws_kernel<4, false>), grid, dim3(256), 0, st, a, G);
+  hipLaunchKernelGGL((xhalo_kernel<W, CS, BM, BN, WM, WN, PRE, LZ, SC>), grid, dim3(256), 0, st, b);
   DBA_LAUNCH_CHECK();
 }
 
 // the whole-image halo conv (ximg_kernel): evaluation forward, 3x3 stride-1 pad-1, square
-// W 16 / 8 / 4, Cs % 32 == 0, fp16 pair (weights pre-split or not), no fused BN / lazy / pair operands
-// (DBA_F32_XIMG=0: off — the implicit GEMM runs)
-template <int W, int IMGS, int BN, int WM, int WN, int NT>
+// W 8 / 4, Cs % 32 == 0, no fused BN / lazy operands (dba_ximg_set(0): off — the tests' A/B
+// against the implicit GEMM)
+template <int W, int IMGS, int BN, int WM, int WN>
 int ximg_go(const XArgs& a, int G, hipStream_t st) {
   XArgs b = a;
   b.tiles_n = ceil_div(a.Ncol, BN);
   const dim3 grid((unsigned)(ceil_div(a.N, IMGS) * b.tiles_n), G, 1);
-  if (a.wp) hipLaunchKernelGGL((ximg_kernel<W, IMGS, BN, WM, WN, true, NT>), grid, dim3(NT), 0, st, b);
-  else hipLaunchKernelGGL((ximg_kernel<W, IMGS, BN, WM, WN, false, NT>), grid, dim3(NT), 0, st, b);
+  if (a.sc_src) hipLaunchKernelGGL((ximg_kernel<W, IMGS, BN, WM, WN, true, true>), grid, dim3(256), 0, st, b);
+  else if (a.wp) hipLaunchKernelGGL((ximg_kernel<W, IMGS, BN, WM, WN, true>), grid, dim3(256), 0, st, b);
+  else hipLaunchKernelGGL((ximg_kernel<W, IMGS, BN, WM, WN, false>), grid, dim3(256), 0, st, b);
   DBA_LAUNCH_CHECK();
 }
 int& ximg_on() {
-  static int on = env_int("DBA_F32_XIMG", 1);
+  static int on = 1;
   return on;
 }
 int ximg_try(const XArgs& a, int G, int KH, int KW, hipStream_t st) {
@@ -2048,65 +1825,48 @@ int ximg_try(const XArgs& a, int G, int KH, int KW, hipStream_t st) {
       c.nJ != 3 || c.bh != -1 || c.bw != -1)
     return -100;
   if (a.Hs != a.Ho || a.Ws != a.Wo || a.Ho != a.Wo || a.Cs % 32 != 0 || a.Ncol % 32 != 0) return -100;
-  if (!a.amax_src || a.in_sexp || a.out_sexp || a.res_sexp || a.bf.mode || a.lz_coef) return -100;
+  if (a.bf.mode || a.lz_coef) return -100;
   if (!aligned16(a.src) || a.src_gstride % 4 || !aligned16(a.w) || a.w_sstride % 4) return -100;
   if (a.wp && (((uintptr_t)a.wp & 15) || a.wp_sstride % 8)) return -100;
-  // 4 waves, BM 128, one patch buffer, 2 blocks per CU (one block's prologue / epilogue runs
-  // under the other's MFMAs).  DBA_F32_XIMG_V=2: 8 waves, BM 256 x BN 64, double-buffered
-  // patches (W 16: 83 + 16 KB, W 8: 102 + 16 KB of LDS; BN 128 spills at the 256 registers of
-  // 2 waves per SIMD), one block per CU — measured slower (eval.layer2 221 vs 282 TF, layer3
-  // 254 vs 314, headline 3.11 vs 3.45 rounds/s same box: profiles/r4/ximg/README.md): the
-  // lone block's prologue and epilogue are exposed
-  static const int v = env_int("DBA_F32_XIMG_V", 1);
-  if (a.Wo == 16 && a.Ncol <= 64 && v >= 2) return ximg_go<16, 1, 64, 4, 2, 512>(a, G, st);
-  if (a.Wo == 8) {
-    if (v >= 2) return ximg_go<8, 4, 64, 4, 2, 512>(a, G, st);
-    return a.Ncol >= 128 ? ximg_go<8, 2, 128, 2, 2, 256>(a, G, st) : ximg_go<8, 2, 64, 2, 2, 256>(a, G, st);
-  }
-  if (a.Wo == 4) return a.Ncol >= 128 ? ximg_go<4, 8, 128, 2, 2, 256>(a, G, st) : ximg_go<4, 8, 64, 2, 2, 256>(a, G, st);
+  if (a.sc_src && (!a.wp || a.sc_C % 32 || a.sc_C > 256 || !aligned16(a.sc_src) || a.sc_gstride % 4 ||
+                   ((uintptr_t)a.sc_wp & 15) || a.sc_wp_sstride % 8))
+    return -100;
+  if (a.Wo == 8) return a.Ncol >= 128 ? ximg_go<8, 2, 128, 2, 2>(a, G, st) : ximg_go<8, 2, 64, 2, 2>(a, G, st);
+  if (a.Wo == 4) return a.Ncol >= 128 ? ximg_go<4, 8, 128, 2, 2>(a, G, st) : ximg_go<4, 8, 64, 2, 2>(a, G, st);
   return -100;
 }
 
 bool flip_dgrad(const XArgs& a) { return a.dsg < 0; }
 
 // the halo kernel's shapes: 3x3 stride-1 pad-1 (fwd) or its stride-1 data gradient, one class,
-// square W 32, Cs 32, Ncol <= 32, aligned fp32 operands (DBA_F32_HALO=0 off)
+// square W 32 (Cs 32, Ncol <= 32) or W 16 (Cs 64, Ncol <= 64), aligned fp32 operands.  (8-row
+// W-32 tiles were faster in isolation, not in the overlapped bench: profiles/r2_halo_tiles_ab.md;
+// a persistent weight-stationary W-32 form tied in isolation and held CUs the training stream
+// needs: 3.06 vs 3.20 rounds/s, profiles/halo_ws_r3.md.)
 int xhalo_try(const XArgs& a, int G, int KH, int KW, hipStream_t st) {
-  static const bool off = env_int("DBA_F32_HALO", 1) == 0;
   const XClass& c = a.cls[0];
-  if (off || KH != 3 || KW != 3 || a.sp != 1 || a.os != 1 || a.splitk != 1 || c.nI != 3 || c.nJ != 3) return -100;
+  if (KH != 3 || KW != 3 || a.sp != 1 || a.os != 1 || a.splitk != 1 || c.nI != 3 || c.nJ != 3) return -100;
   if (!(a.dsg == 1 ? (c.bh == -1 && c.bw == -1) : (c.bh == 1 && c.bw == 1))) return -100;
   if (a.Hs != a.Ho || a.Ws != a.Wo || a.Ho != a.Wo || (a.Ncol & 3) != 0) return -100;
   if (!aligned16(a.src) || !aligned16(a.w) || a.src_gstride % 4 || a.w_sstride % 4) return -100;
-  // 8-row tiles (each wave 64 x 32: two A fragments per B fragment) when they still give the
-  // launch >= 1024 blocks; 4-row tiles otherwise
-  static const bool big_ok = env_int("DBA_F32_HALO_BIG", 0) != 0;   // measured slower in the bench (profiles/r2_halo_tiles_ab.md)
-  const bool big = big_ok && a.Ho % 8 == 0 && (long long)a.N * (a.Ho / 8) * G >= 1024;
-  const bool pairs = a.in_sexp || a.out_sexp || a.res_sexp;
-  if (pairs && !(a.amax_src && a.wp)) return -107;   // fp16-pair activations: evaluation forwards only
-  if (a.lz_coef && (!a.amax_src || pairs || a.wp || flip_dgrad(a))) return -108;   // lazy BN operand: training fwd
-  if (a.Wo == 32 && a.Cs == 32 && a.Ncol <= 32 && a.Ho % 4 == 0) {
-    if (a.lz_coef) return xhalo_go<32, 32, 128, 32, 4, 1, 2, true, false, false, true>(a, G, st);
-    if (a.in_sexp) return xhalo_go<32, 32, 128, 32, 4, 1, 2, true, true, true>(a, G, st);
-    if (a.amax_src && a.Ncol == 32 && !pairs) {
-      const int rc = xhalo_ws_try(a, G, st);
-      if (rc != -100) return rc;
-    }
-    if (a.amax_src && big && !a.wp) return xhalo_go<32, 32, 256, 32, 4, 1, 2, true>(a, G, st);
-    if (a.amax_src && a.wp) return xhalo_go<32, 32, 128, 32, 4, 1, 2, true, true>(a, G, st);
-    if (a.amax_src) return xhalo_go<32, 32, 128, 32, 4, 1, 2, true>(a, G, st);
-    if (planes() == 2) return xhalo_go<32, 32, 128, 32, 4, 1, 2, false>(a, G, st);
-    return xhalo_go<32, 32, 128, 32, 4, 1, 3, false>(a, G, st);
+  if (a.lz_coef && (a.wp || flip_dgrad(a))) return -108;   // lazy BN operand: training forward
+  if (a.Wo == 32 && a.Cs == 32 && a.Ncol <= 32 && a.Ho % 4 == 0 && !a.sc_src) {
+    if (a.lz_coef) return xhalo_go<32, 32, 128, 32, 4, 1, false, true>(a, G, st);
+    if (a.wp) return xhalo_go<32, 32, 128, 32, 4, 1, true>(a, G, st);
+    return xhalo_go<32, 32, 128, 32, 4, 1>(a, G, st);
   }
-  // W 16 / Cs 64 (8-row tiles x 64 channels) on the fp16 pair, where the implicit GEMM's
-  // re-split of every input element per tap is what bounds it (with 3 bf16 planes the MFMA
-  // work dominates and the implicit GEMM was faster: 154 vs 147 TF, kbench_r2_fp32_p3.json)
-  static const bool h16 = env_int("DBA_F32_HALO16", 1) != 0;
-  if (h16 && a.amax_src && a.Wo == 16 && a.Cs == 64 && a.Ncol <= 64 && a.Ho % 8 == 0) {
-    if (a.lz_coef) return xhalo_go<16, 64, 128, 64, 2, 2, 2, true, false, false, true>(a, G, st);
-    if (a.in_sexp) return xhalo_go<16, 64, 128, 64, 2, 2, 2, true, true, true>(a, G, st);
-    if (a.wp) return xhalo_go<16, 64, 128, 64, 2, 2, 2, true, true>(a, G, st);
-    return xhalo_go<16, 64, 128, 64, 2, 2, 2, true>(a, G, st);
+  // W 16 / Cs 64 (8-row tiles x 64 channels): the implicit GEMM's re-split of every input
+  // element per tap is what bounds that shape
+  if (a.Wo == 16 && a.Cs == 64 && a.Ncol <= 64 && a.Ho % 8 == 0) {
+    if (a.sc_src) {   // the fused downsampling shortcut: 32 input channels, pre-split weights
+      if (!a.wp || a.sc_C != 32 || !aligned16(a.sc_src) || a.sc_gstride % 4 || ((uintptr_t)a.sc_wp & 15) ||
+          a.sc_wp_sstride % 8 || flip_dgrad(a))
+        return -100;
+      return xhalo_go<16, 64, 128, 64, 2, 2, true, false, true>(a, G, st);
+    }
+    if (a.lz_coef) return xhalo_go<16, 64, 128, 64, 2, 2, false, true>(a, G, st);
+    if (a.wp) return xhalo_go<16, 64, 128, 64, 2, 2, true>(a, G, st);
+    return xhalo_go<16, 64, 128, 64, 2, 2>(a, G, st);
   }
   return -100;
 }
@@ -2115,11 +1875,11 @@ int xhalo_try(const XArgs& a, int G, int KH, int KW, hipStream_t st) {
 // launches (a lone client's grouped step) take 64-row tiles, the smallest (a lone client's
 // stage-3/4 convs: 32-64 tiles of 64 rows) 32-row tiles with one 32x32 MFMA tile per wave.
 int xconv_bm(long long Mmax, int Ncol, int G, int nclass, int splitk) {
-  static const int bm32_below = env_int("DBA_F32_BM32_BLOCKS", 256);
+  constexpr int kBm32Below = 256;
   const int bn = Ncol <= 32 ? 32 : Ncol <= 64 ? 64 : 128;
   const long long blocks = (long long)ceil_div(Mmax, 128) * ceil_div(Ncol, bn) * G * nclass * splitk;
   int bm = (bn > 32 && blocks < 512) ? 64 : 128;
-  if (bn == 128 && 2 * blocks < bm32_below) bm = 32;
+  if (bn == 128 && 2 * blocks < kBm32Below) bm = 32;
   return bm;
 }
 
@@ -2130,51 +1890,31 @@ long long xconv_sk_count(long long Mmax, int Ncol, int G, int nclass, int splitk
   return (long long)ceil_div(Mmax, bm) * ceil_div(Ncol, bn) * G * nclass;
 }
 
-// in-launch split-K combine on (DBA_F32_SK_INLAUNCH=0: the separate xsplitk_reduce launch)
-bool sk_inlaunch_on() {
-  static const bool on = env_int("DBA_F32_SK_INLAUNCH", 1) != 0;
-  return on;
-}
-
 // the in-launch combine applies: counters given and enough of them, 4-column output vectors,
 // a replica's slab addressable by a 32-bit buffer offset
 // (lone-client 32 x 128 tiles only: at 128-row tiles the reducer's serial slab read costs more
 // than the launch it saves — 10-client step 2.20 -> 2.33 ms, profiles/r3_sk_inlaunch.md)
 bool sk_ok(const int* cnt, long long cnt_n, long long M, int Ncol, int G, int nclass, int s) {
-  return cnt && sk_inlaunch_on() && s <= kSkMax && Ncol > 64 && xconv_bm(M, Ncol, G, nclass, s) == 32 &&
-         (Ncol & 3) == 0 && M * Ncol < (1LL << 29) && cnt_n >= xconv_sk_count(M, Ncol, G, nclass, s);
+  return cnt && s <= kSkMax && Ncol > 64 && xconv_bm(M, Ncol, G, nclass, s) == 32 && (Ncol & 3) == 0 &&
+         M * Ncol < (1LL << 29) && cnt_n >= xconv_sk_count(M, Ncol, G, nclass, s);
 }
 
 int xconv_dispatch(const XArgs& a, long long Mmax, int G, int nclass, int vec, hipStream_t st) {
   // The tile shape never changes a result bit: every output element sees the same k-step
   // order and the same plane-product order within a step.
+  if (!a.amax_src || !a.amax_w) return -109;   // the fp16 pair needs both operand maxima
   const int bm = xconv_bm(Mmax, a.Ncol, G, nclass, a.splitk);
   if (vec == 4 && a.Cs % 32 == 0) vec = 32;
-  if (a.in_sexp) {   // fp16-pair activations (evaluation; the launcher checked wp and vec)
-    if (vec == 32) return xconv_tile<2, 32, true, true, true>(a, Mmax, G, nclass, bm, st);
-    return xconv_tile<2, 4, true, true, true>(a, Mmax, G, nclass, bm, st);
+  if (a.lz_coef) {   // lazy BN operand (training forward; the launcher checked wp and vec)
+    if (vec == 32) return xconv_tile<32, false, true>(a, Mmax, G, nclass, bm, st);
+    return xconv_tile<4, false, true>(a, Mmax, G, nclass, bm, st);
   }
-  if (a.lz_coef) {   // lazy BN operand (training forward; the launcher checked amax, wp, vec)
-    if (vec == 32) return xconv_tile<2, 32, true, false, false, true>(a, Mmax, G, nclass, bm, st);
-    return xconv_tile<2, 4, true, false, false, true>(a, Mmax, G, nclass, bm, st);
+  if (a.wp && vec >= 4) {
+    if (vec == 32) return xconv_tile<32, true>(a, Mmax, G, nclass, bm, st);
+    return xconv_tile<4, true>(a, Mmax, G, nclass, bm, st);
   }
-  if (a.amax_src && a.wp && vec >= 4) {
-    if (vec == 32) return xconv_tile<2, 32, true, true>(a, Mmax, G, nclass, bm, st);
-    return xconv_tile<2, 4, true, true>(a, Mmax, G, nclass, bm, st);
-  }
-  if (a.amax_src) {
-    if (vec == 32) return xconv_tile<2, 32, true>(a, Mmax, G, nclass, bm, st);
-    return vec == 4 ? xconv_tile<2, 4, true>(a, Mmax, G, nclass, bm, st)
-                    : xconv_tile<2, 1, true>(a, Mmax, G, nclass, bm, st);
-  }
-  if (planes() == 2) {
-    if (vec == 32) return xconv_tile<2, 32, false>(a, Mmax, G, nclass, bm, st);
-    return vec == 4 ? xconv_tile<2, 4, false>(a, Mmax, G, nclass, bm, st)
-                    : xconv_tile<2, 1, false>(a, Mmax, G, nclass, bm, st);
-  }
-  if (vec == 32) return xconv_tile<3, 32, false>(a, Mmax, G, nclass, bm, st);
-  return vec == 4 ? xconv_tile<3, 4, false>(a, Mmax, G, nclass, bm, st)
-                  : xconv_tile<3, 1, false>(a, Mmax, G, nclass, bm, st);
+  if (vec == 32) return xconv_tile<32>(a, Mmax, G, nclass, bm, st);
+  return vec == 4 ? xconv_tile<4>(a, Mmax, G, nclass, bm, st) : xconv_tile<1>(a, Mmax, G, nclass, bm, st);
 }
 
 // split-K factor of a forward launch (1 = none).  Decided from the PER-REPLICA geometry only
@@ -2183,20 +1923,16 @@ int xconv_dispatch(const XArgs& a, long long Mmax, int G, int nclass, int vec, h
 // place different client groups on a rank).  Splits a replica below ~128 tiles of 64 rows
 // (a lone client's stage-3/4 convs) into slabs of >= 8 k-steps.
 int xsplitk(long long M, int /*G*/, int Ncol, int K) {
-  static const int off = env_int("DBA_F32_SPLITK", 1) == 0;
-  if (off) return 1;
   const int bn = Ncol <= 32 ? 32 : Ncol <= 64 ? 64 : 128;
   // 128: a lone client's stage-3 convs (64 tiles of 64 rows) split in two — lone step 1.95 ->
-  // 1.85 ms, the 10-client round's training time unchanged (202.4 vs 202.6 ms, r2c_iter1)
-  static const int target = env_int("DBA_F32_SPLITK_TILES", 128);
+  // 1.85 ms, the 10-client round's training time unchanged (202.4 vs 202.6 ms, r2c_iter1);
+  // finer slabs were slower in the bench (348 -> 368 ms per round, profiles/sk_r3/)
+  constexpr int kTarget = 128, kMinK = 8, kMaxS = 8;   // tiles; k-steps per slab; slabs
   const long long tiles = (long long)ceil_div(M, 64) * ceil_div(Ncol, bn);
-  if (tiles >= target) return 1;
+  if (tiles >= kTarget) return 1;
   const int nkt = (K + 31) / 32;
-  // a slab keeps >= DBA_F32_SPLITK_MINK k-steps (default 8), at most DBA_F32_SPLITK_MAX slabs
-  static const int mink = std::max(1, env_int("DBA_F32_SPLITK_MINK", 8));
-  static const int smax = std::max(1, env_int("DBA_F32_SPLITK_MAX", 8));
-  int s = (int)std::min<long long>(smax, (target + tiles - 1) / tiles);
-  while (s > 1 && nkt / s < mink) --s;
+  int s = (int)std::min<long long>(kMaxS, (kTarget + tiles - 1) / tiles);
+  while (s > 1 && nkt / s < kMinK) --s;
   return s;
 }
 
@@ -2230,23 +1966,10 @@ ClassGeom dgrad_classes(int H, int W, int Cin, int Cout, int KH, int KW, int s, 
 
 }  // namespace
 
-// persistent weight-stationary stage-1 halo conv on / off (tests: bitwise A/B); returns the previous
-DBA_EXPORT int dba_xhalo_ws_set(int on) {
-  const int prev = halo_ws_on();
-  if (on >= 0) halo_ws_on() = on;
-  return prev;
-}
-
 // whole-image halo conv (ximg_kernel) on / off (tests: A/B against the implicit GEMM); returns the previous
 DBA_EXPORT int dba_ximg_set(int on) {
   const int prev = ximg_on();
   if (on >= 0) ximg_on() = on;
-  return prev;
-}
-
-DBA_EXPORT int dba_xgemm_set_planes(int p) {
-  const int prev = planes();
-  if (p == 2 || p == 3 || p == kF16) planes() = p;
   return prev;
 }
 
@@ -2272,9 +1995,7 @@ DBA_EXPORT int dba_xconv_fwd(const float* x, long long x_gstride, const float* w
                              long long out_gstride, const int* nvalid, int G, int N, int H, int W, int Cin, int Ho,
                              int Wo, int Cout, int KH, int KW, int stride, int pad, int relu, const int* amax_x,
                              int amax_x_ld, const int* amax_w, int amax_w_ld, int* amax_out, int amax_out_ld,
-                             const uint16_t* wp, long long wp_sstride, float* ws, long long ws_floats,
-                             const int* in_sexp, int* out_sexp, const float* bound,
-                             const int* amax_res, int amax_res_ld, const int* res_sexp, int* sk_cnt,
+                             const uint16_t* wp, long long wp_sstride, float* ws, long long ws_floats, int* sk_cnt,
                              long long sk_cnt_n, const void* bnf, const float* lz_coef, int lz_relu, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   if ((long long)N * H * W * Cin >= (1LL << 29)) return -103;   // 32-bit in-replica byte offsets
@@ -2289,17 +2010,14 @@ DBA_EXPORT int dba_xconv_fwd(const float* x, long long x_gstride, const float* w
   a.amax_src = amax_x; a.amax_w = amax_w; a.amax_out = amax_out;
   a.amax_src_ld = amax_x_ld; a.amax_w_ld = amax_w_ld; a.amax_out_ld = amax_out_ld;
   a.wp = wp; a.wp_sstride = wp_sstride;
-  a.in_sexp = in_sexp; a.out_sexp = out_sexp; a.bound = bound;
-  a.amax_res = amax_res; a.amax_res_ld = amax_res_ld; a.res_sexp = res_sexp;
   a.cls[0] = XClass{KH, KW, -pad, -pad, 0, 0, Ho, Wo, 0};
-  const bool pairs = in_sexp || out_sexp || res_sexp;
-  if (pairs && (!amax_x || !wp || vec < 4 || (Cout & 3) || (out_sexp && !bound))) return -107;
+  if (!amax_x || !amax_w) return -109;   // the fp16 pair needs both operand maxima
   if (bnf) {
     a.bf = *(const BnFuse*)bnf;
-    if (a.bf.mode != 1 || bias || res || relu || pairs || (Cout & 3) || a.bf.C != Cout) return -108;
+    if (a.bf.mode != 1 || bias || res || relu || (Cout & 3) || a.bf.C != Cout) return -108;
   }
   if (lz_coef) {
-    if (!amax_x || wp || pairs || vec < 4 || Cin > 512) return -108;
+    if (wp || vec < 4 || Cin > 512) return -108;
     a.lz_coef = lz_coef; a.lz_relu = lz_relu;
   }
   // a fused BN's finalize launch follows its producer (bnx_tile_go launches its own)
@@ -2309,7 +2027,7 @@ DBA_EXPORT int dba_xconv_fwd(const float* x, long long x_gstride, const float* w
     if (rc == -100) rc = xhalo_try(a, G, KH, KW, st);
     if (rc != -100) return fin(rc);
   }
-  const int s = pairs ? 1 : xsplitk(M, G, Cout, K);
+  const int s = xsplitk(M, G, Cout, K);
   const bool ws_ok = s > 1 && ws != nullptr && ws_floats >= (long long)s * G * M * Cout;
   if (s > 1 && !(ws_ok && sk_ok(sk_cnt, sk_cnt_n, M, Cout, G, 1, s))) {
     // grouped launch: the slabs summed inside each block (same bits as the split launches)
@@ -2344,6 +2062,41 @@ DBA_EXPORT int dba_xconv_fwd(const float* x, long long x_gstride, const float* w
     DBA_LAUNCH_CHECK();
   }
   return fin(xconv_dispatch(a, M, G, 1, vec, st));
+}
+
+// The conv2 of a downsampling BasicBlock with its 1x1 stride-2 shortcut fused (evaluation, BN
+// folded): out = relu(conv3x3(a, w2) + b2 + conv1x1_s2(x2, wsc) + bsc), one launch, the shortcut's
+// output never materialised (xhalo_kernel / ximg_kernel SC).  a [G][N][Ho][Wo][C] fp32, x2
+// [G][N][H2][W2][C2] fp32 (Ho = ceil(H2 / 2)), w2 / wsc pre-split fp16-pair planes per slot.
+// Returns -100 for shapes without a fused kernel (the caller runs the two convs).
+DBA_EXPORT int dba_xdown_fwd(const float* a_, long long a_gstride, const float* w2, long long w2_sstride,
+                             const uint16_t* w2p, long long w2p_sstride, const int* wsel, const float* b2,
+                             long long b_sstride, const float* x2, long long x2_gstride, const uint16_t* wscp,
+                             long long wscp_sstride, const float* bsc, long long bsc_sstride, float* out,
+                             long long out_gstride, const int* nvalid, int G, int N, int Ho, int Wo, int C, int H2,
+                             int W2, int C2, const int* amax_a, int amax_a_ld, const int* amax_w2, int amax_w2_ld,
+                             const int* amax_x2, int amax_x2_ld, const int* amax_wsc, int amax_wsc_ld, int* amax_out,
+                             int amax_out_ld, void* stream) {
+  if (!amax_a || !amax_w2 || !amax_x2 || !amax_wsc || !w2p || !wscp) return -109;
+  if ((Ho - 1) * 2 >= H2 || (Wo - 1) * 2 >= W2 || (long long)N * H2 * W2 * C2 >= (1LL << 29) ||
+      (long long)N * Ho * Wo * C >= (1LL << 29))
+    return -103;
+  XArgs a{};
+  a.src = a_; a.src_gstride = a_gstride; a.w = w2; a.w_sstride = w2_sstride; a.wsel = wsel;
+  a.bias = b2; a.b_sstride = b_sstride; a.res = nullptr; a.out = out; a.out_gstride = out_gstride;
+  a.nvalid = nvalid; a.N = N; a.Hs = Ho; a.Ws = Wo; a.Cs = C; a.Ncol = C; a.Ho = Ho; a.Wo = Wo;
+  a.sp = 1; a.os = 1; a.dsg = 1; a.relu = 1; a.splitk = 1;
+  a.amax_src = amax_a; a.amax_w = amax_w2; a.amax_out = amax_out;
+  a.amax_src_ld = amax_a_ld; a.amax_w_ld = amax_w2_ld; a.amax_out_ld = amax_out_ld;
+  a.wp = w2p; a.wp_sstride = w2p_sstride;
+  a.sc_src = x2; a.sc_gstride = x2_gstride; a.sc_H = H2; a.sc_W = W2; a.sc_C = C2;
+  a.sc_wp = wscp; a.sc_wp_sstride = wscp_sstride;
+  a.sc_amax_src = amax_x2; a.sc_amax_src_ld = amax_x2_ld; a.sc_amax_w = amax_wsc; a.sc_amax_w_ld = amax_wsc_ld;
+  a.sc_bias = bsc; a.sc_b_sstride = bsc_sstride;
+  a.cls[0] = XClass{3, 3, -1, -1, 0, 0, Ho, Wo, 0};
+  hipStream_t st = (hipStream_t)stream;
+  const int rc = ximg_try(a, G, 3, 3, st);
+  return rc != -100 ? rc : xhalo_try(a, G, 3, 3, st);
 }
 
 // dX of a conv from class-packed transposed weights (dba_xtranspose); accum (optional) is
@@ -2436,9 +2189,8 @@ DBA_EXPORT long long dba_xwgrad_ws_floats(int G, int N, int Ho, int Wo, int Cin,
   const int bno = Cout <= 32 ? 32 : Cout <= 64 ? 64 : 128;
   const long long tiles = (long long)ceil_div(Cout, bno) * ceil_div(K, 128);
   const long long M = (long long)N * Ho * Wo;
-  const int target = env_int("DBA_F32_WGRAD_BLOCKS", 256);
-  static const int minrows = std::max(32, env_int("DBA_F32_WGRAD_MINROWS", 256));   // rows per slab
-  long long Z = std::max(1LL, std::min((target + tiles - 1) / tiles, M / minrows));
+  constexpr int kTarget = 256, kMinRows = 256;   // blocks per replica; rows per slab
+  long long Z = std::max(1LL, std::min((kTarget + tiles - 1) / tiles, M / kMinRows));
   int mchunk = (int)((M + Z - 1) / Z);
   mchunk = (mchunk + 31) / 32 * 32;
   Z = (M + mchunk - 1) / mchunk;
@@ -2455,7 +2207,6 @@ DBA_EXPORT int dba_xwgrad(const float* dy, long long dy_gstride, const float* x,
                           int amax_dy_ld, const int* amax_x, int amax_x_ld, float* ws, long long ws_floats, int defer,
                           const float* x_coef, int x_relu, void* stream) {
   hipStream_t st = (hipStream_t)stream;
-  if (x_coef && !amax_dy) return -108;   // lazy BN operand: fp16-pair launches only
   int mchunk = 0;
   const long long need = dba_xwgrad_ws_floats(G, N, Ho, Wo, Cin, Cout, KH, KW, &mchunk);
   if (need > 0 && (ws == nullptr || ws_floats < need)) return -101;
@@ -2475,31 +2226,25 @@ DBA_EXPORT int dba_xwgrad(const float* dy, long long dy_gstride, const float* x,
   if ((long long)N * Ho * Wo * Cout >= (1LL << 29) || (long long)N * H * W * Cin >= (1LL << 29)) return -103;
   const bool v4 = Cin % 4 == 0 && Cout % 4 == 0 && Wo % 4 == 0 && aligned16(dy) && aligned16(x) &&
                   dy_gstride % 4 == 0 && x_gstride % 4 == 0;
-  // output-channel tile: 128 for wide layers; DBA_F32_WGRAD_BNO64_BLOCKS=n takes 64 when a
-  // launch would have fewer than n blocks at 128 (a lone client's stage-3/4 weight gradients:
-  // 144).  Off: lone step 1.774 -> 1.763 ms with n = 256, within run-to-run spread
-  // (scripts/gpu/r2c_iter10.sh).  The tile never changes a bit (same per-element row order
-  // within a slab); Z came from the per-replica geometry above.
-  static const int bno64_below = env_int("DBA_F32_WGRAD_BNO64_BLOCKS", 0);
-  int bno = Cout <= 32 ? 32 : Cout <= 64 ? 64 : 128;
-  if (bno == 128 && (long long)ceil_div(Cout, 128) * a.tiles_k * G * Z < bno64_below) bno = 64;
+  // output-channel tile: 128 for wide layers (64 for a lone client's stage-3/4 weight gradients
+  // when a launch would be short of blocks measured within run-to-run spread: lone step 1.774 ->
+  // 1.763 ms, scripts/gpu/r2c_iter10.sh).  The tile never changes a bit (same per-element row
+  // order within a slab); Z came from the per-replica geometry above.
+  if (!amax_dy || !amax_x) return -109;   // the fp16 pair needs both operand maxima
+  const int bno = Cout <= 32 ? 32 : Cout <= 64 ? 64 : 128;
   const dim3 grid((unsigned)(ceil_div(Cout, bno) * a.tiles_k), G, Z);
-#define XW_GO(BNO_, WN__, WK__, P_, V_, H_, X_) \
-  hipLaunchKernelGGL((xwgrad_kernel<BNO_, 128, WN__, WK__, P_, V_, H_, X_>), grid, dim3(256), 0, st, a)
-#define XW_P(P_, V_, H_, X_)                                  \
-  do {                                                        \
-    if (bno == 32) XW_GO(32, 1, 4, P_, V_, H_, X_);           \
-    else if (bno == 64) XW_GO(64, 2, 2, P_, V_, H_, X_);      \
-    else XW_GO(128, 2, 2, P_, V_, H_, X_);                    \
+#define XW_GO(BNO_, WN__, WK__, V_, X_) \
+  hipLaunchKernelGGL((xwgrad_kernel<BNO_, 128, WN__, WK__, V_, X_>), grid, dim3(256), 0, st, a)
+#define XW_P(V_, X_)                                  \
+  do {                                                \
+    if (bno == 32) XW_GO(32, 1, 4, V_, X_);           \
+    else if (bno == 64) XW_GO(64, 2, 2, V_, X_);      \
+    else XW_GO(128, 2, 2, V_, X_);                    \
   } while (0)
-  if (amax_dy && x_coef) {
-    if (v4) XW_P(2, 4, true, true); else XW_P(2, 1, true, true);
-  } else if (amax_dy) {
-    if (v4) XW_P(2, 4, true, false); else XW_P(2, 1, true, false);
-  } else if (planes() == 2) {
-    if (v4) XW_P(2, 4, false, false); else XW_P(2, 1, false, false);
+  if (x_coef) {
+    if (v4) XW_P(4, true); else XW_P(1, true);
   } else {
-    if (v4) XW_P(3, 4, false, false); else XW_P(3, 1, false, false);
+    if (v4) XW_P(4, false); else XW_P(1, false);
   }
 #undef XW_P
 #undef XW_GO
@@ -2546,14 +2291,6 @@ DBA_EXPORT int dba_amax(const float* x, long long gstride, long long n_per_g, co
   const long long per = nvalid ? per_item * (n_per_g / std::max(1LL, per_item)) : n_per_g;
   const dim3 grid((unsigned)std::max(1LL, std::min(256LL, (per + 4095) / 4096)), G);
   hipLaunchKernelGGL(amax_kernel, grid, dim3(256), 0, st, x, gstride, n_per_g, nvalid, per_item, vec, out, ld);
-  DBA_LAUNCH_CHECK();
-}
-
-// out [slots][2]: {max row L1 of w [slots][rows][rowlen], max |bias|} (bias optional)
-DBA_EXPORT int dba_row_bound(const float* w, long long w_sstride, int rows, int rowlen, const float* bias,
-                             long long b_sstride, int slots, float* out, void* stream) {
-  hipLaunchKernelGGL(row_bound_kernel, dim3(slots, ceil_div(rows, 16)), dim3(256), 0, (hipStream_t)stream, w,
-                     w_sstride, rows, rowlen, bias, b_sstride, out);
   DBA_LAUNCH_CHECK();
 }
 

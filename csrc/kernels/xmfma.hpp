@@ -1,7 +1,7 @@
 // Shared device helpers of the fp32 (split-plane MFMA) conv kernels (xgemm.hip, xblock.hip):
-// buffer loads with out-of-range zero fill, the bf16 / scaled-fp16 plane splits, the per-launch
-// fp16 scales (HScale), fp16-pair activations (PairAct), the swizzled LDS operand images and
-// the compile-time MFMA / staging schedule (mma_half).  See xgemm.hip's header for the math.
+// buffer loads with out-of-range zero fill, the scaled-fp16 pair split, the per-launch fp16
+// scales (HScale), the swizzled LDS operand images and the compile-time MFMA / staging schedule
+// (mma_half).  See xgemm.hip's header for the math.
 #pragma once
 #include "common.hpp"
 #include <type_traits>
@@ -10,11 +10,6 @@
 namespace {
 
 typedef __attribute__((ext_vector_type(2))) float f32x2v;
-typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2v;
-
-__device__ __forceinline__ uint32_t cvt_pk(float a, float b) {
-  return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2v){a, b}, bf16x2v));
-}
 
 // bounds-checked loads: a raw buffer load whose byte offset is past num_records returns zeros,
 // so out-of-image taps and past-K columns need no branch (offset kOOB)
@@ -32,23 +27,7 @@ __device__ __forceinline__ float bload1(__amdgpu_buffer_rsrc_t r, int byte_off) 
   return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, byte_off, 0, 0));
 }
 
-// 4 fp32 values -> P bf16 planes (4 bf16 = 8 bytes each)
-template <int P>
-__device__ __forceinline__ void split4(float a, float b, float c, float d, uint2 (&o)[P]) {
-#pragma unroll
-  for (int p = 0; p < P; ++p) {
-    const uint32_t u0 = cvt_pk(a, b), u1 = cvt_pk(c, d);
-    o[p] = make_uint2(u0, u1);
-    if (p + 1 < P) {
-      a -= __uint_as_float(u0 << 16);
-      b -= __uint_as_float(u0 & 0xffff0000u);
-      c -= __uint_as_float(u1 << 16);
-      d -= __uint_as_float(u1 & 0xffff0000u);
-    }
-  }
-}
-
-// ---- fp16 pair split (H mode): x*2^s = h + l + e, h = f16(x*2^s), l = f16(x*2^s - h),
+// ---- fp16 pair split: x*2^s = h + l + e, h = f16(x*2^s), l = f16(x*2^s - h),
 // |e| <= 2^-22 |x| (11 significant bits per plane against bf16's 8), 3 MFMAs per product
 // (hh + hl + lh; the dropped ll term is <= 2^-22 |xy|).  fp16's exponent range is narrow, so
 // each operand is scaled by a power of two fixed for the whole launch, chosen from the
@@ -78,8 +57,8 @@ __device__ __forceinline__ int hexp(int maxbits) { return min(kSMax, 141 - (maxb
 struct HScale {
   float ma = 1.f, mb = 1.f;   // fill multipliers 2^sa, 2^sb
   int s = 0;                  // the accumulators hold sum * 2^s
-  __device__ __forceinline__ void init(int maxa, int maxb, const int* sexp_a = nullptr, int g = 0) {
-    const int sa = sexp_a ? sexp_a[g] : hexp(maxa), sb = hexp(maxb);
+  __device__ __forceinline__ void init(int maxa, int maxb) {
+    const int sa = hexp(maxa), sb = hexp(maxb);
     ma = __uint_as_float((uint32_t)(sa + 127) << 23);
     mb = __uint_as_float((uint32_t)(sb + 127) << 23);
     s = sa + sb;
@@ -93,30 +72,6 @@ struct HScale {
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[i][j][r] = ldexpf(acc[i][j][r], -s);
   }
-};
-
-// ---- fp16-pair activations (evaluation forwards).  A conv output that only feeds other convs
-// is stored in the split form its consumer needs: every 4 consecutive channels as 16 B =
-// 4 fp16 hi + 4 fp16 lo of x * 2^s (split4h), the same 4 bytes per element as fp32.  The
-// consumer's A staging then only moves bits (no per-tap re-split: the VALU that co-bounds the
-// MFMA in the implicit GEMM, profiles/pmc_eval_r3.md) and a residual read decodes hi + lo.
-// The scale is fixed before the producer runs, from a BOUND of its output: |y| <= L1max(w) *
-// max|x| + max|b| + max|res| (weights' max row L1 per slot from the eval fold, the input's and
-// the residual's max from their producers' amax slots); 2 * bound * 2^s in [2^14, 2^15), so
-// nothing overflows, and an element's absolute error stays below bound * 2^-38 (fp16 subnormal
-// lo planes) or 2^-22 relative — under one fp32 ulp of the tensor's max while the bound is
-// within 2^14 of it.  Every block computes the same s; each writes it to out_sexp[g].
-struct PairAct {
-  __device__ __forceinline__ static float4 decode(uint4 u, float inv) {
-    const f32x2v h0 = unpkh(u.x), h1 = unpkh(u.y), l0 = unpkh(u.z), l1 = unpkh(u.w);
-    return make_float4((h0.x + l0.x) * inv, (h0.y + l0.y) * inv, (h1.x + l1.x) * inv, (h1.y + l1.y) * inv);
-  }
-  __device__ __forceinline__ static uint4 encode(float4 v, float m) {
-    uint2 sp[2];
-    split4h(v.x, v.y, v.z, v.w, m, sp);
-    return make_uint4(sp[0].x, sp[0].y, sp[1].x, sp[1].y);
-  }
-  __device__ __forceinline__ static float mul(int s) { return __uint_as_float((uint32_t)(s + 127) << 23); }
 };
 
 // LDS images: per plane, rows of 32 reduction elements (64 B = 4 x 16-B chunks).  A row's
@@ -142,15 +97,12 @@ __device__ __forceinline__ int pswz(int n) {
 // ``fill(q)`` (q = 0 .. NQ-1) is staging work of the NEXT step (split + LDS stores of one
 // 4-element quarter per call), spread evenly between the MFMAs so the VALU split and the
 // ds_write traffic issue in the MFMA gaps instead of after them.
-// one 32x32x16 MFMA on split planes: bf16 or (H) fp16 operands
+// one 32x32x16 MFMA on fp16 split planes (H: the fp16 pair — the only split of the family)
 template <bool H>
 __device__ __forceinline__ f32x16_t mfma16(const uint4& a, const uint4& b, const f32x16_t& c) {
-  if constexpr (H)
-    return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8_t, a), __builtin_bit_cast(f16x8_t, b), c,
-                                                  0, 0, 0);
-  else
-    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, a), __builtin_bit_cast(bf16x8_t, b),
-                                                   c, 0, 0, 0);
+  static_assert(H, "fp16 pair");
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8_t, a), __builtin_bit_cast(f16x8_t, b), c, 0,
+                                                0, 0);
 }
 
 // compile-time loop: f(std::integral_constant<int, 0>) ... f(integral_constant<N-1>)

@@ -120,11 +120,6 @@ class GroupTrainer:
         if self.trace:
             self.use_graph = False
         self._last_loss: Optional[torch.Tensor] = None
-        # the training step's fp32 operand split (DBA_F32_TRAIN_PLANES; default: the library's,
-        # the scaled fp16 pair on the gradient passes, ops.hip.TRAIN_H_OPS, whose operand maxima
-        # the BN / conv producers fold on the fly)
-        sm = os.environ.get("DBA_F32_TRAIN_PLANES")
-        self.split_mode: Optional[int] = int(sm) if sm else None
         # LoanNet: every client's steps between two phase events run in ONE persistent launch
         # (csrc/kernels/mlp.hip, one workgroup per client) instead of a graph replay per step;
         # DBA_MLP_PERSIST=0 keeps the per-step graph
@@ -134,10 +129,9 @@ class GroupTrainer:
 
     # ------------------------------------------------------------------ step
     def _step(self, b: _GroupBuffers) -> None:
-        # the training step's fp32 split (kernel choice is made at launch, so a captured graph
-        # keeps it): DBA_F32_TRAIN_PLANES, default = the library-wide setting
-        with ops.fp32_split(self.device, self.split_mode, ops.train_h_ops(self.device)), \
-                ops.amax_arena(b.state.shape[0], self.device, counters=SK_COUNTERS):
+        # one zeroed arena for the step's operand-max slots and split-K counters (re-zeroed by
+        # the captured fill at every graph replay)
+        with ops.amax_arena(b.state.shape[0], self.device, counters=SK_COUNTERS):
             self._step_ops(b)
 
     def _step_ops(self, b: _GroupBuffers) -> None:
@@ -231,7 +225,13 @@ class GroupTrainer:
         host = native.pack_steps(clients, G, self.B, T, max_slots)   # [T, D] int32 (C++ runtime)
         sched = to_device(host, self.device)
         if self.persistent:
-            return self._persistent_enqueue(clients, b, sched, T, global_state, on_client_done)
+            res = self._persistent_enqueue(clients, b, sched, T, global_state, on_client_done)
+            if res is not None:
+                return res
+            # the kernel declined the shape (a batch size / layer width other than the
+            # reference LoanNet's, or a device without its LDS budget) before launching
+            # anything: this trainer keeps the per-step graph path from now on
+            self.persistent = False
         if self.use_graph and b.graph is None:
             b._cur = sched[0]
             self._reset(b, global_state)
@@ -271,10 +271,11 @@ class GroupTrainer:
                 "trace": torch.stack(trace) if trace else None}
 
     def _persistent_enqueue(self, clients: List[ClientPlan], b: _GroupBuffers, sched: torch.Tensor, T: int,
-                            global_state: torch.Tensor, on_client_done=None) -> Dict[str, Any]:
+                            global_state: torch.Tensor, on_client_done=None) -> Optional[Dict[str, Any]]:
         """LoanNet: one persistent launch per segment of steps between phase events (the
         snapshots / scaling of :meth:`_phase_end` run between launches, as between graph
-        replays)."""
+        replays).  None when the kernel declines the shape at the first segment (nothing was
+        launched: the caller takes the per-step path)."""
         self._reset(b, global_state)
         G = len(clients)
         events = self._events(clients)
@@ -290,8 +291,10 @@ class GroupTrainer:
                 rc = hip.mlp_train(self.spec, sched, t0, t1, self.B, b.state, b.mom, b.fg, wl.train_store.rows,
                                    wl.train_store.labels, wl.trig_cols, wl.trig_vals, self.target, b.stats,
                                    b.max_slots, b.nan_flag, self.momentum, self.wd)
+                if rc == hip.NOT_HANDLED and t0 == 0:
+                    return None
                 if rc != 0:
-                    raise RuntimeError(f"persistent LoanNet trainer declined the shape ({rc})")
+                    raise RuntimeError(f"persistent LoanNet trainer failed mid-wave ({rc})")
                 t0 = t1
             for (g, ph) in events.get(t1, []):
                 self._phase_end(b, g, ph, snaps[g], pend_dist, g, gn2)

@@ -21,7 +21,6 @@ selecting its weights through ``wsel``.  Reference forward definitions: see
 """
 from __future__ import annotations
 
-import os
 from typing import Callable, Dict, List, Optional, Tuple
 
 import torch
@@ -32,9 +31,6 @@ from .mirror import CIFAR_RESNETS
 from .spec import ModelSpec
 
 Tensor = torch.Tensor
-# DBA_BNX_LAZY=0: training BN+ReLU outputs are stored by an apply pass instead of being applied
-# by their consuming convs (A/B of the lazy operands)
-_LAZY_BN = os.environ.get("DBA_BNX_LAZY", "1") != "0"
 BN_EPS = 1e-5
 BN_MOMENTUM = 0.1
 
@@ -149,22 +145,12 @@ class Ctx:
         self._drop_ctr = 0
         self.act_dtype = act_dtype
         self._wamax = self._weight_scales() if train else None
-        # evaluation forwards of the fp32 family on the HIP backend may keep conv-to-conv
-        # activations as fp16 pairs (ops.hip PairAct, DBA_EVAL_PAIRS=1).  OFF by default: same-box
-        # A/B of the round-4 tree, 20 timed rounds after 5 warm-up rounds, twice each: 2.924 /
-        # 2.976 rounds/s with pairs vs 3.022 / 3.024 without (profiles/r4/bench_pairs*.json) —
-        # faster per conv in isolation (profiles/kbench_r3_eval_pairs.log), slower in the round
-        self.eval_pairs = (not train and folded is not None and act_dtype == torch.float32
-                           and any(t.is_cuda for t, _ in folded.values())
-                           and ops.backend_name(next(iter(folded.values()))[0].device) == "hip"
-                           and os.environ.get("DBA_EVAL_PAIRS", "0") == "1")
 
     def _weight_scales(self) -> Optional[Dict[str, Tensor]]:
-        """fp32 kernels on the fp16 pair (ops.hip F16_PAIR): every conv / linear weight's
-        per-replica max |w| in ONE launch at the start of the step (their operand scales)."""
+        """fp32 kernels on the fp16 pair (xgemm.hip): every conv / linear weight's per-replica
+        max |w| in ONE launch at the start of the step (their operand scales)."""
         wc = self.wcomp
-        if (wc is None or not wc.is_cuda or wc.dtype != torch.float32 or ops.backend_name(wc.device) != "hip"
-                or ops.hip_module().fp32_mode() != ops.hip_module().F16_PAIR):
+        if wc is None or not wc.is_cuda or wc.dtype != torch.float32 or ops.backend_name(wc.device) != "hip":
             return None
         names = [e.name for e in self.spec.params if e.kind in ("conv_w", "lin_w")]
         slots = ops.hip_module().weight_amax(wc, [(self.spec.by_name[n].offset, self.spec.by_name[n].numel)
@@ -200,30 +186,36 @@ class Ctx:
 
     # ------------------------------------------------------------------ layers
     def conv_bn(self, x: Tensor, conv: str, bn: str, stride: int, pad: int, relu: bool,
-                residual: Optional[Tensor] = None, to_conv: bool = True) -> Tensor:
-        """Evaluation: the BN-folded conv (+ bias, residual, ReLU in its epilogue).  ``to_conv``:
-        the output only feeds convs (A operand or residual), so it may stay as fp16-pair
-        activations (ops.hip PairAct); False where a pooling or a linear layer reads it.
-        Training goes through :meth:`bn_conv` / :meth:`bn_out` (fused BN)."""
+                residual: Optional[Tensor] = None) -> Tensor:
+        """Evaluation: the BN-folded conv (+ bias, residual, ReLU in its epilogue).  Training goes
+        through :meth:`bn_conv` / :meth:`bn_out` (fused BN)."""
         if self.train:
             raise RuntimeError("conv_bn is the evaluation form; training uses bn_conv / bn_out")
         wf, bf = self.folded[conv]
-        kw = {"out_pairs": True} if (to_conv and self.eval_pairs) else {}
-        return ops.conv2d(x, wf, self.wsel, stride, pad, bias=bf, residual=residual, relu=relu,
-                          nvalid=self.nvalid, **kw)
+        return ops.conv2d(x, wf, self.wsel, stride, pad, bias=bf, residual=residual, relu=relu, nvalid=self.nvalid)
 
-    def basic_block(self, x: Tensor, pre: str, to_conv: bool = True) -> Tensor:
+    def basic_block(self, x: Tensor, pre: str) -> Tensor:
         """Evaluation of an identity BasicBlock, relu(bn2(conv2(relu(bn1(conv1(x))))) + x), BN
         folded: ONE fused launch where the backend has it (ops.hip.basic_block_eval: the
         32-wide stage; the mid activation stays in LDS), else the two folded convs."""
         w1, b1 = self.folded[pre + "conv1.weight"]
         w2, b2 = self.folded[pre + "conv2.weight"]
-        if not self.eval_pairs and ops.basic_block_ok(x, w1, w2):
+        if ops.basic_block_ok(x, w1, w2):
             return ops.basic_block_eval(x, w1, b1, w2, b2, self.wsel, self.nvalid)
-        a = ops.conv2d(x, w1, self.wsel, 1, 1, bias=b1, relu=True, nvalid=self.nvalid,
-                       **({"out_pairs": True} if self.eval_pairs else {}))
-        return ops.conv2d(a, w2, self.wsel, 1, 1, bias=b2, residual=x, relu=True, nvalid=self.nvalid,
-                          **({"out_pairs": True} if (self.eval_pairs and to_conv) else {}))
+        a = ops.conv2d(x, w1, self.wsel, 1, 1, bias=b1, relu=True, nvalid=self.nvalid)
+        return ops.conv2d(a, w2, self.wsel, 1, 1, bias=b2, residual=x, relu=True, nvalid=self.nvalid)
+
+    def down_block(self, a: Tensor, x: Tensor, pre: str, sc: str) -> Tensor:
+        """Evaluation of a downsampling block's second half, relu(bn2(conv2(a)) + shortcut(x)),
+        with the 1x1 stride-2 shortcut conv ``sc`` (BN folded): ONE launch where the backend has
+        it (ops.hip.down_block_eval: the shortcut as extra k-steps, its output never stored), else
+        the shortcut conv and conv2 with a residual epilogue."""
+        w2, b2 = self.folded[pre + "conv2.weight"]
+        wsc, bsc = self.folded[sc + ".0.weight"]
+        if ops.down_block_ok(a, w2, x, wsc):
+            return ops.down_block_eval(a, w2, b2, x, wsc, bsc, self.wsel, self.nvalid)
+        r = ops.conv2d(x, wsc, self.wsel, 2, 0, bias=bsc, nvalid=self.nvalid)
+        return ops.conv2d(a, w2, self.wsel, 1, 1, bias=b2, residual=r, relu=True, nvalid=self.nvalid)
 
     def stem_block(self, x: Tensor, stem: str, pre: str) -> Optional[Tensor]:
         """Evaluation of the CIFAR stem conv+BN+ReLU followed by the identity BasicBlock
@@ -233,7 +225,7 @@ class Ctx:
         w0, b0 = self.folded[stem]
         w1, b1 = self.folded[pre + "conv1.weight"]
         w2, b2 = self.folded[pre + "conv2.weight"]
-        if self.eval_pairs or not ops.stem_block_ok(x, w0, w1, w2):
+        if not ops.stem_block_ok(x, w0, w1, w2):
             return None
         return ops.stem_block_eval(x, w0, b0, w1, b1, w2, b2, self.wsel, self.nvalid)
 
@@ -251,9 +243,6 @@ class Ctx:
         w = self.w(conv)
         y, st = ops.conv_bn_stats(x, w, self.wsel, stride, pad, self.nvalid, self._bnp(bn), relu)
         a = bs.LazyBN(y, st, relu)
-        if relu and not _LAZY_BN:   # DBA_BNX_LAZY=0: BN+ReLU outputs stored (A/B of the lazy operands)
-            self.tape.record((a,), (x,), self._bn_conv_bwd(x, w, y, st, conv, stride, pad))
-            return self.bn_out(a, None, relu=True, lazy_relu=True)
         self.tape.record((a,), (x,), self._bn_conv_bwd(x, w, y, st, conv, stride, pad))
         return a
 
@@ -275,13 +264,12 @@ class Ctx:
                                      wt=self._wt.get(k), finish=fin),)
         return bwd
 
-    def bn_out(self, a, residual=None, relu: bool = True, lazy_relu: bool = False) -> Tensor:
+    def bn_out(self, a, residual=None, relu: bool = True) -> Tensor:
         """Training: the stored output relu?(BN(a) + residual) of a block (one pass); ``a`` a
         lazy BN output without ReLU, ``residual`` a tensor, a lazy BN output or None.  Its
         gradient is finished (ReLU mask, the sums of a's BN and of a residual BN branch) by
         whoever produces it last."""
-        # lazy_relu: ``a`` is a BN+ReLU output stored here (its affine form, the ReLU below)
-        out = ops.bn_apply(bs.LazyBN(a.y, a.stat, False) if lazy_relu else a, residual, relu, self.nvalid)
+        out = ops.bn_apply(a, residual, relu, self.nvalid)
         branch = isinstance(residual, bs.LazyBN) and not residual.relu
         out._dba_finish = bs.Finish(ya=a.y, sa=a.stat, mask_out=out if relu else None,
                                     yb=residual.y if branch else None, sb=residual.stat if branch else None)
@@ -395,11 +383,11 @@ class Ctx:
 
 
 # ------------------------------------------------------------------- architectures
-def _block_out(ctx: Ctx, a, conv: str, bn: str, pad: int, residual, to_conv: bool):
+def _block_out(ctx: Ctx, a, conv: str, bn: str, pad: int, residual):
     """relu(BN(conv(a)) + residual): evaluation — one BN-folded conv with a fused residual /
     ReLU epilogue; training — the conv (statistics fused) and one apply pass."""
     if not ctx.train:
-        return ctx.conv_bn(a, conv, bn, 1, pad, relu=True, residual=residual, to_conv=to_conv)
+        return ctx.conv_bn(a, conv, bn, 1, pad, relu=True, residual=residual)
     return ctx.bn_out(ctx.bn_conv(a, conv, bn, 1, pad, relu=False), residual, relu=True)
 
 
@@ -419,9 +407,8 @@ def _resnet_cifar(ctx: Ctx, x: Tensor) -> Tensor:
         for bi in range(done if li == 0 else 0, blocks[li]):
             stride = 2 if (li > 0 and bi == 0) else 1
             pre = f"layer{li + 1}.{bi}."
-            final = li == 3 and bi == blocks[li] - 1
             if not ctx.train and not bottleneck and stride == 1 and cin == w:
-                out = ctx.basic_block(out, pre, to_conv=not final)
+                out = ctx.basic_block(out, pre)
                 cin = w
                 continue
             if bottleneck:
@@ -431,11 +418,14 @@ def _resnet_cifar(ctx: Ctx, x: Tensor) -> Tensor:
             else:
                 a = ctx.bn_conv(out, pre + "conv1.weight", pre + "bn1", stride, 1, relu=True)
                 last, p = "2", 1
+                if not ctx.train and stride == 2 and cin != w:   # conv2 + the shortcut in one launch
+                    out, cin = ctx.down_block(a, out, pre, pre + "shortcut"), w
+                    continue
             if stride != 1 or cin != w * exp:
                 sc = ctx.bn_conv(out, pre + "shortcut.0.weight", pre + "shortcut.1", stride, 0, relu=False)
             else:
                 sc = out
-            out = _block_out(ctx, a, pre + f"conv{last}.weight", pre + f"bn{last}", p, sc, to_conv=not final)
+            out = _block_out(ctx, a, pre + f"conv{last}.weight", pre + f"bn{last}", p, sc)
             cin = w * exp
     out = ctx.gap(out)
     G, N = out.shape[:2]
@@ -446,19 +436,23 @@ def _resnet_tiny(ctx: Ctx, x: Tensor) -> Tensor:
     if ctx.train:   # the stem's output feeds the max-pool: stored
         out = ctx.bn_out(ctx.bn_conv(x, "conv1.weight", "bn1", 2, 3, relu=False), None, relu=True)
     else:
-        out = ctx.conv_bn(x, "conv1.weight", "bn1", 2, 3, relu=True, to_conv=False)   # -> max-pool
+        out = ctx.conv_bn(x, "conv1.weight", "bn1", 2, 3, relu=True)   # -> max-pool
     out = ctx.maxpool(out, 3, 2, 1)
     cin = 64
     for li, w in enumerate((64, 128, 256, 512)):
         for bi in range(2):
             stride = 2 if (li > 0 and bi == 0) else 1
             pre = f"layer{li + 1}.{bi}."
+            if not ctx.train and stride == 2 and cin != w:   # conv2 + the downsample in one launch
+                a = ctx.bn_conv(out, pre + "conv1.weight", pre + "bn1", stride, 1, relu=True)
+                out, cin = ctx.down_block(a, out, pre, pre + "downsample"), w
+                continue
             if stride != 1 or cin != w:
                 sc = ctx.bn_conv(out, pre + "downsample.0.weight", pre + "downsample.1", stride, 0, relu=False)
             else:
                 sc = out
             a = ctx.bn_conv(out, pre + "conv1.weight", pre + "bn1", stride, 1, relu=True)
-            out = _block_out(ctx, a, pre + "conv2.weight", pre + "bn2", 1, sc, to_conv=not (li == 3 and bi == 1))
+            out = _block_out(ctx, a, pre + "conv2.weight", pre + "bn2", 1, sc)
             cin = w
     out = ctx.gap(out)
     G, N = out.shape[:2]

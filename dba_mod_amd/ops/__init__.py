@@ -54,23 +54,10 @@ _OPS = ["gather_images", "gather_rows", "conv2d", "conv2d_dgrad", "conv2d_wgrad"
         "avgpool_global_bwd", "dropout", "dropout_bwd", "softmax_xent", "sgd_step", "dist_loss_grad",
         "scale_from_base", "add_noise_scaled", "delta_sum", "sq_dists", "weighted_sum", "gram", "prepare_dgrad_weights", "wgrad_flush",
         "wgrad_prepare", "conv_bn_stats", "bn_apply", "bn_finish", "basic_block_ok", "basic_block_eval",
-        "stem_block_ok", "stem_block_eval"]
+        "stem_block_ok", "stem_block_eval", "down_block_ok", "down_block_eval"]
 
 for _n in _OPS:
     globals()[_n] = _dispatch(_n)
-
-
-def fp32_split(device: torch.device, mode, h_ops=None):
-    """Context: the fp32 kernel family's operand split (``ops.hip.fp32_split``) for the
-    enclosed launches on ``device``; a no-op for the reference backend."""
-    if backend_name(device) == "hip":
-        return hip_module().fp32_split(None if mode is None else int(mode), h_ops)
-    return contextlib.nullcontext()
-
-
-def train_h_ops(device: torch.device):
-    """The conv passes a training step runs on the fp16 pair (``ops.hip.TRAIN_H_OPS``)."""
-    return hip_module().TRAIN_H_OPS if backend_name(device) == "hip" else None
 
 
 def amax_arena(G: int, device: torch.device, counters: int = 0):
@@ -82,6 +69,6 @@ def amax_arena(G: int, device: torch.device, counters: int = 0):
     return contextlib.nullcontext()
 
 
-__all__ = list(_OPS) + ["backend_for", "backend_name", "hip_module", "fp32_split", "train_h_ops", "amax_arena"]
+__all__ = list(_OPS) + ["backend_for", "backend_name", "hip_module", "amax_arena"]
 
 from . import library  # noqa: E402,F401  (torch.library registration of the dba:: ops)

@@ -107,11 +107,7 @@ class BranchReplay:
         return r.view(-1, *([1] * (t.dim() - 1))).to(t.dtype)
 
     def _record(self, out):
-        vals = out
-        if getattr(out, "_dba_pair", None) is not None:   # fp16-pair activations (ops.hip PairAct)
-            from . import hip
-            vals = hip.decode_pairs(out)
-        self.rec.append((vals > 0).cpu())
+        self.rec.append((out > 0).cpu())
         return out
 
     def _decide(self, pre):

@@ -54,14 +54,11 @@ _SIGS = {
     "dba_gram": [_P, _LL, _I, _I, _P, _P, _P],
     "dba_dist_loss_grad": [_P, _LL, _P, _LL, _P, _LL, _I, _P, _P, _F, _P, _P, _P],
     # reference-precision (fp32) family: csrc/kernels/xgemm.hip
-    "dba_xgemm_set_planes": [_I],
-    "dba_xhalo_ws_set": [_I],
     "dba_ximg_set": [_I],
     "dba_xconv_ws_floats": [_I] * 8,
     "dba_xconv_fwd": [_P, _LL, _P, _LL, _P, _P, _LL, _P, _P, _LL, _P] + [_I] * 13 + [_P, _I] * 3 + [_P, _LL] * 2
-    + [_P, _P, _P, _P, _I, _P, _P, _LL, _P, _P, _I, _P],
+    + [_P, _LL, _P, _P, _I, _P],
     "dba_xconv_sk_ints": [_I] * 8,
-    "dba_row_bound": [_P, _LL, _I, _I, _P, _LL, _I, _P, _P],
     "dba_xconv_dgrad": [_P, _LL, _P, _LL, _P, _P, _P, _LL, _P] + [_I] * 12 + [_P, _I] * 2 + [_P, _LL] * 3 + [_P, _P],
     "dba_xsplit_w": [_P, _LL, _LL, _I, _P, _I, _P, _P],
     "dba_amax": [_P, _LL, _LL, _P, _LL, _I, _P, _I, _P],
@@ -81,7 +78,9 @@ _SIGS = {
     + [_P, _P, _P, _I, _P, _I, _P],
     "dba_mlp_train": [_P, _I, _I, _I, _I, _I, _P, _LL, _P, _P, _I, _P, _I, _I, _I, _I, _P, _P, _P, _P, _I, _I,
                       _P, _LL, _I, _P, _F, _F, _P, _P],
-    "dba_xstem_fwd": [_P, _LL, _P, _LL, _P, _P, _LL, _P, _P, _LL, _P] + [_I] * 13 + [_P, _I, _P, _I, _P, _P, _P, _P],
+    "dba_xdown_fwd": [_P, _LL, _P, _LL, _P, _LL, _P, _P, _LL, _P, _LL, _P, _LL, _P, _LL, _P, _LL, _P] + [_I] * 8
+    + [_P, _I] * 5 + [_P],
+    "dba_xstem_fwd": [_P, _LL, _P, _LL, _P, _P, _LL, _P, _P, _LL, _P] + [_I] * 13 + [_P, _I, _P, _P],
 }
 for _name, _args in _SIGS.items():
     _fn = getattr(_L, _name)
@@ -90,7 +89,6 @@ for _name, _args in _SIGS.items():
 _L.dba_xconv_ws_floats.restype = ctypes.c_longlong
 _L.dba_xconv_sk_ints.restype = ctypes.c_longlong
 _L.dba_xwgrad_ws_floats.restype = ctypes.c_longlong
-_MODE = int(_L.dba_xgemm_set_planes(0))   # fp32 split mode (0: query only; DBA_F32_PLANES)
 
 
 class _BnFuse(ctypes.Structure):
@@ -111,6 +109,7 @@ assert ctypes.sizeof(_BnFuse) == int(_L.dba_bnfuse_size()), "BnFuse layout misma
 
 
 NOT_HANDLED = -100   # an entry point declining a shape (the stem kernel: not a stem)
+F16_PAIR = 16        # the fp32 family's operand split: the scaled fp16 pair (xgemm.hip header)
 
 
 def _call(name: str, *args) -> int:
@@ -159,8 +158,6 @@ def _act(t: Tensor, dt: Optional[torch.dtype] = None, what: str = "activation") 
     if dt is not None and t.dtype != dt:
         raise TypeError(f"{what}: dtype {t.dtype} does not match the op's {dt} operands "
                         f"(no silent precision conversion)")
-    if getattr(t, "_dba_pair", None) is not None and what not in ("conv input", "residual"):
-        raise TypeError(f"{what}: an fp16-pair activation (PairAct) can only feed a conv")
     return t.contiguous()
 
 
@@ -191,7 +188,7 @@ def gather_images(src, labels, idx, trig_masks, trig_id, poison_n, target, flip_
     _call("dba_gather_images", src.data_ptr(), _i32(labels).data_ptr(), idx.data_ptr(),
           trig_masks.contiguous().data_ptr(), trig_id.data_ptr(), poison_n.data_ptr(), int(target), _ptr(fs),
           x.data_ptr(), int(out_dtype == torch.float32), y.data_ptr(), G, B, H, W, C, _stream())
-    if _MODE == F16_PAIR and out_dtype == _F32:
+    if out_dtype == _F32:
         x._dba_amax = _unit_amax(G, x.device)   # an upper bound is all the scale needs
     return x, y
 
@@ -240,63 +237,15 @@ def _check_w(w: Tensor, dt: torch.dtype = _F32) -> Tuple[Tensor, int]:
     return _rowview(w)
 
 
-F16_PAIR = 16
-# which conv passes take the fp16 pair in F16_PAIR mode (DBA_F32_H_OPS / DBA_F32_TRAIN_H_OPS; the
-# others take 3 bf16 planes).  Every pass takes the pair by default: against the fp64 oracle
-# with the device's near-tie branches replayed (ops/branches.py), the smoke step's gradient error
-# is 1.63e-6 with the pair in the training forward vs 1.83e-6 with 3 bf16 planes there
-# (torch-fp32 under the same replay: 1.62e-6; profiles/split_policy_r3.md) — the 6-MFMA forward
-# of round 2 was chosen on an oracle without branch matching and buys nothing.
-_H_OPS = set(os.environ.get("DBA_F32_H_OPS", "fwd,dgrad,wgrad").split(","))
-TRAIN_H_OPS = tuple(os.environ.get("DBA_F32_TRAIN_H_OPS", "fwd,dgrad,wgrad").split(","))
-
-
-def set_fp32_planes(planes: int) -> int:
-    """Operand split of the fp32 family (csrc/kernels/xgemm.hip): 3 bf16 planes (6 MFMAs per
-    product), 16 = the scaled fp16 pair (3 MFMAs, 11 significant bits per plane), both at
-    fp32-level error; or 2 bf16 planes (3 MFMAs, ~4e-6 relative).  Returns the previous
-    setting."""
-    global _MODE
-    if planes not in (2, 3, F16_PAIR):
-        raise ValueError("fp32 split mode must be 2, 3 (bf16 planes) or 16 (fp16 pair)")
-    prev = int(_L.dba_xgemm_set_planes(int(planes)))
-    _MODE = int(planes)
-    return prev
-
-
-def set_halo_ws(on: int) -> int:
-    """Persistent weight-stationary stage-1 halo conv (xgemm.hip xhalo_ws_kernel) on / off;
-    -1 queries.  Returns the previous setting."""
-    return int(_L.dba_xhalo_ws_set(int(on)))
-
-
 def set_ximg(on: int) -> int:
     """Whole-image halo conv of the 8 / 4-wide evaluation stages (xgemm.hip ximg_kernel) on /
-    off; -1 queries.  Returns the previous setting."""
+    off; -1 queries.  Returns the previous setting (tests: A/B against the implicit GEMM)."""
     return int(_L.dba_ximg_set(int(on)))
 
 
 def fp32_mode() -> int:
-    return _MODE
-
-
-@contextlib.contextmanager
-def fp32_split(mode: Optional[int], h_ops: Optional[Sequence[str]] = None):
-    """Run the enclosed op launches (host-side: kernel choice happens at launch, so a HIP graph
-    captured inside keeps it) with split mode ``mode`` (None: unchanged) and, in F16_PAIR mode,
-    the fp16 pair on the conv passes ``h_ops`` only (None: unchanged; the others take 3 bf16
-    planes)."""
-    global _H_OPS
-    prev_ops = _H_OPS
-    if h_ops is not None:
-        _H_OPS = set(h_ops)
-    prev = set_fp32_planes(mode) if (mode is not None and mode != _MODE) else None
-    try:
-        yield
-    finally:
-        if prev is not None:
-            set_fp32_planes(prev)
-        _H_OPS = prev_ops
+    """The fp32 family's operand split (one since round 5: the scaled fp16 pair)."""
+    return F16_PAIR
 
 
 # ---- operand max |x| slots of the fp16 pair (csrc/kernels/common.hpp): int32 [16, ld]
@@ -339,11 +288,8 @@ _ARENA: list = []
 
 @contextlib.contextmanager
 def amax_arena(G: int, device, n: int = 256, counters: int = 0):
-    """Slots for the enclosed launches' fp16-pair operand maxima (fp16-pair mode only), and
-    ``counters`` zeroed ints for their in-launch split-K combines (:func:`_sk_counters`)."""
-    if _MODE != F16_PAIR:
-        yield
-        return
+    """Slots for the enclosed launches' fp16-pair operand maxima, and ``counters`` zeroed ints
+    for their in-launch split-K combines (:func:`_sk_counters`)."""
     _ARENA.append(_AmaxArena(G, device, n, counters))
     try:
         yield
@@ -381,9 +327,9 @@ def _amax(t, gstride, n_per_g, nvalid=None, per_item=0):
 
 
 def _amax_out(t):
-    """Zeroed slot for a producer to fold its fp32 output's max into (fp16-pair mode only),
-    attached to ``t`` for its consumers."""
-    if _MODE != F16_PAIR or t.dtype != _F32:
+    """Zeroed slot for a producer to fold its fp32 output's max into, attached to ``t`` for its
+    consumers."""
+    if t.dtype != _F32:
         return None
     a = _amax_new(t.shape[0], t.device)
     t._dba_amax = a
@@ -418,9 +364,9 @@ def split_weights(w, sstride: int, per: int, amax):
 
 
 def _wplanes(w):
-    """(pointer, slot stride) of ``w``'s fp16-pair planes, if split (fp16-pair launches only)."""
+    """(pointer, slot stride) of ``w``'s fp16-pair planes, if split."""
     p = getattr(w, "_dba_planes", None)
-    return (None, 0) if p is None or _MODE != F16_PAIR else (p.data_ptr(), p.stride(0))
+    return (None, 0) if p is None else (p.data_ptr(), p.stride(0))
 
 
 def _amax_w(w, gstride, n):
@@ -437,42 +383,20 @@ def _amax_act(t, nvalid):
     a = getattr(t, "_dba_amax", None)
     if a is not None:
         return a
-    if getattr(t, "_dba_pair", None) is not None:
-        raise RuntimeError("fp16-pair activation without its producer's max slot")
     per_item = t[0, 0].numel()
     a = _amax(t, t.stride(0), t.shape[1] * per_item, nvalid, per_item)
     t._dba_amax = a   # activations are never written in place: the fwd / wgrad pair shares it
     return a
 
 
-def decode_pairs(t: Tensor) -> Tensor:
-    """fp32 values of an fp16-pair activation (PairAct layout: every 4 channels = 4 fp16 hi +
-    4 fp16 lo of x * 2^s[g]) — for oracles and diagnostics; the kernels decode in-register."""
-    sexp = _pair_sexp(t)
-    if sexp is None:
-        return t
-    G, C = t.shape[0], t.shape[-1]
-    h = t.contiguous().view(torch.float16).reshape(*t.shape[:-1], C // 4, 2, 4).float()
-    v = (h[..., 0, :] + h[..., 1, :]).reshape(t.shape)
-    scale = torch.exp2(-sexp.to(torch.float32)).view(G, *([1] * (t.dim() - 1)))
-    return v * scale
-
-
-def _pair_sexp(t):
-    """The per-replica scale exponents of an fp16-pair activation (PairAct), else None."""
-    return getattr(t, "_dba_pair", None)
-
-
-def _xconv_fwd(x, w, wsel, stride, pad, bias, residual, relu, nvalid, out_dtype, out_pairs=False, bnf=None, lz=None):
-    """Reference-precision conv (fp32 in / fp32 out, split MFMA: xgemm.hip).  ``bnf``: the
+def _xconv_fwd(x, w, wsel, stride, pad, bias, residual, relu, nvalid, out_dtype, bnf=None, lz=None):
+    """Reference-precision conv (fp32 in / fp32 out, fp16-pair MFMA: xgemm.hip).  ``bnf``: the
     fused training-BN statistics of the output (bnfuse.hpp); ``lz``: the input is a lazy BN
     output (its coefficients, ReLU, bound slot)."""
     if out_dtype not in (None, _F32):
         raise TypeError(f"fp32 conv cannot emit {out_dtype} (no silent precision conversion)")
     G, N, H, W, Cin = x.shape
-    if out_pairs and getattr(w, "_dba_bound", None) is None and getattr(w, "_dba_bound_src", None) is not None:
-        w._dba_bound = row_bound(w, w._dba_bound_src)   # PairAct output bound, on first use
-    attrs = {k: getattr(w, k) for k in ("_dba_amax", "_dba_planes", "_dba_bound") if hasattr(w, k)}
+    attrs = {k: getattr(w, k) for k in ("_dba_amax", "_dba_planes") if hasattr(w, k)}
     w, ws = _check_w(w, _F32)
     for k, v in attrs.items():
         setattr(w, k, v)
@@ -487,50 +411,27 @@ def _xconv_fwd(x, w, wsel, stride, pad, bias, residual, relu, nvalid, out_dtype,
             raise TypeError(f"conv bias must be fp32 (got {bias.dtype})")
         bias, bs = _rowview(bias)
     res = _act(residual, _F32, "residual") if residual is not None else None
+    ay = _amax_out(y) if bnf is None else None   # the output's max, for its consumers
+    bnf_p = ctypes.byref(bnf) if bnf is not None else None
+    if Cin <= 4:
+        # few-channel image stems: exact-fp32 direct conv (stem.hip), -100 = not a stem shape
+        rc = _call("dba_xstem_fwd", x.data_ptr(), N * H * W * Cin, w.data_ptr(), ws, _ptr(_i32(wsel)), _ptr(bias), bs,
+                   _ptr(res), y.data_ptr(), N * Ho * Wo * Cout, _ptr(_i32(nvalid)), G, N, H, W, Cin, Ho, Wo, Cout,
+                   KH, KW, stride, pad, int(relu), *_aptr(ay), bnf_p, _stream())
+        if rc != NOT_HANDLED:
+            return y
     n = int(_L.dba_xconv_ws_floats(G, N, Ho, Wo, Cin, Cout, KH, KW))
     wsb = torch.empty(n, dtype=_F32, device=x.device) if n > 0 else None
     # split-K launch: slabs combined in the launch when the arena has counters for it
     ncnt = int(_L.dba_xconv_sk_ints(G, N, Ho, Wo, Cin, Cout, KH, KW)) if n > 0 else 0
     cnt = _sk_counters(ncnt, x.device)
-    ax = aw = ay = None
-    if _MODE == F16_PAIR and "fwd" in _H_OPS:
-        ax = lz[2] if lz is not None else _amax_act(x, nvalid)
-        aw = _amax_w(w, ws, Cout * KH * KW * Cin)
-        if bnf is None:
-            ay = _amax_out(y)   # the output's max, for its consumers
-    elif lz is not None or bnf is not None:
-        raise RuntimeError("fused training BN needs the fp16-pair forward (F16_PAIR, 'fwd' in the H ops)")
-    bnf_p = ctypes.byref(bnf) if bnf is not None else None
+    ax = lz[2] if lz is not None else _amax_act(x, nvalid)
+    aw = _amax_w(w, ws, Cout * KH * KW * Cin)
     lz_coef, lz_relu = (lz[0].data_ptr(), int(lz[1])) if lz is not None else (None, 0)
-    # fp16-pair activations (xgemm.hip PairAct; evaluation forwards with pre-split weights):
-    # the input may arrive split, the output may leave split; every user of such a tensor is a
-    # conv of this family (A operand or residual)
-    in_sexp, res_sexp = _pair_sexp(x), (_pair_sexp(residual) if residual is not None else None)
-    pairs_ok = (ax is not None and getattr(w, "_dba_planes", None) is not None and Cin % 4 == 0 and bnf is None)
-    if (in_sexp is not None or res_sexp is not None) and not pairs_ok:
-        raise RuntimeError("fp16-pair activation fed to a conv outside the evaluation pair path")
-    out_sexp = None
-    if out_pairs and pairs_ok and Cout % 4 == 0 and getattr(w, "_dba_bound", None) is not None:
-        out_sexp = torch.empty(G, dtype=torch.int32, device=x.device)   # every block with rows writes it
-    bound = getattr(w, "_dba_bound", None)
-    ares = _amax_act(residual, nvalid) if (residual is not None and out_sexp is not None) else None
-    if Cin <= 4 and out_dtype in (None, _F32):
-        # few-channel image stems: exact-fp32 direct conv (stem.hip), -100 = not a stem shape
-        rc = _call("dba_xstem_fwd", x.data_ptr(), N * H * W * Cin, w.data_ptr(), ws, _ptr(_i32(wsel)), _ptr(bias), bs,
-                   _ptr(res), y.data_ptr(), N * Ho * Wo * Cout, _ptr(_i32(nvalid)), G, N, H, W, Cin, Ho, Wo, Cout,
-                   KH, KW, stride, pad, int(relu), *_aptr(ay), *_aptr(ax if out_sexp is not None else None),
-                   _ptr(out_sexp), _ptr(bound if out_sexp is not None else None), bnf_p, _stream())
-        if rc != NOT_HANDLED:
-            if out_sexp is not None:
-                y._dba_pair = out_sexp
-            return y
     _call("dba_xconv_fwd", x.data_ptr(), N * H * W * Cin, w.data_ptr(), ws, _ptr(_i32(wsel)), _ptr(bias), bs,
           _ptr(res), y.data_ptr(), N * Ho * Wo * Cout, _ptr(_i32(nvalid)), G, N, H, W, Cin, Ho, Wo, Cout, KH, KW,
           stride, pad, int(relu), *_aptr(ax), *_aptr(aw), *_aptr(ay), *_wplanes(w), _ptr(wsb), n,
-          _ptr(in_sexp), _ptr(out_sexp), _ptr(bound if out_sexp is not None else None), *_aptr(ares), _ptr(res_sexp),
           _ptr(cnt), 0 if cnt is None else cnt.numel(), bnf_p, lz_coef, lz_relu, _stream())
-    if out_sexp is not None:
-        y._dba_pair = out_sexp
     return y
 
 
@@ -543,11 +444,10 @@ _BLOCK_SHAPES = {(32, 32)}
 
 
 def basic_block_ok(x, w1, w2) -> bool:
-    """The fused evaluation BasicBlock (csrc/kernels/xblock.hip) takes this block: fp16-pair
-    forwards, fp32 [G, N, W, W, C] input (not PairAct) of a CIFAR ResNet stage, C -> C 3x3
-    weights pre-split at the eval fold.  ``DBA_EVAL_BLOCK=0``: off (the two convs run)."""
-    if not (_EVAL_BLOCK and _MODE == F16_PAIR and "fwd" in _H_OPS and x.dtype == _F32 and x.dim() == 5
-            and _pair_sexp(x) is None):
+    """The fused evaluation BasicBlock (csrc/kernels/xblock.hip) takes this block: fp32
+    [G, N, W, W, C] input of a CIFAR ResNet stage, C -> C 3x3 weights pre-split at the eval fold.
+    ``DBA_EVAL_BLOCK=0``: off (the two convs run; the A/B of profiles/r4/xblock/)."""
+    if not (_EVAL_BLOCK and x.dtype == _F32 and x.dim() == 5):
         return False
     H, W, C = x.shape[2:]
     return (H == W and (W, C) in _BLOCK_SHAPES
@@ -585,8 +485,7 @@ def stem_block_ok(x, w0, w1, w2) -> bool:
     """The stem + first BasicBlock of the 32-wide stage run as one launch (xblock.hip STEM
     variant): [G, N, 32, 32, 3] fp32 images, a 3x3 3 -> 32 stem and the block's weights all
     pre-split at the eval fold.  ``DBA_EVAL_STEM=0``: off (stem launch + fused block)."""
-    if not (_EVAL_STEM and _EVAL_BLOCK and _MODE == F16_PAIR and "fwd" in _H_OPS and x.dtype == _F32
-            and x.dim() == 5 and tuple(x.shape[2:]) == (32, 32, 3)):
+    if not (_EVAL_STEM and _EVAL_BLOCK and x.dtype == _F32 and x.dim() == 5 and tuple(x.shape[2:]) == (32, 32, 3)):
         return False
     return (w0.dtype == _F32 and tuple(w0.shape[1:]) == (32, 3, 3, 3) and getattr(w0, "_dba_planes", None) is not None
             and all(w.dtype == _F32 and tuple(w.shape[1:]) == (32, 3, 3, 32)
@@ -619,16 +518,56 @@ def stem_block_eval(x, w0, b0, w1, b1, w2, b2, wsel=None, nvalid=None):
     return y
 
 
+def down_block_ok(a, w2, x2, wsc) -> bool:
+    """The downsampling block's conv2 + 1x1 stride-2 shortcut run as one launch (xgemm.hip
+    dba_xdown_fwd: the shortcut as extra k-steps of xhalo / ximg): fp32 [G, N, W, W, C] ``a`` at
+    W 16 (C 64, shortcut input 32 channels) or W 8 / 4 (C % 32 == 0, shortcut input C2 % 32 == 0,
+    <= 256), both weights pre-split at the eval fold.  ``DBA_EVAL_DOWN=0``: off (two launches)."""
+    if not (_EVAL_DOWN and a.dtype == _F32 and x2.dtype == _F32 and a.dim() == 5 and x2.dim() == 5):
+        return False
+    H, W, C = a.shape[2:]
+    H2, W2, C2 = x2.shape[2:]
+    if H != W or (H - 1) * 2 >= H2 or (W - 1) * 2 >= W2 or a.shape[:2] != x2.shape[:2]:
+        return False
+    if any(getattr(t, "_dba_planes", None) is None for t in (w2, wsc)):
+        return False
+    if tuple(w2.shape[1:]) != (C, 3, 3, C) or tuple(wsc.shape[1:]) != (C, 1, 1, C2):
+        return False
+    if W == 16:
+        return C == 64 and C2 == 32
+    return W in (8, 4) and C % 32 == 0 and C2 % 32 == 0 and C2 <= 256
+
+
+def down_block_eval(a, w2, b2, x2, wsc, bsc, wsel=None, nvalid=None):
+    """relu(conv3x3(a, w2) + b2 + conv1x1_s2(x2, wsc) + bsc) in one launch (BN folded); callers
+    check :func:`down_block_ok` first."""
+    a = _act(a, _F32, "conv input")
+    x2 = _act(x2, _F32, "shortcut input")
+    G, N, Ho, Wo, C = a.shape
+    _, _, H2, W2, C2 = x2.shape
+    (w2c, ws2), (wscc, wss) = _check_w(w2), _check_w(wsc)
+    aw2, awsc = _amax_w(w2, ws2, C * 9 * C), _amax_w(wsc, wss, C * C2)
+    p2, psc = w2._dba_planes, wsc._dba_planes
+    (b2c, bs2), (bscc, bss) = _rowview(b2), _rowview(bsc)
+    aa, ax2 = _amax_act(a, nvalid), _amax_act(x2, nvalid)
+    y = torch.empty_like(a)
+    ay = _amax_out(y)
+    rc = _call("dba_xdown_fwd", a.data_ptr(), a.stride(0), w2c.data_ptr(), ws2, p2.data_ptr(), p2.stride(0),
+               _ptr(_i32(wsel)), b2c.data_ptr(), bs2, x2.data_ptr(), x2.stride(0), psc.data_ptr(), psc.stride(0),
+               bscc.data_ptr(), bss, y.data_ptr(), y.stride(0), _ptr(_i32(nvalid)), G, N, Ho, Wo, C, H2, W2, C2,
+               *_aptr(aa), *_aptr(aw2), *_aptr(ax2), *_aptr(awsc), *_aptr(ay), _stream())
+    if rc == NOT_HANDLED:
+        raise RuntimeError("xdown_fwd declined a shape down_block_ok accepted")
+    return y
+
+
+_EVAL_DOWN = os.environ.get("DBA_EVAL_DOWN", "1") != "0"
+
+
 def conv2d(x, w, wsel, stride, pad, bias=None, residual=None, relu=False, nvalid=None, out_dtype=None,
-           bn_stats=False, out_pairs=False):
-    """``out_pairs``: the output may be emitted as fp16-pair activations (fp32 family,
-    evaluation with pre-split weights; y._dba_pair set) — only for outputs consumed by convs.
-    ``bn_stats`` is a reference-API hint (training BN goes through :func:`conv_bn_stats`)."""
-    sx = _pair_sexp(x)
-    x = _act(x, _F32, "conv input")
-    if sx is not None:
-        x._dba_pair = sx
-    return _xconv_fwd(x, w, wsel, stride, pad, bias, residual, relu, nvalid, out_dtype, out_pairs)
+           bn_stats=False):
+    """``bn_stats`` is a reference-API hint (training BN goes through :func:`conv_bn_stats`)."""
+    return _xconv_fwd(_act(x, _F32, "conv input"), w, wsel, stride, pad, bias, residual, relu, nvalid, out_dtype)
 
 
 def _xtranspose(items) -> list:
@@ -686,10 +625,8 @@ def _xconv_dgrad(dy, w, wsel, stride, pad, in_hw, nvalid, out_dtype, accum, wt, 
     n = int(_L.dba_xconv_ws_floats(G, N, H, W, Cout, Cin, KH, KW)) if stride == 1 else 0
     wsb = torch.empty(n, dtype=_F32, device=dy.device) if n > 0 else None
     cnt = _sk_counters(int(_L.dba_xconv_sk_ints(G, N, H, W, Cout, Cin, KH, KW)) if n > 0 else 0, dy.device)
-    ad = aw = None
-    if _MODE == F16_PAIR and "dgrad" in _H_OPS:
-        a0 = getattr(w, "_dba_amax", None)   # the forward weights' max is the transpose's
-        ad, aw = _amax_act(dy, nvalid), (a0 if a0 is not None else _amax(wt, per, per))
+    a0 = getattr(w, "_dba_amax", None)   # the forward weights' max is the transpose's
+    ad, aw = _amax_act(dy, nvalid), (a0 if a0 is not None else _amax(wt, per, per))
     bnf = _bnf_bwd(finish, G, N * H * W, dx.device) if (finish is not None and stride == 1) else None
     _call("dba_xconv_dgrad", dy.data_ptr(), N * Ho * Wo * Cout, wt.data_ptr(), per, _ptr(_i32(wsel)), _ptr(acc),
           dx.data_ptr(), N * H * W * Cin, _ptr(_i32(nvalid)), G, N, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad,
@@ -722,8 +659,6 @@ def conv2d_wgrad(dy, x, stride, pad, kh, kw, dw, dbias=None, nvalid=None, defer=
     lx = x if isinstance(x, bs.LazyBN) else None
     dy = _act(dy, _F32, "wgrad dy")
     x = _act(lx.y if lx is not None else x, _F32, "wgrad x")
-    if lx is not None and (_MODE != F16_PAIR or "wgrad" not in _H_OPS):
-        raise RuntimeError("fused training BN: fp16-pair weight gradient")
     G, N, Ho, Wo, Cout = dy.shape
     _, _, H, W, Cin = x.shape
     assert dw.dtype == torch.float32 and _inner_contig(dw)
@@ -731,10 +666,8 @@ def conv2d_wgrad(dy, x, stride, pad, kh, kw, dw, dbias=None, nvalid=None, defer=
     n = int(_L.dba_xwgrad_ws_floats(G, N, Ho, Wo, Cin, Cout, kh, kw, ctypes.byref(mchunk)))
     wsb = torch.empty(n, dtype=_F32, device=dy.device) if n > 0 else None
     nv = _i32(nvalid)
-    ad = ax = None
-    if _MODE == F16_PAIR and "wgrad" in _H_OPS:
-        ad = _amax_act(dy, nvalid)
-        ax = lx.stat.bound if lx is not None else _amax_act(x, nvalid)
+    ad = _amax_act(dy, nvalid)
+    ax = lx.stat.bound if lx is not None else _amax_act(x, nvalid)
     _call("dba_xwgrad", dy.data_ptr(), N * Ho * Wo * Cout, x.data_ptr(), N * H * W * Cin, dw.data_ptr(),
           dw.stride(0), _ptr(nv), G, N, H, W, Cin, Ho, Wo, Cout, kh, kw, stride, pad, *_aptr(ad), *_aptr(ax),
           _ptr(wsb), n, int(defer is not None and n > 0),
@@ -890,7 +823,7 @@ def wgrad_prepare(dy, x, nvalid=None):
     CURRENT stream.  Called before the weight gradient moves to the side stream
     (models/program.py): a max computed there would be read unordered by the data gradient,
     which runs on the main stream and shares ``dy``'s max slot."""
-    if _MODE == F16_PAIR and "wgrad" in _H_OPS and dy.dtype == _F32:
+    if dy.dtype == _F32:
         _amax_act(_act(dy, None, "wgrad dy"), nvalid)
         _amax_act(_act(x, _F32, "wgrad x"), nvalid)
 
@@ -938,26 +871,9 @@ def bn_fold(w, conv_bias, gamma, beta, rmean, rvar, eps, out_dtype):
     _call("dba_bn_fold", w.data_ptr(), w.stride(0), _ptr(cb), gamma.data_ptr(), beta.data_ptr(), rmean.data_ptr(),
           rvar.data_ptr(), ss, float(eps), wf.data_ptr(), bf.data_ptr(), slots, Cout, K, int(out_dtype == _F32),
           _stream())
-    if out_dtype == _F32:
-        wf._dba_amax = _amax(wf, Cout * K, Cout * K)   # the folded weights' scale, once per fold
-        if _MODE == F16_PAIR:
-            split_weights(wf, Cout * K, Cout * K, wf._dba_amax)   # and their fp16 planes
-            # output bound of fp16-pair activations (PairAct, opt-in): computed on first use
-            # (one row_bound launch per conv per fold cost ~1.4 % of the eval kernel time)
-            wf._dba_bound_src = bf
+    wf._dba_amax = _amax(wf, Cout * K, Cout * K)   # the folded weights' scale, once per fold
+    split_weights(wf, Cout * K, Cout * K, wf._dba_amax)   # and their fp16 planes
     return wf, bf
-
-
-def row_bound(w, bias):
-    """[slots, 2] fp32 {max row L1 of w, max |bias|} per weight slot (xgemm.hip row_bound_kernel):
-    the output bound that fixes an evaluation conv's fp16-pair output scale before it runs."""
-    slots, Cout = w.shape[0], w.shape[1]
-    per = w[0].numel()
-    wv, ws = _rowview(w)
-    out = torch.zeros(slots, 2, dtype=torch.float32, device=w.device)   # atomic-max target
-    bv, bs = _rowview(bias) if bias is not None else (None, 0)
-    _call("dba_row_bound", wv.data_ptr(), ws, Cout, per // Cout, _ptr(bv), bs, slots, out.data_ptr(), _stream())
-    return out
 
 
 # --------------------------------------------------------------------------- pooling

@@ -114,10 +114,9 @@ def gather_rows(src: Tensor, labels: Tensor, idx: Tensor, trig_cols: Tensor, tri
 def conv2d(x: Tensor, w: Tensor, wsel: Optional[Tensor], stride: int, pad: int,
            bias: Optional[Tensor] = None, residual: Optional[Tensor] = None,
            relu: bool = False, nvalid: Optional[Tensor] = None,
-           out_dtype: Optional[torch.dtype] = None, bn_stats: bool = False, out_pairs: bool = False) -> Tensor:
+           out_dtype: Optional[torch.dtype] = None, bn_stats: bool = False) -> Tensor:
     """y = act(conv(x, w) + bias + residual); NHWC in/out (K1, K3, K4, K8).  ``bn_stats`` (a
-    hint that y feeds a training BN) and ``out_pairs`` (y may be stored as fp16-pair
-    activations) only matter to the HIP backend."""
+    hint that y feeds a training BN) only matters to the HIP backend."""
     G = x.shape[0]
     outs = []
     for g in range(G):
@@ -161,6 +160,20 @@ def stem_block_eval(x: Tensor, w0: Tensor, b0: Tensor, w1: Tensor, b1: Tensor, w
     BasicBlock of :func:`basic_block_eval`, BN folded (reference models/resnet_cifar.py:80-88)."""
     s = conv2d(x, w0, wsel, 1, 1, bias=b0, relu=True, nvalid=nvalid)
     return basic_block_eval(s, w1, b1, w2, b2, wsel, nvalid)
+
+
+def down_block_ok(a: Tensor, w2: Tensor, x2: Tensor, wsc: Tensor) -> bool:
+    """Whether the backend runs a downsampling block's conv2 with its 1x1 stride-2 shortcut as
+    one fused op (HIP: xgemm.hip dba_xdown_fwd); the reference runs the two convs."""
+    return False
+
+
+def down_block_eval(a: Tensor, w2: Tensor, b2: Tensor, x2: Tensor, wsc: Tensor, bsc: Tensor,
+                    wsel: Optional[Tensor] = None, nvalid: Optional[Tensor] = None) -> Tensor:
+    """relu(conv3x3(a, w2) + b2 + conv1x1_s2(x2, wsc) + bsc), BN folded: the second half of a
+    downsampling BasicBlock with its shortcut (reference models/resnet_cifar.py:24-36), evaluated."""
+    sc = conv2d(x2, wsc, wsel, 2, 0, bias=bsc, nvalid=nvalid)
+    return conv2d(a, w2, wsel, 1, 1, bias=b2, residual=sc, relu=True, nvalid=nvalid)
 
 
 def _valid_mask(t: Tensor, nvalid: Optional[Tensor]) -> Tensor:

@@ -68,7 +68,7 @@ def _time(fn, reps, inner=10):
 
 
 def _bench_fp32(name, G, N, Hh, Cin, Cout, k, s, p, reps, dev):
-    """fwd / dgrad / wgrad of the split-bf16 fp32 family; TFLOP/s counts the real fp32 work."""
+    """fwd / dgrad / wgrad of the fp16-pair fp32 family; TFLOP/s counts the real fp32 work."""
     torch.manual_seed(0)
     x = torch.randn(G, N, Hh, Hh, Cin, device=dev)
     w = torch.randn(G, Cout, k, k, Cin, device=dev) * 0.05
@@ -76,21 +76,13 @@ def _bench_fp32(name, G, N, Hh, Cin, Cout, k, s, p, reps, dev):
     dy = torch.randn(G, N, Ho, Ho, Cout, device=dev)
     flops = 2.0 * G * N * Ho * Ho * Cout * k * k * Cin
     rec = {"shape": name, "dtype": "fp32"}
-    if name.startswith("eval") and H.fp32_mode() == H.F16_PAIR:
+    if name.startswith("eval"):
         # evaluation weights are static: split into fp16-pair planes once (as bn_fold does)
         per = Cout * k * k * Cin
         H.split_weights(w, per, per, H._amax_w(w, per, per))
     ops = [("fwd", lambda: H.conv2d(x, w, None, s, p, relu=True))]
-    if name.startswith("eval") and H.fp32_mode() == H.F16_PAIR and Cin == Cout and Cin % 4 == 0 and s == 1:
-        # fp16-pair activations in and out (ops.hip PairAct): the input is a pair tensor made by a
-        # producer conv of the same shape
-        w._dba_bound = H.row_bound(w, None)
-        x._dba_amax = H._amax_act(x, None)
-        xp = H.conv2d(x, w, None, s, p, relu=True, out_pairs=True)
-        assert getattr(xp, "_dba_pair", None) is not None
-        ops.append(("fwd_pairs", lambda: H.conv2d(xp, w, None, s, p, relu=True, out_pairs=True)))
     block_flops = None
-    if name.startswith("eval") and H.fp32_mode() == H.F16_PAIR and H.basic_block_ok(x, w, w):
+    if name.startswith("eval") and H.basic_block_ok(x, w, w):
         # the whole identity BasicBlock (two convs, the mid activation in LDS: xblock.hip); its
         # TFLOP/s counts both convs' fp32 work
         xb = torch.relu(x)
@@ -100,7 +92,7 @@ def _bench_fp32(name, G, N, Hh, Cin, Cout, k, s, p, reps, dev):
         xb._dba_amax = H._amax_act(xb, None)
         block_flops = 2 * flops
         ops.append(("block", lambda: H.basic_block_eval(xb, w, b1, w2, b2)))
-    if name == "eval.stem" and H.fp32_mode() == H.F16_PAIR:
+    if name == "eval.stem":
         # the stem + layer1.0 (xblock.hip STEM variant) vs the stem launch + fused block; their
         # TFLOP/s count the stem's and both block convs' fp32 work
         wb = [torch.randn(G, 32, 3, 3, 32, device=dev) * 0.05 for _ in range(2)]
@@ -125,20 +117,80 @@ def _bench_fp32(name, G, N, Hh, Cin, Cout, k, s, p, reps, dev):
     return rec
 
 
+def _bench_down(name, G, N, W, C, C2, reps, dev):
+    """A downsampling block's conv2 + 1x1 stride-2 shortcut: fused (one launch, xgemm.hip
+    dba_xdown_fwd) vs the shortcut conv + conv2 with a residual epilogue; TFLOP/s counts both
+    convs' fp32 work."""
+    torch.manual_seed(0)
+    a = torch.relu(torch.randn(G, N, W, W, C, device=dev))
+    x2 = torch.relu(torch.randn(G, N, 2 * W, 2 * W, C2, device=dev))
+    w2 = torch.randn(G, C, 3, 3, C, device=dev) * 0.03
+    wsc = torch.randn(G, C, 1, 1, C2, device=dev) * 0.1
+    for w in (w2, wsc):
+        per = w[0].numel()
+        H.split_weights(w, per, per, H._amax_w(w, per, per))
+    b2, bsc = torch.randn(G, C, device=dev) * 0.1, torch.randn(G, C, device=dev) * 0.1
+    a._dba_amax, x2._dba_amax = H._amax_act(a, None), H._amax_act(x2, None)
+    flops = 2.0 * G * N * W * W * C * (9 * C + C2)
+    rec = {"shape": name, "dtype": "fp32"}
+    ops = [("fused", lambda: H.down_block_eval(a, w2, b2, x2, wsc, bsc)),
+           ("two", lambda: H.conv2d(a, w2, None, 1, 1, bias=b2, relu=True,
+                                    residual=H.conv2d(x2, wsc, None, 2, 0, bias=bsc)))]
+    for tag, fn in ops:
+        t = _time(fn, reps)
+        rec[tag + "_us"] = round(t * 1e6, 1)
+        rec[tag + "_tflops"] = round(flops / t / 1e12, 1)
+    return rec
+
+
+def _bench_eval_chunk(G, N, reps, dev):
+    """The whole BN-folded CIFAR ResNet-18 evaluation forward of G models x N images (the
+    evaluator's chunk: 17 x 1024), through the model program as the round runs it."""
+    from dba_mod_amd.models import program as P
+    from dba_mod_amd.models.spec import get_spec
+    spec = get_spec("resnet18_cifar")
+    torch.manual_seed(0)
+    bank = torch.stack([spec.init_flat(i) for i in range(G)]).to(dev)
+    bank[:, spec.P:] += 0.05 * torch.rand_like(bank[:, spec.P:])
+    folded = P.fold_bank(spec, bank, torch.float32)
+    x = torch.rand(G, N, 32, 32, 3, device=dev)
+    x._dba_amax = H._unit_amax(G, dev)
+    sel = torch.arange(G, dtype=torch.int32, device=dev)
+    nval = torch.full((G,), N, dtype=torch.int32, device=dev)
+
+    def fwd():
+        ctx = P.Ctx(spec, None, None, sel, train=False, folded=folded, nvalid=nval, act_dtype=torch.float32)
+        with H.amax_arena(G, dev):
+            return P.forward(ctx, x)
+
+    t = _time(fwd, reps, inner=1)
+    return {"shape": f"eval.chunk.{G}x{N}", "dtype": "fp32", "fwd_ms": round(t * 1e3, 3),
+            "fwd_tflops": round(G * N * 17.83e9 / 64 / t / 1e12, 1)}
+
+
+DOWN = [("eval.l2.0.down", 17, 1024, 16, 64, 32), ("eval.l3.0.down", 17, 1024, 8, 128, 64),
+        ("eval.l4.0.down", 17, 1024, 4, 256, 128)]
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--json", default=None)
     ap.add_argument("--only", default="", help="substring filter on shape names")
-    ap.add_argument("--planes", type=int, default=16, help="fp32 split: 2 / 3 bf16 planes or 16 (fp16 pair)")
     args = ap.parse_args(argv)
     dev = torch.device("cuda")
     rows = []
-    H.set_fp32_planes(args.planes)
     for name, G, N, Hh, Cin, Cout, k, s, p in SHAPES:
         if args.only not in name:
             continue
         rows.append(_bench_fp32(name, G, N, Hh, Cin, Cout, k, s, p, args.reps, dev))
+        print(json.dumps(rows[-1]), flush=True)
+    for name, G, N, W, C, C2 in DOWN:
+        if args.only in name:
+            rows.append(_bench_down(name, G, N, W, C, C2, args.reps, dev))
+            print(json.dumps(rows[-1]), flush=True)
+    if args.only in "eval.chunk":
+        rows.append(_bench_eval_chunk(17, 1024, max(3, args.reps // 4), dev))
         print(json.dumps(rows[-1]), flush=True)
     if args.json:
         with open(args.json, "w") as f:

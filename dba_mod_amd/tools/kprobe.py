@@ -17,7 +17,6 @@ from dba_mod_amd.ops import hip as H
 def _bn_probe(name: str, dev) -> None:
     Hh, C = {"bn1": (32, 32), "bn2": (16, 64), "bn3": (8, 128)}[name]
     G, N = 10, 64
-    H.set_fp32_planes(H.F16_PAIR)
     x = torch.randn(G, N, Hh, Hh, C, device=dev)
     w = torch.randn(G, C, 3, 3, C, device=dev) * (1.0 / (9 * C) ** 0.5)
     per = C * 9 * C
@@ -44,7 +43,6 @@ def main() -> int:
             # fp32-family forward of a bench_kernels shape (e.g. f32:eval.layer1), 3 calls
             from dba_mod_amd.tools.bench_kernels import SHAPES
             _, G, N, Hh, Cin, Cout, k, s, p = next(r for r in SHAPES if r[0] == name[4:])
-            H.set_fp32_planes(H.F16_PAIR)
             x = torch.randn(G, N, Hh, Hh, Cin, device=dev)
             w = torch.randn(G, Cout, k, k, Cin, device=dev) * 0.05
             per = Cout * k * k * Cin

@@ -51,13 +51,11 @@ def _step(device: torch.device, dtype: torch.dtype, impl, G: int, N: int, seed: 
         elif impl is not ops:
             setattr(ops, k, getattr(impl, k))
     try:
-        # the training step under the trainer's split policy (fl/trainer.py)
-        with ops.fp32_split(device, None, ops.train_h_ops(device) if impl is ops else None):
-            x, y = ops.gather_images(src, labels, idx, masks, trig, pn, 2, None, dtype)
-            ctx = prog.Ctx(spec, state, state, None, train=True, grads=grads, nvalid=nvalid, act_dtype=dtype)
-            logits = prog.forward(ctx, x)
-            loss, correct, dl = ops.softmax_xent(logits, y, True, True, grad_dtype=dtype)
-            ctx.tape.backward(logits, dl)
+        x, y = ops.gather_images(src, labels, idx, masks, trig, pn, 2, None, dtype)
+        ctx = prog.Ctx(spec, state, state, None, train=True, grads=grads, nvalid=nvalid, act_dtype=dtype)
+        logits = prog.forward(ctx, x)
+        loss, correct, dl = ops.softmax_xent(logits, y, True, True, grad_dtype=dtype)
+        ctx.tape.backward(logits, dl)
         g0 = grads.clone()
         lr = torch.full((G,), 0.1, device=device, dtype=torch.float32)
         one = torch.ones(G, dtype=torch.int32, device=device)

@@ -44,8 +44,7 @@ def main(arch, shp, fills, N=16):
         return loss, grads, state
 
     br = BranchReplay(nval)
-    with hip.fp32_split(hip.F16_PAIR):
-        lh, gh, sh = run(hip, torch.device("cuda"), torch.float32, br.wrap(hip))
+    lh, gh, sh = run(hip, torch.device("cuda"), torch.float32, br.wrap(hip))
     br.start_replay()
     R.COMPUTE_DTYPE = torch.float64
     lr_, gr, sr = run(R, torch.device("cpu"), torch.float64, br.wrap(R))

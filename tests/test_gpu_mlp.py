@@ -78,3 +78,18 @@ def test_persistent_is_deterministic(dev, tmp_path):
         for k in a[name].snapshots:
             assert torch.equal(a[name].snapshots[k], b[name].snapshots[k]), (name, k)
         assert np.array_equal(a[name].stats, b[name].stats)
+
+
+def test_other_batch_size_falls_back(dev, tmp_path):
+    """A LOAN run with a batch size the persistent kernel does not take (it is built for the
+    reference's 64) trains on the per-step graph path instead of failing mid-round."""
+    from dba_mod_amd.fl.server import Server
+    from dba_mod_amd.parallel.dist import DistCtx
+    s = Server(_params(tmp_path, batch_size=32), DistCtx(device=dev), write_outputs=False)
+    assert s.trainer.persistent
+    st = s._train_begin(12)
+    res = st["handle"].collect()
+    assert not s.trainer.persistent and res
+    for r in res:
+        for v in r.snapshots.values():
+            assert torch.isfinite(v).all()

@@ -20,9 +20,7 @@ def H():
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     from dba_mod_amd.ops import hip
-    prev = hip.set_fp32_planes(16)   # the step's mode: the arena (and its counters) exists
     yield hip
-    hip.set_fp32_planes(prev)
 
 
 SHAPES = [

@@ -22,9 +22,7 @@ def H():
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     from dba_mod_amd.ops import hip
-    prev = hip.set_fp32_planes(hip.F16_PAIR)
     yield hip
-    hip.set_fp32_planes(prev)
 
 
 @pytest.fixture()
