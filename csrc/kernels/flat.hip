@@ -88,6 +88,28 @@ __global__ void wsum_kernel(const float* __restrict__ pts, long long p_rstride, 
   }
 }
 
+// Reproducible weighted sum (RFA's Weiszfeld average, FoolsGold's weighted gradient): every
+// product q = w_i * p_ik * 2^E is exact in fp64 (two fp32 factors, a power-of-two scale) and is
+// quantised ON ITS OWN onto a fixed two-limb grid, hi = floor(q), lo = floor((q - hi) * 2^53);
+// the limbs are summed as int64 — over the rank's clients here, then over ranks by an int64
+// all-reduce — which is exact and order-free, so the sum does not depend on which rank holds
+// which client (world-1 == world-N bits).  E is chosen by the caller so |q| <= 2^52 / n (no
+// overflow of either limb sum for n <= 512).  out: [2][n] int64 (hi sums, lo sums).
+__global__ void wsum_fixed_kernel(const float* __restrict__ pts, long long p_rstride, const float* __restrict__ w,
+                                  int npts, long long* __restrict__ out, long long n, double scale) {
+  for (long long k = blockIdx.x * (long long)blockDim.x + threadIdx.x; k < n; k += (long long)gridDim.x * blockDim.x) {
+    long long hs = 0, ls = 0;
+    for (int i = 0; i < npts; ++i) {
+      const double q = (double)w[i] * (double)pts[(long long)i * p_rstride + k] * scale;
+      const double hi = floor(q);
+      hs += (long long)hi;
+      ls += (long long)floor((q - hi) * 0x1p53);
+    }
+    out[k] = hs;
+    out[n + k] = ls;
+  }
+}
+
 // slab[z][i][j] = sum over k-chunk z of F[i][k] F[j][k]; one wave per 16x16 tile (f32 MFMA),
 // summed over z in order by gram_finalize (no atomics)
 __global__ __launch_bounds__(64) void gram_kernel(const float* __restrict__ F, long long f_rstride, int n, int d,
@@ -224,6 +246,14 @@ DBA_EXPORT int dba_weighted_sum(const float* pts, long long p_rstride, const flo
   else
     hipLaunchKernelGGL(wsum_kernel<float>, dim3(egrid(n)), dim3(256), 0, (hipStream_t)stream, pts, p_rstride, w, npts,
                        (float*)out, n);
+  DBA_LAUNCH_CHECK();
+}
+
+// out [2][n] int64: the fixed-point limb sums of sum_i w[i] * pts[i] (wsum_fixed_kernel); scale = 2^E
+DBA_EXPORT int dba_weighted_sum_fixed(const float* pts, long long p_rstride, const float* w, int npts, long long* out,
+                                      long long n, double scale, void* stream) {
+  hipLaunchKernelGGL(wsum_fixed_kernel, dim3(egrid(n)), dim3(256), 0, (hipStream_t)stream, pts, p_rstride, w, npts, out,
+                     n, scale);
   DBA_LAUNCH_CHECK();
 }
 

@@ -77,7 +77,7 @@ struct XArgs {
   BnFuse bf;
   const float* lz_coef;
   int lz_relu;
-  // fused downsampling shortcut (evaluation, ximg_kernel / xhalo_kernel SC): out += the 1x1
+  // fused downsampling shortcut (evaluation, xhalo_kernel SC): out += the 1x1
   // stride-2 conv of x2 [G][N][sc_H][sc_W][sc_C] with pre-split weights (sc_wp: per slot 2 planes
   // of Ncol x sc_C fp16) + its bias, as extra k-steps of the same accumulators
   const float* sc_src; long long sc_gstride;
@@ -551,7 +551,7 @@ __global__ __launch_bounds__(256, KS ? 2 : XCONV_MINB) void xconv_kernel(const X
 // (32 input channels: one k-step) runs after the 18 3x3 steps from its own LDS tile
 // (x2[2h][2w] of the block's 128 output pixels, loaded and split at the start), with its own
 // fp16 scales (the accumulators are rescaled once, exactly) and pre-split weights; its output is
-// never written or read back as a residual (ximg_kernel SC: the same scheme).
+// never written or read back as a residual (reference models/resnet_cifar.py:24-36).
 template <int W, int CS, int BM, int BN, int WM, int WN, bool PRE = false, bool LZ = false, bool SC = false>
 __global__ __launch_bounds__(256) void xhalo_kernel(const XArgs a) {
   static_assert(!SC || (PRE && !LZ), "fused shortcut: evaluation, pre-split weights");
@@ -866,18 +866,14 @@ __global__ __launch_bounds__(256) void xhalo_kernel(const XArgs a) {
 // exposes its prologue / epilogue: eval.layer3 254 vs 314 TF, profiles/r4/ximg/README.md.)
 // Weights: the two-stage register / LDS ring of xhalo_kernel.  Epilogue straight from the
 // accumulators (a 32-lane row is 32 consecutive output channels: 128-B segments).
-// SC (a downsampling block's conv2, evaluation): the block's 1x1 stride-2 shortcut conv runs as
-// sc_C / 32 more chunks of ONE tap each after the 3x3 chunks — chunk c's "patch" holds
-// x2[img][2h][2w][32 channels] at the interior pixels and the step reads it at the centre tap,
-// the weights come from the shortcut's pre-split planes — so the shortcut's output is never
-// written or read back as a residual (reference: models/resnet_cifar.py:24-36).  Its operands
-// carry their own fp16 scales: the accumulators are rescaled by 2^(s_sc - s_main) (exact) before
-// the first shortcut step, and its folded bias is added with conv2's in the epilogue.
+// (A fused downsampling shortcut as extra one-tap chunks — each refilling the patch, its loads
+// prefetched only two k-steps ahead — measured slower than the shortcut conv + this kernel with a
+// residual epilogue: 17 x 1024 images, layer3.0 1534 vs 1467 us, layer4.0 1370 vs 1142 us,
+// profiles/r5/down/kbench_ximg_sc.log; the W-16 halo kernel's fused form wins: xhalo_kernel SC.)
 // Deterministic; the chunk-major k order makes its bits differ from the tap-major implicit
 // GEMM's (both fp32 level: tests hold both to the fp64 oracle).
-template <int W, int IMGS, int BN, int WM, int WN, bool PRE, bool SC = false>
+template <int W, int IMGS, int BN, int WM, int WN, bool PRE>
 __global__ __launch_bounds__(256) void ximg_kernel(const XArgs a) {
-  static_assert(!SC || PRE, "fused shortcut: pre-split weights (evaluation)");
   constexpr int P = 2, NT = 256;
   constexpr int PW = W + 2, PI = PW * PW, PP = IMGS * PI;   // padded pixels per image / patch
   constexpr int CC = 32, CH = CC / 8, Q4 = CC / 4;          // chunk channels, 16-B chunks, float4 per pixel
@@ -897,24 +893,18 @@ __global__ __launch_bounds__(256) void ximg_kernel(const XArgs a) {
   const int nv = min(valid_rows(a.nvalid, g, a.N), a.N);
   if (img0 >= nv) return;
   const int slot = a.wsel ? a.wsel[g] : g;
-  const int Cs = a.Cs, K = 9 * Cs, NC = Cs / CC;
-  const int NCT = NC + (SC ? a.sc_C / CC : 0);              // chunks: 3x3 ones, then the shortcut's
-  const int NK = 9 * NC + (NCT - NC);                       // k-steps
+  const int Cs = a.Cs, K = 9 * Cs, NC = Cs / CC, NK = 9 * NC;
   const float* __restrict__ src = a.src + (long long)g * a.src_gstride;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WN, wn = wid % WN;
   const int kq = tid & 7, r0 = tid >> 3;
   const int fr = lane & 31, hf = lane >> 5;
 
-  // ---- patch chunks: chunk cc of images img0 .. img0+IMGS-1, zero padding / invalid images;
-  // a shortcut chunk's interior pixel (h, w) holds x2[2h][2w] (its halo is never read)
+  // ---- patch chunks: chunk cc of images img0 .. img0+IMGS-1, zero padding / invalid images
   constexpr int NE = (PP * Q4 + NT - 1) / NT;
   float4 pv[NE];
   const __amdgpu_buffer_rsrc_t rA = rsrc(src, (long long)a.N * W * W * Cs * 4);
-  [[maybe_unused]] const __amdgpu_buffer_rsrc_t rS =
-      rsrc(SC ? a.sc_src + (long long)g * a.sc_gstride : nullptr, SC ? (long long)a.N * a.sc_H * a.sc_W * a.sc_C * 4 : 0);
   auto pload = [&](int cc) __attribute__((always_inline)) {
-    const bool sc = SC && cc >= NC;
 #pragma unroll
     for (int u = 0; u < NE; ++u) {
       const int e = tid + NT * u;
@@ -922,15 +912,10 @@ __global__ __launch_bounds__(256) void ximg_kernel(const XArgs a) {
       const int im = pp / PI, rem = pp - im * PI;
       const int h = rem / PW - 1, w = rem % PW - 1, img = img0 + im;
       const bool ok = e < PP * Q4 && img < nv && (unsigned)h < (unsigned)W && (unsigned)w < (unsigned)W;
-      if (sc)
-        pv[u] = bload4(rS, ok ? (((img * a.sc_H + 2 * h) * a.sc_W + 2 * w) * a.sc_C + (cc - NC) * CC + q * 4) * 4 : kOOB);
-      else
-        pv[u] = bload4(rA, ok ? (((img * W + h) * W + w) * Cs + cc * CC + q * 4) * 4 : kOOB);
+      pv[u] = bload4(rA, ok ? (((img * W + h) * W + w) * Cs + cc * CC + q * 4) * 4 : kOOB);
     }
   };
   HScale hs;
-  float ma_sc = 1.f;   // SC: the shortcut input's fill multiplier
-  int s_sc = 0;        //     and the shortcut products' accumulator exponent
   auto ppiece = [&](int u, float m) __attribute__((always_inline)) {   // piece u of pv -> the patch
     const int e = tid + NT * u;
     if (e >= PP * Q4) return;
@@ -944,7 +929,7 @@ __global__ __launch_bounds__(256) void ximg_kernel(const XArgs a) {
   };
 
   // ---- weights (pre-split planes, or fp32 split while staging: the same bits): two-stage
-  // pipeline, k-step t = chunk t / 9, tap t % 9 (shortcut step t >= 9 NC: chunk NC + t - 9 NC)
+  // pipeline, k-step t = chunk t / 9, tap t % 9
   int bn_[RB];
 #pragma unroll
   for (int j = 0; j < RB; ++j) {
@@ -955,19 +940,9 @@ __global__ __launch_bounds__(256) void ximg_kernel(const XArgs a) {
   const __amdgpu_buffer_rsrc_t rBh = rsrc(Bh, (long long)a.Ncol * K * 2);
   const __amdgpu_buffer_rsrc_t rBl = rsrc(PRE ? Bh + (a.wp_sstride >> 1) : nullptr, (long long)a.Ncol * K * 2);
   const __amdgpu_buffer_rsrc_t rB = rsrc(a.w + (long long)slot * a.w_sstride, (long long)a.Ncol * K * 4);
-  const uint16_t* Sh = SC ? a.sc_wp + (long long)slot * a.sc_wp_sstride : nullptr;
-  [[maybe_unused]] const __amdgpu_buffer_rsrc_t rSh = rsrc(Sh, SC ? (long long)a.Ncol * a.sc_C * 2 : 0);
-  [[maybe_unused]] const __amdgpu_buffer_rsrc_t rSl =
-      rsrc(SC ? Sh + (a.sc_wp_sstride >> 1) : nullptr, SC ? (long long)a.Ncol * a.sc_C * 2 : 0);
   uint4 rb[2][RB];
   auto gq = [&](int t, int st, int j) __attribute__((always_inline)) {
     const bool ok = bn_[j] >= 0 && t < NK;
-    if (SC && t >= 9 * NC) {
-      const int kb = bn_[j] * a.sc_C + (t - 9 * NC) * CC + kq * 4;
-      const uint2 h = bload8(rSh, ok ? kb * 2 : kOOB), l = bload8(rSl, ok ? kb * 2 : kOOB);
-      rb[st][j] = make_uint4(h.x, h.y, l.x, l.y);
-      return;
-    }
     const int cc = t / 9, tap = t - cc * 9;
     const int kb = bn_[j] * K + tap * Cs + cc * CC + kq * 4;
     if constexpr (PRE) {
@@ -1012,7 +987,7 @@ __global__ __launch_bounds__(256) void ximg_kernel(const XArgs a) {
   }
   // k-step t from weight buffer buf; fill: the weight ring's next step
   auto mma = [&](int t, int buf, int stn) __attribute__((always_inline)) {
-    const int tap = (SC && t >= 9 * NC) ? 4 : t % 9, ti = tap / 3, tj = tap - ti * 3;
+    const int tap = t % 9, ti = tap / 3, tj = tap - ti * 3;
     const int toff = ti * PW + tj;
     const uint4* L = bring + buf * P * BPL;
     sfor<2>([&](auto KK) __attribute__((always_inline)) {
@@ -1039,34 +1014,18 @@ __global__ __launch_bounds__(256) void ximg_kernel(const XArgs a) {
     });
   };
   auto step = [&](int t, int buf, int stn) __attribute__((always_inline)) {
-    const bool scs = SC && t >= 9 * NC;
-    const int c = scs ? NC + (t - 9 * NC) : t / 9;
-    if (SC && t == 9 * NC) {   // the shortcut's products accumulate at their own scale (exact)
-#pragma unroll
-      for (int i = 0; i < MI; ++i)
-#pragma unroll
-        for (int j = 0; j < NJ; ++j)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) acc[i][j][r] = ldexpf(acc[i][j][r], s_sc - hs.s);
-      hs.s = s_sc;
-    }
+    const int c = t / 9;
     mma(t, buf, stn);
     __syncthreads();
-    if ((scs || t - 9 * c == 8) && c + 1 < NCT) {   // the chunk's last k-step, another follows
-      const float m = (SC && c + 1 >= NC) ? ma_sc : hs.ma;
+    if (t - 9 * c == 8 && c + 1 < NC) {   // the chunk's last k-step, another follows
 #pragma unroll
-      for (int u = 0; u < NE; ++u) ppiece(u, m);   // every read of the old patch is done
-      if (c + 2 < NCT) pload(c + 2);
+      for (int u = 0; u < NE; ++u) ppiece(u, hs.ma);   // every read of the old patch is done
+      if (c + 2 < NC) pload(c + 2);
       __syncthreads();
     }
   };
 
   hs.init(amax_read(a.amax_src, a.amax_src_ld, g), amax_read(a.amax_w, a.amax_w_ld, slot));
-  if constexpr (SC) {
-    const int sx = hexp(amax_read(a.sc_amax_src, a.sc_amax_src_ld, g));
-    ma_sc = __uint_as_float((uint32_t)(sx + 127) << 23);
-    s_sc = sx + hexp(amax_read(a.sc_amax_w, a.sc_amax_w_ld, slot));
-  }
 #pragma unroll
   for (int q = 0; q < RB; ++q) {
     gq(0, 0, q);
@@ -1075,7 +1034,7 @@ __global__ __launch_bounds__(256) void ximg_kernel(const XArgs a) {
   pload(0);
 #pragma unroll
   for (int u = 0; u < NE; ++u) ppiece(u, hs.ma);
-  if (NCT > 1) pload(1);
+  if (NC > 1) pload(1);
 #pragma unroll
   for (int q = 0; q < RB; ++q) {
     lput_q(0, 0, q);
@@ -1090,17 +1049,16 @@ __global__ __launch_bounds__(256) void ximg_kernel(const XArgs a) {
   if (t < NK) step(t, 0, 1);
   hs.finish(acc);
 
-  // ---- epilogue from the accumulators: bias (+ the shortcut's), residual, ReLU, max
+  // ---- epilogue from the accumulators: bias, residual, ReLU, max
   float* out = a.out + (long long)g * a.out_gstride;
   const float* bias = a.bias ? a.bias + (long long)slot * a.b_sstride : nullptr;
-  const float* bias2 = (SC && a.sc_bias) ? a.sc_bias + (long long)slot * a.sc_b_sstride : nullptr;
   const float* res = a.res ? a.res + (long long)g * a.out_gstride : nullptr;
   float vmax = 0.f;
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
     const int n = n0 + wn * TN + j * 32 + fr;
     if (n >= a.Ncol) continue;
-    const float bv = (bias ? bias[n] : 0.f) + (bias2 ? bias2[n] : 0.f);
+    const float bv = bias ? bias[n] : 0.f;
 #pragma unroll
     for (int i = 0; i < MI; ++i)
 #pragma unroll
@@ -1109,7 +1067,7 @@ __global__ __launch_bounds__(256) void ximg_kernel(const XArgs a) {
         if (img0 + m / (W * W) >= nv) continue;
         const long long o = (long long)(img0 * W * W + m) * a.Ncol + n;
         float v = acc[i][j][r];
-        if (bias || bias2) v += bv;
+        if (bias) v += bv;
         if (res) v += res[o];
         if (a.relu) v = fmaxf(v, 0.f);
         vmax = fmaxf(vmax, fabsf(v));
@@ -1810,8 +1768,7 @@ int ximg_go(const XArgs& a, int G, hipStream_t st) {
   XArgs b = a;
   b.tiles_n = ceil_div(a.Ncol, BN);
   const dim3 grid((unsigned)(ceil_div(a.N, IMGS) * b.tiles_n), G, 1);
-  if (a.sc_src) hipLaunchKernelGGL((ximg_kernel<W, IMGS, BN, WM, WN, true, true>), grid, dim3(256), 0, st, b);
-  else if (a.wp) hipLaunchKernelGGL((ximg_kernel<W, IMGS, BN, WM, WN, true>), grid, dim3(256), 0, st, b);
+  if (a.wp) hipLaunchKernelGGL((ximg_kernel<W, IMGS, BN, WM, WN, true>), grid, dim3(256), 0, st, b);
   else hipLaunchKernelGGL((ximg_kernel<W, IMGS, BN, WM, WN, false>), grid, dim3(256), 0, st, b);
   DBA_LAUNCH_CHECK();
 }
@@ -1828,9 +1785,7 @@ int ximg_try(const XArgs& a, int G, int KH, int KW, hipStream_t st) {
   if (a.bf.mode || a.lz_coef) return -100;
   if (!aligned16(a.src) || a.src_gstride % 4 || !aligned16(a.w) || a.w_sstride % 4) return -100;
   if (a.wp && (((uintptr_t)a.wp & 15) || a.wp_sstride % 8)) return -100;
-  if (a.sc_src && (!a.wp || a.sc_C % 32 || a.sc_C > 256 || !aligned16(a.sc_src) || a.sc_gstride % 4 ||
-                   ((uintptr_t)a.sc_wp & 15) || a.sc_wp_sstride % 8))
-    return -100;
+  if (a.sc_src) return -100;   // the fused shortcut: xhalo_kernel only (see ximg_kernel)
   if (a.Wo == 8) return a.Ncol >= 128 ? ximg_go<8, 2, 128, 2, 2>(a, G, st) : ximg_go<8, 2, 64, 2, 2>(a, G, st);
   if (a.Wo == 4) return a.Ncol >= 128 ? ximg_go<4, 8, 128, 2, 2>(a, G, st) : ximg_go<4, 8, 64, 2, 2>(a, G, st);
   return -100;
@@ -2066,7 +2021,9 @@ DBA_EXPORT int dba_xconv_fwd(const float* x, long long x_gstride, const float* w
 
 // The conv2 of a downsampling BasicBlock with its 1x1 stride-2 shortcut fused (evaluation, BN
 // folded): out = relu(conv3x3(a, w2) + b2 + conv1x1_s2(x2, wsc) + bsc), one launch, the shortcut's
-// output never materialised (xhalo_kernel / ximg_kernel SC).  a [G][N][Ho][Wo][C] fp32, x2
+// output never materialised (xhalo_kernel SC: the W-16 stage, 64 channels from 32; 17 x 1024
+// images 1348 vs 1886 us for the shortcut conv + the residual-epilogue conv2,
+// profiles/r5/down/kbench_ximg_sc.log).  a [G][N][Ho][Wo][C] fp32, x2
 // [G][N][H2][W2][C2] fp32 (Ho = ceil(H2 / 2)), w2 / wsc pre-split fp16-pair planes per slot.
 // Returns -100 for shapes without a fused kernel (the caller runs the two convs).
 DBA_EXPORT int dba_xdown_fwd(const float* a_, long long a_gstride, const float* w2, long long w2_sstride,
@@ -2094,9 +2051,7 @@ DBA_EXPORT int dba_xdown_fwd(const float* a_, long long a_gstride, const float* 
   a.sc_amax_src = amax_x2; a.sc_amax_src_ld = amax_x2_ld; a.sc_amax_w = amax_wsc; a.sc_amax_w_ld = amax_wsc_ld;
   a.sc_bias = bsc; a.sc_b_sstride = bsc_sstride;
   a.cls[0] = XClass{3, 3, -1, -1, 0, 0, Ho, Wo, 0};
-  hipStream_t st = (hipStream_t)stream;
-  const int rc = ximg_try(a, G, 3, 3, st);
-  return rc != -100 ? rc : xhalo_try(a, G, 3, 3, st);
+  return xhalo_try(a, G, 3, 3, (hipStream_t)stream);
 }
 
 // dX of a conv from class-packed transposed weights (dba_xtranspose); accum (optional) is

@@ -14,6 +14,10 @@ broadcast is needed and every rank ends the round with a bit-identical global mo
   kernel (all n clients in one pass) and one weighted-sum kernel per iteration; weights and
   the stopping test stay on the device (one host read per aggregation).  Quirk D5 (``wv`` undefined if
   converged at iteration 0) resolves to the current weights.
+* The weighted sums of RFA and FoolsGold are REPRODUCIBLE: every product is quantised on its own
+  onto a fixed two-limb int64 grid (:func:`fixed_exponent`, ``ops.weighted_sum_fixed``) and the
+  limbs are summed exactly — over a rank's clients, then over ranks by an int64 all-reduce — so
+  the global model's bits do not depend on the world size or on which rank holds which client.
 * :class:`FoolsGold` — ``helper.py:527-607``: cosine similarity of the clients' final-FC
   gradient features (history-summed with ``fg_use_memory``), pardoning, logit weights,
   weighted gradient sum, then one fresh-SGD server step (BN buffers untouched).
@@ -21,6 +25,7 @@ broadcast is needed and every rank ends the round with a bit-identical global mo
 from __future__ import annotations
 
 import logging
+import math
 from typing import Any, Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
@@ -43,6 +48,26 @@ def fedavg_apply(global_state: torch.Tensor, delta_sum: torch.Tensor, eta: float
     """``w += (eta / no_models) * sum_i delta_i (+ noise)`` from the (all-reduced) fp64 sum of the
     clients' deltas (``ops.delta_sum``: fused HIP kernel on GPU)."""
     ops.add_noise_scaled(global_state[:n_update], delta_sum, eta / no_models, sigma, seed, dp)
+
+
+def fixed_exponent(maxabs: float, n: int) -> int:
+    """E of the fixed-point weighted sums: with weights <= 1 and |points| <= ``maxabs`` (the max
+    over ALL clients, every rank the same), each scaled product |w p 2^E| < 2^52 / n, so neither
+    limb sum of n <= 512 products overflows int64.  The grid step is 2^-(E + 53): ~105 bits below
+    the largest product."""
+    if not n <= 512:
+        raise ValueError("fixed-point weighted sum: at most 512 terms")
+    if not maxabs > 0.0 or not math.isfinite(maxabs):
+        return 0
+    n2 = max(0, math.ceil(math.log2(max(1, n))))
+    _, ex = math.frexp(maxabs)          # maxabs < 2**ex
+    return max(-1000, min(1000, 52 - n2 - ex))
+
+
+def fixed_decode(limbs: torch.Tensor, E: int) -> torch.Tensor:
+    """fp64 value of [2, L] int64 limb sums on the 2^-(E + 53) grid (elementwise, exact up to the
+    final rounding: the same bits for the same limbs)."""
+    return limbs[0].double() * (2.0 ** -E) + limbs[1].double() * (2.0 ** -(E + 53))
 
 
 def _weiszfeld(avg, dists, alphas: torch.Tensor, maxiter: int, eps: float, ftol: float, poll: int = 0):
@@ -105,11 +130,12 @@ def geometric_median(global_state: torch.Tensor, finals: torch.Tensor, num_sampl
     points = finals[:, :n_update] - global_state[None, :n_update]
     a = torch.tensor(num_samples, dtype=torch.float64, device=points.device)
     alphas = a / a.sum()
+    E = fixed_exponent(float(points.abs().max().item()), points.shape[0])
 
     def avg(w: torch.Tensor) -> torch.Tensor:
-        # fp64 accumulation of the (exact in fp64) fp32 products, rounded once: the same
-        # numbers the distributed form reaches from rank partial sums, up to fp64 order
-        return ops.weighted_sum(points, (w / w.sum()).float(), out_dtype=torch.float64).float()
+        # exact fixed-point sum of the products (each quantised on its own): the bits the
+        # distributed form reaches from its rank partials
+        return fixed_decode(ops.weighted_sum_fixed(points, (w / w.sum()).float(), E), E).float()
 
     def dists(m: torch.Tensor) -> torch.Tensor:
         return ops.sq_dists(points, m).double().clamp(min=0.0).sqrt()
@@ -131,14 +157,16 @@ def _rfa_apply(global_state, median, d, wv, eta, dp, sigma, seed, n_update, max_
 
 def geometric_median_distributed(global_state: torch.Tensor, local_finals: torch.Tensor, local_idx: Sequence[int],
                                  num_samples: Sequence[int], eta: float, maxiter: int, dp: bool, sigma: float,
-                                 seed: int, n_update: int, reduce, eps: float = 1e-5, ftol: float = 1e-6,
-                                 max_update_norm: Optional[float] = None
+                                 seed: int, n_update: int, reduce, reduce_max=None, eps: float = 1e-5,
+                                 ftol: float = 1e-6, max_update_norm: Optional[float] = None
                                  ) -> Tuple[bool, List[float], List[float], int]:
     """Weiszfeld with the client deltas resident on their owner ranks (reference
     ``helper.py:320-352``): per iteration each rank forms its partial weighted sum of its own
-    points (``reduce`` = all-reduce of the S-vector) and its points' distances to the median
-    (all-reduce of an n-vector with zeros for other ranks' clients).  Same device-side
-    iteration control and stopping rule as :func:`geometric_median`."""
+    points as fixed-point limbs (``reduce`` = all-reduce of the [2, S] int64 limbs: exact, so the
+    median's bits equal :func:`geometric_median`'s at any world size) and its points' distances
+    to the median (all-reduce of an n-vector with zeros for other ranks' clients: exact).
+    ``reduce_max``: max-all-reduce of a host float (the fixed grid's exponent: the max |delta|
+    over all clients).  Same device-side iteration control and stopping rule."""
     n = len(num_samples)
     dev = global_state.device
     idx = list(local_idx)
@@ -146,14 +174,16 @@ def geometric_median_distributed(global_state: torch.Tensor, local_finals: torch
     a = torch.tensor(num_samples, dtype=torch.float64, device=dev)
     alphas = a / a.sum()
     idx_t = torch.tensor(idx, dtype=torch.int64, device=dev) if idx else None
+    mx = float(points.abs().max().item()) if idx else 0.0
+    E = fixed_exponent(reduce_max(mx) if reduce_max is not None else mx, n)
 
     def avg(w: torch.Tensor) -> torch.Tensor:
         wn = w / w.sum()
         if idx:
-            part = ops.weighted_sum(points, wn[idx_t].float(), out_dtype=torch.float64)
+            part = ops.weighted_sum_fixed(points, wn[idx_t].float(), E)
         else:
-            part = torch.zeros(n_update, dtype=torch.float64, device=dev)
-        return reduce(part).float()
+            part = torch.zeros(2, n_update, dtype=torch.int64, device=dev)
+        return fixed_decode(reduce(part), E).float()
 
     def dists(m: torch.Tensor) -> torch.Tensor:
         full = torch.zeros(n, dtype=torch.float64, device=dev)
@@ -213,7 +243,8 @@ class FoolsGold:
         lo, hi = feat_slice
         wv, alpha = self.weights_from(grads[:, lo:hi], names)
         wts = torch.tensor(wv / len(names), dtype=torch.float32, device=grads.device)
-        agg = ops.weighted_sum(grads, wts)
+        E = fixed_exponent(float(grads.abs().max().item()), len(names))
+        agg = fixed_decode(ops.weighted_sum_fixed(grads, wts, E), E).float()
         return agg, wv, alpha
 
     def weights_from(self, feat_rows: torch.Tensor, names: Sequence[Any]) -> Tuple[np.ndarray, np.ndarray]:

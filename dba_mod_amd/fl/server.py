@@ -608,6 +608,10 @@ class Server:
         self.d.all_reduce_(buf)
         return buf[:t.numel()].view(t.shape)
 
+    def _reduce_max(self, v: float) -> float:
+        """Max of a host float over ranks (no-op at world 1)."""
+        return self.d.all_reduce_max(v) if self.d.enabled else v
+
     def _aggregate(self, plan: RoundPlan, bank: torch.Tensor, local: Dict[str, Any],
                    adversarial: List[Any]) -> None:
         p = self.params
@@ -634,7 +638,7 @@ class Server:
                 updated, wv, alphas, calls = agg.geometric_median_distributed(
                     self.global_state, local["finals"], local["idx"], ns, float(p["eta"]),
                     int(p["geom_median_maxiter"]), bool(p["diff_privacy"]), float(p["sigma"]), dp_seed, n_upd,
-                    reduce=self._reduce, **kw)
+                    reduce=self._reduce, reduce_max=self._reduce_max, **kw)
             self.csv.add_weight_result(names, wv, alphas)
             self._plot_weights(names, wv, alphas, adversarial, plan.epoch)
         elif method == C.AGGR_FOOLSGOLD:
@@ -649,14 +653,17 @@ class Server:
             # ONE all-reduce of the [n, d] features (each row owned by one rank: exact)
             wv, alpha = self.fg.weights_from(self._reduce(feats), names)
             idx = local["idx"]
+            grads = torch.stack([local["fg"][i] for i in idx]) if idx else None
+            # the fixed grid's exponent from the max |gradient| over every rank's clients
+            E = agg.fixed_exponent(self._reduce_max(float(grads.abs().max().item()) if idx else 0.0), n)
             if idx:
-                grads = torch.stack([local["fg"][i] for i in idx])
                 wl = torch.tensor([wv[i] / n for i in idx], dtype=torch.float32, device=self.device)
-                part = ops.weighted_sum(grads, wl, out_dtype=torch.float64)
+                part = ops.weighted_sum_fixed(grads, wl, E)
             else:
-                part = torch.zeros(self.spec.P, dtype=torch.float64, device=self.device)
-            # ONE all-reduce of the wv-weighted P-vector
-            agg_grad = self._reduce(part).float()
+                part = torch.zeros(2, self.spec.P, dtype=torch.int64, device=self.device)
+            # ONE all-reduce of the wv-weighted P-vector's int64 limbs: exact, so the aggregate's
+            # bits do not depend on the world size
+            agg_grad = agg.fixed_decode(self._reduce(part), E).float()
             log.info(f"[foolsgold agg] wv: {wv}")
             agg.foolsgold_server_step(self.global_state, agg_grad, self.spec.P, float(p["eta"]),
                                       float(p["lr"]), float(p["decay"]))

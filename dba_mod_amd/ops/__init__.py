@@ -52,7 +52,7 @@ def _dispatch(name: str):
 
 _OPS = ["gather_images", "gather_rows", "conv2d", "conv2d_dgrad", "conv2d_wgrad", "relu_mask_bwd", "bn_fold", "maxpool2d", "maxpool2d_bwd", "avgpool_global",
         "avgpool_global_bwd", "dropout", "dropout_bwd", "softmax_xent", "sgd_step", "dist_loss_grad",
-        "scale_from_base", "add_noise_scaled", "delta_sum", "sq_dists", "weighted_sum", "gram", "prepare_dgrad_weights", "wgrad_flush",
+        "scale_from_base", "add_noise_scaled", "delta_sum", "sq_dists", "weighted_sum", "weighted_sum_fixed", "gram", "prepare_dgrad_weights", "wgrad_flush",
         "wgrad_prepare", "conv_bn_stats", "bn_apply", "bn_finish", "basic_block_ok", "basic_block_eval",
         "stem_block_ok", "stem_block_eval", "down_block_ok", "down_block_eval"]
 

@@ -89,8 +89,11 @@ class BranchReplay:
             # decisions) on chip: recorded and replayed runs both take the two convs, whose
             # decisions this oracle sees (the fused kernel has its own fp64 test)
             return False
+        # likewise the fused stem block and the fused downsampling block (its shortcut's sum
+        # never leaves the chip): both runs take the separate convs
         return {"conv2d": conv2d, "maxpool2d": maxpool2d, "conv_bn_stats": conv_bn_stats, "bn_apply": bn_apply,
-                "basic_block_ok": basic_block_ok, "stem_block_ok": lambda x, w0, w1, w2: False}
+                "basic_block_ok": basic_block_ok, "stem_block_ok": lambda x, w0, w1, w2: False,
+                "down_block_ok": lambda a, w2, x2, wsc: False}
 
     def _valid(self, t):
         v = torch.zeros(t.shape[:2], dtype=torch.bool)

@@ -29,6 +29,7 @@ _I = ctypes.c_int
 _LL = ctypes.c_longlong
 _F = ctypes.c_float
 _U = ctypes.c_uint
+_D = ctypes.c_double
 
 _SIGS = {
     "dba_gather_images": [_P, _P, _P, _P, _P, _P, _I, _P, _P, _I, _P, _I, _I, _I, _I, _I, _P],
@@ -51,6 +52,7 @@ _SIGS = {
     "dba_gram_chunks": [_I],
     "dba_sq_dists": [_P, _LL, _P, _I, _LL, _P, _P, _P],
     "dba_weighted_sum": [_P, _LL, _P, _I, _P, _LL, _I, _P],
+    "dba_weighted_sum_fixed": [_P, _LL, _P, _I, _P, _LL, _D, _P],
     "dba_gram": [_P, _LL, _I, _I, _P, _P, _P],
     "dba_dist_loss_grad": [_P, _LL, _P, _LL, _P, _LL, _I, _P, _P, _F, _P, _P, _P],
     # reference-precision (fp32) family: csrc/kernels/xgemm.hip
@@ -520,9 +522,10 @@ def stem_block_eval(x, w0, b0, w1, b1, w2, b2, wsel=None, nvalid=None):
 
 def down_block_ok(a, w2, x2, wsc) -> bool:
     """The downsampling block's conv2 + 1x1 stride-2 shortcut run as one launch (xgemm.hip
-    dba_xdown_fwd: the shortcut as extra k-steps of xhalo / ximg): fp32 [G, N, W, W, C] ``a`` at
-    W 16 (C 64, shortcut input 32 channels) or W 8 / 4 (C % 32 == 0, shortcut input C2 % 32 == 0,
-    <= 256), both weights pre-split at the eval fold.  ``DBA_EVAL_DOWN=0``: off (two launches)."""
+    dba_xdown_fwd: the shortcut as an extra k-step of the W-16 halo conv): fp32 [G, N, 16, 16, 64]
+    ``a``, shortcut input [G, N, 32, 32, 32], both weights pre-split at the eval fold — the CIFAR
+    ResNets' layer2.0.  ``DBA_EVAL_DOWN=0``: off (two launches; the same-box A/B of
+    profiles/r5/down/).  (The 8 / 4-wide stages' fused form measured slower than two launches.)"""
     if not (_EVAL_DOWN and a.dtype == _F32 and x2.dtype == _F32 and a.dim() == 5 and x2.dim() == 5):
         return False
     H, W, C = a.shape[2:]
@@ -533,9 +536,7 @@ def down_block_ok(a, w2, x2, wsc) -> bool:
         return False
     if tuple(w2.shape[1:]) != (C, 3, 3, C) or tuple(wsc.shape[1:]) != (C, 1, 1, C2):
         return False
-    if W == 16:
-        return C == 64 and C2 == 32
-    return W in (8, 4) and C % 32 == 0 and C2 % 32 == 0 and C2 <= 256
+    return W == 16 and C == 64 and C2 == 32
 
 
 def down_block_eval(a, w2, b2, x2, wsc, bsc, wsel=None, nvalid=None):
@@ -1029,6 +1030,17 @@ def weighted_sum(points, wts, out_dtype=None):
     out = torch.empty(L, dtype=odt, device=points.device)
     _call("dba_weighted_sum", points.data_ptr(), points.stride(0), wts.float().contiguous().data_ptr(), n,
           out.data_ptr(), L, int(odt == torch.float64), _stream())
+    return out
+
+
+def weighted_sum_fixed(points, wts, E):
+    """[2, L] int64 fixed-point limb sums of sum_i wts[i] * points[i] at scale 2^E (flat.hip
+    wsum_fixed_kernel): order-free, so rank partials all-reduce to world-invariant bits."""
+    assert points.stride(1) == 1 and points.dtype == torch.float32
+    n, L = points.shape
+    out = torch.empty(2, L, dtype=torch.int64, device=points.device)
+    _call("dba_weighted_sum_fixed", points.data_ptr(), points.stride(0), wts.float().contiguous().data_ptr(), n,
+          out.data_ptr(), L, float(2.0 ** E), _stream())
     return out
 
 

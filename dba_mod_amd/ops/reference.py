@@ -546,6 +546,16 @@ def weighted_sum(points: Tensor, wts: Tensor, out_dtype: Optional[torch.dtype] =
     return (wts.double()[:, None] * points.double()).sum(0).to(out_dtype or points.dtype)
 
 
+def weighted_sum_fixed(points: Tensor, wts: Tensor, E: int) -> Tensor:
+    """[2, L] int64 limb sums of sum_i wts[i] * points[i] on the fixed grid 2^-(E + 53): each
+    product (exact in fp64) quantised on its own, hi = floor(q), lo = floor((q - hi) 2^53), q =
+    w p 2^E, then summed exactly (order-free; flat.hip wsum_fixed_kernel is the GPU form)."""
+    q = (wts.float().double()[:, None] * points.double()) * (2.0 ** E)
+    hi = torch.floor(q)
+    lo = torch.floor((q - hi) * 2.0 ** 53)
+    return torch.stack([hi.to(torch.int64).sum(0), lo.to(torch.int64).sum(0)])
+
+
 def gram(feats: Tensor) -> Tensor:
     """F F^T in float64 (K15)."""
     f = feats.double()

@@ -168,8 +168,7 @@ def _bench_eval_chunk(G, N, reps, dev):
             "fwd_tflops": round(G * N * 17.83e9 / 64 / t / 1e12, 1)}
 
 
-DOWN = [("eval.l2.0.down", 17, 1024, 16, 64, 32), ("eval.l3.0.down", 17, 1024, 8, 128, 64),
-        ("eval.l4.0.down", 17, 1024, 4, 256, 128)]
+DOWN = [("eval.l2.0.down", 17, 1024, 16, 64, 32)]
 
 
 def main(argv=None) -> int:

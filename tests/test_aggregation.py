@@ -156,3 +156,28 @@ def test_dist_loss_grad_matches_autograd():
         assert torch.allclose(got[g], wv.grad, atol=1e-10), g
     assert float(dist[1]) == 0.0 and float(dist[2]) == 0.0
     assert abs(float(dist[0]) - float(torch.norm(w[0, :P] - base[0, :P]))) < 1e-6
+
+
+def test_fixed_point_weighted_sum_is_order_free():
+    """The RFA / FoolsGold weighted sum on the fixed two-limb grid: any split of the clients
+    into rank partials (int64 sums, then added) gives the SAME limbs as one pass, in any client
+    order — what makes the distributed aggregation world-invariant — and the decoded value is
+    the fp64 sum to ~1e-15."""
+    from dba_mod_amd.ops import reference as R
+    g = torch.Generator().manual_seed(0)
+    n, L = 10, 5000
+    pts = torch.randn(n, L, generator=g) * torch.exp(3 * torch.randn(n, 1, generator=g))
+    pts[3, :100] *= 1e-9                                   # a wide dynamic range inside a row
+    w = torch.rand(n, generator=g)
+    w = (w / w.sum()).float()
+    E = agg.fixed_exponent(float(pts.abs().max()), n)
+    full = R.weighted_sum_fixed(pts, w, E)
+    for parts in ([[0, 1, 2, 3, 4], [5, 6, 7, 8, 9]], [[9, 2], [0, 5, 7], [1, 3, 4, 6, 8]]):
+        tot = sum(R.weighted_sum_fixed(pts[p], w[p], E) for p in parts)
+        assert torch.equal(tot, full)
+    perm = torch.randperm(n, generator=g)
+    assert torch.equal(R.weighted_sum_fixed(pts[perm], w[perm], E), full)
+    ref = (w.double()[:, None] * pts.double()).sum(0)
+    dec = agg.fixed_decode(full, E)
+    assert ((dec - ref).abs().max() / ref.abs().max()).item() < 1e-14
+    assert agg.fixed_exponent(0.0, n) == 0 and agg.fixed_exponent(float("nan"), n) == 0

@@ -70,24 +70,20 @@ def test_two_ranks_share_one_gpu():
 @pytest.mark.parametrize("agg,extra", [("mean", []), ("geom_median", ["rfa_mode=distributed"]), ("foolsgold", [])])
 def test_cifar_world2(tmp_path, agg, extra):
     """The flagship CIFAR ResNet-18 rounds (fused training BN, attacker 17's model replacement)
-    at world 2 (gloo on the shared GPU) vs world 1: FedAvg bitwise; distributed RFA and
-    FoolsGold to an occasional last-bit difference (fp64 rank partial sums meet in a
-    world-dependent order, then round once to fp32)."""
+    at world 2 (gloo on the shared GPU) vs world 1: bitwise for every aggregation — FedAvg's
+    fp64 delta sums, and the distributed RFA / FoolsGold weighted sums through the exact
+    fixed-point limb all-reduce (fl/aggregate.py fixed_exponent)."""
     import torch
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     args = CIFAR + extra + ["--aggregation", agg]
     one = _bench([sys.executable, "bench.py", *args, "--dump-state", str(tmp_path / "w1.pt")], {})
     two = _bench(_torchrun(2, args) + ["--dump-state", str(tmp_path / "w2.pt")], SHARED)
-    if agg == "mean":
-        _same(one, two)
-        return
+    _same(one, two)
     assert two["world"] == 2 and one["dtype"] == two["dtype"] == "fp32"
     s1 = torch.load(tmp_path / "w1.pt", weights_only=True)
     s2 = torch.load(tmp_path / "w2.pt", weights_only=True)
-    assert ((s1 - s2).norm() / s1.norm()).item() < 1e-6
-    for (e1, a1, _), (e2, a2, _) in zip(one["rounds"], two["rounds"]):
-        assert e1 == e2 and abs(a1 - a2) <= 0.5
+    assert torch.equal(s1, s2)
 
 
 def test_self_spawn_bench_world2():

@@ -209,3 +209,23 @@ def test_torch_library_ops_run_hip():
     pts = torch.randn(5, 10000, generator=g).to(dev)
     assert torch.equal(torch.ops.dba.gram(pts), H.gram(pts))
     assert torch.equal(torch.ops.dba.sq_dists(pts, pts[0]), H.sq_dists(pts, pts[0]))
+
+
+def test_weighted_sum_fixed_matches_reference_bitwise():
+    """flat.hip wsum_fixed_kernel: the same int64 limbs as the CPU reference (every step is an
+    exact fp64 operation or a floor), so the fixed-point RFA / FoolsGold sums agree across
+    devices as well as across world sizes."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from dba_mod_amd.fl import aggregate as agg
+    from dba_mod_amd.ops import hip as H
+    from dba_mod_amd.ops import reference as R
+    g = torch.Generator().manual_seed(1)
+    n, L = 7, 100003
+    pts = torch.randn(n, L, generator=g) * torch.exp(2 * torch.randn(n, 1, generator=g))
+    w = torch.rand(n, generator=g).float()
+    w = w / w.sum()
+    E = agg.fixed_exponent(float(pts.abs().max()), n)
+    got = H.weighted_sum_fixed(pts.cuda(), w.cuda(), E).cpu()
+    assert torch.equal(got, R.weighted_sum_fixed(pts, w, E))

@@ -4,9 +4,10 @@ two-launch form it replaces (GPU only).
 
 relu(conv3x3(a, w2) + b2 + conv1x1_s2(x2, wsc) + bsc) with BN folded into the weights — the
 second half of the downsampling BasicBlock of the reference ``models/resnet_cifar.py:24-36``
-(layer2.0 / 3.0 / 4.0) in evaluation.  The shortcut's products accumulate with their own fp16
-scales (the accumulators are rescaled exactly) and its output is never stored, so the fused form
-agrees with the two launches at fp32 level, not bitwise.  Wide dynamic ranges between the two
+(layer2.0) in evaluation; the 8 / 4-wide stages keep two launches (measured faster).  The
+shortcut's products accumulate with their own fp16 scales (the accumulators are rescaled
+exactly) and its output is never stored, so the fused form agrees with the two launches at fp32
+level, not bitwise.  Wide dynamic ranges between the two
 operand pairs exercise the rescale.
 """
 import struct
@@ -58,12 +59,11 @@ def _case(H, dev, G, N, W, C, C2, sa, sx, seed):
     return a, x2, w2, wsc, b2, bsc, wsel
 
 
-# (G, N, valid images, W, C, C2, scale of a, scale of x2): layer2.0 / 3.0 / 4.0 of the CIFAR
-# ResNet-18 and layer2.0 / 3.0 of the Tiny one, partial tiles, operand ranges far apart
+# (G, N, valid images, W, C, C2, scale of a, scale of x2): layer2.0 of the CIFAR ResNets, partial
+# tiles, operand ranges far apart (both directions)
 @pytest.mark.parametrize("G,N,nv,W,C,C2,sa,sx", [
     (3, 5, (5, 2, 4), 16, 64, 32, 1.0, 1.0), (2, 4, (4, 1), 16, 64, 32, 1e-3, 30.0),
-    (3, 5, (5, 3, 1), 8, 128, 64, 1.0, 1.0), (2, 9, (9, 6), 4, 256, 128, 30.0, 1e-3),
-    (1, 7, (7,), 8, 128, 64, 1e-4, 1.0), (2, 3, (3, 2), 4, 256, 128, 1.0, 1.0)])
+    (2, 9, (9, 6), 16, 64, 32, 30.0, 1e-3), (1, 7, (7,), 16, 64, 32, 1e-4, 1.0)])
 def test_down_block_vs_fp64_and_two_launches(H, R64, G, N, nv, W, C, C2, sa, sx):
     dev = torch.device("cuda")
     a, x2, w2, wsc, b2, bsc, wsel = _case(H, dev, G, N, W, C, C2, sa, sx, G * 100 + N + W)
@@ -86,7 +86,7 @@ def test_down_block_vs_fp64_and_two_launches(H, R64, G, N, nv, W, C, C2, sa, sx)
         assert struct.unpack("<f", struct.pack("<i", int(amax[:, i].max().item())))[0] == m
 
 
-@pytest.mark.parametrize("W,C,C2", [(16, 64, 32), (8, 128, 64), (4, 256, 128)])
+@pytest.mark.parametrize("W,C,C2", [(16, 64, 32)])
 def test_down_block_deterministic_and_group_size_independent(H, W, C, C2):
     """Repeated launches are bitwise identical, and a replica's bits do not depend on how many
     replicas share the launch (world-1 vs world-N runs group models differently)."""

@@ -6,7 +6,7 @@ import re
 
 from conftest import ROOT
 
-_CTYPE = {"int": "i", "unsigned": "u", "float": "f", "long long": "ll"}
+_CTYPE = {"int": "i", "unsigned": "u", "float": "f", "long long": "ll", "double": "d"}
 
 
 def _c_signatures():
@@ -32,7 +32,7 @@ def test_ctypes_signatures_match_c_abi():
     src = open(os.path.join(ROOT, "dba_mod_amd", "ops", "hip.py")).read()
     start = src.index("_SIGS = {")
     block = src[start:src.index("}\n", start) + 1]
-    env = {"_P": "p", "_I": "i", "_LL": "ll", "_F": "f", "_U": "u"}
+    env = {"_P": "p", "_I": "i", "_LL": "ll", "_F": "f", "_U": "u", "_D": "d"}
     table = eval(block.split("=", 1)[1], {}, env)
     c = _c_signatures()
     assert set(table) <= set(c), set(table) - set(c)
