@@ -30,6 +30,7 @@
 #include "common.hpp"
 #include "bnfuse.hpp"
 #include "xmfma.hpp"
+#include "xwgrad_halo.hpp"
 #include <algorithm>
 #include <type_traits>
 #include <utility>
@@ -1793,6 +1794,11 @@ int ximg_try(const XArgs& a, int G, int KH, int KW, hipStream_t st) {
 
 bool flip_dgrad(const XArgs& a) { return a.dsg < 0; }
 
+int& wgrad_halo_on() {
+  static int on = 1;
+  return on;
+}
+
 // the halo kernel's shapes: 3x3 stride-1 pad-1 (fwd) or its stride-1 data gradient, one class,
 // square W 32 (Cs 32, Ncol <= 32) or W 16 (Cs 64, Ncol <= 64), aligned fp32 operands.  (8-row
 // W-32 tiles were faster in isolation, not in the overlapped bench: profiles/r2_halo_tiles_ab.md;
@@ -1920,6 +1926,14 @@ ClassGeom dgrad_classes(int H, int W, int Cin, int Cout, int KH, int KW, int s, 
 }
 
 }  // namespace
+
+// patch-reuse weight gradient (xwgrad_halo.hip) on / off (tests: A/B against the implicit GEMM
+// on the same slabs); returns the previous
+DBA_EXPORT int dba_xwgrad_halo_set(int on) {
+  const int prev = wgrad_halo_on();
+  if (on >= 0) wgrad_halo_on() = on;
+  return prev;
+}
 
 // whole-image halo conv (ximg_kernel) on / off (tests: A/B against the implicit GEMM); returns the previous
 DBA_EXPORT int dba_ximg_set(int on) {
@@ -2141,6 +2155,14 @@ DBA_EXPORT int dba_xtranspose(const void* desc, int n, int slots, long long max_
 // blocks per replica (a lone client fills the chip), chunks of >= 256 rows.
 DBA_EXPORT long long dba_xwgrad_ws_floats(int G, int N, int Ho, int Wo, int Cin, int Cout, int KH, int KW, int* mchunk_out) {
   const int K = KH * KW * Cin;
+  // the narrow stages' 3x3 convs: the patch-reuse kernel's slabs (xwgrad_halo.hip: SPB strips
+  // of 8 rows each; the implicit GEMM takes the same slabs where that kernel declines)
+  const int hrows = (KH == 3 && KW == 3) ? xwgrad_halo_rows(Ho, Wo, Cin, Cout) : 0;
+  if (hrows > 0 && (long long)N * Ho * Wo > hrows) {
+    const long long M = (long long)N * Ho * Wo, Z = (M + hrows - 1) / hrows;
+    if (mchunk_out) *mchunk_out = hrows;
+    return Z * G * Cout * K;
+  }
   const int bno = Cout <= 32 ? 32 : Cout <= 64 ? 64 : 128;
   const long long tiles = (long long)ceil_div(Cout, bno) * ceil_div(K, 128);
   const long long M = (long long)N * Ho * Wo;
@@ -2179,6 +2201,20 @@ DBA_EXPORT int dba_xwgrad(const float* dy, long long dy_gstride, const float* x,
   a.dWo = FDiv{Wo, 1.0f / (float)Wo};
   a.tiles_k = ceil_div(a.K, 128);
   if ((long long)N * Ho * Wo * Cout >= (1LL << 29) || (long long)N * H * W * Cin >= (1LL << 29)) return -103;
+  if (Z > 1 && wgrad_halo_on() && stride == 1 && pad == 1 && KH == 3 && KW == 3 && H == Ho && W == Wo &&
+      Cin == Cout && mchunk == xwgrad_halo_rows(Ho, Wo, Cin, Cout)) {
+    // patch reuse: each staged input element feeds all 9 taps (xwgrad_halo.hip)
+    XWHArgs h{dy, dy_gstride, x, x_gstride, ws, nvalid, N, H, amax_dy, amax_dy_ld, amax_x, amax_x_ld, x_coef, x_relu};
+    const int rc = xwgrad_halo_launch(h, G, W, Cin, st);
+    if (rc != -100) {
+      if (rc != 0 || defer) return rc;
+      const long long per = (long long)Cout * a.K;
+      const dim3 g2((unsigned)std::max(1LL, std::min(1024LL, (per + 255) / 256)), G);
+      hipLaunchKernelGGL(xwgrad_reduce_kernel, g2, dim3(256), 0, st, (const float*)ws, G, per, nvalid, N, Ho * Wo,
+                         mchunk, dw, dw_gstride);
+      DBA_LAUNCH_CHECK();
+    }
+  }
   const bool v4 = Cin % 4 == 0 && Cout % 4 == 0 && Wo % 4 == 0 && aligned16(dy) && aligned16(x) &&
                   dy_gstride % 4 == 0 && x_gstride % 4 == 0;
   // output-channel tile: 128 for wide layers (64 for a lone client's stage-3/4 weight gradients

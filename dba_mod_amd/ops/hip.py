@@ -57,6 +57,7 @@ _SIGS = {
     "dba_dist_loss_grad": [_P, _LL, _P, _LL, _P, _LL, _I, _P, _P, _F, _P, _P, _P],
     # reference-precision (fp32) family: csrc/kernels/xgemm.hip
     "dba_ximg_set": [_I],
+    "dba_xwgrad_halo_set": [_I],
     "dba_xconv_ws_floats": [_I] * 8,
     "dba_xconv_fwd": [_P, _LL, _P, _LL, _P, _P, _LL, _P, _P, _LL, _P] + [_I] * 13 + [_P, _I] * 3 + [_P, _LL] * 2
     + [_P, _LL, _P, _P, _I, _P],
@@ -243,6 +244,12 @@ def set_ximg(on: int) -> int:
     """Whole-image halo conv of the 8 / 4-wide evaluation stages (xgemm.hip ximg_kernel) on /
     off; -1 queries.  Returns the previous setting (tests: A/B against the implicit GEMM)."""
     return int(_L.dba_ximg_set(int(on)))
+
+
+def set_wgrad_halo(on: int) -> int:
+    """Patch-reuse weight gradient of the narrow stages' 3x3 convs (xwgrad_halo.hip) on / off;
+    -1 queries.  Returns the previous setting (tests: A/B against the implicit GEMM)."""
+    return int(_L.dba_xwgrad_halo_set(int(on)))
 
 
 def fp32_mode() -> int:
