@@ -1558,25 +1558,50 @@ __global__ __launch_bounds__(256) void amax_kernel(const float* __restrict__ x, 
   amax_fold(out, ld, g, m);
 }
 
-// dbias[g][n] += sum over valid rows of dy[g][m][n] (fixed order: per-thread strided partial
-// sums, then a fixed LDS tree)
-__global__ __launch_bounds__(256) void xcolsum_kernel(const float* __restrict__ dy, long long dy_gstride, int rows_per_img,
-                                                      const int* __restrict__ nvalid, int N, int C,
-                                                      float* __restrict__ db, long long db_gstride) {
-  __shared__ double red[8][33];
-  const int g = blockIdx.y;
-  const int c = blockIdx.x * 32 + (threadIdx.x & 31), rq = threadIdx.x >> 5;
+// bias gradient db[g][c] += sum over the valid rows of dy[g][r][c], deterministic, in two
+// passes: xcolsum_part sums fixed 256-row chunks (4 row lanes x 64 columns per block, fp64,
+// the lanes met in LDS in lane order) into part[g][chunk][c]; xcolsum_fin sums the chunks in
+// chunk order.  The chunking depends on the replica's own valid rows only.  (The former single
+// pass ran ONE block per 32 columns with a 4608-long serial add chain per thread for MnistNet's
+// conv1 — 36864 rows x 20 channels: 278 us per launch, 70 % of the MNIST training stream,
+// profiles/r5/mnist/streams_before.md.)
+constexpr int kColRows = 256;
+__global__ __launch_bounds__(256) void xcolsum_part_kernel(const float* __restrict__ dy, long long dy_gstride,
+                                                           int rows_per_img, const int* __restrict__ nvalid, int N,
+                                                           int C, double* __restrict__ part, int nchunk) {
+  __shared__ double red[4][64];
+  const int g = blockIdx.y, ch = blockIdx.x;
   const int R = valid_rows(nvalid, g, N) * rows_per_img;
-  double s = 0.0;    // fp64 partials: a long, cancelling column sum stays at fp32 rounding
-  if (c < C)
-    for (int r = rq; r < R; r += 8) s += dy[(long long)g * dy_gstride + (long long)r * C + c];
-  red[rq][threadIdx.x & 31] = s;
-  __syncthreads();
-  if (rq == 0 && c < C) {
-    double t = red[0][threadIdx.x];
-    for (int k = 1; k < 8; ++k) t += red[k][threadIdx.x];
-    db[(long long)g * db_gstride + c] += (float)t;
+  const int r0 = ch * kColRows, r1 = min(R, r0 + kColRows);
+  const int tc = threadIdx.x & 63, tr = threadIdx.x >> 6;
+  const float* __restrict__ d = dy + (long long)g * dy_gstride;
+  for (int c0 = 0; c0 < C; c0 += 64) {
+    const int c = c0 + tc;
+    double s = 0.0;
+    if (c < C)
+#pragma unroll 4
+      for (int r = r0 + tr; r < r1; r += 4) s += d[(long long)r * C + c];
+    red[tr][tc] = s;
+    __syncthreads();
+    if (tr == 0 && c < C)
+      part[((long long)g * nchunk + ch) * C + c] = ((red[0][tc] + red[1][tc]) + red[2][tc]) + red[3][tc];
+    __syncthreads();
   }
+}
+// one wave per column: lane l sums chunks l, l + 64, ... (fp64), then the wave's fixed
+// butterfly — the same order at any launch geometry
+__global__ __launch_bounds__(256) void xcolsum_fin_kernel(const double* __restrict__ part, int rows_per_img,
+                                                          const int* __restrict__ nvalid, int N, int C, int nchunk,
+                                                          float* __restrict__ db, long long db_gstride) {
+  const int g = blockIdx.y, c = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (c >= C) return;
+  const int R = valid_rows(nvalid, g, N) * rows_per_img;
+  const int nc = (R + kColRows - 1) / kColRows;
+  double t = 0.0;
+  for (int k = lane; k < nc; k += 64) t += part[((long long)g * nchunk + k) * C + c];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o, 64);
+  if (lane == 0) db[(long long)g * db_gstride + c] += (float)t;
 }
 
 // ===================================================== fused training BN: standalone pass
@@ -2285,10 +2310,17 @@ DBA_EXPORT int dba_amax(const float* x, long long gstride, long long n_per_g, co
   DBA_LAUNCH_CHECK();
 }
 
+// part: [G][ceil(N * rows_per_img / 256)][C] fp64 workspace (dba_xcolsum_part_doubles)
+DBA_EXPORT long long dba_xcolsum_part_doubles(int G, int N, int rows_per_img, int C) {
+  return (long long)G * ceil_div((long long)N * rows_per_img, kColRows) * C;
+}
 DBA_EXPORT int dba_xcolsum(const float* dy, long long dy_gstride, int rows_per_img, const int* nvalid, int G, int N,
-                           int C, float* db, long long db_gstride, void* stream) {
-  hipLaunchKernelGGL(xcolsum_kernel, dim3(ceil_div(C, 32), G), dim3(256), 0, (hipStream_t)stream, dy, dy_gstride,
-                     rows_per_img, nvalid, N, C, db, db_gstride);
+                           int C, float* db, long long db_gstride, double* part, void* stream) {
+  const int nchunk = ceil_div((long long)N * rows_per_img, kColRows);
+  hipLaunchKernelGGL(xcolsum_part_kernel, dim3(nchunk, G), dim3(256), 0, (hipStream_t)stream, dy, dy_gstride,
+                     rows_per_img, nvalid, N, C, part, nchunk);
+  hipLaunchKernelGGL(xcolsum_fin_kernel, dim3(ceil_div(C, 4), G), dim3(256), 0, (hipStream_t)stream, part,
+                     rows_per_img, nvalid, N, C, nchunk, db, db_gstride);
   DBA_LAUNCH_CHECK();
 }
 

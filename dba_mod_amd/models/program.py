@@ -352,6 +352,8 @@ class Ctx:
         return y
 
     def maxpool(self, x: Tensor, k: int, s: int, p: int) -> Tensor:
+        if not self.train:   # evaluation: no argmax indices
+            return ops.maxpool2d(x, k, s, p, want_ind=False)[0]
         y, ind = ops.maxpool2d(x, k, s, p)
         if self.train:
             shp = tuple(x.shape)

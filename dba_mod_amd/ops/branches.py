@@ -80,9 +80,10 @@ class BranchReplay:
                 k = dict(k, relu=False)
             return self._relu(o_conv(*a, **k))
 
-        def maxpool2d(x, kk, st, p):
-            y, ind = o_mp(x, kk, st, p)
-            return self._pool(x, y, ind)
+        def maxpool2d(x, kk, st, p, want_ind=True):
+            y, ind = o_mp(x, kk, st, p)   # the decisions are recorded / replayed either way
+            y, ind = self._pool(x, y, ind)
+            return y, (ind if want_ind else None)
 
         def basic_block_ok(x, w1, w2):
             # the fused evaluation BasicBlock keeps its mid activation (and so its ReLU

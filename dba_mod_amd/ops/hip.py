@@ -34,7 +34,8 @@ _D = ctypes.c_double
 _SIGS = {
     "dba_gather_images": [_P, _P, _P, _P, _P, _P, _I, _P, _P, _I, _P, _I, _I, _I, _I, _I, _P],
     "dba_gather_rows": [_P, _P, _P, _P, _P, _I, _P, _P, _I, _P, _I, _P, _I, _I, _I, _P],
-    "dba_xcolsum": [_P, _LL, _I, _P, _I, _I, _I, _P, _LL, _P],
+    "dba_xcolsum": [_P, _LL, _I, _P, _I, _I, _I, _P, _LL, _P, _P],
+    "dba_xcolsum_part_doubles": [_I, _I, _I, _I],
     "dba_amax_segments": [_P, _LL, _P, _I, _I, _P, _I, _P],
     "dba_bn_fold": [_P, _LL, _P, _P, _P, _P, _P, _LL, _F, _P, _P, _I, _I, _I, _I, _P],
     "dba_relu_mask_bwd": [_P, _P, _P, _LL, _I, _P],
@@ -92,6 +93,7 @@ for _name, _args in _SIGS.items():
 _L.dba_xconv_ws_floats.restype = ctypes.c_longlong
 _L.dba_xconv_sk_ints.restype = ctypes.c_longlong
 _L.dba_xwgrad_ws_floats.restype = ctypes.c_longlong
+_L.dba_xcolsum_part_doubles.restype = ctypes.c_longlong
 
 
 class _BnFuse(ctypes.Structure):
@@ -687,8 +689,10 @@ def conv2d_wgrad(dy, x, stride, pad, kh, kw, dw, dbias=None, nvalid=None, defer=
                        mchunk.value, G, 0], wsb, nv))
     if dbias is not None:
         assert dbias.dtype == torch.float32 and dbias.stride(1) == 1
+        part = torch.empty(int(_L.dba_xcolsum_part_doubles(G, N, Ho * Wo, Cout)), dtype=torch.float64,
+                           device=dy.device)
         _call("dba_xcolsum", dy.data_ptr(), N * Ho * Wo * Cout, Ho * Wo, _ptr(_i32(nvalid)), G, N, Cout,
-              dbias.data_ptr(), dbias.stride(0), _stream())
+              dbias.data_ptr(), dbias.stride(0), part.data_ptr(), _stream())
     return None
 
 
@@ -885,14 +889,15 @@ def bn_fold(w, conv_bias, gamma, beta, rmean, rvar, eps, out_dtype):
 
 
 # --------------------------------------------------------------------------- pooling
-def maxpool2d(x, k, s, p):
+def maxpool2d(x, k, s, p, want_ind=True):
+    """``want_ind`` False (evaluation): no argmax indices are stored (returns (y, None))."""
     x = _act(x, None, "maxpool input")
     G, N, H, W, C = x.shape
     Ho = (H + 2 * p - k) // s + 1
     Wo = (W + 2 * p - k) // s + 1
     y = torch.empty(G, N, Ho, Wo, C, dtype=x.dtype, device=x.device)
-    ind = torch.empty(G, N, Ho, Wo, C, dtype=torch.int32, device=x.device)
-    _call("dba_maxpool", x.data_ptr(), y.data_ptr(), ind.data_ptr(), G * N, H, W, C, Ho, Wo, k, s, p, _f32(x),
+    ind = torch.empty(G, N, Ho, Wo, C, dtype=torch.int32, device=x.device) if want_ind else None
+    _call("dba_maxpool", x.data_ptr(), y.data_ptr(), _ptr(ind), G * N, H, W, C, Ho, Wo, k, s, p, _f32(x),
           _stream())
     return y, ind
 

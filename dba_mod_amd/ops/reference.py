@@ -371,7 +371,9 @@ def bn_fold(w: Tensor, conv_bias: Optional[Tensor], gamma: Tensor, beta: Tensor,
 
 
 # --------------------------------------------------------------------------- pooling
-def maxpool2d(x: Tensor, k: int, s: int, p: int) -> Tuple[Tensor, Tensor]:
+def maxpool2d(x: Tensor, k: int, s: int, p: int, want_ind: bool = True) -> Tuple[Tensor, Optional[Tensor]]:
+    """K7 max-pool; ``want_ind`` is a HIP hint (evaluation stores no indices): the reference
+    always returns them."""
     G, N, H, W, C = x.shape
     y, ind = F.max_pool2d(_nchw(x.to(_cdt()).reshape(G * N, H, W, C)), k, s, p, return_indices=True)
     return (_nhwc(y).reshape(G, N, y.shape[2], y.shape[3], C).to(x.dtype),

@@ -258,6 +258,12 @@ def test_fp32_pool_relu_loss_fold(H, R64):
         y, ind = H.maxpool2d(x, k, s, p)
         yr, indr = R64.maxpool2d(_c(x), k, s, p)
         assert torch.equal(y.cpu().double(), yr) and torch.equal(ind.cpu(), indr)
+        y2, none = H.maxpool2d(x, k, s, p, want_ind=False)   # evaluation: no indices stored
+        assert none is None and torch.equal(y2, y)
+        x50 = x[..., :10].contiguous()                        # C % 4 != 0: the generic kernel
+        y3, i3 = H.maxpool2d(x50, k, s, p)
+        y3r, i3r = R64.maxpool2d(_c(x50), k, s, p)
+        assert torch.equal(y3.cpu().double(), y3r) and torch.equal(i3.cpu(), i3r)
         dy = torch.randn_like(y)
         assert _rel(H.maxpool2d_bwd(dy, ind, tuple(x.shape), k, s, p),
                     R64.maxpool2d_bwd(_c(dy), indr, tuple(x.shape), k, s, p)) < 1e-7
