@@ -186,6 +186,7 @@ def _run(args) -> int:
 
     sync()
     t0 = time.perf_counter()
+    n_done0 = len(server.train_done_t)
     # round r's evaluation overlaps round r+1's training; the last round is fully evaluated
     # (flushed) inside the timed region, so exactly K complete rounds are timed
     done = server.run_rounds(range(epoch, epoch + args.steps))
@@ -239,6 +240,10 @@ def _run(args) -> int:
             "comm_bytes_per_round": comm_mean,
             "ops_backend": ops.backend_name(dctx.device),
             "fp32_split": _split_label(server),
+            # host time between consecutive rounds' training completions (the first from the
+            # window start): where in the window a rank's critical path lies (poison rounds)
+            "round_ms": [round(1000.0 * (b - a), 1) for a, b in
+                         zip([t0] + server.train_done_t[n_done0:-1], server.train_done_t[n_done0:])],
             "global_acc": round(float(last.get("global_acc", 0.0)), 3),
             "global_asr": round(float(last.get("global_asr", 0.0)), 3),
             "rounds": [[int(r["epoch"]), round(float(r.get("global_acc", 0.0)), 2), round(float(r.get("global_asr", 0.0)), 2)]

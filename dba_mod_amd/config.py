@@ -93,6 +93,10 @@ _DEFAULTS: Dict[str, Any] = {
     "synthetic_noise": None,       # synthetic image pixel-noise sigma (None: per-dataset default)
     "synthetic_shared": None,      # fraction of the class template shared by all classes
     "synthetic_clutter": None,     # weight of the per-image random background field
+    "synthetic_sky": None,         # fraction of images with a saturated bright top band (None: per dataset)
+    "synthetic_margin": None,      # exactly black border width in pixels (None: per dataset)
+    "synthetic_sky_rows": None,    # rows of the bright band (row 0 saturated; None: 3)
+    "synthetic_contrast": None,    # [lo, hi] per-image contrast range (None: [0.6, 1.2])
     "compute_dtype": "fp32",      # fp32 = reference precision (split fp32 operands on the 16-bit MFMA)
     "eval_batch_size": 1024,      # per-model eval chunk (reference: 64; a free parameter, D13)
     "aggregate_bn_buffers": True,  # D2: deltas/aggregation include BN running stats

@@ -95,9 +95,18 @@ def _smooth_fields(rng: np.random.RandomState, n: int, h: int, w: int, c: int, c
 def make_image_dataset(counts: List[int], h: int, w: int, c: int, seed: int,
                        noise: float = 0.15, shift: int = 3, coarse: int = 4,
                        shared: float = 0.75, clutter: float = 0.0, strokes: bool = False,
+                       sky: float = 0.0, sky_rows: int = 3, margin: int = 0,
+                       contrast: Tuple[float, float] = (0.6, 1.2),
                        templates: Optional[np.ndarray] = None,
                        name: str = "") -> Tuple[ImageDataset, np.ndarray]:
-    """Generate a dataset; returns (dataset, class templates) so train/test share templates."""
+    """Generate a dataset; returns (dataset, class templates) so train/test share templates.
+
+    ``sky``: fraction of images whose top ``sky_rows`` rows fade to saturated white (row 0
+    exactly 255), like the bright sky at the top of many natural photographs.  ``margin``: an
+    exactly black border of that many pixels (MNIST digits are size-normalised into the central
+    20 x 20 box of the 28 x 28 frame, so its 4-pixel border is always 0).  Both shape what a pixel
+    trigger in the top rows competes with: a white trigger is invisible on a white sky, and a
+    trigger in a border that benign data never lights is never unlearned by benign updates."""
     rng = np.random.RandomState(seed)
     k = len(counts)
     if templates is None:
@@ -113,6 +122,7 @@ def make_image_dataset(counts: List[int], h: int, w: int, c: int, seed: int,
             templates = np.clip((templates - 0.5) * 5.0, 0.0, 1.0).astype(np.float32)
     labels = _class_order_labels(counts, rng)
     n = labels.shape[0]
+    contrast_lo, contrast_hi = float(contrast[0]), float(contrast[1])
     out = np.empty((n, h, w, c), dtype=np.uint8)
     chunk = 4096
     for s in range(0, n, chunk):
@@ -120,7 +130,7 @@ def make_image_dataset(counts: List[int], h: int, w: int, c: int, seed: int,
         lab = labels[s:e]
         dy = rng.randint(0, 2 * shift + 1, size=e - s)
         dx = rng.randint(0, 2 * shift + 1, size=e - s)
-        contrast = rng.uniform(0.6, 1.2, size=(e - s, 1, 1, 1)).astype(np.float32)
+        contrast = rng.uniform(contrast_lo, contrast_hi, size=(e - s, 1, 1, 1)).astype(np.float32)
         bright = rng.uniform(-0.15, 0.15, size=(e - s, 1, 1, 1)).astype(np.float32)
         imgs = np.empty((e - s, h, w, c), dtype=np.float32)
         for i in range(e - s):
@@ -136,6 +146,16 @@ def make_image_dataset(counts: List[int], h: int, w: int, c: int, seed: int,
         else:
             imgs = (imgs - 0.5) * contrast + 0.5 + bright
         imgs += rng.randn(e - s, h, w, c).astype(np.float32) * noise
+        if sky > 0:
+            # (drawn per chunk after the pixel noise, so the other streams are unchanged)
+            bright = rng.rand(e - s) < sky
+            fade = np.maximum(0.0, 1.0 - np.arange(h, dtype=np.float32) / float(sky_rows))[None, :, None, None]
+            imgs = np.where(bright[:, None, None, None], imgs + (1.0 - imgs) * fade, imgs)
+        if margin > 0:
+            imgs[:, :margin] = 0.0
+            imgs[:, h - margin:] = 0.0
+            imgs[:, :, :margin] = 0.0
+            imgs[:, :, w - margin:] = 0.0
         out[s:e] = np.clip(imgs * 255.0 + 0.5, 0, 255).astype(np.uint8)
     return ImageDataset(out, labels, k, name), templates
 
@@ -149,8 +169,10 @@ def _scaled_counts(counts: List[int], total: Optional[int]) -> List[int]:
 
 def synthetic_image_pair(kind: str, seed: int = 1, train_size: Optional[int] = None,
                          test_size: Optional[int] = None, noise: Optional[float] = None,
-                         shared: Optional[float] = None,
-                         clutter: Optional[float] = None) -> Tuple[ImageDataset, ImageDataset]:
+                         shared: Optional[float] = None, clutter: Optional[float] = None,
+                         sky: Optional[float] = None, margin: Optional[int] = None,
+                         sky_rows: Optional[int] = None,
+                         contrast: Optional[Tuple[float, float]] = None) -> Tuple[ImageDataset, ImageDataset]:
     """(train, test) synthetic datasets for 'mnist' | 'cifar' | 'tiny-imagenet-200'.
 
     ``noise`` (pixel-noise sigma) and ``shared`` (template fraction common to all classes) set
@@ -181,6 +203,14 @@ def synthetic_image_pair(kind: str, seed: int = 1, train_size: Optional[int] = N
         kw["shared"] = float(shared)
     if clutter is not None:
         kw["clutter"] = float(clutter)
+    if sky is not None:
+        kw["sky"] = float(sky)
+    if margin is not None:
+        kw["margin"] = int(margin)
+    if sky_rows is not None:
+        kw["sky_rows"] = int(sky_rows)
+    if contrast is not None:
+        kw["contrast"] = (float(contrast[0]), float(contrast[1]))
     train, tmpl = make_image_dataset(tr_c, h, w, c, seed=seed * 1000 + 1, name=f"{kind}-train", **kw)
     test, _ = make_image_dataset(te_c, h, w, c, seed=seed * 1000 + 2, templates=tmpl,
                                  name=f"{kind}-test", **kw)

@@ -146,6 +146,7 @@ class Server:
         self._early_stream = None
         self._unlaunched: Optional[Dict[str, Any]] = None    # trained + aggregated, eval not enqueued
         self._launched: List[Dict[str, Any]] = []             # eval enqueued, not yet recorded
+        self.train_done_t: List[float] = []   # host time each round's training was collected
         if self.device.type == "cuda" and bool(params.get("overlap_eval", True)):
             # training runs on a HIGH-priority stream (its kernels are small and latency-bound,
             # they win every CU that frees up); evaluation fills the rest at default priority
@@ -347,6 +348,7 @@ class Server:
         plan, epoch, early = st["plan"], st["epoch"], st["early"]
         with self.timer.phase("train"):
             results = st["handle"].collect()
+        self.train_done_t.append(time.perf_counter())   # per-round pacing (bench "round_ms")
         if early is not None and self._early_stream is not None:
             early.event = torch.cuda.Event()        # every local test of this round is enqueued
             early.event.record(self._early_stream)

@@ -81,7 +81,11 @@ def build_workload(params: C.Params, device: torch.device) -> Workload:
                                                      test_size=params["synthetic_test_size"],
                                                      noise=params["synthetic_noise"],
                                                      shared=params["synthetic_shared"],
-                                                     clutter=params["synthetic_clutter"])
+                                                     clutter=params["synthetic_clutter"],
+                                                     sky=params["synthetic_sky"],
+                                                     margin=params["synthetic_margin"],
+                                                     sky_rows=params["synthetic_sky_rows"],
+                                                     contrast=params["synthetic_contrast"])
     else:
         train, test = {C.TYPE_MNIST: readers.read_mnist, C.TYPE_CIFAR: readers.read_cifar,
                        C.TYPE_TINYIMAGENET: readers.read_tiny}[t](data_dir)

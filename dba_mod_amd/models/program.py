@@ -258,6 +258,8 @@ class Ctx:
                                   nvalid=self.nvalid, defer=self._wdefer)
             if not need_dx:
                 return (None,)
+            if dy is None:   # (only the stem's weight gradient forms dy without storing it)
+                raise RuntimeError(f"{conv}: the weight gradient did not store dy for the data gradient")
             acc = self.tape.pop_grad(x)
             fin = self.tape.finish_spec(x) if self.tape.is_last(x) else None
             return (ops.conv2d_dgrad(dy, w, self.wsel, stride, pad, in_hw, nvalid=self.nvalid, accum=acc,

@@ -68,11 +68,13 @@ _SIGS = {
     "dba_amax": [_P, _LL, _LL, _P, _LL, _I, _P, _I, _P],
     "dba_xtranspose": [_P, _I, _I, _LL, _P, _P],
     "dba_xwgrad_ws_floats": [_I] * 8 + [_P],
+    "dba_xwgrad_stem_ws_floats": [_I] * 6,
     "dba_xwgrad": [_P, _LL, _P, _LL, _P, _LL, _P] + [_I] * 12 + [_P, _I] * 2 + [_P, _LL, _I] + [_P, _I, _P],
     # fused training BN (csrc/kernels/bnfuse.hpp)
     "dba_bnx_rows": [_P, _P, _P, _LL, _P, _I, _I, _I, _P, _F, _P],
     "dba_bnx_apply": [_P, _P, _P, _P, _P, _I, _I, _P, _LL, _P, _I, _I, _I, _I, _P, _I, _P],
     "dba_bnfuse_size": [],
+    "dba_xwgrad_stem": [_P, _LL, _P, _P, _P, _LL, _P, _P, _I, _I, _I, _I, _P],
     "dba_bnx_dy": [_P, _P, _P, _P, _LL, _P, _I, _I, _I, _I, _P, _I, _P],
     "dba_xwgrad_reduce_batch": [_P, _I, _I, _LL, _P],
     # fused evaluation BasicBlock, with or without the image stem (csrc/kernels/xblock.hip)
@@ -93,6 +95,7 @@ for _name, _args in _SIGS.items():
 _L.dba_xconv_ws_floats.restype = ctypes.c_longlong
 _L.dba_xconv_sk_ints.restype = ctypes.c_longlong
 _L.dba_xwgrad_ws_floats.restype = ctypes.c_longlong
+_L.dba_xwgrad_stem_ws_floats.restype = ctypes.c_longlong
 _L.dba_xcolsum_part_doubles.restype = ctypes.c_longlong
 
 
@@ -252,6 +255,19 @@ def set_wgrad_halo(on: int) -> int:
     """Patch-reuse weight gradient of the narrow stages' 3x3 convs (xwgrad_halo.hip) on / off;
     -1 queries.  Returns the previous setting (tests: A/B against the implicit GEMM)."""
     return int(_L.dba_xwgrad_halo_set(int(on)))
+
+
+_STEM_WGRAD = True
+
+
+def set_stem_wgrad(on: int) -> int:
+    """The stem's own weight gradient (xwgrad_stem.hip) on / off; -1 queries.  Returns the
+    previous setting (tests: A/B against the implicit GEMM)."""
+    global _STEM_WGRAD
+    prev = int(_STEM_WGRAD)
+    if on >= 0:
+        _STEM_WGRAD = bool(on)
+    return prev
 
 
 def fp32_mode() -> int:
@@ -657,8 +673,11 @@ def conv2d_wgrad(dy, x, stride, pad, kh, kw, dw, dbias=None, nvalid=None, defer=
     """``defer`` (a list, fp32 family): the slab reduction is queued there and run for the whole
     backward pass by :func:`wgrad_flush` (one launch instead of one per conv).  ``dy`` may be a
     ``LazyGrad`` (a training BN's input gradient, staged from (d, y); its value is stored once
-    and returned for the data gradient) and ``x`` a ``LazyBN`` (a training BN's output, staged
-    from y)."""
+    and returned for the data gradient — except for the 3-channel stem, whose input has no
+    gradient: its weight gradient forms dy while staging and returns None) and ``x`` a ``LazyBN``
+    (a training BN's output, staged from y)."""
+    if _stem_wgrad_ok(dy, x, stride, pad, kh, kw, dbias):
+        return _stem_wgrad(dy, x, dw, nvalid, defer)
     if isinstance(dy, bs.LazyGrad):
         # the BN input gradient stored by one elementwise pass (bnx_dy_kernel; staging it from
         # (d, y) in the weight gradient was slower: profiles/r4/bnx/ab_steps.md), then the plain
@@ -693,6 +712,44 @@ def conv2d_wgrad(dy, x, stride, pad, kh, kw, dw, dbias=None, nvalid=None, defer=
                            device=dy.device)
         _call("dba_xcolsum", dy.data_ptr(), N * Ho * Wo * Cout, Ho * Wo, _ptr(_i32(nvalid)), G, N, Cout,
               dbias.data_ptr(), dbias.stride(0), part.data_ptr(), _stream())
+    return None
+
+
+_STEM_PER = 32 * 27   # the stem weight gradient's [32][3][3][3] elements
+
+
+def _stem_wgrad_ok(dy, x, stride, pad, kh, kw, dbias) -> bool:
+    """The 3 -> 32 channel 3x3 stride-1 stem (xwgrad_stem.hip) of a stored input."""
+    if not _STEM_WGRAD or dbias is not None or isinstance(x, bs.LazyBN) or (stride, pad, kh, kw) != (1, 1, 3, 3):
+        return False
+    d = dy.d if isinstance(dy, bs.LazyGrad) else dy
+    if x.dim() != 5 or x.shape[-1] != 3 or x.dtype != _F32 or d.dtype != _F32 or d.shape[-1] != 32:
+        return False
+    G, N, H, W, _ = x.shape
+    return tuple(d.shape) == (G, N, H, W, 32) and int(_L.dba_xwgrad_stem_ws_floats(G, N, H, W, 3, 32)) > 0
+
+
+def _stem_wgrad(dy, x, dw, nvalid, defer):
+    """Stem weight gradient: one 256-pixel slab per workgroup (exact fp32 FMAs), reduced by the
+    batched slab reduction with ``mchunk`` 256; a ``LazyGrad`` dy is formed while staging."""
+    lg = dy if isinstance(dy, bs.LazyGrad) else None
+    d = _act(lg.d if lg is not None else dy, _F32, "wgrad dy")
+    y = None
+    if lg is not None:
+        y = _act(lg.y, _F32, "BN input")
+        assert y.shape == d.shape and y.stride(0) == d.stride(0)
+    x = _act(x, _F32, "wgrad x")
+    assert dw.dtype == torch.float32 and _inner_contig(dw) and dw[0].numel() == _STEM_PER
+    G, N, H, W, _ = x.shape
+    wsb = torch.empty(int(_L.dba_xwgrad_stem_ws_floats(G, N, H, W, 3, 32)), dtype=_F32, device=x.device)
+    nv = _i32(nvalid)
+    _call("dba_xwgrad_stem", d.data_ptr(), d.stride(0), _ptr(y), _ptr(lg.stat.coef) if lg is not None else None,
+          x.data_ptr(), x.stride(0), wsb.data_ptr(), _ptr(nv), G, N, H, W, _stream())
+    entry = ([wsb.data_ptr(), dw.data_ptr(), dw.stride(0), _STEM_PER, _ptr(nv) or 0, N, H * W, 256, G, 0], wsb, nv)
+    if defer is not None:
+        defer.append(entry)
+    else:
+        wgrad_flush([entry])
     return None
 
 

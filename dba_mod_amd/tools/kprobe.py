@@ -3,7 +3,8 @@
 BN conv ``bn1``-``bn3`` (10 replicas x 64 images; ResNet stages 1-3: 32x32 x 32, 16x16 x 64,
 8x8 x 128 channels: a 3x3 conv with the BN statistics in its epilogue, the lazy BN+ReLU
 consumed by a second conv, and the fused backward finish), as ``scripts/gpu/pmc_bn.sh``
-profiles them."""
+profiles them; ``blk`` / ``stemblk``: the fused evaluation BasicBlock of the 32-wide stage /
+the stem + layer1.0 block on 17 x 1024 images (``xblock.hip``)."""
 from __future__ import annotations
 
 import sys
@@ -39,6 +40,25 @@ def main() -> int:
     for name in which:
         if name.startswith("bn"):
             _bn_probe(name, dev)
+        elif name in ("blk", "stemblk"):
+            G, N, C = 17, 1024, 32
+            w1, w2 = [torch.randn(G, C, 3, 3, C, device=dev) * 0.06 for _ in range(2)]
+            for w in (w1, w2):
+                H.split_weights(w, C * 9 * C, C * 9 * C, H._amax_w(w, C * 9 * C, C * 9 * C))
+            b1, b2 = torch.zeros(G, C, device=dev), torch.zeros(G, C, device=dev)
+            if name == "blk":
+                x = torch.relu(torch.randn(G, N, 32, 32, C, device=dev))
+                for _ in range(3):
+                    with H.amax_arena(G, dev):
+                        H.basic_block_eval(x, w1, b1, w2, b2)
+            else:
+                img = torch.rand(G, N, 32, 32, 3, device=dev)
+                w0 = torch.randn(G, C, 3, 3, 3, device=dev) * 0.3
+                H.split_weights(w0, C * 27, C * 27, H._amax_w(w0, C * 27, C * 27))
+                b0 = torch.zeros(G, C, device=dev)
+                for _ in range(3):
+                    with H.amax_arena(G, dev):
+                        H.stem_block_eval(img, w0, b0, w1, b1, w2, b2)
         elif name.startswith("f32:"):
             # fp32-family forward of a bench_kernels shape (e.g. f32:eval.layer1), 3 calls
             from dba_mod_amd.tools.bench_kernels import SHAPES

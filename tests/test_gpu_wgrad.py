@@ -114,3 +114,81 @@ def test_wgrad_halo_deterministic_and_group_size_independent(H, W, C):
     assert torch.equal(full, run(slice(0, G)))
     for i in range(G):
         assert torch.equal(run(slice(i, i + 1))[0], full[i]), i
+
+
+# ------------------------------------------------------------------ the 3-channel stem
+def _stem_case(dev, G, N, nv, W, seed, lazy):
+    g = torch.Generator().manual_seed(seed)
+    x = torch.rand(G, N, W, W, 3, generator=g).to(dev)           # image values in [0, 1]
+    d = torch.randn(G, N, W, W, 32, generator=g).to(dev)
+    for i in range(G):
+        d[i, nv[i]:] = 0
+    if not lazy:
+        return x, d, d.double()
+    y = torch.randn(G, N, W, W, 32, generator=g).to(dev) * 2 + 0.5
+    coef = torch.zeros(G, bs.ROWS, 32, device=dev)
+    coef[:, bs.A] = (torch.rand(G, 32, generator=g) + 0.5).to(dev)
+    coef[:, bs.B] = (torch.randn(G, 32, generator=g) * 0.1).to(dev)
+    coef[:, bs.K] = (torch.randn(G, 32, generator=g) * 0.1).to(dev)
+    sh = (G, 1, 1, 1, 32)
+    dyv = coef[:, bs.A].double().reshape(sh) * d.double() + coef[:, bs.B].double().reshape(sh) * y.double() \
+        + coef[:, bs.K].double().reshape(sh)
+    for i in range(G):
+        dyv[i, nv[i]:] = 0
+    st = bs.BnStat(coef, None, None)
+    return x, bs.LazyGrad(d, y, st), dyv
+
+
+@pytest.mark.parametrize("G,N,nv,W,lazy", [(2, 3, (3, 1), 32, False), (3, 2, (2, 0, 1), 32, True),
+                                           (1, 64, (64,), 32, True), (2, 2, (2, 1), 64, False),
+                                           (2, 2, (1, 2), 64, True)])
+def test_stem_wgrad_vs_fp64_and_implicit_gemm(H, R64, G, N, nv, W, lazy):
+    """dW of the 3 -> 32 stem (CIFAR 32-wide, Tiny 64-wide images), stored or lazy BN input
+    gradient, partly valid / empty replicas, deferred and immediate slab reduction into a
+    strided flat view (accumulating)."""
+    dev = torch.device("cuda")
+    x, dy, dyv = _stem_case(dev, G, N, nv, W, 300 + G * 10 + N + W, lazy)
+    nvalid = torch.tensor(nv, dtype=torch.int32, device=dev)
+    per = 32 * 27
+    flat = torch.zeros(G, per + 64, device=dev)
+    dw = flat[:, :per].view(G, 32, 3, 3, 3)
+    assert H.set_stem_wgrad(-1) == 1
+    defer = []
+    assert H.conv2d_wgrad(dy, x, 1, 1, 3, 3, dw, None, nvalid=nvalid, defer=defer) is None
+    assert len(defer) == 1
+    H.wgrad_flush(defer)
+    H.conv2d_wgrad(dy, x, 1, 1, 3, 3, dw, None, nvalid=nvalid)             # immediate reduce
+    assert flat[:, per:].abs().max().item() == 0.0, "wrote past its view"
+    ref = torch.zeros(G, 32, 3, 3, 3, dtype=torch.float64)
+    R64.conv2d_wgrad(dyv.cpu(), x.double().cpu(), 1, 1, 3, 3, ref, None)
+    # the implicit-GEMM weight gradient of the same (stored) dy
+    old = torch.zeros(G, 32, 3, 3, 3, device=dev)
+    prev = H.set_stem_wgrad(0)
+    try:
+        H.conv2d_wgrad(dyv.float().contiguous(), x, 1, 1, 3, 3, old, None, nvalid=nvalid)
+    finally:
+        H.set_stem_wgrad(prev)
+    for i in range(G):
+        if nv[i] == 0:
+            assert flat[i].abs().max().item() == 0.0
+            continue
+        e1, e0 = _rel(dw[i], 2 * ref[i]), _rel(old[i], ref[i])
+        assert e1 < 1e-6, f"replica {i}: stem wgrad {e1:.2e} (implicit GEMM {e0:.2e})"
+
+
+def test_stem_wgrad_deterministic_and_group_size_independent(H):
+    dev = torch.device("cuda")
+    G, N = 3, 4
+    x, dy, _ = _stem_case(dev, G, N, (N,) * G, 32, 77, True)
+
+    def run(sl):
+        lg = bs.LazyGrad(dy.d[sl].contiguous(), dy.y[sl].contiguous(),
+                         bs.BnStat(dy.stat.coef[sl].contiguous(), None, None))
+        dw = torch.zeros(lg.d.shape[0], 32, 3, 3, 3, device=dev)
+        H.conv2d_wgrad(lg, x[sl].contiguous(), 1, 1, 3, 3, dw, None)
+        return dw
+
+    full = run(slice(0, G))
+    assert torch.equal(full, run(slice(0, G)))
+    for i in range(G):
+        assert torch.equal(run(slice(i, i + 1))[0], full[i]), i
