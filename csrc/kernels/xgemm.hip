@@ -1755,9 +1755,17 @@ int xconv_go(const XArgs& a, long long Mmax, int G, int nclass, hipStream_t st) 
 // accumulators), at most kKslabMax slabs (more go through HBM + the reduce / BN pass).  Serial
 // slabs cost the launch its split-K parallelism: at 8 slabs (stage 4) the 10-client step's split
 // convs took 385 vs 352 us with the reduce passes included (profiles/r4/kslab/).
-constexpr int kKslabMax = 2;
+// split-K policy (per-replica geometry only: any setting keeps world-1 == world-N bits):
+// target tiles, minimum k-steps per slab, maximum slabs, maximum in-block slabs (KS)
+struct SplitPolicy {
+  int target = 128, min_k = 8, max_s = 8, kslab_max = 2;
+};
+SplitPolicy& split_policy() {
+  static SplitPolicy p;
+  return p;
+}
 int xconv_ks(const XArgs& a, long long M, int G, int vec, hipStream_t st) {
-  if (a.kslab > kKslabMax || a.Ncol <= 64 || a.Cs % 32 || vec < 4 || a.splitk != 1 || a.kslab < 2) return -100;
+  if (a.kslab > split_policy().kslab_max || a.Ncol <= 64 || a.Cs % 32 || vec < 4 || a.splitk != 1 || a.kslab < 2) return -100;
   if (a.lz_coef) return xconv_go<64, 128, 2, 2, 32, false, true, true>(a, M, G, 1, st);
   if (a.wp) return xconv_go<64, 128, 2, 2, 32, true, false, true>(a, M, G, 1, st);
   return xconv_go<64, 128, 2, 2, 32, false, false, true>(a, M, G, 1, st);
@@ -1913,7 +1921,8 @@ int xsplitk(long long M, int /*G*/, int Ncol, int K) {
   // 128: a lone client's stage-3 convs (64 tiles of 64 rows) split in two — lone step 1.95 ->
   // 1.85 ms, the 10-client round's training time unchanged (202.4 vs 202.6 ms, r2c_iter1);
   // finer slabs were slower in the bench (348 -> 368 ms per round, profiles/sk_r3/)
-  constexpr int kTarget = 128, kMinK = 8, kMaxS = 8;   // tiles; k-steps per slab; slabs
+  const int kTarget = split_policy().target, kMinK = split_policy().min_k;   // tiles; k-steps per slab
+  const int kMaxS = std::min(kSkMax, split_policy().max_s);                  // slabs
   const long long tiles = (long long)ceil_div(M, 64) * ceil_div(Ncol, bn);
   if (tiles >= kTarget) return 1;
   const int nkt = (K + 31) / 32;
@@ -1954,6 +1963,16 @@ ClassGeom dgrad_classes(int H, int W, int Cin, int Cout, int KH, int KW, int s, 
 
 // patch-reuse weight gradient (xwgrad_halo.hip) on / off (tests: A/B against the implicit GEMM
 // on the same slabs); returns the previous
+// the split-K policy (negative: keep); returns 0 (tools / A-B runs: tools.bench_step --split)
+DBA_EXPORT int dba_xsplit_policy(int target, int min_k, int max_s, int kslab_max) {
+  SplitPolicy& p = split_policy();
+  if (target > 0) p.target = target;
+  if (min_k > 0) p.min_k = min_k;
+  if (max_s > 0) p.max_s = std::min(max_s, kSkMax);
+  if (kslab_max > 0) p.kslab_max = kslab_max;
+  return 0;
+}
+
 DBA_EXPORT int dba_xwgrad_halo_set(int on) {
   const int prev = wgrad_halo_on();
   if (on >= 0) wgrad_halo_on() = on;

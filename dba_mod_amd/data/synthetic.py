@@ -194,9 +194,23 @@ def synthetic_image_pair(kind: str, seed: int = 1, train_size: Optional[int] = N
     # accuracy with moderate margins, attackers reaching ~100% local ASR in their poison
     # epochs.  Low-clutter/high-noise images are separable with huge logit margins and a
     # pixel trigger then never beats the clean evidence (local ASR < 10%).
+    #
+    # Attack window (round 5, profiles/r5/calib/): the DBA triggers must compose the way the
+    # paper's do — a single local trigger partial, the union of four near-complete — and a
+    # MNIST backdoor must outlive a few benign rounds.  CIFAR: 15 % of the images have a
+    # saturated white top row (bright sky), on which the row-0 local triggers are invisible, so
+    # no single local trigger carries the global one (ASR 13 / 12 / 22 % after the first three
+    # poison rounds, 100 % after the fourth, on two warm-start lengths; a 3-row or 30 % sky
+    # kills the attack, none lets the first trigger reach 93-100 %).  MNIST: digits are
+    # size-normalised into the central 20 x 20 box like the real set (a 4-pixel black border:
+    # the trigger rows are never lit by benign data, so benign updates do not unlearn the
+    # backdoor) and classes share half their template (smaller margins): global ASR 84-86 %
+    # after round 12, 47-56 % still at round 19 (was 7 %).
     kw = {"coarse": coarse, "noise": 0.05, "shared": 0.6, "clutter": 0.5}
+    if kind == "cifar":
+        kw.update({"sky": 0.15, "sky_rows": 1})
     if kind == "mnist":
-        kw = {"coarse": 5, "noise": 0.05, "shared": 0.3, "clutter": 0.0, "strokes": True, "shift": 2}
+        kw = {"coarse": 5, "noise": 0.05, "shared": 0.5, "clutter": 0.0, "strokes": True, "shift": 2, "margin": 4}
     if noise is not None:
         kw["noise"] = float(noise)
     if shared is not None:

@@ -32,10 +32,15 @@ def main(argv=None) -> int:
     ap.add_argument("--clients", type=int, default=0,
                     help="keep only the k longest clients (k=1: the lone-attacker latency regime)")
     ap.add_argument("--dtype", choices=("fp32", "bf16"), default="fp32")
+    ap.add_argument("--split", default=None,
+                    help="split-K policy target,min_k,max_s,kslab_max (ops.hip.set_split_policy)")
     ap.add_argument("--rccl", action="store_true",
                     help="create a world-1 RCCL communicator first (one all-reduce): its effect on step time")
     args = ap.parse_args(argv)
     dev = torch.device("cuda")
+    if args.split:
+        from ..ops import hip as H
+        H.set_split_policy(*[int(v) for v in args.split.split(",")])
     if args.rccl:
         from ..parallel.dist import init_distributed
         os.environ.update(DBA_FORCE_PG="1", MASTER_ADDR="127.0.0.1", MASTER_PORT=os.environ.get("MASTER_PORT", "29561"))
@@ -72,7 +77,7 @@ def main(argv=None) -> int:
         torch.cuda.synchronize()
         for t in range(T):
             times[int(active[t])].append(ev[t][0].elapsed_time(ev[t][1]))
-    out = {"steps": int(T), "groups": G, "dtype": args.dtype,
+    out = {"steps": int(T), "groups": G, "dtype": args.dtype, "split": args.split,
            "ms_per_step_by_active": {k: round(float(np.median(v)), 3) for k, v in sorted(times.items())},
            "steps_by_active": {k: len(v) // args.reps for k, v in sorted(times.items())}}
     print(json.dumps(out))
