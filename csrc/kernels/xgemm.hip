@@ -59,6 +59,7 @@ struct XArgs {
   int sp, os, dsg, relu;
   int splitk, tiles_n;
   int kslab;                                 // xconv KS: split-K slabs summed in the block (1: none)
+  int xcd;                                   // xhalo: XCD-aware block order (common.hpp xcd_block)
   long long zstride;                         // split-K: slab z at out + z * zstride
   const int* amax_src;                       // H: max |src| slot [kAmaxSub][amax_src_ld] (common.hpp)
   const int* amax_w;                         // H: max |w| slot, indexed by weight slot
@@ -183,6 +184,9 @@ __device__ __forceinline__ bool sk_combine(const XArgs& a, float* Ct, const long
 // arithmetic of a.kslab split-K launches summed in z order (xsplitk_reduce / sk_combine), so a
 // grouped launch reproduces a lone client's split-K bits without the slab round trip through
 // HBM or the separate reduce / statistics pass
+// (A 4-stage register pipeline for the lone client's 32 x 128 tiles — loads issued 4 k-steps
+// ahead instead of 2 — measured no faster: lone step 1.640 / 1.638 vs 1.646 / 1.589 ms, same
+// box, profiles/r5/deep/.  Those launches are not bound by operand-load latency.)
 template <int BM, int BN, int WM, int WN, int VEC, bool PW = false, bool LZ = false, bool KS = false>
 __global__ __launch_bounds__(256, KS ? 2 : XCONV_MINB) void xconv_kernel(const XArgs a) {
   static_assert(!LZ || VEC >= 4, "lazy BN operand: 4-channel vectors");
@@ -573,9 +577,10 @@ __global__ __launch_bounds__(256) void xhalo_kernel(const XArgs a) {
   __shared__ __attribute__((aligned(16))) uint4 scbuf[SC ? P * SPL : 4];
   __shared__ long long orow[BM];
 
-  const int g = blockIdx.y;
+  int bx, g;
+  xcd_block(a.xcd, bx, g);
   const int HT = a.Ho / TR;                               // row tiles per image
-  const int tn = blockIdx.x % a.tiles_n, tm = blockIdx.x / a.tiles_n;
+  const int tn = bx % a.tiles_n, tm = bx / a.tiles_n;
   const int img = tm / HT, h0 = (tm - img * HT) * TR;
   const int n0 = tn * BN;
   const int nv_img = valid_rows(a.nvalid, g, a.N);
@@ -1785,10 +1790,17 @@ int xconv_tile(const XArgs& a, long long Mmax, int G, int nclass, int bm, hipStr
 
 bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
+// XCD-aware block order of the halo / block kernels (dba_xcd_set)
+int& xcd_on() {
+  static int on = 1;
+  return on;
+}
+
 template <int W, int CS, int BM, int BN, int WM, int WN, bool PRE = false, bool LZ = false, bool SC = false>
 int xhalo_go(const XArgs& a, int G, hipStream_t st) {
   XArgs b = a;
   b.tiles_n = ceil_div(a.Ncol, BN);
+  b.xcd = xcd_on();
   const dim3 grid((unsigned)(a.N * (a.Ho / (BM / W)) * b.tiles_n), G, 1);
   hipLaunchKernelGGL((xhalo_kernel<W, CS, BM, BN, WM, WN, PRE, LZ, SC>), grid, dim3(256), 0, st, b);
   DBA_LAUNCH_CHECK();
@@ -1971,6 +1983,13 @@ DBA_EXPORT int dba_xsplit_policy(int target, int min_k, int max_s, int kslab_max
   if (max_s > 0) p.max_s = std::min(max_s, kSkMax);
   if (kslab_max > 0) p.kslab_max = kslab_max;
   return 0;
+}
+
+// XCD-aware block order of the halo convs and fused blocks on / off (A/B); returns the previous
+DBA_EXPORT int dba_xcd_set(int on) {
+  const int prev = xcd_on();
+  if (on >= 0) xcd_on() = on;
+  return prev;
 }
 
 DBA_EXPORT int dba_xwgrad_halo_set(int on) {

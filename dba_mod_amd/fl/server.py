@@ -167,6 +167,9 @@ class Server:
             plr = params["pretrain_lr"]
             self.pretrain(int(params["pretrain_rounds"]), float(params["pretrain_eta"]),
                           float(plr) if plr is not None else None)
+        if params["is_poison"]:
+            # the lone-client graph (a poison round's attacker tail) captured before round 1
+            self.trainer.prewarm(1)
 
     # ------------------------------------------------------------------ model
     def _init_model(self) -> None:

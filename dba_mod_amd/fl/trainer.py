@@ -126,6 +126,11 @@ class GroupTrainer:
         self.persistent = (self.spec.arch == "loan" and self.device.type == "cuda" and self.alpha == 1.0
                            and not self.trace and ops.backend_name(self.device) == "hip"
                            and os.environ.get("DBA_MLP_PERSIST", "1") != "0")
+        # per-client epoch slots of the step statistics: sized once for the longest phase the
+        # config can run (benign and poison rounds then share one buffer set and one captured
+        # graph per group size, so a poison round captures nothing new)
+        ep = max(1, int(params["internal_epochs"]), int(params["internal_poison_epochs"]))
+        self.min_slots = 1 << (ep - 1).bit_length()
 
     # ------------------------------------------------------------------ step
     def _step(self, b: _GroupBuffers) -> None:
@@ -169,6 +174,18 @@ class GroupTrainer:
         if key not in self._bufs:
             self._bufs[key] = _GroupBuffers(self.spec, G, self.B, max_slots, self.device, self.fg)
         return self._bufs[key]
+
+    def prewarm(self, G: int) -> None:
+        """Allocate the G-client buffers and capture their step graph ahead of use (an
+        all-inactive descriptor: every kernel skips every replica).  The server does this for
+        the lone-client shape at start-up, so the first poison round's lone attacker tail does
+        not pay the capture (~45 ms) inside the attack window."""
+        if not self.use_graph or self.persistent:
+            return
+        b = self._buffers(G, self.min_slots)
+        if b.graph is None:
+            b._cur = torch.zeros(b.D, dtype=torch.int32, device=self.device)
+            self._run_step(b)
 
     def _run_step(self, b: _GroupBuffers) -> None:
         if not self.use_graph:
@@ -219,7 +236,7 @@ class GroupTrainer:
         if G == 0:
             return None
         max_slots = max(sum(ph.internal_epochs for ph in c.phases) for c in clients)
-        max_slots = 1 << (max_slots - 1).bit_length()
+        max_slots = max(self.min_slots, 1 << (max_slots - 1).bit_length())
         b = self._buffers(G, max_slots)
         T = max(len(c.steps) for c in clients)
         host = native.pack_steps(clients, G, self.B, T, max_slots)   # [T, D] int32 (C++ runtime)

@@ -62,8 +62,10 @@ def test_mnist_single_shot_asr_jumps(tmp_path):
     """SURVEY §7.3 acceptance: after a benign warm start, the global ASR jumps in the
     single-shot poison round (adversary 41, round 12; scale 100, eta 0.1 = model
     replacement, ``image_train.py:166-171``) — BASELINE.json config #1 on CPU."""
+    # (the round-4 generator — full-frame strokes, 30 % shared templates — learns in 5 CPU
+    # warm-start rounds at this size; the calibrated attack window is tests/test_attack_window.py)
     p = mnist_params(tmp_path, synthetic_train_size=12000, synthetic_test_size=1000, eval_batch_size=500,
-                     pretrain_rounds=5)
+                     pretrain_rounds=5, synthetic_shared=0.3, synthetic_margin=0)
     s = Server(p, DistCtx(), write_outputs=False)
     r11 = s.run_round(11)
     r12 = s.run_round(12)

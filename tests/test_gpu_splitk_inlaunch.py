@@ -164,3 +164,4 @@ def test_inlaunch_combine_many_launches_in_one_graph(H):
         torch.cuda.synchronize()
         for a, b in zip(outs, ref):
             assert torch.equal(a, b)
+
