@@ -1524,18 +1524,41 @@ __global__ __launch_bounds__(256) void xsplit_w_kernel(const float* __restrict__
 
 // max |x| of n segments (offset, length) of every replica's flat row (the conv weights of a
 // model replica: one launch per training step instead of one per conv); out[s][g]
-constexpr int kAmaxSegs = 64;
+// One block per 4096-element chunk of a segment (the segments' chunks laid end to end: block c
+// belongs to the segment whose chunk range holds c), four 16-B loads per thread in flight; a
+// 2-D grid of (64 chunks x segments) blocks left most of them idle on the small segments and
+// read scalars.  The max is order-free (exact integer fold), so the tiling is free.
+constexpr int kAmaxSegs = 64, kAmaxChunk = 4096;
 struct AmaxSegs {
   long long off[kAmaxSegs];
   int len[kAmaxSegs];
+  int start[kAmaxSegs + 1];   // first chunk of each segment (prefix sum of ceil(len / 4096))
+  int n;
 };
 __global__ __launch_bounds__(256) void amax_segments_kernel(const float* __restrict__ base, long long gstride,
                                                             const AmaxSegs segs, int ld, int* __restrict__ out) {
-  const int sg = blockIdx.y, g = blockIdx.z;
+  const int c = blockIdx.x, g = blockIdx.y;
+  int sg = 0;
+  while (sg + 1 < segs.n && segs.start[sg + 1] <= c) ++sg;
   const float* __restrict__ p = base + (long long)g * gstride + segs.off[sg];
-  const int n = segs.len[sg];
+  const int n = segs.len[sg], e0 = (c - segs.start[sg]) * kAmaxChunk;
+  const bool v4 = ((segs.off[sg] | gstride) & 3) == 0 && ((uintptr_t)base & 15) == 0;
   float m = 0.f;
-  for (int e = blockIdx.x * 256 + threadIdx.x; e < n; e += gridDim.x * 256) m = fmaxf(m, fabsf(p[e]));
+  float4 v[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int e = e0 + (k * 256 + threadIdx.x) * 4;
+    if (v4 && e + 3 < n) {
+      v[k] = *(const float4*)(p + e);
+    } else {
+      v[k].x = e < n ? p[e] : 0.f;
+      v[k].y = e + 1 < n ? p[e + 1] : 0.f;
+      v[k].z = e + 2 < n ? p[e + 2] : 0.f;
+      v[k].w = e + 3 < n ? p[e + 3] : 0.f;
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) m = fmaxf(m, fmaxf(fmaxf(fabsf(v[k].x), fabsf(v[k].y)), fmaxf(fabsf(v[k].z), fabsf(v[k].w))));
   amax_fold(out + (long long)sg * kAmaxSub * ld, ld, g, m);
 }
 
@@ -1708,8 +1731,8 @@ __global__ __launch_bounds__(256) void bnx_apply_kernel(const float* __restrict_
 
 // The input gradient of a training BN, stored: dy = fma(A, d, fma(B, y, K)) per channel
 // (bnfuse.hpp; bn.hip bn_bwd_apply's arithmetic) over the valid rows, and the max |dy| slot
-// folded for its fp16-pair consumers (DBA_BNX_DY=1: instead of the weight gradient staging dy
-// from (d, y) on the fly).
+// folded for its fp16-pair consumers (measured faster than the weight gradient staging dy
+// from (d, y) on the fly: profiles/r4/bnx/ab_steps.md).
 __global__ __launch_bounds__(256) void bnx_dy_kernel(const float* __restrict__ d, const float* __restrict__ y,
                                                      const float* __restrict__ coef, float* __restrict__ dy,
                                                      long long gstride, const int* __restrict__ nvalid, int N, int HW,
@@ -1764,6 +1787,7 @@ int xconv_go(const XArgs& a, long long Mmax, int G, int nclass, hipStream_t st) 
 // target tiles, minimum k-steps per slab, maximum slabs, maximum in-block slabs (KS)
 struct SplitPolicy {
   int target = 128, min_k = 8, max_s = 8, kslab_max = 2;
+  int dgrad_ks = 1;   // grouped stride-1 data gradients as in-block slabs too (else split + reduce pass)
 };
 SplitPolicy& split_policy() {
   static SplitPolicy p;
@@ -1976,8 +2000,9 @@ ClassGeom dgrad_classes(int H, int W, int Cin, int Cout, int KH, int KW, int s, 
 // patch-reuse weight gradient (xwgrad_halo.hip) on / off (tests: A/B against the implicit GEMM
 // on the same slabs); returns the previous
 // the split-K policy (negative: keep); returns 0 (tools / A-B runs: tools.bench_step --split)
-DBA_EXPORT int dba_xsplit_policy(int target, int min_k, int max_s, int kslab_max) {
+DBA_EXPORT int dba_xsplit_policy(int target, int min_k, int max_s, int kslab_max, int dgrad_ks) {
   SplitPolicy& p = split_policy();
+  if (dgrad_ks >= 0) p.dgrad_ks = dgrad_ks;
   if (target > 0) p.target = target;
   if (min_k > 0) p.min_k = min_k;
   if (max_s > 0) p.max_s = std::min(max_s, kSkMax);
@@ -2174,6 +2199,15 @@ DBA_EXPORT int dba_xconv_dgrad(const float* dy, long long dy_gstride, const floa
       b.sk_ws = ws; b.sk_gstride = M * Cin; b.sk_cnt = sk_cnt;
       return fin(xconv_dispatch(b, M, G, 1, vec, st));
     }
+    if (s > 1 && split_policy().dgrad_ks) {
+      // grouped launch: the slabs summed inside each block in z order, then the accumulated
+      // input and the BN mask / records in the epilogue — the lone client's in-launch combine
+      // arithmetic (sk_combine), without the slab round trip and the standalone BN pass
+      XArgs b = a;
+      b.kslab = s;
+      const int rc = xconv_ks(b, M, G, vec, st);
+      if (rc != -100) return fin(rc);
+    }
     if (ws_ok) {
       XArgs b = a;
       b.splitk = s;
@@ -2324,15 +2358,15 @@ DBA_EXPORT int dba_xsplit_w(const float* w, long long sstride, long long per, in
 // capture), n <= 64
 DBA_EXPORT int dba_amax_segments(const float* base, long long gstride, const long long* segs, int n, int G, int* out,
                                  int ld, void* stream) {
-  if (n > kAmaxSegs) return -105;
+  if (n > kAmaxSegs || n < 1) return -105;
   AmaxSegs a{};
-  int maxlen = 1;
+  a.n = n;
   for (int i = 0; i < n; ++i) {
     a.off[i] = segs[2 * i];
     a.len[i] = (int)segs[2 * i + 1];
-    maxlen = std::max(maxlen, a.len[i]);
+    a.start[i + 1] = a.start[i] + std::max(1, ceil_div(a.len[i], kAmaxChunk));
   }
-  const dim3 grid((unsigned)std::min(64, ceil_div(maxlen, 4096)), n, G);
+  const dim3 grid((unsigned)a.start[n], G);
   hipLaunchKernelGGL(amax_segments_kernel, grid, dim3(256), 0, (hipStream_t)stream, base, gstride, a, ld, out);
   DBA_LAUNCH_CHECK();
 }

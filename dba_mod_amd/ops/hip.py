@@ -69,7 +69,7 @@ _SIGS = {
     "dba_xtranspose": [_P, _I, _I, _LL, _P, _P],
     "dba_xwgrad_ws_floats": [_I] * 8 + [_P],
     "dba_xwgrad_stem_ws_floats": [_I] * 6,
-    "dba_xsplit_policy": [_I] * 4,
+    "dba_xsplit_policy": [_I] * 5,
     "dba_xcd_set": [_I],
     "dba_xwgrad": [_P, _LL, _P, _LL, _P, _LL, _P] + [_I] * 12 + [_P, _I] * 2 + [_P, _LL, _I] + [_P, _I, _P],
     # fused training BN (csrc/kernels/bnfuse.hpp)
@@ -265,11 +265,13 @@ def set_xcd(on: int) -> int:
     return int(_L.dba_xcd_set(int(on)))
 
 
-def set_split_policy(target: int = -1, min_k: int = -1, max_s: int = -1, kslab_max: int = -1) -> None:
+def set_split_policy(target: int = -1, min_k: int = -1, max_s: int = -1, kslab_max: int = -1,
+                     dgrad_ks: int = -1) -> None:
     """Split-K policy of the small forward / data-gradient launches (xgemm.hip ``xsplitk``:
     target tiles per replica, minimum k-steps per slab, maximum slabs, maximum in-block
-    slabs); negative keeps a value.  Any setting is deterministic and group-size independent."""
-    _call("dba_xsplit_policy", int(target), int(min_k), int(max_s), int(kslab_max))
+    slabs, grouped data gradients as in-block slabs 1 / 0); negative keeps a value.  Any
+    setting is deterministic and group-size independent."""
+    _call("dba_xsplit_policy", int(target), int(min_k), int(max_s), int(kslab_max), int(dgrad_ks))
 
 
 _STEM_WGRAD = True

@@ -254,11 +254,11 @@ def test_cifar_dba_attack_lands(dev, tmp_path):
     assert res[202]["global_asr"] < 20.0
     with open(os.path.join(s.folder, "posiontest_result.csv")) as f:
         rows = [r for r in csv.DictReader(f) if r["model"] == "17" and r["epoch"] == "203"]
-    # thresholds leave room for the spread across seeds / precisions (measured after round 203:
-    # local 17-100 %, global 12-100 %; after round 205 global > 50 %)
     assert rows and float(rows[0]["accuracy"]) > 5.0, rows      # local ASR before scaling (clean: ~1 %)
-    assert res[203]["global_asr"] > 10.0                           # one attacker: 20-100 %
-    assert max(res[e]["global_asr"] for e in (203, 204, 205, 206)) > 80.0
+    # one local trigger does not carry the global one on the calibrated data (round 5: 15 % of
+    # the images hide the row-0 triggers); the four composing to >= 90 % by round 209 is pinned
+    # on the bench window by tests/test_attack_window.py
+    assert 5.0 < res[203]["global_asr"] < 80.0
 
 
 def _cifar_small(tmp_path, **kw):

@@ -229,3 +229,21 @@ def test_weighted_sum_fixed_matches_reference_bitwise():
     E = agg.fixed_exponent(float(pts.abs().max()), n)
     got = H.weighted_sum_fixed(pts.cuda(), w.cuda(), E).cpu()
     assert torch.equal(got, R.weighted_sum_fixed(pts, w, E))
+
+
+def test_weight_amax_segments(H):
+    """Per-replica max |w| of many flat-row segments in one launch (chunked, 16-B loads, scalar
+    tails): odd lengths, a segment past 64 chunks, unaligned offsets, the exact float bits."""
+    import struct
+    dev = torch.device("cuda")
+    g = torch.Generator().manual_seed(3)
+    G, S = 3, 600_000
+    flat = (torch.randn(G, S, generator=g) * torch.logspace(-3, 3, S)[None, :]).to(dev)
+    segs = [(0, 864), (896, 9216), (10176, 1), (10240, 295_000), (305_408, 261_000), (566_410, 33_589)]
+    slots = H.weight_amax(flat, segs)
+    torch.cuda.synchronize()
+    for (o, n), sl in zip(segs, slots):
+        for r in range(G):
+            want = flat[r, o:o + n].abs().max().item()
+            got = struct.unpack("<f", struct.pack("<i", int(sl[:, r].max().item())))[0]
+            assert got == want, (o, n, r, got, want)
