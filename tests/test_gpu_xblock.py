@@ -172,3 +172,4 @@ def test_xcd_block_order_is_bitwise_neutral(H):
     for a, b, nv in zip(outs[0], outs[1], ((7, 3, 5), (5, 3, 4), (7, 3, 5))):
         for i, n in enumerate(nv):   # (rows past a replica's valid images are not written)
             assert torch.equal(a[i, :n], b[i, :n])
+
