@@ -234,18 +234,34 @@ __device__ __forceinline__ void bnf_finalize_block(const BnFuse& f, int g, int c
 #pragma unroll
   for (int q = 0; q < 4; ++q) red[tid][q] = a[q];
   __syncthreads();
-  for (int w = 128; w > 0; w >>= 1) {
-    if (tid < w) {
-      const double v[4] = {red[tid + w][0], red[tid + w][1], red[tid + w][2], red[tid + w][3]};
-      double x[4] = {red[tid][0], red[tid][1], red[tid][2], red[tid][3]};
-      bnf_acc(x, v, f.mode);
+  // the fixed pairwise tree (tid <- tid + w, w = 128 .. 1): the two cross-wave levels through
+  // LDS, the six in-wave levels as shuffles — the same pairs in the same order as an LDS level
+  // each, without their barriers (every combine is commutative)
+  if (tid < 128) {
+    const double v[4] = {red[tid + 128][0], red[tid + 128][1], red[tid + 128][2], red[tid + 128][3]};
+    double x[4] = {red[tid][0], red[tid][1], red[tid][2], red[tid][3]};
+    bnf_acc(x, v, f.mode);
 #pragma unroll
-      for (int q = 0; q < 4; ++q) red[tid][q] = x[q];
-    }
-    __syncthreads();
+    for (int q = 0; q < 4; ++q) red[tid][q] = x[q];
+  }
+  __syncthreads();
+  if (tid >= 64) return;
+  double x[4];
+  {
+    const double v[4] = {red[tid + 64][0], red[tid + 64][1], red[tid + 64][2], red[tid + 64][3]};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) x[q] = red[tid][q];
+    bnf_acc(x, v, f.mode);
+  }
+#pragma unroll
+  for (int w = 32; w > 0; w >>= 1) {
+    double v[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) v[q] = __shfl_down(x[q], w, 64);
+    bnf_acc(x, v, f.mode);   // (lanes >= w compute values no later level reads)
   }
   if (tid != 0) return;
-  const double t[4] = {red[0][0], red[0][1], red[0][2], red[0][3]};
+  const double t[4] = {x[0], x[1], x[2], x[3]};
   float bb = 0.f;
   const float ba = bnf_finalize_channel(f, g, c, t, (double)Mv, &bb);
   if (f.amax_a && ba > 0.f) atomicMax(f.amax_a + (c % kAmaxSub) * f.amax_ld + g, __float_as_int(ba));
