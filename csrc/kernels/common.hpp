@@ -121,21 +121,6 @@ __device__ __forceinline__ int amax_read(const int* amax, int ld, int g) {
   return __builtin_amdgcn_readfirstlane(v);
 }
 
-// XCD-aware block order (cdna_hip_programming.md T1): the hardware deals consecutive blocks
-// round-robin over the 8 XCDs; this bijection gives every XCD a contiguous run of the logical
-// order, so neighbouring tiles (which share halo rows) meet in one XCD's L2.  Pure scheduling:
-// no result depends on it.  Writes the logical (x, y) of this block of a 2-D grid.
-__device__ __forceinline__ void xcd_block(int on, int& bx, int& by) {
-  bx = blockIdx.x;
-  by = blockIdx.y;
-  if (!on) return;
-  const int n = gridDim.x * gridDim.y, orig = blockIdx.x + gridDim.x * blockIdx.y;
-  const int q = n >> 3, r = n & 7, x = orig & 7;
-  const int L = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (orig >> 3);
-  by = L / gridDim.x;
-  bx = L - by * gridDim.x;
-}
-
 __device__ __forceinline__ int valid_rows(const int* nvalid, int g, int n_per_group) {
   return nvalid ? nvalid[g] : n_per_group;
 }

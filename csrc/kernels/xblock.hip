@@ -39,8 +39,6 @@
 #include "common.hpp"
 #include "xmfma.hpp"
 
-extern "C" int dba_xcd_set(int on);   // xgemm.hip: the XCD-aware block order switch
-
 namespace {
 
 struct XBArgs {
@@ -60,7 +58,6 @@ struct XBArgs {
   const uint16_t* w0p; long long w0_sstride;
   const float* b0; long long b0_sstride;
   const int* amax_w0;
-  int xcd;                                 // XCD-aware block order (common.hpp xcd_block)
 };
 
 constexpr int kW = 32, kC = 32, kTR = 8;      // image width, channels, output rows per block
@@ -84,9 +81,8 @@ __global__ __launch_bounds__(256) void xblock_kernel(const XBArgs a) {
   __shared__ float red[3][4];                // block maxima: image (STEM), stem output (STEM), mid
   __shared__ float im[STEM ? kIm : 1];
 
-  int bx, g;
-  xcd_block(a.xcd, bx, g);
-  const int img = bx / (kW / kTR), h0 = (bx % (kW / kTR)) * kTR;
+  const int g = blockIdx.y;
+  const int img = blockIdx.x / (kW / kTR), h0 = (blockIdx.x % (kW / kTR)) * kTR;
   if (img >= valid_rows(a.nvalid, g, a.N)) return;
   const int slot = a.wsel ? a.wsel[g] : g;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -419,7 +415,7 @@ DBA_EXPORT int dba_xblock_fwd(const float* x, long long x_gstride, float* out, l
   if ((long long)N * H * W * C >= (1LL << 29)) return -103;
   XBArgs a{x, x_gstride, out, out_gstride, wsel, w1p, w2p, wp_sstride, b1, b2, b_sstride, nvalid, N,
            amax_x, amax_x_ld, amax_w1, amax_w2, amax_w_ld, amax_out, amax_out_ld,
-           nullptr, 0, nullptr, 0, nullptr, dba_xcd_set(-1)};
+           nullptr, 0, nullptr, 0, nullptr};
   hipLaunchKernelGGL(xblock_kernel<false>, dim3((unsigned)(N * (kW / kTR)), G), dim3(256), 0, (hipStream_t)stream, a);
   DBA_LAUNCH_CHECK();
 }
@@ -444,7 +440,7 @@ DBA_EXPORT int dba_xblock_stem_fwd(const float* img, long long img_gstride, floa
   if ((long long)N * H * W * C >= (1LL << 29)) return -103;
   XBArgs a{img, img_gstride, out, out_gstride, wsel, w1p, w2p, wp_sstride, b1, b2, b_sstride, nvalid, N,
            nullptr, 0, amax_w1, amax_w2, amax_w_ld, amax_out, amax_out_ld,
-           w0p, w0_sstride, b0, b0_sstride, amax_w0, dba_xcd_set(-1)};
+           w0p, w0_sstride, b0, b0_sstride, amax_w0};
   hipLaunchKernelGGL(xblock_kernel<true>, dim3((unsigned)(N * (kW / kTR)), G), dim3(256), 0, (hipStream_t)stream, a);
   DBA_LAUNCH_CHECK();
 }

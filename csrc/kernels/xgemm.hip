@@ -59,7 +59,6 @@ struct XArgs {
   int sp, os, dsg, relu;
   int splitk, tiles_n;
   int kslab;                                 // xconv KS: split-K slabs summed in the block (1: none)
-  int xcd;                                   // xhalo: XCD-aware block order (common.hpp xcd_block)
   long long zstride;                         // split-K: slab z at out + z * zstride
   const int* amax_src;                       // H: max |src| slot [kAmaxSub][amax_src_ld] (common.hpp)
   const int* amax_w;                         // H: max |w| slot, indexed by weight slot
@@ -577,10 +576,9 @@ __global__ __launch_bounds__(256) void xhalo_kernel(const XArgs a) {
   __shared__ __attribute__((aligned(16))) uint4 scbuf[SC ? P * SPL : 4];
   __shared__ long long orow[BM];
 
-  int bx, g;
-  xcd_block(a.xcd, bx, g);
+  const int g = blockIdx.y;
   const int HT = a.Ho / TR;                               // row tiles per image
-  const int tn = bx % a.tiles_n, tm = bx / a.tiles_n;
+  const int tn = blockIdx.x % a.tiles_n, tm = blockIdx.x / a.tiles_n;
   const int img = tm / HT, h0 = (tm - img * HT) * TR;
   const int n0 = tn * BN;
   const int nv_img = valid_rows(a.nvalid, g, a.N);
@@ -1207,25 +1205,46 @@ __global__ __launch_bounds__(256) void xwgrad_kernel(const XWArgs a) {
         }
         return;
       }
-      // the 4 rows are consecutive output pixels of one output row (Wo % 4 == 0): decode once
-      int img = 0, p = 0, q = 0;
-      if (m0 < me) {
-        img = fdiv(m0, a.dHoWo);
-        const int rem = m0 - img * HoWo;
-        p = fdiv(rem, a.dWo);
-        q = rem - p * a.Wo;
-      }
-      const int h = p * a.stride - a.pad + xkh[0];
-      const bool hok = xkv[0] && (unsigned)h < (unsigned)a.H;
-      const int xrow = (img * a.H + h) * a.W;
       unsigned okm = 0u;
+      if (a.Wo % 4 == 0) {
+        // the 4 rows are consecutive output pixels of one output row: decode once
+        int img = 0, p = 0, q = 0;
+        if (m0 < me) {
+          img = fdiv(m0, a.dHoWo);
+          const int rem = m0 - img * HoWo;
+          p = fdiv(rem, a.dWo);
+          q = rem - p * a.Wo;
+        }
+        const int h = p * a.stride - a.pad + xkh[0];
+        const bool hok = xkv[0] && (unsigned)h < (unsigned)a.H;
+        const int xrow = (img * a.H + h) * a.W;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int w = (q + r) * a.stride - a.pad + xkw[0];
-        const bool ok = m0 + r < me && hok && (unsigned)w < (unsigned)a.W;
-        const float4 v = bload4(rX, ok ? ((xrow + w) * a.Cin + xc[0]) * 4 : kOOB);
-        xv[st][r][0] = v.x; xv[st][r][1] = v.y; xv[st][r][2] = v.z; xv[st][r][3] = v.w;
-        okm |= ok ? (0xfu << (r * 4)) : 0u;
+        for (int r = 0; r < 4; ++r) {
+          const int w = (q + r) * a.stride - a.pad + xkw[0];
+          const bool ok = m0 + r < me && hok && (unsigned)w < (unsigned)a.W;
+          const float4 v = bload4(rX, ok ? ((xrow + w) * a.Cin + xc[0]) * 4 : kOOB);
+          xv[st][r][0] = v.x; xv[st][r][1] = v.y; xv[st][r][2] = v.z; xv[st][r][3] = v.w;
+          okm |= ok ? (0xfu << (r * 4)) : 0u;
+        }
+      } else {
+        // narrow outputs (Wo 2 / 1: the 64-wide stem's last stage): the 4 rows may span output
+        // rows or images, decoded per row; the same 4 channel vectors as the scalar path loads
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = m0 + r;
+          int img = 0, p = 0, q = 0;
+          if (m < me) {
+            img = fdiv(m, a.dHoWo);
+            const int rem = m - img * HoWo;
+            p = fdiv(rem, a.dWo);
+            q = rem - p * a.Wo;
+          }
+          const int h = p * a.stride - a.pad + xkh[0], w = q * a.stride - a.pad + xkw[0];
+          const bool ok = m < me && xkv[0] && (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W;
+          const float4 v = bload4(rX, ok ? (((img * a.H + h) * a.W + w) * a.Cin + xc[0]) * 4 : kOOB);
+          xv[st][r][0] = v.x; xv[st][r][1] = v.y; xv[st][r][2] = v.z; xv[st][r][3] = v.w;
+          okm |= ok ? (0xfu << (r * 4)) : 0u;
+        }
       }
       if constexpr (XLZ) s_xok[st] = okm;
     } else {
@@ -1814,17 +1833,10 @@ int xconv_tile(const XArgs& a, long long Mmax, int G, int nclass, int bm, hipStr
 
 bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
-// XCD-aware block order of the halo / block kernels (dba_xcd_set)
-int& xcd_on() {
-  static int on = 1;
-  return on;
-}
-
 template <int W, int CS, int BM, int BN, int WM, int WN, bool PRE = false, bool LZ = false, bool SC = false>
 int xhalo_go(const XArgs& a, int G, hipStream_t st) {
   XArgs b = a;
   b.tiles_n = ceil_div(a.Ncol, BN);
-  b.xcd = xcd_on();
   const dim3 grid((unsigned)(a.N * (a.Ho / (BM / W)) * b.tiles_n), G, 1);
   hipLaunchKernelGGL((xhalo_kernel<W, CS, BM, BN, WM, WN, PRE, LZ, SC>), grid, dim3(256), 0, st, b);
   DBA_LAUNCH_CHECK();
@@ -2008,13 +2020,6 @@ DBA_EXPORT int dba_xsplit_policy(int target, int min_k, int max_s, int kslab_max
   if (max_s > 0) p.max_s = std::min(max_s, kSkMax);
   if (kslab_max > 0) p.kslab_max = kslab_max;
   return 0;
-}
-
-// XCD-aware block order of the halo convs and fused blocks on / off (A/B); returns the previous
-DBA_EXPORT int dba_xcd_set(int on) {
-  const int prev = xcd_on();
-  if (on >= 0) xcd_on() = on;
-  return prev;
 }
 
 DBA_EXPORT int dba_xwgrad_halo_set(int on) {
@@ -2312,8 +2317,8 @@ DBA_EXPORT int dba_xwgrad(const float* dy, long long dy_gstride, const float* x,
       DBA_LAUNCH_CHECK();
     }
   }
-  const bool v4 = Cin % 4 == 0 && Cout % 4 == 0 && Wo % 4 == 0 && aligned16(dy) && aligned16(x) &&
-                  dy_gstride % 4 == 0 && x_gstride % 4 == 0;
+  const bool v4 = Cin % 4 == 0 && Cout % 4 == 0 && aligned16(dy) && aligned16(x) && dy_gstride % 4 == 0 &&
+                  x_gstride % 4 == 0;
   // output-channel tile: 128 for wide layers (64 for a lone client's stage-3/4 weight gradients
   // when a launch would be short of blocks measured within run-to-run spread: lone step 1.774 ->
   // 1.763 ms, scripts/gpu/r2c_iter10.sh).  The tile never changes a bit (same per-element row

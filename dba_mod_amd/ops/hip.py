@@ -70,7 +70,6 @@ _SIGS = {
     "dba_xwgrad_ws_floats": [_I] * 8 + [_P],
     "dba_xwgrad_stem_ws_floats": [_I] * 6,
     "dba_xsplit_policy": [_I] * 5,
-    "dba_xcd_set": [_I],
     "dba_xwgrad": [_P, _LL, _P, _LL, _P, _LL, _P] + [_I] * 12 + [_P, _I] * 2 + [_P, _LL, _I] + [_P, _I, _P],
     # fused training BN (csrc/kernels/bnfuse.hpp)
     "dba_bnx_rows": [_P, _P, _P, _LL, _P, _I, _I, _I, _P, _F, _P],
@@ -257,12 +256,6 @@ def set_wgrad_halo(on: int) -> int:
     """Patch-reuse weight gradient of the narrow stages' 3x3 convs (xwgrad_halo.hip) on / off;
     -1 queries.  Returns the previous setting (tests: A/B against the implicit GEMM)."""
     return int(_L.dba_xwgrad_halo_set(int(on)))
-
-
-def set_xcd(on: int) -> int:
-    """XCD-aware block order of the halo convs and fused evaluation blocks (common.hpp
-    ``xcd_block``) on / off; -1 queries.  Pure scheduling: results are bit-identical."""
-    return int(_L.dba_xcd_set(int(on)))
 
 
 def set_split_policy(target: int = -1, min_k: int = -1, max_s: int = -1, kslab_max: int = -1,

@@ -176,11 +176,8 @@ def main(argv=None) -> int:
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--json", default=None)
     ap.add_argument("--only", default="", help="substring filter on shape names")
-    ap.add_argument("--xcd", type=int, default=-1, help="XCD-aware block order 1 / 0 (default: the library's)")
     args = ap.parse_args(argv)
     dev = torch.device("cuda")
-    if args.xcd >= 0:
-        H.set_xcd(args.xcd)
     rows = []
     for name, G, N, Hh, Cin, Cout, k, s, p in SHAPES:
         if args.only not in name:

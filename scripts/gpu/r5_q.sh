@@ -18,3 +18,9 @@ grep -E "bnx_finalize|bnx_tile|bnx_dy|amax_seg" $O/step${c}_trace.md
 done) || exit 1
 timeout -k 10 400 python bench.py --steps 20 --warmup 5 > $O/bench.log 2>&1 || { tail -20 $O/bench.log; exit 1; }
 python3 -c "import json; j=json.loads(open('$O/bench.log').read().strip().splitlines()[-1]); print('bench', j['value'], j['state_sha'], j['rounds'][6])"
+# Tiny-ImageNet-200: which kernels dominate its round
+(cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/tiny -o tiny -- python3 $R/bench.py --config $R/configs/tiny_200.yaml --pretrain-rounds 0 --steps 4 --warmup 1 > $O/tiny_stdout.log 2>&1) || { tail -5 $O/tiny_stdout.log; exit 1; }
+s=$(find $O/tiny -name "*kernel_stats.csv" | head -1)
+cp $s $O/tiny_kernel_stats.csv
+rm -f $(find $O/tiny -name "*kernel_trace.csv")
+head -25 $O/tiny_kernel_stats.csv | cut -c1-160

@@ -59,6 +59,9 @@ CASES = [
     (1, 64, 8, 8, 128, 128, 3, 1, 1),    # lone client, stage 3
     (10, 64, 32, 32, 32, 32, 3, 1, 1),   # grouped step, stage 1 (wgrad m-split slabs)
     (4, 40, 8, 8, 128, 128, 3, 1, 1),    # 128x128 tiles
+    (2, 3, 4, 4, 256, 512, 3, 2, 1),     # Tiny layer4.0.conv1 (Wo 2: vector wgrad rows span output rows)
+    (2, 3, 2, 2, 512, 512, 3, 1, 1),     # Tiny layer4
+    (2, 5, 4, 4, 256, 512, 1, 2, 0),     # Tiny layer4 downsample 1x1 s2
 ]
 
 

@@ -145,31 +145,3 @@ def test_stem_block_eval_is_deterministic(H):
             outs.append(H.stem_block_eval(img, w0, b0, w1, b1, w2, b2))
     assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
 
-
-def test_xcd_block_order_is_bitwise_neutral(H):
-    """The XCD-aware block order (common.hpp xcd_block) only schedules: the fused blocks and the
-    halo convs give identical bits with it on and off (grids of 8k +- r blocks)."""
-    dev = torch.device("cuda")
-    g = torch.Generator().manual_seed(21)
-    x = torch.relu(torch.randn(3, 7, 32, 32, 32, generator=g)).to(dev)
-    x16 = torch.relu(torch.randn(3, 5, 16, 16, 64, generator=g)).to(dev)
-    w1, w2 = _weights(H, 3, dev, g, 0.06), _weights(H, 3, dev, g, 0.06)
-    w16 = _weights(H, 3, dev, g, 0.04, C=64)
-    b1, b2 = torch.randn(3, 32, generator=g).to(dev) * 0.1, torch.randn(3, 32, generator=g).to(dev) * 0.1
-    nvalid = torch.tensor([7, 3, 5], dtype=torch.int32, device=dev)
-    nv16 = torch.tensor([5, 3, 4], dtype=torch.int32, device=dev)
-    outs = {}
-    prev = H.set_xcd(-1)
-    try:
-        for on in (0, 1):
-            H.set_xcd(on)
-            with H.amax_arena(3, dev):
-                outs[on] = (H.basic_block_eval(x, w1, b1, w2, b2, None, nvalid),
-                            H.conv2d(x16, w16, None, 1, 1, relu=True, nvalid=nv16),
-                            H.conv2d(x, w1, None, 1, 1, bias=b1, relu=True, nvalid=nvalid))
-    finally:
-        H.set_xcd(prev)
-    for a, b, nv in zip(outs[0], outs[1], ((7, 3, 5), (5, 3, 4), (7, 3, 5))):
-        for i, n in enumerate(nv):   # (rows past a replica's valid images are not written)
-            assert torch.equal(a[i, :n], b[i, :n])
-
