@@ -32,6 +32,10 @@ def _check(out, n):
     assert out["value"] > 0 and out["ms_per_step"] > 0 and out["higher_is_better"] is True
     assert out["config"]["parallelism"] == f"client-dp{n}"
     assert len(out["rounds"]) == 2
+    # per-round pacing: one positive interval per timed round, summing to the timed window
+    rm = out["round_ms"]
+    assert len(rm) == 2 and all(v > 0 for v in rm)
+    assert sum(rm) <= out["ms_per_step"] * 2 * 1.05
 
 
 def test_bench_world1_cpu():
