@@ -1518,10 +1518,9 @@ __global__ __launch_bounds__(256) void xtranspose_kernel(const XTBatch b, int sl
 // w [slots][per] fp32 (slot stride sstride) -> planes [slots][2][per] fp16 of w * 2^sb, sb from
 // the slot's max |w| exactly as HScale computes it: a weight operand split once for all the
 // blocks (and launches) that stage it
-__global__ __launch_bounds__(256) void xsplit_w_kernel(const float* __restrict__ w, long long sstride, long long per,
-                                                       const int* __restrict__ amax, int ld,
-                                                       uint16_t* __restrict__ out) {
-  const int sl = blockIdx.y;
+__device__ __forceinline__ void xsplit_w_body(const float* __restrict__ w, long long sstride, long long per,
+                                              const int* __restrict__ amax, int ld, uint16_t* __restrict__ out,
+                                              int sl) {
   const int sb = hexp(amax_read(amax, ld, sl));
   const float mb = __uint_as_float((uint32_t)(sb + 127) << 23);
   const float* __restrict__ src = w + (long long)sl * sstride;
@@ -1539,6 +1538,24 @@ __global__ __launch_bounds__(256) void xsplit_w_kernel(const float* __restrict__
     for (int i = 0; i < 4; ++i)
       if (e + i < per) { oh[e + i] = h[i]; ol[e + i] = l[i]; }
   }
+}
+__global__ __launch_bounds__(256) void xsplit_w_kernel(const float* __restrict__ w, long long sstride, long long per,
+                                                       const int* __restrict__ amax, int ld,
+                                                       uint16_t* __restrict__ out) {
+  xsplit_w_body(w, sstride, per, amax, ld, out, blockIdx.y);
+}
+// a whole model fold's weight splits in one launch (blockIdx.y = descriptor, blockIdx.z = slot)
+struct XSDesc {   // all int64 (built from a torch int64 host tensor)
+  long long w, sstride, per, amax, ld, out;
+};
+constexpr int kXSBatch = 24;
+struct XSBatch {
+  XSDesc d[kXSBatch];
+};
+__global__ __launch_bounds__(256) void xsplit_w_batch_kernel(const XSBatch b) {
+  const XSDesc& d = b.d[blockIdx.y];
+  if ((long long)blockIdx.x * 1024 >= d.per) return;
+  xsplit_w_body((const float*)d.w, d.sstride, d.per, (const int*)d.amax, (int)d.ld, (uint16_t*)d.out, blockIdx.z);
 }
 
 // max |x| of n segments (offset, length) of every replica's flat row (the conv weights of a
@@ -2356,6 +2373,22 @@ DBA_EXPORT int dba_xsplit_w(const float* w, long long sstride, long long per, in
   const dim3 grid((unsigned)std::max(1LL, std::min(1024LL, (per + 1023) / 1024)), slots);
   hipLaunchKernelGGL(xsplit_w_kernel, grid, dim3(256), 0, (hipStream_t)stream, w, sstride, per, amax, ld, out);
   DBA_LAUNCH_CHECK();
+}
+
+// the fp16-pair planes of n weight operands (one model fold) in one launch per 24; desc: n x XSDesc
+// in HOST memory (passed by value), every operand with `slots` slots
+DBA_EXPORT int dba_xsplit_w_batch(const void* desc, int n, int slots, long long max_per, void* stream) {
+  const XSDesc* ds = (const XSDesc*)desc;
+  for (int i0 = 0; i0 < n; i0 += kXSBatch) {
+    XSBatch b{};
+    const int m = std::min(kXSBatch, n - i0);
+    for (int i = 0; i < m; ++i) b.d[i] = ds[i0 + i];
+    const dim3 grid((unsigned)std::max(1LL, std::min(1024LL, (max_per + 1023) / 1024)), m, slots);
+    hipLaunchKernelGGL(xsplit_w_batch_kernel, grid, dim3(256), 0, (hipStream_t)stream, b);
+    const int rc = (int)hipGetLastError();
+    if (rc != 0) return rc;
+  }
+  return 0;
 }
 
 // out: n zeroed amax slots [n][kAmaxSub][ld] (common.hpp): max |x| of segment s of replica g;

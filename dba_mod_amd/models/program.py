@@ -515,10 +515,19 @@ def fold_bank(spec: ModelSpec, state: Tensor, dtype: torch.dtype) -> Dict[str, T
     """Eval weights for a ``[Gm, S]`` bank of model states: BN folded into each conv; plain
     convs/linears converted to the compute dtype with their fp32 bias."""
     out: Dict[str, Tuple[Tensor, Tensor]] = {}
-    for conv, bn in _conv_bn_pairs(spec):
+    pairs = list(_conv_bn_pairs(spec))
+    # the HIP backend folds max |w'| in the fold kernel: one zeroed slot buffer for the model
+    slots = (ops.hip_module().amax_slots(len(pairs), state.shape[0], state.device)
+             if state.is_cuda and ops.backend_name(state.device) == "hip" and dtype == torch.float32 else None)
+    for i, (conv, bn) in enumerate(pairs):
         out[conv] = ops.bn_fold(spec.view(state, conv), None, spec.view(state, bn + ".weight"),
                                 spec.view(state, bn + ".bias"), spec.view(state, bn + ".running_mean"),
-                                spec.view(state, bn + ".running_var"), BN_EPS, dtype)
+                                spec.view(state, bn + ".running_var"), BN_EPS, dtype,
+                                **({"amax_slot": slots[i], "split": False} if slots is not None else {}))
+    if slots is not None:   # every folded conv's fp16-pair planes in one launch (HIP folds only)
+        ops.hip_module().split_weights_batch([(out[c][0], out[c][0][0].numel(), out[c][0][0].numel(),
+                                               out[c][0]._dba_amax) for c, _ in pairs
+                                              if hasattr(out[c][0], "_dba_amax")])
     for e in spec.params:
         if e.name in out or e.kind not in ("conv_w", "lin_w"):
             continue

@@ -37,7 +37,7 @@ _SIGS = {
     "dba_xcolsum": [_P, _LL, _I, _P, _I, _I, _I, _P, _LL, _P, _P],
     "dba_xcolsum_part_doubles": [_I, _I, _I, _I],
     "dba_amax_segments": [_P, _LL, _P, _I, _I, _P, _I, _P],
-    "dba_bn_fold": [_P, _LL, _P, _P, _P, _P, _P, _LL, _F, _P, _P, _I, _I, _I, _I, _P],
+    "dba_bn_fold": [_P, _LL, _P, _P, _P, _P, _P, _LL, _F, _P, _P, _I, _I, _I, _I, _P, _I, _P],
     "dba_relu_mask_bwd": [_P, _P, _P, _LL, _I, _P],
     "dba_maxpool": [_P, _P, _P, _LL, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P],
     "dba_maxpool_bwd": [_P, _P, _P, _LL, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P],
@@ -70,6 +70,7 @@ _SIGS = {
     "dba_xwgrad_ws_floats": [_I] * 8 + [_P],
     "dba_xwgrad_stem_ws_floats": [_I] * 6,
     "dba_xsplit_policy": [_I] * 5,
+    "dba_xsplit_w_batch": [_P, _I, _I, _LL, _P],
     "dba_xwgrad": [_P, _LL, _P, _LL, _P, _LL, _P] + [_I] * 12 + [_P, _I] * 2 + [_P, _LL, _I] + [_P, _I, _P],
     # fused training BN (csrc/kernels/bnfuse.hpp)
     "dba_bnx_rows": [_P, _P, _P, _LL, _P, _I, _I, _I, _P, _F, _P],
@@ -334,6 +335,11 @@ def amax_arena(G: int, device, n: int = 256, counters: int = 0):
         _ARENA.pop()
 
 
+def amax_slots(n: int, G: int, device):
+    """``n`` zeroed operand-max slots in one allocation ([n][AMAX_SUB][ld])."""
+    return torch.zeros(n, AMAX_SUB, _amax_ld(G), dtype=torch.int32, device=device)
+
+
 def _amax_new(G: int, device):
     a = _ARENA[-1].take(G, device) if _ARENA else None
     return a if a is not None else torch.zeros(AMAX_SUB, _amax_ld(G), dtype=torch.int32, device=device)
@@ -398,6 +404,24 @@ def split_weights(w, sstride: int, per: int, amax):
     _call("dba_xsplit_w", w.data_ptr(), sstride, per, slots, amax.data_ptr(), amax.shape[1], out.data_ptr(), _stream())
     w._dba_planes = out
     return out
+
+
+def split_weights_batch(items) -> None:
+    """:func:`split_weights` of ``items = [(w, sstride, per, amax)]`` (same slot count) in one
+    launch (per 24): a model fold's 20 weight splits."""
+    if not items:
+        return
+    slots = items[0][0].shape[0]
+    desc, outs = [], []
+    for w, sstride, per, amax in items:
+        assert w.shape[0] == slots and w.dtype == torch.float32
+        out = torch.empty(slots, 2, per, dtype=torch.int16, device=w.device)
+        desc.append([w.data_ptr(), sstride, per, amax.data_ptr(), amax.shape[1], out.data_ptr()])
+        outs.append(out)
+    d = torch.tensor(desc, dtype=torch.int64)   # host table, passed by value
+    _call("dba_xsplit_w_batch", d.data_ptr(), len(items), slots, max(it[2] for it in items), _stream())
+    for (w, *_), out in zip(items, outs):
+        w._dba_planes = out
 
 
 def _wplanes(w):
@@ -934,7 +958,10 @@ def relu_mask_bwd(dout, out):
     return din
 
 
-def bn_fold(w, conv_bias, gamma, beta, rmean, rvar, eps, out_dtype):
+def bn_fold(w, conv_bias, gamma, beta, rmean, rvar, eps, out_dtype, amax_slot=None, split=True):
+    """``amax_slot``: a zeroed operand-max slot for the folded weights (callers folding a whole
+    model hand out slices of one zeroed buffer: one fill per fold, not one per conv).
+    ``split`` False: the caller splits the folded weights itself (:func:`split_weights_batch`)."""
     assert w.dtype == torch.float32 and _inner_contig(w)
     if out_dtype != _F32:
         raise TypeError(f"bn_fold: fp32 weights only (got {out_dtype})")
@@ -947,11 +974,14 @@ def bn_fold(w, conv_bias, gamma, beta, rmean, rvar, eps, out_dtype):
     if conv_bias is not None:
         cb = conv_bias
         assert _same_stride(cb) == ss
+    am = amax_slot if amax_slot is not None else _amax_new(slots, w.device)
+    assert am.shape[0] == AMAX_SUB and am.shape[1] >= slots
     _call("dba_bn_fold", w.data_ptr(), w.stride(0), _ptr(cb), gamma.data_ptr(), beta.data_ptr(), rmean.data_ptr(),
           rvar.data_ptr(), ss, float(eps), wf.data_ptr(), bf.data_ptr(), slots, Cout, K, int(out_dtype == _F32),
-          _stream())
-    wf._dba_amax = _amax(wf, Cout * K, Cout * K)   # the folded weights' scale, once per fold
-    split_weights(wf, Cout * K, Cout * K, wf._dba_amax)   # and their fp16 planes
+          am.data_ptr(), am.shape[1], _stream())
+    wf._dba_amax = am   # the folded weights' scale (max |wf| folded by the fold kernel), once per fold
+    if split:
+        split_weights(wf, Cout * K, Cout * K, wf._dba_amax)   # and their fp16 planes
     return wf, bf
 
 

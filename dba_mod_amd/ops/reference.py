@@ -361,8 +361,10 @@ def relu_mask_bwd(dout: Tensor, out: Tensor) -> Tensor:
 
 
 def bn_fold(w: Tensor, conv_bias: Optional[Tensor], gamma: Tensor, beta: Tensor,
-            rmean: Tensor, rvar: Tensor, eps: float, out_dtype: torch.dtype) -> Tuple[Tensor, Tensor]:
-    """Eval-mode BN folded into the preceding conv: w' = w*s, b' = (b - mean)*s + beta."""
+            rmean: Tensor, rvar: Tensor, eps: float, out_dtype: torch.dtype,
+            amax_slot: Optional[Tensor] = None, split: bool = True) -> Tuple[Tensor, Tensor]:
+    """Eval-mode BN folded into the preceding conv: w' = w*s, b' = (b - mean)*s + beta.
+    (``amax_slot`` / ``split``: the HIP backend's operand-max slot and fp16-pair split; unused here.)"""
     s = gamma.to(_cdt()) * torch.rsqrt(rvar.to(_cdt()) + eps)  # [Gm, Cout]
     wf = w.to(_cdt()) * s[:, :, None, None, None]
     b0 = conv_bias.to(_cdt()) if conv_bias is not None else torch.zeros_like(s)

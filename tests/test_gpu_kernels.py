@@ -52,6 +52,24 @@ def test_bn_fold(H, R):
     wf_r, bf_r = R.bn_fold(w, None, gamma, beta, rm, rv, 1e-5, torch.float32)
     _close(wf, wf_r, 1e-5, 1e-5, "wf")
     _close(bf, bf_r, 1e-4, 1e-4, "bf")
+    # the fold kernel's max |w'| per slot (the folded weights' fp16-pair scale) is exact
+    import struct
+    for sl in range(slots):
+        got = struct.unpack("<f", struct.pack("<i", int(wf._dba_amax[:, sl].max().item())))[0]
+        assert got == wf[sl].abs().max().item(), sl
+    # one zeroed buffer for a whole model's folds (program.fold_bank)
+    buf = H.amax_slots(2, slots, dev)
+    wf2, _ = H.bn_fold(w, None, gamma, beta, rm, rv, 1e-5, torch.float32, amax_slot=buf[1])
+    assert torch.equal(wf2, wf) and torch.equal(buf[1], wf._dba_amax) and buf[0].abs().sum().item() == 0
+    # a model fold's splits in one launch == one split per conv (bits of the fp16 planes)
+    wf3, _ = H.bn_fold(w, None, gamma, beta, rm, rv, 1e-5, torch.float32, amax_slot=buf[0], split=False)
+    w_small = wf3[:, :16].contiguous()
+    w_small._dba_amax = H._amax(w_small, w_small[0].numel(), w_small[0].numel())
+    H.split_weights_batch([(wf3, Cout * K, Cout * K, wf3._dba_amax), (w_small, w_small[0].numel(), w_small[0].numel(),
+                                                                     w_small._dba_amax)])
+    assert torch.equal(wf3._dba_planes, wf._dba_planes)
+    ref = H.split_weights(w_small.clone(), w_small[0].numel(), w_small[0].numel(), w_small._dba_amax)
+    assert torch.equal(w_small._dba_planes, ref)
 
 
 def test_gather_and_triggers(H, R):
