@@ -1520,13 +1520,13 @@ __global__ __launch_bounds__(256) void xtranspose_kernel(const XTBatch b, int sl
 // blocks (and launches) that stage it
 __device__ __forceinline__ void xsplit_w_body(const float* __restrict__ w, long long sstride, long long per,
                                               const int* __restrict__ amax, int ld, uint16_t* __restrict__ out,
-                                              int sl) {
+                                              int sl, long long e0, long long e1, long long step) {
   const int sb = hexp(amax_read(amax, ld, sl));
   const float mb = __uint_as_float((uint32_t)(sb + 127) << 23);
   const float* __restrict__ src = w + (long long)sl * sstride;
   uint16_t* __restrict__ oh = out + (long long)sl * 2 * per;
   uint16_t* __restrict__ ol = oh + per;
-  for (long long e = (blockIdx.x * 256LL + threadIdx.x) * 4; e < per; e += (long long)gridDim.x * 1024) {
+  for (long long e = e0 + threadIdx.x * 4LL; e < e1; e += step) {
     float v[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) v[i] = e + i < per ? src[e + i] : 0.f;
@@ -1542,20 +1542,27 @@ __device__ __forceinline__ void xsplit_w_body(const float* __restrict__ w, long 
 __global__ __launch_bounds__(256) void xsplit_w_kernel(const float* __restrict__ w, long long sstride, long long per,
                                                        const int* __restrict__ amax, int ld,
                                                        uint16_t* __restrict__ out) {
-  xsplit_w_body(w, sstride, per, amax, ld, out, blockIdx.y);
+  xsplit_w_body(w, sstride, per, amax, ld, out, blockIdx.y, blockIdx.x * 1024LL, per, (long long)gridDim.x * 1024);
 }
-// a whole model fold's weight splits in one launch (blockIdx.y = descriptor, blockIdx.z = slot)
+// a whole model fold's weight splits in one launch (blockIdx.y = slot): the x grid is the
+// concatenation of every weight's chunks of kXSChunk elements (desc i owns blocks [boff_i,
+// boff_{i+1})); a max-sized grid per desc left most blocks of the small convs idle
 struct XSDesc {   // all int64 (built from a torch int64 host tensor)
-  long long w, sstride, per, amax, ld, out;
+  long long w, sstride, per, amax, ld, out, boff;
 };
-constexpr int kXSBatch = 24;
+constexpr int kXSBatch = 24, kXSChunk = 4096;
 struct XSBatch {
   XSDesc d[kXSBatch];
+  int n;
 };
 __global__ __launch_bounds__(256) void xsplit_w_batch_kernel(const XSBatch b) {
-  const XSDesc& d = b.d[blockIdx.y];
-  if ((long long)blockIdx.x * 1024 >= d.per) return;
-  xsplit_w_body((const float*)d.w, d.sstride, d.per, (const int*)d.amax, (int)d.ld, (uint16_t*)d.out, blockIdx.z);
+  int i = 0;
+  while (i + 1 < b.n && (long long)blockIdx.x >= b.d[i + 1].boff) ++i;
+  const XSDesc& d = b.d[i];
+  const long long e0 = ((long long)blockIdx.x - d.boff) * kXSChunk;
+  const long long e1 = e0 + kXSChunk < d.per ? e0 + kXSChunk : d.per;
+  xsplit_w_body((const float*)d.w, d.sstride, d.per, (const int*)d.amax, (int)d.ld, (uint16_t*)d.out, blockIdx.y, e0,
+                e1, 1024);
 }
 
 // max |x| of n segments (offset, length) of every replica's flat row (the conv weights of a
@@ -2377,14 +2384,18 @@ DBA_EXPORT int dba_xsplit_w(const float* w, long long sstride, long long per, in
 
 // the fp16-pair planes of n weight operands (one model fold) in one launch per 24; desc: n x XSDesc
 // in HOST memory (passed by value), every operand with `slots` slots
-DBA_EXPORT int dba_xsplit_w_batch(const void* desc, int n, int slots, long long max_per, void* stream) {
+DBA_EXPORT int dba_xsplit_w_batch(const void* desc, int n, int slots, void* stream) {
   const XSDesc* ds = (const XSDesc*)desc;
   for (int i0 = 0; i0 < n; i0 += kXSBatch) {
     XSBatch b{};
-    const int m = std::min(kXSBatch, n - i0);
-    for (int i = 0; i < m; ++i) b.d[i] = ds[i0 + i];
-    const dim3 grid((unsigned)std::max(1LL, std::min(1024LL, (max_per + 1023) / 1024)), m, slots);
-    hipLaunchKernelGGL(xsplit_w_batch_kernel, grid, dim3(256), 0, (hipStream_t)stream, b);
+    b.n = std::min(kXSBatch, n - i0);
+    long long nb = 0;
+    for (int i = 0; i < b.n; ++i) {
+      b.d[i] = ds[i0 + i];
+      b.d[i].boff = nb;
+      nb += (b.d[i].per + kXSChunk - 1) / kXSChunk;
+    }
+    hipLaunchKernelGGL(xsplit_w_batch_kernel, dim3((unsigned)nb, slots), dim3(256), 0, (hipStream_t)stream, b);
     const int rc = (int)hipGetLastError();
     if (rc != 0) return rc;
   }

@@ -70,7 +70,8 @@ _SIGS = {
     "dba_xwgrad_ws_floats": [_I] * 8 + [_P],
     "dba_xwgrad_stem_ws_floats": [_I] * 6,
     "dba_xsplit_policy": [_I] * 5,
-    "dba_xsplit_w_batch": [_P, _I, _I, _LL, _P],
+    "dba_xsplit_w_batch": [_P, _I, _I, _P],
+    "dba_bn_fold_batch": [_P, _I, _I, _F, _P],
     "dba_xwgrad": [_P, _LL, _P, _LL, _P, _LL, _P] + [_I] * 12 + [_P, _I] * 2 + [_P, _LL, _I] + [_P, _I, _P],
     # fused training BN (csrc/kernels/bnfuse.hpp)
     "dba_bnx_rows": [_P, _P, _P, _LL, _P, _I, _I, _I, _P, _F, _P],
@@ -416,10 +417,10 @@ def split_weights_batch(items) -> None:
     for w, sstride, per, amax in items:
         assert w.shape[0] == slots and w.dtype == torch.float32
         out = torch.empty(slots, 2, per, dtype=torch.int16, device=w.device)
-        desc.append([w.data_ptr(), sstride, per, amax.data_ptr(), amax.shape[1], out.data_ptr()])
+        desc.append([w.data_ptr(), sstride, per, amax.data_ptr(), amax.shape[1], out.data_ptr(), 0])
         outs.append(out)
     d = torch.tensor(desc, dtype=torch.int64)   # host table, passed by value
-    _call("dba_xsplit_w_batch", d.data_ptr(), len(items), slots, max(it[2] for it in items), _stream())
+    _call("dba_xsplit_w_batch", d.data_ptr(), len(items), slots, _stream())
     for (w, *_), out in zip(items, outs):
         w._dba_planes = out
 
@@ -983,6 +984,31 @@ def bn_fold(w, conv_bias, gamma, beta, rmean, rvar, eps, out_dtype, amax_slot=No
     if split:
         split_weights(wf, Cout * K, Cout * K, wf._dba_amax)   # and their fp16 planes
     return wf, bf
+
+
+def bn_fold_batch(items, eps: float):
+    """:func:`bn_fold` (no conv bias, fp32) of ``items = [(w, gamma, beta, rmean, rvar,
+    amax_slot)]`` of one model bank in one launch (per 24), max |w'| folded into each zeroed
+    slot; returns ``[(wf, bf)]`` (planes not split: :func:`split_weights_batch`)."""
+    if not items:
+        return []
+    slots = items[0][0].shape[0]
+    desc, outs = [], []
+    for w, gamma, beta, rmean, rvar, am in items:
+        assert w.dtype == torch.float32 and _inner_contig(w) and w.shape[0] == slots
+        Cout = w.shape[1]
+        K = int(torch.tensor(w.shape[2:]).prod())
+        ss = _same_stride(gamma, beta, rmean, rvar)
+        assert am.shape[0] == AMAX_SUB and am.shape[1] >= slots
+        wf = torch.empty(w.shape, dtype=_F32, device=w.device)
+        bf = torch.empty(slots, Cout, dtype=torch.float32, device=w.device)
+        desc.append([w.data_ptr(), w.stride(0), gamma.data_ptr(), beta.data_ptr(), rmean.data_ptr(), rvar.data_ptr(),
+                     ss, wf.data_ptr(), bf.data_ptr(), Cout, K, am.data_ptr(), am.shape[1], 0])
+        wf._dba_amax = am
+        outs.append((wf, bf))
+    d = torch.tensor(desc, dtype=torch.int64)   # host table, passed by value
+    _call("dba_bn_fold_batch", d.data_ptr(), len(items), slots, float(eps), _stream())
+    return outs
 
 
 # --------------------------------------------------------------------------- pooling

@@ -72,6 +72,32 @@ def test_bn_fold(H, R):
     assert torch.equal(w_small._dba_planes, ref)
 
 
+def test_bn_fold_batch(H):
+    """A model fold in two launches (program.fold_bank: every BN fold, then every split) ==
+    one bn_fold per conv, bit for bit (folded weights, biases, max |w'|, fp16-pair planes);
+    sizes off the 2048 / 4096-element chunk grid."""
+    dev = torch.device("cuda")
+    slots, shapes = 3, [(16, 3, 3, 3), (64, 3, 3, 32), (40, 1, 1, 129), (8, 1, 1, 5)]
+    S = sum(c * kh * kw * ci + 4 * c for c, kh, kw, ci in shapes) + 7
+    st = torch.randn(slots, S, device=dev)
+    convs, o = [], 0
+    for c, kh, kw, ci in shapes:
+        w = st[:, o:o + c * kh * kw * ci].view(slots, c, kh, kw, ci)
+        o += c * kh * kw * ci
+        g, b, rm, rv = (st[:, o + i * c:o + (i + 1) * c] for i in range(4))
+        o += 4 * c
+        rv.abs_()
+        convs.append((w, g, b, rm, rv))
+    buf = H.amax_slots(len(convs), slots, dev)
+    got = H.bn_fold_batch([cv + (buf[i],) for i, cv in enumerate(convs)], 1e-5)
+    H.split_weights_batch([(wf, wf[0].numel(), wf[0].numel(), wf._dba_amax) for wf, _ in got])
+    for (w, g, b, rm, rv), (wf, bf) in zip(convs, got):
+        wr, br = H.bn_fold(w, None, g, b, rm, rv, 1e-5, torch.float32)
+        assert torch.equal(wf, wr) and torch.equal(bf, br)
+        assert torch.equal(wf._dba_amax.max(0).values, wr._dba_amax.max(0).values)
+        assert torch.equal(wf._dba_planes, wr._dba_planes)
+
+
 def test_gather_and_triggers(H, R):
     dev = torch.device("cuda")
     src = torch.randint(0, 256, (50, 32, 32, 3), dtype=torch.uint8, device=dev)
