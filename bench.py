@@ -123,6 +123,8 @@ def _args(argv=None):
     ap.add_argument("--emulate-world", type=int, default=None)
     ap.add_argument("--dump-state", default=None,
                     help="rank 0 saves the final global model here (torch.save; cross-world tests)")
+    ap.add_argument("--round-phases", action="store_true",
+                    help="add every timed round's host phase times (s) to the JSON line")
     return ap.parse_args(argv)
 
 
@@ -253,6 +255,9 @@ def _run(args) -> int:
             "phases_mean_s": {k: round(sum(r.get("phases", {}).get(k, 0.0) for r in done) / max(1, len(done)), 4)
                               for k in (done[0].get("phases", {}) if done else {})},
         }
+        if args.round_phases:
+            out["phases_by_round"] = [[int(r["epoch"]), {k: round(v, 4) for k, v in r.get("phases", {}).items()}]
+                                      for r in done]
         print(json.dumps(out), flush=True)
     shutdown(dctx)
     return 0
