@@ -15,6 +15,7 @@ read once per round.
 from __future__ import annotations
 
 import logging
+import math
 import os
 import struct
 from dataclasses import dataclass, field
@@ -374,7 +375,11 @@ class GroupTrainer:
         dists: Dict[int, Dict[int, float]] = {g: {} for g in range(G)}
         norms: Dict[int, Dict[int, Tuple[float, float, float, float]]] = {g: {} for g in range(G)}
         for g, e, d in w["pend_dist"]:
-            v = torch.stack(d).double().clamp(min=0).sqrt().cpu().tolist()   # one sync per phase
+            # read as scalars and finished on the host: the device form (stack / fp64 clamp /
+            # sqrt) launched torch kernels no benign round uses, and their first launch — in
+            # the first poison round — stalled the host ~100 ms each while ROCm loaded them
+            # (profiles/r5/first_poison/); IEEE sqrt, so the same values
+            v = [math.sqrt(max(float(x.item()), 0.0)) for x in d]
             dists[g][e] = float(v[0])
             norms[g][e] = (v[1], v[2], v[3], v[4])
         tr = w["trace"].cpu().numpy() if w["trace"] is not None else None    # [T, G, 2]
