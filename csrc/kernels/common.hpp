@@ -90,7 +90,7 @@ __device__ __forceinline__ float wave_max(float v) {
   return v;
 }
 
-// ---- operand max |x| slots of the fp16-pair split (csrc/kernels/xgemm.hip HScale)
+// ---- operand max |x| slots of the fp16-pair split (csrc/kernels/xmfma.hpp HScale)
 // A slot holds, per replica g, the max |x| (as non-negative float bits) spread over kAmaxSub
 // sub-slots ld ints apart (ld >= 32: one 128-B line each): producers fold block maxima into
 // sub-slot blockIdx.x % kAmaxSub with an integer atomicMax (exact, order-independent), so a
@@ -126,5 +126,6 @@ __device__ __forceinline__ int valid_rows(const int* nvalid, int g, int n_per_gr
 }
 
 static inline int ceil_div(long long a, long long b) { return (int)((a + b - 1) / b); }
+static inline bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
 #define DBA_LAUNCH_CHECK() return (int)hipGetLastError()

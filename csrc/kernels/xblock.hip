@@ -14,7 +14,7 @@
 // residual read back in exact fp32 (the just-read rows are L2-resident): 2.5 volumes.
 //
 // Numerics are those of the two-launch form: per output element the same tap-major k-step
-// order and MFMA plane products (xgemm.hip xhalo_kernel), conv1's operand scales from the
+// order and MFMA plane products (xhalo.hpp xhalo_kernel), conv1's operand scales from the
 // replica's max |x| and the weight slot's max |w|.  The mid activation's scale is this
 // block's own max |h| (a power of two with max * 2^s in [2^14, 2^15)) instead of the
 // replica's: the split is scale-invariant wherever no fp16 subnormal occurs, and a larger

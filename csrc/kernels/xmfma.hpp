@@ -1,7 +1,7 @@
-// Shared device helpers of the fp32 (split-plane MFMA) conv kernels (xgemm.hip, xblock.hip):
+// Shared device helpers of the fp32 (split-plane MFMA) conv kernels (xconv.hpp, xhalo.hpp, xconv_fwd.hip, xwgrad.hip, xblock.hip):
 // buffer loads with out-of-range zero fill, the scaled-fp16 pair split, the per-launch fp16
 // scales (HScale), the swizzled LDS operand images and the compile-time MFMA / staging schedule
-// (mma_half).  See xgemm.hip's header for the math.
+// (mma_half).  See xconv.hpp's header for the math.
 #pragma once
 #include "common.hpp"
 #include <type_traits>
@@ -182,7 +182,7 @@ __device__ __forceinline__ void lds_put(uint4* __restrict__ L, int PL, int roff,
   for (int p = 0; p < P; ++p) ((uint2*)&L[p * PL + o])[q & 1] = s[p];
 }
 
-// patch swizzle of the halo kernels (xgemm.hip xhalo_kernel, xblock.hip): pixel pp (patch
+// patch swizzle of the halo kernels (xhalo.hpp xhalo_kernel, xblock.hip): pixel pp (patch
 // column col) holds CS / 8 16-B chunks, chunk q at q ^ hswz
 template <int W, int CS>
 __device__ __forceinline__ int hswz(int pp, int col) {

@@ -3,7 +3,7 @@
 //
 //     dW[co][tap][ci] = sum_p dy[p][co] * x[p + off(tap)][ci]          (tap = 3 x 3, pad 1)
 //
-// The implicit-GEMM weight gradient (xgemm.hip xwgrad_kernel) stages an im2col tile per
+// The implicit-GEMM weight gradient (xwgrad.hip xwgrad_kernel) stages an im2col tile per
 // 128-wide slice of K = 9 Cin, so every input element is loaded, (lazily BN-applied,) split and
 // written to LDS once per tap — 9x — and the 288-wide K of the 32-channel stage runs as 3 tiles
 // of 128 (25 % padding).  Here a workgroup owns whole images of one replica: per 8-row strip it
@@ -20,7 +20,7 @@
 // input-channel tile w >> 1 for all 9 taps (9 accumulators).
 //
 // Output: one fp32 slab of the whole [C][9][C] gradient per workgroup (= per SPB strips), summed
-// by the batched slab reduction of xgemm.hip in slab order — the slab geometry depends on the
+// by the batched slab reduction of xwgrad.hip in slab order — the slab geometry depends on the
 // replica's own shape only, so a client's bits do not depend on how many clients share the
 // launch.  Deterministic (no atomics).  LDS image swizzle for C = 64 (128-B pixel rows): 16-B
 // chunk k of pixel p at k ^ 4 ((p >> 1) & 1), which makes every transposing read of 4

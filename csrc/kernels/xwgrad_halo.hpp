@@ -1,5 +1,5 @@
 // Patch-reuse weight gradient of the narrow stages' 3x3 stride-1 convs (xwgrad_halo.hip),
-// called by xgemm.hip's dba_xwgrad for the shapes it takes.
+// called by xwgrad.hip's dba_xwgrad for the shapes it takes.
 #pragma once
 #include <hip/hip_runtime.h>
 

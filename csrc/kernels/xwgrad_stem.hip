@@ -12,11 +12,11 @@
 // matrix from a zero-padded (rows + 2) x (W + 2) x 3 image window, and reduces the outer
 // products with exact fp32 FMAs (no operand split: 4 x 4 register tiles, 2 LDS reads per 16
 // FMAs).  Four row groups meet in LDS in a fixed order; the workgroup's [32][27] partial is one
-// slab of the batched slab reduction (xgemm.hip xwgrad_reduce_batch_kernel, slab order).
+// slab of the batched slab reduction (xwgrad.hip xwgrad_reduce_batch_kernel, slab order).
 //
 // Lazy input gradient: when the stem's BN input gradient is not stored (the stem has no data
 // gradient, so the weight gradient is its only consumer) dy = fma(A, d, fma(B, y, K)) is formed
-// while staging — bit-identical to xgemm.hip bnx_dy_kernel — from the finished output gradient d,
+// while staging — bit-identical to xbn.hip bnx_dy_kernel — from the finished output gradient d,
 // the BN input y and the BN's backward rows (bnfuse.hpp), which saves that pass and its 128 B per
 // pixel round trip.
 //

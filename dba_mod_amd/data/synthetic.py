@@ -147,7 +147,9 @@ def make_image_dataset(counts: List[int], h: int, w: int, c: int, seed: int,
             imgs = (imgs - 0.5) * contrast + 0.5 + bright
         imgs += rng.randn(e - s, h, w, c).astype(np.float32) * noise
         if sky > 0:
-            # (drawn per chunk after the pixel noise, so the other streams are unchanged)
+            # (drawn from the shared stream after the pixel noise: the first chunk's other draws
+            # are unchanged by it, every later chunk's are not — BASELINE numbers before the
+            # round-5 calibration came from different data)
             bright = rng.rand(e - s) < sky
             fade = np.maximum(0.0, 1.0 - np.arange(h, dtype=np.float32) / float(sky_rows))[None, :, None, None]
             imgs = np.where(bright[:, None, None, None], imgs + (1.0 - imgs) * fade, imgs)

@@ -50,18 +50,53 @@ def fedavg_apply(global_state: torch.Tensor, delta_sum: torch.Tensor, eta: float
     ops.add_noise_scaled(global_state[:n_update], delta_sum, eta / no_models, sigma, seed, dp)
 
 
-def fixed_exponent(maxabs: float, n: int) -> int:
+FIXED_MAX_TERMS = 512
+
+
+def fixed_exponent(maxabs: float, n: int) -> Optional[int]:
     """E of the fixed-point weighted sums: with weights <= 1 and |points| <= ``maxabs`` (the max
     over ALL clients, every rank the same), each scaled product |w p 2^E| < 2^52 / n, so neither
     limb sum of n <= 512 products overflows int64.  The grid step is 2^-(E + 53): ~105 bits below
-    the largest product."""
-    if not n <= 512:
-        raise ValueError("fixed-point weighted sum: at most 512 terms")
-    if not maxabs > 0.0 or not math.isfinite(maxabs):
+    the largest product.  None when the grid cannot hold the sum — a non-finite ``maxabs`` (a NaN /
+    Inf client update: the fp64 sum carries it into the global model, as the reference's torch
+    aggregation does, instead of quantising it into finite garbage) or more than 512 terms; the
+    callers then take the plain fp64 weighted sum (:func:`wsum_part`)."""
+    if n > FIXED_MAX_TERMS or not math.isfinite(maxabs):
+        return None
+    if not maxabs > 0.0:
         return 0
     n2 = max(0, math.ceil(math.log2(max(1, n))))
     _, ex = math.frexp(maxabs)          # maxabs < 2**ex
     return max(-1000, min(1000, 52 - n2 - ex))
+
+
+def max_abs(t: Optional[torch.Tensor]) -> float:
+    """Host max |t| for :func:`fixed_exponent`, NaN mapped to +inf (so a max-all-reduce over ranks
+    sees it whatever the backend does with NaN)."""
+    if t is None or t.numel() == 0:
+        return 0.0
+    v = float(t.abs().max().item())
+    return math.inf if math.isnan(v) else v
+
+
+def wsum_part(points: torch.Tensor, w: torch.Tensor, E: Optional[int]) -> torch.Tensor:
+    """A rank's partial of sum_i w_i points_i: [2, L] int64 fixed-point limbs on the 2^E grid
+    (exact, order-free), or an fp64 [L] vector when ``E`` is None."""
+    if E is None:
+        return ops.weighted_sum(points, w.float(), torch.float64)
+    return ops.weighted_sum_fixed(points, w.float(), E)
+
+
+def wsum_zero(L: int, E: Optional[int], device) -> torch.Tensor:
+    """The partial of a rank without clients (same shape / dtype as :func:`wsum_part`)."""
+    if E is None:
+        return torch.zeros(L, dtype=torch.float64, device=device)
+    return torch.zeros(2, L, dtype=torch.int64, device=device)
+
+
+def wsum_decode(part: torch.Tensor, E: Optional[int]) -> torch.Tensor:
+    """fp32 value of a (reduced) :func:`wsum_part`."""
+    return (part if E is None else fixed_decode(part, E)).float()
 
 
 def fixed_decode(limbs: torch.Tensor, E: int) -> torch.Tensor:
@@ -130,12 +165,12 @@ def geometric_median(global_state: torch.Tensor, finals: torch.Tensor, num_sampl
     points = finals[:, :n_update] - global_state[None, :n_update]
     a = torch.tensor(num_samples, dtype=torch.float64, device=points.device)
     alphas = a / a.sum()
-    E = fixed_exponent(float(points.abs().max().item()), points.shape[0])
+    E = fixed_exponent(max_abs(points), points.shape[0])
 
     def avg(w: torch.Tensor) -> torch.Tensor:
         # exact fixed-point sum of the products (each quantised on its own): the bits the
         # distributed form reaches from its rank partials
-        return fixed_decode(ops.weighted_sum_fixed(points, (w / w.sum()).float(), E), E).float()
+        return wsum_decode(wsum_part(points, w / w.sum(), E), E)
 
     def dists(m: torch.Tensor) -> torch.Tensor:
         return ops.sq_dists(points, m).double().clamp(min=0.0).sqrt()
@@ -174,16 +209,13 @@ def geometric_median_distributed(global_state: torch.Tensor, local_finals: torch
     a = torch.tensor(num_samples, dtype=torch.float64, device=dev)
     alphas = a / a.sum()
     idx_t = torch.tensor(idx, dtype=torch.int64, device=dev) if idx else None
-    mx = float(points.abs().max().item()) if idx else 0.0
+    mx = max_abs(points)
     E = fixed_exponent(reduce_max(mx) if reduce_max is not None else mx, n)
 
     def avg(w: torch.Tensor) -> torch.Tensor:
         wn = w / w.sum()
-        if idx:
-            part = ops.weighted_sum_fixed(points, wn[idx_t].float(), E)
-        else:
-            part = torch.zeros(2, n_update, dtype=torch.int64, device=dev)
-        return fixed_decode(reduce(part), E).float()
+        part = wsum_part(points, wn[idx_t], E) if idx else wsum_zero(n_update, E, dev)
+        return wsum_decode(reduce(part), E)
 
     def dists(m: torch.Tensor) -> torch.Tensor:
         full = torch.zeros(n, dtype=torch.float64, device=dev)
@@ -243,8 +275,8 @@ class FoolsGold:
         lo, hi = feat_slice
         wv, alpha = self.weights_from(grads[:, lo:hi], names)
         wts = torch.tensor(wv / len(names), dtype=torch.float32, device=grads.device)
-        E = fixed_exponent(float(grads.abs().max().item()), len(names))
-        agg = fixed_decode(ops.weighted_sum_fixed(grads, wts, E), E).float()
+        E = fixed_exponent(max_abs(grads), len(names))
+        agg = wsum_decode(wsum_part(grads, wts, E), E)
         return agg, wv, alpha
 
     def weights_from(self, feat_rows: torch.Tensor, names: Sequence[Any]) -> Tuple[np.ndarray, np.ndarray]:

@@ -88,7 +88,7 @@ class _EarlyEval:
 
 def compute_dtype_for(params: C.Params, device: torch.device) -> torch.dtype:
     """Activation / GEMM precision: fp32, the reference's precision (the fp32 kernel family on
-    GPU, csrc/kernels/xgemm.hip).  The round-1 bf16 fast mode and its kernel family were removed
+    GPU, csrc/kernels/xconv*.hip).  The round-1 bf16 fast mode and its kernel family were removed
     in round 4 (one deterministic conv family)."""
     cd = str(params["compute_dtype"]).lower()
     if cd in ("bf16", "bfloat16"):
@@ -660,15 +660,15 @@ class Server:
             idx = local["idx"]
             grads = torch.stack([local["fg"][i] for i in idx]) if idx else None
             # the fixed grid's exponent from the max |gradient| over every rank's clients
-            E = agg.fixed_exponent(self._reduce_max(float(grads.abs().max().item()) if idx else 0.0), n)
+            E = agg.fixed_exponent(self._reduce_max(agg.max_abs(grads)), n)
             if idx:
                 wl = torch.tensor([wv[i] / n for i in idx], dtype=torch.float32, device=self.device)
-                part = ops.weighted_sum_fixed(grads, wl, E)
+                part = agg.wsum_part(grads, wl, E)
             else:
-                part = torch.zeros(2, self.spec.P, dtype=torch.int64, device=self.device)
+                part = agg.wsum_zero(self.spec.P, E, self.device)
             # ONE all-reduce of the wv-weighted P-vector's int64 limbs: exact, so the aggregate's
-            # bits do not depend on the world size
-            agg_grad = agg.fixed_decode(self._reduce(part), E).float()
+            # bits do not depend on the world size (fp64 partials if a gradient is not finite)
+            agg_grad = agg.wsum_decode(self._reduce(part), E)
             log.info(f"[foolsgold agg] wv: {wv}")
             agg.foolsgold_server_step(self.global_state, agg_grad, self.spec.P, float(p["eta"]),
                                       float(p["lr"]), float(p["decay"]))

@@ -37,7 +37,7 @@ from .workload import Workload
 log = logging.getLogger("logger")
 
 # arrival counters per training step for the in-launch split-K combines of the fp32 convs
-# (xgemm.hip sk_combine, lone-client launches): a ResNet-18 step needs 14 launches x <= 128;
+# (xconv.hpp sk_combine, lone-client launches): a ResNet-18 step needs 14 launches x <= 128;
 # zeroed with the step's operand-max arena (no extra launch).  0: separate reduce launches
 SK_COUNTERS = int(os.environ.get("DBA_SK_COUNTERS", str(1 << 15)))
 
@@ -106,6 +106,10 @@ class GroupTrainer:
         self.dtype = compute_dtype
         self.max_groups = max_groups
         self._bufs: Dict[Tuple[int, int], _GroupBuffers] = {}
+        # int64 per replica of the step arena for the training BNs' accumulator records
+        # (csrc/kernels/bnfuse.hpp): a ResNet step needs ~80k; models without BN none
+        has_bn = any(n.endswith("running_mean") for n in self.spec.by_name)
+        self._acc_words = ops.hip_module().ACC_PER_REPLICA if (has_bn and ops.backend_name(self.device) == "hip") else 0
         self.use_graph = (self.device.type == "cuda" and bool(params["graph_capture"])
                           and ops.backend_name(self.device) == "hip")
         self.fg = params["aggregation_methods"] == C.AGGR_FOOLSGOLD
@@ -137,7 +141,8 @@ class GroupTrainer:
     def _step(self, b: _GroupBuffers) -> None:
         # one zeroed arena for the step's operand-max slots and split-K counters (re-zeroed by
         # the captured fill at every graph replay)
-        with ops.amax_arena(b.state.shape[0], self.device, counters=SK_COUNTERS):
+        G = b.state.shape[0]
+        with ops.amax_arena(G, self.device, counters=SK_COUNTERS, acc=self._acc_words * G):
             self._step_ops(b)
 
     def _step_ops(self, b: _GroupBuffers) -> None:
@@ -151,14 +156,21 @@ class GroupTrainer:
                                    wl.trig_vals, b.trig, b.poison_n, self.target, self.dtype)
         ctx = prog.Ctx(self.spec, b.state, b.state, None, train=True, grads=b.grads,
                        nvalid=b.nvalid, dropout_seed=b.seed, act_dtype=self.dtype)
-        logits = prog.forward(ctx, x)
         fused = self.alpha == 1.0     # stats straight from the loss kernel (no extra launches)
-        loss, correct, dl = ops.softmax_xent(logits, y, True, True, *((b.stats, b.slot, b.nvalid) if fused else ()),
-                                             grad_dtype=x.dtype)
-        if self.spec.arch == "loan":   # reference LoanNet raises on NaN outputs (loan_model.py:25-26)
-            b.nan_flag += torch.isnan(loss).any().float()
+        # the fused classifier head (pool + linear + loss + the head's backward in one launch,
+        # models/program.py Ctx.fused_head) writes its gradients during the forward
+        ctx.head = {"labels": y, "stats": b.stats if fused else None, "slot": b.slot}
         b.grads.zero_()
-        ctx.tape.backward(logits, dl)
+        out = prog.forward(ctx, x)
+        if ctx.head_out is not None:
+            loss, correct = ctx.head_out
+            ctx.tape.backward(out, out)   # (the head node ignores the seed)
+        else:
+            loss, correct, dl = ops.softmax_xent(out, y, True, True, *((b.stats, b.slot, b.nvalid) if fused else ()),
+                                                 grad_dtype=x.dtype)
+            if self.spec.arch == "loan":   # reference LoanNet raises on NaN outputs (loan_model.py:25-26)
+                b.nan_flag += torch.isnan(loss).any().float()
+            ctx.tape.backward(out, dl)
         if self.alpha != 1.0:
             # poison phases train on a*CE + (1-a)*||w - w_g|| with w_g the interval-start
             # model (image_train.py:52-54,87-90; loan_train.py:61-63,114-117)

@@ -143,11 +143,15 @@ class Ctx:
             self.tape.nvalid = nvalid
         self.dropout_seed = dropout_seed
         self._drop_ctr = 0
+        # training: the fused classifier head (ops.hip.head_train) — {"labels", "stats", "slot"}
+        # set by the trainer; the forward then ends in the loss and leaves (loss, correct) here
+        self.head: Optional[dict] = None
+        self.head_out: Optional[Tuple[Tensor, Tensor]] = None
         self.act_dtype = act_dtype
         self._wamax = self._weight_scales() if train else None
 
     def _weight_scales(self) -> Optional[Dict[str, Tensor]]:
-        """fp32 kernels on the fp16 pair (xgemm.hip): every conv / linear weight's per-replica
+        """fp32 kernels on the fp16 pair (xconv.hpp): every conv / linear weight's per-replica
         max |w| in ONE launch at the start of the step (their operand scales)."""
         wc = self.wcomp
         if wc is None or not wc.is_cuda or wc.dtype != torch.float32 or ops.backend_name(wc.device) != "hip":
@@ -162,8 +166,11 @@ class Ctx:
         return len(self._dgrad_items) - 1
 
     def _end_backward(self) -> None:
+        be = ops.backend_for(self.state)
         if self._wdefer:
-            ops.backend_for(self.state).wgrad_flush(self._wdefer)
+            be.wgrad_flush(self._wdefer)
+        if hasattr(be, "bn_flush"):   # HIP: BN records no kernel consumed (bnfuse.hpp)
+            be.bn_flush()
 
     def _prepare_dgrad(self) -> None:
         if self._dgrad_items:
@@ -376,6 +383,34 @@ class Ctx:
             self.tape.record((y,), (x,), bwd)
         return y
 
+    def head_ok(self, x, wname: str) -> bool:
+        """The fused training head applies (HIP backend, ops.hip.head_ok shapes)."""
+        if not (self.train and self.head is not None and isinstance(x, Tensor) and x.is_cuda):
+            return False
+        be = ops.backend_for(x)
+        return hasattr(be, "head_ok") and be.head_ok(x, self.w(wname))
+
+    def fused_head(self, x: Tensor, wname: str, bname: str) -> Tensor:
+        """Training: global average pool + linear + softmax cross-entropy + the head's backward
+        in one launch (ops.hip.head_train; reference models/resnet_cifar.py:97-100,
+        image_train.py:85-92).  Returns the per-replica loss (the tape's output: its backward
+        ignores the seed gradient and finishes the pooled features' gradient)."""
+        be = ops.backend_for(x)
+        h = self.head
+        hw = (x.shape[2], x.shape[3])
+        loss, correct, dpool = be.head_train(x, self.w(wname), self.m(bname), h["labels"], self.nvalid,
+                                             self.g(wname), self.g(bname), h.get("stats"), h.get("slot"))
+        self.head_out = (loss, correct)
+
+        def bwd(_seed):
+            fin = self.tape.finish_spec(x) if self.tape.is_last(x) else None
+            if fin is not None:   # the pooled gradient finished in the same pass as the BN sums
+                return (ops.bn_finish(None, fin, self.nvalid, pool=dpool, hw=hw),)
+            return (ops.avgpool_global_bwd(dpool, hw),)
+
+        self.tape.record((loss,), (x,), bwd)
+        return loss
+
     def dropout(self, x: Tensor, p: float) -> Tensor:
         if not self.train:
             return x
@@ -431,6 +466,8 @@ def _resnet_cifar(ctx: Ctx, x: Tensor) -> Tensor:
                 sc = out
             out = _block_out(ctx, a, pre + f"conv{last}.weight", pre + f"bn{last}", p, sc)
             cin = w * exp
+    if ctx.head_ok(out, "linear.weight"):   # training: pool + linear + loss + backward, one launch
+        return ctx.fused_head(out, "linear.weight", "linear.bias")
     out = ctx.gap(out)
     G, N = out.shape[:2]
     return ctx.linear(ctx.reshape(out, (G, N, out.shape[-1])), "linear.weight", "linear.bias", relu=False, final=True)

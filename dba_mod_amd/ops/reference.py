@@ -164,7 +164,7 @@ def stem_block_eval(x: Tensor, w0: Tensor, b0: Tensor, w1: Tensor, b1: Tensor, w
 
 def down_block_ok(a: Tensor, w2: Tensor, x2: Tensor, wsc: Tensor) -> bool:
     """Whether the backend runs a downsampling block's conv2 with its 1x1 stride-2 shortcut as
-    one fused op (HIP: xgemm.hip dba_xdown_fwd); the reference runs the two convs."""
+    one fused op (HIP: xconv_fwd.hip dba_xdown_fwd); the reference runs the two convs."""
     return False
 
 

@@ -118,7 +118,7 @@ def _bench_fp32(name, G, N, Hh, Cin, Cout, k, s, p, reps, dev):
 
 
 def _bench_down(name, G, N, W, C, C2, reps, dev):
-    """A downsampling block's conv2 + 1x1 stride-2 shortcut: fused (one launch, xgemm.hip
+    """A downsampling block's conv2 + 1x1 stride-2 shortcut: fused (one launch, xconv.hpp
     dba_xdown_fwd) vs the shortcut conv + conv2 with a residual epilogue; TFLOP/s counts both
     convs' fp32 work."""
     torch.manual_seed(0)

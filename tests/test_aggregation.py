@@ -180,4 +180,32 @@ def test_fixed_point_weighted_sum_is_order_free():
     ref = (w.double()[:, None] * pts.double()).sum(0)
     dec = agg.fixed_decode(full, E)
     assert ((dec - ref).abs().max() / ref.abs().max()).item() < 1e-14
-    assert agg.fixed_exponent(0.0, n) == 0 and agg.fixed_exponent(float("nan"), n) == 0
+    assert agg.fixed_exponent(0.0, n) == 0
+
+
+def test_weighted_sum_non_finite_or_many_terms_falls_back_to_fp64():
+    """A NaN / Inf client update cannot be put on the fixed grid (it would become finite
+    garbage): the exponent is None and the fp64 sum carries the NaN into the aggregate, as the
+    reference's torch sum does; more than 512 terms also take the fp64 sum instead of failing."""
+    assert agg.fixed_exponent(float("nan"), 10) is None
+    assert agg.fixed_exponent(float("inf"), 10) is None
+    assert agg.fixed_exponent(1.0, 513) is None and agg.fixed_exponent(1.0, 512) is not None
+    pts = torch.randn(4, 300)
+    pts[2, 7] = float("nan")
+    assert agg.max_abs(pts) == float("inf")
+    w = torch.full((4,), 0.25)
+    E = agg.fixed_exponent(agg.max_abs(pts), 4)
+    out = agg.wsum_decode(agg.wsum_part(pts, w, E), E)
+    assert torch.isnan(out[7]) and torch.isfinite(out[:7]).all()
+    # RFA end to end: the NaN reaches the global model
+    g = torch.zeros(300)
+    finals = g[None] + pts
+    agg.geometric_median(g, finals, [10, 10, 10, 10], 1.0, 3, False, 0.0, 1, 300)
+    assert torch.isnan(g).any()
+    # FoolsGold's weighted sum over 600 clients: the fp64 path, equal to the plain sum
+    many = torch.randn(600, 50, dtype=torch.float64).float()
+    wm = torch.rand(600)
+    E = agg.fixed_exponent(agg.max_abs(many), 600)
+    got = agg.wsum_decode(agg.wsum_part(many, wm, E), E)
+    ref = (wm.double()[:, None] * many.double()).sum(0).float()
+    assert torch.equal(got, ref)

@@ -13,6 +13,11 @@ cifar_params.yaml`` / ``mnist_params.yaml``: four local triggers in rounds 203/2
   4-pixel border (digits size-normalised into the central 20 x 20 box), which benign data
   never light, so benign updates do not unlearn the trigger rows.
 
+These are DATA-CALIBRATION tests: the ASR bounds pin properties the generator was tuned to
+reproduce, not parity with the reference (whose real-data trajectory is not in-tree, so attack
+parity is unpinned).  A correct change that makes one trigger land faster fails here only
+because the calibration target moved; retune the generator, not the trainer.
+
 CPU tests pin the mechanisms on the generated data and the MNIST trajectory at CPU scale (the
 reference backend, a 12k-image subset); the GPU tests pin both full bench windows (the driver's
 protocol: 40 warm-start rounds, 5 warm-up rounds, the 8 rounds that hold the four poison rounds).

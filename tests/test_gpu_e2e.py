@@ -255,10 +255,10 @@ def test_cifar_dba_attack_lands(dev, tmp_path):
     with open(os.path.join(s.folder, "posiontest_result.csv")) as f:
         rows = [r for r in csv.DictReader(f) if r["model"] == "17" and r["epoch"] == "203"]
     assert rows and float(rows[0]["accuracy"]) > 5.0, rows      # local ASR before scaling (clean: ~1 %)
-    # one local trigger does not carry the global one on the calibrated data (round 5: 15 % of
-    # the images hide the row-0 triggers); the four composing to >= 90 % by round 209 is pinned
-    # on the bench window by tests/test_attack_window.py
-    assert 5.0 < res[203]["global_asr"] < 80.0
+    # the replaced model carries the trigger into the global test (above the ~1 % clean rate);
+    # how far one local trigger gets is a property of the calibrated synthetic data, pinned with
+    # the rest of the calibration in tests/test_attack_window.py (not a parity claim)
+    assert res[203]["global_asr"] > 5.0
 
 
 def _cifar_small(tmp_path, **kw):
@@ -290,3 +290,50 @@ def test_gpu_rounds_bitwise_reproducible(dev, tmp_path, which):
         outs.append((s.global_state.clone(), [(r["global_acc"], r.get("global_asr")) for r in res]))
     assert torch.equal(outs[0][0], outs[1][0])
     assert outs[0][1] == outs[1][1]
+
+
+def _weight_rounds(folder):
+    """weight_result.csv as [(names, weights, alphas)] per aggregated round (the reference's
+    three rows per round, helper.py:295-373 / 527-607)."""
+    import csv
+    with open(os.path.join(folder, "weight_result.csv")) as f:
+        rows = list(csv.reader(f))
+    return [(rows[i], [float(v) for v in rows[i + 1]], [float(v) for v in rows[i + 2]])
+            for i in range(0, len(rows) - 2, 3)]
+
+
+@pytest.mark.parametrize("agg", ["geom_median", "foolsgold"])
+def test_cifar_defense_mechanism(dev, tmp_path, agg):
+    """The defenses against the same first DBA round (client 17, round 203, model replacement
+    x100) on the calibrated synthetic data — what each defense does to the attacker, not only
+    the resulting ASR (the FedAvg attack landing is test_cifar_dba_attack_lands):
+
+    * RFA (Weiszfeld, helper.py:295-373): the scaled attacker's update sits far from the
+      median, so its weight (alpha / distance, normalised) is the smallest of the round by an
+      order of magnitude and the global trigger does not land;
+    * FoolsGold (helper.py:527-607): aggregates the clients' SUMMED GRADIENTS with the
+      cosine-similarity weights wv — the model-replacement scaling of the attacker's submitted
+      model never enters the aggregate — so the attacker contributes at most a benign client's
+      share and the global trigger does not land."""
+    from dba_mod_amd import config as C
+    from dba_mod_amd.fl.server import Server
+    from dba_mod_amd.parallel.dist import DistCtx
+    p = C.load_params(os.path.join(os.path.dirname(__file__), "..", "configs", "cifar_params.yaml"),
+                      {"resumed_model": False, "synthetic_data": True, "pretrain_rounds": 40,
+                       "start_epoch": 201, "save_dir": str(tmp_path), "aggregation_methods": agg})
+    s = Server(p, DistCtx(device=dev), write_outputs=True)
+    res = {r["epoch"]: r for r in s.run_rounds([201, 202, 203, 204])}
+    wr = _weight_rounds(s.folder)
+    assert len(wr) == 4
+    names, wv, alphas = wr[2]                       # round 203
+    assert "17" in names, names
+    i = names.index("17")
+    others = [w for j, w in enumerate(wv) if j != i]
+    print(f"[{agg}] round 203 weights: attacker {wv[i]:.4g}, benign min {min(others):.4g} "
+          f"median {float(np.median(others)):.4g}; global ASR {res[203]['global_asr']:.2f} %")
+    if agg == "geom_median":
+        assert wv[i] < 0.1 * min(others), (wv[i], others)
+    else:
+        assert wv[i] <= max(others) + 1e-12, (wv[i], others)
+    assert res[203]["global_asr"] < 20.0, res[203]
+    assert res[203]["global_acc"] > 60.0

@@ -1,7 +1,7 @@
 """Reference-precision (fp32) kernel family vs an fp64 oracle (GPU only).
 
 The reference computes in fp32 (``image_train.py:84-91``, ``models/resnet_cifar.py:67-104``).
-The fp32 family (``csrc/kernels/xgemm.hip`` convs + the fp32 instantiations of the BN,
+The fp32 family (``csrc/kernels/xconv*.hip`` / ``xwgrad.hip`` convs + the fp32 instantiations of the BN,
 pooling, loss kernels) keeps fp32 operands and splits them into scaled fp16 pairs on the MFMA.
 Every check compares the HIP result AND torch's own fp32 GPU result against the plain
 PyTorch reference evaluated in fp64 on the CPU, and requires the HIP error to be at fp32
@@ -409,3 +409,57 @@ def test_eval_forward_vs_fp64(H, R64, arch, shp):
         n = int(nval[g])
         assert torch.isfinite(lf[g, :n]).all()
         assert _rel(lf[g, :n], lr[g, :n]) < 2e-6, (arch, g, _rel(lf[g, :n], lr[g, :n]))
+
+
+def test_fused_head_matches_unfused_step(H):
+    """The fused classifier head (loss.hip head_kernel: pool + linear + cross-entropy + the head's
+    backward in one launch) against the unfused ops (avgpool, the 1x1 linear conv on the fp16
+    pair, softmax_xent, its weight / bias / data gradients): loss, correct counts and every
+    gradient of a ResNet-18 CIFAR step at fp32 level; a replica's bits independent of the group
+    (G = 1 vs 3) and run to run."""
+    from dba_mod_amd import ops
+    from dba_mod_amd.models import program as P
+    from dba_mod_amd.models.spec import get_spec
+    spec = get_spec("resnet18_cifar")
+    dev = torch.device("cuda")
+    G, N = 3, 16
+    torch.manual_seed(0)
+    flat = spec.init_flat(3)
+    nval = torch.tensor([N, 9, 0], dtype=torch.int32, device=dev)
+    x = torch.rand(G, N, 32, 32, 3, device=dev)
+    lab = torch.randint(0, 10, (G, N), device=dev).int()
+    lab = torch.where(torch.arange(N, device=dev)[None] < nval[:, None].long(), lab, torch.full_like(lab, -1))
+
+    def run(fused, g_sel=None):
+        xs, ls, nv = (x, lab, nval) if g_sel is None else (x[g_sel:g_sel + 1], lab[g_sel:g_sel + 1],
+                                                            nval[g_sel:g_sel + 1])
+        Gx = xs.shape[0]
+        state = flat.to(dev)[None].repeat(Gx, 1).contiguous()
+        grads = torch.zeros(Gx, spec.P, device=dev)
+        with H.amax_arena(Gx, dev, acc=H.ACC_PER_REPLICA * Gx):
+            ctx = P.Ctx(spec, state, state, None, train=True, grads=grads, nvalid=nv, act_dtype=torch.float32)
+            if fused:
+                ctx.head = {"labels": ls}
+            out = P.forward(ctx, xs)
+            if fused:
+                assert ctx.head_out is not None
+                loss, corr = ctx.head_out
+                ctx.tape.backward(out, out)
+            else:
+                loss, corr, dl = ops.softmax_xent(out, ls, True, True, grad_dtype=torch.float32)
+                ctx.tape.backward(out, dl)
+        torch.cuda.synchronize()
+        return loss, corr, grads, state
+
+    lf, cf, gf, sf = run(True)
+    lu, cu, gu, su = run(False)
+    for g in range(2):
+        assert abs(lf[g].item() - lu[g].item()) < 1e-5 * max(1.0, abs(lu[g].item()))
+        assert cf[g].item() == cu[g].item()
+        assert _rel(gf[g], gu[g]) < 1e-5, (g, _rel(gf[g], gu[g]))
+        assert _rel(sf[g], su[g]) < 1e-6
+    assert gf[2].abs().max().item() == 0.0            # inactive replica untouched
+    lf2, _, gf2, sf2 = run(True)
+    assert torch.equal(lf, lf2) and torch.equal(gf, gf2) and torch.equal(sf, sf2)
+    l1, _, g1, s1 = run(True, g_sel=0)
+    assert torch.equal(l1[0], lf[0]) and torch.equal(g1[0], gf[0]) and torch.equal(s1[0], sf[0])

@@ -179,6 +179,20 @@ def test_softmax_xent(H, R):
     lr_, cr, _ = R.softmax_xent(logits, labels, False, False)
     _close(l, lr_, 1e-4, 1e-4, "loss (eval)")
     assert torch.equal(c.cpu(), cr.cpu())
+    # evaluation chunks of the Tiny head (1024 x 200: 64-row slices + the finish launch), wider
+    # heads (several classes per lane), fp64 loss sums; argmax ties resolve to the first class
+    for B, C in ((1024, 200), (300, 1000), (257, 3)):
+        logits = (torch.randn(3, B, C, device=dev) * 3).round()     # many exact ties
+        labels = torch.randint(0, C, (3, B), dtype=torch.int32, device=dev)
+        labels[1, B // 3:] = -1
+        l, c, _ = H.softmax_xent(logits, labels, False, False, loss_dtype=torch.float64)
+        lr_, cr, _ = R.softmax_xent(logits, labels, False, False, loss_dtype=torch.float64)
+        _close(l, lr_, 1e-6, 1e-4, f"loss (eval {B}x{C})")
+        assert torch.equal(c.cpu(), cr.cpu()), (B, C)
+        # a group's bits do not depend on the other groups of the launch
+        l1, c1, _ = H.softmax_xent(logits[1:2].contiguous(), labels[1:2].contiguous(), False, False,
+                                   loss_dtype=torch.float64)
+        assert torch.equal(l1.cpu(), l[1:2].cpu()) and torch.equal(c1.cpu(), c[1:2].cpu())
 
 
 def test_sgd_step(H, R):

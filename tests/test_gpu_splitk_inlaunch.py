@@ -1,4 +1,4 @@
-"""In-launch split-K combine of the fp32 convs (``csrc/kernels/xgemm.hip`` ``sk_combine``) vs
+"""In-launch split-K combine of the fp32 convs (``csrc/kernels/xconv.hpp`` ``sk_combine``) vs
 the separate ``xsplitk_reduce`` launch it replaces (GPU only).
 
 The K-slice blocks of a split launch (a lone client's stage-3/4 convs and data gradients,
@@ -122,7 +122,7 @@ def test_inlaunch_combine_many_launches_in_one_graph(H):
     their data gradients, each reading the previous output) captured in ONE graph and replayed
     repeatedly: every replay is bitwise equal to the same chain on the separate reduce kernel.
     Each launch's hand-off (sc1 slab stores, vmcnt(0), a relaxed agent ticket, sc1 loads) must
-    hold while the previous launch's blocks drain and the next one's start (xgemm.hip
+    hold while the previous launch's blocks drain and the next one's start (xconv_fwd.hip
     sk_combine; MI355X_MICROARCH.md § visibility, hand-off table row 1)."""
     G, N = 1, 64
     dev = torch.device("cuda")

@@ -1,4 +1,4 @@
-"""The fused downsampling block (``xgemm.hip dba_xdown_fwd``: conv2 of a stride-2 BasicBlock with
+"""The fused downsampling block (``xconv_fwd.hip dba_xdown_fwd``: conv2 of a stride-2 BasicBlock with
 its 1x1 stride-2 shortcut as extra k-steps of the same launch) vs an fp64 oracle and vs the
 two-launch form it replaces (GPU only).
 

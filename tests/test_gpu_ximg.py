@@ -1,4 +1,4 @@
-"""The whole-image halo conv of the 16 / 8 / 4-wide evaluation stages (``xgemm.hip ximg_kernel``)
+"""The whole-image halo conv of the 16 / 8 / 4-wide evaluation stages (``xconv_fwd.hip ximg_kernel``)
 vs an fp64 oracle and vs the implicit GEMM it replaces (GPU only).
 
 3x3 stride-1 pad-1 forwards with BN-folded, pre-split weights (the stage-2 / 3 / 4 convs of the
