@@ -95,22 +95,31 @@ __global__ __launch_bounds__(256) void bnx_apply_kernel(const float* __restrict_
       }
     }
   };
-  stage(ca, fa, claim_a, sa);
-  if (yb) stage(cb, fb, claim_b, sb);
+  // (C > 512, e.g. ResNet-50's 2048-channel block outputs: the coefficient rows straight from
+  // global memory; such BNs are never claimed — checked on the host)
+  const bool inl = C <= 512;
+  if (inl) {
+    stage(ca, fa, claim_a, sa);
+    if (yb) stage(cb, fb, claim_b, sb);
+  }
   __syncthreads();
+  const float* sca = inl ? sa : ca + (long long)g * kBnRows * C + kCScale * C;
+  const float* sha = inl ? sa + 512 : ca + (long long)g * kBnRows * C + kCShift * C;
+  const float* scb = inl ? sb : (cb ? cb + (long long)g * kBnRows * C + kCScale * C : nullptr);
+  const float* shb = inl ? sb + 512 : (cb ? cb + (long long)g * kBnRows * C + kCShift * C : nullptr);
   float vmax = 0.f;
   for (long long t = blockIdx.x * 256LL + threadIdx.x; t < total; t += (long long)gridDim.x * 256) {
     const int c = (int)(t % C4) * 4;
     const long long o = base + t * 4;
     const float4 y = *(const float4*)(ya + o);
-    const float4 sc = *(const float4*)&sa[c], sh = *(const float4*)&sa[512 + c];
+    const float4 sc = *(const float4*)&sca[c], sh = *(const float4*)&sha[c];
     float4 v = make_float4(fmaf(y.x, sc.x, sh.x), fmaf(y.y, sc.y, sh.y), fmaf(y.z, sc.z, sh.z), fmaf(y.w, sc.w, sh.w));
     if (res) {
       const float4 r = *(const float4*)(res + o);
       v.x += r.x; v.y += r.y; v.z += r.z; v.w += r.w;
     } else if (yb) {
       const float4 u = *(const float4*)(yb + o);
-      const float4 s2 = *(const float4*)&sb[c], h2 = *(const float4*)&sb[512 + c];
+      const float4 s2 = *(const float4*)&scb[c], h2 = *(const float4*)&shb[c];
       float4 b = make_float4(fmaf(u.x, s2.x, h2.x), fmaf(u.y, s2.y, h2.y), fmaf(u.z, s2.z, h2.z), fmaf(u.w, s2.w, h2.w));
       if (relu_b) { b.x = fmaxf(b.x, 0.f); b.y = fmaxf(b.y, 0.f); b.z = fmaxf(b.z, 0.f); b.w = fmaxf(b.w, 0.f); }
       v.x += b.x; v.y += b.y; v.z += b.z; v.w += b.w;
@@ -139,10 +148,11 @@ __global__ __launch_bounds__(256) void bnx_dy_kernel(const float* __restrict__ d
   if (Mv <= 0) return;
   const long long total = (long long)Mv * C4;
   const long long base = (long long)g * gstride;
+  const bool inl = C <= 512;   // (wider BNs: the coefficient rows from global memory, never claimed)
+  const float* cf = coef + (long long)g * kBnRows * C;
   if (claim) {
     bnf_consume_bwd(f, f.which, g, Mv, kA, kB, kK, blockIdx.x == 0);
-  } else {
-    const float* cf = coef + (long long)g * kBnRows * C;
+  } else if (inl) {
     for (int c = threadIdx.x; c < C; c += 256) {
       kA[c] = cf[kCA * C + c];
       kB[c] = cf[kCB * C + c];
@@ -150,12 +160,15 @@ __global__ __launch_bounds__(256) void bnx_dy_kernel(const float* __restrict__ d
     }
     __syncthreads();
   }
+  const float* pA = inl ? kA : cf + kCA * C;
+  const float* pB = inl ? kB : cf + kCB * C;
+  const float* pK = inl ? kK : cf + kCK * C;
   float vmax = 0.f;
   for (long long t = blockIdx.x * 256LL + threadIdx.x; t < total; t += (long long)gridDim.x * 256) {
     const int c = (int)(t % C4) * 4;
     const long long o = base + t * 4;
     const float4 dv = *(const float4*)(d + o), yv = *(const float4*)(y + o);
-    const float4 A = *(const float4*)&kA[c], B = *(const float4*)&kB[c], K = *(const float4*)&kK[c];
+    const float4 A = *(const float4*)&pA[c], B = *(const float4*)&pB[c], K = *(const float4*)&pK[c];
     const float4 v = make_float4(fmaf(A.x, dv.x, fmaf(B.x, yv.x, K.x)), fmaf(A.y, dv.y, fmaf(B.y, yv.y, K.y)),
                                  fmaf(A.z, dv.z, fmaf(B.z, yv.z, K.z)), fmaf(A.w, dv.w, fmaf(B.w, yv.w, K.w)));
     vmax = fmaxf(vmax, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
@@ -204,7 +217,7 @@ DBA_EXPORT int dba_bnx_apply(const float* ya, const float* ca, const float* res,
                              int relu_b, int relu, float* out, long long gstride, const int* nvalid, int G, int N, int HW, int C,
                              int* amax, int amax_ld, const void* fa, const void* fb, void* stream) {
   if (C & 3) return -102;
-  if (C > 512) return -108;
+  if (C > 512 && (fa || fb)) return -108;
   const BnFuse za{}, ba = fa ? *(const BnFuse*)fa : za, bb = fb ? *(const BnFuse*)fb : za;
   if ((fa && (ba.mode != 1 || ba.C != C)) || (fb && (bb.mode != 1 || bb.C != C || !yb))) return -108;
   const long long per = (long long)N * HW * (C / 4);
@@ -221,7 +234,7 @@ DBA_EXPORT int dba_bnx_dy(const float* d, const float* y, const float* coef, flo
                           const int* nvalid, int G, int N, int HW, int C, int* amax, int amax_ld, const void* f,
                           void* stream) {
   if (C & 3) return -102;
-  if (C > 512) return -108;
+  if (C > 512 && f) return -108;
   const BnFuse z{}, bf = f ? *(const BnFuse*)f : z;
   if (f && (bf.mode != 2 || bf.C != C)) return -108;
   const long long per = (long long)N * HW * (C / 4);

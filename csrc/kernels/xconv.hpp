@@ -625,10 +625,13 @@ int xconv_tile(const XArgs& a, long long Mmax, int G, int nclass, int bm, hipStr
 
 
 // the implicit GEMM's tile rows for a launch (xconv_tile maps it to the kernel's BM).  Small
-// launches (a lone client's grouped step) take 64-row tiles, the smallest (a lone client's
-// stage-3/4 convs: 32-64 tiles of 64 rows) 32-row tiles with one 32x32 MFMA tile per wave.
+// launches (a lone client's grouped step) take 64-row tiles, the smallest (the stage-3/4 convs
+// of 1-3 clients: 32-64 tiles of 64 rows per replica) 32-row tiles with one 32x32 MFMA tile per
+// wave — which also admits them to the in-launch split-K combine (sk_ok).  (Round 6: 512, was
+// 256 = the lone client only; a 2-client step's stage-3/4 convs then took the in-block-slab or
+// slab + standalone BN pass forms: 7 bnx_tile launches of 16 us per step.)
 int xconv_bm(long long Mmax, int Ncol, int G, int nclass, int splitk) {
-  constexpr int kBm32Below = 256;
+  constexpr int kBm32Below = 512;
   const int bn = Ncol <= 32 ? 32 : Ncol <= 64 ? 64 : 128;
   const long long blocks = (long long)ceil_div(Mmax, 128) * ceil_div(Ncol, bn) * G * nclass * splitk;
   int bm = (bn > 32 && blocks < 512) ? 64 : 128;

@@ -845,7 +845,8 @@ def set_bn_claim(on: int) -> int:
 
 
 def _claim(st, kind: str):
-    return st.claim(kind) if _BN_CLAIM else None
+    # (the consumers stage a record's coefficients in LDS: BNs of <= 512 channels)
+    return st.claim(kind) if (_BN_CLAIM and st.C <= 512) else None
 
 
 def bn_flush() -> None:
