@@ -1230,10 +1230,14 @@ def softmax_xent(logits, labels, mean, want_grad, stats=None, slot=None, nvalid=
     return (loss64 if loss64 is not None else loss), correct, dl
 
 
+_FUSED_HEAD = os.environ.get("DBA_FUSED_HEAD", "1") != "0"
+
+
 def head_ok(x, w) -> bool:
     """The fused classifier head (loss.hip head_kernel) takes this training head: fp32 last block
-    output [G, N, H, W, C] (C <= 512, N <= 256) and a linear layer of <= 16 classes."""
-    return (x.dtype == _F32 and x.dim() == 5 and x.shape[-1] <= 512 and x.shape[-1] % 4 == 0 and x.shape[1] <= 256
+    output [G, N, H, W, C] (C <= 512, N <= 256) and a linear layer of <= 16 classes.
+    ``DBA_FUSED_HEAD=0``: off (the unfused ops; A/B)."""
+    return (_FUSED_HEAD and x.dtype == _F32 and x.dim() == 5 and x.shape[-1] <= 512 and x.shape[-1] % 4 == 0 and x.shape[1] <= 256
             and w.dim() == 3 and w.shape[1] <= 16 and w.shape[2] == x.shape[-1] and w.dtype == _F32
             and w.stride(2) == 1 and w.stride(1) == w.shape[2])
 

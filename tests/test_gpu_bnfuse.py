@@ -285,6 +285,8 @@ def test_consumer_finalize_bitwise_equals_standalone(H, arch, shp, G):
     nval = torch.tensor([N, 9, 5][:G], dtype=torch.int32, device=dev)
     x = torch.rand(G, N, *shp, device=dev)
     lab = torch.randint(0, spec.num_classes, (G, N), device=dev).int()
+    # rows past a replica's valid count are padding (label -1), as the trainer's gather makes them
+    lab = torch.where(torch.arange(N, device=dev)[None] < nval[:, None].long(), lab, torch.full_like(lab, -1))
 
     def run():
         state = flat.to(dev)[None].repeat(G, 1).contiguous()
@@ -299,17 +301,6 @@ def test_consumer_finalize_bitwise_equals_standalone(H, arch, shp, G):
         torch.cuda.synchronize()
         return loss, grads, state
 
-    prev = H.set_bn_claim(0)
-    try:
-        l0, g0, s0 = run()
-    finally:
-        H.set_bn_claim(prev)
-    H.set_bn_claim(1)
-    l1, g1, s1 = run()
-    l2, g2, s2 = run()
-    H.set_bn_claim(prev)
-    assert torch.equal(l1, l2) and torch.equal(g1, g2) and torch.equal(s1, s2), "claim path not reproducible"
-
     def where(a, b):
         bad = (a != b).nonzero()
         if not len(bad):
@@ -318,6 +309,20 @@ def test_consumer_finalize_bitwise_equals_standalone(H, arch, shp, G):
         name = next((e.name for e in spec.params + spec.buffers if e.offset <= i < e.offset + e.numel), "?")
         return f"{len(bad)} differ, first replica {r} index {i} ({name}): {a[r, i].item()} vs {b[r, i].item()}"
 
+    prev = H.set_bn_claim(0)
+    try:
+        l0, g0, s0 = run()
+        l0b, g0b, s0b = run()
+    finally:
+        H.set_bn_claim(prev)
+    H.set_bn_claim(1)
+    l1, g1, s1 = run()
+    l2, g2, s2 = run()
+    H.set_bn_claim(prev)
+    assert torch.equal(l0, l0b) and torch.equal(g0, g0b) and torch.equal(s0, s0b), \
+        ("standalone path not reproducible", where(g0, g0b), where(s0, s0b))
+    assert torch.equal(l1, l2) and torch.equal(g1, g2) and torch.equal(s1, s2), \
+        ("claim path not reproducible", where(g1, g2), where(s1, s2))
     assert torch.equal(l0, l1), (l0, l1)
     assert torch.equal(g0, g1), where(g0, g1)
     assert torch.equal(s0, s1), where(s0, s1)

@@ -29,12 +29,17 @@ SHAPES = [
     (1, 64, 8, 128, 128, 64),    # lone client, stage 3
     (1, 64, 8, 128, 128, 23),    # lone client, last (partial) batch
     (1, 40, 4, 256, 256, 40),
+    # round 6: launches of up to 3 clients take the 32 x 128 tiles and the combine too
+    (2, 64, 8, 128, 128, None),  # two clients, stage 3 (one partly valid)
+    (3, 64, 4, 256, 256, None),  # three clients, stage 4 (full, partial, inactive)
 ]
 
 
 def test_inlaunch_combine_scope(H):
-    """Groups take 64 / 128-row tiles, where the separate reduce launch is cheaper."""
-    assert int(H._L.dba_xconv_sk_ints(3, 64, 8, 8, 128, 128, 3, 3)) == 0
+    """Launches of up to 3 clients' stage-3/4 convs take the combine; larger groups take 64 /
+    128-row tiles, where the separate reduce launch is cheaper."""
+    assert int(H._L.dba_xconv_sk_ints(3, 64, 8, 8, 128, 128, 3, 3)) > 0
+    assert int(H._L.dba_xconv_sk_ints(4, 64, 8, 8, 128, 128, 3, 3)) == 0
     assert int(H._L.dba_xconv_sk_ints(10, 64, 4, 4, 256, 256, 3, 3)) == 0
     assert int(H._L.dba_xconv_sk_ints(1, 64, 16, 16, 64, 64, 3, 3)) == 0   # no split
 
