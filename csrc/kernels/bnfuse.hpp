@@ -385,6 +385,52 @@ __device__ __forceinline__ void bnf_tile_records(const BnFuse& f, float* Ct, con
     }
   }
   __syncthreads();   // every thread is done reading Ct
+  const int ka = bnf_kacc(mode), nl = mode == 1 ? 6 : 9;
+  const int sub = (m0 / BM) % f.nsub;
+  constexpr int TPC = 256 / BN;   // threads sharing a column when 256 % BN == 0
+  if constexpr (256 % BN == 0 && KA * (256 - BN) * 8 <= BM * BN * 4) {
+    // a thread's pairs all lie in column threadIdx.x % BN: their limbs add in registers, then the
+    // column's TPC threads meet in LDS (lane-contiguous int64 slots), then one atomic set per column
+    long long t[KA];
+#pragma unroll
+    for (int k = 0; k < KA; ++k) t[k] = 0;
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+#pragma unroll
+      for (int k = 0; k < KA; ++k)
+        if (k < nl) t[k] += lim[u][k];
+        else t[k] = (long long)max((unsigned long long)t[k], (unsigned long long)lim[u][k]);
+    }
+    const int cc = threadIdx.x % BN, j = threadIdx.x / BN;
+    if constexpr (TPC > 1) {
+      long long* L = reinterpret_cast<long long*>(Ct);
+      if (j > 0) {
+#pragma unroll
+        for (int k = 0; k < KA; ++k) L[(k * (TPC - 1) + j - 1) * BN + cc] = t[k];
+      }
+      __syncthreads();
+      if (j == 0) {
+#pragma unroll
+        for (int i = 0; i < TPC - 1; ++i)
+#pragma unroll
+          for (int k = 0; k < KA; ++k) {
+            const long long v = L[(k * (TPC - 1) + i) * BN + cc];
+            if (k < nl) t[k] += v;
+            else t[k] = (long long)max((unsigned long long)t[k], (unsigned long long)v);
+          }
+      }
+    }
+    const int n = n0 + cc;
+    if (j == 0 && n < C) {
+      unsigned long long* dst = (unsigned long long*)(f.acc + (((long long)g * C + n) * f.nsub + sub) * ka);
+      for (int k = 0; k < nl; ++k)
+        if (t[k] != 0) __hip_atomic_fetch_add(dst + k, (unsigned long long)t[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      for (int k = nl; k < ka; ++k)
+        if (t[k] != 0) __hip_atomic_fetch_max(dst + k, (unsigned long long)t[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if constexpr (TPC > 1) __syncthreads();   // (LDS reads done before the caller reuses Ct)
+    return;
+  }
   long long* L = reinterpret_cast<long long*>(Ct);
 #pragma unroll
   for (int u = 0; u < PER; ++u) {
@@ -395,8 +441,6 @@ __device__ __forceinline__ void bnf_tile_records(const BnFuse& f, float* Ct, con
     }
   }
   __syncthreads();
-  const int ka = bnf_kacc(mode), nl = mode == 1 ? 6 : 9;
-  const int sub = (m0 / BM) % f.nsub;
   for (int cc = threadIdx.x; cc < BN; cc += 256) {
     const int n = n0 + cc;
     if (n >= C) continue;

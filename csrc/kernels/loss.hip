@@ -202,67 +202,67 @@ DBA_EXPORT int dba_softmax_xent(const float* logits, const int* labels, int G, i
 }
 
 // ============================================================ fused classifier head (training)
-// The CIFAR ResNets' head of a training step in ONE launch per replica group: global average
-// pool of the last block output, the linear layer, softmax cross-entropy + correct count (+ the
-// per-client statistics slots), and the head's backward — dlogits, the linear layer's bias and
-// weight gradients and the gradient of the pooled features (the BN finish pass consumes it:
+// The CIFAR ResNets' head of a training step in TWO launches: global average pool of the last
+// block output, the linear layer, softmax cross-entropy + correct count (+ the per-client
+// statistics slots), and the head's backward — dlogits, the linear layer's bias and weight
+// gradients and the gradient of the pooled features (the BN finish pass consumes it:
 // xbn.hip bnx_tile_kernel's pooled mode).  Reference: models/resnet_cifar.py:97-100
 // (avg_pool2d, view, linear) and image_train.py:85-92 (cross_entropy, backward).
-// Replaces ~8 launches of a lone client's step (avgpool, the 1x1 linear conv, xent, two bias
-// column sums, the FC weight gradient + its slab, the 1x1 data gradient, operand maxima).
+// Replaces ~8 launches of a step (avgpool, the 1x1 linear conv, xent, two bias column sums,
+// the FC weight gradient + its slab, the 1x1 data gradient, operand maxima).
+//   head_rows_kernel  grid (row blocks of 4, replicas): pools its rows (every pixel load of a
+//                     row issued at once), logits, cross-entropy, dlogits, the rows' pooled-
+//                     feature gradient; writes pooled / dlogits rows and the block's (loss,
+//                     correct) partial;
+//   head_fin_kernel   grid (column blocks, replicas): the weight gradient (row quarters, then
+//                     the quarters in a fixed order), the bias gradient, the partials in block
+//                     order and the statistics slots.
 // Arithmetic: the pool is avgpool_kernel's (channel sums in pixel order, / HW); every dot
 // product is an exact-fp32 FMA chain in a fixed order (4 lanes x strided quarters for the
-// logits, then a fixed butterfly; row order for the gradients): fp32-level, deterministic, and
-// a replica's bits depend on its own rows only.  One block per replica: K <= 16 classes,
-// C <= 512 features, N <= 256 rows (checked on the host).
+// logits, then a fixed butterfly; 4 row quarters for the weight gradient): fp32-level, deterministic, and
+// a replica's bits depend on its own rows only.  K <= 16 classes, C <= 512 features, N <= 256
+// rows, HW <= 64 pixels (checked on the host).  (A one-launch form with one block per replica
+// was slower than the unfused ops: its pooling pass is one CU streaming the replica's whole
+// last activation.)
 namespace {
 
-constexpr int kHeadK = 16;
+constexpr int kHeadK = 16, kHeadRows = 4, kHeadHW = 64;
 
-__global__ __launch_bounds__(256) void head_kernel(
+__global__ __launch_bounds__(256) void head_rows_kernel(
     const float* __restrict__ feat, long long f_gstride, int N, int HW, int C, const float* __restrict__ W,
     long long w_sstride, const float* __restrict__ bias, long long b_sstride, int K, const int* __restrict__ labels,
-    const int* __restrict__ nvalid, float* __restrict__ pooled, float* __restrict__ dW, long long dw_gstride,
-    float* __restrict__ db, long long db_gstride, float* __restrict__ dpool, float* __restrict__ loss_out,
-    float* __restrict__ corr_out, float* __restrict__ stats, long long stats_stride, const int* __restrict__ slot,
-    int max_slots, int mean) {
-  __shared__ float Wl[kHeadK * 512];
-  __shared__ float lg[256 * kHeadK];     // logits, then dlogits, [n][k]
-  const int g = blockIdx.x, tid = threadIdx.x;
+    const int* __restrict__ nvalid, float* __restrict__ pooled, float* __restrict__ dlog, float* __restrict__ dpool,
+    double* __restrict__ part, int mean) {
+  __shared__ __attribute__((aligned(16))) float pl[kHeadRows * 512];   // the block's pooled rows
+  __shared__ float lg[kHeadRows * kHeadK];                             // logits, then dlogits
+  const int g = blockIdx.y, nb = gridDim.x, tid = threadIdx.x;
   const int nv = valid_rows(nvalid, g, N);
+  const int r0 = blockIdx.x * kHeadRows, nr = max(0, min(kHeadRows, nv - r0));
   const int* lab = labels + (long long)g * N;
   const float* fg = feat + (long long)g * f_gstride;
-  float* pg = pooled + (long long)g * N * C;
-  for (int e = tid; e < K * C; e += 256) Wl[e] = W[(long long)g * w_sstride + e];
-  // 1. pooled[n][c] = (sum over pixels in order) / HW
+  const float* Wg = W + (long long)g * w_sstride;
+  // 1. pooled[n][c] = (sum over pixels in order) / HW: a thread's (row, 4-channel) item, all its
+  //    pixel loads issued before the adds
   const int C4 = C >> 2;
-  for (int e = tid; e < nv * C4; e += 256) {
+  for (int e = tid; e < nr * C4; e += 256) {
     const int n = e / C4, c = (e - n * C4) * 4;
+    const float* src = fg + (long long)(r0 + n) * HW * C + c;
+    float4 v[kHeadHW / 4];
     float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int i = 0; i < HW; ++i) {
-      const float4 v = *(const float4*)(fg + ((long long)n * HW + i) * C + c);
-      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    for (int i0 = 0; i0 < HW; i0 += kHeadHW / 4) {
+#pragma unroll
+      for (int i = 0; i < kHeadHW / 4; ++i)
+        if (i0 + i < HW) v[i] = *(const float4*)(src + (long long)(i0 + i) * C);
+#pragma unroll
+      for (int i = 0; i < kHeadHW / 4; ++i)
+        if (i0 + i < HW) { s.x += v[i].x; s.y += v[i].y; s.z += v[i].z; s.w += v[i].w; }
     }
     const float hw = (float)HW;
-    *(float4*)(pg + (long long)n * C + c) = make_float4(s.x / hw, s.y / hw, s.z / hw, s.w / hw);
+    const float4 p = make_float4(s.x / hw, s.y / hw, s.z / hw, s.w / hw);
+    *(float4*)&pl[n * C + c] = p;
+    *(float4*)(pooled + ((long long)g * N + r0 + n) * C + c) = p;
   }
-  __syncthreads();
-  // 2. logits[n][k]: 4 lanes per (row, class), quarter q sums c = q, q + 4, ... (FMA chain), then
-  //    the butterfly (q0 + q1) + (q2 + q3), then + bias
-  const float* bg = bias + (long long)g * b_sstride;
-  for (int p0 = 0; p0 < nv * K; p0 += 64) {
-    const int p = p0 + (tid >> 2), q = tid & 3;
-    const bool live = p < nv * K;
-    const int n = live ? p / K : 0, k = live ? p - n * K : 0;
-    float s = 0.f;
-    if (live)
-      for (int c = q; c < C; c += 4) s = fmaf(pg[(long long)n * C + c], Wl[k * C + c], s);
-    s += __shfl_xor(s, 1, kWave);
-    s += __shfl_xor(s, 2, kWave);
-    if (live && q == 0) lg[n * kHeadK + k] = s + bg[k];
-  }
-  __syncthreads();
-  // 3. softmax cross-entropy per row (xent_kernel's arithmetic, L = 1), dlogits into lg
+  // the replica's valid labels (the mean's divisor)
   __shared__ int scnt[4];
   int cnt = 0;
   for (int b = tid; b < N; b += 256) cnt += lab[b] >= 0;
@@ -270,68 +270,168 @@ __global__ __launch_bounds__(256) void head_kernel(
   if ((tid & 63) == 0) scnt[tid >> 6] = cnt;
   __syncthreads();
   const int ncnt = scnt[0] + scnt[1] + scnt[2] + scnt[3];
+  // 2. logits: 4 lanes per (row, class), quarter q sums c = q, q + 4, ... (FMA chain), then the
+  //    butterfly (q0 + q1) + (q2 + q3), then + bias
+  {
+    const int p = tid >> 2, q = tid & 3;
+    const bool live = p < nr * K;
+    const int n = live ? p / K : 0, k = live ? p - n * K : 0;
+    float s = 0.f;
+    if (live) {
+#pragma unroll 8
+      for (int c = q; c < C; c += 4) s = fmaf(pl[n * C + c], Wg[k * C + c], s);
+    }
+    s += __shfl_xor(s, 1, kWave);
+    s += __shfl_xor(s, 2, kWave);
+    if (live && q == 0) lg[n * kHeadK + k] = s + bias[(long long)g * b_sstride + k];
+  }
+  static_assert(kHeadRows * kHeadK * 4 <= 256, "one pass of 4-lane groups");
+  __syncthreads();
+  // 3. softmax cross-entropy per row (xent_kernel's arithmetic, L = 1), dlogits into lg
   const float scale = (mean && ncnt > 0) ? 1.0f / (float)ncnt : 1.0f;
   double wl = 0.0;
   float wc = 0.f;
-  for (int b = tid; b < nv; b += 256) {
-    float* x = lg + b * kHeadK;
-    const int y = lab[b];
+  if (tid < nr) {
+    float* x = lg + tid * kHeadK;
+    const int y = lab[r0 + tid];
     if (y < 0) {
       for (int c = 0; c < K; ++c) x[c] = 0.f;
-      continue;
+    } else {
+      float mx = x[0];
+      int am = 0;
+      for (int c = 1; c < K; ++c)
+        if (x[c] > mx) { mx = x[c]; am = c; }
+      float se = 0.f;
+      for (int c = 0; c < K; ++c) se += __expf(x[c] - mx);
+      const float lse = mx + __logf(se);
+      wl = (double)(lse - x[y]);
+      wc = (am == y) ? 1.f : 0.f;
+      for (int c = 0; c < K; ++c) x[c] = (__expf(x[c] - lse) - (c == y ? 1.f : 0.f)) * scale;
     }
-    float mx = x[0];
-    int am = 0;
-    for (int c = 1; c < K; ++c)
-      if (x[c] > mx) { mx = x[c]; am = c; }
-    float se = 0.f;
-    for (int c = 0; c < K; ++c) se += __expf(x[c] - mx);
-    const float lse = mx + __logf(se);
-    wl += (double)(lse - x[y]);
-    wc += (am == y) ? 1.f : 0.f;
-    for (int c = 0; c < K; ++c) x[c] = (__expf(x[c] - lse) - (c == y ? 1.f : 0.f)) * scale;
+    for (int c = 0; c < K; ++c) dlog[((long long)g * N + r0 + tid) * kHeadK + c] = x[c];
   }
-  xent_block_sum(wl, wc);   // (its barrier also publishes the dlogits)
-  if (tid == 0) xent_write(g, wl, wc, ncnt, mean, loss_out, nullptr, corr_out, stats, stats_stride, slot, max_slots, nvalid);
-  if (nv == 0) return;      // an inactive replica: no gradients written
-  // 4. bias and weight gradients (rows in order), 5. the pooled features' gradient (classes in order)
-  float* dbg = db + (long long)g * db_gstride;
-  float* dwg = dW + (long long)g * dw_gstride;
-  float* dpg = dpool + (long long)g * N * C;
-  if (tid < K) {
+  xent_block_sum(wl, wc);   // (its barriers also publish the dlogits)
+  if (tid == 0) {
+    part[((long long)g * nb + blockIdx.x) * 2] = wl;
+    part[((long long)g * nb + blockIdx.x) * 2 + 1] = (double)wc;
+  }
+  // 4. the rows' pooled-feature gradient: dpool[n][c] = sum_k dl[n][k] W[k][c] (classes in order)
+  for (int e = tid; e < nr * C; e += 256) {
+    const int n = e / C, c = e - n * C;
     float s = 0.f;
-    for (int n = 0; n < nv; ++n) s += lg[n * kHeadK + tid];
-    dbg[tid] = s;
+    for (int k = 0; k < K; ++k) s = fmaf(lg[n * kHeadK + k], Wg[k * C + c], s);
+    dpool[((long long)g * N + r0 + n) * C + c] = s;
   }
-  for (int c = tid; c < C; c += 256) {
-    for (int k = 0; k < K; ++k) {
-      float s = 0.f;
-      for (int n = 0; n < nv; ++n) s = fmaf(lg[n * kHeadK + k], pg[(long long)n * C + c], s);
-      dwg[k * C + c] = s;
+}
+
+// grid (column blocks of 64, replicas): the weight gradient dW[k][c] = sum over the valid rows
+// of dl[n][k] pooled[n][c] — a wave per row quarter (rows q, q + 4, ...; FMA chains), the
+// quarters added (q0 + q1) + (q2 + q3); column block 0 also the bias gradient (rows in order),
+// (loss, correct) from the row blocks' partials in block order and the statistics slots
+__global__ __launch_bounds__(256) void head_fin_kernel(
+    int N, int C, int K, const int* __restrict__ labels, const int* __restrict__ nvalid,
+    const float* __restrict__ pooled, const float* __restrict__ dlog, const double* __restrict__ part, int nb,
+    float* __restrict__ dW, long long dw_gstride, float* __restrict__ db, long long db_gstride,
+    float* __restrict__ loss_out, float* __restrict__ corr_out, float* __restrict__ stats, long long stats_stride,
+    const int* __restrict__ slot, int max_slots, int mean) {
+  const int g = blockIdx.y, tid = threadIdx.x;
+  const int nv = valid_rows(nvalid, g, N);
+  if (blockIdx.x == 0) {
+    const int* lab = labels + (long long)g * N;
+    __shared__ int scnt[4];
+    int cnt = 0;
+    for (int b = tid; b < N; b += 256) cnt += lab[b] >= 0;
+    for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o, kWave);
+    if ((tid & 63) == 0) scnt[tid >> 6] = cnt;
+    double wl = 0.0, wc = 0.0;
+    for (int s = tid; s < nb; s += 256) {
+      wl += part[((long long)g * nb + s) * 2];
+      wc += part[((long long)g * nb + s) * 2 + 1];
     }
-    for (int n = 0; n < nv; ++n) {
+    float wcf = (float)wc;
+    xent_block_sum(wl, wcf);
+    if (tid == 0)
+      xent_write(g, wl, wcf, scnt[0] + scnt[1] + scnt[2] + scnt[3], mean, loss_out, nullptr, corr_out, stats,
+                 stats_stride, slot, max_slots, nvalid);
+    if (nv > 0 && tid < K) {   // rows in order, 16 loads in flight per trip
+      const float* dl = dlog + (long long)g * N * kHeadK;
       float s = 0.f;
-      for (int k = 0; k < K; ++k) s = fmaf(lg[n * kHeadK + k], Wl[k * C + c], s);
-      dpg[(long long)n * C + c] = s;
+      for (int n0 = 0; n0 < nv; n0 += 16) {
+        float v[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) v[r] = n0 + r < nv ? dl[(n0 + r) * kHeadK + tid] : 0.f;
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          if (n0 + r < nv) s += v[r];
+      }
+      db[(long long)g * db_gstride + tid] = s;
     }
+  }
+  if (nv == 0) return;   // an inactive replica: no gradients written
+  __shared__ float sq[3][kHeadK][64];
+  const float* dl = dlog + (long long)g * N * kHeadK;
+  const float* pg = pooled + (long long)g * N * C;
+  const int q = tid >> 6, c = blockIdx.x * 64 + (tid & 63);
+  const bool live = c < C;
+  float s[kHeadK];
+#pragma unroll
+  for (int k = 0; k < kHeadK; ++k) s[k] = 0.f;
+  for (int n0 = q; n0 < nv; n0 += 16) {   // 4 of the quarter's rows per trip, loads first
+    float p[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int n = n0 + 4 * r;
+      p[r] = (live && n < nv) ? pg[(long long)n * C + c] : 0.f;
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int n = n0 + 4 * r;
+      if (n < nv) {
+#pragma unroll
+        for (int k = 0; k < kHeadK; ++k)
+          if (k < K) s[k] = fmaf(dl[n * kHeadK + k], p[r], s[k]);
+      }
+    }
+  }
+  if (q > 0) {
+#pragma unroll
+    for (int k = 0; k < kHeadK; ++k) sq[q - 1][k][tid & 63] = s[k];
+  }
+  __syncthreads();
+  if (q == 0 && live) {
+#pragma unroll
+    for (int k = 0; k < kHeadK; ++k)
+      if (k < K)
+        dW[(long long)g * dw_gstride + k * C + c] =
+            (s[k] + sq[0][k][tid]) + (sq[1][k][tid] + sq[2][k][tid]);
   }
 }
 
 }  // namespace
 
+// workspace doubles of dba_head_train (the row blocks' loss partials)
+DBA_EXPORT long long dba_head_part_doubles(int G, int N) {
+  return 2LL * G * ((N + kHeadRows - 1) / kHeadRows);
+}
+
 // feat [G][N][H][W][C] (replica stride f_gstride) fp32, W / bias the replicas' rows [G][K][C] /
-// [G][K] (strides), labels [G][N] int (< 0: padding), nvalid [G]; pooled / dpool [G][N][C] fp32
-// workspace / output; dW [G][K][C], db [G][K] (strides) overwritten for active replicas.
+// [G][K] (strides), labels [G][N] int (< 0: padding), nvalid [G]; pooled / dpool [G][N][C] fp32,
+// dlog [G][N][16] fp32 and part (dba_head_part_doubles) workspaces / outputs; dW [G][K][C],
+// db [G][K] (strides) overwritten for active replicas.
 DBA_EXPORT int dba_head_train(const float* feat, long long f_gstride, int G, int N, int HW, int C, const float* W,
                               long long w_sstride, const float* bias, long long b_sstride, int K, const int* labels,
-                              const int* nvalid, float* pooled, float* dW, long long dw_gstride, float* db,
-                              long long db_gstride, float* dpool, float* loss, float* correct, float* stats,
-                              long long stats_stride, const int* slot, int max_slots, int mean, void* stream) {
-  if (K < 1 || K > kHeadK || C > 512 || (C & 3) || N > 256 || (((uintptr_t)feat | (uintptr_t)pooled |
-      (uintptr_t)dpool) & 15) || (f_gstride & 3))
+                              const int* nvalid, float* pooled, float* dlog, double* part, float* dW,
+                              long long dw_gstride, float* db, long long db_gstride, float* dpool, float* loss,
+                              float* correct, float* stats, long long stats_stride, const int* slot, int max_slots,
+                              int mean, void* stream) {
+  if (K < 1 || K > kHeadK || C > 512 || (C & 3) || N > 256 || HW > kHeadHW || HW < 1 ||
+      (((uintptr_t)feat | (uintptr_t)pooled | (uintptr_t)dpool) & 15) || (f_gstride & 3))
     return -100;
-  hipLaunchKernelGGL(head_kernel, dim3(G), dim3(256), 0, (hipStream_t)stream, feat, f_gstride, N, HW, C, W, w_sstride,
-                     bias, b_sstride, K, labels, nvalid, pooled, dW, dw_gstride, db, db_gstride, dpool, loss, correct,
-                     stats, stats_stride, slot, max_slots, mean);
+  const int nb = (N + kHeadRows - 1) / kHeadRows;
+  hipLaunchKernelGGL(head_rows_kernel, dim3(nb, G), dim3(256), 0, (hipStream_t)stream, feat, f_gstride, N, HW, C, W,
+                     w_sstride, bias, b_sstride, K, labels, nvalid, pooled, dlog, dpool, part, mean);
+  hipLaunchKernelGGL(head_fin_kernel, dim3((C + 63) / 64, G), dim3(256), 0, (hipStream_t)stream, N, C, K, labels, nvalid, pooled,
+                     dlog, part, nb, dW, dw_gstride, db, db_gstride, loss, correct, stats, stats_stride, slot,
+                     max_slots, mean);
   DBA_LAUNCH_CHECK();
 }

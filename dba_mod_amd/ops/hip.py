@@ -46,8 +46,9 @@ _SIGS = {
     "dba_dropout": [_P, _P, _I, _P, _U, _F, _LL, _I, _P],
     "dba_softmax_xent": [_P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _LL, _P, _I, _P, _I, _P, _P, _P],
     "dba_softmax_xent_part_doubles": [_I, _I],
-    "dba_head_train": [_P, _LL, _I, _I, _I, _I, _P, _LL, _P, _LL, _I, _P, _P, _P, _P, _LL, _P, _LL, _P, _P, _P, _P,
-                       _LL, _P, _I, _I, _P],
+    "dba_head_train": [_P, _LL, _I, _I, _I, _I, _P, _LL, _P, _LL, _I, _P, _P, _P, _P, _P, _P, _LL, _P, _LL, _P, _P,
+                       _P, _P, _LL, _P, _I, _I, _P],
+    "dba_head_part_doubles": [_I, _I],
     "dba_sgd_step": [_P, _LL, _P, _P, _P, _P, _P, _F, _F, _P, _I, _I, _P],
     "dba_scale_from_base": [_P, _P, _F, _P, _LL, _P],
     "dba_add_noise_scaled": [_P, _P, _LL, _F, _F, _U, _I, _I, _P],
@@ -105,6 +106,7 @@ _L.dba_xwgrad_ws_floats.restype = ctypes.c_longlong
 _L.dba_xwgrad_stem_ws_floats.restype = ctypes.c_longlong
 _L.dba_xcolsum_part_doubles.restype = ctypes.c_longlong
 _L.dba_softmax_xent_part_doubles.restype = ctypes.c_longlong
+_L.dba_head_part_doubles.restype = ctypes.c_longlong
 
 
 class _BnFuse(ctypes.Structure):
@@ -812,10 +814,16 @@ ACC_PER_REPLICA = 1 << 17              # arena int64 per replica for a training 
 ACC_STATS = {"arena": 0, "fallback": 0}
 
 
+_ACC_ROWS = int(os.environ.get("DBA_ACC_ROWS", "4096"))
+_ACC_NSUB_MAX = int(os.environ.get("DBA_ACC_NSUB", "8"))
+
+
 def _acc_nsub(M: int) -> int:
-    """Spread copies of a BN accumulator record per channel: one per 4096 rows of a replica, at
-    most 8, so each copy takes a bounded number of the producers' tile atomics."""
-    return max(1, min(8, M // 4096))
+    """Spread copies of a BN accumulator record per channel: one per ``DBA_ACC_ROWS`` rows of a
+    replica, at most ``DBA_ACC_NSUB``, so each copy takes a bounded number of the producers' tile
+    atomics (device-scope atomics are performed past the per-XCD L2s: same-address ones
+    serialise)."""
+    return max(1, min(_ACC_NSUB_MAX, M // _ACC_ROWS))
 
 
 def _acc_new(n: int, device):
@@ -830,7 +838,7 @@ def _acc_new(n: int, device):
 
 
 _LIVE_PENDING: list = []   # every record not yet finalised (bn_flush)
-_BN_CLAIM = True
+_BN_CLAIM = os.environ.get("DBA_BN_CLAIM", "1") != "0"   # DBA_BN_CLAIM=0: standalone finalizes (A/B)
 
 
 def set_bn_claim(on: int) -> int:
@@ -1234,16 +1242,17 @@ _FUSED_HEAD = os.environ.get("DBA_FUSED_HEAD", "1") != "0"
 
 
 def head_ok(x, w) -> bool:
-    """The fused classifier head (loss.hip head_kernel) takes this training head: fp32 last block
-    output [G, N, H, W, C] (C <= 512, N <= 256) and a linear layer of <= 16 classes.
+    """The fused classifier head (loss.hip head_rows_kernel) takes this training head: fp32 last
+    block output [G, N, H, W, C] (C <= 512, N <= 256, H * W <= 64) and a linear layer of <= 16 classes.
     ``DBA_FUSED_HEAD=0``: off (the unfused ops; A/B)."""
     return (_FUSED_HEAD and x.dtype == _F32 and x.dim() == 5 and x.shape[-1] <= 512 and x.shape[-1] % 4 == 0 and x.shape[1] <= 256
+            and x.shape[2] * x.shape[3] <= 64
             and w.dim() == 3 and w.shape[1] <= 16 and w.shape[2] == x.shape[-1] and w.dtype == _F32
             and w.stride(2) == 1 and w.stride(1) == w.shape[2])
 
 
 def head_train(x, w, b, labels, nvalid, dw, db, stats=None, slot=None, mean=True):
-    """The training head in one launch (loss.hip head_kernel): pooled = avgpool(x), logits =
+    """The training head in two launches (loss.hip head_rows_kernel / head_fin_kernel): pooled = avgpool(x), logits =
     pooled W^T + b, softmax cross-entropy (mean over valid rows) + correct count (+ ``stats``
     slots), and its backward: ``dw`` / ``db`` overwritten for the active replicas, the pooled
     features' gradient returned.  Returns (loss [G], correct [G], dpool [G, N, 1, 1, C])."""
@@ -1252,6 +1261,8 @@ def head_train(x, w, b, labels, nvalid, dw, db, stats=None, slot=None, mean=True
     K = w.shape[1]
     assert head_ok(x, w) and b.stride(-1) == 1 and dw.stride(-1) == 1 and db.stride(-1) == 1
     pooled = torch.empty(G, N, C, dtype=_F32, device=x.device)
+    dlog = torch.empty(G, N, 16, dtype=_F32, device=x.device)
+    part = torch.empty(int(_L.dba_head_part_doubles(G, N)), dtype=torch.float64, device=x.device)
     dpool = torch.empty(G, N, 1, 1, C, dtype=_F32, device=x.device)
     loss = torch.empty(G, dtype=_F32, device=x.device)
     correct = torch.empty(G, dtype=_F32, device=x.device)
@@ -1260,7 +1271,8 @@ def head_train(x, w, b, labels, nvalid, dw, db, stats=None, slot=None, mean=True
         ms = stats.shape[1] // G
         sp, ss, slp = stats.data_ptr(), stats.shape[1], _i32(slot).data_ptr()
     rc = _call("dba_head_train", x.data_ptr(), x.stride(0), G, N, H * W_, C, w.data_ptr(), w.stride(0), b.data_ptr(),
-               b.stride(0), K, _i32(labels).data_ptr(), _ptr(_i32(nvalid)), pooled.data_ptr(), dw.data_ptr(),
+               b.stride(0), K, _i32(labels).data_ptr(), _ptr(_i32(nvalid)), pooled.data_ptr(), dlog.data_ptr(),
+               part.data_ptr(), dw.data_ptr(),
                dw.stride(0), db.data_ptr(), db.stride(0), dpool.data_ptr(), loss.data_ptr(), correct.data_ptr(), sp, ss,
                slp, ms, int(bool(mean)), _stream())
     if rc == NOT_HANDLED:
