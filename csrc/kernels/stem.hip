@@ -12,8 +12,8 @@
 // slots); the pixel's receptive field streams through registers one kernel row at a time.
 // Every output is an fp32 FMA chain in fixed (kh, kw, ci) order: exact fp32 arithmetic and
 // deterministic.  Epilogue: bias, residual, ReLU, the fp16-pair max slot of the output
-// (common.hpp amax_fold) and, for a training BN, the fused BN statistics (bnfuse.hpp
-// bnf_tile_records: integer accumulator atomics).
+// (common.hpp amax_fold) and, for a training BN, the level-0 records of the fused BN statistics
+// (bnfuse.hpp bnf_tile_records' definition).
 #include "common.hpp"
 #include "bnfuse.hpp"
 
@@ -40,7 +40,6 @@ __global__ __launch_bounds__(256) void xstem_kernel(const StemArgs a) {
   static_assert(COUT % CPT == 0 && CPT % 4 == 0, "channel groups of 4");
   __shared__ __attribute__((aligned(16))) float wt[K * COUT];          // [k][COUT]
   __shared__ __attribute__((aligned(16))) float tile[PIX * COUT];       // BN statistics tile
-  __shared__ long long srow[PIX];                                       // its valid rows
 
   const int g = blockIdx.y;
   const int tid = threadIdx.x;
@@ -112,17 +111,31 @@ __global__ __launch_bounds__(256) void xstem_kernel(const StemArgs a) {
         acc[c4 * 4] = v.x; acc[c4 * 4 + 1] = v.y; acc[c4 * 4 + 2] = v.z; acc[c4 * 4 + 3] = v.w;
       }
     }
-    if constexpr (PIX % kBnGrp == 0) {
     if (want_stats) {   // statistics of the raw output (fused BN implies no bias / residual / ReLU)
       if (pl < PIX) {
 #pragma unroll
         for (int c = 0; c < CPT; ++c) tile[pl * COUT + c0 + c] = live ? acc[c] : 0.f;
       }
-      if (tid < PIX) srow[tid] = m0 + tid < Mv ? 0 : -1;
       __syncthreads();
-      bnf_tile_records<PIX, COUT>(a.bf, tile, srow, g, m0, 0, Mv);   // (bnfuse.hpp: accumulator atomics)
+      if (a.bf.mode == 1) {   // level-0 records (bnfuse.hpp bnf_tile_records' order)
+        const int gv = ceil_div_d(Mv, kBnGrp);
+        for (int e = tid; e < (PIX / 32) * COUT; e += 256) {
+          const int grp = e / COUT, c = e - grp * COUT, b = m0 / 32 + grp;
+          if (b >= gv) continue;
+          double r4[4];
+          bnf_init(r4, 1);
+          for (int r = 0; r < 32; ++r) {
+            if (m0 + grp * 32 + r >= Mv) break;
+            const double v = (double)tile[(grp * 32 + r) * COUT + c];
+            r4[0] += v;
+            r4[1] = fma(v, v, r4[1]);
+            r4[2] = fmax(r4[2], v);
+            r4[3] = fmin(r4[3], v);
+          }
+          bnf_store_rec(a.bf.rec0 + (((long long)g * COUT + c) * a.bf.ngrp + b) * 4, r4[0], r4[1], r4[2], r4[3]);
+        }
+      }
       __syncthreads();
-    }
     }
   }
   if (a.amax_out) amax_fold(a.amax_out, a.amax_ld, g, vmax);
@@ -137,7 +150,8 @@ int stem_go(const StemArgs& a, int G, hipStream_t st) {
   const dim3 grid((unsigned)ceil_div(M, PIX * ITER), G);
   hipLaunchKernelGGL((xstem_kernel<KH, KW, CIN, COUT, CPT, ITER>), grid, dim3(256), 0, st, a);
   const int rc = (int)hipGetLastError();
-  return rc;   // (the fused BN's record is finalised by its first consumer: bnfuse.hpp)
+  if (rc != 0 || !a.bf.mode) return rc;
+  return bnx_finalize_go(a.bf, a.nvalid, G, a.N, a.Ho * a.Wo, st);   // the fused BN's finalize
 }
 
 }  // namespace

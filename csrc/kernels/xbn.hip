@@ -1,6 +1,6 @@
 // fp32 family, the fused training BN's standalone passes (bnfuse.hpp): the tile pass over a
 // materialised tensor / split-K slabs / a pooled gradient, the stored block output (apply), the
-// stored BN input gradient (dy), and the standalone record finalisation.
+// stored BN input gradient (dy).
 #include "common.hpp"
 #include "bnfuse.hpp"
 #include <algorithm>
@@ -11,8 +11,8 @@ namespace {
 // A tile pass over a MATERIALISED tensor, for the producers whose epilogue cannot reduce: the
 // split-K slabs of multi-replica launches (summed here in z order, xsplitk_reduce's order, plus
 // the dgrad's accumulated branch), stride-s data gradients, the global average pool's gradient,
-// max-pool gradients.  Same 128-row tiles of whole groups, same accumulator records
-// (bnf_tile_records) as the conv epilogues, so the statistics are the same bits whichever
+// max-pool gradients.  Same 128-row tiles of whole groups, same level-0 records
+// (bnf_tile_records) and finalize launch as the conv epilogues, so the statistics are the same bits whichever
 // kernel produced them.  mode 1: statistics of the value (stored to dst
 // when dst is given); mode 2: d = mask(value) -> dst (may alias src).  value = src, or the sum of
 // S slabs ws[z] (+ accum), or pool[g][img][c] * pool_scale (elementwise.hip avgpool_bwd's value).
@@ -67,60 +67,33 @@ __global__ __launch_bounds__(256) void bnx_tile_kernel(const BnFuse f, const flo
 // relu?(fma(ya, scale_a, shift_a) + r), r = res (identity shortcut) or fma(yb, scale_b, shift_b)
 // (a shortcut conv's BN; relu_b: a lazy BN+ReLU output, e.g. the stem's) or 0 — bn.hip
 // bn_apply's arithmetic; folds max |out| for the fp16-pair operand scale of its consumers.
-// Valid rows only.  A BN whose record is still pending (claim_a / claim_b) has its coefficients
-// derived in the prologue (bnfuse.hpp bnf_consume_fwd; block 0 of each replica writes them).
+// Valid rows only.
 __global__ __launch_bounds__(256) void bnx_apply_kernel(const float* __restrict__ ya, const float* __restrict__ ca,
                                                         const float* __restrict__ res, const float* __restrict__ yb,
                                                         const float* __restrict__ cb, int relu_b, int relu,
                                                         float* __restrict__ out,
                                                         long long gstride, const int* __restrict__ nvalid, int N,
-                                                        int HW, int C, int* __restrict__ amax, int amax_ld,
-                                                        const BnFuse fa, int claim_a, const BnFuse fb, int claim_b) {
-  __shared__ __attribute__((aligned(16))) float sa[1024];   // scale | shift (C <= 512: checked on the host)
-  __shared__ __attribute__((aligned(16))) float sb[1024];
+                                                        int HW, int C, int* __restrict__ amax, int amax_ld) {
   const int g = blockIdx.y;
   const int C4 = C >> 2;
-  const int Mv = valid_rows(nvalid, g, N) * HW;
-  if (Mv <= 0) return;
-  const long long total = (long long)Mv * C4;
+  const long long total = (long long)valid_rows(nvalid, g, N) * HW * C4;
   const long long base = (long long)g * gstride;
-  auto stage = [&](const float* cf, const BnFuse& f, int claim, float* sx) __attribute__((always_inline)) {
-    if (claim) {
-      bnf_consume_fwd(f, g, Mv, sx, sx + 512, blockIdx.x == 0);
-    } else {
-      const float* c0 = cf + (long long)g * kBnRows * C;
-      for (int c = threadIdx.x; c < C; c += 256) {
-        sx[c] = c0[kCScale * C + c];
-        sx[512 + c] = c0[kCShift * C + c];
-      }
-    }
-  };
-  // (C > 512, e.g. ResNet-50's 2048-channel block outputs: the coefficient rows straight from
-  // global memory; such BNs are never claimed — checked on the host)
-  const bool inl = C <= 512;
-  if (inl) {
-    stage(ca, fa, claim_a, sa);
-    if (yb) stage(cb, fb, claim_b, sb);
-  }
-  __syncthreads();
-  const float* sca = inl ? sa : ca + (long long)g * kBnRows * C + kCScale * C;
-  const float* sha = inl ? sa + 512 : ca + (long long)g * kBnRows * C + kCShift * C;
-  const float* scb = inl ? sb : (cb ? cb + (long long)g * kBnRows * C + kCScale * C : nullptr);
-  const float* shb = inl ? sb + 512 : (cb ? cb + (long long)g * kBnRows * C + kCShift * C : nullptr);
+  const float* cag = ca + (long long)g * kBnRows * C;
+  const float* cbg = cb ? cb + (long long)g * kBnRows * C : nullptr;
   float vmax = 0.f;
   for (long long t = blockIdx.x * 256LL + threadIdx.x; t < total; t += (long long)gridDim.x * 256) {
     const int c = (int)(t % C4) * 4;
     const long long o = base + t * 4;
     const float4 y = *(const float4*)(ya + o);
-    const float4 sc = *(const float4*)&sca[c], sh = *(const float4*)&sha[c];
+    const float4 sc = *(const float4*)(cag + kCScale * C + c), sh = *(const float4*)(cag + kCShift * C + c);
     float4 v = make_float4(fmaf(y.x, sc.x, sh.x), fmaf(y.y, sc.y, sh.y), fmaf(y.z, sc.z, sh.z), fmaf(y.w, sc.w, sh.w));
     if (res) {
       const float4 r = *(const float4*)(res + o);
       v.x += r.x; v.y += r.y; v.z += r.z; v.w += r.w;
     } else if (yb) {
       const float4 u = *(const float4*)(yb + o);
-      const float4 s2 = *(const float4*)&scb[c], h2 = *(const float4*)&shb[c];
-      float4 b = make_float4(fmaf(u.x, s2.x, h2.x), fmaf(u.y, s2.y, h2.y), fmaf(u.z, s2.z, h2.z), fmaf(u.w, s2.w, h2.w));
+      const float4 sb = *(const float4*)(cbg + kCScale * C + c), hb = *(const float4*)(cbg + kCShift * C + c);
+      float4 b = make_float4(fmaf(u.x, sb.x, hb.x), fmaf(u.y, sb.y, hb.y), fmaf(u.z, sb.z, hb.z), fmaf(u.w, sb.w, hb.w));
       if (relu_b) { b.x = fmaxf(b.x, 0.f); b.y = fmaxf(b.y, 0.f); b.z = fmaxf(b.z, 0.f); b.w = fmaxf(b.w, 0.f); }
       v.x += b.x; v.y += b.y; v.z += b.z; v.w += b.w;
     }
@@ -132,43 +105,25 @@ __global__ __launch_bounds__(256) void bnx_apply_kernel(const float* __restrict_
 }
 
 // The input gradient of a training BN, stored: dy = fma(A, d, fma(B, y, K)) per channel
-// (bnfuse.hpp; bn.hip bn_bwd_apply's arithmetic) over the valid rows (measured faster than the
-// weight gradient staging dy from (d, y) on the fly: profiles/r4/bnx/ab_steps.md).  claim: the
-// BN's backward record is still pending — A / B / K derived in the prologue (bnfuse.hpp
-// bnf_consume_bwd), block 0 of each replica accumulating dgamma / dbeta and folding the dy bound.
+// (bnfuse.hpp; bn.hip bn_bwd_apply's arithmetic) over the valid rows, and the max |dy| slot
+// folded for its fp16-pair consumers (measured faster than the weight gradient staging dy
+// from (d, y) on the fly: profiles/r4/bnx/ab_steps.md).
 __global__ __launch_bounds__(256) void bnx_dy_kernel(const float* __restrict__ d, const float* __restrict__ y,
                                                      const float* __restrict__ coef, float* __restrict__ dy,
                                                      long long gstride, const int* __restrict__ nvalid, int N, int HW,
-                                                     int C, int* __restrict__ amax, int amax_ld, const BnFuse f,
-                                                     int claim) {
-  __shared__ __attribute__((aligned(16))) float kA[512], kB[512], kK[512];
+                                                     int C, int* __restrict__ amax, int amax_ld) {
   const int g = blockIdx.y;
   const int C4 = C >> 2;
-  const int Mv = valid_rows(nvalid, g, N) * HW;
-  if (Mv <= 0) return;
-  const long long total = (long long)Mv * C4;
+  const long long total = (long long)valid_rows(nvalid, g, N) * HW * C4;
   const long long base = (long long)g * gstride;
-  const bool inl = C <= 512;   // (wider BNs: the coefficient rows from global memory, never claimed)
   const float* cf = coef + (long long)g * kBnRows * C;
-  if (claim) {
-    bnf_consume_bwd(f, f.which, g, Mv, kA, kB, kK, blockIdx.x == 0);
-  } else if (inl) {
-    for (int c = threadIdx.x; c < C; c += 256) {
-      kA[c] = cf[kCA * C + c];
-      kB[c] = cf[kCB * C + c];
-      kK[c] = cf[kCK * C + c];
-    }
-    __syncthreads();
-  }
-  const float* pA = inl ? kA : cf + kCA * C;
-  const float* pB = inl ? kB : cf + kCB * C;
-  const float* pK = inl ? kK : cf + kCK * C;
   float vmax = 0.f;
   for (long long t = blockIdx.x * 256LL + threadIdx.x; t < total; t += (long long)gridDim.x * 256) {
     const int c = (int)(t % C4) * 4;
     const long long o = base + t * 4;
     const float4 dv = *(const float4*)(d + o), yv = *(const float4*)(y + o);
-    const float4 A = *(const float4*)&pA[c], B = *(const float4*)&pB[c], K = *(const float4*)&pK[c];
+    const float4 A = *(const float4*)(cf + kCA * C + c), B = *(const float4*)(cf + kCB * C + c),
+                 K = *(const float4*)(cf + kCK * C + c);
     const float4 v = make_float4(fmaf(A.x, dv.x, fmaf(B.x, yv.x, K.x)), fmaf(A.y, dv.y, fmaf(B.y, yv.y, K.y)),
                                  fmaf(A.z, dv.z, fmaf(B.z, yv.z, K.z)), fmaf(A.w, dv.w, fmaf(B.w, yv.w, K.w)));
     vmax = fmaxf(vmax, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
@@ -187,7 +142,8 @@ int bnx_tile_go(const BnFuse& f, const float* src, float* dst, long long gstride
   const dim3 grid((unsigned)(ceil_div((long long)N * HW, 128) * ceil_div(f.C, 64)), G);
   hipLaunchKernelGGL(bnx_tile_kernel, grid, dim3(256), 0, st, f, src, dst, gstride, nvalid, N, HW, pool, pool_scale, ws,
                      S, zstride, accum);
-  return (int)hipGetLastError();
+  const int rc = (int)hipGetLastError();
+  return rc != 0 ? rc : bnx_finalize_go(f, nvalid, G, N, HW, st);   // the pass's BN finalize
 }
 }  // namespace xg
 using xg::bnx_tile_go;
@@ -204,43 +160,26 @@ DBA_EXPORT int dba_bnx_rows(const void* bnf, const float* src, float* dst, long 
 
 DBA_EXPORT int dba_bnfuse_size() { return (int)sizeof(BnFuse); }
 
-// the standalone finalisation of a fused BN's accumulator record (bnfuse.hpp), for consumers that
-// do not derive the coefficients themselves; bnf: a BnFuse in host memory (passed by value)
-
-DBA_EXPORT int dba_bnx_finalize(const void* bnf, const int* nvalid, int G, int N, int HW, void* stream) {
-  const BnFuse f = *(const BnFuse*)bnf;
-  if (f.mode < 1 || f.mode > 2 || !f.acc || f.nsub < 1) return -108;
-  return bnx_finalize_go(f, nvalid, G, N, HW, (hipStream_t)stream);
-}
-
 DBA_EXPORT int dba_bnx_apply(const float* ya, const float* ca, const float* res, const float* yb, const float* cb,
                              int relu_b, int relu, float* out, long long gstride, const int* nvalid, int G, int N, int HW, int C,
-                             int* amax, int amax_ld, const void* fa, const void* fb, void* stream) {
+                             int* amax, int amax_ld, void* stream) {
   if (C & 3) return -102;
-  if (C > 512 && (fa || fb)) return -108;
-  const BnFuse za{}, ba = fa ? *(const BnFuse*)fa : za, bb = fb ? *(const BnFuse*)fb : za;
-  if ((fa && (ba.mode != 1 || ba.C != C)) || (fb && (bb.mode != 1 || bb.C != C || !yb))) return -108;
   const long long per = (long long)N * HW * (C / 4);
   const long long cap = std::max(1LL, 8192LL / std::max(1, G));
   const dim3 grid((unsigned)std::max(1LL, std::min(cap, (per + 255) / 256)), G);
   hipLaunchKernelGGL(bnx_apply_kernel, grid, dim3(256), 0, (hipStream_t)stream, ya, ca, res, yb, cb, relu_b, relu, out,
-                     gstride, nvalid, N, HW, C, amax, amax_ld, ba, fa ? 1 : 0, bb, fb ? 1 : 0);
+                     gstride,
+                     nvalid, N, HW, C, amax, amax_ld);
   DBA_LAUNCH_CHECK();
 }
 
-// f (optional): the BN's pending backward record (bnfuse.hpp), derived in the launch
-
 DBA_EXPORT int dba_bnx_dy(const float* d, const float* y, const float* coef, float* dy, long long gstride,
-                          const int* nvalid, int G, int N, int HW, int C, int* amax, int amax_ld, const void* f,
-                          void* stream) {
+                          const int* nvalid, int G, int N, int HW, int C, int* amax, int amax_ld, void* stream) {
   if (C & 3) return -102;
-  if (C > 512 && f) return -108;
-  const BnFuse z{}, bf = f ? *(const BnFuse*)f : z;
-  if (f && (bf.mode != 2 || bf.C != C)) return -108;
   const long long per = (long long)N * HW * (C / 4);
   const long long cap = std::max(1LL, 8192LL / std::max(1, G));
   const dim3 grid((unsigned)std::max(1LL, std::min(cap, (per + 255) / 256)), G);
   hipLaunchKernelGGL(bnx_dy_kernel, grid, dim3(256), 0, (hipStream_t)stream, d, y, coef, dy, gstride, nvalid, N, HW, C,
-                     amax, amax_ld, bf, f ? 1 : 0);
+                     amax, amax_ld);
   DBA_LAUNCH_CHECK();
 }

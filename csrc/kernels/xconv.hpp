@@ -97,10 +97,6 @@ struct XArgs {
   BnFuse bf;
   const float* lz_coef;
   int lz_relu;
-  // lz_claim: the source BN's record is still pending (bnfuse.hpp) — every block derives its
-  // coefficients and bound in the prologue from lzf, block (0, g, 0) writes them for later kernels
-  BnFuse lzf;
-  int lz_claim;
   // fused downsampling shortcut (evaluation, xhalo_kernel SC): out += the 1x1
   // stride-2 conv of x2 [G][N][sc_H][sc_W][sc_C] with pre-split weights (sc_wp: per slot 2 planes
   // of Ncol x sc_C fp16) + its bias, as extra k-steps of the same accumulators
@@ -233,17 +229,11 @@ __global__ __launch_bounds__(256, KS ? 2 : XCONV_MINB) void xconv_kernel(const X
   if (m0 >= Mv) return;
   const int slot = a.wsel ? a.wsel[g] : g;
   const int Cs = a.Cs;
-  [[maybe_unused]] int lz_bound = 0;
   if constexpr (LZ) {   // the source BN's scale / shift (Cs <= 512: checked on the host)
-    if (a.lz_claim) {   // from its pending record (block-uniform)
-      const int Ms = valid_rows(a.nvalid, g, a.N) * a.Hs * a.Ws;
-      lz_bound = __float_as_int(bnf_consume_fwd(a.lzf, g, Ms, lzc, lzc + 512, blockIdx.x == 0 && blockIdx.z == 0));
-    } else {
-      const float* cf = a.lz_coef + (long long)g * kBnRows * Cs;
-      for (int c = threadIdx.x; c < Cs; c += 256) {
-        lzc[c] = cf[kCScale * Cs + c];
-        lzc[512 + c] = cf[kCShift * Cs + c];
-      }
+    const float* cf = a.lz_coef + (long long)g * kBnRows * Cs;
+    for (int c = threadIdx.x; c < Cs; c += 256) {
+      lzc[c] = cf[kCScale * Cs + c];
+      lzc[512 + c] = cf[kCShift * Cs + c];
     }
   }
   const int K = c.nI * c.nJ * Cs;
@@ -390,7 +380,7 @@ __global__ __launch_bounds__(256, KS ? 2 : XCONV_MINB) void xconv_kernel(const X
   };
   // quarter q of stage st -> LDS buffer buf
   HScale hs;
-  hs.init((LZ && a.lz_claim) ? lz_bound : amax_read(a.amax_src, a.amax_src_ld, g), amax_read(a.amax_w, a.amax_w_ld, slot));
+  hs.init(amax_read(a.amax_src, a.amax_src_ld, g), amax_read(a.amax_w, a.amax_w_ld, slot));
   auto lput_q = [&](int buf, int st, int q) __attribute__((always_inline)) {
     uint4* L = lds + buf * P * PL;
     uint2 sp[P];

@@ -112,18 +112,16 @@ DBA_EXPORT int dba_xconv_dgrad(const float* dy, long long dy_gstride, const floa
   a.amax_src = amax_dy; a.amax_w = amax_w;
   a.amax_src_ld = amax_dy_ld; a.amax_w_ld = amax_w_ld;
   a.wp = wp; a.wp_sstride = wp_sstride;
-  if (bnf) {   // the backward BN mask + reduce of the gradient in the epilogue (every class of a
-              // stride-s gradient reduces its own rows: the integer records do not care which rows a
-              // tile holds, bnfuse.hpp)
+  if (bnf) {   // the backward BN mask + reduce of the gradient (stride-1 data gradients: one class)
     a.bf = *(const BnFuse*)bnf;
-    if (a.bf.mode != 2 || (Cin & 3) || a.bf.C != Cin) return -108;
+    if (a.bf.mode != 2 || stride != 1 || (Cin & 3) || a.bf.C != Cin) return -108;
   }
   long long Mmax = 0;
   for (int i = 0; i < cg.n; ++i) {
     a.cls[i] = cg.c[i];
     Mmax = std::max(Mmax, (long long)N * cg.c[i].Hq * cg.c[i].Wq);
   }
-  auto fin = [&](int rc) { return rc; };   // (the record's consumer finalises it: bnfuse.hpp)
+  auto fin = [&](int rc) { return (rc == 0 && a.bf.mode) ? bnx_finalize_go(a.bf, nvalid, G, N, H * W, st) : rc; };
   if (stride == 1) {
     const int rc = xhalo_try(a, G, KH, KW, st);
     if (rc != -100) return fin(rc);

@@ -319,7 +319,7 @@ DBA_EXPORT int dba_xconv_fwd(const float* x, long long x_gstride, const float* w
                              int Wo, int Cout, int KH, int KW, int stride, int pad, int relu, const int* amax_x,
                              int amax_x_ld, const int* amax_w, int amax_w_ld, int* amax_out, int amax_out_ld,
                              const uint16_t* wp, long long wp_sstride, float* ws, long long ws_floats, int* sk_cnt,
-                             long long sk_cnt_n, const void* bnf, const float* lz_coef, int lz_relu, const void* lzf,
+                             long long sk_cnt_n, const void* bnf, const float* lz_coef, int lz_relu,
                              void* stream) {
   hipStream_t st = (hipStream_t)stream;
   if ((long long)N * H * W * Cin >= (1LL << 29)) return -103;   // 32-bit in-replica byte offsets
@@ -343,14 +343,9 @@ DBA_EXPORT int dba_xconv_fwd(const float* x, long long x_gstride, const float* w
   if (lz_coef) {
     if (wp || vec < 4 || Cin > 512) return -108;
     a.lz_coef = lz_coef; a.lz_relu = lz_relu;
-    if (lzf) {   // the source BN's record is pending: this launch finalises it (bnfuse.hpp)
-      a.lzf = *(const BnFuse*)lzf;
-      a.lz_claim = 1;
-      if (a.lzf.mode != 1 || a.lzf.C != Cin || !a.lzf.acc) return -108;
-    }
   }
-  // (a fused BN's record is finalised by its first consumer, or dba_bnx_finalize: bnfuse.hpp)
-  auto fin = [&](int rc) { return rc; };
+  // a fused BN's finalize launch follows its producer (bnx_tile_go launches its own)
+  auto fin = [&](int rc) { return (rc == 0 && a.bf.mode) ? bnx_finalize_go(a.bf, nvalid, G, N, Ho * Wo, st) : rc; };
   if (stride == 1) {
     int rc = ximg_try(a, G, KH, KW, st);
     if (rc == -100) rc = xhalo_try(a, G, KH, KW, st);

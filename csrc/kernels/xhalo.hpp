@@ -98,24 +98,16 @@ __global__ __launch_bounds__(256) void xhalo_kernel(const XArgs a) {
       sv[u] = bload4(rS, ok ? (((img * a.sc_H + h) * a.sc_W + w) * 32 + q * 4) * 4 : kOOB);
     }
   }
-  // LZ: the source BN's scale / shift in LDS — from its coefficient rows, or derived from its
-  // pending record (lz_claim: bnfuse.hpp bnf_consume_fwd, block 0 of each replica the writer)
-  int src_bits;
+  // LZ: the source BN's scale / shift in LDS (from its coefficient rows)
   if constexpr (LZ) {
-    if (a.lz_claim) {
-      src_bits = __float_as_int(bnf_consume_fwd(a.lzf, g, nv_img * a.Hs * a.Ws, lzs, lzs + CS, blockIdx.x == 0));
-    } else {
-      const float* cf = a.lz_coef + (long long)g * kBnRows * CS;
-      for (int c = tid; c < CS; c += 256) {
-        lzs[c] = cf[kCScale * CS + c];
-        lzs[CS + c] = cf[kCShift * CS + c];
-      }
-      __syncthreads();
-      src_bits = amax_read(a.amax_src, a.amax_src_ld, g);
+    const float* cf = a.lz_coef + (long long)g * kBnRows * CS;
+    for (int c = tid; c < CS; c += 256) {
+      lzs[c] = cf[kCScale * CS + c];
+      lzs[CS + c] = cf[kCShift * CS + c];
     }
-  } else {
-    src_bits = amax_read(a.amax_src, a.amax_src_ld, g);
+    __syncthreads();
   }
+  const int src_bits = amax_read(a.amax_src, a.amax_src_ld, g);
   HScale hs;
   hs.init(src_bits, amax_read(a.amax_w, a.amax_w_ld, slot));
   [[maybe_unused]] int s_sc = 0;

@@ -106,10 +106,6 @@ class GroupTrainer:
         self.dtype = compute_dtype
         self.max_groups = max_groups
         self._bufs: Dict[Tuple[int, int], _GroupBuffers] = {}
-        # int64 per replica of the step arena for the training BNs' accumulator records
-        # (csrc/kernels/bnfuse.hpp): a ResNet step needs ~80k; models without BN none
-        has_bn = any(n.endswith("running_mean") for n in self.spec.by_name)
-        self._acc_words = ops.hip_module().ACC_PER_REPLICA if (has_bn and ops.backend_name(self.device) == "hip") else 0
         self.use_graph = (self.device.type == "cuda" and bool(params["graph_capture"])
                           and ops.backend_name(self.device) == "hip")
         self.fg = params["aggregation_methods"] == C.AGGR_FOOLSGOLD
@@ -141,8 +137,7 @@ class GroupTrainer:
     def _step(self, b: _GroupBuffers) -> None:
         # one zeroed arena for the step's operand-max slots and split-K counters (re-zeroed by
         # the captured fill at every graph replay)
-        G = b.state.shape[0]
-        with ops.amax_arena(G, self.device, counters=SK_COUNTERS, acc=self._acc_words * G):
+        with ops.amax_arena(b.state.shape[0], self.device, counters=SK_COUNTERS):
             self._step_ops(b)
 
     def _step_ops(self, b: _GroupBuffers) -> None:
@@ -157,8 +152,9 @@ class GroupTrainer:
         ctx = prog.Ctx(self.spec, b.state, b.state, None, train=True, grads=b.grads,
                        nvalid=b.nvalid, dropout_seed=b.seed, act_dtype=self.dtype)
         fused = self.alpha == 1.0     # stats straight from the loss kernel (no extra launches)
-        # the fused classifier head (pool + linear + loss + the head's backward in one launch,
-        # models/program.py Ctx.fused_head) writes its gradients during the forward
+        # the opt-in fused classifier head (pool + linear + loss + the head's backward in two
+        # launches, models/program.py Ctx.fused_head, DBA_FUSED_HEAD=1) writes its gradients
+        # during the forward
         ctx.head = {"labels": y, "stats": b.stats if fused else None, "slot": b.slot}
         b.grads.zero_()
         out = prog.forward(ctx, x)

@@ -166,11 +166,8 @@ class Ctx:
         return len(self._dgrad_items) - 1
 
     def _end_backward(self) -> None:
-        be = ops.backend_for(self.state)
         if self._wdefer:
-            be.wgrad_flush(self._wdefer)
-        if hasattr(be, "bn_flush"):   # HIP: BN records no kernel consumed (bnfuse.hpp)
-            be.bn_flush()
+            ops.backend_for(self.state).wgrad_flush(self._wdefer)
 
     def _prepare_dgrad(self) -> None:
         if self._dgrad_items:
@@ -392,7 +389,7 @@ class Ctx:
 
     def fused_head(self, x: Tensor, wname: str, bname: str) -> Tensor:
         """Training: global average pool + linear + softmax cross-entropy + the head's backward
-        in one launch (ops.hip.head_train; reference models/resnet_cifar.py:97-100,
+        in two launches (ops.hip.head_train, opt-in DBA_FUSED_HEAD=1; reference models/resnet_cifar.py:97-100,
         image_train.py:85-92).  Returns the per-replica loss (the tape's output: its backward
         ignores the seed gradient and finishes the pooled features' gradient)."""
         be = ops.backend_for(x)
@@ -466,7 +463,7 @@ def _resnet_cifar(ctx: Ctx, x: Tensor) -> Tensor:
                 sc = out
             out = _block_out(ctx, a, pre + f"conv{last}.weight", pre + f"bn{last}", p, sc)
             cin = w * exp
-    if ctx.head_ok(out, "linear.weight"):   # training: pool + linear + loss + backward, one launch
+    if ctx.head_ok(out, "linear.weight"):   # training, opt-in: pool + linear + loss + backward fused
         return ctx.fused_head(out, "linear.weight", "linear.bias")
     out = ctx.gap(out)
     G, N = out.shape[:2]

@@ -60,13 +60,12 @@ for _n in _OPS:
     globals()[_n] = _dispatch(_n)
 
 
-def amax_arena(G: int, device: torch.device, counters: int = 0, acc: int = 0):
+def amax_arena(G: int, device: torch.device, counters: int = 0):
     """Context: one zeroed allocation for the fp16-pair operand-max slots of the enclosed
     launches (``ops.hip.amax_arena``), plus ``counters`` arrival counters for their in-launch
-    split-K combines and ``acc`` int64 for the training BNs' accumulator records; a no-op off
-    the HIP backend."""
+    split-K combines; a no-op off the HIP backend."""
     if backend_name(device) == "hip":
-        return hip_module().amax_arena(G, device, counters=counters, acc=acc)
+        return hip_module().amax_arena(G, device, counters=counters)
     return contextlib.nullcontext()
 
 

@@ -41,43 +41,15 @@ class BnParams:
 class BnStat:
     """A training BN's per-step state: ``coef [G, ROWS, C]`` (forward: mean, 1/std, scale,
     shift, max / min of y; backward: A, B, K) and, on the HIP backend, the operand-max slots of
-    its lazy output (``bound``) and of its input gradient (``dbound``).
-
-    On the HIP backend the producing kernels leave the statistics in an integer accumulator
-    record (``csrc/kernels/bnfuse.hpp``) and the coefficient rows are written by the record's
-    first consumer.  ``pending`` holds the record(s) not yet finalised: a record-aware consumer
-    :meth:`claim` s one (its kernel derives the coefficients and writes them); reading ``coef``
-    finalises whatever is still pending with the standalone finalize launch, so every other
-    reader sees final rows."""
+    its lazy output (``bound``) and of its input gradient (``dbound``)."""
 
     def __init__(self, coef: Tensor, params: BnParams, bound: Any = None) -> None:
-        self._coef, self.params, self.bound = coef, params, bound
+        self.coef, self.params, self.bound = coef, params, bound
         self.dbound: Any = None
-        self.pending: List[Any] = []
-
-    @property
-    def coef(self) -> Tensor:
-        while self.pending:
-            self.pending[0]()          # launches the finalize and removes itself
-        return self._coef
-
-    @property
-    def coef_raw(self) -> Tensor:
-        """The coefficient rows' storage (pointer for a kernel that writes or finalises them)."""
-        return self._coef
-
-    def claim(self, kind: str) -> Any:
-        """Take the pending record of ``kind`` ("fwd" / "bwd") for a record-aware consumer (None:
-        nothing pending — the rows are final)."""
-        for p in self.pending:
-            if p.kind == kind:
-                p.detach()
-                return p
-        return None
 
     @property
     def C(self) -> int:
-        return self._coef.shape[-1]
+        return self.coef.shape[-1]
 
 
 class LazyBN:

@@ -65,7 +65,7 @@ _SIGS = {
     "dba_xwgrad_halo_set": [_I],
     "dba_xconv_ws_floats": [_I] * 8,
     "dba_xconv_fwd": [_P, _LL, _P, _LL, _P, _P, _LL, _P, _P, _LL, _P] + [_I] * 13 + [_P, _I] * 3 + [_P, _LL] * 2
-    + [_P, _LL, _P, _P, _I, _P, _P],
+    + [_P, _LL, _P, _P, _I, _P],
     "dba_xconv_sk_ints": [_I] * 8,
     "dba_xconv_dgrad": [_P, _LL, _P, _LL, _P, _P, _P, _LL, _P] + [_I] * 12 + [_P, _I] * 2 + [_P, _LL] * 3 + [_P, _P],
     "dba_xsplit_w": [_P, _LL, _LL, _I, _P, _I, _P, _P],
@@ -79,11 +79,10 @@ _SIGS = {
     "dba_xwgrad": [_P, _LL, _P, _LL, _P, _LL, _P] + [_I] * 12 + [_P, _I] * 2 + [_P, _LL, _I] + [_P, _I, _P],
     # fused training BN (csrc/kernels/bnfuse.hpp)
     "dba_bnx_rows": [_P, _P, _P, _LL, _P, _I, _I, _I, _P, _F, _P],
-    "dba_bnx_apply": [_P, _P, _P, _P, _P, _I, _I, _P, _LL, _P, _I, _I, _I, _I, _P, _I, _P, _P, _P],
+    "dba_bnx_apply": [_P, _P, _P, _P, _P, _I, _I, _P, _LL, _P, _I, _I, _I, _I, _P, _I, _P],
     "dba_bnfuse_size": [],
-    "dba_bnx_finalize": [_P, _P, _I, _I, _I, _P],
     "dba_xwgrad_stem": [_P, _LL, _P, _P, _P, _LL, _P, _P, _I, _I, _I, _I, _P],
-    "dba_bnx_dy": [_P, _P, _P, _P, _LL, _P, _I, _I, _I, _I, _P, _I, _P, _P],
+    "dba_bnx_dy": [_P, _P, _P, _P, _LL, _P, _I, _I, _I, _I, _P, _I, _P],
     "dba_xwgrad_reduce_batch": [_P, _I, _I, _LL, _P],
     # fused evaluation BasicBlock, with or without the image stem (csrc/kernels/xblock.hip)
     "dba_xblock_fwd": [_P, _LL, _P, _LL, _P, _P, _P, _LL, _P, _P, _LL, _P] + [_I] * 6
@@ -112,15 +111,15 @@ _L.dba_head_part_doubles.restype = ctypes.c_longlong
 class _BnFuse(ctypes.Structure):
     """Mirror of csrc/kernels/bnfuse.hpp ``BnFuse`` (passed by host pointer, copied by value
     into the kernel arguments at launch: graph-capture safe)."""
-    _fields_ = [("mode", _I), ("C", _I), ("nsub", _I),
-                ("acc", _P),
+    _fields_ = [("mode", _I), ("C", _I), ("ngrp", _I),
+                ("rec0", _P),
                 ("coef_a", _P), ("gamma_a", _P), ("beta_a", _P), ("rm_a", _P), ("rv_a", _P),
                 ("p_gstride", _LL), ("momentum", _F), ("eps", _F), ("relu", _I),
                 ("amax_a", _P), ("amax_ld", _I),
                 ("ya", _P), ("yb", _P), ("y_gstride", _LL),
                 ("coef_b", _P), ("gamma_b", _P), ("amax_b", _P),
                 ("dgamma_a", _P), ("dbeta_a", _P), ("dgamma_b", _P), ("dbeta_b", _P), ("gr_gstride", _LL),
-                ("mask_out", _P), ("mask_lazy", _I), ("which", _I)]
+                ("mask_out", _P), ("mask_lazy", _I)]
 
 
 assert ctypes.sizeof(_BnFuse) == int(_L.dba_bnfuse_size()), "BnFuse layout mismatch (rebuild the kernels)"
@@ -307,23 +306,14 @@ class _AmaxArena:
     (captured into the training step's graph: re-zeroed at every replay) instead of one per
     producer."""
 
-    def __init__(self, G: int, device, n: int, counters: int = 0, acc: int = 0) -> None:
+    def __init__(self, G: int, device, n: int, counters: int = 0) -> None:
         self.G, self.ld, self.next = G, _amax_ld(G), 0
         slots = n * AMAX_SUB * self.ld
-        counters += counters & 1          # (the int64 region starts 8-B aligned)
-        flat = torch.zeros(slots + counters + 2 * acc, dtype=torch.int32, device=device)
+        flat = torch.zeros(slots + counters, dtype=torch.int32, device=device)
         self.buf = flat[:slots].view(n, AMAX_SUB, self.ld)
         # arrival counters of the in-launch split-K combines (xconv.hpp sk_combine), zeroed by
         # the same fill
-        self.cnt, self.cnt_next = flat[slots:slots + counters], 0
-        # the fused training BNs' integer accumulator records (bnfuse.hpp), zeroed by the same fill
-        self.acc, self.acc_next = flat[slots + counters:].view(torch.int64), 0
-
-    def acc_take(self, n: int, device):
-        if device != self.acc.device or self.acc_next + n > self.acc.numel():
-            return None
-        self.acc_next += n
-        return self.acc[self.acc_next - n:self.acc_next]
+        self.cnt, self.cnt_next = flat[slots:], 0
 
     def counters(self, n: int, device):
         if n <= 0 or device != self.cnt.device or self.cnt_next + n > self.cnt.numel():
@@ -342,11 +332,10 @@ _ARENA: list = []
 
 
 @contextlib.contextmanager
-def amax_arena(G: int, device, n: int = 256, counters: int = 0, acc: int = 0):
-    """Slots for the enclosed launches' fp16-pair operand maxima, ``counters`` zeroed ints
-    for their in-launch split-K combines (:func:`_sk_counters`) and ``acc`` zeroed int64 for the
-    fused training BNs' accumulator records (:func:`_acc_new`)."""
-    _ARENA.append(_AmaxArena(G, device, n, counters, acc))
+def amax_arena(G: int, device, n: int = 256, counters: int = 0):
+    """Slots for the enclosed launches' fp16-pair operand maxima, and ``counters`` zeroed ints
+    for their in-launch split-K combines (:func:`_sk_counters`)."""
+    _ARENA.append(_AmaxArena(G, device, n, counters))
     try:
         yield
     finally:
@@ -507,11 +496,10 @@ def _xconv_fwd(x, w, wsel, stride, pad, bias, residual, relu, nvalid, out_dtype,
     ax = lz[2] if lz is not None else _amax_act(x, nvalid)
     aw = _amax_w(w, ws, Cout * KH * KW * Cin)
     lz_coef, lz_relu = (lz[0].data_ptr(), int(lz[1])) if lz is not None else (None, 0)
-    lzf = ctypes.byref(lz[3].f) if (lz is not None and lz[3] is not None) else None
     _call("dba_xconv_fwd", x.data_ptr(), N * H * W * Cin, w.data_ptr(), ws, _ptr(_i32(wsel)), _ptr(bias), bs,
           _ptr(res), y.data_ptr(), N * Ho * Wo * Cout, _ptr(_i32(nvalid)), G, N, H, W, Cin, Ho, Wo, Cout, KH, KW,
           stride, pad, int(relu), *_aptr(ax), *_aptr(aw), *_aptr(ay), *_wplanes(w), _ptr(wsb), n,
-          _ptr(cnt), 0 if cnt is None else cnt.numel(), bnf_p, lz_coef, lz_relu, lzf, _stream())
+          _ptr(cnt), 0 if cnt is None else cnt.numel(), bnf_p, lz_coef, lz_relu, _stream())
     return y
 
 
@@ -707,7 +695,7 @@ def _xconv_dgrad(dy, w, wsel, stride, pad, in_hw, nvalid, out_dtype, accum, wt, 
     cnt = _sk_counters(int(_L.dba_xconv_sk_ints(G, N, H, W, Cout, Cin, KH, KW)) if n > 0 else 0, dy.device)
     a0 = getattr(w, "_dba_amax", None)   # the forward weights' max is the transpose's
     ad, aw = _amax_act(dy, nvalid), (a0 if a0 is not None else _amax(wt, per, per))
-    bnf = _bnf_bwd(finish, G, N * H * W, dx.device) if finish is not None else None
+    bnf = _bnf_bwd(finish, G, N * H * W, dx.device) if (finish is not None and stride == 1) else None
     _call("dba_xconv_dgrad", dy.data_ptr(), N * Ho * Wo * Cout, wt.data_ptr(), per, _ptr(_i32(wsel)), _ptr(acc),
           dx.data_ptr(), N * H * W * Cin, _ptr(_i32(nvalid)), G, N, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad,
           *_aptr(ad), *_aptr(aw), *_wplanes(wt), _ptr(wsb), n, _ptr(cnt), 0 if cnt is None else cnt.numel(),
@@ -715,7 +703,6 @@ def _xconv_dgrad(dy, w, wsel, stride, pad, in_hw, nvalid, out_dtype, accum, wt, 
     if finish is None:
         return dx
     if bnf is not None:
-        _pend_bwd(bnf, nvalid, G, N, H * W, finish.stats())
         return bs.Fin(dx, finish.stats())
     return bn_finish(dx, finish, nvalid)   # stride-s data gradient: the standalone pass
 
@@ -809,116 +796,13 @@ def _stem_wgrad(dy, x, dw, nvalid, defer):
 
 
 # ------------------------------------------------------------ fused training BN (bnfuse.hpp)
-ACC_F, ACC_B = 8, 10                   # bnfuse.hpp kAccF / kAccB: int64 per record copy
-ACC_PER_REPLICA = 1 << 17              # arena int64 per replica for a training step's records
-ACC_STATS = {"arena": 0, "fallback": 0}
-
-
-_ACC_ROWS = int(os.environ.get("DBA_ACC_ROWS", "4096"))
-_ACC_NSUB_MAX = int(os.environ.get("DBA_ACC_NSUB", "8"))
-
-
-def _acc_nsub(M: int) -> int:
-    """Spread copies of a BN accumulator record per channel: one per ``DBA_ACC_ROWS`` rows of a
-    replica, at most ``DBA_ACC_NSUB``, so each copy takes a bounded number of the producers' tile
-    atomics (device-scope atomics are performed past the per-XCD L2s: same-address ones
-    serialise)."""
-    return max(1, min(_ACC_NSUB_MAX, M // _ACC_ROWS))
-
-
-def _acc_new(n: int, device):
-    """``n`` zeroed int64 of a BN accumulator record: from the enclosing arena (one fill per
-    training step), else its own zeroed allocation."""
-    a = _ARENA[-1].acc_take(n, device) if _ARENA else None
-    if a is not None:
-        ACC_STATS["arena"] += 1
-        return a
-    ACC_STATS["fallback"] += 1
-    return torch.zeros(n, dtype=torch.int64, device=device)
-
-
-_LIVE_PENDING: list = []   # every record not yet finalised (bn_flush)
-_BN_CLAIM = os.environ.get("DBA_BN_CLAIM", "1") != "0"   # DBA_BN_CLAIM=0: standalone finalizes (A/B)
-
-
-def set_bn_claim(on: int) -> int:
-    """Record-aware consumers finalise pending BN records in their own launch (on, the default)
-    or every record gets the standalone finalize launch (off: the A/B and the bitwise test of the
-    two paths); -1 queries.  Returns the previous setting."""
-    global _BN_CLAIM
-    prev = int(_BN_CLAIM)
-    if on >= 0:
-        _BN_CLAIM = bool(on)
-    return prev
-
-
-def _claim(st, kind: str):
-    # (the consumers stage a record's coefficients in LDS: BNs of <= 512 channels)
-    return st.claim(kind) if (_BN_CLAIM and st.C <= 512) else None
-
-
-def bn_flush() -> None:
-    """Finalise every BN record still pending (the end of a training step's backward pass: a
-    record nobody consumed still owes its running-statistic / gradient updates)."""
-    while _LIVE_PENDING:
-        _LIVE_PENDING[0]()
-
-
-class _Pending:
-    """A fused BN's accumulator record whose coefficient rows are not written yet (bnfuse.hpp).
-    Calling it launches the standalone finalisation (``dba_bnx_finalize``); a record-aware
-    consumer :meth:`~dba_mod_amd.ops.bnstate.BnStat.claim` s it instead and derives the
-    coefficients in its own kernel."""
-
-    def __init__(self, kind: str, f, nvalid, G: int, N: int, HW: int, stats) -> None:
-        self.kind, self.f, self.nvalid, self.G, self.N, self.HW = kind, f, _i32(nvalid), G, N, HW
-        self.stats = list(stats)
-        for st in self.stats:
-            st.pending.append(self)
-        _LIVE_PENDING.append(self)
-
-    def detach(self) -> None:
-        for st in self.stats:
-            if self in st.pending:
-                st.pending.remove(self)
-        if self in _LIVE_PENDING:
-            _LIVE_PENDING.remove(self)
-
-    def __call__(self) -> None:
-        self.detach()
-        _call("dba_bnx_finalize", ctypes.byref(self.f), _ptr(self.nvalid), self.G, self.N, self.HW, _stream())
-
-
-def _bnf_copy(f):
-    g = _BnFuse()
-    ctypes.memmove(ctypes.byref(g), ctypes.byref(f), ctypes.sizeof(_BnFuse))
-    g._keep = f._keep
-    return g
-
-
-def _pend_bwd(f, nvalid, G: int, N: int, HW: int, stats) -> None:
-    """The pending backward record of a finished gradient, one per BN: BN a's part, and for a
-    residual sum of two BNs BN b's part (its pointers moved into the ``a`` fields, ``which`` 1),
-    so each BN's consumer finalises its own coefficients / gradient sums."""
-    fa = _bnf_copy(f)
-    fa.coef_b = fa.gamma_b = fa.amax_b = fa.dgamma_b = fa.dbeta_b = None
-    _Pending("bwd", fa, nvalid, G, N, HW, stats[:1])
-    if len(stats) > 1:
-        fb = _bnf_copy(f)
-        fb.coef_a, fb.gamma_a, fb.amax_a = f.coef_b, f.gamma_b, f.amax_b
-        fb.dgamma_a, fb.dbeta_a = f.dgamma_b, f.dbeta_b
-        fb.coef_b = fb.gamma_b = fb.amax_b = fb.dgamma_b = fb.dbeta_b = None
-        fb.which = 1
-        _Pending("bwd", fb, nvalid, G, N, HW, stats[1:2])
-
-
 def _bnf_common(mode: int, G: int, M: int, C: int, device):
-    """A fused BN pass (bnfuse.hpp) over M rows per replica: its zeroed accumulator record."""
-    nsub = _acc_nsub(M)
-    acc = _acc_new(G * C * nsub * (ACC_F if mode == 1 else ACC_B), device)
+    """A fused BN pass (bnfuse.hpp) over M rows per replica: its level-0 record workspace."""
+    ngrp = (M + 31) // 32
+    rec0 = torch.empty(G * C * ngrp * 4, dtype=torch.float64, device=device)
     f = _BnFuse()
-    f.mode, f.C, f.nsub, f.acc = mode, C, nsub, acc.data_ptr()
-    f._keep = (acc,)   # alive until the record is finalised
+    f.mode, f.C, f.ngrp, f.rec0 = mode, C, ngrp, rec0.data_ptr()
+    f._keep = (rec0,)   # alive until the launches have been enqueued
     return f
 
 
@@ -933,7 +817,6 @@ def _bnf_fwd(p: "bs.BnParams", relu: bool, G: int, M: int, C: int, device):
     f.rm_a, f.rv_a, f.p_gstride = p.rmean.data_ptr(), p.rvar.data_ptr(), ps
     f.momentum, f.eps, f.relu = float(p.momentum), float(p.eps), int(relu)
     f.amax_a, f.amax_ld = bound.data_ptr(), bound.shape[1]
-    f._keep = f._keep + (coef, bound, p.gamma, p.beta, p.rmean, p.rvar)   # until the record is finalised
     return f, st
 
 
@@ -967,9 +850,6 @@ def _bnf_bwd(fin: "bs.Finish", G: int, M: int, device):
         f.mask_out = mo.data_ptr()
         keep.append(mo)
     f.mask_lazy = int(bool(fin.lazy))
-    keep += [sa.coef_raw, sa.dbound, pa.gamma, pa.dgamma, pa.dbeta]
-    if sb is not None:
-        keep += [sb.coef_raw, sb.dbound, sb.params.gamma, sb.params.dgamma, sb.params.dbeta]
     f._keep = f._keep + tuple(keep)
     return f
 
@@ -982,11 +862,8 @@ def _bnx_dy(lg, nvalid):
     assert y.shape == d.shape
     dy = torch.empty_like(d)
     am = lg.stat.dbound
-    pend = _claim(lg.stat, "bwd")   # finalised by this pass (bnfuse.hpp bnf_consume_bwd)
-    coef = lg.stat.coef_raw if pend is not None else lg.stat.coef
-    _call("dba_bnx_dy", d.data_ptr(), y.data_ptr(), coef.data_ptr(), dy.data_ptr(), d.stride(0),
-          _ptr(_i32(nvalid)), G, N, H * W, C, *_aptr(None), ctypes.byref(pend.f) if pend is not None else None,
-          _stream())
+    _call("dba_bnx_dy", d.data_ptr(), y.data_ptr(), lg.stat.coef.data_ptr(), dy.data_ptr(), d.stride(0),
+          _ptr(_i32(nvalid)), G, N, H * W, C, *_aptr(None), _stream())
     dy._dba_amax = am
     return dy
 
@@ -999,9 +876,7 @@ def conv_bn_stats(x, w, wsel, stride, pad, nvalid, p, relu):
     if isinstance(x, bs.LazyBN):
         if x.stat.bound is None:
             raise RuntimeError("lazy BN operand without its bound slot")
-        # a pending record is finalised by this conv (bnfuse.hpp bnf_consume_fwd): no launch of its own
-        pend = _claim(x.stat, "fwd")
-        lz = (x.stat.coef_raw if pend is not None else x.stat.coef, x.relu, x.stat.bound, pend)
+        lz = (x.stat.coef, x.relu, x.stat.bound)
         x = x.y
     x = _act(x, _F32, "conv input")
     G, N, H, W, Cin = x.shape
@@ -1010,7 +885,6 @@ def conv_bn_stats(x, w, wsel, stride, pad, nvalid, p, relu):
     Wo = (W + 2 * pad - KW) // stride + 1
     f, st = _bnf_fwd(p, relu, G, N * Ho * Wo, Cout, x.device)
     y = _xconv_fwd(x, w, wsel, stride, pad, None, None, False, nvalid, None, bnf=f, lz=lz)
-    _Pending("fwd", f, nvalid, G, N, Ho * Wo, [st])
     return y, st
 
 
@@ -1023,21 +897,14 @@ def bn_apply(a, residual, relu, nvalid=None):
     am = _amax_out(out)
     res = yb = cb = None
     relu_b = 0
-    # pending BN records are finalised by this pass (bnfuse.hpp bnf_consume_fwd)
-    pa = _claim(a.stat, "fwd")
-    ca = a.stat.coef_raw if pa is not None else a.stat.coef
-    pb = None
     if isinstance(residual, bs.LazyBN):
-        pb = _claim(residual.stat, "fwd")
-        yb, relu_b = _act(residual.y, _F32, "BN input"), int(residual.relu)
-        cb = residual.stat.coef_raw if pb is not None else residual.stat.coef
+        yb, cb, relu_b = _act(residual.y, _F32, "BN input"), residual.stat.coef, int(residual.relu)
         assert yb.shape == y.shape
     elif residual is not None:
         res = _act(residual, _F32, "residual")
         assert res.shape == y.shape
-    _call("dba_bnx_apply", y.data_ptr(), ca.data_ptr(), _ptr(res), _ptr(yb), _ptr(cb), relu_b, int(relu),
-          out.data_ptr(), y.stride(0), _ptr(_i32(nvalid)), G, N, H * W, C, *_aptr(am),
-          ctypes.byref(pa.f) if pa is not None else None, ctypes.byref(pb.f) if pb is not None else None, _stream())
+    _call("dba_bnx_apply", y.data_ptr(), a.stat.coef.data_ptr(), _ptr(res), _ptr(yb), _ptr(cb), relu_b, int(relu),
+          out.data_ptr(), y.stride(0), _ptr(_i32(nvalid)), G, N, H * W, C, *_aptr(am), _stream())
     return out
 
 
@@ -1059,7 +926,6 @@ def bn_finish(g, fin, nvalid=None, pool=None, hw=None):
     inv_hw = float(torch.tensor(1.0, dtype=torch.float32) / torch.tensor(float(H * W), dtype=torch.float32))
     _call("dba_bnx_rows", ctypes.byref(f), _ptr(src), d.data_ptr(), ya.stride(0), _ptr(_i32(nvalid)), G, N, H * W,
           _ptr(pool), inv_hw, _stream())
-    _pend_bwd(f, nvalid, G, N, H * W, fin.stats())
     return bs.Fin(d, fin.stats())
 
 
@@ -1238,13 +1104,14 @@ def softmax_xent(logits, labels, mean, want_grad, stats=None, slot=None, nvalid=
     return (loss64 if loss64 is not None else loss), correct, dl
 
 
-_FUSED_HEAD = os.environ.get("DBA_FUSED_HEAD", "1") != "0"
+_FUSED_HEAD = os.environ.get("DBA_FUSED_HEAD", "0") == "1"
 
 
 def head_ok(x, w) -> bool:
     """The fused classifier head (loss.hip head_rows_kernel) takes this training head: fp32 last
     block output [G, N, H, W, C] (C <= 512, N <= 256, H * W <= 64) and a linear layer of <= 16 classes.
-    ``DBA_FUSED_HEAD=0``: off (the unfused ops; A/B)."""
+    Opt-in (``DBA_FUSED_HEAD=1``): its logits are fp32 FMA chains, not the fp16-pair MFMA of the
+    unfused 1x1 conv, so a step's bits differ from the default path's."""
     return (_FUSED_HEAD and x.dtype == _F32 and x.dim() == 5 and x.shape[-1] <= 512 and x.shape[-1] % 4 == 0 and x.shape[1] <= 256
             and x.shape[2] * x.shape[3] <= 64
             and w.dim() == 3 and w.shape[1] <= 16 and w.shape[2] == x.shape[-1] and w.dtype == _F32

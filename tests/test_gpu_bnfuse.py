@@ -258,72 +258,9 @@ def test_pooled_gradient_finish(H, R64):
     out = torch.relu(torch.randn(G, N, 4, 4, C, generator=gen)).to(dev)
     pool = torch.randn(G, N, 1, 1, C, generator=gen).to(dev)
     r = H.bn_finish(None, bs.Finish(ya=ya, sa=sa, mask_out=out), nvalid, pool=pool, hw=(4, 4))
-    H.bn_flush()   # the pass leaves the BN's record pending for its consumer (bnfuse.hpp): finalise it
     rr = R64.bn_finish(None, bs.Finish(ya=ya.double().cpu(), sa=bs.BnStat(cf.double(), pa_r),
                                        mask_out=out.double().cpu()), nvalid.cpu(), pool=pool.double().cpu(), hw=(4, 4))
     for g in range(G):
         n = int(nvalid[g])
         assert _rel(r.d[g, :n], rr.d[g, :n]) < 1e-6
         assert _rel(grads[g, :2 * C], grads_r[g, :2 * C]) < 1e-5
-
-
-@pytest.mark.parametrize("arch,shp,G", [("resnet18_cifar", (32, 32, 3), 1), ("resnet18_cifar", (32, 32, 3), 3),
-                                        ("resnet18_tiny", (64, 64, 3), 2)])
-def test_consumer_finalize_bitwise_equals_standalone(H, arch, shp, G):
-    """The BN records finalised by their consumers (the lazy-operand conv, the apply pass, the
-    dy pass: bnfuse.hpp bnf_consume_fwd / bnf_consume_bwd) give the SAME bits as the standalone
-    finalize launch — loss, every gradient, the running statistics — in a whole training step;
-    and the step has ~one launch per BN fewer."""
-    from dba_mod_amd import ops
-    from dba_mod_amd.models import program as P
-    from dba_mod_amd.models.spec import get_spec
-    spec = get_spec(arch)
-    dev = torch.device("cuda")
-    N = 16
-    torch.manual_seed(0)
-    flat = spec.init_flat(3)
-    nval = torch.tensor([N, 9, 5][:G], dtype=torch.int32, device=dev)
-    x = torch.rand(G, N, *shp, device=dev)
-    lab = torch.randint(0, spec.num_classes, (G, N), device=dev).int()
-    # rows past a replica's valid count are padding (label -1), as the trainer's gather makes them
-    lab = torch.where(torch.arange(N, device=dev)[None] < nval[:, None].long(), lab, torch.full_like(lab, -1))
-
-    def run():
-        state = flat.to(dev)[None].repeat(G, 1).contiguous()
-        grads = torch.zeros(G, spec.P, device=dev)
-        H.bn_flush()   # (records earlier tests left unconsumed)
-        with H.amax_arena(G, dev, acc=H.ACC_PER_REPLICA * G):
-            ctx = P.Ctx(spec, state, state, None, train=True, grads=grads, nvalid=nval, act_dtype=torch.float32)
-            logits = P.forward(ctx, x)
-            loss, _, dl = ops.softmax_xent(logits, lab, True, True, grad_dtype=torch.float32)
-            ctx.tape.backward(logits, dl)
-        assert not H._LIVE_PENDING   # every record consumed or flushed by the backward pass
-        torch.cuda.synchronize()
-        return loss, grads, state
-
-    def where(a, b):
-        bad = (a != b).nonzero()
-        if not len(bad):
-            return "equal"
-        r, i = int(bad[0, 0]), int(bad[0, 1])
-        name = next((e.name for e in spec.params + spec.buffers if e.offset <= i < e.offset + e.numel), "?")
-        return f"{len(bad)} differ, first replica {r} index {i} ({name}): {a[r, i].item()} vs {b[r, i].item()}"
-
-    prev = H.set_bn_claim(0)
-    try:
-        l0, g0, s0 = run()
-        l0b, g0b, s0b = run()
-    finally:
-        H.set_bn_claim(prev)
-    H.set_bn_claim(1)
-    l1, g1, s1 = run()
-    l2, g2, s2 = run()
-    H.set_bn_claim(prev)
-    assert torch.equal(l0, l0b) and torch.equal(g0, g0b) and torch.equal(s0, s0b), \
-        ("standalone path not reproducible", where(g0, g0b), where(s0, s0b))
-    assert torch.equal(l1, l2) and torch.equal(g1, g2) and torch.equal(s1, s2), \
-        ("claim path not reproducible", where(g1, g2), where(s1, s2))
-    assert torch.equal(l0, l1), (l0, l1)
-    assert torch.equal(g0, g1), where(g0, g1)
-    assert torch.equal(s0, s1), where(s0, s1)
-    assert torch.isfinite(g1).all() and g1.abs().max() > 0

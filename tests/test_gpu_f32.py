@@ -411,9 +411,9 @@ def test_eval_forward_vs_fp64(H, R64, arch, shp):
         assert _rel(lf[g, :n], lr[g, :n]) < 2e-6, (arch, g, _rel(lf[g, :n], lr[g, :n]))
 
 
-def test_fused_head_matches_unfused_step(H):
-    """The fused classifier head (loss.hip head_kernel: pool + linear + cross-entropy + the head's
-    backward in one launch) against the unfused ops (avgpool, the 1x1 linear conv on the fp16
+def test_fused_head_matches_unfused_step(H, monkeypatch):
+    """The opt-in fused classifier head (loss.hip head_rows_kernel / head_fin_kernel: pool +
+    linear + cross-entropy + the head's backward in two launches) against the unfused ops (avgpool, the 1x1 linear conv on the fp16
     pair, softmax_xent, its weight / bias / data gradients): loss, correct counts and every
     gradient of a ResNet-18 CIFAR step at fp32 level; a replica's bits independent of the group
     (G = 1 vs 3) and run to run."""
@@ -422,6 +422,7 @@ def test_fused_head_matches_unfused_step(H):
     from dba_mod_amd.models.spec import get_spec
     spec = get_spec("resnet18_cifar")
     dev = torch.device("cuda")
+    monkeypatch.setattr(H, "_FUSED_HEAD", True)
     G, N = 3, 16
     torch.manual_seed(0)
     flat = spec.init_flat(3)
@@ -436,7 +437,7 @@ def test_fused_head_matches_unfused_step(H):
         Gx = xs.shape[0]
         state = flat.to(dev)[None].repeat(Gx, 1).contiguous()
         grads = torch.zeros(Gx, spec.P, device=dev)
-        with H.amax_arena(Gx, dev, acc=H.ACC_PER_REPLICA * Gx):
+        with H.amax_arena(Gx, dev):
             ctx = P.Ctx(spec, state, state, None, train=True, grads=grads, nvalid=nv, act_dtype=torch.float32)
             if fused:
                 ctx.head = {"labels": ls}
