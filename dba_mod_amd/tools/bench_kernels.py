@@ -39,6 +39,8 @@ SHAPES = [
     ("train.l3.0.sc", 10, 64, 16, 64, 128, 1, 2, 0),
     ("train.l4.0.conv1", 10, 64, 8, 128, 256, 3, 2, 1),
     ("train.l4.0.sc", 10, 64, 8, 128, 256, 1, 2, 0),
+    ("tiny.stem", 1, 64, 64, 3, 64, 7, 2, 3),       # Tiny-ImageNet 7x7/2 stem, a lone client
+    ("tiny.stem10", 10, 64, 64, 3, 64, 7, 2, 3),    # ... 10 clients
 ]
 
 
@@ -109,6 +111,9 @@ def _bench_fp32(name, G, N, Hh, Cin, Cout, k, s, p, reps, dev):
         dw = torch.zeros(G, Cout, k, k, Cin, device=dev)
         ops += [("dgrad", lambda: H.conv2d_dgrad(dy, w, None, s, p, (Hh, Hh), wt=wt)),
                 ("wgrad", lambda: H.conv2d_wgrad(dy, x, s, p, k, k, dw))]
+    if name.startswith("tiny.stem"):   # the stem's weight gradient (the stem has no data gradient)
+        dw = torch.zeros(G, Cout, k, k, Cin, device=dev)
+        ops.append(("wgrad", lambda: H.conv2d_wgrad(dy, x, s, p, k, k, dw)))
     for tag, fn in ops:
         t = _time(fn, reps)
         rec[tag + "_us"] = round(t * 1e6, 1)

@@ -62,6 +62,7 @@ FWD = [
     (1, 64, 8, 8, 128, 128, 3, 1, 1),    # lone client stage 3: split-K, in-launch combine
     (3, 64, 4, 4, 256, 256, 3, 1, 1),    # grouped stage 4: split-K, separate reduce + standalone pass
     (3, 5, 32, 32, 3, 32, 3, 1, 1),      # CIFAR stem
+    (2, 3, 64, 64, 3, 64, 7, 2, 3),      # Tiny stem
 ]
 
 
@@ -264,3 +265,4 @@ def test_pooled_gradient_finish(H, R64):
         n = int(nvalid[g])
         assert _rel(r.d[g, :n], rr.d[g, :n]) < 1e-6
         assert _rel(grads[g, :2 * C], grads_r[g, :2 * C]) < 1e-5
+
