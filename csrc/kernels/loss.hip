@@ -160,16 +160,20 @@ __global__ __launch_bounds__(kXentThreads) void xent_finish_kernel(
   xent_write(g, wl, wcf, n, mean, loss_out, loss64, corr_out, stats, stats_stride, slot, max_slots, nvalid);
 }
 
+// the round-5 form (a thread per row, one block per group) for every shape: the A/B of the
+// kernel bench (tools/bench_kernels xent rows); never set by the framework
+int g_xent_r5 = 0;
+
 template <typename T>
 int xent_go(const float* logits, const int* labels, int G, int B, int C, int mean, T* dl, float* loss,
             double* loss64, float* correct, float* stats, long long stats_stride, const int* slot, int max_slots,
             const int* nvalid, double* part, hipStream_t st) {
-  const int S = (B <= kXentThreads || part == nullptr) ? 1 : (B + kXentSliceRows - 1) / kXentSliceRows;
+  const int S = (B <= kXentThreads || part == nullptr || g_xent_r5) ? 1 : (B + kXentSliceRows - 1) / kXentSliceRows;
   const dim3 grid(S, G);
 #define XENT_L(LL)                                                                                            \
   hipLaunchKernelGGL((xent_kernel<T, LL>), grid, dim3(kXentThreads), 0, st, logits, labels, B, C, mean, dl, loss, \
                      loss64, correct, stats, stats_stride, slot, max_slots, nvalid, part)
-  if (C <= 16) XENT_L(1);   // a thread per row (the 10-class heads: the segment shuffles cost more)
+  if (C <= 16 || g_xent_r5) XENT_L(1);   // a thread per row (the 10-class heads: the segment shuffles cost more)
   else if (C <= 32) XENT_L(32);
   else XENT_L(64);
 #undef XENT_L
@@ -180,6 +184,12 @@ int xent_go(const float* logits, const int* labels, int G, int B, int C, int mea
 }
 
 }  // namespace
+
+DBA_EXPORT int dba_xent_r5_set(int on) {
+  const int prev = g_xent_r5;
+  if (on >= 0) g_xent_r5 = on;
+  return prev;
+}
 
 // doubles of the slice-partial workspace of a softmax_xent launch (0: one slice per group)
 DBA_EXPORT long long dba_softmax_xent_part_doubles(int G, int B) {

@@ -46,6 +46,7 @@ _SIGS = {
     "dba_dropout": [_P, _P, _I, _P, _U, _F, _LL, _I, _P],
     "dba_softmax_xent": [_P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _LL, _P, _I, _P, _I, _P, _P, _P],
     "dba_softmax_xent_part_doubles": [_I, _I],
+    "dba_xent_r5_set": [_I],
     "dba_head_train": [_P, _LL, _I, _I, _I, _I, _P, _LL, _P, _LL, _I, _P, _P, _P, _P, _P, _P, _LL, _P, _LL, _P, _P,
                        _P, _P, _LL, _P, _I, _I, _P],
     "dba_head_part_doubles": [_I, _I],

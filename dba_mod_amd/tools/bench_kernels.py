@@ -175,6 +175,28 @@ def _bench_eval_chunk(G, N, reps, dev):
 
 DOWN = [("eval.l2.0.down", 17, 1024, 16, 64, 32)]
 
+# softmax cross-entropy (loss.hip): G groups x B rows x C classes — Tiny-ImageNet's evaluation
+# chunk and training step, CIFAR's evaluation chunk and training step
+XENT = [("xent.tiny.eval", 1, 1024, 200), ("xent.tiny.train", 10, 64, 200), ("xent.cifar.eval", 17, 1024, 10),
+        ("xent.cifar.train", 10, 64, 10)]
+
+
+def _bench_xent(name, G, B, C, reps, dev):
+    torch.manual_seed(0)
+    logits = torch.randn(G, B, C, device=dev) * 3
+    labels = torch.randint(0, C, (G, B), device=dev, dtype=torch.int32)
+    t_grad = _time(lambda: H.softmax_xent(logits, labels, True, True, grad_dtype=torch.float32), reps)
+    t_eval = _time(lambda: H.softmax_xent(logits, labels, False, False), reps)
+    prev = H._L.dba_xent_r5_set(1)   # the round-5 kernel form (a thread per row, a block per group)
+    try:
+        t_grad5 = _time(lambda: H.softmax_xent(logits, labels, True, True, grad_dtype=torch.float32), reps)
+        t_eval5 = _time(lambda: H.softmax_xent(logits, labels, False, False), reps)
+    finally:
+        H._L.dba_xent_r5_set(prev)
+    return {"shape": name, "G": G, "B": B, "C": C, "train_us": round(t_grad * 1e6, 2),
+            "eval_us": round(t_eval * 1e6, 2), "r5_train_us": round(t_grad5 * 1e6, 2),
+            "r5_eval_us": round(t_eval5 * 1e6, 2)}
+
 
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser()
@@ -192,6 +214,10 @@ def main(argv=None) -> int:
     for name, G, N, W, C, C2 in DOWN:
         if args.only in name:
             rows.append(_bench_down(name, G, N, W, C, C2, args.reps, dev))
+            print(json.dumps(rows[-1]), flush=True)
+    for name, G, B, C in XENT:
+        if args.only in name:
+            rows.append(_bench_xent(name, G, B, C, args.reps, dev))
             print(json.dumps(rows[-1]), flush=True)
     if args.only in "eval.chunk":
         rows.append(_bench_eval_chunk(17, 1024, max(3, args.reps // 4), dev))
