@@ -2,14 +2,15 @@
 // Replaces log_softmax/cross_entropy/argmax/eq/sum and the per-batch `.item()` host syncs
 // of the reference (image_train.py:85,104-105; test.py:34-37): counters stay on device.
 //
-// A row belongs to a SEGMENT of L lanes (L = the power of two >= C, clamped to [32, 64]: 64 for
-// Tiny-ImageNet's 200 classes; heads of <= 16 classes — CIFAR / MNIST / LOAN — keep one thread
-// per row, L = 1, where the segment shuffles cost more than the short serial loops): the lanes read the row's logits
+// A row belongs to a SEGMENT of L lanes (L = 16 up to 512 classes — Tiny-ImageNet's 200: 13
+// per lane, 16 rows in flight per block — 64 beyond; heads of <= 16 classes — CIFAR / MNIST /
+// LOAN — keep one thread per row, L = 1, where the segment shuffles cost more than the short
+// serial loops): the lanes read the row's logits
 // coalesced (class c on lane c % L), and max / argmax / sum-exp are fixed butterflies inside the
 // segment, so a 256-thread block works on 256 / L rows at once.  (Round 1-5 form: one thread per
 // row looping serially over C with row-strided reads — 92.6 us per 1024 x 200 evaluation chunk.)
 //
-// Large groups (evaluation chunks) are cut into 64-row slices, one block per (slice, group), so a
+// Large groups (evaluation chunks) are cut into 32-row slices, one block per (slice, group), so a
 // launch fills the chip; each block writes its slice's (loss, correct) partial and a one-block-
 // per-group finish launch sums the partials in slice order.  Training batches (<= 256 rows) are
 // one slice: one launch, which also accumulates the step's (loss, correct, valid rows) straight
@@ -23,7 +24,7 @@
 namespace {
 
 constexpr int kXentThreads = 256;
-constexpr int kXentSliceRows = 64;
+constexpr int kXentSliceRows = 32;
 
 template <int L>
 __device__ __forceinline__ float seg_sum(float v) {
@@ -173,8 +174,11 @@ int xent_go(const float* logits, const int* labels, int G, int B, int C, int mea
 #define XENT_L(LL)                                                                                            \
   hipLaunchKernelGGL((xent_kernel<T, LL>), grid, dim3(kXentThreads), 0, st, logits, labels, B, C, mean, dl, loss, \
                      loss64, correct, stats, stats_stride, slot, max_slots, nvalid, part)
-  if (C <= 16 || g_xent_r5) XENT_L(1);   // a thread per row (the 10-class heads: the segment shuffles cost more)
-  else if (C <= 32) XENT_L(32);
+  // a thread per row for the 10-class heads (the segment shuffles cost more); 16-lane segments up
+  // to 512 classes (Tiny's 200: 13 per lane, 16 rows in flight per block — 64-lane segments left
+  // a 64-row group 16 serial passes: 41 vs 15 us for 10 x 64 x 200, tools/bench_kernels xent rows)
+  if (C <= 16 || g_xent_r5) XENT_L(1);
+  else if (C <= 512) XENT_L(16);
   else XENT_L(64);
 #undef XENT_L
   if (S > 1)

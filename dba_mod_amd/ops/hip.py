@@ -1097,7 +1097,7 @@ def softmax_xent(logits, labels, mean, want_grad, stats=None, slot=None, nvalid=
         assert ms * G == stats.shape[1]
         slot_, nv_ = _i32(slot), _i32(nvalid)
         sp, ss, slp, nvp = stats.data_ptr(), stats.shape[1], slot_.data_ptr(), nv_.data_ptr()
-    npart = int(_L.dba_softmax_xent_part_doubles(G, B))   # large groups: 64-row slices, one block each
+    npart = int(_L.dba_softmax_xent_part_doubles(G, B))   # large groups: 32-row slices, one block each
     part = torch.empty(npart, dtype=torch.float64, device=lf.device) if npart > 0 else None
     _call("dba_softmax_xent", lf.data_ptr(), _i32(labels).data_ptr(), G, B, C, int(bool(mean)), _ptr(dl),
           loss.data_ptr(), correct.data_ptr(), sp, ss, slp, ms, nvp, int(gdt == _F32), _ptr(loss64), _ptr(part),
