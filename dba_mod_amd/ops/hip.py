@@ -458,6 +458,9 @@ def _amax_act(t, nvalid):
     return a
 
 
+_EVAL_STEM_MFMA = os.environ.get("DBA_EVAL_STEM7_MFMA", "1") != "0"
+
+
 def _xconv_fwd(x, w, wsel, stride, pad, bias, residual, relu, nvalid, out_dtype, bnf=None, lz=None):
     """Reference-precision conv (fp32 in / fp32 out, fp16-pair MFMA: xconv.hpp).  ``bnf``: the
     fused training-BN statistics of the output (bnfuse.hpp); ``lz``: the input is a lazy BN
@@ -482,7 +485,13 @@ def _xconv_fwd(x, w, wsel, stride, pad, bias, residual, relu, nvalid, out_dtype,
     res = _act(residual, _F32, "residual") if residual is not None else None
     ay = _amax_out(y) if bnf is None else None   # the output's max, for its consumers
     bnf_p = ctypes.byref(bnf) if bnf is not None else None
-    if Cin <= 4:
+    # evaluation of a wide stem (Tiny-ImageNet's 7x7, K = 147; its weights pre-split at the
+    # eval fold) runs on the fp16-pair MFMAs: the exact-FMA stem kernel reaches ~64 TFLOP/s of
+    # VALU there and took 15 % of a Tiny round's GPU time (profiles/r6/tiny/).  Training keeps
+    # the exact kernel (the training bits), and so do the K = 27 / 25 stems, whose one-k-step
+    # MFMA tiles are all prologue and epilogue.
+    eval_mfma = (_EVAL_STEM_MFMA and "_dba_planes" in attrs and bnf is None and KH * KW * Cin > 64)
+    if Cin <= 4 and not eval_mfma:
         # few-channel image stems: exact-fp32 direct conv (stem.hip), -100 = not a stem shape
         rc = _call("dba_xstem_fwd", x.data_ptr(), N * H * W * Cin, w.data_ptr(), ws, _ptr(_i32(wsel)), _ptr(bias), bs,
                    _ptr(res), y.data_ptr(), N * Ho * Wo * Cout, _ptr(_i32(nvalid)), G, N, H, W, Cin, Ho, Wo, Cout,

@@ -39,6 +39,7 @@ SHAPES = [
     ("train.l3.0.sc", 10, 64, 16, 64, 128, 1, 2, 0),
     ("train.l4.0.conv1", 10, 64, 8, 128, 256, 3, 2, 1),
     ("train.l4.0.sc", 10, 64, 8, 128, 256, 1, 2, 0),
+    ("eval.tiny.stem", 1, 1024, 64, 3, 64, 7, 2, 3),  # Tiny-ImageNet 7x7/2 stem, an eval chunk
     ("tiny.stem", 1, 64, 64, 3, 64, 7, 2, 3),       # Tiny-ImageNet 7x7/2 stem, a lone client
     ("tiny.stem10", 10, 64, 64, 3, 64, 7, 2, 3),    # ... 10 clients
 ]
@@ -83,6 +84,15 @@ def _bench_fp32(name, G, N, Hh, Cin, Cout, k, s, p, reps, dev):
         per = Cout * k * k * Cin
         H.split_weights(w, per, per, H._amax_w(w, per, per))
     ops = [("fwd", lambda: H.conv2d(x, w, None, s, p, relu=True))]
+    if name == "eval.tiny.stem":   # the exact-FMA stem kernel it replaces in evaluation
+
+        def fma_fwd():
+            prev, H._EVAL_STEM_MFMA = H._EVAL_STEM_MFMA, False
+            try:
+                return H.conv2d(x, w, None, s, p, relu=True)
+            finally:
+                H._EVAL_STEM_MFMA = prev
+        ops.append(("fwd_fma", fma_fwd))
     block_flops = None
     if name.startswith("eval") and H.basic_block_ok(x, w, w):
         # the whole identity BasicBlock (two convs, the mid activation in LDS: xblock.hip); its
