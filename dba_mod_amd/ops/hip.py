@@ -459,6 +459,7 @@ def _amax_act(t, nvalid):
 
 
 _EVAL_STEM_MFMA = os.environ.get("DBA_EVAL_STEM7_MFMA", "1") != "0"
+_EVAL_STEM_PAD = True   # (the kernel bench's A/B of the channel padding)
 
 
 def _xconv_fwd(x, w, wsel, stride, pad, bias, residual, relu, nvalid, out_dtype, bnf=None, lz=None):
@@ -491,6 +492,20 @@ def _xconv_fwd(x, w, wsel, stride, pad, bias, residual, relu, nvalid, out_dtype,
     # the exact kernel (the training bits), and so do the K = 27 / 25 stems, whose one-k-step
     # MFMA tiles are all prologue and epilogue.
     eval_mfma = (_EVAL_STEM_MFMA and "_dba_planes" in attrs and bnf is None and KH * KW * Cin > 64)
+    if eval_mfma and Cin % 4 and _EVAL_STEM_PAD and lz is None:
+        # ... with the channels zero-padded to a multiple of 4: the implicit GEMM then stages
+        # one 16-B load per tap instead of Cin scalar loads (the zero channel adds K, never a bit
+        # of the sums beyond the fp16-pair grid: 0 * w = 0)
+        cp = 4 - Cin % 4
+        x4 = torch.nn.functional.pad(x, (0, cp))
+        x4._dba_amax = _amax_act(x, nvalid)
+        w4 = torch.nn.functional.pad(w, (0, cp)).contiguous()
+        per4 = w4[0].numel()
+        a4 = attrs.get("_dba_amax")
+        split_weights(w4, per4, per4, a4 if a4 is not None else _amax_w(w4, per4, per4))
+        if a4 is not None:
+            w4._dba_amax = a4
+        return _xconv_fwd(x4, w4, wsel, stride, pad, bias, residual, relu, nvalid, out_dtype)
     if Cin <= 4 and not eval_mfma:
         # few-channel image stems: exact-fp32 direct conv (stem.hip), -100 = not a stem shape
         rc = _call("dba_xstem_fwd", x.data_ptr(), N * H * W * Cin, w.data_ptr(), ws, _ptr(_i32(wsel)), _ptr(bias), bs,

@@ -93,6 +93,14 @@ def _bench_fp32(name, G, N, Hh, Cin, Cout, k, s, p, reps, dev):
             finally:
                 H._EVAL_STEM_MFMA = prev
         ops.append(("fwd_fma", fma_fwd))
+
+        def nopad_fwd():
+            prev, H._EVAL_STEM_PAD = H._EVAL_STEM_PAD, False
+            try:
+                return H.conv2d(x, w, None, s, p, relu=True)
+            finally:
+                H._EVAL_STEM_PAD = prev
+        ops.append(("fwd_nopad", nopad_fwd))
     block_flops = None
     if name.startswith("eval") and H.basic_block_ok(x, w, w):
         # the whole identity BasicBlock (two convs, the mid activation in LDS: xblock.hip); its
