@@ -489,8 +489,9 @@ def _xconv_fwd(x, w, wsel, stride, pad, bias, residual, relu, nvalid, out_dtype,
     # evaluation of a wide stem (Tiny-ImageNet's 7x7, K = 147; its weights pre-split at the
     # eval fold) runs on the fp16-pair MFMAs: the exact-FMA stem kernel reaches ~64 TFLOP/s of
     # VALU there and took 15 % of a Tiny round's GPU time (profiles/r6/tiny/).  Training keeps
-    # the exact kernel (the training bits), and so do the K = 27 / 25 stems, whose one-k-step
-    # MFMA tiles are all prologue and epilogue.
+    # the exact kernel (the training bits; on the MFMAs a Tiny lone step was 2.126 vs 2.142 ms,
+    # profiles/r6/tiny/train_stem_ab.md), and so do the K = 27 / 25 stems, whose one-k-step MFMA
+    # tiles are all prologue and epilogue.
     eval_mfma = (_EVAL_STEM_MFMA and "_dba_planes" in attrs and bnf is None and KH * KW * Cin > 64)
     if eval_mfma and Cin % 4 and _EVAL_STEM_PAD and lz is None:
         # ... with the channels zero-padded to a multiple of 4: the implicit GEMM then stages
